@@ -1,0 +1,286 @@
+/*
+ * oracle.c -- CPU restatement of Reflow's memoization hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (reflow_amd/, the
+ * C-ABI library libreflow_hip.so) links, loads or calls this file.  It is
+ * used only by tests/ (as the parity checker), by __graft_entry__.smoke()
+ * (as the checker) and by bench.py's cpu_baseline leg (as the timed CPU
+ * port).  It is never the thing measured on the GPU and never a fallback.
+ *
+ * Restated algorithms (reference = LDuderino/reflow @ v0, /root/reference):
+ *   - SHA-256 (FIPS 180-4).  The reference uses Go crypto/sha256 through
+ *     reflow.Digester = digest.Digester(crypto.SHA256)  (flow.go:36) and
+ *     streams whole files into it (repository/file/repository.go:50-63).
+ *   - digest.WriteDigest framing (grailbio/base/digest, not vendored):
+ *     0x00 0x05 || 32 hash bytes  (pinned by the goldens).
+ *   - MurmurHash3 x64_128, seed 0, streaming semantics of
+ *     vendor/github.com/spaolacci/murmur3/murmur128.go:56-171, murmur.go:34-59.
+ *   - Bloom filter probe/add of vendor/github.com/willf/bloom/bloom.go:
+ *     baseHashes :94-104, location :107-115, Add :144-150, Test :182-190,
+ *     with bitset.Test/Set of vendor/github.com/willf/bitset/bitset.go:143-156.
+ *   - bloomlive.T.Contains keys = WriteDigest(d) (internal/bloomlive/bloomlive.go:30-36).
+ *
+ * Pinned by: reference golden digests (flow_test.go:33-34, executor_test.go:77,
+ * syntax/digest_test.go:25, values/digest_test.go:28) through
+ * oracle/reflow_oracle.py, FIPS-180 known answers, and the SMHasher
+ * MurmurHash3_x64_128 verification value 0x6384BA69.  Bloom bit locations
+ * have no reference known-answer test ("parity unpinned" beyond the
+ * SMHasher pin of murmur3 and the restated arithmetic), see DESIGN.md.
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+#include <stdlib.h>
+#include <pthread.h>
+
+/* ------------------------------------------------------------------ */
+/* SHA-256, portable scalar (FIPS 180-4 §6.2)                          */
+/* ------------------------------------------------------------------ */
+static const uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+#define ROR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+
+static void sha256_compress(uint32_t st[8], const uint8_t blk[64]) {
+    uint32_t w[64];
+    for (int t = 0; t < 16; ++t)
+        w[t] = ((uint32_t)blk[4 * t] << 24) | ((uint32_t)blk[4 * t + 1] << 16) |
+               ((uint32_t)blk[4 * t + 2] << 8) | (uint32_t)blk[4 * t + 3];
+    for (int t = 16; t < 64; ++t) {
+        uint32_t s0 = ROR(w[t - 15], 7) ^ ROR(w[t - 15], 18) ^ (w[t - 15] >> 3);
+        uint32_t s1 = ROR(w[t - 2], 17) ^ ROR(w[t - 2], 19) ^ (w[t - 2] >> 10);
+        w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+    }
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    for (int t = 0; t < 64; ++t) {
+        uint32_t S1 = ROR(e, 6) ^ ROR(e, 11) ^ ROR(e, 25);
+        uint32_t ch = (e & f) ^ (~e & g);
+        uint32_t t1 = h + S1 + ch + K256[t] + w[t];
+        uint32_t S0 = ROR(a, 2) ^ ROR(a, 13) ^ ROR(a, 22);
+        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        uint32_t t2 = S0 + mj;
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+void orc_sha256(const uint8_t *msg, uint64_t len, uint8_t out[32]) {
+    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint64_t full = len / 64;
+    for (uint64_t i = 0; i < full; ++i) sha256_compress(st, msg + 64 * i);
+    uint8_t tail[128];
+    uint64_t rem = len - 64 * full;
+    memset(tail, 0, sizeof tail);
+    if (rem) memcpy(tail, msg + 64 * full, rem);
+    tail[rem] = 0x80;
+    uint64_t tl = (rem + 9 <= 64) ? 64 : 128;
+    uint64_t bits = len * 8;
+    for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    sha256_compress(st, tail);
+    if (tl == 128) sha256_compress(st, tail + 64);
+    for (int i = 0; i < 8; ++i) {
+        out[4 * i] = (uint8_t)(st[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(st[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(st[i] >> 8);
+        out[4 * i + 3] = (uint8_t)st[i];
+    }
+}
+
+/* Batched form used by the CPU baseline: message i = arena[offs[i] .. +lens[i]).
+ * Work is split over nthreads pthreads in a round-robin over messages, the CPU
+ * analogue of local/executor.go:522-538 (errgroup, DigestLimiter=60). */
+typedef struct {
+    const uint8_t *arena; const uint64_t *offs, *lens; uint64_t n; uint8_t *out;
+    int tid, nth;
+} sha_job;
+
+static void *sha_worker(void *p) {
+    sha_job *j = (sha_job *)p;
+    for (uint64_t i = (uint64_t)j->tid; i < j->n; i += (uint64_t)j->nth)
+        orc_sha256(j->arena + j->offs[i], j->lens[i], j->out + 32 * i);
+    return NULL;
+}
+
+void orc_sha256_batch(const uint8_t *arena, const uint64_t *offs, const uint64_t *lens,
+                      uint64_t n, uint8_t *out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t th[256];
+    sha_job jobs[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (sha_job){arena, offs, lens, n, out, t, nthreads};
+        pthread_create(&th[t], NULL, sha_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+/* ------------------------------------------------------------------ */
+/* Synthetic content generator (shared spec with the device generator) */
+/* word q of stream s = mix64(s + (q+1)*0x9E3779B97F4A7C15), LE bytes. */
+/* This is splitmix64 in its counter form.              */
+/* ------------------------------------------------------------------ */
+static inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+void orc_fill_stream(uint64_t seed, uint8_t *dst, uint64_t len) {
+    uint64_t q = 0;
+    for (; 8 * q + 8 <= len; ++q) {
+        uint64_t v = mix64(seed + (q + 1) * 0x9E3779B97F4A7C15ULL);
+        memcpy(dst + 8 * q, &v, 8);
+    }
+    if (8 * q < len) {
+        uint64_t v = mix64(seed + (q + 1) * 0x9E3779B97F4A7C15ULL);
+        memcpy(dst + 8 * q, &v, len - 8 * q);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* MurmurHash3 x64_128, seed 0 (murmur128.go:56-171)                   */
+/* ------------------------------------------------------------------ */
+static const uint64_t C1 = 0x87c37b91114253d5ULL, C2 = 0x4cf5ad432745937fULL;
+static inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33; return k;
+}
+static inline uint64_t ld64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+
+void orc_mm3_128(const uint8_t *data, uint64_t len, uint32_t seed, uint64_t out[2]) {
+    uint64_t h1 = seed, h2 = seed;
+    uint64_t nb = len / 16;
+    for (uint64_t i = 0; i < nb; ++i) {
+        uint64_t k1 = ld64(data + 16 * i), k2 = ld64(data + 16 * i + 8);
+        k1 *= C1; k1 = rotl64(k1, 31); k1 *= C2; h1 ^= k1;
+        h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+        k2 *= C2; k2 = rotl64(k2, 33); k2 *= C1; h2 ^= k2;
+        h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+    }
+    const uint8_t *t = data + 16 * nb;
+    uint64_t k1 = 0, k2 = 0;
+    switch (len & 15) {
+    case 15: k2 ^= (uint64_t)t[14] << 48; /* fallthrough */
+    case 14: k2 ^= (uint64_t)t[13] << 40; /* fallthrough */
+    case 13: k2 ^= (uint64_t)t[12] << 32; /* fallthrough */
+    case 12: k2 ^= (uint64_t)t[11] << 24; /* fallthrough */
+    case 11: k2 ^= (uint64_t)t[10] << 16; /* fallthrough */
+    case 10: k2 ^= (uint64_t)t[9] << 8;   /* fallthrough */
+    case 9:  k2 ^= (uint64_t)t[8];
+             k2 *= C2; k2 = rotl64(k2, 33); k2 *= C1; h2 ^= k2; /* fallthrough */
+    case 8:  k1 ^= (uint64_t)t[7] << 56;  /* fallthrough */
+    case 7:  k1 ^= (uint64_t)t[6] << 48;  /* fallthrough */
+    case 6:  k1 ^= (uint64_t)t[5] << 40;  /* fallthrough */
+    case 5:  k1 ^= (uint64_t)t[4] << 32;  /* fallthrough */
+    case 4:  k1 ^= (uint64_t)t[3] << 24;  /* fallthrough */
+    case 3:  k1 ^= (uint64_t)t[2] << 16;  /* fallthrough */
+    case 2:  k1 ^= (uint64_t)t[1] << 8;   /* fallthrough */
+    case 1:  k1 ^= (uint64_t)t[0];
+             k1 *= C1; k1 = rotl64(k1, 31); k1 *= C2; h1 ^= k1;
+    }
+    h1 ^= len; h2 ^= len;
+    h1 += h2; h2 += h1;
+    h1 = fmix64(h1); h2 = fmix64(h2);
+    h1 += h2; h2 += h1;
+    out[0] = h1; out[1] = h2;
+}
+
+/* ------------------------------------------------------------------ */
+/* Bloom filter (willf/bloom v2.0.3, willf/bitset v1.1.2)              */
+/* ------------------------------------------------------------------ */
+/* baseHashes (bloom.go:94-104): (h1,h2)=mm3(data), (h3,h4)=mm3(data||0x01).
+ * The streaming hasher keeps its state after Sum128, so the second pair is
+ * the one-shot hash of the 1-byte-extended message. */
+void orc_bloom_base_hashes(const uint8_t *data, uint64_t len, uint64_t h[4]) {
+    uint8_t buf[256];
+    uint8_t *p = len + 1 <= sizeof buf ? buf : (uint8_t *)malloc(len + 1);
+    memcpy(p, data, len);
+    p[len] = 1;
+    orc_mm3_128(p, len, 0, h);
+    orc_mm3_128(p, len + 1, 0, h + 2);
+    if (p != buf) free(p);
+}
+
+/* location (bloom.go:107-110), before the "% m" of :113-115. */
+uint64_t orc_bloom_location(const uint64_t h[4], uint64_t i) {
+    return h[i % 2] + i * h[2 + (((i + (i % 2)) % 4) / 2)];
+}
+
+/* Test (bloom.go:182-190) with bitset.Test (bitset.go:143-149):
+ * bit loc in word loc>>6, mask 1<<(loc&63); loc >= length ⇒ false. */
+int orc_bloom_test(const uint64_t *words, uint64_t length, uint64_t m, uint64_t k,
+                   const uint8_t *data, uint64_t len) {
+    uint64_t h[4];
+    orc_bloom_base_hashes(data, len, h);
+    for (uint64_t i = 0; i < k; ++i) {
+        uint64_t loc = orc_bloom_location(h, i) % m;
+        if (loc >= length) return 0;
+        if (!((words[loc >> 6] >> (loc & 63)) & 1)) return 0;
+    }
+    return 1;
+}
+
+/* Add (bloom.go:144-150), bitset.Set (bitset.go:151-156).  The caller sizes
+ * words for max(length, m) bits; *length grows like extendSetMaybe. */
+void orc_bloom_add(uint64_t *words, uint64_t *length, uint64_t m, uint64_t k,
+                   const uint8_t *data, uint64_t len) {
+    uint64_t h[4];
+    orc_bloom_base_hashes(data, len, h);
+    for (uint64_t i = 0; i < k; ++i) {
+        uint64_t loc = orc_bloom_location(h, i) % m;
+        if (loc >= *length) *length = loc + 1;
+        words[loc >> 6] |= 1ULL << (loc & 63);
+    }
+}
+
+/* bloomlive.T.Contains over a batch of 32-byte digests
+ * (internal/bloomlive/bloomlive.go:30-36): key = 00 05 || digest. */
+typedef struct {
+    const uint64_t *words; uint64_t length, m, k; const uint8_t *d32; uint64_t n;
+    uint8_t *out; int tid, nth;
+} probe_job;
+
+static void *probe_worker(void *p) {
+    probe_job *j = (probe_job *)p;
+    uint8_t key[34];
+    key[0] = 0; key[1] = 5;
+    for (uint64_t i = (uint64_t)j->tid; i < j->n; i += (uint64_t)j->nth) {
+        memcpy(key + 2, j->d32 + 32 * i, 32);
+        j->out[i] = (uint8_t)orc_bloom_test(j->words, j->length, j->m, j->k, key, 34);
+    }
+    return NULL;
+}
+
+void orc_bloomlive_contains_batch(const uint64_t *words, uint64_t length, uint64_t m, uint64_t k,
+                                  const uint8_t *d32, uint64_t n, uint8_t *out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    probe_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (probe_job){words, length, m, k, d32, n, out, t, nthreads};
+        pthread_create(&th[t], NULL, probe_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+void orc_bloomlive_add_batch(uint64_t *words, uint64_t *length, uint64_t m, uint64_t k,
+                             const uint8_t *d32, uint64_t n) {
+    uint8_t key[34];
+    key[0] = 0; key[1] = 5;
+    for (uint64_t i = 0; i < n; ++i) {
+        memcpy(key + 2, d32 + 32 * i, 32);
+        orc_bloom_add(words, length, m, k, key, 34);
+    }
+}

@@ -1,0 +1,299 @@
+"""CPU restatement (oracle) of Reflow's digest / cache-key / probe path.
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module, and only as the checker (or, for the
+cpu_baseline, as the timed CPU port).  The product (reflow_amd/, the C-ABI
+library) never imports it.
+
+What it restates (reference = LDuderino/reflow @ v0 under /root/reference):
+  * digest framing  WD(d) = 0x00 0x05 || d          (grailbio/base/digest, not
+    vendored; pinned by the goldens below)
+  * Fileset.WriteDigest / Digest                   executor.go:205-233
+  * Op.DigestString (stale table, OpData->"maxOp")  op_string.go:11-21
+  * Flow.WriteDigest / Digest (V1 inline, V2 WD)   flow.go:653-750, writeN :909-913
+  * Flow.PhysicalDigest / CacheKeys                flow.go:764-802
+  * Canonicalize config merge (HashV1)             flow.go:814-843, 47-50
+  * values.WriteDigest (for the values golden)     values/values.go:270-393
+  * bloom / murmur3 / SHA-256 arithmetic           oracle.c (via ctypes)
+
+Pinned against the reference's own golden vectors (tests/test_oracle_golden.py):
+  flow_test.go:33 (V1), flow_test.go:34 (V2), executor_test.go:77,
+  syntax/digest_test.go:25, values/digest_test.go:28.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import struct
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    """Load oracle/liboracle.so (building it with make if absent)."""
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        L = ctypes.CDLL(path)
+        u8p = ctypes.c_void_p
+        L.orc_sha256.argtypes = [u8p, ctypes.c_uint64, u8p]
+        L.orc_sha256_batch.argtypes = [u8p, u8p, u8p, ctypes.c_uint64, u8p, ctypes.c_int]
+        L.orc_fill_stream.argtypes = [ctypes.c_uint64, u8p, ctypes.c_uint64]
+        L.orc_mm3_128.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p]
+        L.orc_bloom_base_hashes.argtypes = [u8p, ctypes.c_uint64, u8p]
+        L.orc_bloom_location.argtypes = [u8p, ctypes.c_uint64]
+        L.orc_bloom_location.restype = ctypes.c_uint64
+        L.orc_bloom_test.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                     u8p, ctypes.c_uint64]
+        L.orc_bloom_test.restype = ctypes.c_int
+        L.orc_bloom_add.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p,
+                                    ctypes.c_uint64]
+        L.orc_bloomlive_contains_batch.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64,
+                                                   ctypes.c_uint64, u8p, ctypes.c_uint64, u8p,
+                                                   ctypes.c_int]
+        L.orc_bloomlive_add_batch.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p,
+                                              ctypes.c_uint64]
+        _LIB = L
+    return _LIB
+
+
+def _buf(b: bytes):
+    return ctypes.c_char_p(b) if b else ctypes.c_char_p(b"\0")
+
+
+# --------------------------------------------------------------------------
+# SHA-256 and digest framing
+# --------------------------------------------------------------------------
+def sha256(b: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_sha256(_buf(b), len(b), out)
+    return out.raw
+
+
+def WD(d: bytes) -> bytes:
+    """digest.WriteDigest: big-endian uint16(crypto.SHA256 = 5), then the hash."""
+    assert len(d) == 32
+    return b"\x00\x05" + d
+
+
+def digest_string(d: bytes) -> str:
+    return "sha256:" + d.hex()
+
+
+def from_string(s: str) -> bytes:
+    return sha256(s.encode())
+
+
+def fill_stream(seed: int, n: int) -> bytes:
+    out = ctypes.create_string_buffer(max(n, 1))
+    lib().orc_fill_stream(ctypes.c_uint64(seed & (2**64 - 1)), out, n)
+    return out.raw[:n]
+
+
+# --------------------------------------------------------------------------
+# Fileset (executor.go:25-38, 205-233)
+# --------------------------------------------------------------------------
+class OFileset:
+    def __init__(self, map=None, list=None):
+        self.map = map  # dict path -> (id32, size)
+        self.list = list  # list of OFileset or None
+
+    def material(self) -> bytes:
+        if self.list is not None:  # List wins when non-nil (executor.go:216-219)
+            return b"".join(v.material() for v in self.list)
+        out = []
+        for path in sorted((self.map or {}).keys(), key=lambda s: s.encode()):
+            out.append(path.encode() + WD(self.map[path][0]))
+        return b"".join(out)
+
+    def digest(self) -> bytes:
+        return sha256(self.material())
+
+
+# --------------------------------------------------------------------------
+# Flow (flow.go)
+# --------------------------------------------------------------------------
+OPS = ["OpExec", "OpIntern", "OpExtern", "OpGroupby", "OpMap", "OpCollect", "OpMerge",
+       "OpVal", "OpPullup", "OpK", "OpCoerce", "OpRequirements", "OpData"]
+OP = {name: i + 1 for i, name in enumerate(OPS)}
+_DIGEST_NAMES = ["OpExec", "OpIntern", "OpExtern", "OpGroupby", "OpMap", "OpCollect",
+                 "OpMerge", "OpVal", "OpPullup", "OpK", "OpCoerce", "OpRequirements", "maxOp"]
+
+
+def op_digest_string(op: int) -> str:
+    """op_string.go:15-21: the generated table is one entry stale, so OpData
+    digests as "maxOp"."""
+    i = op - 1
+    if i < 0 or i >= len(_DIGEST_NAMES):
+        return "Op(%d)" % op
+    return _DIGEST_NAMES[i]
+
+
+def writeN(n: int) -> bytes:
+    return struct.pack("<Q", n & (2**64 - 1))
+
+
+class OFlow:
+    def __init__(self, op, deps=(), **kw):
+        self.op = OP[op] if isinstance(op, str) else op
+        self.deps = list(deps)
+        self.parent = kw.get("parent")
+        self.hashv1 = kw.get("hashv1", False)
+        self.image = kw.get("image", "")
+        self.cmd = kw.get("cmd", "")
+        self.url = kw.get("url", "")
+        self.re = kw.get("re", "")
+        self.repl = kw.get("repl", "")
+        self.mapflow = kw.get("mapflow")
+        self.argmap = kw.get("argmap")  # None or list of (out: bool, index: int)
+        self.flow_digest = kw.get("flow_digest")
+        self.value = kw.get("value")  # OFileset or None
+        self.done = kw.get("done", False)
+        self.data = kw.get("data", b"")
+        self.err = kw.get("err", False)
+
+    # Flow.WriteDigest (flow.go:675-750)
+    def material(self, universe: bytes = b"", v1=False) -> bytes:
+        v1 = v1 or self.hashv1
+        w = [universe]
+        if self.op == OP["OpRequirements"]:
+            return universe + self.deps[0].material(universe, v1)
+        if self.parent is not None:
+            return universe + self.parent.material(universe, v1)
+        for d in self.deps:
+            w.append(d.material(universe, v1) if v1 else WD(d.digest(universe, v1)))
+        w.append(op_digest_string(self.op).encode())
+        w.append(self.params(universe, v1))
+        return b"".join(w)
+
+    def params(self, universe, v1) -> bytes:
+        op = self.op
+        if op in (OP["OpIntern"], OP["OpExtern"]):
+            return self.url.encode()
+        if op == OP["OpExec"]:
+            return self.image.encode() + self.cmd.encode() + self.argbytes()
+        if op == OP["OpGroupby"]:
+            return self.re.encode()
+        if op == OP["OpMap"]:
+            return self.mapflow.material(universe, v1)
+        if op == OP["OpCollect"]:
+            return self.re.encode() + self.repl.encode()
+        if op == OP["OpVal"]:
+            if self.err:
+                raise ValueError("error OpVal digests are random (flow.go:722-731)")
+            if self.value is not None:
+                return self.value.material()
+            assert self.flow_digest is not None, "invalid flow digest"
+            return WD(self.flow_digest)
+        if op in (OP["OpK"], OP["OpCoerce"]):
+            assert self.flow_digest is not None, "invalid flow digest"
+            return WD(self.flow_digest)
+        if op == OP["OpData"]:
+            return self.data
+        return b""  # OpMerge, OpPullup
+
+    def argbytes(self) -> bytes:
+        out = b""
+        for is_out, idx in (self.argmap or []):
+            out += writeN(-idx if is_out else idx)
+        return out
+
+    def digest(self, universe: bytes = b"", v1=False) -> bytes:
+        return sha256(self.material(universe, v1))
+
+    # Flow.PhysicalDigest (flow.go:764-792); None == zero digest
+    def physical_material(self):
+        if self.op not in (OP["OpExtern"], OP["OpExec"]):
+            return None
+        w = []
+        for d in self.deps:
+            if not d.done:
+                return None
+            w.append(d.value.material())
+        if self.op == OP["OpExtern"]:
+            w.append(self.url.encode())
+        else:
+            w.append(self.image.encode() + self.cmd.encode() + self.argbytes())
+        return b"".join(w)
+
+    def physical_digest(self):
+        m = self.physical_material()
+        return None if m is None else sha256(m)
+
+    # Flow.CacheKeys (flow.go:796-802)
+    def cache_keys(self, universe: bytes = b"", v1=False):
+        keys = []
+        p = self.physical_digest()
+        if p is not None:
+            keys.append(p)
+        keys.append(self.digest(universe, v1))
+        return keys
+
+
+# --------------------------------------------------------------------------
+# values.WriteDigest subset (values/values.go:290-393) for the values golden
+# --------------------------------------------------------------------------
+KIND = {"Int": 2, "String": 3, "Struct": 12, "Map": 9}
+
+
+def values_int(n: int) -> bytes:
+    # big.Int.Bytes(): big-endian magnitude, no leading zeros
+    return bytes([KIND["Int"]]) + (n.to_bytes((n.bit_length() + 7) // 8, "big") if n else b"")
+
+
+def values_string(s: str) -> bytes:
+    return bytes([KIND["String"]]) + s.encode()
+
+
+def values_struct(fields: dict) -> bytes:
+    """fields: name -> material; sorted by name, LE64 length prefix."""
+    out = bytes([KIND["Struct"]]) + writeN(len(fields))
+    for k in sorted(fields, key=lambda s: s.encode()):
+        out += fields[k]
+    return out
+
+
+def values_map(entries) -> bytes:
+    """entries: list of (key material, value material); sorted by key digest."""
+    out = bytes([KIND["Map"]]) + writeN(len(entries))
+    for km, vm in sorted(entries, key=lambda e: sha256(e[0])):
+        out += km + vm
+    return out
+
+
+# --------------------------------------------------------------------------
+# Bloom / murmur3 wrappers
+# --------------------------------------------------------------------------
+def mm3_128(data: bytes, seed: int = 0):
+    out = (ctypes.c_uint64 * 2)()
+    lib().orc_mm3_128(_buf(data), len(data), seed, out)
+    return out[0], out[1]
+
+
+def bloom_base_hashes(data: bytes):
+    out = (ctypes.c_uint64 * 4)()
+    lib().orc_bloom_base_hashes(_buf(data), len(data), out)
+    return tuple(out)
+
+
+def bloom_locations(data: bytes, k: int, m: int):
+    h = (ctypes.c_uint64 * 4)(*bloom_base_hashes(data))
+    return [lib().orc_bloom_location(h, i) % m for i in range(k)]
+
+
+def estimate_parameters(n: int, p: float):
+    """bloom.go:120-124 (float64 math; filters carry m,k -- never recompute)."""
+    import math
+    m = int(math.ceil(-1 * float(n) * math.log(p) / math.pow(math.log(2), 2)))
+    k = int(math.ceil(math.log(2) * float(m) / float(n)))
+    return m, k
+
+
+def sha256_hashlib(b: bytes) -> bytes:
+    """Independent FIPS-180 implementation used to cross-check oracle.c."""
+    return hashlib.sha256(b).digest()
