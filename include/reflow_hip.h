@@ -1,0 +1,181 @@
+/*
+ * reflow_hip.h -- C-ABI of the MI355X memoization engine (libreflow_hip.so).
+ *
+ * Drop-in boundary for Reflow's data-parallel memoization hot path
+ * (reference: LDuderino/reflow @ v0, paths relative to /root/reference).
+ * Every entry point is batched: the reference's per-call Go interfaces
+ * (one io.Writer per file, one goroutine per cache lookup) are coalesced by
+ * the host shim into device batches (INTEGRATION.md shows the cgo binding).
+ *
+ * Conventions
+ *   - Plain pointers and sizes; no C++ or torch types cross this boundary.
+ *   - Every function returns an rf_status (0 = RF_OK).  On failure
+ *     rf_last_error() returns a thread-local message.  No exception crosses.
+ *   - Host buffers are caller-owned and not retained after return (cgo rule).
+ *     Device buffers passed to *_device functions are caller-owned HBM.
+ *   - "stream" arguments are hipStream_t values passed as void* (NULL = the
+ *     context's own stream).  *_device functions are asynchronous on it.
+ *   - A digest is 32 raw SHA-256 bytes.  WD(d) = 0x00 0x05 || d (34 bytes) is
+ *     the grailbio/base/digest.WriteDigest framing the reference hashes.
+ *
+ * The product path is the HIP path only: if the gfx950 code object cannot be
+ * loaded or no device is present, rf_init fails with RF_EDEVICE -- there is
+ * no CPU fallback behind this ABI.
+ */
+#ifndef REFLOW_HIP_H
+#define REFLOW_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes; the shim maps them onto errors.Kind (errors/errors.go:39-76). */
+typedef enum {
+    RF_OK = 0,
+    RF_EINVAL = 1,     /* errors.Invalid: malformed input, bad graph, cycle */
+    RF_EIO = 2,        /* errors.Unavailable: reading an input file failed   */
+    RF_EINTEGRITY = 3, /* errors.Integrity: digest mismatch on verify        */
+    RF_EDEVICE = 4,    /* errors.Unavailable: HIP runtime / device failure   */
+    RF_ENOMEM = 5,     /* errors.ResourcesExhausted: HBM or host allocation  */
+    RF_ENOTFOUND = 6   /* errors.NotExist                                     */
+} rf_status;
+
+typedef struct rf_ctx rf_ctx;
+typedef struct rf_sha_plan rf_sha_plan;
+typedef struct rf_graph rf_graph;
+typedef struct rf_bloom rf_bloom;
+
+/* ---- context ----------------------------------------------------------- */
+/* Bind a context to HIP device `device` (one process per GPU).  Replaces the
+ * process-global reflow.Digester (flow.go:36) as the owner of device state. */
+int rf_init(int device, rf_ctx **out);
+void rf_destroy(rf_ctx *ctx);
+const char *rf_last_error(void);
+int rf_device_count(int *n);
+/* Blocks until all work queued on the context's stream finished. */
+int rf_sync(rf_ctx *ctx);
+/* Version string, e.g. "reflow-hip 0.1 gfx950". */
+const char *rf_version(void);
+
+/* ---- K1: batched SHA-256 (Digester.NewWriter/FromBytes, Repository.Put) --
+ * Replaces the per-file io.Copy into Digester.NewWriter() at
+ * repository/file/repository.go:50-63 (Install) and :237-264 (Put), driven by
+ * the ≤60-goroutine loop of local/executor.go:514-557.  out32[i] = SHA256(msg i). */
+int rf_sha256_batch(rf_ctx *ctx, const uint8_t *const *msgs, const uint64_t *lens, uint64_t n,
+                    uint8_t *out32);
+
+/* Same, messages given as one host arena + offsets. */
+int rf_sha256_arena(rf_ctx *ctx, const uint8_t *arena, const uint64_t *offs, const uint64_t *lens,
+                    uint64_t n, uint8_t *out32);
+
+/* Device-resident form.  A plan is built once from host-side offsets and
+ * lengths (it orders messages largest-first and decides which messages run
+ * wave-per-message); rf_sha_plan_run then digests messages already in HBM.
+ * Requirements: offs[i] % 16 == 0.  out is n*32 bytes of device memory. */
+int rf_sha_plan_create(rf_ctx *ctx, const uint64_t *offs, const uint64_t *lens, uint64_t n,
+                       uint32_t flags, rf_sha_plan **out);
+int rf_sha_plan_run(rf_sha_plan *plan, const void *d_arena, void *d_out32, void *stream);
+typedef struct {
+    uint64_t n_msgs, n_solo;     /* messages; messages run wave-per-message */
+    uint64_t total_blocks;       /* Σ ceil((len+9)/64): algorithmic unit of K1 */
+    uint64_t max_blocks;         /* critical path of the largest message       */
+    uint64_t total_bytes;
+    float last_ms_lanes, last_ms_solo, last_ms_total; /* HIP-event times of the last run */
+} rf_sha_stats;
+int rf_sha_plan_stats(rf_sha_plan *plan, rf_sha_stats *out);
+void rf_sha_plan_destroy(rf_sha_plan *plan);
+/* flags for rf_sha_plan_create */
+#define RF_SHA_NO_SOLO 1u      /* every message lane-per-message */
+#define RF_SHA_ALL_SOLO 2u     /* every message wave-per-message */
+
+/* Synthetic data generator (bench / tests): fills d_arena so that message i
+ * is the splitmix64 counter stream with seed (seed ^ i). */
+int rf_gen_fill(rf_ctx *ctx, void *d_arena, const uint64_t *d_offs, const uint64_t *d_lens,
+                uint64_t n, uint64_t seed, uint64_t arena_bytes, void *stream);
+
+/* ---- Fileset digest (Fileset.Digest/WriteDigest, executor.go:205-233) ----
+ * n_sets filesets; set s owns groups [set_group[s], set_group[s+1]); group g
+ * owns entries [group_entry[g], group_entry[g+1]).  A Map fileset is one
+ * group; a List fileset contributes its (flattened, depth-first) Map leaves as
+ * consecutive groups ("List wins if non-nil", executor.go:216-219).  Entries
+ * within a group are sorted bytewise here (sort.Strings).  Material per group
+ * = Σ path ‖ WD(id).  out32[s] = SHA256(material of set s). */
+int rf_fileset_digest_batch(rf_ctx *ctx, uint64_t n_sets, const uint64_t *set_group,
+                            const uint64_t *group_entry, const char *const *paths,
+                            const uint32_t *path_lens, const uint8_t *ids32, uint8_t *out32);
+
+/* ---- K2/K3: incremental digest DAG (Flow.Digest / CacheKeys) ------------
+ * The host lowers a Flow graph (flow.go:653-802) into hash JOBS over digest
+ * SLOTS.  Job j hashes a byte template (its digest material, flow.go:675-750
+ * or the physical material of :764-792) into slot out_slot[j]; the template
+ * has "holes": hole h of job j places the 32 digest bytes of slot
+ * hole_slot[h] at byte hole_pos[h] of the material (the host already wrote
+ * the 0x00 0x05 WD prefix in front of each hole).  Slots written by no job
+ * are inputs (e.g. File IDs).  Jobs must form a DAG over slots. */
+typedef struct {
+    uint32_t n_jobs, n_slots;
+    const uint32_t *out_slot;    /* [n_jobs]                                    */
+    const uint64_t *tmpl_off;    /* [n_jobs] byte offset of job j's template in blob */
+    const uint32_t *tmpl_len;    /* [n_jobs] material length (bytes)            */
+    const uint64_t *hole_ptr;    /* [n_jobs+1] CSR into hole_pos/hole_slot      */
+    const uint32_t *hole_pos;    /* byte position of the 32 digest bytes         */
+    const uint32_t *hole_slot;   /* slot whose digest fills the hole            */
+    const uint8_t *blob;         /* templates                                   */
+    uint64_t blob_len;
+} rf_graph_desc;
+
+int rf_graph_load(rf_ctx *ctx, const rf_graph_desc *desc, rf_graph **out);
+void rf_graph_destroy(rf_graph *g);
+/* Set input-slot digests (e.g. changed File IDs); marks their transitive
+ * dependents dirty.  Setting a job's output slot is RF_EINVAL. */
+int rf_graph_set_slots(rf_graph *g, const uint32_t *slots, const uint8_t *digests32, uint32_t n);
+/* Device-resident form of set_slots (indices and digests in HBM). */
+int rf_graph_set_slots_device(rf_graph *g, const void *d_slots, const void *d_digests32, uint32_t n,
+                              void *stream);
+/* Recompute dirty jobs level by level (K3 frontier + K2 node digests).
+ * full != 0 recomputes every job.  Early cut-off: a job whose digest did not
+ * change does not dirty its consumers.  *out_recomputed (may be NULL) receives
+ * the number of jobs hashed (synchronises). */
+int rf_graph_recompute(rf_graph *g, int full, uint64_t *out_recomputed);
+/* Asynchronous form (no count readback). */
+int rf_graph_recompute_async(rf_graph *g, int full, void *stream);
+int rf_graph_get_slots(rf_graph *g, const uint32_t *slots, uint32_t n, uint8_t *out32);
+typedef struct {
+    uint32_t n_jobs, n_slots, n_levels, max_level_jobs;
+    uint64_t total_blocks, hole_count, template_bytes;
+    uint64_t last_recomputed;
+    float last_ms;
+} rf_graph_stats;
+int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
+
+/* ---- K4: bloomlive / assoc probe (bloom.go:182-190, bloomlive.go:30-36) --
+ * Filters cache-key lookups before Assoc.Get (eval.go:1202-1220) and serves
+ * Liveset.Contains for Repository.Collect (repository/file/repository.go:304-327). */
+/* words: bitset words (uint64, bit i in word i>>6); length = bitset length in bits. */
+int rf_bloom_load(rf_ctx *ctx, uint64_t m, uint64_t k, const uint64_t *words, uint64_t nwords,
+                  uint64_t length, rf_bloom **out);
+/* Go JSON wire form {"m":M,"k":K,"b":"<base64url(BE64 len ‖ BE64 words)>"} (bloom.go:264-286). */
+int rf_bloom_load_json(rf_ctx *ctx, const char *json, size_t len, rf_bloom **out);
+/* Go binary wire form BE64 m ‖ BE64 k ‖ BE64 len ‖ BE64 words (bloom.go:290-325). */
+int rf_bloom_load_binary(rf_ctx *ctx, const uint8_t *buf, size_t len, rf_bloom **out);
+/* New empty filter with m bits and k hashes (bloom.New, bloom.go:81-83). */
+int rf_bloom_new(rf_ctx *ctx, uint64_t m, uint64_t k, rf_bloom **out);
+void rf_bloom_destroy(rf_bloom *b);
+/* out[i] = Contains(digest i): key = WD(d), all k bits set. */
+int rf_bloom_probe(rf_bloom *b, const uint8_t *digests32, uint64_t n, uint8_t *out);
+int rf_bloom_probe_device(rf_bloom *b, const void *d_digests32, uint64_t n, void *d_out,
+                          void *stream);
+/* Add WD(d) for each digest (eval.go:848-858 build side). */
+int rf_bloom_add(rf_bloom *b, const uint8_t *digests32, uint64_t n);
+int rf_bloom_add_device(rf_bloom *b, const void *d_digests32, uint64_t n, void *stream);
+/* Read back m, k, length and the words (nwords = ceil(length/64) capacity). */
+int rf_bloom_params(rf_bloom *b, uint64_t *m, uint64_t *k, uint64_t *length, uint64_t *nwords);
+int rf_bloom_words(rf_bloom *b, uint64_t *words, uint64_t nwords);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* REFLOW_HIP_H */

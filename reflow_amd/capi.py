@@ -1,0 +1,375 @@
+"""ctypes binding of include/reflow_hip.h (libreflow_hip.so).
+
+This is plumbing for the Python test-suite and bench.py: every call goes
+through the C-ABI into the gfx950 kernels.  There is no CPU fallback: if the
+library or a gfx950 device is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libreflow_hip.so")
+
+RF_OK, RF_EINVAL, RF_EIO, RF_EINTEGRITY, RF_EDEVICE, RF_ENOMEM, RF_ENOTFOUND = range(7)
+RF_SHA_NO_SOLO = 1
+RF_SHA_ALL_SOLO = 2
+
+# Every symbol include/reflow_hip.h declares (checked by tests/test_capi_symbols.py).
+EXPORTS = [
+    "rf_init", "rf_destroy", "rf_last_error", "rf_device_count", "rf_sync", "rf_version",
+    "rf_sha256_batch", "rf_sha256_arena", "rf_sha_plan_create", "rf_sha_plan_run",
+    "rf_sha_plan_stats", "rf_sha_plan_destroy", "rf_gen_fill", "rf_fileset_digest_batch",
+    "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
+    "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
+    "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
+    "rf_bloom_destroy", "rf_bloom_probe", "rf_bloom_probe_device", "rf_bloom_add",
+    "rf_bloom_add_device", "rf_bloom_params", "rf_bloom_words",
+]
+
+
+class RfError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("rf error %d: %s" % (code, msg))
+        self.code = code
+
+
+class ShaStats(ctypes.Structure):
+    _fields_ = [("n_msgs", ctypes.c_uint64), ("n_solo", ctypes.c_uint64),
+                ("total_blocks", ctypes.c_uint64), ("max_blocks", ctypes.c_uint64),
+                ("total_bytes", ctypes.c_uint64), ("last_ms_lanes", ctypes.c_float),
+                ("last_ms_solo", ctypes.c_float), ("last_ms_total", ctypes.c_float)]
+
+
+class GraphDesc(ctypes.Structure):
+    _fields_ = [("n_jobs", ctypes.c_uint32), ("n_slots", ctypes.c_uint32),
+                ("out_slot", ctypes.c_void_p), ("tmpl_off", ctypes.c_void_p),
+                ("tmpl_len", ctypes.c_void_p), ("hole_ptr", ctypes.c_void_p),
+                ("hole_pos", ctypes.c_void_p), ("hole_slot", ctypes.c_void_p),
+                ("blob", ctypes.c_void_p), ("blob_len", ctypes.c_uint64)]
+
+
+class GraphStats(ctypes.Structure):
+    _fields_ = [("n_jobs", ctypes.c_uint32), ("n_slots", ctypes.c_uint32),
+                ("n_levels", ctypes.c_uint32), ("max_level_jobs", ctypes.c_uint32),
+                ("total_blocks", ctypes.c_uint64), ("hole_count", ctypes.c_uint64),
+                ("template_bytes", ctypes.c_uint64), ("last_recomputed", ctypes.c_uint64),
+                ("last_ms", ctypes.c_float)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libreflow_hip.so.  Raises if it was not built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libreflow_hip.so not built: run __graft_entry__.build() "
+                               "(make -C reflow_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        sigs = {
+            "rf_init": ([i32, vp], i32), "rf_destroy": ([vp], None),
+            "rf_last_error": ([], ctypes.c_char_p), "rf_device_count": ([vp], i32),
+            "rf_sync": ([vp], i32), "rf_version": ([], ctypes.c_char_p),
+            "rf_sha256_batch": ([vp, vp, vp, u64, vp], i32),
+            "rf_sha256_arena": ([vp, vp, vp, vp, u64, vp], i32),
+            "rf_sha_plan_create": ([vp, vp, vp, u64, u32, vp], i32),
+            "rf_sha_plan_run": ([vp, vp, vp, vp], i32),
+            "rf_sha_plan_stats": ([vp, vp], i32), "rf_sha_plan_destroy": ([vp], None),
+            "rf_gen_fill": ([vp, vp, vp, vp, u64, u64, u64, vp], i32),
+            "rf_fileset_digest_batch": ([vp, u64, vp, vp, vp, vp, vp, vp], i32),
+            "rf_graph_load": ([vp, vp, vp], i32), "rf_graph_destroy": ([vp], None),
+            "rf_graph_set_slots": ([vp, vp, vp, u32], i32),
+            "rf_graph_set_slots_device": ([vp, vp, vp, u32, vp], i32),
+            "rf_graph_recompute": ([vp, i32, vp], i32),
+            "rf_graph_recompute_async": ([vp, i32, vp], i32),
+            "rf_graph_get_slots": ([vp, vp, u32, vp], i32),
+            "rf_graph_stats_get": ([vp, vp], i32),
+            "rf_bloom_load": ([vp, u64, u64, vp, u64, u64, vp], i32),
+            "rf_bloom_load_json": ([vp, ctypes.c_char_p, ctypes.c_size_t, vp], i32),
+            "rf_bloom_load_binary": ([vp, vp, ctypes.c_size_t, vp], i32),
+            "rf_bloom_new": ([vp, u64, u64, vp], i32), "rf_bloom_destroy": ([vp], None),
+            "rf_bloom_probe": ([vp, vp, u64, vp], i32),
+            "rf_bloom_probe_device": ([vp, vp, u64, vp, vp], i32),
+            "rf_bloom_add": ([vp, vp, u64], i32),
+            "rf_bloom_add_device": ([vp, vp, u64, vp], i32),
+            "rf_bloom_params": ([vp, vp, vp, vp, vp], i32),
+            "rf_bloom_words": ([vp, vp, u64], i32),
+        }
+        for name, (args, res) in sigs.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != RF_OK:
+        raise RfError(rc, lib().rf_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    rc = lib().rf_device_count(ctypes.byref(n))
+    return n.value if rc == RF_OK else 0
+
+
+class Context:
+    """One rf_ctx bound to one HIP device (one process per GPU)."""
+
+    def __init__(self, device=0):
+        self._h = ctypes.c_void_p()
+        _check(lib().rf_init(device, ctypes.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().rf_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def sync(self):
+        _check(lib().rf_sync(self._h))
+
+    # ---- K1 -----------------------------------------------------------
+    def sha256_batch(self, msgs):
+        """SHA-256 of each bytes object (Digester.FromBytes, batched)."""
+        n = len(msgs)
+        if n == 0:
+            return []
+        bufs = [ctypes.create_string_buffer(bytes(m), max(len(m), 1)) for m in msgs]
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        lens = np.array([len(m) for m in msgs], dtype=np.uint64)
+        out = np.zeros(32 * n, dtype=np.uint8)
+        _check(lib().rf_sha256_batch(self._h, ptrs, _ptr(lens), n, _ptr(out)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+    def sha256_arena(self, arena: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> np.ndarray:
+        n = len(lens)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        _check(lib().rf_sha256_arena(self._h, _ptr(arena), _ptr(offs), _ptr(lens), n, _ptr(out)))
+        return out
+
+    def sha_plan(self, offs, lens, flags=0):
+        return ShaPlan(self, offs, lens, flags)
+
+    def gen_fill(self, d_arena, d_offs, d_lens, n, seed, arena_bytes, stream=None):
+        _check(lib().rf_gen_fill(self._h, d_arena, d_offs, d_lens, n, seed & (2**64 - 1),
+                                 arena_bytes, stream))
+
+    # ---- Fileset --------------------------------------------------------
+    def fileset_digest_batch(self, sets):
+        """sets: list of filesets, each a list of groups (a Map is one group,
+        a List its flattened Map leaves); a group is a list of (path, id32)."""
+        set_group = [0]
+        group_entry = [0]
+        paths, ids = [], []
+        for groups in sets:
+            for g in groups:
+                for path, id32 in g:
+                    paths.append(path.encode() if isinstance(path, str) else path)
+                    ids.append(id32)
+                group_entry.append(len(paths))
+            set_group.append(len(group_entry) - 1)
+        n = len(sets)
+        sg = np.array(set_group, dtype=np.uint64)
+        ge = np.array(group_entry, dtype=np.uint64)
+        pb = [ctypes.create_string_buffer(p, max(len(p), 1)) for p in paths]
+        pp = (ctypes.c_void_p * max(len(paths), 1))(*[ctypes.addressof(b) for b in pb])
+        pl = np.array([len(p) for p in paths] or [0], dtype=np.uint32)
+        idb = np.frombuffer(b"".join(ids) or b"\0" * 32, dtype=np.uint8).copy()
+        out = np.zeros(32 * n, dtype=np.uint8)
+        _check(lib().rf_fileset_digest_batch(self._h, n, _ptr(sg), _ptr(ge), pp, _ptr(pl),
+                                             _ptr(idb), _ptr(out)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+
+class ShaPlan:
+    def __init__(self, ctx: Context, offs, lens, flags=0):
+        self.ctx = ctx
+        self._offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        self._lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        self._h = ctypes.c_void_p()
+        _check(lib().rf_sha_plan_create(ctx.handle, _ptr(self._offs), _ptr(self._lens),
+                                        len(self._lens), flags, ctypes.byref(self._h)))
+
+    def run(self, d_arena: int, d_out: int, stream=None):
+        _check(lib().rf_sha_plan_run(self._h, d_arena, d_out, stream))
+
+    def stats(self) -> ShaStats:
+        s = ShaStats()
+        _check(lib().rf_sha_plan_stats(self._h, ctypes.byref(s)))
+        return s
+
+    def close(self):
+        if self._h:
+            lib().rf_sha_plan_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Graph:
+    """rf_graph: jobs over digest slots (see include/reflow_hip.h)."""
+
+    def __init__(self, ctx: Context, n_slots, out_slot, tmpl_off, tmpl_len, hole_ptr, hole_pos,
+                 hole_slot, blob: bytes | np.ndarray):
+        self.ctx = ctx
+        self._keep = dict(
+            out_slot=np.ascontiguousarray(out_slot, dtype=np.uint32),
+            tmpl_off=np.ascontiguousarray(tmpl_off, dtype=np.uint64),
+            tmpl_len=np.ascontiguousarray(tmpl_len, dtype=np.uint32),
+            hole_ptr=np.ascontiguousarray(hole_ptr, dtype=np.uint64),
+            hole_pos=np.ascontiguousarray(hole_pos, dtype=np.uint32),
+            hole_slot=np.ascontiguousarray(hole_slot, dtype=np.uint32),
+            blob=np.frombuffer(bytes(blob), dtype=np.uint8) if isinstance(blob, (bytes, bytearray))
+            else np.ascontiguousarray(blob, dtype=np.uint8),
+        )
+        k = self._keep
+        d = GraphDesc(len(k["out_slot"]), n_slots, _ptr(k["out_slot"]), _ptr(k["tmpl_off"]),
+                      _ptr(k["tmpl_len"]), _ptr(k["hole_ptr"]),
+                      _ptr(k["hole_pos"]) if len(k["hole_pos"]) else None,
+                      _ptr(k["hole_slot"]) if len(k["hole_slot"]) else None,
+                      _ptr(k["blob"]) if len(k["blob"]) else None, len(k["blob"]))
+        self._h = ctypes.c_void_p()
+        _check(lib().rf_graph_load(ctx.handle, ctypes.byref(d), ctypes.byref(self._h)))
+        self._keep = None  # not retained by the library
+
+    def set_slots(self, slots, digests: np.ndarray):
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        dg = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1)
+        _check(lib().rf_graph_set_slots(self._h, _ptr(slots), _ptr(dg), len(slots)))
+
+    def set_slots_device(self, d_slots, d_digests, n, stream=None):
+        _check(lib().rf_graph_set_slots_device(self._h, d_slots, d_digests, n, stream))
+
+    def recompute(self, full=False) -> int:
+        n = ctypes.c_uint64(0)
+        _check(lib().rf_graph_recompute(self._h, 1 if full else 0, ctypes.byref(n)))
+        return n.value
+
+    def recompute_async(self, full=False, stream=None):
+        _check(lib().rf_graph_recompute_async(self._h, 1 if full else 0, stream))
+
+    def get_slots(self, slots) -> np.ndarray:
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        out = np.zeros((len(slots), 32), dtype=np.uint8)
+        _check(lib().rf_graph_get_slots(self._h, _ptr(slots), len(slots), _ptr(out)))
+        return out
+
+    def stats(self) -> GraphStats:
+        s = GraphStats()
+        _check(lib().rf_graph_stats_get(self._h, ctypes.byref(s)))
+        return s
+
+    def close(self):
+        if self._h:
+            lib().rf_graph_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Bloom:
+    """rf_bloom: device-resident willf/bloom filter with bloomlive semantics."""
+
+    def __init__(self, ctx: Context, handle):
+        self.ctx = ctx
+        self._h = handle
+
+    @classmethod
+    def load(cls, ctx, m, k, words: np.ndarray, length):
+        h = ctypes.c_void_p()
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        _check(lib().rf_bloom_load(ctx.handle, m, k, _ptr(w) if len(w) else None, len(w), length,
+                                   ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def new(cls, ctx, m, k):
+        h = ctypes.c_void_p()
+        _check(lib().rf_bloom_new(ctx.handle, m, k, ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_json(cls, ctx, js: bytes):
+        h = ctypes.c_void_p()
+        _check(lib().rf_bloom_load_json(ctx.handle, js, len(js), ctypes.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_binary(cls, ctx, buf: bytes):
+        h = ctypes.c_void_p()
+        b = np.frombuffer(buf, dtype=np.uint8).copy()
+        _check(lib().rf_bloom_load_binary(ctx.handle, _ptr(b), len(b), ctypes.byref(h)))
+        return cls(ctx, h)
+
+    def probe(self, digests: np.ndarray) -> np.ndarray:
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1)
+        n = len(d) // 32
+        out = np.zeros(n, dtype=np.uint8)
+        _check(lib().rf_bloom_probe(self._h, _ptr(d), n, _ptr(out)))
+        return out
+
+    def probe_device(self, d_digests, n, d_out, stream=None):
+        _check(lib().rf_bloom_probe_device(self._h, d_digests, n, d_out, stream))
+
+    def add(self, digests: np.ndarray):
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1)
+        _check(lib().rf_bloom_add(self._h, _ptr(d), len(d) // 32))
+
+    def add_device(self, d_digests, n, stream=None):
+        _check(lib().rf_bloom_add_device(self._h, d_digests, n, stream))
+
+    def params(self):
+        m, k, ln, nw = (ctypes.c_uint64() for _ in range(4))
+        _check(lib().rf_bloom_params(self._h, ctypes.byref(m), ctypes.byref(k), ctypes.byref(ln),
+                                     ctypes.byref(nw)))
+        return m.value, k.value, ln.value, nw.value
+
+    def words(self) -> np.ndarray:
+        _, _, _, nw = self.params()
+        out = np.zeros(nw, dtype=np.uint64)
+        _check(lib().rf_bloom_words(self._h, _ptr(out) if nw else None, nw))
+        return out
+
+    def close(self):
+        if self._h:
+            lib().rf_bloom_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,969 @@
+// capi.cpp -- implementation of include/reflow_hip.h (the drop-in C-ABI).
+//
+// Host-side runtime around the gfx950 kernels: contexts and streams, the K1
+// planner (largest-first order, lane- vs wave-per-message split), the
+// Fileset material builder (executor.go:214-233), the digest-DAG loader
+// (levels, reverse edges, padded templates) and the bloom wire formats
+// (bloom.go:264-325, bitset.go:628-721).  No CPU fallback: every digest is
+// computed by a HIP kernel; a missing device or code object is RF_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "reflow_hip.h"
+
+using namespace rf;
+
+// ---------------------------------------------------------------------------
+// errors
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPC(x)                                                                              \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return fail(RF_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+#define ARG(cond, msg)                                   \
+    do {                                                 \
+        if (!(cond)) return fail(RF_EINVAL, "%s", msg); \
+    } while (0)
+
+extern "C" const char* rf_last_error(void) { return g_err.c_str(); }
+extern "C" const char* rf_version(void) { return "reflow-hip 0.1 gfx950"; }
+
+// ---------------------------------------------------------------------------
+// device buffers
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostBuf {  // pinned staging
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1 << 16);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
+};
+
+struct rf_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    DevBuf d_arena, d_out, d_tmp;
+    HostBuf h_stage;
+};
+
+struct DevGuard {
+    explicit DevGuard(int d) { (void)hipSetDevice(d); }
+};
+
+extern "C" int rf_device_count(int* n) {
+    ARG(n, "null out");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *n = 0;
+        return fail(RF_EDEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *n = c;
+    return RF_OK;
+}
+
+extern "C" int rf_init(int device, rf_ctx** out) {
+    ARG(out, "null out");
+    *out = nullptr;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess || c == 0)
+        return fail(RF_EDEVICE, "no HIP device (%s)", hipGetErrorString(e));
+    if (device < 0 || device >= c) return fail(RF_EINVAL, "device %d out of range [0,%d)", device, c);
+    HIPC(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPC(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RF_EDEVICE, "device %d is %s; this library is built for gfx950 only", device,
+                    prop.gcnArchName);
+    e = probe_kernels();
+    if (e != hipSuccess)
+        return fail(RF_EDEVICE, "gfx950 code object not loadable: %s", hipGetErrorString(e));
+    rf_ctx* ctx = new rf_ctx();
+    ctx->device = device;
+    ctx->n_cu = prop.multiProcessorCount;
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(RF_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = ctx;
+    return RF_OK;
+}
+
+extern "C" void rf_destroy(rf_ctx* ctx) {
+    if (!ctx) return;
+    DevGuard g(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->d_arena.release();
+    ctx->d_out.release();
+    ctx->d_tmp.release();
+    ctx->h_stage.release();
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" int rf_sync(rf_ctx* ctx) {
+    ARG(ctx, "null ctx");
+    DevGuard g(ctx->device);
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+static hipStream_t pick(rf_ctx* ctx, void* stream) {
+    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+// ---------------------------------------------------------------------------
+// K1 planner
+struct rf_sha_plan {
+    rf_ctx* ctx = nullptr;
+    uint64_t n = 0;
+    uint32_t n_lanes = 0, n_solo = 0, grid = 0, n_shards = 1;
+    DevBuf d_offs, d_lens, d_order, d_heads;  // d_order = [lanes order | solo order]
+    hipStream_t side = nullptr;
+    hipEvent_t e0 = nullptr, e_solo = nullptr, e_lanes = nullptr, e1 = nullptr;
+    bool ran = false;
+    rf_sha_stats st{};
+};
+
+// Cycle model used only to decide lane- vs wave-per-message:
+// a lane retires one block per ~1464 issued instructions; a wave alone on its
+// SIMD issues one instruction per 4 cycles; the chip issues one wave-
+// instruction per 2 cycles per SIMD.  The solo chain issues ~920 per block.
+static void plan_split(const std::vector<uint64_t>& nb, std::vector<uint32_t>& order, uint32_t n_cu,
+                       uint32_t flags, uint32_t* n_solo_out) {
+    const uint64_t n = nb.size();
+    order.resize(n);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return nb[a] > nb[b]; });
+    uint32_t n_solo = 0;
+    if (flags & RF_SHA_ALL_SOLO) {
+        n_solo = (uint32_t)n;
+    } else if (!(flags & RF_SHA_NO_SOLO)) {
+        const double n_simd = 4.0 * n_cu;
+        const uint64_t cap = (uint64_t)n_cu * 4;
+        double remaining = 0;
+        for (uint64_t i = 0; i < n; ++i) remaining += (double)nb[i];
+        for (uint64_t i = 0; i < n && n_solo < cap; ++i) {
+            const double b = (double)nb[order[i]];
+            if (b < 1024) break;
+            const double t_lane = b * 1464.0 * 4.0;
+            const double t_rest = (remaining - b) * 1464.0 * 2.0 / (n_simd * 64.0);
+            if (t_lane <= t_rest) break;
+            remaining -= b;
+            ++n_solo;
+        }
+    }
+    // solo messages go to the back of `order`: [lanes..., solo...]
+    std::vector<uint32_t> o2;
+    o2.reserve(n);
+    for (uint64_t i = n_solo; i < n; ++i) o2.push_back(order[i]);
+    for (uint64_t i = 0; i < n_solo; ++i) o2.push_back(order[i]);
+    order.swap(o2);
+    *n_solo_out = n_solo;
+}
+
+static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens, uint64_t n,
+                              uint32_t flags, rf_sha_plan** out) {
+    ARG(ctx && out, "null argument");
+    ARG(n == 0 || (offs && lens), "null offs/lens");
+    ARG(n < 0xffffffffull, "too many messages");
+    *out = nullptr;
+    DevGuard g(ctx->device);
+    std::vector<uint64_t> nb(n);
+    uint64_t total_blocks = 0, max_blocks = 0, total_bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offs[i] % 16) return fail(RF_EINVAL, "offs[%llu] not 16-byte aligned", (unsigned long long)i);
+        nb[i] = (lens[i] + 9 + 63) / 64;
+        total_blocks += nb[i];
+        max_blocks = std::max(max_blocks, nb[i]);
+        total_bytes += lens[i];
+    }
+    auto* p = new rf_sha_plan();
+    p->ctx = ctx;
+    p->n = n;
+    std::vector<uint32_t> order;
+    uint32_t n_solo = 0;
+    plan_split(nb, order, (uint32_t)ctx->n_cu, flags, &n_solo);
+    p->n_solo = n_solo;
+    p->n_lanes = (uint32_t)(n - n_solo);
+    // The lanes kernel is persistent: enough 256-thread blocks for every lane
+    // message, capped at 5 blocks per CU (its VGPR-limited residency).
+    const uint64_t want = (p->n_lanes + sha_lanes_block() - 1) / sha_lanes_block();
+    p->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->n_cu * 5));
+    p->n_shards = std::max<uint32_t>(1, std::min<uint32_t>(64, p->grid * 4));
+    hipError_t e = hipSuccess;
+    if ((e = p->d_offs.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
+        (e = p->d_lens.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
+        (e = p->d_order.ensure(4 * std::max<uint64_t>(n, 1))) != hipSuccess ||
+        (e = p->d_heads.ensure(4 * 64)) != hipSuccess) {
+        delete p;
+        return fail(RF_ENOMEM, "plan alloc: %s", hipGetErrorString(e));
+    }
+    if (n) {
+        HIPC(hipMemcpy(p->d_offs.p, offs, 8 * n, hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(p->d_lens.p, lens, 8 * n, hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(p->d_order.p, order.data(), 4 * n, hipMemcpyHostToDevice));
+    }
+    HIPC(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+    HIPC(hipEventCreate(&p->e0));
+    HIPC(hipEventCreate(&p->e_solo));
+    HIPC(hipEventCreate(&p->e_lanes));
+    HIPC(hipEventCreate(&p->e1));
+    p->st.n_msgs = n;
+    p->st.n_solo = n_solo;
+    p->st.total_blocks = total_blocks;
+    p->st.max_blocks = max_blocks;
+    p->st.total_bytes = total_bytes;
+    *out = p;
+    return RF_OK;
+}
+
+extern "C" int rf_sha_plan_create(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens,
+                                  uint64_t n, uint32_t flags, rf_sha_plan** out) {
+    ARG(ctx, "null ctx");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return plan_create_nolock(ctx, offs, lens, n, flags, out);
+}
+
+static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hipStream_t s) {
+    HIPC(hipEventRecord(p->e0, s));
+    HIPC(hipMemsetAsync(p->d_heads.p, 0, 4 * 64, s));
+    const uint32_t* order = p->d_order.as<uint32_t>();
+    if (p->n_solo) {
+        HIPC(hipStreamWaitEvent(p->side, p->e0, 0));
+        SoloArgs sa{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(),
+                    p->d_lens.as<uint64_t>(), order + p->n_lanes, p->n_solo,
+                    static_cast<uint8_t*>(d_out)};
+        HIPC(launch_sha_solo(sa, p->side));
+        HIPC(hipEventRecord(p->e_solo, p->side));
+    }
+    if (p->n_lanes) {
+        LanesArgs la{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(),
+                     p->d_lens.as<uint64_t>(), order, p->n_lanes, p->n_shards,
+                     p->d_heads.as<uint32_t>(), static_cast<uint8_t*>(d_out)};
+        HIPC(launch_sha_lanes(la, p->grid, s));
+    }
+    HIPC(hipEventRecord(p->e_lanes, s));
+    if (p->n_solo) HIPC(hipStreamWaitEvent(s, p->e_solo, 0));
+    HIPC(hipEventRecord(p->e1, s));
+    p->ran = true;
+    return RF_OK;
+}
+
+extern "C" int rf_sha_plan_run(rf_sha_plan* p, const void* d_arena, void* d_out32, void* stream) {
+    ARG(p, "null plan");
+    ARG(p->n == 0 || (d_arena && d_out32), "null device buffer");
+    std::lock_guard<std::mutex> lk(p->ctx->mu);
+    DevGuard g(p->ctx->device);
+    return plan_run_locked(p, d_arena, d_out32, pick(p->ctx, stream));
+}
+
+extern "C" int rf_sha_plan_stats(rf_sha_plan* p, rf_sha_stats* out) {
+    ARG(p && out, "null argument");
+    DevGuard g(p->ctx->device);
+    if (p->ran) {
+        HIPC(hipEventSynchronize(p->e1));
+        float ms = 0;
+        HIPC(hipEventElapsedTime(&ms, p->e0, p->e1));
+        p->st.last_ms_total = ms;
+        HIPC(hipEventElapsedTime(&ms, p->e0, p->e_lanes));
+        p->st.last_ms_lanes = p->n_lanes ? ms : 0.f;
+        if (p->n_solo) {
+            HIPC(hipEventElapsedTime(&ms, p->e0, p->e_solo));
+            p->st.last_ms_solo = ms;
+        } else {
+            p->st.last_ms_solo = 0.f;
+        }
+    }
+    *out = p->st;
+    return RF_OK;
+}
+
+extern "C" void rf_sha_plan_destroy(rf_sha_plan* p) {
+    if (!p) return;
+    DevGuard g(p->ctx->device);
+    if (p->side) {
+        (void)hipStreamSynchronize(p->side);
+        (void)hipStreamDestroy(p->side);
+    }
+    for (hipEvent_t ev : {p->e0, p->e_solo, p->e_lanes, p->e1})
+        if (ev) (void)hipEventDestroy(ev);
+    p->d_offs.release();
+    p->d_lens.release();
+    p->d_order.release();
+    p->d_heads.release();
+    delete p;
+}
+
+// Host-buffer batch: pack into pinned staging with 64-B aligned starts,
+// upload, plan, run, download.
+static int sha_host_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
+                           const std::vector<uint64_t>& lens, uint64_t arena_bytes,
+                           uint8_t* out32) {
+    const uint64_t n = lens.size();
+    HIPC(ctx->d_arena.ensure(arena_bytes + 64));
+    HIPC(ctx->d_out.ensure(32 * n));
+    HIPC(hipMemcpyAsync(ctx->d_arena.p, ctx->h_stage.p, arena_bytes, hipMemcpyHostToDevice,
+                        ctx->stream));
+    rf_sha_plan* p = nullptr;
+    int rc = plan_create_nolock(ctx, offs.data(), lens.data(), n, 0, &p);
+    if (rc) return rc;
+    rc = plan_run_locked(p, ctx->d_arena.p, ctx->d_out.p, ctx->stream);
+    if (rc == RF_OK) {
+        hipError_t e = hipMemcpyAsync(out32, ctx->d_out.p, 32 * n, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) rc = fail(RF_EDEVICE, "sha256 batch: %s", hipGetErrorString(e));
+    }
+    rf_sha_plan_destroy(p);
+    return rc;
+}
+
+extern "C" int rf_sha256_batch(rf_ctx* ctx, const uint8_t* const* msgs, const uint64_t* lens,
+                               uint64_t n, uint8_t* out32) {
+    ARG(ctx && (n == 0 || (msgs && lens && out32)), "null argument");
+    if (n == 0) return RF_OK;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard g(ctx->device);
+    std::vector<uint64_t> offs(n), ls(lens, lens + n);
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        ARG(msgs[i] || lens[i] == 0, "null message with nonzero length");
+        offs[i] = pos;
+        pos += (lens[i] + 63) & ~63ull;
+    }
+    HIPC(ctx->h_stage.ensure(pos + 64));
+    for (uint64_t i = 0; i < n; ++i)
+        if (lens[i]) memcpy(ctx->h_stage.bytes() + offs[i], msgs[i], lens[i]);
+    return sha_host_packed(ctx, offs, ls, pos, out32);
+}
+
+extern "C" int rf_sha256_arena(rf_ctx* ctx, const uint8_t* arena, const uint64_t* offs,
+                               const uint64_t* lens, uint64_t n, uint8_t* out32) {
+    ARG(ctx && (n == 0 || (arena && offs && lens && out32)), "null argument");
+    if (n == 0) return RF_OK;
+    std::vector<const uint8_t*> ptrs(n);
+    for (uint64_t i = 0; i < n; ++i) ptrs[i] = arena + offs[i];
+    return rf_sha256_batch(ctx, ptrs.data(), lens, n, out32);
+}
+
+extern "C" int rf_gen_fill(rf_ctx* ctx, void* d_arena, const uint64_t* d_offs,
+                           const uint64_t* d_lens, uint64_t n, uint64_t seed, uint64_t arena_bytes,
+                           void* stream) {
+    ARG(ctx && d_arena && (n == 0 || (d_offs && d_lens)), "null argument");
+    ARG(arena_bytes % 16 == 0, "arena_bytes must be a multiple of 16");
+    DevGuard g(ctx->device);
+    HIPC(launch_gen_fill(static_cast<uint8_t*>(d_arena), d_offs, d_lens, n, seed, arena_bytes,
+                         pick(ctx, stream)));
+    return RF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Fileset digest (executor.go:205-233)
+extern "C" int rf_fileset_digest_batch(rf_ctx* ctx, uint64_t n_sets, const uint64_t* set_group,
+                                       const uint64_t* group_entry, const char* const* paths,
+                                       const uint32_t* path_lens, const uint8_t* ids32,
+                                       uint8_t* out32) {
+    ARG(ctx && set_group && out32, "null argument");
+    if (n_sets == 0) return RF_OK;
+    const uint64_t n_groups = set_group[n_sets];
+    ARG(n_groups == 0 || group_entry, "null group_entry");
+    const uint64_t n_entries = n_groups ? group_entry[n_groups] : 0;
+    ARG(n_entries == 0 || (paths && path_lens && ids32), "null entries");
+    std::vector<uint64_t> offs(n_sets), lens(n_sets);
+    std::vector<uint32_t> idx;
+    std::vector<uint8_t> mat;
+    // material of set s = Σ over its groups, entries sorted bytewise:
+    // path ‖ 0x00 0x05 ‖ id
+    std::vector<uint8_t> arena;
+    for (uint64_t s = 0; s < n_sets; ++s) {
+        ARG(set_group[s] <= set_group[s + 1], "set_group not monotone");
+        offs[s] = arena.size();
+        for (uint64_t gi = set_group[s]; gi < set_group[s + 1]; ++gi) {
+            ARG(group_entry[gi] <= group_entry[gi + 1], "group_entry not monotone");
+            idx.resize(group_entry[gi + 1] - group_entry[gi]);
+            std::iota(idx.begin(), idx.end(), (uint32_t)group_entry[gi]);
+            std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+                const size_t la = path_lens[a], lb = path_lens[b];
+                const int c = memcmp(paths[a], paths[b], std::min(la, lb));
+                return c < 0 || (c == 0 && la < lb);
+            });
+            for (uint32_t e : idx) {
+                arena.insert(arena.end(), paths[e], paths[e] + path_lens[e]);
+                arena.push_back(0x00);
+                arena.push_back(0x05);
+                arena.insert(arena.end(), ids32 + 32ull * e, ids32 + 32ull * e + 32);
+            }
+        }
+        lens[s] = arena.size() - offs[s];
+    }
+    if (arena.empty()) arena.push_back(0);
+    return rf_sha256_arena(ctx, arena.data(), offs.data(), lens.data(), n_sets, out32);
+}
+
+// ---------------------------------------------------------------------------
+// Digest DAG
+struct rf_graph {
+    rf_ctx* ctx = nullptr;
+    GraphDev g;
+    std::vector<int64_t> producer;   // slot -> external job or -1
+    std::vector<uint32_t> ext2int;   // external job id -> internal
+    bool initialized = false;
+    DevBuf b_job_slot, b_job_off, b_job_nblk, b_hole_ptr, b_hole_pos, b_hole_slot, b_cons_ptr,
+        b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_counts, b_tmp_idx, b_tmp_dig;
+    uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
+    uint32_t max_level_jobs = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool timed = false;
+};
+
+extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out) {
+    ARG(ctx && d && out, "null argument");
+    *out = nullptr;
+    const uint32_t J = d->n_jobs, S = d->n_slots;
+    ARG(J == 0 || (d->out_slot && d->tmpl_off && d->tmpl_len && d->hole_ptr), "null job arrays");
+    ARG(d->hole_ptr == nullptr || d->hole_ptr[0] == 0 || J == 0, "hole_ptr[0] must be 0");
+    const uint64_t H = J ? d->hole_ptr[J] : 0;
+    ARG(H == 0 || (d->hole_pos && d->hole_slot), "null hole arrays");
+    ARG(H < 0xffffffffull, "too many holes");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    auto* gr = new rf_graph();
+    std::unique_ptr<rf_graph, void (*)(rf_graph*)> guard(gr, [](rf_graph* x) { rf_graph_destroy(x); });
+    gr->ctx = ctx;
+    gr->producer.assign(S, -1);
+    std::vector<uint32_t> nblk(J);
+    for (uint32_t j = 0; j < J; ++j) {
+        const uint32_t s = d->out_slot[j];
+        if (s >= S) return fail(RF_EINVAL, "job %u: out_slot %u >= n_slots %u", j, s, S);
+        if (gr->producer[s] >= 0) return fail(RF_EINVAL, "slot %u written by jobs %lld and %u", s,
+                                              (long long)gr->producer[s], j);
+        gr->producer[s] = j;
+        if (d->tmpl_off[j] + d->tmpl_len[j] > d->blob_len)
+            return fail(RF_EINVAL, "job %u: template outside blob", j);
+        if (d->hole_ptr[j + 1] < d->hole_ptr[j]) return fail(RF_EINVAL, "hole_ptr not monotone");
+        uint64_t last_end = 0;
+        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) {
+            if (d->hole_slot[h] >= S) return fail(RF_EINVAL, "job %u: hole slot out of range", j);
+            if ((uint64_t)d->hole_pos[h] + 32 > d->tmpl_len[j])
+                return fail(RF_EINVAL, "job %u: hole past template end", j);
+            if (h > d->hole_ptr[j] && d->hole_pos[h] < last_end)
+                return fail(RF_EINVAL, "job %u: holes unsorted or overlapping", j);
+            last_end = (uint64_t)d->hole_pos[h] + 32;
+        }
+        nblk[j] = (uint32_t)((d->tmpl_len[j] + 9 + 63) / 64);
+    }
+    // topological levels (Kahn)
+    std::vector<uint32_t> indeg(J, 0), level(J, 0);
+    std::vector<uint64_t> cptr(S + 1, 0);  // slot -> consumer jobs (external ids)
+    for (uint64_t h = 0; h < H; ++h) cptr[d->hole_slot[h] + 1]++;
+    for (uint32_t s = 0; s < S; ++s) cptr[s + 1] += cptr[s];
+    std::vector<uint32_t> cjob(H);
+    {
+        std::vector<uint64_t> fillp(cptr.begin(), cptr.end() - 1);
+        for (uint32_t j = 0; j < J; ++j)
+            for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) {
+                const uint32_t s = d->hole_slot[h];
+                cjob[fillp[s]++] = j;
+                if (gr->producer[s] >= 0) indeg[j]++;
+            }
+    }
+    std::vector<uint32_t> q;
+    q.reserve(J);
+    for (uint32_t j = 0; j < J; ++j)
+        if (!indeg[j]) q.push_back(j);
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+        const uint32_t j = q[qi], s = d->out_slot[j];
+        for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
+            const uint32_t k = cjob[c];
+            level[k] = std::max(level[k], level[j] + 1);
+            if (--indeg[k] == 0) q.push_back(k);
+        }
+    }
+    if (q.size() != J) return fail(RF_EINVAL, "job graph has a cycle (%zu of %u jobs ordered)", q.size(), J);
+    uint32_t L = 0;
+    for (uint32_t j = 0; j < J; ++j) L = std::max(L, level[j] + 1);
+    // internal order: level ascending, blocks descending (similar lanes per wave)
+    std::vector<uint32_t> perm(J);
+    std::iota(perm.begin(), perm.end(), 0u);
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+        return level[a] != level[b] ? level[a] < level[b] : nblk[a] > nblk[b];
+    });
+    gr->ext2int.assign(J, 0);
+    for (uint32_t i = 0; i < J; ++i) gr->ext2int[perm[i]] = i;
+    gr->g.lvl_start.assign(L + 1, 0);
+    for (uint32_t j = 0; j < J; ++j) gr->g.lvl_start[level[j] + 1]++;
+    for (uint32_t l = 0; l < L; ++l) {
+        gr->max_level_jobs = std::max(gr->max_level_jobs, gr->g.lvl_start[l + 1]);
+        gr->g.lvl_start[l + 1] += gr->g.lvl_start[l];
+    }
+    // host arrays in internal order; padded templates
+    std::vector<uint32_t> job_slot(J), job_nblk(J), hole_ptr(J + 1, 0), hole_pos(H), hole_slot(H);
+    std::vector<uint64_t> job_off(J);
+    uint64_t tb = 0;
+    for (uint32_t i = 0; i < J; ++i) {
+        const uint32_t j = perm[i];
+        job_slot[i] = d->out_slot[j];
+        job_nblk[i] = nblk[j];
+        job_off[i] = tb;
+        tb += 64ull * nblk[j];
+        gr->total_blocks += nblk[j];
+        const uint64_t hs = d->hole_ptr[j], he = d->hole_ptr[j + 1];
+        hole_ptr[i + 1] = hole_ptr[i] + (uint32_t)(he - hs);
+        for (uint64_t h = hs; h < he; ++h) {
+            hole_pos[hole_ptr[i] + (h - hs)] = d->hole_pos[h];
+            hole_slot[hole_ptr[i] + (h - hs)] = d->hole_slot[h];
+        }
+    }
+    std::vector<uint8_t> tmpl(std::max<uint64_t>(tb, 64), 0);
+    for (uint32_t i = 0; i < J; ++i) {
+        const uint32_t j = perm[i];
+        uint8_t* t = tmpl.data() + job_off[i];
+        const uint64_t len = d->tmpl_len[j];
+        if (len) memcpy(t, d->blob + d->tmpl_off[j], len);
+        t[len] = 0x80;
+        const uint64_t bits = len * 8;
+        uint8_t* e = t + 64ull * job_nblk[i];
+        for (int b = 0; b < 8; ++b) e[-1 - b] = (uint8_t)(bits >> (8 * b));
+    }
+    std::vector<uint32_t> cons_ptr(S + 1), cons_job(H);
+    for (uint32_t s = 0; s <= S; ++s) cons_ptr[s] = (uint32_t)cptr[s];
+    for (uint64_t c = 0; c < H; ++c) cons_job[c] = gr->ext2int[cjob[c]];
+    gr->hole_count = H;
+    gr->tmpl_bytes = tb;
+    // upload
+    GraphDev& G = gr->g;
+    G.n_jobs = J;
+    G.n_slots = S;
+    G.n_levels = L;
+    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
+        hipError_t e = b.ensure(std::max<size_t>(bytes, 64));
+        if (e != hipSuccess) return e;
+        return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
+    };
+    hipError_t e;
+    if ((e = up(gr->b_job_slot, job_slot.data(), 4ull * J)) != hipSuccess ||
+        (e = up(gr->b_job_off, job_off.data(), 8ull * J)) != hipSuccess ||
+        (e = up(gr->b_job_nblk, job_nblk.data(), 4ull * J)) != hipSuccess ||
+        (e = up(gr->b_hole_ptr, hole_ptr.data(), 4ull * (J + 1))) != hipSuccess ||
+        (e = up(gr->b_hole_pos, hole_pos.data(), 4ull * H)) != hipSuccess ||
+        (e = up(gr->b_hole_slot, hole_slot.data(), 4ull * H)) != hipSuccess ||
+        (e = up(gr->b_cons_ptr, cons_ptr.data(), 4ull * (S + 1))) != hipSuccess ||
+        (e = up(gr->b_cons_job, cons_job.data(), 4ull * H)) != hipSuccess ||
+        (e = up(gr->b_tmpl, tmpl.data(), tmpl.size())) != hipSuccess ||
+        (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
+        (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
+        (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
+        (e = gr->b_counts.ensure(4ull * (L + 1))) != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
+                    hipGetErrorString(e));
+    HIPC(hipMemset(gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
+    HIPC(hipMemset(gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
+    G.job_slot = gr->b_job_slot.as<uint32_t>();
+    G.job_off = gr->b_job_off.as<uint64_t>();
+    G.job_nblk = gr->b_job_nblk.as<uint32_t>();
+    G.hole_ptr = gr->b_hole_ptr.as<uint32_t>();
+    G.hole_pos = gr->b_hole_pos.as<uint32_t>();
+    G.hole_slot = gr->b_hole_slot.as<uint32_t>();
+    G.cons_ptr = gr->b_cons_ptr.as<uint32_t>();
+    G.cons_job = gr->b_cons_job.as<uint32_t>();
+    G.tmpl = gr->b_tmpl.as<uint8_t>();
+    G.slots = gr->b_slots.as<uint8_t>();
+    G.dirty = gr->b_dirty.as<uint32_t>();
+    G.list = gr->b_list.as<uint32_t>();
+    G.counts = gr->b_counts.as<uint32_t>();
+    HIPC(hipEventCreate(&gr->e0));
+    HIPC(hipEventCreate(&gr->e1));
+    guard.release();
+    *out = gr;
+    return RF_OK;
+}
+
+extern "C" void rf_graph_destroy(rf_graph* gr) {
+    if (!gr) return;
+    if (gr->ctx) {
+        DevGuard dg(gr->ctx->device);
+        for (DevBuf* b : {&gr->b_job_slot, &gr->b_job_off, &gr->b_job_nblk, &gr->b_hole_ptr,
+                          &gr->b_hole_pos, &gr->b_hole_slot, &gr->b_cons_ptr, &gr->b_cons_job,
+                          &gr->b_tmpl, &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_counts,
+                          &gr->b_tmp_idx, &gr->b_tmp_dig})
+            b->release();
+        if (gr->e0) (void)hipEventDestroy(gr->e0);
+        if (gr->e1) (void)hipEventDestroy(gr->e1);
+    }
+    delete gr;
+}
+
+static int graph_check_inputs(rf_graph* gr, const uint32_t* slots, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) {
+        if (slots[i] >= gr->g.n_slots) return fail(RF_EINVAL, "slot %u out of range", slots[i]);
+        if (gr->producer[slots[i]] >= 0)
+            return fail(RF_EINVAL, "slot %u is the output of job %lld", slots[i],
+                        (long long)gr->producer[slots[i]]);
+    }
+    return RF_OK;
+}
+
+extern "C" int rf_graph_set_slots(rf_graph* gr, const uint32_t* slots, const uint8_t* digests32,
+                                  uint32_t n) {
+    ARG(gr && (n == 0 || (slots && digests32)), "null argument");
+    if (!n) return RF_OK;
+    if (int rc = graph_check_inputs(gr, slots, n)) return rc;
+    rf_ctx* ctx = gr->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    HIPC(gr->b_tmp_idx.ensure(4ull * n));
+    HIPC(gr->b_tmp_dig.ensure(32ull * n));
+    HIPC(hipMemcpyAsync(gr->b_tmp_idx.p, slots, 4ull * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(hipMemcpyAsync(gr->b_tmp_dig.p, digests32, 32ull * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(launch_graph_mark_slots(gr->g, gr->b_tmp_idx.as<uint32_t>(), gr->b_tmp_dig.as<uint8_t>(), n,
+                                 ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, const void* d_digests32,
+                                         uint32_t n, void* stream) {
+    ARG(gr && (n == 0 || (d_slots && d_digests32)), "null argument");
+    DevGuard dg(gr->ctx->device);
+    HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
+                                 static_cast<const uint8_t*>(d_digests32), n, pick(gr->ctx, stream)));
+    return RF_OK;
+}
+
+static int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
+    GraphDev& G = gr->g;
+    if (!gr->initialized) full = 1;
+    const size_t dirty_bytes = 4ull * ((G.n_jobs + 31) / 32 + 1);
+    HIPC(hipEventRecord(gr->e0, s));
+    if (full) HIPC(hipMemsetAsync(G.dirty, 0xff, dirty_bytes, s));
+    HIPC(hipMemsetAsync(G.counts, 0, 4ull * (G.n_levels + 1), s));
+    for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
+    HIPC(hipMemsetAsync(G.dirty, 0, dirty_bytes, s));
+    HIPC(hipEventRecord(gr->e1, s));
+    gr->timed = true;
+    gr->initialized = true;
+    return RF_OK;
+}
+
+extern "C" int rf_graph_recompute_async(rf_graph* gr, int full, void* stream) {
+    ARG(gr, "null graph");
+    std::lock_guard<std::mutex> lk(gr->ctx->mu);
+    DevGuard dg(gr->ctx->device);
+    return graph_recompute_locked(gr, full, pick(gr->ctx, stream));
+}
+
+extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomputed) {
+    ARG(gr, "null graph");
+    rf_ctx* ctx = gr->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    if (int rc = graph_recompute_locked(gr, full, ctx->stream)) return rc;
+    std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
+    if (gr->g.n_levels)
+        HIPC(hipMemcpyAsync(counts.data(), gr->g.counts, 4ull * gr->g.n_levels,
+                            hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    uint64_t tot = 0;
+    for (uint32_t l = 0; l < gr->g.n_levels; ++l) tot += counts[l];
+    gr->last_recomputed = tot;
+    if (out_recomputed) *out_recomputed = tot;
+    return RF_OK;
+}
+
+extern "C" int rf_graph_get_slots(rf_graph* gr, const uint32_t* slots, uint32_t n, uint8_t* out32) {
+    ARG(gr && (n == 0 || (slots && out32)), "null argument");
+    if (!n) return RF_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (slots[i] >= gr->g.n_slots) return fail(RF_EINVAL, "slot %u out of range", slots[i]);
+    rf_ctx* ctx = gr->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    HIPC(gr->b_tmp_idx.ensure(4ull * n));
+    HIPC(gr->b_tmp_dig.ensure(32ull * n));
+    HIPC(hipMemcpyAsync(gr->b_tmp_idx.p, slots, 4ull * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(launch_gather_slots(gr->g.slots, gr->b_tmp_idx.as<uint32_t>(), n, gr->b_tmp_dig.as<uint8_t>(),
+                             ctx->stream));
+    HIPC(hipMemcpyAsync(out32, gr->b_tmp_dig.p, 32ull * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
+    ARG(gr && out, "null argument");
+    DevGuard dg(gr->ctx->device);
+    memset(out, 0, sizeof *out);
+    out->n_jobs = gr->g.n_jobs;
+    out->n_slots = gr->g.n_slots;
+    out->n_levels = gr->g.n_levels;
+    out->max_level_jobs = gr->max_level_jobs;
+    out->total_blocks = gr->total_blocks;
+    out->hole_count = gr->hole_count;
+    out->template_bytes = gr->tmpl_bytes;
+    out->last_recomputed = gr->last_recomputed;
+    if (gr->timed) {
+        HIPC(hipEventSynchronize(gr->e1));
+        HIPC(hipEventElapsedTime(&out->last_ms, gr->e0, gr->e1));
+    }
+    return RF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Bloom filter
+struct rf_bloom {
+    rf_ctx* ctx = nullptr;
+    BloomDev b;
+    DevBuf words, len_dev, keys, out;
+};
+
+static int bloom_make(rf_ctx* ctx, uint64_t m, uint64_t k, const uint64_t* words, uint64_t nwords,
+                      uint64_t length, rf_bloom** out) {
+    ARG(ctx && out, "null argument");
+    ARG(m >= 1, "bloom m must be >= 1 (location() divides by m)");
+    ARG(k < (1ull << 31), "bloom k too large");
+    // bitset words needed for `length` bits (bitset.go:89-94)
+    const uint64_t need = (length + 63) / 64;
+    ARG(nwords >= need, "fewer words than the bitset length needs");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    auto* bl = new rf_bloom();
+    bl->ctx = ctx;
+    // capacity: enough words for any location < m (Add may grow length to m)
+    const uint64_t cap = std::max<uint64_t>(std::max(nwords, (m + 63) / 64), 1);
+    hipError_t e;
+    if ((e = bl->words.ensure(8 * cap)) != hipSuccess || (e = bl->len_dev.ensure(8)) != hipSuccess) {
+        delete bl;
+        return fail(RF_ENOMEM, "bloom alloc: %s", hipGetErrorString(e));
+    }
+    HIPC(hipMemset(bl->words.p, 0, 8 * cap));
+    if (nwords && words) HIPC(hipMemcpy(bl->words.p, words, 8 * nwords, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(bl->len_dev.p, &length, 8, hipMemcpyHostToDevice));
+    bl->b.m = m;
+    bl->b.k = k;
+    bl->b.length = length;
+    bl->b.nwords = cap;
+    bl->b.words = bl->words.as<uint64_t>();
+    bl->b.len_dev = bl->len_dev.as<uint64_t>();
+    *out = bl;
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_load(rf_ctx* ctx, uint64_t m, uint64_t k, const uint64_t* words,
+                             uint64_t nwords, uint64_t length, rf_bloom** out) {
+    return bloom_make(ctx, m, k, words, nwords, length, out);
+}
+
+extern "C" int rf_bloom_new(rf_ctx* ctx, uint64_t m, uint64_t k, rf_bloom** out) {
+    // bloom.New: max(1,m), max(1,k), bitset.New(m) (length = m as given)
+    return bloom_make(ctx, std::max<uint64_t>(1, m), std::max<uint64_t>(1, k), nullptr, 0, m, out);
+}
+
+static uint64_t be64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+    return v;
+}
+
+static int bloom_from_bitset_bytes(rf_ctx* ctx, uint64_t m, uint64_t k, const uint8_t* p, size_t n,
+                                   rf_bloom** out) {
+    ARG(n >= 8, "truncated bitset");
+    const uint64_t length = be64(p);
+    const uint64_t nw = (length + 63) / 64;
+    ARG((n - 8) / 8 >= nw, "truncated bitset words");
+    std::vector<uint64_t> w(nw);
+    for (uint64_t i = 0; i < nw; ++i) w[i] = be64(p + 8 + 8 * i);
+    return bloom_make(ctx, m, k, w.data(), nw, length, out);
+}
+
+extern "C" int rf_bloom_load_binary(rf_ctx* ctx, const uint8_t* buf, size_t len, rf_bloom** out) {
+    ARG(buf && len >= 16, "truncated bloom binary");
+    return bloom_from_bitset_bytes(ctx, be64(buf), be64(buf + 8), buf + 16, len - 16, out);
+}
+
+static int b64url_val(char c) {
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    if (c == '-') return 62;
+    if (c == '_') return 63;
+    return -1;
+}
+
+static bool json_uint(const std::string& s, const char* key, uint64_t* v) {
+    const std::string k = std::string("\"") + key + "\"";
+    size_t p = s.find(k);
+    if (p == std::string::npos) return false;
+    p = s.find(':', p + k.size());
+    if (p == std::string::npos) return false;
+    ++p;
+    while (p < s.size() && isspace((unsigned char)s[p])) ++p;
+    if (p >= s.size() || !isdigit((unsigned char)s[p])) return false;
+    uint64_t x = 0;
+    while (p < s.size() && isdigit((unsigned char)s[p])) x = x * 10 + (uint64_t)(s[p++] - '0');
+    *v = x;
+    return true;
+}
+
+extern "C" int rf_bloom_load_json(rf_ctx* ctx, const char* json, size_t len, rf_bloom** out) {
+    ARG(json, "null json");
+    const std::string s(json, len);
+    uint64_t m = 0, k = 0;
+    ARG(json_uint(s, "m", &m) && json_uint(s, "k", &k), "bloom json: missing m or k");
+    size_t p = s.find("\"b\"");
+    ARG(p != std::string::npos, "bloom json: missing b");
+    p = s.find('"', s.find(':', p) + 1);
+    ARG(p != std::string::npos, "bloom json: b is not a string");
+    const size_t q = s.find('"', p + 1);
+    ARG(q != std::string::npos, "bloom json: unterminated b");
+    std::vector<uint8_t> bytes;
+    uint32_t acc = 0;
+    int nbits = 0;
+    for (size_t i = p + 1; i < q; ++i) {
+        const char c = s[i];
+        if (c == '=') break;
+        const int v = b64url_val(c);
+        ARG(v >= 0, "bloom json: bad base64url character");
+        acc = (acc << 6) | (uint32_t)v;
+        nbits += 6;
+        if (nbits >= 8) {
+            nbits -= 8;
+            bytes.push_back((uint8_t)(acc >> nbits));
+        }
+    }
+    return bloom_from_bitset_bytes(ctx, m, k, bytes.data(), bytes.size(), out);
+}
+
+extern "C" void rf_bloom_destroy(rf_bloom* bl) {
+    if (!bl) return;
+    DevGuard dg(bl->ctx->device);
+    bl->words.release();
+    bl->len_dev.release();
+    bl->keys.release();
+    bl->out.release();
+    delete bl;
+}
+
+extern "C" int rf_bloom_probe_device(rf_bloom* bl, const void* d_digests32, uint64_t n, void* d_out,
+                                     void* stream) {
+    ARG(bl && (n == 0 || (d_digests32 && d_out)), "null argument");
+    DevGuard dg(bl->ctx->device);
+    HIPC(launch_bloom_probe(bl->b, static_cast<const uint8_t*>(d_digests32), n,
+                            static_cast<uint8_t*>(d_out), pick(bl->ctx, stream)));
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_probe(rf_bloom* bl, const uint8_t* digests32, uint64_t n, uint8_t* out) {
+    ARG(bl && (n == 0 || (digests32 && out)), "null argument");
+    if (!n) return RF_OK;
+    rf_ctx* ctx = bl->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    HIPC(bl->keys.ensure(32 * n));
+    HIPC(bl->out.ensure(n));
+    HIPC(hipMemcpyAsync(bl->keys.p, digests32, 32 * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(launch_bloom_probe(bl->b, bl->keys.as<uint8_t>(), n, bl->out.as<uint8_t>(), ctx->stream));
+    HIPC(hipMemcpyAsync(out, bl->out.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_add_device(rf_bloom* bl, const void* d_digests32, uint64_t n, void* stream) {
+    ARG(bl && (n == 0 || d_digests32), "null argument");
+    DevGuard dg(bl->ctx->device);
+    HIPC(launch_bloom_add(bl->b, static_cast<const uint8_t*>(d_digests32), n, pick(bl->ctx, stream)));
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_add(rf_bloom* bl, const uint8_t* digests32, uint64_t n) {
+    ARG(bl && (n == 0 || digests32), "null argument");
+    if (!n) return RF_OK;
+    rf_ctx* ctx = bl->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    HIPC(bl->keys.ensure(32 * n));
+    HIPC(hipMemcpyAsync(bl->keys.p, digests32, 32 * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(launch_bloom_add(bl->b, bl->keys.as<uint8_t>(), n, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_params(rf_bloom* bl, uint64_t* m, uint64_t* k, uint64_t* length,
+                               uint64_t* nwords) {
+    ARG(bl, "null bloom");
+    DevGuard dg(bl->ctx->device);
+    uint64_t len = 0;
+    HIPC(hipMemcpy(&len, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
+    if (m) *m = bl->b.m;
+    if (k) *k = bl->b.k;
+    if (length) *length = len;
+    if (nwords) *nwords = (len + 63) / 64;
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_words(rf_bloom* bl, uint64_t* words, uint64_t nwords) {
+    ARG(bl && (nwords == 0 || words), "null argument");
+    ARG(nwords <= bl->b.nwords, "nwords exceeds filter capacity");
+    DevGuard dg(bl->ctx->device);
+    if (nwords) HIPC(hipMemcpy(words, bl->b.words, 8 * nwords, hipMemcpyDeviceToHost));
+    return RF_OK;
+}

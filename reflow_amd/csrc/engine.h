@@ -1,0 +1,79 @@
+// engine.h -- internal declarations shared by the HIP translation units and
+// the C-ABI implementation (capi.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace rf {
+
+// ---- K1: batched SHA-256 -------------------------------------------------
+// Lane-per-message kernel with a sharded dynamic work queue.
+struct LanesArgs {
+    const uint8_t* arena;
+    const uint64_t* offs;   // [n] byte offsets (16-B aligned)
+    const uint64_t* lens;   // [n]
+    const uint32_t* order;  // [n_order] message ids in processing order (largest first)
+    uint32_t n_order;
+    uint32_t n_shards;      // queue shards; message q belongs to shard q % n_shards
+    uint32_t* heads;        // [n_shards] next position per shard (pre-set)
+    uint8_t* out;           // [n][32]
+};
+hipError_t launch_sha_lanes(const LanesArgs& a, uint32_t grid, hipStream_t s);
+uint32_t sha_lanes_block();
+
+// Wave-per-message kernel for long messages (critical path of skewed sets).
+struct SoloArgs {
+    const uint8_t* arena;
+    const uint64_t* offs;
+    const uint64_t* lens;
+    const uint32_t* order;  // [n_order] message ids
+    uint32_t n_order;
+    uint8_t* out;
+};
+hipError_t launch_sha_solo(const SoloArgs& a, hipStream_t s);
+
+// Checks that the gfx950 code object of this library loads on the device.
+hipError_t probe_kernels();
+
+hipError_t launch_gen_fill(uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n,
+                           uint64_t seed, uint64_t arena_bytes, hipStream_t s);
+
+// ---- K2/K3: digest DAG -----------------------------------------------------
+struct GraphDev {
+    uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;
+    // jobs in internal (level) order
+    uint32_t* job_slot = nullptr;    // [J] output slot
+    uint64_t* job_off = nullptr;     // [J] offset of the padded template in tmpl
+    uint32_t* job_nblk = nullptr;    // [J] SHA blocks of the padded template
+    uint32_t* hole_ptr = nullptr;    // [J+1]
+    uint32_t* hole_pos = nullptr;    // [H]
+    uint32_t* hole_slot = nullptr;   // [H]
+    uint32_t* cons_ptr = nullptr;    // [S+1] slot -> consumer jobs (internal ids)
+    uint32_t* cons_job = nullptr;    // [C]
+    uint8_t* tmpl = nullptr;         // padded templates
+    uint8_t* slots = nullptr;        // [S][32] digest table
+    uint32_t* dirty = nullptr;       // [(J+31)/32] dirty bitset over internal ids
+    uint32_t* list = nullptr;        // [J] compacted dirty jobs of the current level
+    uint32_t* counts = nullptr;      // [L] dirty jobs per level (and [L] = total)
+    std::vector<uint32_t> lvl_start; // host copy [L+1]
+};
+hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
+                                   uint32_t n, hipStream_t s);
+hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s);
+hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
+                               hipStream_t s);
+
+// ---- K4: bloom probe ---------------------------------------------------------
+struct BloomDev {
+    uint64_t m = 1, k = 1, length = 0, nwords = 0;
+    uint64_t* words = nullptr;
+    uint64_t* len_dev = nullptr;  // device copy of length (grows on add)
+};
+hipError_t launch_bloom_probe(const BloomDev& b, const uint8_t* d32, uint64_t n, uint8_t* out,
+                              hipStream_t s);
+hipError_t launch_bloom_add(const BloomDev& b, const uint8_t* d32, uint64_t n, hipStream_t s);
+
+}  // namespace rf

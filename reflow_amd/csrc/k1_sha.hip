@@ -1,0 +1,254 @@
+// k1_sha.hip -- K1: batched multi-message SHA-256 for gfx950.
+//
+// Replaces the per-file SHA-256 of repository/file/repository.go:50-63
+// (Install: io.Copy into reflow.Digester.NewWriter()) that
+// local/executor.go:514-557 runs in <=60 goroutines, and Repository.Put
+// (repository/file/repository.go:237-264).  File.ID = SHA256(bytes).
+//
+// Two kernels, chosen per message by the host planner (capi.cpp):
+//   k1_sha256_lanes  one LANE per message, 64 messages per wave, lanes pull new
+//                    messages from a sharded work queue as they finish, so a
+//                    wave never idles on its longest member.
+//   k1_sha256_solo   one WAVE per long message: the 64 lanes expand the message
+//                    schedule (K[t]+W[t]) of 64 consecutive blocks in parallel
+//                    into LDS, then run the serial round chain reading those
+//                    words by broadcast.  This cuts the per-block issue count of
+//                    the critical chain from ~1464 to ~1000 instructions.  It
+//                    runs at raised wave priority beside the lanes kernel.
+// SHA-256 is Merkle-Damgard: one message's blocks are strictly serial and
+// bit-exactness forbids tree hashing, so a skewed set is bounded below by its
+// largest message (skew-aware roofline).
+#include "engine.h"
+#include "sha256_dev.h"
+
+namespace rf {
+
+constexpr uint32_t kLanesBlock = 256;
+constexpr uint32_t kNone = 0xffffffffu;
+
+__device__ __forceinline__ void store_digest(uint8_t* out, const ShaState& st) {
+    uint4 lo, hi;
+    lo.x = bswap32(st.h[0]); lo.y = bswap32(st.h[1]); lo.z = bswap32(st.h[2]); lo.w = bswap32(st.h[3]);
+    hi.x = bswap32(st.h[4]); hi.y = bswap32(st.h[5]); hi.z = bswap32(st.h[6]); hi.w = bswap32(st.h[7]);
+    reinterpret_cast<uint4*>(out)[0] = lo;
+    reinterpret_cast<uint4*>(out)[1] = hi;
+}
+
+// Build the 16 big-endian words of block `blk` of message (p, len).
+__device__ __forceinline__ void load_block(uint32_t (&w)[16], const uint8_t* p, uint64_t len,
+                                           uint64_t blk) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + blk * 64u);
+    const int64_t rem = (int64_t)len - (int64_t)(blk * 64u);
+    if (rem >= 64) {
+        const uint4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
+        w[0] = bswap32(r0.x); w[1] = bswap32(r0.y); w[2] = bswap32(r0.z); w[3] = bswap32(r0.w);
+        w[4] = bswap32(r1.x); w[5] = bswap32(r1.y); w[6] = bswap32(r1.z); w[7] = bswap32(r1.w);
+        w[8] = bswap32(r2.x); w[9] = bswap32(r2.y); w[10] = bswap32(r2.z); w[11] = bswap32(r2.w);
+        w[12] = bswap32(r3.x); w[13] = bswap32(r3.y); w[14] = bswap32(r3.z); w[15] = bswap32(r3.w);
+    } else {
+        // Tail: load only the 16-B chunks that hold message bytes; a chunk that
+        // holds one valid byte lies inside that byte's aligned 16 B, never past
+        // the allocation's last page.
+        uint32_t raw[16];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint4 r = make_uint4(0, 0, 0, 0);
+            if (rem > 16 * c) r = q[c];
+            raw[4 * c] = r.x; raw[4 * c + 1] = r.y; raw[4 * c + 2] = r.z; raw[4 * c + 3] = r.w;
+        }
+        sha256_pad_words(w, raw, len, blk);
+    }
+}
+
+__global__ __launch_bounds__(kLanesBlock) void k1_sha256_lanes(LanesArgs a) {
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t shard = (gtid >> 6) % a.n_shards;
+    uint32_t tries = 0;
+
+    auto fetch = [&]() -> uint32_t {
+        while (tries < a.n_shards) {
+            const uint32_t pl = atomicAdd(&a.heads[shard], 1u);
+            const uint64_t q = (uint64_t)pl * a.n_shards + shard;
+            if (q < a.n_order) return a.order[q];
+            shard = (shard + 1 == a.n_shards) ? 0u : shard + 1;
+            ++tries;
+        }
+        return kNone;
+    };
+
+    uint32_t id = fetch();
+    const uint8_t* p = nullptr;
+    uint64_t len = 0, nb = 0, blk = 0;
+    ShaState st;
+    st.init();
+    if (id != kNone) {
+        p = a.arena + a.offs[id];
+        len = a.lens[id];
+        nb = sha256_nblocks(len);
+    }
+    while (__any(id != kNone)) {
+        if (id != kNone) {
+            uint32_t w[16];
+            load_block(w, p, len, blk);
+            sha256_compress(st, w);
+            ++blk;
+            if (blk == nb) {
+                store_digest(a.out + 32ull * id, st);
+                id = fetch();
+                st.init();
+                blk = 0;
+                if (id != kNone) {
+                    p = a.arena + a.offs[id];
+                    len = a.lens[id];
+                    nb = sha256_nblocks(len);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Solo: one wave per message.
+// LDS: kw[blk][t] = K[t] + W_t for 64 blocks, rows padded to 68 words so a
+// lane's 16-B stores of its own row spread over the banks; the chain reads a
+// row with wave-uniform (broadcast) ds_read_b128.
+constexpr uint32_t kRow = 68;
+
+__global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ __attribute__((aligned(16))) uint32_t kw[64 * kRow];
+    constexpr uint32_t K[64] = RF_SHA_K;
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t q = blockIdx.x; q < a.n_order; q += gridDim.x) {
+        const uint32_t id = a.order[q];
+        const uint8_t* p = a.arena + a.offs[id];
+        const uint64_t len = a.lens[id];
+        const uint64_t nb = sha256_nblocks(len);
+        ShaState st;
+        st.init();
+        for (uint64_t c = 0; c < nb; c += 64) {
+            const uint64_t b = c + lane;
+            if (b < nb) {
+                uint32_t w[16];
+                load_block(w, p, len, b);
+                uint32_t* row = &kw[lane * kRow];
+#pragma unroll
+                for (int t = 0; t < 64; ++t) {
+                    uint32_t wt;
+                    if (t < 16) {
+                        wt = w[t];
+                    } else {
+                        wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) +
+                             w[t & 15];
+                        w[t & 15] = wt;
+                    }
+                    row[t] = K[t] + wt;
+                }
+            }
+            __syncthreads();
+            const uint32_t cnt = (uint32_t)((nb - c) < 64 ? (nb - c) : 64);
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const uint4* r4 = reinterpret_cast<const uint4*>(&kw[j * kRow]);
+                uint32_t a0 = st.h[0], b0 = st.h[1], c0 = st.h[2], d0 = st.h[3];
+                uint32_t e0 = st.h[4], f0 = st.h[5], g0 = st.h[6], h0 = st.h[7];
+#pragma unroll
+                for (int t4 = 0; t4 < 16; ++t4) {
+                    const uint4 v = r4[t4];
+                    const uint32_t kv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t t1 = add3v(h0 + kv[u], bsig1(e0), ch(e0, f0, g0));
+                        h0 = g0; g0 = f0; f0 = e0; e0 = d0 + t1;
+                        const uint32_t an = add3v(t1, bsig0(a0), maj(a0, b0, c0));
+                        d0 = c0; c0 = b0; b0 = a0; a0 = an;
+                    }
+                }
+                st.h[0] += a0; st.h[1] += b0; st.h[2] += c0; st.h[3] += d0;
+                st.h[4] += e0; st.h[5] += f0; st.h[6] += g0; st.h[7] += h0;
+            }
+            __syncthreads();
+        }
+        if (lane == 0) store_digest(a.out + 32ull * id, st);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic content: word q of message i = mix64((seed ^ i) + (q+1)*G), LE.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_gen_fill(uint8_t* arena, const uint64_t* offs,
+                                                  const uint64_t* lens, uint64_t n, uint64_t seed,
+                                                  uint64_t nchunks) {
+    constexpr uint64_t G = 0x9E3779B97F4A7C15ull;
+    uint64_t cur = 0, cur_lo = 1, cur_hi = 0;  // empty range forces a search
+    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < nchunks;
+         x += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = x * 16;
+        if (!(o >= cur_lo && o < cur_hi)) {
+            // last message with offs[i] <= o
+            uint64_t lo = 0, hi = n;
+            while (hi - lo > 1) {
+                const uint64_t mid = (lo + hi) / 2;
+                if (offs[mid] <= o) lo = mid; else hi = mid;
+            }
+            cur = lo;
+            cur_lo = offs[lo];
+            cur_hi = cur_lo + ((lens[lo] + 15) & ~15ull);
+        }
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (n > 0 && o >= cur_lo && o < cur_hi) {
+            const uint64_t rel = o - cur_lo;
+            const uint64_t s = seed ^ cur;
+            const uint64_t q = rel / 8;
+            const uint64_t w0 = mix64(s + (q + 1) * G), w1 = mix64(s + (q + 2) * G);
+            v = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+            const uint64_t len = lens[cur];
+            if (rel + 16 > len) {  // zero bytes past the message end
+                uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t valid = (int64_t)len - (int64_t)(rel + 4 * j);
+                    if (valid <= 0) vv[j] = 0;
+                    else if (valid < 4) vv[j] &= (1u << (8 * valid)) - 1;
+                }
+                v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+            }
+        }
+        reinterpret_cast<uint4*>(arena)[x] = v;
+    }
+}
+
+uint32_t sha_lanes_block() { return kLanesBlock; }
+
+hipError_t probe_kernels() {
+    hipFuncAttributes attr;
+    return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k1_sha256_lanes));
+}
+
+hipError_t launch_sha_lanes(const LanesArgs& a, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(k1_sha256_lanes, dim3(grid), dim3(kLanesBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sha_solo(const SoloArgs& a, hipStream_t s) {
+    if (a.n_order == 0) return hipSuccess;
+    hipLaunchKernelGGL(k1_sha256_solo, dim3(a.n_order), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_fill(uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n,
+                           uint64_t seed, uint64_t arena_bytes, hipStream_t s) {
+    const uint64_t nchunks = arena_bytes / 16;
+    uint64_t grid = (nchunks + 255) / 256;
+    if (grid > 16384) grid = 16384;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_fill, dim3((uint32_t)grid), dim3(256), 0, s, arena, offs, lens, n,
+                       seed, nchunks);
+    return hipGetLastError();
+}
+
+}  // namespace rf

@@ -1,0 +1,175 @@
+// k4_bloom.hip -- K4: batched bloomlive / assoc probe and build.
+//
+// Replaces bloomlive.T.Contains (/root/reference/internal/bloomlive/bloomlive.go:30-36)
+// -> bloom.Test (vendor/github.com/willf/bloom/bloom.go:182-190) -> baseHashes
+// (:94-104, murmur3 x64_128 seed 0, vendor/github.com/spaolacci/murmur3/
+// murmur128.go:56-171) -> location (:107-115) -> bitset.Test
+// (vendor/github.com/willf/bitset/bitset.go:143-149); and the build side
+// bloom.Add (:144-150) used by eval.go:848-858.
+//
+// Key = WD(d) = 00 05 || d (34 bytes).  (h1,h2) = mm3(key), (h3,h4) =
+// mm3(key || 0x01): both share the two 16-byte body blocks, so the body is
+// mixed once and finalised twice.  loc_i = (h[i%2] + i*h[2+((i+i%2)%4)/2])
+// mod m with an exact 64-bit Barrett reduction.  One lane per probe; all k
+// filter words are requested before any is tested (memory-level parallelism
+// instead of the reference's early exit).
+#include "engine.h"
+
+namespace rf {
+
+constexpr uint64_t kC1 = 0x87c37b91114253d5ull, kC2 = 0x4cf5ad432745937full;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// Base hashes of WD(d) for a digest given as four little-endian u64 words.
+__device__ __forceinline__ void base_hashes_wd(const uint64_t (&D)[4], uint64_t (&h)[4]) {
+    const uint64_t key0 = 0x0500ull | (D[0] << 16);
+    const uint64_t key1 = (D[0] >> 48) | (D[1] << 16);
+    const uint64_t key2 = (D[1] >> 48) | (D[2] << 16);
+    const uint64_t key3 = (D[2] >> 48) | (D[3] << 16);
+    const uint64_t tail = D[3] >> 48;  // bytes d30 d31
+    uint64_t h1 = 0, h2 = 0;
+    const uint64_t ks[4] = {key0, key1, key2, key3};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        uint64_t k1 = ks[2 * b], k2 = ks[2 * b + 1];
+        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+        h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+        k2 *= kC2; k2 = rotl64(k2, 33); k2 *= kC1; h2 ^= k2;
+        h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+    }
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        // tail of 2 bytes (len 34) or 3 bytes (len 35: || 0x01); k2 part empty
+        uint64_t k1 = f == 0 ? tail : (tail | (1ull << 16));
+        const uint64_t len = f == 0 ? 34 : 35;
+        uint64_t a = h1, b = h2;
+        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; a ^= k1;
+        a ^= len; b ^= len;
+        a += b; b += a;
+        a = fmix64(a); b = fmix64(b);
+        a += b; b += a;
+        h[2 * f] = a;
+        h[2 * f + 1] = b;
+    }
+}
+
+// x mod m, exact: mu = floor((2^64-1)/m) from the host; q underestimates
+// floor(x/m) by at most 2.
+__device__ __forceinline__ uint64_t mod_m(uint64_t x, uint64_t m, uint64_t mu) {
+    const uint64_t q = __umul64hi(x, mu);
+    uint64_t r = x - q * m;
+    if (r >= m) r -= m;
+    if (r >= m) r -= m;
+    return r;
+}
+
+__device__ __forceinline__ uint64_t bloom_loc(const uint64_t (&h)[4], uint32_t i) {
+    const uint64_t ii = i;
+    return h[ii % 2] + ii * h[2 + (((ii + (ii % 2)) % 4) / 2)];
+}
+
+__device__ __forceinline__ void load_digest64(const uint8_t* d, uint64_t (&D)[4]) {
+    const ulonglong2* p = reinterpret_cast<const ulonglong2*>(d);
+    const ulonglong2 a = p[0], b = p[1];
+    D[0] = a.x; D[1] = a.y; D[2] = b.x; D[3] = b.y;
+}
+
+constexpr uint32_t kKMax = 16;
+
+__global__ __launch_bounds__(256) void k4_bloom_probe(const uint64_t* __restrict__ words,
+                                                      const uint64_t* __restrict__ len_dev,
+                                                      uint64_t m, uint64_t mu, uint32_t k,
+                                                      const uint8_t* __restrict__ d32, uint64_t n,
+                                                      uint8_t* __restrict__ out) {
+    const uint64_t length = *len_dev;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t D[4], h[4];
+        load_digest64(d32 + 32 * i, D);
+        base_hashes_wd(D, h);
+        bool hit = true;
+        if (k <= kKMax) {
+            uint64_t w[kKMax];
+            uint32_t bit[kKMax];
+#pragma unroll
+            for (uint32_t j = 0; j < kKMax; ++j) {
+                w[j] = ~0ull;
+                bit[j] = 0;
+                if (j < k) {
+                    const uint64_t loc = mod_m(bloom_loc(h, j), m, mu);
+                    if (loc >= length) {
+                        hit = false;
+                    } else {
+                        w[j] = words[loc >> 6];
+                        bit[j] = (uint32_t)(loc & 63);
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kKMax; ++j) hit = hit && ((w[j] >> bit[j]) & 1ull);
+        } else {
+            for (uint32_t j = 0; j < k && hit; ++j) {
+                const uint64_t loc = mod_m(bloom_loc(h, j), m, mu);
+                hit = loc < length && ((words[loc >> 6] >> (loc & 63)) & 1ull);
+            }
+        }
+        out[i] = hit ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k4_bloom_add(unsigned long long* __restrict__ words,
+                                                    unsigned long long* __restrict__ len_dev,
+                                                    uint64_t m, uint64_t mu, uint32_t k,
+                                                    const uint8_t* __restrict__ d32, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t D[4], h[4];
+        load_digest64(d32 + 32 * i, D);
+        base_hashes_wd(D, h);
+        uint64_t maxloc = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint64_t loc = mod_m(bloom_loc(h, j), m, mu);
+            atomicOr(&words[loc >> 6], 1ull << (loc & 63));
+            maxloc = loc > maxloc ? loc : maxloc;
+        }
+        // bitset.Set grows length to loc+1 when loc >= length (bitset.go:151-156)
+        atomicMax(len_dev, (unsigned long long)(maxloc + 1));
+    }
+}
+
+static uint64_t barrett_mu(uint64_t m) { return m ? (~0ull) / m : 0; }
+
+static uint32_t grid_for(uint64_t items) {
+    uint64_t g = (items + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 16384) g = 16384;
+    return (uint32_t)g;
+}
+
+hipError_t launch_bloom_probe(const BloomDev& b, const uint8_t* d32, uint64_t n, uint8_t* out,
+                              hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k4_bloom_probe, dim3(grid_for(n)), dim3(256), 0, s, b.words, b.len_dev, b.m,
+                       barrett_mu(b.m), (uint32_t)b.k, d32, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_bloom_add(const BloomDev& b, const uint8_t* d32, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k4_bloom_add, dim3(grid_for(n)), dim3(256), 0, s,
+                       reinterpret_cast<unsigned long long*>(b.words),
+                       reinterpret_cast<unsigned long long*>(b.len_dev), b.m, barrett_mu(b.m),
+                       (uint32_t)b.k, d32, n);
+    return hipGetLastError();
+}
+
+}  // namespace rf
