@@ -1,0 +1,402 @@
+#!/usr/bin/env python3
+"""bench.py -- Reflow memoization hot path on MI355X (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+
+Primary line (value): SHA-256 digest GB/s of configs[1], the 64 GiB
+FASTQ/BAM-like skewed Fileset (4 KiB-2 GiB files), HBM-resident, on each GPU
+(weak scaling: every rank digests its own 64 GiB set).  A step = one
+rf_sha_plan_run over the whole set (all File IDs of the Fileset).
+
+Secondary, in the same JSON line:
+  "incremental"  configs[2]: 10M-node 1000align DAG, 1% of leaf File IDs
+                 changed per step -> K3 frontier + K2 recompute (Mnodes/s of
+                 dirty nodes, and effective graph nodes/s); RCCL all-gather of
+                 the per-rank root digests when N > 1.
+  "probe"        configs[4]: 1e9 bloomlive probes against a 1e8-key filter.
+  "cpu_baseline" the oracle's C port on the host cores (rank 0, N=1).
+
+The only process-wide runtime is the engine's own (libreflow_hip.so); torch is
+used only for torch.distributed (gloo, CPU) to bootstrap RCCL and to take the
+max over ranks.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from reflow_amd import capi  # noqa: E402
+from reflow_amd.workloads import Dag1000, GiB, arena_layout, c2_sizes  # noqa: E402
+
+# ---- hardware constants (MI355X_MICROARCH.md) ------------------------------
+CLOCK_HZ = 2.4e9
+N_CU = 256
+VALU_LANE_OPS = N_CU * 4 * 32 * CLOCK_HZ      # int32 VALU lane-ops/s (= FP32 FMA rate)
+SHA_OPS_PER_BLOCK = 1464                        # canonical ops per 64-B block
+SHA_VALU_PEAK_GBS = VALU_LANE_OPS / SHA_OPS_PER_BLOCK * 64 / 1e9
+CHAIN_INSTR_PER_BLOCK = 64 * 14                 # minimal gfx950 round: 14 VALU
+WAVE_ISSUE_CYCLES = 4                           # one wave alone: 1 VALU / 4 cycles
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+class Dist:
+    def __init__(self, n_gpus):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+        if n_gpus != self.world and self.world > 1:
+            log("warning: --gpus %d but WORLD_SIZE %d" % (n_gpus, self.world))
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def bcast_bytes(self, b):
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+
+def timed_steps(dist, ctx, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    ctx.sync()
+    dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        fn()
+        if steps > 2:
+            pass
+    ctx.sync()
+    dist.barrier()
+    t1 = time.perf_counter()
+    return dist.max(t1 - t0)
+
+
+# ---------------------------------------------------------------- C2: SHA --
+def bench_sha(args, dist, ctx):
+    seed = 0x5EED0002 if dist.world == 1 else 0x5EED0004 + dist.rank
+    total = int(args.sha_gib * GiB)
+    lens = c2_sizes(total_bytes=total, seed=seed)
+    offs, arena_bytes = arena_layout(lens)
+    arena = ctx.alloc(arena_bytes)
+    d_offs, d_lens = ctx.upload(offs), ctx.upload(lens)
+    out = ctx.alloc(32 * len(lens))
+    ctx.gen_fill(arena.ptr, d_offs.ptr, d_lens.ptr, len(lens), seed, arena_bytes)
+    ctx.sync()
+    plan = ctx.sha_plan(offs, lens, 0)
+    st = plan.stats()
+    log("C2: %d files, %.1f GiB, %d wave-per-message, max file %.2f GiB"
+        % (len(lens), lens.sum() / GiB, st.n_solo, lens.max() / GiB))
+    solo_ms, lanes_ms = [], []
+
+    def step():
+        plan.run(arena.ptr, out.ptr)
+        s = plan.stats()  # synchronises: per-kernel HIP-event times of this run
+        solo_ms.append(s.last_ms_solo)
+        lanes_ms.append(s.last_ms_lanes)
+        log("  sha step: total %.1f ms (solo %.1f, lanes %.1f)" % (s.last_ms_total, s.last_ms_solo,
+                                                                    s.last_ms_lanes))
+
+    t = timed_steps(dist, ctx, step, args.steps, args.warmup)
+    solo_ms, lanes_ms = solo_ms[args.warmup:], lanes_ms[args.warmup:]
+    bytes_all = dist.sum(float(lens.sum())) * args.steps
+    gbs = bytes_all / t / 1e9
+    # roofline of the dominant kernel (the longer of solo / lanes)
+    order = np.argsort(-lens.astype(np.int64), kind="stable")
+    solo_ids = order[:st.n_solo]
+    lane_ids = order[st.n_solo:]
+    nblk = (lens.astype(np.int64) + 9 + 63) // 64
+    dom = "k1_sha256_solo" if np.mean(solo_ms or [0]) >= np.mean(lanes_ms or [0]) else "k1_sha256_lanes"
+    ids = solo_ids if dom == "k1_sha256_solo" else lane_ids
+    dom_ms = float(np.mean(solo_ms if dom == "k1_sha256_solo" else lanes_ms))
+    dom_bytes = float(lens[ids].sum())
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    # skew-aware floor: the longest serial chain vs chip VALU throughput
+    t_chain = float(nblk[ids].max()) * CHAIN_INSTR_PER_BLOCK * WAVE_ISSUE_CYCLES / CLOCK_HZ
+    t_valu = float(nblk[ids].sum()) * SHA_OPS_PER_BLOCK / VALU_LANE_OPS
+    t_floor = max(t_chain, t_valu)
+    peak = dom_bytes / t_floor / 1e9
+    roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
+            "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": None,
+            "peak_kind": "skew-aware: max(longest message chain at 14 VALU/round x 4 cyc/issue @2.4GHz,"
+                         " sum blocks x 1464 ops / INT32 VALU peak)",
+            "valu_peak_GBps": round(SHA_VALU_PEAK_GBS, 1),
+            "frac_of_valu_peak": round(achieved / SHA_VALU_PEAK_GBS, 6),
+            "launch_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes,
+            "critical_chain_blocks": int(nblk[ids].max())}
+    res = dict(value=gbs, ms_per_step=t / args.steps * 1e3, roofline=roof,
+               files=int(len(lens)), bytes_per_gpu=int(lens.sum()), n_solo=int(st.n_solo),
+               lanes_ms=float(np.mean(lanes_ms)) if lanes_ms else 0.0)
+    # keep digests of a host-checkable sample for the cpu_baseline cross-check
+    res["_digests"] = out.to_numpy().reshape(-1, 32)
+    res["_lens"], res["_seed"] = lens, seed
+    plan.close()
+    for b in (arena, d_offs, d_lens, out):
+        b.free()
+    return res
+
+
+# ------------------------------------------------------- C3: incremental --
+def bench_dag(args, dist, ctx, comm):
+    S = args.dag_samples
+    t0 = time.perf_counter()
+    dag = Dag1000(S, args.dag_pairs, seed=0x5EED0003 + 1000003 * dist.rank)
+    a = dag.arrays()
+    g = capi.Graph(ctx, a["n_slots"], a["out_slot"], a["tmpl_off"], a["tmpl_len"], a["hole_ptr"],
+                   a["hole_pos"], a["hole_slot"], a["blob"])
+    del a
+    g.set_slots(dag.file_slots, dag.leaf_ids)
+    log("C3: %d nodes, %d jobs built+loaded in %.1f s" % (dag.n_nodes, dag.n_jobs, time.perf_counter() - t0))
+    ctx.timer_start()
+    g.recompute(full=True)
+    full_ms = ctx.timer_stop()
+    slots, old, new = dag.change_set(0.01)
+    d_slots = ctx.upload(slots)
+    d_old, d_new = ctx.upload(old), ctx.upload(new)
+    roots = dag.kinds["XS"].out_slot
+    d_roots_idx = ctx.upload(roots)
+    d_gather = ctx.alloc(32 * len(roots) * max(dist.world, 1))
+    d_local = ctx.alloc(32 * len(roots))
+    # one counted step to learn the dirty-set size
+    g.set_slots(slots, new)
+    n_dirty_jobs = g.recompute(full=False)
+    g.set_slots(slots, old)
+    g.recompute(full=False)
+    pairs = np.unique(slots // 2)
+    n_dirty_nodes = n_dirty_jobs - len(pairs)  # minus the pE1 physical keys
+    state = {"v": 0}
+
+    def step():
+        ver = d_new if state["v"] == 0 else d_old
+        state["v"] ^= 1
+        g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
+        g.recompute_async(False, ctx.stream)
+        if comm is not None:  # boundary digests (per-sample roots) to every rank
+            g.gather_device(d_roots_idx.ptr, len(roots), d_local.ptr, ctx.stream)
+            comm.allgather(d_local.ptr, d_gather.ptr, 32 * len(roots), ctx.stream)
+
+    steps = args.dag_steps
+    t = timed_steps(dist, ctx, step, steps, 2)
+    ctx.timer_start()
+    for _ in range(steps):
+        step()
+    dev_ms = ctx.timer_stop() / steps
+    total_dirty_nodes = dist.sum(n_dirty_nodes) * steps
+    res = {"workload": "1000align DAG S=%d P=%d per GPU, 1%% leaf File IDs toggled per step" % (S, args.dag_pairs),
+           "nodes_per_gpu": dag.n_nodes, "jobs_per_gpu": dag.n_jobs,
+           "dirty_nodes_per_step": int(n_dirty_nodes), "dirty_jobs_per_step": int(n_dirty_jobs),
+           "ms_per_step": t / steps * 1e3, "device_ms_per_step": dev_ms,
+           "mnodes_per_s": total_dirty_nodes / t / 1e6,
+           "effective_mnodes_per_s": dist.sum(dag.n_nodes) * steps / t / 1e6,
+           "full_recompute_ms": full_ms,
+           "full_recompute_mnodes_per_s": dag.n_nodes / (full_ms * 1e-3) / 1e6,
+           "levels": g.stats().n_levels}
+    # full-recompute roofline (VALU): all template blocks hashed
+    st = g.stats()
+    ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
+    res["roofline_full"] = {"bound": "valu", "achieved": round(ach, 2), "peak": round(SHA_VALU_PEAK_GBS, 1),
+                            "unit": "GB/s", "frac": round(ach / SHA_VALU_PEAK_GBS, 4)}
+    g.close()
+    return res, dag
+
+
+# --------------------------------------------------------------- C5: probe --
+def bench_probe(args, dist, ctx):
+    n_ins, n_probe = args.probe_keys, args.probes
+    m = int(math.ceil(-1 * float(n_ins) * math.log(0.001) / math.pow(math.log(2), 2)))
+    k = int(math.ceil(math.log(2) * float(m) / float(n_ins)))
+    keys = ctx.alloc(32 * n_probe)
+    # probes: [inserted keys x (n_probe/2n_ins)] ++ [fresh]; generated on device
+    half = n_probe // 2
+    lens = np.array([32 * n_ins, 32 * (n_probe - half)], dtype=np.uint64)
+    offs = np.array([0, 32 * half], dtype=np.uint64)
+    d_offs, d_lens = ctx.upload(offs), ctx.upload(lens)
+    ctx.gen_fill(keys.ptr, d_offs.ptr, d_lens.ptr, 2, 0x5EED0005 + dist.rank, 32 * n_probe)
+    ctx.sync()
+    rep = half // n_ins
+    for r in range(1, rep):
+        capi._check(capi.lib().rf_memcpy_d2d(ctx.handle, keys.ptr + 32 * n_ins * r, keys.ptr, 32 * n_ins))
+    b = capi.Bloom.new(ctx, m, k)
+    ctx.timer_start()
+    b.add_device(keys.ptr, n_ins, ctx.stream)
+    add_ms = ctx.timer_stop()
+    out = ctx.alloc(n_probe)
+
+    def step():
+        b.probe_device(keys.ptr, n_probe, out.ptr, ctx.stream)
+
+    t = timed_steps(dist, ctx, step, args.probe_steps, 1)
+    ctx.timer_start()
+    step()
+    dev_ms = ctx.timer_stop()
+    hits = int(out.to_numpy().astype(np.int64).sum())
+    fresh = n_probe - rep * n_ins
+    fp = (hits - rep * n_ins) / max(fresh, 1)
+    bpp = 32 + 8 * k + 1
+    ach = n_probe * bpp / (dev_ms * 1e-3) / 1e9
+    res = {"workload": "bloomlive probe: n=%d keys (m=%d bits, %.1f MiB, k=%d), %d probes (50%% present)"
+                       % (n_ins, m, m / 8 / 2**20, k, n_probe),
+           "gprobes_per_s": dist.sum(n_probe) * args.probe_steps / t / 1e9,
+           "device_ms": dev_ms, "add_ms": add_ms, "false_positive_rate": fp,
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_probe": bpp,
+                        "note": "filter fits the 256 MiB Infinity Cache at n=1e8"}}
+    for x in (keys, out, d_offs, d_lens):
+        x.free()
+    b.close()
+    return res
+
+
+# ----------------------------------------------------------- CPU baseline --
+def cpu_baseline(args, sha, dag):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+
+    import reflow_oracle as O  # the oracle: cpu_baseline leg only
+    L = O.lib()
+    threads = min(16, os.cpu_count() or 1)
+    lens = sha["_lens"]
+    # bounded sample of the same workload: files in generation order up to the
+    # byte budget (the same skewed mix, big files included)
+    budget = int(args.cpu_sample_gib * GiB)
+    csum = np.cumsum(lens.astype(np.int64))
+    n = int(np.searchsorted(csum, budget)) + 1
+    n = min(n, len(lens))
+    s_lens = lens[:n].copy()
+    s_offs, total = arena_layout(s_lens, align=64)
+    arena = np.zeros(total, dtype=np.uint8)
+    L.orc_fill_batch(sha["_seed"], arena.ctypes.data, s_offs.ctypes.data, s_lens.ctypes.data, n, threads)
+    out = np.zeros((n, 32), dtype=np.uint8)
+    order = np.argsort(-s_lens.astype(np.int64), kind="stable").astype(np.uint64)  # LPT
+    o_offs, o_lens = s_offs[order].copy(), s_lens[order].copy()
+    t0 = time.perf_counter()
+    L.orc_sha256_batch(arena.ctypes.data, o_offs.ctypes.data, o_lens.ctypes.data, n, out.ctypes.data,
+                       threads)
+    dt = time.perf_counter() - t0
+    back = np.empty_like(out)
+    back[order.astype(np.int64)] = out
+    match = bool((back == sha["_digests"][:n]).all())
+    res = {"value": float(s_lens.sum()) / dt / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
+           "sample": "first %d files (%.2f GiB, largest %.2f GiB) of the same C2 set, oracle/oracle.c "
+                     "scalar SHA-256, %d pthreads, largest-first" % (n, s_lens.sum() / GiB,
+                                                                    s_lens.max() / GiB, threads),
+           "seconds": dt, "gpu_digests_match": match}
+    del arena
+    # C3 port: full recompute of a bounded sample DAG, 1 thread (Canonicalize is serial)
+    if dag is not None:
+        small = Dag1000(max(1, args.cpu_dag_samples), dag.P)
+        a = small.arrays()
+        order = np.zeros(small.n_jobs, dtype=np.uint64)
+        # topological order = kinds in construction order (each kind only reads earlier ones)
+        order[:] = np.arange(small.n_jobs, dtype=np.uint64)
+        slots = np.zeros((small.n_slots, 32), dtype=np.uint8)
+        slots[small.file_slots] = small.leaf_ids
+        t0 = time.perf_counter()
+        L.orc_graph_eval(small.n_jobs, order.ctypes.data, a["out_slot"].ctypes.data,
+                         a["tmpl_off"].ctypes.data, a["tmpl_len"].ctypes.data, a["hole_ptr"].ctypes.data,
+                         a["hole_pos"].ctypes.data, a["hole_slot"].ctypes.data, a["blob"].ctypes.data,
+                         slots.ctypes.data)
+        dt = time.perf_counter() - t0
+        res["dag"] = {"value": small.n_nodes / dt / 1e6, "unit": "Mnodes/s (full recompute)", "cores": 1,
+                      "kind": "port", "sample": "1000align DAG S=%d P=%d (%d nodes, %d jobs), "
+                      "oracle/oracle.c orc_graph_eval" % (small.S, small.P, small.n_nodes, small.n_jobs),
+                      "seconds": dt}
+    _ = ctypes
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--sha-gib", type=float, default=64.0)
+    ap.add_argument("--dag-samples", type=int, default=22075)  # ~10M nodes at P=32
+    ap.add_argument("--dag-pairs", type=int, default=32)
+    ap.add_argument("--dag-steps", type=int, default=20)
+    ap.add_argument("--probe-keys", type=int, default=100_000_000)
+    ap.add_argument("--probes", type=int, default=1_000_000_000)
+    ap.add_argument("--probe-steps", type=int, default=3)
+    ap.add_argument("--cpu-sample-gib", type=float, default=8.0)
+    ap.add_argument("--cpu-dag-samples", type=int, default=200)
+    ap.add_argument("--skip", default="", help="comma list of: dag,probe,cpu")
+    args = ap.parse_args()
+    skip = set(filter(None, args.skip.split(",")))
+
+    dist = Dist(args.gpus)
+    ctx = capi.Context(dist.local)
+    comm = None
+    if dist.world > 1:
+        uid = dist.bcast_bytes(capi.Comm.unique_id() if dist.rank == 0 else None)
+        comm = capi.Comm(ctx, dist.world, dist.rank, uid)
+
+    sha = bench_sha(args, dist, ctx)
+    dag_res, dag = (None, None)
+    if "dag" not in skip:
+        dag_res, dag = bench_dag(args, dist, ctx, comm)
+    probe = None if "probe" in skip else bench_probe(args, dist, ctx)
+    cpu = None
+    if dist.rank == 0 and dist.world == 1 and "cpu" not in skip:
+        cpu = cpu_baseline(args, sha, dag)
+
+    if dist.rank == 0:
+        line = {
+            "metric": "SHA-256 digest GB/s + incremental cache-key recompute Mnodes/s, 1/2/4/8 GPU",
+            "value": round(sha["value"], 4), "unit": "GB/s", "n_gpus": dist.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(sha["ms_per_step"], 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 content generated in HBM)",
+            "config": {"workload": "configs[1]: 64 GiB FASTQ/BAM-like Fileset per GPU, %d files 4 KiB-2 GiB "
+                                   "(98%% log-uniform 4 KiB-1 MiB, 2%% 64 MiB-2 GiB), SHA-256 of every file"
+                                   % sha["files"],
+                       "parallelism": "files sharded per GPU (independent); RCCL only for DAG root digests"},
+            "roofline": sha["roofline"],
+            "cpu_baseline": cpu,
+            "incremental": dag_res,
+            "probe": probe,
+        }
+        print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -60,6 +60,34 @@ int rf_sync(rf_ctx *ctx);
 /* Version string, e.g. "reflow-hip 0.1 gfx950". */
 const char *rf_version(void);
 
+/* ---- device memory and timing -------------------------------------------
+ * The engine owns its HIP runtime; callers (the cgo shim, bench.py, tests)
+ * allocate HBM through these so no second runtime enters the process. */
+int rf_malloc(rf_ctx *ctx, uint64_t bytes, void **out);
+int rf_free(rf_ctx *ctx, void *p);
+int rf_memcpy_h2d(rf_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int rf_memcpy_d2h(rf_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int rf_memset_d(rf_ctx *ctx, void *dst, int value, uint64_t bytes);
+int rf_memcpy_d2d(rf_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+/* The context's hipStream_t. */
+void *rf_stream(rf_ctx *ctx);
+/* HIP-event timer on the context stream: start, then stop returns ms. */
+int rf_timer_start(rf_ctx *ctx);
+int rf_timer_stop(rf_ctx *ctx, float *ms);
+
+/* ---- RCCL over xGMI (multi-GPU: one process per GPU) ----------------------
+ * Bootstrap: rank 0 calls rf_comm_unique_id and ships the 128 bytes to the
+ * other ranks out of band (bench.py uses torch.distributed/gloo on the CPU). */
+typedef struct rf_comm rf_comm;
+int rf_comm_unique_id(uint8_t id[128]);
+int rf_comm_init(rf_ctx *ctx, int nranks, int rank, const uint8_t id[128], rf_comm **out);
+void rf_comm_destroy(rf_comm *comm);
+/* d_recv[r*bytes .. +bytes) = rank r's d_send (ncclAllGather). */
+int rf_comm_allgather(rf_comm *comm, const void *d_send, void *d_recv, uint64_t bytes, void *stream);
+/* In-place bitwise OR of nwords uint64 across ranks.  RCCL has no OR
+ * reduction: all-gather of the packed words + a local OR kernel. */
+int rf_comm_allreduce_or(rf_comm *comm, void *d_words, uint64_t nwords, void *stream);
+
 /* ---- K1: batched SHA-256 (Digester.NewWriter/FromBytes, Repository.Put) --
  * Replaces the per-file io.Copy into Digester.NewWriter() at
  * repository/file/repository.go:50-63 (Install) and :237-264 (Put), driven by
@@ -143,6 +171,9 @@ int rf_graph_recompute(rf_graph *g, int full, uint64_t *out_recomputed);
 /* Asynchronous form (no count readback). */
 int rf_graph_recompute_async(rf_graph *g, int full, void *stream);
 int rf_graph_get_slots(rf_graph *g, const uint32_t *slots, uint32_t n, uint8_t *out32);
+/* Device-resident gather: d_out32[i] = slot d_slots[i] (e.g. boundary digests
+ * for rf_comm_allgather).  Asynchronous on `stream`. */
+int rf_graph_gather_device(rf_graph *g, const void *d_slots, uint32_t n, void *d_out32, void *stream);
 typedef struct {
     uint32_t n_jobs, n_slots, n_levels, max_level_jobs;
     uint64_t total_blocks, hole_count, template_bytes;

@@ -146,6 +146,60 @@ void orc_fill_stream(uint64_t seed, uint8_t *dst, uint64_t len) {
     }
 }
 
+typedef struct {
+    uint64_t seed; uint8_t *arena; const uint64_t *offs, *lens; uint64_t n; int tid, nth;
+} fill_job;
+
+static void *fill_worker(void *p) {
+    fill_job *j = (fill_job *)p;
+    for (uint64_t i = (uint64_t)j->tid; i < j->n; i += (uint64_t)j->nth)
+        orc_fill_stream(j->seed ^ i, j->arena + j->offs[i], j->lens[i]);
+    return NULL;
+}
+
+/* message i = stream (seed ^ i), the layout rf_gen_fill produces on device. */
+void orc_fill_batch(uint64_t seed, uint8_t *arena, const uint64_t *offs, const uint64_t *lens,
+                    uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    fill_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (fill_job){seed, arena, offs, lens, n, t, nthreads};
+        pthread_create(&th[t], NULL, fill_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+/* ------------------------------------------------------------------ */
+/* Digest-DAG evaluation (CPU port of Flow.Digest / PhysicalDigest):    */
+/* jobs given as rf_graph_desc arrays, evaluated in the caller's        */
+/* topological order: copy the material, write WD digests of the        */
+/* referenced slots into the holes, SHA-256 into the output slot.       */
+/* This is the recursive WriteDigest of flow.go:675-750 with the memo   */
+/* of :653-658, one SHA-256 per job, single thread like Canonicalize.   */
+/* ------------------------------------------------------------------ */
+void orc_graph_eval(uint64_t n_jobs, const uint64_t *order, const uint32_t *out_slot,
+                    const uint64_t *tmpl_off, const uint32_t *tmpl_len, const uint64_t *hole_ptr,
+                    const uint32_t *hole_pos, const uint32_t *hole_slot, const uint8_t *blob,
+                    uint8_t *slots32) {
+    uint8_t *buf = NULL;
+    size_t cap = 0;
+    for (uint64_t q = 0; q < n_jobs; ++q) {
+        const uint64_t j = order ? order[q] : q;
+        const uint32_t len = tmpl_len[j];
+        if (len > cap) {
+            cap = len * 2 + 64;
+            buf = (uint8_t *)realloc(buf, cap);
+        }
+        memcpy(buf, blob + tmpl_off[j], len);
+        for (uint64_t h = hole_ptr[j]; h < hole_ptr[j + 1]; ++h)
+            memcpy(buf + hole_pos[h], slots32 + 32ull * hole_slot[h], 32);
+        orc_sha256(buf, len, slots32 + 32ull * out_slot[j]);
+    }
+    free(buf);
+}
+
 /* ------------------------------------------------------------------ */
 /* MurmurHash3 x64_128, seed 0 (murmur128.go:56-171)                   */
 /* ------------------------------------------------------------------ */

@@ -58,6 +58,8 @@ def lib():
                                                    ctypes.c_int]
         L.orc_bloomlive_add_batch.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p,
                                               ctypes.c_uint64]
+        L.orc_fill_batch.argtypes = [ctypes.c_uint64, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_int]
+        L.orc_graph_eval.argtypes = [ctypes.c_uint64, u8p, u8p, u8p, u8p, u8p, u8p, u8p, u8p, u8p]
         _LIB = L
     return _LIB
 

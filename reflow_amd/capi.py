@@ -28,6 +28,9 @@ EXPORTS = [
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
     "rf_bloom_destroy", "rf_bloom_probe", "rf_bloom_probe_device", "rf_bloom_add",
     "rf_bloom_add_device", "rf_bloom_params", "rf_bloom_words",
+    "rf_malloc", "rf_free", "rf_memcpy_h2d", "rf_memcpy_d2h", "rf_memset_d", "rf_stream",
+    "rf_timer_start", "rf_timer_stop", "rf_comm_unique_id", "rf_comm_init", "rf_comm_destroy",
+    "rf_comm_allgather", "rf_comm_allreduce_or", "rf_memcpy_d2d", "rf_graph_gather_device",
 ]
 
 
@@ -100,6 +103,15 @@ def lib():
             "rf_bloom_add_device": ([vp, vp, u64, vp], i32),
             "rf_bloom_params": ([vp, vp, vp, vp, vp], i32),
             "rf_bloom_words": ([vp, vp, u64], i32),
+            "rf_malloc": ([vp, u64, vp], i32), "rf_free": ([vp, vp], i32),
+            "rf_memcpy_h2d": ([vp, vp, vp, u64], i32), "rf_memcpy_d2h": ([vp, vp, vp, u64], i32),
+            "rf_memset_d": ([vp, vp, i32, u64], i32), "rf_stream": ([vp], vp),
+            "rf_timer_start": ([vp], i32), "rf_timer_stop": ([vp, vp], i32),
+            "rf_comm_unique_id": ([vp], i32), "rf_comm_init": ([vp, i32, i32, vp, vp], i32),
+            "rf_comm_destroy": ([vp], None), "rf_comm_allgather": ([vp, vp, vp, u64, vp], i32),
+            "rf_comm_allreduce_or": ([vp, vp, u64, vp], i32),
+            "rf_memcpy_d2d": ([vp, vp, vp, u64], i32),
+            "rf_graph_gather_device": ([vp, vp, u32, vp, vp], i32),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -146,6 +158,28 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    # ---- device memory (HBM owned through the engine's HIP runtime) ------
+    def alloc(self, nbytes) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
+    def upload(self, arr: np.ndarray) -> "DeviceBuffer":
+        arr = np.ascontiguousarray(arr)
+        b = DeviceBuffer(self, arr.nbytes)
+        b.copy_from(arr)
+        return b
+
+    def timer_start(self):
+        _check(lib().rf_timer_start(self._h))
+
+    def timer_stop(self) -> float:
+        ms = ctypes.c_float(0)
+        _check(lib().rf_timer_stop(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    @property
+    def stream(self):
+        return lib().rf_stream(self._h)
 
     def sync(self):
         _check(lib().rf_sync(self._h))
@@ -204,6 +238,73 @@ class Context:
         _check(lib().rf_fileset_digest_batch(self._h, n, _ptr(sg), _ptr(ge), pp, _ptr(pl),
                                              _ptr(idb), _ptr(out)))
         return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+
+class DeviceBuffer:
+    """HBM allocated through rf_malloc; .ptr is the device address."""
+
+    def __init__(self, ctx: Context, nbytes):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        _check(lib().rf_malloc(ctx.handle, self.nbytes, ctypes.byref(p)))
+        self._p = p
+
+    @property
+    def ptr(self):
+        return self._p.value
+
+    def copy_from(self, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _check(lib().rf_memcpy_h2d(self.ctx.handle, self._p, arr.ctypes.data, arr.nbytes))
+
+    def to_numpy(self, dtype=np.uint8, count=None) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = self.nbytes // dt.itemsize if count is None else count
+        out = np.empty(n, dtype=dt)
+        _check(lib().rf_memcpy_d2h(self.ctx.handle, out.ctypes.data, self._p, out.nbytes))
+        return out
+
+    def zero(self):
+        _check(lib().rf_memset_d(self.ctx.handle, self._p, 0, self.nbytes))
+
+    def free(self):
+        if self._p and self._p.value:
+            lib().rf_free(self.ctx.handle, self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Comm:
+    """RCCL communicator (one rank per GPU) inside the engine."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        b = ctypes.create_string_buffer(128)
+        _check(lib().rf_comm_unique_id(b))
+        return b.raw
+
+    def __init__(self, ctx: Context, nranks, rank, uid: bytes):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        _check(lib().rf_comm_init(ctx.handle, nranks, rank, ctypes.c_char_p(uid), ctypes.byref(self._h)))
+
+    def allgather(self, d_send, d_recv, nbytes, stream=None):
+        _check(lib().rf_comm_allgather(self._h, d_send, d_recv, nbytes, stream))
+
+    def allreduce_or(self, d_words, nwords, stream=None):
+        _check(lib().rf_comm_allreduce_or(self._h, d_words, nwords, stream))
+
+    def close(self):
+        if self._h:
+            lib().rf_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
 
 
 class ShaPlan:
@@ -276,6 +377,9 @@ class Graph:
 
     def recompute_async(self, full=False, stream=None):
         _check(lib().rf_graph_recompute_async(self._h, 1 if full else 0, stream))
+
+    def gather_device(self, d_slots, n, d_out, stream=None):
+        _check(lib().rf_graph_gather_device(self._h, d_slots, n, d_out, stream))
 
     def get_slots(self, slots) -> np.ndarray:
         slots = np.ascontiguousarray(slots, dtype=np.uint32)

@@ -18,6 +18,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "engine.h"
 #include "reflow_hip.h"
 
@@ -103,6 +105,7 @@ struct rf_ctx {
     std::mutex mu;
     DevBuf d_arena, d_out, d_tmp;
     HostBuf h_stage;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
 };
 
 struct DevGuard {
@@ -158,6 +161,8 @@ extern "C" void rf_destroy(rf_ctx* ctx) {
     ctx->d_out.release();
     ctx->d_tmp.release();
     ctx->h_stage.release();
+    if (ctx->t0) (void)hipEventDestroy(ctx->t0);
+    if (ctx->t1) (void)hipEventDestroy(ctx->t1);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -171,6 +176,146 @@ extern "C" int rf_sync(rf_ctx* ctx) {
 
 static hipStream_t pick(rf_ctx* ctx, void* stream) {
     return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+// ---------------------------------------------------------------------------
+// device memory / timing
+extern "C" int rf_malloc(rf_ctx* ctx, uint64_t bytes, void** out) {
+    ARG(ctx && out, "null argument");
+    DevGuard g(ctx->device);
+    *out = nullptr;
+    hipError_t e = hipMalloc(out, std::max<uint64_t>(bytes, 16));
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "hipMalloc(%llu): %s",
+                    (unsigned long long)bytes, hipGetErrorString(e));
+    return RF_OK;
+}
+
+extern "C" int rf_free(rf_ctx* ctx, void* p) {
+    ARG(ctx, "null ctx");
+    DevGuard g(ctx->device);
+    if (p) HIPC(hipFree(p));
+    return RF_OK;
+}
+
+extern "C" int rf_memcpy_h2d(rf_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    ARG(ctx && (bytes == 0 || (dst && src)), "null argument");
+    DevGuard g(ctx->device);
+    if (bytes) HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_memcpy_d2h(rf_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    ARG(ctx && (bytes == 0 || (dst && src)), "null argument");
+    DevGuard g(ctx->device);
+    if (bytes) HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_memset_d(rf_ctx* ctx, void* dst, int value, uint64_t bytes) {
+    ARG(ctx && (bytes == 0 || dst), "null argument");
+    DevGuard g(ctx->device);
+    if (bytes) HIPC(hipMemsetAsync(dst, value, bytes, ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_memcpy_d2d(rf_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    ARG(ctx && (bytes == 0 || (dst && src)), "null argument");
+    DevGuard g(ctx->device);
+    if (bytes) HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return RF_OK;
+}
+
+extern "C" void* rf_stream(rf_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+extern "C" int rf_timer_start(rf_ctx* ctx) {
+    ARG(ctx, "null ctx");
+    DevGuard g(ctx->device);
+    if (!ctx->t0) HIPC(hipEventCreate(&ctx->t0));
+    if (!ctx->t1) HIPC(hipEventCreate(&ctx->t1));
+    HIPC(hipEventRecord(ctx->t0, ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_timer_stop(rf_ctx* ctx, float* ms) {
+    ARG(ctx && ms && ctx->t0, "timer not started");
+    DevGuard g(ctx->device);
+    HIPC(hipEventRecord(ctx->t1, ctx->stream));
+    HIPC(hipEventSynchronize(ctx->t1));
+    HIPC(hipEventElapsedTime(ms, ctx->t0, ctx->t1));
+    return RF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RCCL
+struct rf_comm {
+    rf_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    DevBuf scratch;
+};
+
+#define NCCLC(x)                                                                          \
+    do {                                                                                  \
+        ncclResult_t r_ = (x);                                                            \
+        if (r_ != ncclSuccess) return fail(RF_EDEVICE, "%s: %s", #x, ncclGetErrorString(r_)); \
+    } while (0)
+
+extern "C" int rf_comm_unique_id(uint8_t id[128]) {
+    ARG(id, "null id");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    NCCLC(ncclGetUniqueId(&u));
+    memcpy(id, &u, 128);
+    return RF_OK;
+}
+
+extern "C" int rf_comm_init(rf_ctx* ctx, int nranks, int rank, const uint8_t id[128], rf_comm** out) {
+    ARG(ctx && id && out && nranks >= 1 && rank >= 0 && rank < nranks, "bad comm arguments");
+    DevGuard g(ctx->device);
+    ncclUniqueId u;
+    memcpy(&u, id, 128);
+    auto* c = new rf_comm();
+    c->ctx = ctx;
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return fail(RF_EDEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    *out = c;
+    return RF_OK;
+}
+
+extern "C" void rf_comm_destroy(rf_comm* c) {
+    if (!c) return;
+    DevGuard g(c->ctx->device);
+    c->scratch.release();
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+}
+
+extern "C" int rf_comm_allgather(rf_comm* c, const void* d_send, void* d_recv, uint64_t bytes,
+                                 void* stream) {
+    ARG(c && (bytes == 0 || (d_send && d_recv)), "null argument");
+    DevGuard g(c->ctx->device);
+    NCCLC(ncclAllGather(d_send, d_recv, bytes, ncclUint8, c->comm, pick(c->ctx, stream)));
+    return RF_OK;
+}
+
+extern "C" int rf_comm_allreduce_or(rf_comm* c, void* d_words, uint64_t nwords, void* stream) {
+    ARG(c && (nwords == 0 || d_words), "null argument");
+    DevGuard g(c->ctx->device);
+    if (!nwords) return RF_OK;
+    hipStream_t s = pick(c->ctx, stream);
+    HIPC(c->scratch.ensure(8ull * nwords * c->nranks));
+    NCCLC(ncclAllGather(d_words, c->scratch.p, nwords, ncclUint64, c->comm, s));
+    HIPC(launch_or_reduce(c->scratch.as<uint64_t>(), nwords, c->nranks,
+                          static_cast<uint64_t*>(d_words), s));
+    return RF_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -746,6 +891,15 @@ extern "C" int rf_graph_get_slots(rf_graph* gr, const uint32_t* slots, uint32_t 
                              ctx->stream));
     HIPC(hipMemcpyAsync(out32, gr->b_tmp_dig.p, 32ull * n, hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_graph_gather_device(rf_graph* gr, const void* d_slots, uint32_t n, void* d_out32,
+                                      void* stream) {
+    ARG(gr && (n == 0 || (d_slots && d_out32)), "null argument");
+    DevGuard dg(gr->ctx->device);
+    HIPC(launch_gather_slots(gr->g.slots, static_cast<const uint32_t*>(d_slots), n,
+                             static_cast<uint8_t*>(d_out32), pick(gr->ctx, stream)));
     return RF_OK;
 }
 

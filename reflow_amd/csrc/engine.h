@@ -66,6 +66,9 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipSt
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);
 
+hipError_t launch_or_reduce(const uint64_t* gathered, uint64_t nwords, int nranks, uint64_t* out,
+                            hipStream_t s);
+
 // ---- K4: bloom probe ---------------------------------------------------------
 struct BloomDev {
     uint64_t m = 1, k = 1, length = 0, nwords = 0;

@@ -184,6 +184,17 @@ __global__ __launch_bounds__(256) void k_gather_slots(const uint8_t* __restrict_
     }
 }
 
+// OR of nranks gathered copies of an nwords bitset (RCCL has no bitwise OR).
+__global__ __launch_bounds__(256) void k_or_reduce(const uint64_t* __restrict__ g, uint64_t nwords,
+                                                   int nranks, uint64_t* __restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nwords;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t v = 0;
+        for (int r = 0; r < nranks; ++r) v |= g[(uint64_t)r * nwords + i];
+        out[i] = v;
+    }
+}
+
 static uint32_t grid_for(uint64_t items, uint32_t cap) {
     uint64_t g = (items + 255) / 256;
     if (g < 1) g = 1;
@@ -209,6 +220,14 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                g.job_nblk, g.hole_ptr, g.hole_pos,  g.hole_slot, g.cons_ptr, g.cons_job,
                g.tmpl,     g.slots,    g.dirty};
     hipLaunchKernelGGL(k2_hash, dim3(grid_for(e - b, 8192)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_or_reduce(const uint64_t* gathered, uint64_t nwords, int nranks, uint64_t* out,
+                            hipStream_t s) {
+    if (!nwords) return hipSuccess;
+    hipLaunchKernelGGL(k_or_reduce, dim3(grid_for(nwords, 4096)), dim3(256), 0, s, gathered, nwords,
+                       nranks, out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,419 @@
+"""Synthetic workloads of BASELINE.json's configs.
+
+  c2_sizes     64 GiB FASTQ/BAM-like Fileset: 98% of files log-uniform in
+               [4 KiB, 1 MiB], 2% log-uniform in [64 MiB, 2 GiB] (seed 0x5EED0002)
+  Dag1000      1000align-shaped Flow DAG (doc/1000align/1000align.rf:36-47,
+               align.rf:54-97, bam.rf:12-42) lowered straight to rf_graph jobs,
+               vectorised so 10M-100M nodes build in seconds; 1% of leaf
+               File IDs change per step (seed 0x5EED0003): new = SHA256(old||"v2")
+  c5_keys      probe keys for the bloomlive filter (seed 0x5EED0005)
+
+The digest grammar is SURVEY App. A (flow.go:675-792).  Dag1000.oflow()
+builds the same graph as oracle flows for small S so tests can check the
+vectorised lowering against the oracle.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+import struct
+
+import numpy as np
+
+KiB, MiB, GiB = 1 << 10, 1 << 20, 1 << 30
+
+
+# --------------------------------------------------------------------- C2 --
+def c2_sizes(total_bytes=64 * GiB, seed=0x5EED0002, small=(4 * KiB, 1 * MiB),
+             big=(64 * MiB, 2 * GiB), big_frac=0.02):
+    """File sizes until their sum reaches total_bytes (last file trimmed)."""
+    rng = np.random.default_rng(seed)
+    out, acc = [], 0
+    while acc < total_bytes:
+        lo, hi = big if rng.random() < big_frac else small
+        n = int(math.exp(rng.uniform(math.log(lo), math.log(hi))))
+        n = min(n, total_bytes - acc)
+        out.append(n)
+        acc += n
+    return np.array(out, dtype=np.uint64)
+
+
+def arena_layout(lens, align=256):
+    """Offsets of messages packed at `align`-byte boundaries; total bytes."""
+    lens = np.asarray(lens, dtype=np.uint64)
+    padded = (lens + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum(padded[:-1])
+    total = int(padded.sum()) if len(lens) else 16
+    return offs, max(total, 16)
+
+
+# --------------------------------------------------------------------- C5 --
+def c5_keys(n, seed=0x5EED0005):
+    return np.random.default_rng(seed).integers(0, 256, size=(n, 32), dtype=np.uint8)
+
+
+# --------------------------------------------------------------------- C3 --
+def _h(s: bytes) -> bytes:
+    return hashlib.sha256(s).digest()
+
+
+def _le64(n: int) -> bytes:
+    return struct.pack("<q", n)
+
+
+WD0 = b"\x00\x05" + b"\0" * 32  # WD prefix + hole placeholder
+
+FD_COERCE_FILE = _h(b"file.fs$file")
+FD_FORCE = _h(b"grail.com/reflow/syntax.Eval.Force")
+FD_TO_FILESET = _h(b"grail.com/reflow/syntax.coerceFlowToFileset")
+FD_EXEC_OUT = _h(b"grail.com/reflow/syntax.Eval.coerceExecOutput")
+FD_MERGE = _h(b"grail.com/reflow/syntax.Eval.Force.merge")
+BWA = b"biocontainers/bwa"
+SAMTOOLS = b"biocontainers/samtools"
+REF_URL = b"s3://1000genomes/technical/reference/human_g1k_v37.fasta.gz"
+INDEX_CMD = (b"\n\tgunzip -c %s > %s/g1k_v37.fa || true\n\tcd %s\n\tbwa index -a bwtsw g1k_v37.fa\n")
+INDEX_FILES = [b"g1k_v37.fa", b"g1k_v37.fa.amb", b"g1k_v37.fa.ann", b"g1k_v37.fa.bwt",
+               b"g1k_v37.fa.pac", b"g1k_v37.fa.sa"]
+
+
+def _argmap(n_in):
+    """in(0..n_in-1), out(0): writeN(index) / writeN(-index) (flow.go:707-712)."""
+    return b"".join(_le64(i) for i in range(n_in)) + _le64(-0)
+
+
+def _digits(a: np.ndarray, width: int) -> np.ndarray:
+    """[n, width] ASCII decimal digits of a (zero padded)."""
+    a = np.asarray(a, dtype=np.int64)
+    out = np.empty((len(a), width), dtype=np.uint8)
+    x = a.copy()
+    for j in range(width - 1, -1, -1):
+        out[:, j] = 48 + (x % 10)
+        x //= 10
+    return out
+
+
+class _Kind:
+    """One node kind: a template of fixed length, per-instance digit fields,
+    per-instance literal byte fields and holes."""
+
+    def __init__(self, name, tmpl: bytes, count: int):
+        self.name, self.tmpl, self.count = name, tmpl, count
+        self.digit_fields = []   # (pos, width, values[count])
+        self.byte_fields = []    # (pos, values[count, k])
+        self.holes = []          # (pos, slot[count])
+        self.out_slot = None
+
+    def digits(self, pos, width, values):
+        self.digit_fields.append((pos, width, np.asarray(values)))
+
+    def bytes_at(self, pos, values):
+        self.byte_fields.append((pos, np.asarray(values, dtype=np.uint8)))
+
+    def hole(self, pos, slots):
+        self.holes.append((pos, np.asarray(slots, dtype=np.uint32)))
+
+
+class Dag1000:
+    """1000align-shaped DAG: S samples x P read pairs (~S*(14P+5) nodes).
+
+    Per pair: V1,V2 = Val(Fileset{".": File}) leaves (File IDs are input slots)
+      C1,C2 = Coerce ; E1 = Exec(bwa mem, [R2,C1,C2]) ; C3 ; K1 ; C4 ;
+      E2 = Exec(samtools view) ; C5 ; K2 ; C6 ; E3 = Exec(samtools sort) ; C7
+    Per sample: KS = K(C7 x P) (wide fan-in) ; CS1 ; ES = Exec(merge) ; CS2 ;
+      XS = Extern(s3://out/...)
+    Shared: R0 = Intern(ref) ; R1 = Exec(bwa index) ; R2 = Coerce
+    Physical keys (flow.go:764-792) for every Exec/Extern whose deps are done.
+    """
+
+    PAIR_KINDS = ["V1", "V2", "C1", "C2", "E1", "C3", "K1", "C4", "E2", "C5", "K2", "C6", "E3", "C7"]
+    SAMPLE_KINDS = ["KS", "CS1", "ES", "CS2", "XS"]
+
+    def __init__(self, S: int, P: int = 32, seed=0x5EED0003):
+        self.S, self.P, self.seed = S, P, seed
+        self.Q = S * P
+        self.n_nodes = 3 + self.Q * 14 + S * 5
+        self._build()
+
+    # deterministic "previous run" values
+    def file_id(self, i):  # File ID of leaf file i (2 per pair)
+        return _h(b"file:%d:%d" % (self.seed, i))
+
+    def out_id(self, tag, i):  # output File ID of exec instance i
+        return _h(b"out:%s:%d:%d" % (tag, self.seed, i))
+
+    def _ids(self, fn, n):
+        return np.frombuffer(b"".join(fn(i) for i in range(n)), dtype=np.uint8).reshape(n, 32)
+
+    def _build(self):
+        S, P, Q = self.S, self.P, self.Q
+        kinds = {}
+        # slots: [file slots 2Q][logical slots per kind][physical slots]
+        next_slot = [2 * Q]
+
+        def alloc(n):
+            b = next_slot[0]
+            next_slot[0] += n
+            return np.arange(b, b + n, dtype=np.uint32)
+
+        q = np.arange(Q)
+        s_of_q = q // P
+        p_of_q = q % P
+        sidx = np.arange(S)
+
+        # shared
+        k = _Kind("R0", b"OpIntern" + REF_URL, 1)
+        k.out_slot = alloc(1)
+        kinds["R0"] = k
+        idx_cmd = INDEX_CMD % (b"%s", b"%s", b"%s")
+        k = _Kind("R1", WD0 + b"OpExec" + BWA + idx_cmd + _argmap(1), 1)
+        k.hole(2, kinds["R0"].out_slot)
+        k.out_slot = alloc(1)
+        kinds["R1"] = k
+        k = _Kind("R2", WD0 + b"OpCoerce" + b"\x00\x05" + FD_EXEC_OUT, 1)
+        k.hole(2, kinds["R1"].out_slot)
+        k.out_slot = alloc(1)
+        kinds["R2"] = k
+
+        def coerce(name, dep_slots, fd, count):
+            kk = _Kind(name, WD0 + b"OpCoerce" + b"\x00\x05" + fd, count)
+            kk.hole(2, dep_slots)
+            kk.out_slot = alloc(count)
+            kinds[name] = kk
+            return kk
+
+        def kcont(name, dep_slots, fd, count):
+            kk = _Kind(name, WD0 + b"OpK" + b"\x00\x05" + fd, count)
+            kk.hole(2, dep_slots)
+            kk.out_slot = alloc(count)
+            kinds[name] = kk
+            return kk
+
+        # leaves: material "OpVal" + "." + WD(file id)
+        for j, name in enumerate(["V1", "V2"]):
+            kk = _Kind(name, b"OpVal" + b"." + WD0, Q)
+            kk.hole(8, 2 * q + j)
+            kk.out_slot = alloc(Q)
+            kinds[name] = kk
+        coerce("C1", kinds["V1"].out_slot, FD_COERCE_FILE, Q)
+        coerce("C2", kinds["V2"].out_slot, FD_COERCE_FILE, Q)
+        # E1: bwa mem, deps [R2, C1, C2]
+        cmd1 = (b'\n\t\tbwa mem -R "@RG\\tID:S0000000_P000\\tSM:S0000000" -t 32 \\\n'
+                b'\t\t\t%s/g1k_v37.fa %s %s > %s\n\t')
+        pre = 3 * 34 + len(b"OpExec") + len(BWA)
+        k = _Kind("E1", WD0 * 3 + b"OpExec" + BWA + cmd1 + _argmap(3), Q)
+        k.hole(2, np.repeat(kinds["R2"].out_slot, Q))
+        k.hole(36, kinds["C1"].out_slot)
+        k.hole(70, kinds["C2"].out_slot)
+        c = cmd1.index(b"S0000000_P000")
+        k.digits(pre + c + 1, 7, s_of_q)
+        k.digits(pre + c + 10, 3, p_of_q)
+        c2 = cmd1.index(b"SM:S0000000")
+        k.digits(pre + c2 + 4, 7, s_of_q)
+        k.out_slot = alloc(Q)
+        kinds["E1"] = k
+        coerce("C3", kinds["E1"].out_slot, FD_EXEC_OUT, Q)
+        kcont("K1", kinds["C3"].out_slot, FD_FORCE, Q)
+        coerce("C4", kinds["K1"].out_slot, FD_TO_FILESET, Q)
+        cmd2 = b"\n\t\t< %s samtools view -Sb - > %s # S0000000_P000\n\t"
+        pre2 = 34 + len(b"OpExec") + len(SAMTOOLS)
+        k = _Kind("E2", WD0 + b"OpExec" + SAMTOOLS + cmd2 + _argmap(1), Q)
+        k.hole(2, kinds["C4"].out_slot)
+        c = cmd2.index(b"S0000000_P000")
+        k.digits(pre2 + c + 1, 7, s_of_q)
+        k.digits(pre2 + c + 10, 3, p_of_q)
+        k.out_slot = alloc(Q)
+        kinds["E2"] = k
+        coerce("C5", kinds["E2"].out_slot, FD_EXEC_OUT, Q)
+        kcont("K2", kinds["C5"].out_slot, FD_FORCE, Q)
+        coerce("C6", kinds["K2"].out_slot, FD_TO_FILESET, Q)
+        cmd3 = b"\n\t\tsamtools sort --threads 64 -o %s %s # S0000000_P000\n\t"
+        k = _Kind("E3", WD0 + b"OpExec" + SAMTOOLS + cmd3 + _argmap(1), Q)
+        k.hole(2, kinds["C6"].out_slot)
+        c = cmd3.index(b"S0000000_P000")
+        k.digits(pre2 + c + 1, 7, s_of_q)
+        k.digits(pre2 + c + 10, 3, p_of_q)
+        k.out_slot = alloc(Q)
+        kinds["E3"] = k
+        coerce("C7", kinds["E3"].out_slot, FD_EXEC_OUT, Q)
+        # per sample: wide K over the P sorted BAMs
+        k = _Kind("KS", WD0 * P + b"OpK" + b"\x00\x05" + FD_MERGE, S)
+        c7 = kinds["C7"].out_slot.reshape(S, P)
+        for j in range(P):
+            k.hole(34 * j + 2, c7[:, j])
+        k.out_slot = alloc(S)
+        kinds["KS"] = k
+        coerce("CS1", kinds["KS"].out_slot, FD_TO_FILESET, S)
+        cmdm = b"\n\t\tsamtools merge -@64 %s %s # S0000000\n\t"
+        k = _Kind("ES", WD0 + b"OpExec" + SAMTOOLS + cmdm + _argmap(1), S)
+        k.hole(2, kinds["CS1"].out_slot)
+        k.digits(pre2 + cmdm.index(b"S0000000") + 1, 7, sidx)
+        k.out_slot = alloc(S)
+        kinds["ES"] = k
+        coerce("CS2", kinds["ES"].out_slot, FD_EXEC_OUT, S)
+        url = b"s3://1000genomes-out/S0000000.bam"
+        k = _Kind("XS", WD0 + b"OpExtern" + url, S)
+        k.hole(2, kinds["CS2"].out_slot)
+        k.digits(34 + len(b"OpExtern") + url.index(b"S0000000") + 1, 7, sidx)
+        k.out_slot = alloc(S)
+        kinds["XS"] = k
+        self.n_logical_slots = next_slot[0] - 2 * Q
+
+        # ---- physical keys: concat FM(dep values) || suffix ------------------
+        # values: R0 -> {".": ref}; R1/R2 -> index dir; V*/C1/C2 -> {".": file};
+        # E1..C7 outputs -> {".": out}; KS/CS1 -> list of P bams; ES/CS2 -> {".": merged}
+        self.ref_id = _h(b"ref:%d" % self.seed)
+        self.index_ids = [_h(b"index:%d:%s" % (self.seed, f)) for f in INDEX_FILES]
+        fm_index = b"".join(f + b"\x00\x05" + i for f, i in zip(INDEX_FILES, self.index_ids))
+        fm_dot = lambda: b"." + WD0  # noqa: E731  ("." + WD(hole/literal))
+
+        k = _Kind("pR1", b"." + b"\x00\x05" + self.ref_id + BWA + idx_cmd + _argmap(1), 1)
+        k.out_slot = alloc(1)
+        kinds["pR1"] = k
+        # E1: FM(R2 value = index dir) + FM(C1 value) + FM(C2 value) + suffix
+        e1_suffix = kinds["E1"].tmpl[3 * 34 + len(b"OpExec"):]
+        k = _Kind("pE1", fm_index + fm_dot() + fm_dot() + e1_suffix, Q)
+        k.hole(len(fm_index) + 3, 2 * q)
+        k.hole(len(fm_index) + 35 + 3, 2 * q + 1)
+        for pos, width, vals in kinds["E1"].digit_fields:
+            k.digits(pos - 3 * 34 - len(b"OpExec") + len(fm_index) + 70, width, vals)
+        k.out_slot = alloc(Q)
+        kinds["pE1"] = k
+        # E2: dep C4's value = E1's output {".": out_e1}; E3: C6 -> out_e2
+        for name, src, tag in [("pE2", "E2", b"e1"), ("pE3", "E3", b"e2")]:
+            suffix = kinds[src].tmpl[34 + len(b"OpExec"):]
+            kk = _Kind(name, b"." + b"\x00\x05" + b"\0" * 32 + suffix, Q)
+            kk.bytes_at(3, self._ids(lambda i, t=tag: self.out_id(t, i), Q))
+            for pos, width, vals in kinds[src].digit_fields:
+                kk.digits(pos - 34 - len(b"OpExec") + 35, width, vals)
+            kk.out_slot = alloc(Q)
+            kinds[name] = kk
+        # ES: dep CS1's value = list of P sorted bams (paths "." each)
+        suffix = kinds["ES"].tmpl[34 + len(b"OpExec"):]
+        kk = _Kind("pES", (b"." + b"\x00\x05" + b"\0" * 32) * P + suffix, S)
+        bam_ids = self._ids(lambda i: self.out_id(b"e3", i), Q).reshape(S, P, 32)
+        for j in range(P):
+            kk.bytes_at(35 * j + 3, bam_ids[:, j, :])
+        for pos, width, vals in kinds["ES"].digit_fields:
+            kk.digits(pos - 34 - len(b"OpExec") + 35 * P, width, vals)
+        kk.out_slot = alloc(S)
+        kinds["pES"] = kk
+        # XS extern: dep CS2 value = {".": merged} + URL
+        kk = _Kind("pXS", b"." + b"\x00\x05" + b"\0" * 32 + url, S)
+        kk.bytes_at(3, self._ids(lambda i: self.out_id(b"es", i), S))
+        kk.digits(35 + url.index(b"S0000000") + 1, 7, sidx)
+        kk.out_slot = alloc(S)
+        kinds["pXS"] = kk
+
+        self.kinds = kinds
+        self.n_slots = next_slot[0]
+        self.n_jobs = sum(kk.count for kk in kinds.values())
+        self.file_slots = np.arange(2 * Q, dtype=np.uint32)
+        self.leaf_ids = self._ids(self.file_id, 2 * Q)
+
+    # -------------------------------------------------------------- lowering
+    def arrays(self):
+        """rf_graph_desc arrays (out_slot, tmpl_off, tmpl_len, hole_ptr,
+        hole_pos, hole_slot, blob)."""
+        out_slot, off, ln, nh, hpos, hslot, blobs = [], [], [], [], [], [], []
+        base = 0
+        for kk in self.kinds.values():
+            L = len(kk.tmpl)
+            L16 = (L + 15) // 16 * 16
+            arr = np.zeros((kk.count, L16), dtype=np.uint8)
+            arr[:, :L] = np.frombuffer(kk.tmpl, dtype=np.uint8)
+            for pos, width, vals in kk.digit_fields:
+                arr[:, pos:pos + width] = _digits(vals, width)
+            for pos, vals in kk.byte_fields:
+                arr[:, pos:pos + vals.shape[1]] = vals
+            blobs.append(arr.reshape(-1))
+            out_slot.append(kk.out_slot)
+            off.append(base + np.arange(kk.count, dtype=np.uint64) * np.uint64(L16))
+            ln.append(np.full(kk.count, L, dtype=np.uint32))
+            nh.append(np.full(kk.count, len(kk.holes), dtype=np.uint64))
+            if kk.holes:
+                hpos.append(np.tile(np.array([p for p, _ in kk.holes], dtype=np.uint32), kk.count))
+                hslot.append(np.stack([sl for _, sl in kk.holes], axis=1).reshape(-1))
+            base += kk.count * L16
+        hole_ptr = np.zeros(self.n_jobs + 1, dtype=np.uint64)
+        hole_ptr[1:] = np.cumsum(np.concatenate(nh))
+        return dict(n_slots=self.n_slots, out_slot=np.concatenate(out_slot),
+                    tmpl_off=np.concatenate(off), tmpl_len=np.concatenate(ln), hole_ptr=hole_ptr,
+                    hole_pos=np.concatenate(hpos), hole_slot=np.concatenate(hslot).astype(np.uint32),
+                    blob=np.concatenate(blobs))
+
+    def change_set(self, frac=0.01, seed=0x5EED0003):
+        """File slots to change (1% of leaf files) and their two versions:
+        v_old = current IDs, v_new = SHA256(old || "v2")."""
+        rng = np.random.default_rng(seed)
+        n = max(1, int(round(frac * len(self.file_slots))))
+        pick = np.sort(rng.choice(len(self.file_slots), size=n, replace=False)).astype(np.uint32)
+        old = self.leaf_ids[pick]
+        new = np.frombuffer(b"".join(_h(o.tobytes() + b"v2") for o in old), dtype=np.uint8).reshape(n, 32)
+        return self.file_slots[pick], old, new
+
+    # ------------------------------------------------ oracle twin (small S)
+    def oflow(self, file_ids=None):
+        """The same graph as reflow_oracle.OFlow objects (test infrastructure).
+        Returns (nodes by kind name -> list, physical-bearing nodes)."""
+        from reflow_oracle import OFileset, OFlow  # noqa: imported only by tests
+        S, P, Q = self.S, self.P, self.Q
+        fid = (lambda i: self.leaf_ids[i].tobytes()) if file_ids is None else file_ids
+        T = {name: [] for name in self.kinds}
+        one = lambda i: OFileset(map={".": (i, 0)})  # noqa: E731
+        idx_cmd = INDEX_CMD % (b"%s", b"%s", b"%s")
+        r0 = OFlow("OpIntern", url=REF_URL.decode(), done=True, value=one(self.ref_id))
+        r1 = OFlow("OpExec", [r0], image=BWA.decode(), cmd=idx_cmd.decode(), argmap=[(False, 0), (True, 0)],
+                   done=True, value=OFileset(map={f.decode(): (i, 0) for f, i in zip(INDEX_FILES, self.index_ids)}))
+        r2 = OFlow("OpCoerce", [r1], flow_digest=FD_EXEC_OUT, done=True, value=r1.value)
+        T["R0"], T["R1"], T["R2"] = [r0], [r1], [r2]
+
+        def cmd_of(kind, i):
+            kk = self.kinds[kind]
+            L = len(kk.tmpl)
+            arr = np.frombuffer(kk.tmpl, dtype=np.uint8).copy()
+            for pos, width, vals in kk.digit_fields:
+                arr[pos:pos + width] = _digits(vals[i:i + 1], width)[0]
+            return arr[:L].tobytes()
+
+        def exec_cmd(kind, i, ndeps, image):
+            t = cmd_of(kind, i)
+            body = t[ndeps * 34 + len(b"OpExec") + len(image):]
+            return body[:len(body) - 8 * (ndeps + 1)].decode()
+
+        c7s = []
+        for i in range(Q):
+            v1 = OFlow("OpVal", value=one(fid(2 * i)), done=True)
+            v2 = OFlow("OpVal", value=one(fid(2 * i + 1)), done=True)
+            c1 = OFlow("OpCoerce", [v1], flow_digest=FD_COERCE_FILE, done=True, value=v1.value)
+            c2 = OFlow("OpCoerce", [v2], flow_digest=FD_COERCE_FILE, done=True, value=v2.value)
+            e1 = OFlow("OpExec", [r2, c1, c2], image=BWA.decode(), cmd=exec_cmd("E1", i, 3, BWA),
+                       argmap=[(False, 0), (False, 1), (False, 2), (True, 0)], done=True,
+                       value=one(self.out_id(b"e1", i)))
+            c3 = OFlow("OpCoerce", [e1], flow_digest=FD_EXEC_OUT, done=True, value=e1.value)
+            k1 = OFlow("OpK", [c3], flow_digest=FD_FORCE, done=True, value=e1.value)
+            c4 = OFlow("OpCoerce", [k1], flow_digest=FD_TO_FILESET, done=True, value=e1.value)
+            e2 = OFlow("OpExec", [c4], image=SAMTOOLS.decode(), cmd=exec_cmd("E2", i, 1, SAMTOOLS),
+                       argmap=[(False, 0), (True, 0)], done=True, value=one(self.out_id(b"e2", i)))
+            c5 = OFlow("OpCoerce", [e2], flow_digest=FD_EXEC_OUT, done=True, value=e2.value)
+            k2 = OFlow("OpK", [c5], flow_digest=FD_FORCE, done=True, value=e2.value)
+            c6 = OFlow("OpCoerce", [k2], flow_digest=FD_TO_FILESET, done=True, value=e2.value)
+            e3 = OFlow("OpExec", [c6], image=SAMTOOLS.decode(), cmd=exec_cmd("E3", i, 1, SAMTOOLS),
+                       argmap=[(False, 0), (True, 0)], done=True, value=one(self.out_id(b"e3", i)))
+            c7 = OFlow("OpCoerce", [e3], flow_digest=FD_EXEC_OUT, done=True, value=e3.value)
+            for name, f in zip(self.PAIR_KINDS, [v1, v2, c1, c2, e1, c3, k1, c4, e2, c5, k2, c6, e3, c7]):
+                T[name].append(f)
+            c7s.append(c7)
+        for s in range(S):
+            deps = c7s[s * P:(s + 1) * P]
+            ks = OFlow("OpK", deps, flow_digest=FD_MERGE, done=True,
+                       value=OFileset(list=[d.value for d in deps]))
+            cs1 = OFlow("OpCoerce", [ks], flow_digest=FD_TO_FILESET, done=True, value=ks.value)
+            es = OFlow("OpExec", [cs1], image=SAMTOOLS.decode(), cmd=exec_cmd("ES", s, 1, SAMTOOLS),
+                       argmap=[(False, 0), (True, 0)], done=True, value=one(self.out_id(b"es", s)))
+            cs2 = OFlow("OpCoerce", [es], flow_digest=FD_EXEC_OUT, done=True, value=es.value)
+            xs = OFlow("OpExtern", [cs2], url="s3://1000genomes-out/S%07d.bam" % s)
+            for name, f in zip(self.SAMPLE_KINDS, [ks, cs1, es, cs2, xs]):
+                T[name].append(f)
+        return T

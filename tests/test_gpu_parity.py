@@ -72,28 +72,27 @@ def _device_arena(lens, align=256):
 def test_plan_gen_fill_device(ctx, flags):
     """rf_gen_fill + rf_sha_plan_run on HBM-resident data (the bench path),
     lanes-only / solo-only / planner mix."""
-    import torch
     from reflow_amd import capi
     rng = random.Random(10 + flags)
     lens = [rng.choice([0, 1, 55, 56, 64, 4096, rng.randint(1, 300000), rng.randint(1, 3000)])
             for _ in range(120)] + [2_000_000, 1_100_000]
     offs, total = _device_arena(lens)
-    d_arena = torch.empty(total, dtype=torch.uint8, device="cuda")
-    d_offs = torch.from_numpy(offs).cuda()
-    d_lens = torch.from_numpy(np.array(lens, dtype=np.uint64)).cuda()
-    d_out = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
+    d_arena = ctx.alloc(total)
+    d_offs = ctx.upload(offs)
+    d_lens = ctx.upload(np.array(lens, dtype=np.uint64))
+    d_out = ctx.alloc(len(lens) * 32)
     seed = 0x5EED0002
-    ctx.gen_fill(d_arena.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), len(lens), seed, total)
+    ctx.gen_fill(d_arena.ptr, d_offs.ptr, d_lens.ptr, len(lens), seed, total)
     plan = ctx.sha_plan(offs, np.array(lens, dtype=np.uint64), flags)
-    plan.run(d_arena.data_ptr(), d_out.data_ptr())
+    plan.run(d_arena.ptr, d_out.ptr)
     ctx.sync()
     st = plan.stats()
     if flags == capi.RF_SHA_ALL_SOLO:
         assert st.n_solo == len(lens)
     if flags == capi.RF_SHA_NO_SOLO:
         assert st.n_solo == 0
-    out = d_out.cpu().numpy().reshape(-1, 32)
-    arena = d_arena.cpu().numpy()
+    out = d_out.to_numpy().reshape(-1, 32)
+    arena = d_arena.to_numpy()
     for i, n in enumerate(lens):
         want = O.sha256(O.fill_stream(seed ^ i, n))
         # generator parity too: device bytes == oracle stream

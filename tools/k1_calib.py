@@ -7,7 +7,6 @@ import sys
 import time
 
 import numpy as np
-import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from reflow_amd import capi  # noqa: E402
@@ -20,16 +19,16 @@ def run_case(ctx, name, lens, flags, reps=3):
     for i, n in enumerate(lens):
         offs[i] = pos
         pos += (int(n) + 255) // 256 * 256
-    arena = torch.empty(max(pos, 16), dtype=torch.uint8, device="cuda")
-    d_offs = torch.from_numpy(offs).cuda()
-    d_lens = torch.from_numpy(lens).cuda()
-    out = torch.empty(len(lens) * 32, dtype=torch.uint8, device="cuda")
-    ctx.gen_fill(arena.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), len(lens), 1, arena.numel())
+    arena = ctx.alloc(max(pos, 16))
+    d_offs = ctx.upload(offs)
+    d_lens = ctx.upload(lens)
+    out = ctx.alloc(len(lens) * 32)
+    ctx.gen_fill(arena.ptr, d_offs.ptr, d_lens.ptr, len(lens), 1, arena.nbytes)
     ctx.sync()
     plan = ctx.sha_plan(offs, lens, flags)
     best = None
     for _ in range(reps):
-        plan.run(arena.data_ptr(), out.data_ptr())
+        plan.run(arena.ptr, out.ptr)
         st = plan.stats()
         best = st.last_ms_total if best is None else min(best, st.last_ms_total)
     st = plan.stats()
@@ -40,7 +39,7 @@ def run_case(ctx, name, lens, flags, reps=3):
           % (name, len(lens), float(lens.sum()), st.n_solo, best, gbs, ops / (best * 1e-3) / 1e12,
              st.max_blocks), flush=True)
     plan.close()
-    del arena
+    arena.free()
 
 
 def main():

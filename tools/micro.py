@@ -1,0 +1,47 @@
+"""Runs the K1 diagnostic microbenchmarks (tools/micro.hip) on the GPU."""
+import ctypes
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "_micro.so")
+
+
+def build():
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                           "-fPIC", "-Wno-unused-value", "-shared", os.path.join(HERE, "micro.hip"), "-o", SO])
+
+
+def main():
+    if not os.path.exists(SO) or (len(sys.argv) > 1 and sys.argv[1] == "build"):
+        build()
+        if len(sys.argv) > 1 and sys.argv[1] == "build":
+            return
+    L = ctypes.CDLL(SO)
+    L.micro_compute.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.micro_compute.restype = ctypes.c_float
+    L.micro_loads.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+    L.micro_loads.restype = ctypes.c_float
+    peak = 256 * 128 * 2.4e9
+    for grid in [256, 512, 1024, 1280, 2048]:
+        nblk = 256
+        ms = L.micro_compute(grid, nblk)
+        ops = grid * 256 * nblk * 1464
+        print("compute grid=%5d waves/SIMD=%.1f  %.3f ms  %.2f Tops/s  (%.0f%% of 78.6)  %.0f GB/s-equiv"
+              % (grid, grid / 256.0, ms, ops / ms / 1e9, 100 * ops / ms / 1e9 / (peak / 1e12) / 1e3 * 1e3 / 1e3,
+                 grid * 256 * nblk * 64 / ms / 1e6), flush=True)
+    KB = 1024
+    for layout, stride, nlanes, nblk, pf in [
+        (1, 0, 65536, 1024, 0), (1, 0, 65536, 1024, 1), (1, 0, 262144, 256, 0), (1, 0, 262144, 256, 1),
+        (0, 64 * KB, 65536, 1024, 0), (0, 64 * KB, 65536, 1024, 1), (0, 64 * KB + 256, 65536, 1024, 1),
+        (0, 16 * KB, 262144, 256, 0), (0, 16 * KB, 262144, 256, 1), (0, 16 * KB + 256, 262144, 256, 1),
+        (0, 16 * KB + 64, 262144, 256, 1), (0, 4 * KB, 262144, 64, 1), (0, 4 * KB + 64, 262144, 64, 1)]:
+        ms = L.micro_loads(stride, nblk, nlanes, layout, pf)
+        b = nlanes * nblk * 64
+        print("loads layout=%d stride=%7d lanes=%7d nblk=%5d prefetch=%d  %.3f ms  %.1f GB/s  %.2f Tops/s"
+              % (layout, stride, nlanes, nblk, pf, ms, b / ms / 1e6, b / 64 * 1464 / ms / 1e9), flush=True)
+
+
+if __name__ == "__main__":
+    main()
