@@ -937,13 +937,13 @@ static int bloom_make(rf_ctx* ctx, uint64_t m, uint64_t k, const uint64_t* words
     ARG(k < (1ull << 31), "bloom k too large");
     // bitset words needed for `length` bits (bitset.go:89-94)
     const uint64_t need = (length + 63) / 64;
-    ARG(nwords >= need, "fewer words than the bitset length needs");
+    ARG(!words || nwords >= need, "fewer words than the bitset length needs");
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
     auto* bl = new rf_bloom();
     bl->ctx = ctx;
     // capacity: enough words for any location < m (Add may grow length to m)
-    const uint64_t cap = std::max<uint64_t>(std::max(nwords, (m + 63) / 64), 1);
+    const uint64_t cap = std::max<uint64_t>(std::max(std::max(nwords, need), (m + 63) / 64), 1);
     hipError_t e;
     if ((e = bl->words.ensure(8 * cap)) != hipSuccess || (e = bl->len_dev.ensure(8)) != hipSuccess) {
         delete bl;

@@ -60,23 +60,44 @@ __device__ __forceinline__ void load_block(uint32_t (&w)[16], const uint8_t* p, 
     }
 }
 
+// Wave-cooperative dequeue: the lanes that need a message are counted with a
+// ballot and served by ONE atomicAdd per wave on the wave's queue shard
+// (message position q belongs to shard q % n_shards; LPT order is kept across
+// shards).  Per-lane atomics on a shared counter serialise at ~0.1-0.3 us each
+// (measured: 262k messages took 80 ms), the wave form costs one per wave.
+// shard/tries are wave-uniform; an exhausted shard moves the whole wave on.
+__device__ __forceinline__ uint32_t wave_fetch(const LanesArgs& a, bool need, uint32_t& shard,
+                                               uint32_t& tries) {
+    const uint32_t lane = __lane_id();
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t got = kNone;
+    uint64_t mask = __ballot(need);
+    while (mask && tries < a.n_shards) {
+        const uint32_t cnt = (uint32_t)__popcll(mask);
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&a.heads[shard], cnt);
+        base = __shfl(base, leader, 64);
+        const bool mine = (mask >> lane) & 1ull;
+        if (mine) {
+            const uint64_t q = (uint64_t)(base + (uint32_t)__popcll(mask & lt)) * a.n_shards + shard;
+            if (q < a.n_order) got = a.order[q];
+        }
+        mask = __ballot(mine && got == kNone);
+        if (mask) {  // this shard ran dry for some lanes: the wave moves on
+            shard = (shard + 1 == a.n_shards) ? 0u : shard + 1;
+            ++tries;
+        }
+    }
+    return got;
+}
+
 __global__ __launch_bounds__(kLanesBlock) void k1_sha256_lanes(LanesArgs a) {
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t shard = (gtid >> 6) % a.n_shards;
     uint32_t tries = 0;
 
-    auto fetch = [&]() -> uint32_t {
-        while (tries < a.n_shards) {
-            const uint32_t pl = atomicAdd(&a.heads[shard], 1u);
-            const uint64_t q = (uint64_t)pl * a.n_shards + shard;
-            if (q < a.n_order) return a.order[q];
-            shard = (shard + 1 == a.n_shards) ? 0u : shard + 1;
-            ++tries;
-        }
-        return kNone;
-    };
-
-    uint32_t id = fetch();
+    uint32_t id = wave_fetch(a, true, shard, tries);
     const uint8_t* p = nullptr;
     uint64_t len = 0, nb = 0, blk = 0;
     ShaState st;
@@ -87,6 +108,7 @@ __global__ __launch_bounds__(kLanesBlock) void k1_sha256_lanes(LanesArgs a) {
         nb = sha256_nblocks(len);
     }
     while (__any(id != kNone)) {
+        bool done = false;
         if (id != kNone) {
             uint32_t w[16];
             load_block(w, p, len, blk);
@@ -94,14 +116,19 @@ __global__ __launch_bounds__(kLanesBlock) void k1_sha256_lanes(LanesArgs a) {
             ++blk;
             if (blk == nb) {
                 store_digest(a.out + 32ull * id, st);
-                id = fetch();
-                st.init();
-                blk = 0;
-                if (id != kNone) {
-                    p = a.arena + a.offs[id];
-                    len = a.lens[id];
-                    nb = sha256_nblocks(len);
-                }
+                done = true;
+            }
+        }
+        // wave-uniform point: one dequeue for every lane that finished
+        const uint32_t nid = wave_fetch(a, done, shard, tries);
+        if (done) {
+            id = nid;
+            st.init();
+            blk = 0;
+            if (id != kNone) {
+                p = a.arena + a.offs[id];
+                len = a.lens[id];
+                nb = sha256_nblocks(len);
             }
         }
     }

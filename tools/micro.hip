@@ -61,6 +61,60 @@ __global__ __launch_bounds__(256) void k_loads(const uint8_t* arena, uint64_t st
     out[g] = st.h[0];
 }
 
+// C: issue rate of single VALU opcodes: 8 independent chains per lane, each
+// iteration 8 instructions, opcode selected by template (inline asm so the
+// compiler keeps the exact instruction).
+template <int OP>
+__global__ __launch_bounds__(256) void k_op(uint32_t iters, uint32_t* out) {
+    uint32_t r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = threadIdx.x * 7 + j;
+    const uint32_t c = blockIdx.x | 1;
+    for (uint32_t i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[j]) : "v"(c));
+            if constexpr (OP == 1) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(r[j]));
+            if constexpr (OP == 2) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(r[j]) : "v"(c));
+            if constexpr (OP == 3) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(r[j]) : "v"(c));
+            if constexpr (OP == 4) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[j]) : "v"(c));
+            if constexpr (OP == 5) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(r[j]) : "v"(c));
+            if constexpr (OP == 6) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(r[j]));
+            if constexpr (OP == 7) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(r[j]) : "v"(c));
+        }
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x ^= r[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+struct OArgs { int op; uint32_t grid, iters; uint32_t* out; };
+static void run_op(void* p) {
+    auto* a = (OArgs*)p;
+    switch (a->op) {
+    case 0: hipLaunchKernelGGL(k_op<0>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    case 1: hipLaunchKernelGGL(k_op<1>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    case 2: hipLaunchKernelGGL(k_op<2>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    case 3: hipLaunchKernelGGL(k_op<3>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    case 4: hipLaunchKernelGGL(k_op<4>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    case 5: hipLaunchKernelGGL(k_op<5>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    case 6: hipLaunchKernelGGL(k_op<6>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    default: hipLaunchKernelGGL(k_op<7>, dim3(a->grid), dim3(256), 0, 0, a->iters, a->out); break;
+    }
+}
+
+static float time_launch(void (*fn)(void*), void* arg);
+
+extern "C" float micro_op(int op, uint32_t grid, uint32_t iters) {
+    uint32_t* out;
+    if (hipMalloc(&out, (size_t)grid * 256 * 4) != hipSuccess) return -2.f;
+    OArgs a{op, grid, iters, out};
+    float ms = time_launch(run_op, &a);
+    hipFree(out);
+    return ms;
+}
+
 static float time_launch(void (*fn)(void*), void* arg) {
     hipEvent_t a, b;
     hipEventCreate(&a);

@@ -23,6 +23,17 @@ def main():
     L.micro_compute.restype = ctypes.c_float
     L.micro_loads.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
     L.micro_loads.restype = ctypes.c_float
+    L.micro_op.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32]
+    L.micro_op.restype = ctypes.c_float
+    names = ["v_add_u32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32", "v_xor_b32", "v_perm_b32",
+             "v_lshrrev_b32", "v_fma_f32"]
+    for op, name in enumerate(names):
+        for grid in [256, 2048]:
+            iters = 4096
+            ms = L.micro_op(op, grid, iters)
+            n = grid * 256 * iters * 8
+            print("op %-16s grid=%5d (%d waves/SIMD)  %.3f ms  %.2f T lane-ops/s  (%.0f%% of 78.6)"
+                  % (name, grid, grid // 256, ms, n / ms / 1e9, 100 * n / ms / 1e9 / 78.64), flush=True)
     peak = 256 * 128 * 2.4e9
     for grid in [256, 512, 1024, 1280, 2048]:
         nblk = 256
