@@ -324,6 +324,7 @@ struct rf_sha_plan {
     rf_ctx* ctx = nullptr;
     uint64_t n = 0;
     uint32_t n_lanes = 0, n_solo = 0, grid = 0, n_shards = 1;
+    bool duo = true;  // wave-per-message kernel: two-lane chain (default) or one-lane
     DevBuf d_offs, d_lens, d_order, d_heads;  // d_order = [lanes order | solo order]
     hipStream_t side = nullptr;
     hipEvent_t e0 = nullptr, e_solo = nullptr, e_lanes = nullptr, e1 = nullptr;
@@ -391,6 +392,7 @@ static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t*
     uint32_t n_solo = 0;
     plan_split(nb, order, (uint32_t)ctx->n_cu, flags, &n_solo);
     p->n_solo = n_solo;
+    p->duo = !(flags & RF_SHA_ONE_LANE_CHAIN);
     p->n_lanes = (uint32_t)(n - n_solo);
     // The lanes kernel is persistent: enough 256-thread blocks for every lane
     // message, capped at 5 blocks per CU (its VGPR-limited residency).
@@ -440,7 +442,7 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
         SoloArgs sa{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(),
                     p->d_lens.as<uint64_t>(), order + p->n_lanes, p->n_solo,
                     static_cast<uint8_t*>(d_out)};
-        HIPC(launch_sha_solo(sa, p->side));
+        HIPC(launch_sha_solo(sa, p->duo, p->side));
         HIPC(hipEventRecord(p->e_solo, p->side));
     }
     if (p->n_lanes) {
@@ -619,6 +621,7 @@ struct rf_graph {
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
     uint32_t max_level_jobs = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipGraphExec_t exec_inc = nullptr, exec_full = nullptr;
     bool timed = false;
 };
 
@@ -795,6 +798,8 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);
+        if (gr->exec_inc) (void)hipGraphExecDestroy(gr->exec_inc);
+        if (gr->exec_full) (void)hipGraphExecDestroy(gr->exec_full);
     }
     delete gr;
 }
@@ -836,15 +841,45 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
     return RF_OK;
 }
 
-static int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
+// The per-level launch sequence (2 kernels per level + 2 memsets) only reads
+// device-side counts, so it is fixed for a loaded graph: capture it once per
+// mode into a hipGraph and replay (kernel boundaries ~1.5 us instead of a host
+// launch each; MI355X_MICROARCH "boundary" / "graph-replay-floor").
+static int graph_enqueue(rf_graph* gr, int full, hipStream_t s) {
     GraphDev& G = gr->g;
-    if (!gr->initialized) full = 1;
     const size_t dirty_bytes = 4ull * ((G.n_jobs + 31) / 32 + 1);
-    HIPC(hipEventRecord(gr->e0, s));
     if (full) HIPC(hipMemsetAsync(G.dirty, 0xff, dirty_bytes, s));
     HIPC(hipMemsetAsync(G.counts, 0, 4ull * (G.n_levels + 1), s));
     for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
     HIPC(hipMemsetAsync(G.dirty, 0, dirty_bytes, s));
+    return RF_OK;
+}
+
+static int graph_capture(rf_graph* gr, int full, hipGraphExec_t* out) {
+    hipStream_t cs = nullptr;
+    HIPC(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t graph = nullptr;
+    int rc = RF_OK;
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+        rc = graph_enqueue(gr, full, cs);
+        e = hipStreamEndCapture(cs, &graph);
+    }
+    if (e == hipSuccess && rc == RF_OK) e = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipStreamDestroy(cs);
+    if (rc != RF_OK) return rc;
+    if (e != hipSuccess) return fail(RF_EDEVICE, "graph capture: %s", hipGetErrorString(e));
+    return RF_OK;
+}
+
+static int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
+    if (!gr->initialized) full = 1;
+    hipGraphExec_t& ex = full ? gr->exec_full : gr->exec_inc;
+    if (!ex && gr->g.n_levels)
+        if (int rc = graph_capture(gr, full, &ex)) return rc;
+    HIPC(hipEventRecord(gr->e0, s));
+    if (ex) HIPC(hipGraphLaunch(ex, s));
     HIPC(hipEventRecord(gr->e1, s));
     gr->timed = true;
     gr->initialized = true;

@@ -33,7 +33,8 @@ struct SoloArgs {
     uint32_t n_order;
     uint8_t* out;
 };
-hipError_t launch_sha_solo(const SoloArgs& a, hipStream_t s);
+// duo: the round chain on two lanes (k1_sha256_duo); else one lane (k1_sha256_solo)
+hipError_t launch_sha_solo(const SoloArgs& a, bool duo, hipStream_t s);
 
 // Checks that the gfx950 code object of this library loads on the device.
 hipError_t probe_kernels();

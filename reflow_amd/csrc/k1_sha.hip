@@ -200,6 +200,94 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Duo: one wave per long message, the round chain split over two lanes.
+// Lanes with (lane & 8) == 0 ("e-lanes") hold (e,f,g,h); their partners
+// lane^8 ("a-lanes") hold (a,b,c,d).  One instruction stream serves both:
+//   S = Σ1(e) | Σ0(a)            3 v_alignbit with per-lane amounts + xor3
+//   F = Ch(e,f,g) | Maj(a,b,c)   Maj(a,b,c) = Ch(a^c, b, c): sel = X0^(X2&M)
+//   R = Z + S + F                Z = h+K+W on e-lanes, 0 on a-lanes
+//   N = D[lane^8] + R            D = R (e-lanes) | d (a-lanes), DPP row_ror:8
+// so e-lanes get e' = d + T1 and a-lanes a' = T1 + Σ0 + Maj: 11 VALU per
+// round instead of 14 on one lane.  K+W comes from LDS as in the solo kernel.
+__global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ __attribute__((aligned(16))) uint32_t kw[64 * kRow];
+    constexpr uint32_t K[64] = RF_SHA_K;
+    const uint32_t lane = threadIdx.x;
+    const bool elane = (lane & 8) == 0;
+    const uint32_t sh1 = elane ? 6 : 2, sh2 = elane ? 11 : 13, sh3 = elane ? 25 : 22;
+    const uint32_t M = elane ? 0u : ~0u;
+    for (uint32_t q = blockIdx.x; q < a.n_order; q += gridDim.x) {
+        const uint32_t id = a.order[q];
+        const uint8_t* p = a.arena + a.offs[id];
+        const uint64_t len = a.lens[id];
+        const uint64_t nb = sha256_nblocks(len);
+        // e-lanes: H4..H7, a-lanes: H0..H3
+        uint32_t H0 = elane ? 0x510e527fu : 0x6a09e667u, H1 = elane ? 0x9b05688cu : 0xbb67ae85u;
+        uint32_t H2 = elane ? 0x1f83d9abu : 0x3c6ef372u, H3 = elane ? 0x5be0cd19u : 0xa54ff53au;
+        for (uint64_t c = 0; c < nb; c += 64) {
+            const uint64_t b = c + lane;
+            if (b < nb) {
+                uint32_t w[16];
+                load_block(w, p, len, b);
+                uint32_t* row = &kw[lane * kRow];
+#pragma unroll
+                for (int t = 0; t < 64; ++t) {
+                    uint32_t wt;
+                    if (t < 16) {
+                        wt = w[t];
+                    } else {
+                        wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) +
+                             w[t & 15];
+                        w[t & 15] = wt;
+                    }
+                    row[t] = K[t] + wt;
+                }
+            }
+            __syncthreads();
+            const uint32_t cnt = (uint32_t)((nb - c) < 64 ? (nb - c) : 64);
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const uint4* r4 = reinterpret_cast<const uint4*>(&kw[j * kRow]);
+                uint32_t X0 = H0, X1 = H1, X2 = H2, X3 = H3;
+                uint4 v = r4[0];
+                uint32_t Z = elane ? X3 + v.x : 0u;
+#pragma unroll
+                for (int t4 = 0; t4 < 16; ++t4) {
+                    const uint4 vn = t4 < 15 ? r4[t4 + 1] : make_uint4(0, 0, 0, 0);
+                    const uint32_t kv[5] = {v.x, v.y, v.z, v.w, vn.x};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t S = xor3(__builtin_amdgcn_alignbit(X0, X0, sh1),
+                                                __builtin_amdgcn_alignbit(X0, X0, sh2),
+                                                __builtin_amdgcn_alignbit(X0, X0, sh3));
+                        const uint32_t sel = __builtin_amdgcn_bitop3_b32(X0, X2, M, 0x78);
+                        const uint32_t F = __builtin_amdgcn_bitop3_b32(sel, X1, X2, 0xCA);
+                        const uint32_t R = add3v(Z, S, F);
+                        const uint32_t D = elane ? R : X3;
+                        // two independent VALU between D's write and its DPP read
+                        // cover the VALU->DPP hazard (no s_nop)
+                        const uint32_t T = X2 + kv[u + 1];
+                        Z = elane ? T : 0u;
+                        const uint32_t N =
+                            (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D, 0x128, 0xF, 0xF, false) + R;
+                        X3 = X2; X2 = X1; X1 = X0; X0 = N;
+                    }
+                    v = vn;
+                }
+                H0 += X0; H1 += X1; H2 += X2; H3 += X3;
+            }
+            __syncthreads();
+        }
+        // lane 8 (a-lane) holds H0..H3, lane 0 (e-lane) H4..H7
+        if (lane == 0 || lane == 8) {
+            uint4 o;
+            o.x = bswap32(H0); o.y = bswap32(H1); o.z = bswap32(H2); o.w = bswap32(H3);
+            reinterpret_cast<uint4*>(a.out + 32ull * id)[lane == 0 ? 1 : 0] = o;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic content: word q of message i = mix64((seed ^ i) + (q+1)*G), LE.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -261,9 +349,12 @@ hipError_t launch_sha_lanes(const LanesArgs& a, uint32_t grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_sha_solo(const SoloArgs& a, hipStream_t s) {
+hipError_t launch_sha_solo(const SoloArgs& a, bool duo, hipStream_t s) {
     if (a.n_order == 0) return hipSuccess;
-    hipLaunchKernelGGL(k1_sha256_solo, dim3(a.n_order), dim3(64), 0, s, a);
+    if (duo)
+        hipLaunchKernelGGL(k1_sha256_duo, dim3(a.n_order), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(k1_sha256_solo, dim3(a.n_order), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

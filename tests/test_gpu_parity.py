@@ -68,10 +68,11 @@ def _device_arena(lens, align=256):
     return np.array(offs, dtype=np.uint64), max(pos, 16)
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2])
+@pytest.mark.parametrize("flags", [0, 1, 2, 6])
 def test_plan_gen_fill_device(ctx, flags):
     """rf_gen_fill + rf_sha_plan_run on HBM-resident data (the bench path),
-    lanes-only / solo-only / planner mix."""
+    planner mix / lanes-only / wave-per-message with the two-lane chain /
+    wave-per-message with the one-lane chain."""
     from reflow_amd import capi
     rng = random.Random(10 + flags)
     lens = [rng.choice([0, 1, 55, 56, 64, 4096, rng.randint(1, 300000), rng.randint(1, 3000)])
@@ -87,7 +88,7 @@ def test_plan_gen_fill_device(ctx, flags):
     plan.run(d_arena.ptr, d_out.ptr)
     ctx.sync()
     st = plan.stats()
-    if flags == capi.RF_SHA_ALL_SOLO:
+    if flags & capi.RF_SHA_ALL_SOLO:
         assert st.n_solo == len(lens)
     if flags == capi.RF_SHA_NO_SOLO:
         assert st.n_solo == 0

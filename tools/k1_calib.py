@@ -57,7 +57,8 @@ def main():
         run_case(ctx, "many 131072x64KiB", [64 * KB] * 131072, capi.RF_SHA_NO_SOLO)
     # single-message chain rates
     run_case(ctx, "1x16MiB lane", [16 * MB], capi.RF_SHA_NO_SOLO, reps=2)
-    run_case(ctx, "1x16MiB solo", [16 * MB], capi.RF_SHA_ALL_SOLO, reps=2)
+    run_case(ctx, "1x16MiB solo(1-lane)", [16 * MB], capi.RF_SHA_ALL_SOLO | capi.RF_SHA_ONE_LANE_CHAIN, reps=2)
+    run_case(ctx, "1x16MiB duo", [16 * MB], capi.RF_SHA_ALL_SOLO, reps=2)
     run_case(ctx, "256x4MiB solo", [4 * MB] * 256, capi.RF_SHA_ALL_SOLO, reps=2)
     run_case(ctx, "1024x4MiB solo", [4 * MB] * 1024, capi.RF_SHA_ALL_SOLO, reps=2)
     run_case(ctx, "1024x4MiB lanes", [4 * MB] * 1024, capi.RF_SHA_NO_SOLO, reps=2)
