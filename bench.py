@@ -41,13 +41,29 @@ N_CU = 256
 VALU_LANE_OPS = N_CU * 4 * 32 * CLOCK_HZ      # int32 VALU lane-ops/s (= FP32 FMA rate)
 SHA_OPS_PER_BLOCK = 1464                        # canonical ops per 64-B block
 SHA_VALU_PEAK_GBS = VALU_LANE_OPS / SHA_OPS_PER_BLOCK * 64 / 1e9
-CHAIN_INSTR_PER_BLOCK = 64 * 14                 # minimal gfx950 round: 14 VALU
+CHAIN_INSTR_PER_BLOCK = 64 * 11                 # two-lane round: 11 VALU issue slots
 WAVE_ISSUE_CYCLES = 4                           # one wave alone: 1 VALU / 4 cycles
 HBM_PEAK_GBS = 8000.0
 
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
+    --pmc FETCH_SIZE/WRITE_SIZE summary (tools/pmc_summary.py, corrected as
+    MI355X_MICROARCH.md prescribes), or None.  The PMC passes run the same
+    default workloads as this script."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not paths:
+        return None, None
+    d = json.load(open(paths[-1]))
+    v = d.get("rf::" + kernel)
+    if not v:
+        return None, None
+    return v["traffic_bytes_per_launch"], os.path.relpath(paths[-1], ROOT)
 
 
 class Dist:
@@ -143,9 +159,12 @@ def bench_sha(args, dist, ctx):
     solo_ids = order[:st.n_solo]
     lane_ids = order[st.n_solo:]
     nblk = (lens.astype(np.int64) + 9 + 63) // 64
-    dom = "k1_sha256_solo" if np.mean(solo_ms or [0]) >= np.mean(lanes_ms or [0]) else "k1_sha256_lanes"
-    ids = solo_ids if dom == "k1_sha256_solo" else lane_ids
-    dom_ms = float(np.mean(solo_ms if dom == "k1_sha256_solo" else lanes_ms))
+    # dominant kernel: the one that holds the largest message (its chain is the
+    # critical path); wave-per-message runs k1_sha256_duo by default
+    wave_mode = st.n_solo > 0
+    dom = "k1_sha256_duo" if wave_mode else "k1_sha256_lanes"
+    ids = solo_ids if wave_mode else lane_ids
+    dom_ms = float(np.mean(solo_ms if wave_mode else lanes_ms))
     dom_bytes = float(lens[ids].sum())
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     # skew-aware floor: the longest serial chain vs chip VALU throughput
@@ -153,9 +172,12 @@ def bench_sha(args, dist, ctx):
     t_valu = float(nblk[ids].sum()) * SHA_OPS_PER_BLOCK / VALU_LANE_OPS
     t_floor = max(t_chain, t_valu)
     peak = dom_bytes / t_floor / 1e9
+    traffic, tsrc = pmc_traffic(dom)
     roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
-            "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": None,
-            "peak_kind": "skew-aware: max(longest message chain at 14 VALU/round x 4 cyc/issue @2.4GHz,"
+            "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+            "traffic_source": tsrc, "traffic_over_algorithmic": (round(traffic / dom_bytes, 3)
+                                                                 if traffic else None),
+            "peak_kind": "skew-aware: max(longest message chain at 11 VALU/round x 4 cyc/issue @2.4GHz,"
                          " sum blocks x 1464 ops / INT32 VALU peak)",
             "valu_peak_GBps": round(SHA_VALU_PEAK_GBS, 1),
             "frac_of_valu_peak": round(achieved / SHA_VALU_PEAK_GBS, 6),
@@ -271,13 +293,16 @@ def bench_probe(args, dist, ctx):
     fp = (hits - rep * n_ins) / max(fresh, 1)
     bpp = 32 + 8 * k + 1
     ach = n_probe * bpp / (dev_ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic("k4_bloom_probe")
     res = {"workload": "bloomlive probe: n=%d keys (m=%d bits, %.1f MiB, k=%d), %d probes (50%% present)"
                        % (n_ins, m, m / 8 / 2**20, k, n_probe),
            "gprobes_per_s": dist.sum(n_probe) * args.probe_steps / t / 1e9,
            "device_ms": dev_ms, "add_ms": add_ms, "false_positive_rate": fp,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_probe": bpp,
-                        "note": "filter fits the 256 MiB Infinity Cache at n=1e8"}}
+                        "traffic": traffic, "traffic_source": tsrc,
+                        "note": "filter fits the 256 MiB Infinity Cache at n=1e8; each random 8-B "
+                                "word read moves a 64-B line (traffic/launch ~ 5.7x algorithmic)"}}
     for x in (keys, out, d_offs, d_lens):
         x.free()
     b.close()

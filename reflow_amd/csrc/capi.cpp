@@ -616,8 +616,8 @@ struct rf_graph {
     std::vector<int64_t> producer;   // slot -> external job or -1
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
-    DevBuf b_job_slot, b_job_off, b_job_nblk, b_hole_ptr, b_hole_pos, b_hole_slot, b_cons_ptr,
-        b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_counts, b_tmp_idx, b_tmp_dig;
+    DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_counts, b_tmp_idx,
+        b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
     uint32_t max_level_jobs = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -705,24 +705,31 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         gr->max_level_jobs = std::max(gr->max_level_jobs, gr->g.lvl_start[l + 1]);
         gr->g.lvl_start[l + 1] += gr->g.lvl_start[l];
     }
-    // host arrays in internal order; padded templates
-    std::vector<uint32_t> job_slot(J), job_nblk(J), hole_ptr(J + 1, 0), hole_pos(H), hole_slot(H);
+    // host arrays in internal order: 32-B job records, {pos, slot} holes,
+    // padded templates (64-B blocks, FIPS padding pre-applied)
+    std::vector<uint32_t> meta(8ull * J, 0), holes(2ull * H);
     std::vector<uint64_t> job_off(J);
-    uint64_t tb = 0;
+    uint64_t tb = 0, hcur = 0;
     for (uint32_t i = 0; i < J; ++i) {
         const uint32_t j = perm[i];
-        job_slot[i] = d->out_slot[j];
-        job_nblk[i] = nblk[j];
+        const uint32_t s = d->out_slot[j];
         job_off[i] = tb;
+        uint32_t* m = &meta[8ull * i];
+        m[0] = (uint32_t)(tb / 64);
+        m[1] = nblk[j];
+        m[2] = (uint32_t)hcur;
+        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h, ++hcur) {
+            holes[2 * hcur] = d->hole_pos[h];
+            holes[2 * hcur + 1] = d->hole_slot[h];
+        }
+        m[3] = (uint32_t)hcur;
+        m[4] = s;
+        m[5] = (uint32_t)cptr[s];
+        m[6] = (uint32_t)cptr[s + 1];
         tb += 64ull * nblk[j];
         gr->total_blocks += nblk[j];
-        const uint64_t hs = d->hole_ptr[j], he = d->hole_ptr[j + 1];
-        hole_ptr[i + 1] = hole_ptr[i] + (uint32_t)(he - hs);
-        for (uint64_t h = hs; h < he; ++h) {
-            hole_pos[hole_ptr[i] + (h - hs)] = d->hole_pos[h];
-            hole_slot[hole_ptr[i] + (h - hs)] = d->hole_slot[h];
-        }
     }
+    if (tb / 64 >= 0xffffffffull) return fail(RF_EINVAL, "templates exceed 256 GiB");
     std::vector<uint8_t> tmpl(std::max<uint64_t>(tb, 64), 0);
     for (uint32_t i = 0; i < J; ++i) {
         const uint32_t j = perm[i];
@@ -731,7 +738,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         if (len) memcpy(t, d->blob + d->tmpl_off[j], len);
         t[len] = 0x80;
         const uint64_t bits = len * 8;
-        uint8_t* e = t + 64ull * job_nblk[i];
+        uint8_t* e = t + 64ull * nblk[j];
         for (int b = 0; b < 8; ++b) e[-1 - b] = (uint8_t)(bits >> (8 * b));
     }
     std::vector<uint32_t> cons_ptr(S + 1), cons_job(H);
@@ -750,35 +757,25 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
     };
     hipError_t e;
-    if ((e = up(gr->b_job_slot, job_slot.data(), 4ull * J)) != hipSuccess ||
-        (e = up(gr->b_job_off, job_off.data(), 8ull * J)) != hipSuccess ||
-        (e = up(gr->b_job_nblk, job_nblk.data(), 4ull * J)) != hipSuccess ||
-        (e = up(gr->b_hole_ptr, hole_ptr.data(), 4ull * (J + 1))) != hipSuccess ||
-        (e = up(gr->b_hole_pos, hole_pos.data(), 4ull * H)) != hipSuccess ||
-        (e = up(gr->b_hole_slot, hole_slot.data(), 4ull * H)) != hipSuccess ||
+    if ((e = up(gr->b_meta, meta.data(), 32ull * J)) != hipSuccess ||
+        (e = up(gr->b_holes, holes.data(), 8ull * H)) != hipSuccess ||
         (e = up(gr->b_cons_ptr, cons_ptr.data(), 4ull * (S + 1))) != hipSuccess ||
         (e = up(gr->b_cons_job, cons_job.data(), 4ull * H)) != hipSuccess ||
         (e = up(gr->b_tmpl, tmpl.data(), tmpl.size())) != hipSuccess ||
         (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
         (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
-        (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_counts.ensure(4ull * (L + 1))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
                     hipGetErrorString(e));
     HIPC(hipMemset(gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
     HIPC(hipMemset(gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
-    G.job_slot = gr->b_job_slot.as<uint32_t>();
-    G.job_off = gr->b_job_off.as<uint64_t>();
-    G.job_nblk = gr->b_job_nblk.as<uint32_t>();
-    G.hole_ptr = gr->b_hole_ptr.as<uint32_t>();
-    G.hole_pos = gr->b_hole_pos.as<uint32_t>();
-    G.hole_slot = gr->b_hole_slot.as<uint32_t>();
+    G.meta = gr->b_meta.as<uint4>();
+    G.holes = gr->b_holes.as<uint2>();
     G.cons_ptr = gr->b_cons_ptr.as<uint32_t>();
     G.cons_job = gr->b_cons_job.as<uint32_t>();
     G.tmpl = gr->b_tmpl.as<uint8_t>();
     G.slots = gr->b_slots.as<uint8_t>();
     G.dirty = gr->b_dirty.as<uint32_t>();
-    G.list = gr->b_list.as<uint32_t>();
     G.counts = gr->b_counts.as<uint32_t>();
     HIPC(hipEventCreate(&gr->e0));
     HIPC(hipEventCreate(&gr->e1));
@@ -791,10 +788,8 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
     if (!gr) return;
     if (gr->ctx) {
         DevGuard dg(gr->ctx->device);
-        for (DevBuf* b : {&gr->b_job_slot, &gr->b_job_off, &gr->b_job_nblk, &gr->b_hole_ptr,
-                          &gr->b_hole_pos, &gr->b_hole_slot, &gr->b_cons_ptr, &gr->b_cons_job,
-                          &gr->b_tmpl, &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_counts,
-                          &gr->b_tmp_idx, &gr->b_tmp_dig})
+        for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
+                          &gr->b_slots, &gr->b_dirty, &gr->b_counts, &gr->b_tmp_idx, &gr->b_tmp_dig})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);

@@ -46,19 +46,17 @@ hipError_t launch_gen_fill(uint8_t* arena, const uint64_t* offs, const uint64_t*
 struct GraphDev {
     uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;
     // jobs in internal (level) order
-    uint32_t* job_slot = nullptr;    // [J] output slot
-    uint64_t* job_off = nullptr;     // [J] offset of the padded template in tmpl
-    uint32_t* job_nblk = nullptr;    // [J] SHA blocks of the padded template
-    uint32_t* hole_ptr = nullptr;    // [J+1]
-    uint32_t* hole_pos = nullptr;    // [H]
-    uint32_t* hole_slot = nullptr;   // [H]
+    // job record, 32 B, one pair of 16-B loads per job:
+    //   meta[2j]   = {template offset / 64, blocks, hole_begin, hole_end}
+    //   meta[2j+1] = {out slot, consumer_begin, consumer_end, 0}
+    uint4* meta = nullptr;           // [2J]
+    uint2* holes = nullptr;          // [H] {byte position, slot}
     uint32_t* cons_ptr = nullptr;    // [S+1] slot -> consumer jobs (internal ids)
     uint32_t* cons_job = nullptr;    // [C]
     uint8_t* tmpl = nullptr;         // padded templates
     uint8_t* slots = nullptr;        // [S][32] digest table
     uint32_t* dirty = nullptr;       // [(J+31)/32] dirty bitset over internal ids
-    uint32_t* list = nullptr;        // [J] compacted dirty jobs of the current level
-    uint32_t* counts = nullptr;      // [L] dirty jobs per level (and [L] = total)
+    uint32_t* counts = nullptr;      // [L] jobs hashed per level
     std::vector<uint32_t> lvl_start; // host copy [L+1]
 };
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,

@@ -6,22 +6,29 @@
 // (eval.go:240-272 -> Canonicalize flow.go:814-843); here only the transitive
 // dependents of changed inputs are rehashed.
 //
-// Data layout in HBM (DESIGN.md "Digest DAG"):
+// Data layout in HBM (DESIGN.md "Data layout"):
 //   tmpl      per job, its digest material with SHA padding already applied
 //             (64-B aligned, nblk*64 bytes); WD holes carry the 0x00 0x05
 //             prefix and 32 bytes that are rewritten from the slot table.
+//   meta      32-B job record (template offset, blocks, hole range, out slot,
+//             consumer range): two 16-B loads per job.
+//   holes     {byte position, slot} pairs.
 //   slots     [S][32] digest table (node digests, physical keys, File IDs).
-//   dirty     bitset over jobs in level order; list/counts per level.
+//   dirty     bitset over jobs in level order.
 //   cons      slot -> consumer jobs (reverse edges for the frontier).
-// Per level: k3_compact turns the level's dirty bits into a dense job list
-// (wave ballot/popcount prefix + one atomic per wave); k2_hash gives each
-// listed job one lane: patch its holes from the slot table, hash its blocks,
-// write the slot, and -- only if the digest changed -- set its consumers'
-// dirty bits (early cut-off).
+// One launch per level (k2_level): each workgroup owns 256 x 32 consecutive
+// jobs of the level, compacts its dirty bits into an LDS list (K3: wave
+// popcount prefix + a 4-wave block scan, no global list, no atomics), then its
+// lanes hash the listed jobs one lane per job: patch holes from the slot
+// table, hash the padded template, write the slot and -- only if the digest
+// changed -- atomicOr the consumers' dirty bits (early cut-off).
 #include "engine.h"
 #include "sha256_dev.h"
 
 namespace rf {
+
+constexpr uint32_t kLevelBlock = 256;
+constexpr uint32_t kJobsPerBlock = kLevelBlock * 32;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     const uint32_t lane = threadIdx.x & 63;
@@ -31,37 +38,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
         if (lane >= (uint32_t)d) v += t;
     }
     return v;
-}
-
-// K3: compact dirty jobs of internal range [s, e) into list; counts[lvl] += n.
-__global__ __launch_bounds__(256) void k3_compact(const uint32_t* __restrict__ dirty, uint32_t s,
-                                                  uint32_t e, uint32_t* __restrict__ list,
-                                                  uint32_t* __restrict__ counts, uint32_t lvl) {
-    const uint32_t w_lo = s >> 5, w_hi = (e + 31) >> 5;  // words [w_lo, w_hi)
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < (w_hi - w_lo);
-         base += gridDim.x * blockDim.x) {
-        const uint32_t wi = w_lo + base + threadIdx.x;
-        uint32_t bits = 0;
-        if (wi < w_hi) {
-            bits = dirty[wi];
-            const uint32_t first = wi << 5;
-            if (first < s) bits &= ~0u << (s - first);
-            if (first + 32 > e) bits &= (e - first >= 32) ? ~0u : ((1u << (e - first)) - 1u);
-        }
-        const uint32_t c = __popc(bits);
-        const uint32_t incl = wave_incl_scan(c);
-        const uint32_t total = __shfl(incl, 63, 64);
-        uint32_t wbase = 0;
-        if (lane == 63 && total) wbase = atomicAdd(&counts[lvl], total);
-        wbase = __shfl(wbase, 63, 64);
-        uint32_t pos = wbase + incl - c;
-        while (bits) {
-            const uint32_t b = __ffs(bits) - 1;
-            bits &= bits - 1;
-            list[pos++] = (wi << 5) + b;
-        }
-    }
 }
 
 // Write the 32 digest bytes D (as 8 little-endian words) at byte `pos` of a
@@ -80,73 +56,100 @@ __device__ __forceinline__ void patch_digest(uint32_t* wb, uint32_t pos, const u
     }
 }
 
-struct HashArgs {
-    const uint32_t* list;
-    const uint32_t* counts;
-    uint32_t lvl;
+struct LevelArgs {
+    uint32_t s, e, lvl;  // internal job range of the level
     int full;
-    const uint32_t* job_slot;
-    const uint64_t* job_off;
-    const uint32_t* job_nblk;
-    const uint32_t* hole_ptr;
-    const uint32_t* hole_pos;
-    const uint32_t* hole_slot;
-    const uint32_t* cons_ptr;
+    const uint4* meta;
+    const uint2* holes;
     const uint32_t* cons_job;
     uint8_t* tmpl;
     uint8_t* slots;
     uint32_t* dirty;
+    uint32_t* counts;
 };
 
-__global__ __launch_bounds__(256) void k2_hash(HashArgs a) {
-    const uint32_t n = a.counts[a.lvl];
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t p = a.list[i];
-        uint8_t* t = a.tmpl + a.job_off[p];
-        uint32_t* tw = reinterpret_cast<uint32_t*>(t);
-        // 1. patch holes from the slot table
-        for (uint32_t h = a.hole_ptr[p]; h < a.hole_ptr[p + 1]; ++h) {
-            const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * a.hole_slot[h]);
-            const uint4 lo = src[0], hi = src[1];
-            const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-            patch_digest(tw, a.hole_pos[h], D);
-        }
-        // 2. hash the padded template (full blocks only)
-        ShaState st;
-        st.init();
-        const uint32_t nb = a.job_nblk[p];
-        const uint4* q = reinterpret_cast<const uint4*>(t);
-        for (uint32_t b = 0; b < nb; ++b) {
-            const uint4 r0 = q[4 * b], r1 = q[4 * b + 1], r2 = q[4 * b + 2], r3 = q[4 * b + 3];
-            uint32_t w[16] = {bswap32(r0.x), bswap32(r0.y), bswap32(r0.z), bswap32(r0.w),
-                              bswap32(r1.x), bswap32(r1.y), bswap32(r1.z), bswap32(r1.w),
-                              bswap32(r2.x), bswap32(r2.y), bswap32(r2.z), bswap32(r2.w),
-                              bswap32(r3.x), bswap32(r3.y), bswap32(r3.z), bswap32(r3.w)};
-            sha256_compress(st, w);
-        }
-        uint4 nlo, nhi;
-        nlo.x = bswap32(st.h[0]); nlo.y = bswap32(st.h[1]); nlo.z = bswap32(st.h[2]); nlo.w = bswap32(st.h[3]);
-        nhi.x = bswap32(st.h[4]); nhi.y = bswap32(st.h[5]); nhi.z = bswap32(st.h[6]); nhi.w = bswap32(st.h[7]);
-        // 3. store; propagate only on change (early cut-off)
-        const uint32_t slot = a.job_slot[p];
-        uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * slot);
-        bool changed = true;
+__device__ __forceinline__ void hash_job(const LevelArgs& a, uint32_t p) {
+    const uint4 m0 = a.meta[2 * p], m1 = a.meta[2 * p + 1];
+    uint8_t* t = a.tmpl + 64ull * m0.x;
+    uint32_t* tw = reinterpret_cast<uint32_t*>(t);
+    // 1. patch holes from the slot table
+    for (uint32_t h = m0.z; h < m0.w; ++h) {
+        const uint2 hp = a.holes[h];
+        const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * hp.y);
+        const uint4 lo = src[0], hi = src[1];
+        const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        patch_digest(tw, hp.x, D);
+    }
+    // 2. hash the padded template (full blocks only)
+    ShaState st;
+    st.init();
+    const uint4* q = reinterpret_cast<const uint4*>(t);
+    for (uint32_t b = 0; b < m0.y; ++b) {
+        const uint4 r0 = q[4 * b], r1 = q[4 * b + 1], r2 = q[4 * b + 2], r3 = q[4 * b + 3];
+        uint32_t w[16] = {bswap32(r0.x), bswap32(r0.y), bswap32(r0.z), bswap32(r0.w),
+                          bswap32(r1.x), bswap32(r1.y), bswap32(r1.z), bswap32(r1.w),
+                          bswap32(r2.x), bswap32(r2.y), bswap32(r2.z), bswap32(r2.w),
+                          bswap32(r3.x), bswap32(r3.y), bswap32(r3.z), bswap32(r3.w)};
+        sha256_compress(st, w);
+    }
+    uint4 nlo, nhi;
+    nlo.x = bswap32(st.h[0]); nlo.y = bswap32(st.h[1]); nlo.z = bswap32(st.h[2]); nlo.w = bswap32(st.h[3]);
+    nhi.x = bswap32(st.h[4]); nhi.y = bswap32(st.h[5]); nhi.z = bswap32(st.h[6]); nhi.w = bswap32(st.h[7]);
+    // 3. store; propagate only on change (early cut-off)
+    uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * m1.x);
+    bool changed = true;
+    if (!a.full) {
+        const uint4 olo = dst[0], ohi = dst[1];
+        changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                  (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
+    }
+    if (changed) {
+        dst[0] = nlo;
+        dst[1] = nhi;
         if (!a.full) {
-            const uint4 olo = dst[0], ohi = dst[1];
-            changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
-                      (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
-        }
-        if (changed) {
-            dst[0] = nlo;
-            dst[1] = nhi;
-            if (!a.full) {
-                for (uint32_t c = a.cons_ptr[slot]; c < a.cons_ptr[slot + 1]; ++c) {
-                    const uint32_t j = a.cons_job[c];
-                    atomicOr(&a.dirty[j >> 5], 1u << (j & 31));
-                }
+            for (uint32_t c = m1.y; c < m1.z; ++c) {
+                const uint32_t j = a.cons_job[c];
+                atomicOr(&a.dirty[j >> 5], 1u << (j & 31));
             }
         }
     }
+}
+
+__global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
+    __shared__ uint32_t lst[kJobsPerBlock];
+    __shared__ uint32_t wsum[kLevelBlock / 64];
+    const uint32_t w_lo = a.s >> 5, w_hi = (a.e + 31) >> 5;
+    const uint32_t wi = w_lo + blockIdx.x * kLevelBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // K3: this block's slice of the dirty bitset -> LDS job list
+    uint32_t bits = 0;
+    if (wi < w_hi) {
+        bits = a.dirty[wi];
+        const uint32_t first = wi << 5;
+        if (first < a.s) bits &= ~0u << (a.s - first);
+        if (first + 32 > a.e) bits &= (a.e - first >= 32) ? ~0u : ((1u << (a.e - first)) - 1u);
+    }
+    const uint32_t c = __popc(bits);
+    const uint32_t incl = wave_incl_scan(c);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kLevelBlock / 64; ++k) {
+        const uint32_t v = wsum[k];
+        wbase += k < wave ? v : 0;
+        total += v;
+    }
+    uint32_t pos = wbase + incl - c;
+    while (bits) {
+        const uint32_t b = __ffs(bits) - 1;
+        bits &= bits - 1;
+        lst[pos++] = (wi << 5) + b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && total) atomicAdd(&a.counts[a.lvl], total);
+    // K2: one lane per listed job
+    for (uint32_t i = threadIdx.x; i < total; i += kLevelBlock) hash_job(a, lst[i]);
 }
 
 // set_slots: write input digests, dirty their consumers when they changed.
@@ -214,12 +217,9 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
     const uint32_t words = ((e + 31) >> 5) - (b >> 5);
-    hipLaunchKernelGGL(k3_compact, dim3(grid_for(words, 2048)), dim3(256), 0, s, g.dirty, b, e,
-                       g.list, g.counts, lvl);
-    HashArgs a{g.list,     g.counts,   lvl,         full,        g.job_slot, g.job_off,
-               g.job_nblk, g.hole_ptr, g.hole_pos,  g.hole_slot, g.cons_ptr, g.cons_job,
-               g.tmpl,     g.slots,    g.dirty};
-    hipLaunchKernelGGL(k2_hash, dim3(grid_for(e - b, 8192)), dim3(256), 0, s, a);
+    const uint32_t grid = (words + kLevelBlock - 1) / kLevelBlock;
+    LevelArgs a{b, e, lvl, full, g.meta, g.holes, g.cons_job, g.tmpl, g.slots, g.dirty, g.counts};
+    hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
     return hipGetLastError();
 }
 

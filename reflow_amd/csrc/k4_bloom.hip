@@ -98,24 +98,28 @@ __global__ __launch_bounds__(256) void k4_bloom_probe(const uint64_t* __restrict
         base_hashes_wd(D, h);
         bool hit = true;
         if (k <= kKMax) {
-            uint64_t w[kKMax];
-            uint32_t bit[kKMax];
+            // all locations first (pure VALU), then two fetch phases: the first
+            // kPhase1 words decide most absent keys (a filter at its design
+            // load has ~half its bits set), the rest are fetched together only
+            // for the keys still alive.  Same answer as the sequential Test.
+            uint64_t loc[kKMax];
 #pragma unroll
             for (uint32_t j = 0; j < kKMax; ++j) {
-                w[j] = ~0ull;
-                bit[j] = 0;
-                if (j < k) {
-                    const uint64_t loc = mod_m(bloom_loc(h, j), m, mu);
-                    if (loc >= length) {
-                        hit = false;
-                    } else {
-                        w[j] = words[loc >> 6];
-                        bit[j] = (uint32_t)(loc & 63);
-                    }
-                }
+                loc[j] = j < k ? mod_m(bloom_loc(h, j), m, mu) : 0;
+                if (j < k && loc[j] >= length) hit = false;
             }
+            constexpr uint32_t kPhase1 = 2;
+            uint64_t w[kKMax];
 #pragma unroll
-            for (uint32_t j = 0; j < kKMax; ++j) hit = hit && ((w[j] >> bit[j]) & 1ull);
+            for (uint32_t j = 0; j < kPhase1; ++j) w[j] = (hit && j < k) ? words[loc[j] >> 6] : ~0ull;
+#pragma unroll
+            for (uint32_t j = 0; j < kPhase1; ++j) hit = hit && ((w[j] >> (loc[j] & 63)) & 1ull);
+            if (hit && k > kPhase1) {
+#pragma unroll
+                for (uint32_t j = kPhase1; j < kKMax; ++j) w[j] = j < k ? words[loc[j] >> 6] : ~0ull;
+#pragma unroll
+                for (uint32_t j = kPhase1; j < kKMax; ++j) hit = hit && ((w[j] >> (loc[j] & 63)) & 1ull);
+            }
         } else {
             for (uint32_t j = 0; j < k && hit; ++j) {
                 const uint64_t loc = mod_m(bloom_loc(h, j), m, mu);

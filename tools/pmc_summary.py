@@ -1,0 +1,50 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
+
+    python tools/pmc_summary.py FETCH_DIR/x_counter_collection.csv WRITE_DIR/x_counter_collection.csv OUT.json
+
+FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB.  Per
+MI355X_MICROARCH.md (HBM / rocprofv3): on gfx950 FETCH_SIZE reads exactly
+half of the bytes of a wide coalesced streaming read (128-B requests tallied
+at 64 B), so `fetch_bytes_corrected` = 2 x FETCH_SIZE x 1024 for kernels whose
+reads are wide coalesced streams (K1: 64 B per lane, 4 KiB per wave); for
+random 8-B gathers (K4) the raw figure is reported (uncalibrated access width:
+the guide gives no correction), and Infinity-Cache hits are counted too."""
+import collections
+import csv
+import json
+import sys
+
+WIDE_STREAM = {"rf::k1_sha256_duo", "rf::k1_sha256_solo", "rf::k1_sha256_lanes"}
+
+
+def load(path):
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0]
+        agg[k][0] += 1
+        agg[k][1] += float(r["Counter_Value"])
+    return agg
+
+
+def main():
+    f, w, out = sys.argv[1:4]
+    F, W = load(f), load(w)
+    res = {}
+    for k in sorted(set(F) | set(W)):
+        nf, vf = F.get(k, [0, 0.0])
+        nw, vw = W.get(k, [0, 0.0])
+        fb = vf / max(nf, 1) * 1024
+        wb = vw / max(nw, 1) * 1024
+        corr = 2.0 if k in WIDE_STREAM else 1.0
+        res[k] = {"calls": nf, "fetch_bytes_raw": fb, "fetch_bytes_corrected": fb * corr,
+                  "fetch_correction": corr, "write_bytes": wb,
+                  "traffic_bytes_per_launch": fb * corr + wb}
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in res.items():
+        print("%-36s traffic/launch %.4e B (fetch raw %.4e x%.0f, write %.4e)"
+              % (k, v["traffic_bytes_per_launch"], v["fetch_bytes_raw"], v["fetch_correction"],
+                 v["write_bytes"]))
+
+
+if __name__ == "__main__":
+    main()
