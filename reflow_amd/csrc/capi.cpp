@@ -616,8 +616,8 @@ struct rf_graph {
     std::vector<int64_t> producer;   // slot -> external job or -1
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
-    DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_counts, b_tmp_idx,
-        b_tmp_dig;
+    DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_counts,
+        b_tmp_idx, b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
     uint32_t max_level_jobs = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -764,6 +764,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         (e = up(gr->b_tmpl, tmpl.data(), tmpl.size())) != hipSuccess ||
         (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
         (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
+        (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_counts.ensure(4ull * (L + 1))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
                     hipGetErrorString(e));
@@ -776,6 +777,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     G.tmpl = gr->b_tmpl.as<uint8_t>();
     G.slots = gr->b_slots.as<uint8_t>();
     G.dirty = gr->b_dirty.as<uint32_t>();
+    G.list = gr->b_list.as<uint32_t>();
     G.counts = gr->b_counts.as<uint32_t>();
     HIPC(hipEventCreate(&gr->e0));
     HIPC(hipEventCreate(&gr->e1));
@@ -789,7 +791,8 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
     if (gr->ctx) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
-                          &gr->b_slots, &gr->b_dirty, &gr->b_counts, &gr->b_tmp_idx, &gr->b_tmp_dig})
+                          &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_counts, &gr->b_tmp_idx,
+                          &gr->b_tmp_dig})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);

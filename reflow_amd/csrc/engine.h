@@ -56,6 +56,7 @@ struct GraphDev {
     uint8_t* tmpl = nullptr;         // padded templates
     uint8_t* slots = nullptr;        // [S][32] digest table
     uint32_t* dirty = nullptr;       // [(J+31)/32] dirty bitset over internal ids
+    uint32_t* list = nullptr;        // [J] compacted dirty jobs of the current level
     uint32_t* counts = nullptr;      // [L] jobs hashed per level
     std::vector<uint32_t> lvl_start; // host copy [L+1]
 };

@@ -327,3 +327,24 @@ def test_bloom_edge_filters(ctx):
     b2 = capi.Bloom.load(ctx, m, k, words, 256)
     want = _oracle_probe(words, 256, m, k, keys.tobytes(), 50)
     assert (b2.probe(keys) == want).all()
+
+
+# --------------------------------------------------------------- RCCL --
+def test_rccl_single_rank_allgather_and_or(ctx):
+    """rf_comm_* over RCCL with one rank (the 1-GPU box): all-gather copies the
+    boundary digests, the OR all-reduce (all-gather + OR kernel) is identity."""
+    from reflow_amd import capi
+    uid = capi.Comm.unique_id()
+    comm = capi.Comm(ctx, 1, 0, uid)
+    rng = np.random.default_rng(2)
+    words = rng.integers(0, 2**63, size=1000, dtype=np.uint64)
+    d = ctx.upload(words)
+    comm.allreduce_or(d.ptr, len(words), ctx.stream)
+    ctx.sync()
+    assert (d.to_numpy(np.uint64) == words).all()
+    src = ctx.upload(rng.integers(0, 256, size=32 * 77, dtype=np.uint8))
+    dst = ctx.alloc(32 * 77)
+    comm.allgather(src.ptr, dst.ptr, 32 * 77, ctx.stream)
+    ctx.sync()
+    assert (dst.to_numpy() == src.to_numpy()).all()
+    comm.close()
