@@ -1,0 +1,243 @@
+// reflow_host.hpp -- C++ host-side mirror of Reflow's memoization API over the
+// C-ABI in reflow_hip.h.
+//
+// The reference is Go (no Go toolchain in this image), so the host side above
+// the ABI is C++ with the reference's names and meaning:
+//   Digest / WriteDigest      grailbio/base/digest (00 05 || sha256)
+//   Digester                  reflow.Digester (flow.go:36), batched on the GPU
+//   File / Fileset            executor.go:25-38, WriteDigest :214-233
+//   Op / Config / Flow        flow.go:40-301, Op.DigestString op_string.go:15-21
+//   flow::Exec/Intern/...     test/flow/constructor.go:17-74
+//   Eval                      Flow.Digest / PhysicalDigest / CacheKeys /
+//                             Canonicalize (flow.go:653-843), lowered to
+//                             rf_graph jobs and computed by the HIP kernels
+//   Liveset                   bloomlive.T (internal/bloomlive/bloomlive.go)
+// Every digest is computed by libreflow_hip.so on the device.
+#pragma once
+
+#include <array>
+#include <cstring>
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "reflow_hip.h"
+
+namespace reflow {
+
+struct Error : std::exception {
+    int code;
+    std::string msg;
+    Error(int c, std::string m) : code(c), msg(std::move(m)) {}
+    const char* what() const noexcept override { return msg.c_str(); }
+};
+
+// ---- digest ----------------------------------------------------------------
+struct Digest {
+    std::array<uint8_t, 32> b{};
+    bool IsZero() const;
+    std::string Hex() const;
+    std::string String() const;  // "sha256:<64 hex>"
+    std::string Short() const;   // "sha256:<8 hex>"
+    bool Less(const Digest& o) const { return b < o.b; }
+    bool operator==(const Digest& o) const { return b == o.b; }
+    bool operator!=(const Digest& o) const { return b != o.b; }
+    static bool Parse(const std::string& s, Digest* out);
+};
+struct DigestHash {
+    size_t operator()(const Digest& d) const {
+        size_t h;
+        memcpy(&h, d.b.data(), sizeof h);
+        return h;
+    }
+};
+// digest.WriteDigest: big-endian uint16(crypto.SHA256 = 5) then the 32 bytes.
+void WriteDigest(std::string& w, const Digest& d);
+
+// ---- engine (one rf_ctx per GPU) -------------------------------------------
+class Engine {
+   public:
+    explicit Engine(int device = 0);
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+    rf_ctx* ctx() const { return ctx_; }
+
+   private:
+    rf_ctx* ctx_ = nullptr;
+};
+
+void Check(int rc);  // throws Error with rf_last_error()
+
+// reflow.Digester: FromBytes/FromString, batched.
+class Digester {
+   public:
+    explicit Digester(Engine& e) : e_(e) {}
+    Digest FromBytes(const std::string& b) { return FromBytesBatch({b})[0]; }
+    Digest FromString(const std::string& s) { return FromBytes(s); }
+    std::vector<Digest> FromBytesBatch(const std::vector<std::string>& msgs);
+
+   private:
+    Engine& e_;
+};
+
+// ---- values ------------------------------------------------------------------
+struct File {
+    Digest ID;
+    int64_t Size = 0;
+};
+
+struct Fileset {
+    std::optional<std::vector<Fileset>> List;  // non-nil List wins (executor.go:216-219)
+    std::map<std::string, File> Map;           // std::map = sort.Strings order
+    void WriteDigest(std::string& w) const;
+    size_t N() const;
+    bool Empty() const;
+};
+
+// Fileset.Digest for many filesets in one device call.
+std::vector<Digest> FilesetDigests(Engine& e, const std::vector<const Fileset*>& v);
+
+// ---- flows -------------------------------------------------------------------
+enum Op : int {
+    OpExec = 1, OpIntern, OpExtern, OpGroupby, OpMap, OpCollect, OpMerge, OpVal, OpPullup, OpK,
+    OpCoerce, OpRequirements, OpData
+};
+// op_string.go:15-21 (the generated table is one entry stale: OpData -> "maxOp")
+std::string DigestString(Op op);
+
+struct ExecArg {
+    bool Out = false;
+    int Index = 0;
+};
+
+struct Config {
+    bool HashV1 = false;
+    void Merge(const Config& d) { HashV1 = HashV1 || d.HashV1; }
+};
+
+struct Flow {
+    Op op = OpVal;
+    Flow* Parent = nullptr;
+    std::vector<Flow*> Deps;
+    Config config;
+    std::string Image, Cmd;           // OpExec
+    std::string URL;                  // OpIntern/OpExtern: url.URL.String() bytes
+    std::string Re, Repl;             // OpGroupby/OpCollect: regexp.String(), Repl
+    Flow* MapFlow = nullptr;          // OpMap (MapInit already applied)
+    std::optional<std::vector<ExecArg>> Argmap;
+    Digest FlowDigest;                // OpVal (non-Fileset), OpK, OpCoerce
+    bool Done = false;                // State == FlowDone
+    std::optional<Fileset> Value;     // Fileset value
+    bool Err = false;                 // error values digest randomly (not supported here)
+    std::string Data;                 // OpData
+};
+
+// Owns Flow nodes (the Go GC's job in the reference).
+class FlowArena {
+   public:
+    Flow* New(Flow f) {
+        nodes_.push_back(std::move(f));
+        return &nodes_.back();
+    }
+
+   private:
+    std::deque<Flow> nodes_;
+};
+
+// test/flow/constructor.go:17-74
+namespace flow {
+Flow* Exec(FlowArena& a, const std::string& image, const std::string& cmd, std::vector<Flow*> deps);
+Flow* Intern(FlowArena& a, const std::string& url);
+Flow* Extern(FlowArena& a, const std::string& url, Flow* dep);
+Flow* Groupby(FlowArena& a, const std::string& re, Flow* dep);
+Flow* Collect(FlowArena& a, const std::string& re, const std::string& repl, Flow* dep);
+// MapFunc is applied to &Flow{Op: OpVal, Value: Fileset{}} (MapInit, flow.go:315-317)
+template <class F>
+Flow* Map(FlowArena& a, F fn, Flow* dep) {
+    Flow* v = a.New(Flow{});
+    v->op = OpVal;
+    v->Value = Fileset{};
+    Flow f;
+    f.op = OpMap;
+    f.Deps = {dep};
+    f.MapFlow = fn(v);
+    return a.New(std::move(f));
+}
+Flow* Merge(FlowArena& a, std::vector<Flow*> deps);
+Flow* Pullup(FlowArena& a, std::vector<Flow*> deps);
+Flow* Val(FlowArena& a, const Fileset& v);
+Flow* Data(FlowArena& a, const std::string& b);
+}  // namespace flow
+
+// Canonicalize (flow.go:814-843): copies merged with `config`, semantically
+// equal nodes (equal digests) collapsed to the first one in visit order.
+// Digests come from the device (two graph evaluations).
+Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config,
+                   const std::string& universe = "");
+
+// Batched Flow.Digest / PhysicalDigest / CacheKeys over a whole DAG: the DAG
+// is lowered to rf_graph jobs (one logical job per node, one physical job per
+// OpExec/OpExtern whose deps are Done) and evaluated on the device.  With
+// file_slots, every File.ID inside Fileset values becomes an input slot, so
+// SetFileID + Recompute re-derive only the dependents (incremental).
+class Eval {
+   public:
+    Eval(Engine& e, std::string universe = "", bool file_slots = false);
+    ~Eval();
+    void Add(Flow* root);
+    void Build();  // rf_graph_load + full recompute
+    Digest FlowDigest(const Flow* f) const;
+    std::optional<Digest> PhysicalDigest(const Flow* f) const;
+    std::vector<Digest> CacheKeys(const Flow* f) const;
+    // Change one File ID wherever Fileset values reference it (needs file_slots).
+    void SetFileID(const Digest& old_id, const Digest& new_id);
+    uint64_t Recompute(bool full = false);
+    size_t Jobs() const { return jobs_.size(); }
+
+   private:
+    struct Job {
+        std::string tmpl;
+        std::vector<std::pair<uint32_t, uint32_t>> holes;  // (byte pos, slot)
+        uint32_t out;
+    };
+    void material(const Flow* f, bool v1, std::string& out, std::vector<std::pair<uint32_t, uint32_t>>& holes);
+    void fileset_material(const Fileset& v, std::string& out,
+                          std::vector<std::pair<uint32_t, uint32_t>>& holes);
+    uint32_t lower(const Flow* f);
+    void lower_physical(const Flow* f);
+    uint32_t new_slot() { return n_slots_++; }
+
+    Engine& e_;
+    std::string U_;
+    bool file_slots_;
+    uint32_t n_slots_ = 0;
+    std::vector<Job> jobs_;
+    std::unordered_map<const Flow*, uint32_t> logical_, physical_, job_of_;
+    std::unordered_map<Digest, uint32_t, DigestHash> file_slot_;
+    rf_graph* g_ = nullptr;
+    mutable std::vector<uint8_t> cache_;  // all slots after the last recompute
+    mutable bool cache_ok_ = false;
+    void fetch() const;
+};
+
+// bloomlive.T over the device filter: Contains batched.
+class Liveset {
+   public:
+    Liveset(Engine& e, uint64_t m, uint64_t k);          // bloom.New
+    static Liveset FromJSON(Engine& e, const std::string& js);
+    Liveset(Liveset&& o) noexcept : b_(o.b_) { o.b_ = nullptr; }
+    ~Liveset();
+    void Add(const std::vector<Digest>& ds);
+    std::vector<bool> Contains(const std::vector<Digest>& ds);
+
+   private:
+    explicit Liveset(rf_bloom* b) : b_(b) {}
+    rf_bloom* b_ = nullptr;
+};
+
+}  // namespace reflow

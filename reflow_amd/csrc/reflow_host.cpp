@@ -1,0 +1,501 @@
+// reflow_host.cpp -- C++ host-side mirror of Reflow's memoization API
+// (include/reflow_host.hpp) over the C-ABI.  Lowering follows the byte grammar
+// of flow.go:675-792 / executor.go:214-233; every SHA-256 is
+// computed by the device through rf_graph_* / rf_sha256_batch /
+// rf_fileset_digest_batch.
+#include "reflow_host.hpp"
+
+#include <algorithm>
+#include <functional>
+#include <unordered_set>
+
+namespace reflow {
+
+void Check(int rc) {
+    if (rc != RF_OK) throw Error(rc, rf_last_error());
+}
+
+// ---- Digest -----------------------------------------------------------------
+bool Digest::IsZero() const {
+    for (uint8_t x : b)
+        if (x) return false;
+    return true;
+}
+
+std::string Digest::Hex() const {
+    static const char* hx = "0123456789abcdef";
+    std::string s(64, '0');
+    for (int i = 0; i < 32; ++i) {
+        s[2 * i] = hx[b[i] >> 4];
+        s[2 * i + 1] = hx[b[i] & 15];
+    }
+    return s;
+}
+
+std::string Digest::String() const { return "sha256:" + Hex(); }
+std::string Digest::Short() const { return "sha256:" + Hex().substr(0, 8); }
+
+bool Digest::Parse(const std::string& s, Digest* out) {
+    if (s.size() != 7 + 64 || s.compare(0, 7, "sha256:") != 0) return false;
+    auto nib = [](char c) -> int {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        return -1;
+    };
+    for (int i = 0; i < 32; ++i) {
+        const int hi = nib(s[7 + 2 * i]), lo = nib(s[8 + 2 * i]);
+        if (hi < 0 || lo < 0) return false;
+        out->b[i] = (uint8_t)(hi << 4 | lo);
+    }
+    return true;
+}
+
+void WriteDigest(std::string& w, const Digest& d) {
+    w.push_back('\0');
+    w.push_back('\5');
+    w.append(reinterpret_cast<const char*>(d.b.data()), 32);
+}
+
+// ---- Engine / Digester -----------------------------------------------------
+Engine::Engine(int device) { Check(rf_init(device, &ctx_)); }
+Engine::~Engine() { rf_destroy(ctx_); }
+
+std::vector<Digest> Digester::FromBytesBatch(const std::vector<std::string>& msgs) {
+    std::vector<const uint8_t*> p(msgs.size());
+    std::vector<uint64_t> n(msgs.size());
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        p[i] = reinterpret_cast<const uint8_t*>(msgs[i].data());
+        n[i] = msgs[i].size();
+    }
+    std::vector<Digest> out(msgs.size());
+    if (!msgs.empty())
+        Check(rf_sha256_batch(e_.ctx(), p.data(), n.data(), msgs.size(), out[0].b.data()));
+    return out;
+}
+
+// ---- Fileset ------------------------------------------------------------------
+void Fileset::WriteDigest(std::string& w) const {
+    if (List) {
+        for (const Fileset& v : *List) v.WriteDigest(w);
+        return;
+    }
+    for (const auto& [path, file] : Map) {  // std::map: bytewise order == sort.Strings
+        w += path;
+        reflow::WriteDigest(w, file.ID);
+    }
+}
+
+size_t Fileset::N() const {
+    size_t n = Map.size();
+    if (List)
+        for (const Fileset& v : *List) n += v.N();
+    return n;
+}
+
+bool Fileset::Empty() const {
+    if (List)
+        for (const Fileset& v : *List)
+            if (!v.Empty()) return false;
+    return Map.empty();
+}
+
+std::vector<Digest> FilesetDigests(Engine& e, const std::vector<const Fileset*>& v) {
+    std::vector<uint64_t> set_group{0}, group_entry{0};
+    std::vector<const char*> paths;
+    std::vector<uint32_t> plen;
+    std::vector<uint8_t> ids;
+    std::function<void(const Fileset&)> groups = [&](const Fileset& f) {
+        if (f.List) {
+            for (const Fileset& c : *f.List) groups(c);
+            return;
+        }
+        for (const auto& [path, file] : f.Map) {
+            paths.push_back(path.data());
+            plen.push_back((uint32_t)path.size());
+            ids.insert(ids.end(), file.ID.b.begin(), file.ID.b.end());
+        }
+        group_entry.push_back(paths.size());
+    };
+    for (const Fileset* f : v) {
+        groups(*f);
+        set_group.push_back(group_entry.size() - 1);
+    }
+    std::vector<Digest> out(v.size());
+    if (!v.empty())
+        Check(rf_fileset_digest_batch(e.ctx(), v.size(), set_group.data(), group_entry.data(),
+                                      paths.data(), plen.data(), ids.data(), out[0].b.data()));
+    return out;
+}
+
+// ---- flows ----------------------------------------------------------------------
+std::string DigestString(Op op) {
+    static const char* names[] = {"OpExec", "OpIntern", "OpExtern", "OpGroupby", "OpMap",
+                                  "OpCollect", "OpMerge", "OpVal", "OpPullup", "OpK",
+                                  "OpCoerce", "OpRequirements", "maxOp"};
+    const int i = (int)op - 1;
+    if (i < 0 || i >= 13) return "Op(" + std::to_string((int)op) + ")";
+    return names[i];
+}
+
+namespace flow {
+Flow* Exec(FlowArena& a, const std::string& image, const std::string& cmd, std::vector<Flow*> deps) {
+    Flow f;
+    f.op = OpExec;
+    f.Deps = std::move(deps);
+    f.Image = image;
+    f.Cmd = cmd;
+    return a.New(std::move(f));
+}
+Flow* Intern(FlowArena& a, const std::string& url) {
+    Flow f;
+    f.op = OpIntern;
+    f.URL = url;
+    return a.New(std::move(f));
+}
+Flow* Extern(FlowArena& a, const std::string& url, Flow* dep) {
+    Flow f;
+    f.op = OpExtern;
+    f.URL = url;
+    f.Deps = {dep};
+    return a.New(std::move(f));
+}
+Flow* Groupby(FlowArena& a, const std::string& re, Flow* dep) {
+    Flow f;
+    f.op = OpGroupby;
+    f.Re = re;
+    f.Deps = {dep};
+    return a.New(std::move(f));
+}
+Flow* Collect(FlowArena& a, const std::string& re, const std::string& repl, Flow* dep) {
+    Flow f;
+    f.op = OpCollect;
+    f.Re = re;
+    f.Repl = repl;
+    f.Deps = {dep};
+    return a.New(std::move(f));
+}
+Flow* Merge(FlowArena& a, std::vector<Flow*> deps) {
+    Flow f;
+    f.op = OpMerge;
+    f.Deps = std::move(deps);
+    return a.New(std::move(f));
+}
+Flow* Pullup(FlowArena& a, std::vector<Flow*> deps) {
+    Flow f;
+    f.op = OpPullup;
+    f.Deps = std::move(deps);
+    return a.New(std::move(f));
+}
+Flow* Val(FlowArena& a, const Fileset& v) {  // Fileset.Flow: OpVal, FlowDone
+    Flow f;
+    f.op = OpVal;
+    f.Value = v;
+    f.Done = true;
+    return a.New(std::move(f));
+}
+Flow* Data(FlowArena& a, const std::string& b) {
+    Flow f;
+    f.op = OpData;
+    f.Data = b;
+    return a.New(std::move(f));
+}
+}  // namespace flow
+
+// ---- Eval: lowering to rf_graph jobs ------------------------------------------
+static void writeN(std::string& w, int64_t n) {
+    const uint64_t u = (uint64_t)n;
+    for (int i = 0; i < 8; ++i) w.push_back((char)(u >> (8 * i)));
+}
+
+static void exec_suffix(const Flow* f, std::string& w) {
+    w += f->Image;
+    w += f->Cmd;
+    if (f->Argmap)
+        for (const ExecArg& a : *f->Argmap) writeN(w, a.Out ? -(int64_t)a.Index : a.Index);
+}
+
+Eval::Eval(Engine& e, std::string universe, bool file_slots)
+    : e_(e), U_(std::move(universe)), file_slots_(file_slots) {}
+
+Eval::~Eval() {
+    if (g_) rf_graph_destroy(g_);
+}
+
+void Eval::fileset_material(const Fileset& v, std::string& out,
+                            std::vector<std::pair<uint32_t, uint32_t>>& holes) {
+    if (v.List) {
+        for (const Fileset& c : *v.List) fileset_material(c, out, holes);
+        return;
+    }
+    for (const auto& [path, file] : v.Map) {
+        out += path;
+        if (file_slots_) {
+            auto it = file_slot_.find(file.ID);
+            uint32_t s;
+            if (it == file_slot_.end()) {
+                s = new_slot();
+                file_slot_.emplace(file.ID, s);
+            } else {
+                s = it->second;
+            }
+            out.push_back('\0');
+            out.push_back('\5');
+            holes.emplace_back((uint32_t)out.size(), s);
+            out.append(32, '\0');
+        } else {
+            WriteDigest(out, file.ID);
+        }
+    }
+}
+
+// Flow.WriteDigest (flow.go:675-750) with WD(dep.Digest()) as holes.
+void Eval::material(const Flow* f, bool v1, std::string& out,
+                    std::vector<std::pair<uint32_t, uint32_t>>& holes) {
+    v1 = v1 || f->config.HashV1;
+    out += U_;
+    if (f->op == OpRequirements) {
+        material(f->Deps.at(0), v1, out, holes);
+        return;
+    }
+    if (f->Parent) {
+        material(f->Parent, v1, out, holes);
+        return;
+    }
+    for (const Flow* d : f->Deps) {
+        if (v1) {
+            material(d, v1, out, holes);
+        } else {
+            const uint32_t s = lower(d);
+            out.push_back('\0');
+            out.push_back('\5');
+            holes.emplace_back((uint32_t)out.size(), s);
+            out.append(32, '\0');
+        }
+    }
+    out += DigestString(f->op);
+    switch (f->op) {
+    case OpIntern:
+    case OpExtern: out += f->URL; break;
+    case OpExec: exec_suffix(f, out); break;
+    case OpGroupby: out += f->Re; break;
+    case OpMap: material(f->MapFlow, v1, out, holes); break;
+    case OpCollect: out += f->Re; out += f->Repl; break;
+    case OpVal:
+        if (f->Err) throw Error(RF_EINVAL, "error OpVal digests are random (flow.go:722-731)");
+        if (f->Value) {
+            fileset_material(*f->Value, out, holes);
+        } else {
+            if (f->FlowDigest.IsZero()) throw Error(RF_EINVAL, "invalid flow digest");
+            WriteDigest(out, f->FlowDigest);
+        }
+        break;
+    case OpK:
+    case OpCoerce:
+        if (f->FlowDigest.IsZero()) throw Error(RF_EINVAL, "invalid flow digest");
+        WriteDigest(out, f->FlowDigest);
+        break;
+    case OpData: out += f->Data; break;
+    default: break;  // OpMerge, OpPullup
+    }
+}
+
+uint32_t Eval::lower(const Flow* f) {
+    auto it = logical_.find(f);
+    if (it != logical_.end()) return it->second;
+    Job j;
+    material(f, false, j.tmpl, j.holes);
+    j.out = new_slot();
+    logical_[f] = j.out;
+    jobs_.push_back(std::move(j));
+    return logical_[f];
+}
+
+// Flow.PhysicalDigest (flow.go:764-792): no Universe, no op name, no WD.
+void Eval::lower_physical(const Flow* f) {
+    if (f->op != OpExec && f->op != OpExtern) return;
+    if (physical_.count(f)) return;
+    for (const Flow* d : f->Deps)
+        if (!d->Done) return;
+    Job j;
+    for (const Flow* d : f->Deps) {
+        if (!d->Value) throw Error(RF_EINVAL, "done dependency without a Fileset value");
+        fileset_material(*d->Value, j.tmpl, j.holes);
+    }
+    if (f->op == OpExtern)
+        j.tmpl += f->URL;
+    else
+        exec_suffix(f, j.tmpl);
+    j.out = new_slot();
+    physical_[f] = j.out;
+    jobs_.push_back(std::move(j));
+}
+
+void Eval::Add(Flow* root) {
+    std::vector<const Flow*> stack{root};
+    std::unordered_set<const Flow*> seen;
+    while (!stack.empty()) {
+        const Flow* f = stack.back();
+        stack.pop_back();
+        if (!f || !seen.insert(f).second) continue;
+        lower(f);
+        lower_physical(f);
+        for (const Flow* d : f->Deps) stack.push_back(d);
+        if (f->MapFlow) stack.push_back(f->MapFlow);
+        if (f->Parent) stack.push_back(f->Parent);
+    }
+}
+
+void Eval::Build() {
+    const uint32_t J = (uint32_t)jobs_.size();
+    std::vector<uint32_t> out_slot(J), tmpl_len(J), hole_pos, hole_slot;
+    std::vector<uint64_t> tmpl_off(J), hole_ptr(J + 1, 0);
+    std::string blob;
+    for (uint32_t i = 0; i < J; ++i) {
+        const Job& j = jobs_[i];
+        out_slot[i] = j.out;
+        tmpl_off[i] = blob.size();
+        tmpl_len[i] = (uint32_t)j.tmpl.size();
+        blob += j.tmpl;
+        for (auto [pos, slot] : j.holes) {
+            hole_pos.push_back(pos);
+            hole_slot.push_back(slot);
+        }
+        hole_ptr[i + 1] = hole_pos.size();
+    }
+    rf_graph_desc d{J,
+                    n_slots_,
+                    out_slot.data(),
+                    tmpl_off.data(),
+                    tmpl_len.data(),
+                    hole_ptr.data(),
+                    hole_pos.data(),
+                    hole_slot.data(),
+                    reinterpret_cast<const uint8_t*>(blob.data()),
+                    blob.size()};
+    if (g_) rf_graph_destroy(g_);
+    g_ = nullptr;
+    Check(rf_graph_load(e_.ctx(), &d, &g_));
+    if (!file_slot_.empty()) {
+        std::vector<uint32_t> s;
+        std::vector<uint8_t> ids;
+        for (const auto& [id, slot] : file_slot_) {
+            s.push_back(slot);
+            ids.insert(ids.end(), id.b.begin(), id.b.end());
+        }
+        Check(rf_graph_set_slots(g_, s.data(), ids.data(), (uint32_t)s.size()));
+    }
+    Recompute(true);
+}
+
+uint64_t Eval::Recompute(bool full) {
+    uint64_t n = 0;
+    Check(rf_graph_recompute(g_, full ? 1 : 0, &n));
+    cache_ok_ = false;
+    return n;
+}
+
+void Eval::fetch() const {
+    if (cache_ok_) return;
+    std::vector<uint32_t> idx(n_slots_);
+    for (uint32_t i = 0; i < n_slots_; ++i) idx[i] = i;
+    cache_.assign(32ull * n_slots_, 0);
+    if (n_slots_) Check(rf_graph_get_slots(g_, idx.data(), n_slots_, cache_.data()));
+    cache_ok_ = true;
+}
+
+Digest Eval::FlowDigest(const Flow* f) const {
+    fetch();
+    Digest d;
+    memcpy(d.b.data(), cache_.data() + 32ull * logical_.at(f), 32);
+    return d;
+}
+
+std::optional<Digest> Eval::PhysicalDigest(const Flow* f) const {
+    auto it = physical_.find(f);
+    if (it == physical_.end()) return std::nullopt;
+    fetch();
+    Digest d;
+    memcpy(d.b.data(), cache_.data() + 32ull * it->second, 32);
+    return d;
+}
+
+// CacheKeys (flow.go:796-802): most to least concrete.
+std::vector<Digest> Eval::CacheKeys(const Flow* f) const {
+    std::vector<Digest> keys;
+    if (auto p = PhysicalDigest(f)) keys.push_back(*p);
+    keys.push_back(FlowDigest(f));
+    return keys;
+}
+
+void Eval::SetFileID(const Digest& old_id, const Digest& new_id) {
+    auto it = file_slot_.find(old_id);
+    if (it == file_slot_.end()) throw Error(RF_ENOTFOUND, "file id not referenced: " + old_id.String());
+    const uint32_t s = it->second;
+    file_slot_.erase(it);
+    file_slot_[new_id] = s;
+    Check(rf_graph_set_slots(g_, &s, new_id.b.data(), 1));
+}
+
+// ---- Canonicalize ------------------------------------------------------------
+Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const std::string& U) {
+    // 1. one copy per original node, config merged, deps (and MapFlow) pointing
+    //    at copies -- the f.Copy()/Config.Merge/recursion of flow.go:820-839.
+    std::unordered_map<const Flow*, Flow*> copy;
+    std::vector<Flow*> post;  // copies in post-order (the order of m.Put)
+    std::function<Flow*(Flow*)> rec = [&](Flow* f) -> Flow* {
+        auto it = copy.find(f);
+        if (it != copy.end()) return it->second;
+        Flow c = *f;
+        c.config.Merge(config);
+        Flow* cp = arena.New(std::move(c));
+        copy[f] = cp;
+        for (Flow*& d : cp->Deps) d = rec(d);
+        if (cp->MapFlow) cp->MapFlow = rec(cp->MapFlow);
+        post.push_back(cp);
+        return cp;
+    };
+    Flow* croot = rec(root);
+    // 2. digests of every copy on the device
+    Eval ev(e, U);
+    ev.Add(croot);
+    ev.Build();
+    // 3. flowMap.Put: first copy with a digest wins; deps re-pointed at it
+    //    (equal digests by construction, so digests do not change)
+    std::unordered_map<Digest, Flow*, DigestHash> m;
+    std::unordered_map<Flow*, Flow*> canon;
+    for (Flow* c : post) {
+        const Digest d = ev.FlowDigest(c);
+        auto it = m.find(d);
+        canon[c] = (it == m.end()) ? (m[d] = c) : it->second;
+    }
+    for (Flow* c : post) {
+        for (Flow*& d : c->Deps) d = canon[d];
+        if (c->MapFlow) c->MapFlow = canon[c->MapFlow];
+    }
+    return canon[croot];
+}
+
+// ---- Liveset ---------------------------------------------------------------------
+Liveset::Liveset(Engine& e, uint64_t m, uint64_t k) { Check(rf_bloom_new(e.ctx(), m, k, &b_)); }
+
+Liveset Liveset::FromJSON(Engine& e, const std::string& js) {
+    rf_bloom* b = nullptr;
+    Check(rf_bloom_load_json(e.ctx(), js.data(), js.size(), &b));
+    return Liveset(b);
+}
+
+Liveset::~Liveset() {
+    if (b_) rf_bloom_destroy(b_);
+}
+
+void Liveset::Add(const std::vector<Digest>& ds) {
+    if (!ds.empty()) Check(rf_bloom_add(b_, ds[0].b.data(), ds.size()));
+}
+
+std::vector<bool> Liveset::Contains(const std::vector<Digest>& ds) {
+    std::vector<uint8_t> out(ds.size());
+    if (!ds.empty()) Check(rf_bloom_probe(b_, ds[0].b.data(), ds.size(), out.data()));
+    return std::vector<bool>(out.begin(), out.end());
+}
+
+}  // namespace reflow

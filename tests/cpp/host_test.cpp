@@ -1,0 +1,191 @@
+// host_test.cpp -- the reference's digest tests, restated against the C++ host
+// mirror (include/reflow_hip_host.hpp) running on the device.
+//   TestDigestStability   flow_test.go:24-44
+//   TestCanonicalize      flow_test.go:46-58
+//   TestValueDigest       executor_test.go:62-86
+//   TestDigestExec        syntax/digest_test.go:13-29 (the evaluated flow chain)
+//   TestCacheKeys         flow.go:764-802 (physical key first)
+//   TestIncremental       SetFileID + Recompute == a fresh evaluation
+//   TestLiveset           bloomlive Contains over Add
+// Exit status 0 iff every check passes.
+#include <cstdio>
+#include <string>
+
+#include "reflow_host.hpp"
+
+using namespace reflow;
+
+static int failures = 0;
+#define EXPECT(cond, ...)                                   \
+    do {                                                    \
+        if (!(cond)) {                                      \
+            ++failures;                                     \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);                   \
+            fprintf(stderr, "\n");                          \
+        }                                                   \
+    } while (0)
+
+static Flow* stable_flow(FlowArena& a) {
+    Flow* intern = flow::Intern(a, "internurl");
+    Flow* collect = flow::Collect(a, ".*", "$0", intern);
+    Flow* groupby = flow::Groupby(a, "foo-(.*)", collect);
+    Flow* mapflow = flow::Map(a, [&](Flow* f) { return flow::Exec(a, "image", "command", {f}); }, groupby);
+    return flow::Extern(a, "externurl", mapflow);
+}
+
+static void TestDigestStability(Engine& e) {
+    const char* v1 = "sha256:5a3a916fe9a11b67f9a0dbd67f6fac0f986dd67803267e79f25f866ca9781e2f";
+    const char* v2 = "sha256:02751e46c573a31747a30b05c2b73b2eb556fb45fb4c0aaf88d170f4b5e6d4e7";
+    FlowArena a;
+    Flow* stable = stable_flow(a);
+    Flow* c = Canonicalize(e, a, stable, Config{true});
+    Eval ev1(e);
+    ev1.Add(c);
+    ev1.Build();
+    EXPECT(ev1.FlowDigest(c).String() == v1, "V1 got %s", ev1.FlowDigest(c).String().c_str());
+    Eval ev2(e);
+    ev2.Add(stable);
+    ev2.Build();
+    EXPECT(ev2.FlowDigest(stable).String() == v2, "V2 got %s", ev2.FlowDigest(stable).String().c_str());
+}
+
+static void TestCanonicalize(Engine& e) {
+    FlowArena a;
+    Flow* i1 = flow::Intern(a, "url");
+    Flow* i2 = flow::Intern(a, "url");
+    Flow* merged = flow::Merge(a, {i1, i2});
+    Eval ev(e);
+    ev.Add(merged);
+    ev.Build();
+    Flow* canon = Canonicalize(e, a, merged, Config{});
+    Eval evc(e);
+    evc.Add(canon);
+    evc.Build();
+    EXPECT(evc.FlowDigest(canon) == ev.FlowDigest(merged), "canonical digest changed");
+    EXPECT(canon->Deps[0] == canon->Deps[1], "flow is not canonical");
+}
+
+static void TestValueDigest(Engine& e) {
+    Digester D(e);
+    File f1{D.FromString("foo"), 3}, f2{D.FromString("bar"), 3}, f3{D.FromString("a/b/c"), 5};
+    Fileset v1, v2, vlist;
+    v1.Map = {{"foo", f1}, {"bar", f2}};
+    v2.Map = {{"a/b/c", f3}, {"bar", f2}};
+    vlist.List = std::vector<Fileset>{v1, v2};
+    auto d = FilesetDigests(e, {&v1, &v2, &vlist});
+    EXPECT(d[0] != d[1], "did not expect v1, v2 to have the same digest");
+    EXPECT(d[2].String() == "sha256:d60e67ce9e89548b502a5ad7968e99caed0d388f0a991b906f41a7ba65adb31f",
+           "vlist got %s", d[2].String().c_str());
+    EXPECT(vlist.N() == 4, "N");
+}
+
+static void TestDigestExec(Engine& e) {
+    Digester D(e);
+    FlowArena a;
+    auto coerce = [&](Flow* dep, const char* fd) {
+        Flow f;
+        f.op = OpCoerce;
+        f.Deps = {dep};
+        f.FlowDigest = D.FromString(fd);
+        return a.New(std::move(f));
+    };
+    Flow* intern = flow::Intern(a, "s3://blah");
+    Flow* c1 = coerce(intern, "file.fs$file");
+    Flow k;
+    k.op = OpK;
+    k.Deps = {c1};
+    k.FlowDigest = D.FromString("grail.com/reflow/syntax.Eval.Force");
+    Flow* kf = a.New(std::move(k));
+    Flow* c2 = coerce(kf, "grail.com/reflow/syntax.coerceFlowToFileset");
+    Flow* ex = flow::Exec(a, "ubuntu", " cp %s %s ", {c2});
+    ex->Argmap = std::vector<ExecArg>{{false, 0}, {true, 0}};
+    Flow* c3 = coerce(ex, "grail.com/reflow/syntax.Eval.coerceExecOutput");
+    Eval ev(e);
+    ev.Add(c3);
+    ev.Build();
+    EXPECT(ev.FlowDigest(c3).String() ==
+               "sha256:ceff79828962397af02d8e2ea30cf6388f2858e0deefbecaa73fad1c6fc88816",
+           "exec chain got %s", ev.FlowDigest(c3).String().c_str());
+}
+
+static Fileset one(const Digest& id) {
+    Fileset v;
+    v.Map = {{".", File{id, 1}}};
+    return v;
+}
+
+static void TestCacheKeysAndIncremental(Engine& e) {
+    Digester D(e);
+    FlowArena a;
+    Digest ida = D.FromString("a"), idb = D.FromString("b");
+    Flow* va = flow::Val(a, one(ida));
+    Flow* vb = flow::Val(a, one(idb));
+    Flow* ex = flow::Exec(a, "img", "cmd %s %s", {va, vb});
+    ex->Argmap = std::vector<ExecArg>{{false, 0}, {false, 1}, {true, 0}};
+    Flow* root = flow::Extern(a, "s3://out", ex);
+    Eval ev(e, "", /*file_slots=*/true);
+    ev.Add(root);
+    ev.Build();
+    auto keys = ev.CacheKeys(ex);
+    EXPECT(keys.size() == 2, "exec over done values has physical + logical keys");
+    EXPECT(ev.CacheKeys(root).size() == 1, "extern over an unfinished exec has only the logical key");
+    // physical material = FM(va) || FM(vb) || image || cmd || argmap
+    std::string pm;
+    va->Value->WriteDigest(pm);
+    vb->Value->WriteDigest(pm);
+    pm += "imgcmd %s %s";
+    for (int64_t n : {0, 1, 0}) {
+        const uint64_t u = (uint64_t)n;
+        for (int i = 0; i < 8; ++i) pm.push_back((char)(u >> (8 * i)));
+    }
+    EXPECT(keys[0] == D.FromBytes(pm), "physical digest");
+    // incremental: change b's ID, compare with a fresh evaluation
+    Digest idb2 = D.FromString("b2");
+    ev.SetFileID(idb, idb2);
+    const uint64_t n = ev.Recompute();
+    vb->Value = one(idb2);
+    Eval fresh(e, "", true);
+    fresh.Add(root);
+    fresh.Build();
+    for (Flow* f : {va, vb, ex, root})
+        EXPECT(ev.FlowDigest(f) == fresh.FlowDigest(f), "incremental != fresh");
+    EXPECT(ev.CacheKeys(ex)[0] == fresh.CacheKeys(ex)[0], "physical incremental != fresh");
+    EXPECT(n == 4, "recomputed %llu jobs, want 4 (vb, ex, ex physical, root)", (unsigned long long)n);
+}
+
+static void TestLiveset(Engine& e) {
+    Digester D(e);
+    std::vector<std::string> in, out;
+    for (int i = 0; i < 1000; ++i) in.push_back("live" + std::to_string(i));
+    for (int i = 0; i < 1000; ++i) out.push_back("dead" + std::to_string(i));
+    auto din = D.FromBytesBatch(in), dout = D.FromBytesBatch(out);
+    Liveset live(e, 14378, 10);  // NewWithEstimates(1000, 0.001)
+    live.Add(din);
+    auto got = live.Contains(din);
+    int fp = 0;
+    for (bool b : got) EXPECT(b, "false negative");
+    for (bool b : live.Contains(dout)) fp += b;
+    EXPECT(fp < 20, "false positives %d", fp);
+}
+
+int main() {
+    try {
+        Engine e(0);
+        TestDigestStability(e);
+        TestCanonicalize(e);
+        TestValueDigest(e);
+        TestDigestExec(e);
+        TestCacheKeysAndIncremental(e);
+        TestLiveset(e);
+    } catch (const std::exception& ex) {
+        fprintf(stderr, "exception: %s\n", ex.what());
+        return 2;
+    }
+    if (failures) {
+        fprintf(stderr, "%d failure(s)\n", failures);
+        return 1;
+    }
+    printf("PASS\n");
+    return 0;
+}
