@@ -206,9 +206,30 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
 //   S = Σ1(e) | Σ0(a)            3 v_alignbit with per-lane amounts + xor3
 //   F = Ch(e,f,g) | Maj(a,b,c)   Maj(a,b,c) = Ch(a^c, b, c): sel = X0^(X2&M)
 //   R = Z + S + F                Z = h+K+W on e-lanes, 0 on a-lanes
-//   N = D[lane^8] + R            D = R (e-lanes) | d (a-lanes), DPP row_ror:8
-// so e-lanes get e' = d + T1 and a-lanes a' = T1 + Σ0 + Maj: 11 VALU per
+//   N = X3[lane^8] + R (e-lanes) | R[lane^8] + R (a-lanes), DPP row_ror:8
+// so e-lanes get e' = d + T1 and a-lanes a' = T1 + Σ0 + Maj: 10 VALU per
 // round instead of 14 on one lane.  K+W comes from LDS as in the solo kernel.
+// One duo round on the state registers (x0,x1,x2,x3); the new X0 is written
+// into x3's register (old X3 is dead after the round).  Bank-masked DPP
+// (banks 0-1 = e-lanes 0-7, banks 2-3 = a-lanes 8-15 of each 16-lane row;
+// masked lanes keep their value):
+//   e-lanes: N = X3[lane^8] + R = d + T1
+//   e-lanes: Z = X2 + K+W(t+1)   (a-lanes keep Z = 0)
+//   a-lanes: N = R[lane^8] + R = T1 + Σ0 + Maj
+// The second add puts two wait states between R's write and the third's DPP
+// read of R (VALU->DPP hazard); X3/X2 were written rounds earlier.
+#define RF_DUO_ROUND(x0, x1, x2, x3, kw)                                                  \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t"                              \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t"                              \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t"                              \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                            \
+    "v_bitop3_b32 %[t1], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                     \
+    "v_bitop3_b32 %[t1], %[t1], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                    \
+    "v_add3_u32 %[t2], %[z], %[t0], %[t1]\n\t"                                           \
+    "v_add_u32_dpp %[" x3 "], %[" x3 "], %[t2] row_ror:8 row_mask:0xf bank_mask:0x3\n\t" \
+    "v_add_u32_dpp %[z], %[" x2 "], %[" kw "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t" \
+    "v_add_u32_dpp %[" x3 "], %[t2], %[t2] row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+
 __global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ __attribute__((aligned(16))) uint32_t kw[64 * kRow];
@@ -249,30 +270,26 @@ __global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
             for (uint32_t j = 0; j < cnt; ++j) {
                 const uint4* r4 = reinterpret_cast<const uint4*>(&kw[j * kRow]);
                 uint32_t X0 = H0, X1 = H1, X2 = H2, X3 = H3;
-                uint4 v = r4[0];
+                uint4 v = r4[0], vn = r4[1];
                 uint32_t Z = elane ? X3 + v.x : 0u;
 #pragma unroll
                 for (int t4 = 0; t4 < 16; ++t4) {
-                    const uint4 vn = t4 < 15 ? r4[t4 + 1] : make_uint4(0, 0, 0, 0);
-                    const uint32_t kv[5] = {v.x, v.y, v.z, v.w, vn.x};
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t S = xor3(__builtin_amdgcn_alignbit(X0, X0, sh1),
-                                                __builtin_amdgcn_alignbit(X0, X0, sh2),
-                                                __builtin_amdgcn_alignbit(X0, X0, sh3));
-                        const uint32_t sel = __builtin_amdgcn_bitop3_b32(X0, X2, M, 0x78);
-                        const uint32_t F = __builtin_amdgcn_bitop3_b32(sel, X1, X2, 0xCA);
-                        const uint32_t R = add3v(Z, S, F);
-                        const uint32_t D = elane ? R : X3;
-                        // two independent VALU between D's write and its DPP read
-                        // cover the VALU->DPP hazard (no s_nop)
-                        const uint32_t T = X2 + kv[u + 1];
-                        Z = elane ? T : 0u;
-                        const uint32_t N =
-                            (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D, 0x128, 0xF, 0xF, false) + R;
-                        X3 = X2; X2 = X1; X1 = X0; X0 = N;
-                    }
+                    // LDS reads run two groups ahead of the chain
+                    const uint4 vnn = t4 < 14 ? r4[t4 + 2] : make_uint4(0, 0, 0, 0);
+                    uint32_t t0, t1, t2;
+                    // Four rounds per asm block: the state rotates through the
+                    // four registers and is back in place after four rounds, so
+                    // the compiler's pad after an asm block is paid once per 4.
+                    asm volatile(RF_DUO_ROUND("a", "b", "c", "d", "k1")
+                                 RF_DUO_ROUND("d", "a", "b", "c", "k2")
+                                 RF_DUO_ROUND("c", "d", "a", "b", "k3")
+                                 RF_DUO_ROUND("b", "c", "d", "a", "k4")
+                                 : [a] "+v"(X0), [b] "+v"(X1), [c] "+v"(X2), [d] "+v"(X3),
+                                   [z] "+v"(Z), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+                                 : [s1] "v"(sh1), [s2] "v"(sh2), [s3] "v"(sh3), [m] "v"(M),
+                                   [k1] "v"(v.y), [k2] "v"(v.z), [k3] "v"(v.w), [k4] "v"(vn.x));
                     v = vn;
+                    vn = vnn;
                 }
                 H0 += X0; H1 += X1; H2 += X2; H3 += X3;
             }

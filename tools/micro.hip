@@ -89,6 +89,114 @@ __global__ __launch_bounds__(256) void k_op(uint32_t iters, uint32_t* out) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+#define RF_E " row_ror:8 row_mask:0xf bank_mask:0x3"
+#define RF_Q " quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3"
+#define RF_A " row_ror:8 row_mask:0xf bank_mask:0xc"
+#define MDUO(x0, x1, x2, x3, sfx, e, q, aa)                                          \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t"                          \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t"                          \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t"                          \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                        \
+    "v_bitop3_b32 %[t1], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                 \
+    "v_bitop3_b32 %[t1], %[t1], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                \
+    "v_add3_u32 %[t2], %[z], %[t0], %[t1]\n\t"                                       \
+    "v_add_u32" sfx " %[" x3 "], %[" x3 "], %[t2]" e "\n\t"                          \
+    "v_add_u32" sfx " %[z], %[" x2 "], %[k]" q "\n\t"                                \
+    "v_add_u32" sfx " %[" x3 "], %[t2], %[t2]" aa "\n\t"
+
+// lag-2 duo step: a-lanes run two rounds behind the e-lanes, so the
+// cross-lane value is one step old and no instruction depends on the one
+// right before it (9 VALU per round).
+#define LAG2(x0, x1, x2, x3, z, zn)                                                 \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t"                          \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t"                          \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t"                          \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                 \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                        \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[k]\n\t"                                 \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"                               \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+
+// D: single-wave latency: one dependent chain per lane (grid 1 x 64), so
+// the time per instruction is the issue-to-dependent-issue latency.  OP 8/9
+// run the duo round (10 instructions) with DPP / with plain adds.
+template <int OP>
+__global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint64_t* cyc) {
+    uint32_t r = threadIdx.x * 7 + 1, x1 = r * 3, x2 = r * 5, x3 = r * 9, z = r & 8 ? 0 : r;
+    const uint32_t c = blockIdx.x | 1, s1 = threadIdx.x & 8 ? 2 : 6, s2 = threadIdx.x & 8 ? 13 : 11,
+                   s3 = threadIdx.x & 8 ? 22 : 25, m = threadIdx.x & 8 ? ~0u : 0u;
+    uint32_t t0, t1, t2, t3 = 0, zy = r;
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+    for (uint32_t i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j == 0) {
+#define X8(i) i "\n\t" i "\n\t" i "\n\t" i "\n\t" i "\n\t" i "\n\t" i "\n\t" i "\n\t"
+                if constexpr (OP == 0) asm volatile(X8("v_add_u32 %0, %0, %1") : "+v"(r) : "v"(c));
+                if constexpr (OP == 1) asm volatile(X8("v_alignbit_b32 %0, %0, %0, 7") : "+v"(r));
+                if constexpr (OP == 2) asm volatile(X8("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96") : "+v"(r) : "v"(c));
+                if constexpr (OP == 3) asm volatile(X8("v_add3_u32 %0, %0, %1, %1") : "+v"(r) : "v"(c));
+                if constexpr (OP == 4)
+                    asm volatile(X8("v_add_u32_dpp %0, %1, %0 row_ror:8 row_mask:0xf bank_mask:0xf") : "+v"(r) : "v"(c));
+                if constexpr (OP == 5)
+                    asm volatile(X8("v_add_u32_dpp %0, %1, %0 row_ror:8 row_mask:0xf bank_mask:0x3") : "+v"(r) : "v"(c));
+                if constexpr (OP == 6) asm volatile(X8("v_add_u32 %0, %1, %1") : "=v"(t0) : "v"(c));  // independent
+                if constexpr (OP == 7) asm volatile(X8("v_add_u32 %0, %0, %1\n\ts_nop 0") : "+v"(r) : "v"(c));
+#undef X8
+            }
+            if (OP == 8 && (j & 3) == 0)
+                asm volatile(MDUO("a", "b", "c", "d", "_dpp", RF_E, RF_Q, RF_A)
+                             MDUO("d", "a", "b", "c", "_dpp", RF_E, RF_Q, RF_A)
+                             MDUO("c", "d", "a", "b", "_dpp", RF_E, RF_Q, RF_A)
+                             MDUO("b", "c", "d", "a", "_dpp", RF_E, RF_Q, RF_A)
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if (OP == 9 && (j & 3) == 0)
+                asm volatile(MDUO("a", "b", "c", "d", "", "", "", "")
+                             MDUO("d", "a", "b", "c", "", "", "", "")
+                             MDUO("c", "d", "a", "b", "", "", "", "")
+                             MDUO("b", "c", "d", "a", "", "", "", "")
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if (OP == 10 && (j & 3) == 0)
+                asm volatile(LAG2("a", "b", "c", "d", "z", "y") LAG2("d", "a", "b", "c", "y", "z")
+                             LAG2("c", "d", "a", "b", "z", "y") LAG2("b", "c", "d", "a", "y", "z")
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [y] "+v"(zy), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+        }
+    }
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = r ^ x1 ^ x2 ^ x3 ^ z ^ t0 ^ zy ^ t3;
+    if (threadIdx.x == 0) *cyc = c1 - c0;
+}
+
+struct LtArgs { int op; uint32_t iters; uint32_t* out; uint64_t* cyc; };
+static void run_lat(void* p) {
+    auto* a = (LtArgs*)p;
+#define RF_LAT(N) case N: hipLaunchKernelGGL(k_lat<N>, dim3(1), dim3(64), 0, 0, a->iters, a->out, a->cyc); break;
+    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) default: RF_LAT(10) }
+#undef RF_LAT
+}
+
+static float time_launch(void (*fn)(void*), void* arg);
+
+// Returns ms; *cycles = s_memtime delta of the timed launch.
+extern "C" float micro_lat(int op, uint32_t iters, uint64_t* cycles) {
+    uint32_t* out;
+    uint64_t* cyc;
+    if (hipMalloc(&out, 64 * 4) != hipSuccess || hipMalloc(&cyc, 8) != hipSuccess) return -2.f;
+    LtArgs a{op, iters, out, cyc};
+    float ms = time_launch(run_lat, &a);
+    hipMemcpy(cycles, cyc, 8, hipMemcpyDeviceToHost);
+    hipFree(out);
+    hipFree(cyc);
+    return ms;
+}
+
 struct OArgs { int op; uint32_t grid, iters; uint32_t* out; };
 static void run_op(void* p) {
     auto* a = (OArgs*)p;

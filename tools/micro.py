@@ -25,6 +25,21 @@ def main():
     L.micro_loads.restype = ctypes.c_float
     L.micro_op.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32]
     L.micro_op.restype = ctypes.c_float
+    L.micro_lat.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
+    L.micro_lat.restype = ctypes.c_float
+    lat_names = ["dep v_add_u32", "dep v_alignbit", "dep v_bitop3", "dep v_add3", "dep add_dpp ror8",
+                 "dep add_dpp ror8 bank", "indep v_add_u32", "dep add+s_nop0", "duo round (dpp)",
+                 "duo round (plain)", "lag2 step"]
+    for op, name in enumerate(lat_names):
+        iters = 1 << 17
+        cyc = ctypes.c_uint64(0)
+        ms = L.micro_lat(op, iters, ctypes.byref(cyc))
+        n = iters * 8 * (9 if op == 10 else 10 if op >= 8 else 1)
+        print("lat %-22s 1 wave  %.3f ms  %.2f ns/instr  memtime %.2f ticks/instr  %s"
+              % (name, ms, ms * 1e6 / n, cyc.value / n, "(%.1f ns/round)" % (ms * 1e6 / (iters * 8)) if op >= 8 else ""),
+              flush=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "lat":
+        return
     names = ["v_add_u32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32", "v_xor_b32", "v_perm_b32",
              "v_lshrrev_b32", "v_fma_f32"]
     for op, name in enumerate(names):
