@@ -200,52 +200,132 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Duo: one wave per long message, the round chain split over two lanes.
-// Lanes with (lane & 8) == 0 ("e-lanes") hold (e,f,g,h); their partners
-// lane^8 ("a-lanes") hold (a,b,c,d).  One instruction stream serves both:
-//   S = Σ1(e) | Σ0(a)            3 v_alignbit with per-lane amounts + xor3
-//   F = Ch(e,f,g) | Maj(a,b,c)   Maj(a,b,c) = Ch(a^c, b, c): sel = X0^(X2&M)
-//   R = Z + S + F                Z = h+K+W on e-lanes, 0 on a-lanes
-//   N = X3[lane^8] + R (e-lanes) | R[lane^8] + R (a-lanes), DPP row_ror:8
-// so e-lanes get e' = d + T1 and a-lanes a' = T1 + Σ0 + Maj: 10 VALU per
-// round instead of 14 on one lane.  K+W comes from LDS as in the solo kernel.
-// One duo round on the state registers (x0,x1,x2,x3); the new X0 is written
-// into x3's register (old X3 is dead after the round).  Bank-masked DPP
-// (banks 0-1 = e-lanes 0-7, banks 2-3 = a-lanes 8-15 of each 16-lane row;
-// masked lanes keep their value):
-//   e-lanes: N = X3[lane^8] + R = d + T1
-//   e-lanes: Z = X2 + K+W(t+1)   (a-lanes keep Z = 0)
-//   a-lanes: N = R[lane^8] + R = T1 + Σ0 + Maj
-// The second add puts two wait states between R's write and the third's DPP
-// read of R (VALU->DPP hazard); X3/X2 were written rounds earlier.
-#define RF_DUO_ROUND(x0, x1, x2, x3, kw)                                                  \
-    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t"                              \
-    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t"                              \
-    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t"                              \
-    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                            \
-    "v_bitop3_b32 %[t1], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                     \
-    "v_bitop3_b32 %[t1], %[t1], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                    \
-    "v_add3_u32 %[t2], %[z], %[t0], %[t1]\n\t"                                           \
-    "v_add_u32_dpp %[" x3 "], %[" x3 "], %[t2] row_ror:8 row_mask:0xf bank_mask:0x3\n\t" \
-    "v_add_u32_dpp %[z], %[" x2 "], %[" kw "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t" \
-    "v_add_u32_dpp %[" x3 "], %[t2], %[t2] row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+// Duo: one wave per long message, the round chain split over two lanes and
+// staggered by two rounds.
+//
+// Lanes with (lane & 8) == 0 ("e-lanes") run the e-half of round s; their
+// partners lane^8 ("a-lanes") run the a-half of round s-2 in the same
+// instruction stream.  With the state kept as the sequences e(r), a(r)
+// (f = e(r-1), ..., d = a(r-3)) one round is
+//   e-lanes: e(r+1) = Z + Σ1(e) + Ch(e,f,g),  Z = h + K+W(r) + d
+//   a-lanes: a(r+1) = Z + Σ0(a) + Maj(a,b,c), Z = T1(r) = e(r+1) - d
+// i.e. the same  R = Z + S + F  on both halves (3 v_alignbit with per-lane
+// amounts + xor3; Maj(a,b,c) = Ch(a^c, b, c) via sel = X0 ^ (X2 & M)).  The
+// Z of the next step needs one cross-lane value that is already a step old
+// on both halves -- the partner's X0 (a(r-2) for the e-lane, e(r+2-2) for
+// the a-lane, two rounds behind) -- so it is
+//   Zt = (X2 ^ M) + k      e: g + K+W(r+1)     a: -c   (k = 1)
+//   Z' = X0[lane^8] + Zt   one full-mask DPP add
+// 9 VALU per round and no instruction reads the result of the one before
+// it (a dependent VALU costs ~6-7 cycles against 4 for an independent one,
+// tools/micro.hip "lat").  Block boundaries: each half applies its own
+// feed-forward (bank-masked DPP adds) when it reaches round 0 of the next
+// block; the Z values that straddle the boundary read partner values from
+// before the partner's feed-forward and get per-block corrections
+// (c63/c64/c65 below).  A message starts from a zero raw state with
+// chaining value IV, so block 0 takes the same path as every other block.
+//
+// Registers: the state rotates through four registers (the new X0 goes into
+// the old X3's register), so after four steps the mapping is back in place;
+// one asm block runs four steps and the compiler's pad after an asm block is
+// paid once per four rounds.
+#define RF_LAG_STEP(x0, x1, x2, x3, z, zn, k)                                              \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t"                                 \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t"                                 \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t"                                 \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                        \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                               \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                       \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[" k "]\n\t"                                    \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"                                      \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+
+#define RF_LAG_GROUP                                        \
+    RF_LAG_STEP("a", "b", "c", "d", "z", "y", "k1")         \
+    RF_LAG_STEP("d", "a", "b", "c", "y", "z", "k2")         \
+    RF_LAG_STEP("c", "d", "a", "b", "z", "y", "k3")         \
+    RF_LAG_STEP("b", "c", "d", "a", "y", "z", "k4")
+
+// X += H then H = X on the lanes of one half (bank mask 0x3 = e-lanes,
+// 0xc = a-lanes); DPP identity only for the bank mask.
+#define RF_LAG_FF(bm, x0, x1, x2, x3)                                                                 \
+    "v_add_u32_dpp %[" x0 "], %[h0], %[" x0 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t" \
+    "v_add_u32_dpp %[" x1 "], %[h1], %[" x1 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t" \
+    "v_add_u32_dpp %[" x2 "], %[h2], %[" x2 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t" \
+    "v_add_u32_dpp %[" x3 "], %[h3], %[" x3 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t" \
+    "v_mov_b32_dpp %[h0], %[" x0 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"            \
+    "v_mov_b32_dpp %[h1], %[" x1 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"            \
+    "v_mov_b32_dpp %[h2], %[" x2 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"            \
+    "v_mov_b32_dpp %[h3], %[" x3 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"
+
+// H += X on one half (final feed-forward; X stays as it is)
+#define RF_LAG_FIN(bm, x0, x1, x2, x3)                                                                \
+    "v_add_u32_dpp %[h0], %[h0], %[" x0 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"     \
+    "v_add_u32_dpp %[h1], %[h1], %[" x1 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"     \
+    "v_add_u32_dpp %[h2], %[h2], %[" x2 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"     \
+    "v_add_u32_dpp %[h3], %[h3], %[" x3 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"
+
+#define RF_LAG_STATE [a] "+v"(Pa), [b] "+v"(Pb), [c] "+v"(Pc), [d] "+v"(Pd), [z] "+v"(Z), [y] "+v"(Y)
+#define RF_LAG_TMP [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+#define RF_LAG_H [h0] "+v"(Hr0), [h1] "+v"(Hr1), [h2] "+v"(Hr2), [h3] "+v"(Hr3)
+#define RF_LAG_IN(k1v, k2v, k3v, k4v) \
+    [s1] "v"(sh1), [s2] "v"(sh2), [s3] "v"(sh3), [m] "v"(M), [k1] "v"(k1v), [k2] "v"(k2v), [k3] "v"(k3v), [k4] "v"(k4v)
+
+namespace lag {
+constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                            0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+}  // namespace lag
+
+// Block-boundary corrections for the next boundary, from this block's
+// chaining value H (both halves have applied it by the end of group 0):
+//   c63: Z of the e-lanes' next round 0 = h + d + (K+W added at block start)
+//        e: H7 + H3     a: 1
+//   c64: e: + H2 (the partner's d is not fed forward yet)   a: - H4
+//   c65: e: + H1                                            a: - H3
+// (v_subrev_u32_dpp does not permute the operand one would expect; the
+// negation goes through a temporary and a plain DPP move, t0 being free after
+// the group's last step.)
+#define RF_LAG_CORR                                                                          \
+    "v_sub_u32 %[t0], %[zero], %[h0]\n\t"                                                    \
+    "v_add_u32_dpp %[c63], %[h3], %[h3] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"            \
+    "v_mov_b32_dpp %[c63], %[one] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n\t"        \
+    "v_mov_b32_dpp %[c64], %[h2] row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                   \
+    "v_mov_b32_dpp %[c64], %[t0] row_ror:8 row_mask:0xf bank_mask:0xc\n\t"                   \
+    "v_mov_b32_dpp %[c65], %[h1] row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                   \
+    "v_sub_u32_dpp %[c65], %[zero], %[h3] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n\t"
 
 __global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
     __builtin_amdgcn_s_setprio(3);
-    __shared__ __attribute__((aligned(16))) uint32_t kw[64 * kRow];
+    // 64 K+W rows, then the a-lanes' k row: word 0 = 0 (block-start add),
+    // the rest 1 (Zt = -c)
+    __shared__ __attribute__((aligned(16))) uint32_t kw[65 * kRow];
     constexpr uint32_t K[64] = RF_SHA_K;
     const uint32_t lane = threadIdx.x;
+    uint32_t* const ones = &kw[64 * kRow];
+    ones[lane] = lane ? 1u : 0u;
+    if (lane < 4) ones[64 + lane] = 1u;
     const bool elane = (lane & 8) == 0;
     const uint32_t sh1 = elane ? 6 : 2, sh2 = elane ? 11 : 13, sh3 = elane ? 25 : 22;
     const uint32_t M = elane ? 0u : ~0u;
+    const uint32_t one = 1u, zero = 0u;
     for (uint32_t q = blockIdx.x; q < a.n_order; q += gridDim.x) {
         const uint32_t id = a.order[q];
         const uint8_t* p = a.arena + a.offs[id];
         const uint64_t len = a.lens[id];
         const uint64_t nb = sha256_nblocks(len);
-        // e-lanes: H4..H7, a-lanes: H0..H3
-        uint32_t H0 = elane ? 0x510e527fu : 0x6a09e667u, H1 = elane ? 0x9b05688cu : 0xbb67ae85u;
-        uint32_t H2 = elane ? 0x1f83d9abu : 0x3c6ef372u, H3 = elane ? 0x5be0cd19u : 0xa54ff53au;
+        // Start as if after a block whose raw final state is zero with
+        // chaining value IV: the feed-forward of block 0's group 0 then
+        // produces the IV state and the corrections below are the general
+        // ones for H = IV.
+        uint32_t Hr0 = elane ? lag::IV[4] : lag::IV[0], Hr1 = elane ? lag::IV[5] : lag::IV[1];
+        uint32_t Hr2 = elane ? lag::IV[6] : lag::IV[2], Hr3 = elane ? lag::IV[7] : lag::IV[3];
+        uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
+        uint32_t Z = elane ? lag::IV[7] + lag::IV[3] : 0u, Y = 0;
+        uint32_t c63 = 0;
+        uint32_t c64 = elane ? lag::IV[2] : 0u - lag::IV[4];
+        uint32_t c65 = elane ? lag::IV[1] : 0u - lag::IV[3];
+        uint32_t t0, t1, t2, t3;
+        __syncthreads();
         for (uint64_t c = 0; c < nb; c += 64) {
             const uint64_t b = c + lane;
             if (b < nb) {
@@ -267,38 +347,62 @@ __global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
             }
             __syncthreads();
             const uint32_t cnt = (uint32_t)((nb - c) < 64 ? (nb - c) : 64);
+            // e-lanes read row j, a-lanes the ones row: a bit-select of byte
+            // offsets (no per-lane branch)
+            const uint32_t ones_off = 64 * kRow * 4;
+            const uint4* r4 = reinterpret_cast<const uint4*>(
+                reinterpret_cast<const char*>(kw) + (M & ones_off));
+            uint4 v = r4[0], vn = r4[1];
             for (uint32_t j = 0; j < cnt; ++j) {
-                const uint4* r4 = reinterpret_cast<const uint4*>(&kw[j * kRow]);
-                uint32_t X0 = H0, X1 = H1, X2 = H2, X3 = H3;
-                uint4 v = r4[0], vn = r4[1];
-                uint32_t Z = elane ? X3 + v.x : 0u;
+                // the next row (clamped at the chunk end; its values are then
+                // not used) -- its first 32 B are read during groups 14-15
+                const uint32_t nrow_off = (j + 1 < cnt ? j + 1 : j) * kRow * 4;
+                const uint4* r4n = reinterpret_cast<const uint4*>(
+                    reinterpret_cast<const char*>(kw) + ((M & ones_off) | (~M & nrow_off)));
+                uint4 vnn = r4[2];
+                {
+                    // e-lanes enter the block at step 0, a-lanes at step 2
+                    const uint32_t k1 = v.y + c64, k2 = v.z + c65;
+                    asm volatile("s_nop 1\n\t" RF_LAG_FF("0x3", "a", "b", "c", "d")
+                                 "v_add_u32 %[z], %[z], %[kw0]\n\t"
+                                 RF_LAG_STEP("a", "b", "c", "d", "z", "y", "k1")
+                                 RF_LAG_STEP("d", "a", "b", "c", "y", "z", "k2")
+                                 RF_LAG_FF("0xc", "c", "d", "a", "b")
+                                 RF_LAG_STEP("c", "d", "a", "b", "z", "y", "k3")
+                                 RF_LAG_STEP("b", "c", "d", "a", "y", "z", "k4")
+                                 RF_LAG_CORR
+                                 : RF_LAG_STATE, RF_LAG_TMP, RF_LAG_H,
+                                   [c63] "=&v"(c63), [c64] "+v"(c64), [c65] "+v"(c65)
+                                 : RF_LAG_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one),
+                                   [zero] "v"(zero));
+                }
+                v = vn;
+                vn = vnn;
 #pragma unroll
-                for (int t4 = 0; t4 < 16; ++t4) {
+                for (int g = 1; g < 16; ++g) {
                     // LDS reads run two groups ahead of the chain
-                    const uint4 vnn = t4 < 14 ? r4[t4 + 2] : make_uint4(0, 0, 0, 0);
-                    uint32_t t0, t1, t2;
-                    // Four rounds per asm block: the state rotates through the
-                    // four registers and is back in place after four rounds, so
-                    // the compiler's pad after an asm block is paid once per 4.
-                    asm volatile(RF_DUO_ROUND("a", "b", "c", "d", "k1")
-                                 RF_DUO_ROUND("d", "a", "b", "c", "k2")
-                                 RF_DUO_ROUND("c", "d", "a", "b", "k3")
-                                 RF_DUO_ROUND("b", "c", "d", "a", "k4")
-                                 : [a] "+v"(X0), [b] "+v"(X1), [c] "+v"(X2), [d] "+v"(X3),
-                                   [z] "+v"(Z), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
-                                 : [s1] "v"(sh1), [s2] "v"(sh2), [s3] "v"(sh3), [m] "v"(M),
-                                   [k1] "v"(v.y), [k2] "v"(v.z), [k3] "v"(v.w), [k4] "v"(vn.x));
+                    vnn = g < 14 ? r4[g + 2] : r4n[g - 14];
+                    const uint32_t k4 = g == 15 ? c63 : vn.x;
+                    asm volatile(RF_LAG_GROUP : RF_LAG_STATE, RF_LAG_TMP : RF_LAG_IN(v.y, v.z, v.w, k4));
                     v = vn;
                     vn = vnn;
                 }
-                H0 += X0; H1 += X1; H2 += X2; H3 += X3;
+                r4 = r4n;
             }
             __syncthreads();
         }
+        // tail: the e-lanes are done (H += X, X untouched so the a-lanes' last
+        // Z reads raw e(64)); the a-lanes run rounds 62 and 63, then H += X.
+        asm volatile("s_nop 1\n\t" RF_LAG_FIN("0x3", "a", "b", "c", "d")
+                     RF_LAG_STEP("a", "b", "c", "d", "z", "y", "k1")
+                     RF_LAG_STEP("d", "a", "b", "c", "y", "z", "k2")
+                     RF_LAG_FIN("0xc", "c", "d", "a", "b")
+                     : RF_LAG_STATE, RF_LAG_TMP, RF_LAG_H
+                     : RF_LAG_IN(one, one, one, one));
         // lane 8 (a-lane) holds H0..H3, lane 0 (e-lane) H4..H7
         if (lane == 0 || lane == 8) {
             uint4 o;
-            o.x = bswap32(H0); o.y = bswap32(H1); o.z = bswap32(H2); o.w = bswap32(H3);
+            o.x = bswap32(Hr0); o.y = bswap32(Hr1); o.z = bswap32(Hr2); o.w = bswap32(Hr3);
             reinterpret_cast<uint4*>(a.out + 32ull * id)[lane == 0 ? 1 : 0] = o;
         }
     }

@@ -127,6 +127,9 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
     const uint32_t c = blockIdx.x | 1, s1 = threadIdx.x & 8 ? 2 : 6, s2 = threadIdx.x & 8 ? 13 : 11,
                    s3 = threadIdx.x & 8 ? 22 : 25, m = threadIdx.x & 8 ? ~0u : 0u;
     uint32_t t0, t1, t2, t3 = 0, zy = r;
+    uint32_t q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = r + j;
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
     for (uint32_t i = 0; i < iters; ++i) {
 #pragma unroll
@@ -161,6 +164,35 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
                              : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
                                [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
                              : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if constexpr (OP >= 11 && OP <= 17) {
+                if (j == 0) {
+#define I8(ins) ins("0") ins("1") ins("2") ins("3") ins("4") ins("5") ins("6") ins("7")
+#define IALIGN(n) "v_alignbit_b32 %[r" n "], %[r" n "], %[r" n "], 7\n\t"
+#define IADD(n) "v_add_u32 %[r" n "], %[r" n "], %[c]\n\t"
+#define IBOP(n) "v_bitop3_b32 %[r" n "], %[r" n "], %[c], %[e] bitop3:0x96\n\t"
+#define IDPP(n) "v_add_u32_dpp %[r" n "], %[c], %[r" n "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+#define IBOPS(n) "v_bitop3_b32 %[r" n "], %[r" n "], %[r" n "], %[c] bitop3:0x96\n\t"
+#define R8 [r0] "+v"(q[0]), [r1] "+v"(q[1]), [r2] "+v"(q[2]), [r3] "+v"(q[3]), [r4] "+v"(q[4]), \
+           [r5] "+v"(q[5]), [r6] "+v"(q[6]), [r7] "+v"(q[7])
+                    if constexpr (OP == 11) asm volatile(I8(IALIGN) : R8);
+                    if constexpr (OP == 12) asm volatile(I8(IADD) : R8 : [c] "v"(c));
+                    if constexpr (OP == 13) asm volatile(I8(IBOP) : R8 : [c] "v"(c), [e] "v"(s1));
+                    if constexpr (OP == 14) asm volatile(I8(IDPP) : R8 : [c] "v"(c));
+                    if constexpr (OP == 15) asm volatile(I8(IBOPS) : R8 : [c] "v"(c));
+                    // explicit registers: c in bank 1, e in bank 2, r in banks 0/3 (16)
+                    // or r in bank 1 with c (17)
+                    if constexpr (OP == 16)
+                        asm volatile(I8(IBOP) : [r0] "+{v40}"(q[0]), [r1] "+{v43}"(q[1]), [r2] "+{v44}"(q[2]),
+                                     [r3] "+{v47}"(q[3]), [r4] "+{v48}"(q[4]), [r5] "+{v51}"(q[5]),
+                                     [r6] "+{v52}"(q[6]), [r7] "+{v55}"(q[7])
+                                     : [c] "{v61}"(c), [e] "{v62}"(s1));
+                    if constexpr (OP == 17)
+                        asm volatile(I8(IBOP) : [r0] "+{v41}"(q[0]), [r1] "+{v45}"(q[1]), [r2] "+{v49}"(q[2]),
+                                     [r3] "+{v53}"(q[3]), [r4] "+{v57}"(q[4]), [r5] "+{v65}"(q[5]),
+                                     [r6] "+{v69}"(q[6]), [r7] "+{v73}"(q[7])
+                                     : [c] "{v61}"(c), [e] "{v62}"(s1));
+                }
+            }
             if (OP == 10 && (j & 3) == 0)
                 asm volatile(LAG2("a", "b", "c", "d", "z", "y") LAG2("d", "a", "b", "c", "y", "z")
                              LAG2("c", "d", "a", "b", "z", "y") LAG2("b", "c", "d", "a", "y", "z")
@@ -170,7 +202,7 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
         }
     }
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
-    out[threadIdx.x] = r ^ x1 ^ x2 ^ x3 ^ z ^ t0 ^ zy ^ t3;
+    out[threadIdx.x] = r ^ x1 ^ x2 ^ x3 ^ z ^ t0 ^ zy ^ t3 ^ q[0] ^ q[1] ^ q[2] ^ q[3] ^ q[4] ^ q[5] ^ q[6] ^ q[7];
     if (threadIdx.x == 0) *cyc = c1 - c0;
 }
 
@@ -178,7 +210,7 @@ struct LtArgs { int op; uint32_t iters; uint32_t* out; uint64_t* cyc; };
 static void run_lat(void* p) {
     auto* a = (LtArgs*)p;
 #define RF_LAT(N) case N: hipLaunchKernelGGL(k_lat<N>, dim3(1), dim3(64), 0, 0, a->iters, a->out, a->cyc); break;
-    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) default: RF_LAT(10) }
+    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) RF_LAT(10) RF_LAT(11) RF_LAT(12) RF_LAT(13) RF_LAT(14) RF_LAT(15) RF_LAT(16) default: RF_LAT(17) }
 #undef RF_LAT
 }
 
