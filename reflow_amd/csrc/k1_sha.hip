@@ -141,10 +141,31 @@ __global__ __launch_bounds__(kLanesBlock) void k1_sha256_lanes(LanesArgs a) {
 // row with wave-uniform (broadcast) ds_read_b128.
 constexpr uint32_t kRow = 68;
 
+// Lane l of a wave writes row l = K[t] + W_t of block c + l (if it exists).
+__device__ __forceinline__ void fill_kw_rows(uint32_t* kw, const uint8_t* p, uint64_t len, uint64_t nb,
+                                             uint64_t c, uint32_t lane) {
+    constexpr uint32_t K[64] = RF_SHA_K;
+    const uint64_t b = c + lane;
+    if (b >= nb) return;
+    uint32_t w[16];
+    load_block(w, p, len, b);
+    uint32_t* row = &kw[lane * kRow];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+            w[t & 15] = wt;
+        }
+        row[t] = K[t] + wt;
+    }
+}
+
 __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ __attribute__((aligned(16))) uint32_t kw[64 * kRow];
-    constexpr uint32_t K[64] = RF_SHA_K;
     const uint32_t lane = threadIdx.x;
     for (uint32_t q = blockIdx.x; q < a.n_order; q += gridDim.x) {
         const uint32_t id = a.order[q];
@@ -154,24 +175,7 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
         ShaState st;
         st.init();
         for (uint64_t c = 0; c < nb; c += 64) {
-            const uint64_t b = c + lane;
-            if (b < nb) {
-                uint32_t w[16];
-                load_block(w, p, len, b);
-                uint32_t* row = &kw[lane * kRow];
-#pragma unroll
-                for (int t = 0; t < 64; ++t) {
-                    uint32_t wt;
-                    if (t < 16) {
-                        wt = w[t];
-                    } else {
-                        wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) +
-                             w[t & 15];
-                        w[t & 15] = wt;
-                    }
-                    row[t] = K[t] + wt;
-                }
-            }
+            fill_kw_rows(kw, p, len, nb, c, lane);
             __syncthreads();
             const uint32_t cnt = (uint32_t)((nb - c) < 64 ? (nb - c) : 64);
             for (uint32_t j = 0; j < cnt; ++j) {
@@ -294,16 +298,23 @@ constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
     "v_mov_b32_dpp %[c65], %[h1] row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                   \
     "v_sub_u32_dpp %[c65], %[zero], %[h3] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n\t"
 
-__global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
-    __builtin_amdgcn_s_setprio(3);
-    // 64 K+W rows, then the a-lanes' k row: word 0 = 0 (block-start add),
-    // the rest 1 (Zt = -c)
-    __shared__ __attribute__((aligned(16))) uint32_t kw[65 * kRow];
-    constexpr uint32_t K[64] = RF_SHA_K;
-    const uint32_t lane = threadIdx.x;
-    uint32_t* const ones = &kw[64 * kRow];
-    ones[lane] = lane ? 1u : 0u;
-    if (lane < 4) ones[64 + lane] = 1u;
+// Two waves: wave 0 runs the chain, wave 1 expands the next 64 blocks'
+// K+W rows into the other half of a double buffer meanwhile (one barrier per
+// 64 blocks), so the chain never waits for HBM or the message schedule.
+__global__ __launch_bounds__(128) void k1_sha256_duo(SoloArgs a) {
+    // two buffers of 64 K+W rows, then the a-lanes' k row: word 0 = 0
+    // (block-start add), the rest 1 (Zt = -c)
+    __shared__ __attribute__((aligned(16))) uint32_t kw[129 * kRow];
+    // wave-uniform (SGPR) so the role branches below are scalar branches and
+    // each wave meets exactly one barrier per chunk
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t* const ones = &kw[128 * kRow];
+    if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        ones[lane] = lane ? 1u : 0u;
+        if (lane < 4) ones[64 + lane] = 1u;
+    }
     const bool elane = (lane & 8) == 0;
     const uint32_t sh1 = elane ? 6 : 2, sh2 = elane ? 11 : 13, sh3 = elane ? 25 : 22;
     const uint32_t M = elane ? 0u : ~0u;
@@ -325,38 +336,24 @@ __global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
         uint32_t c64 = elane ? lag::IV[2] : 0u - lag::IV[4];
         uint32_t c65 = elane ? lag::IV[1] : 0u - lag::IV[3];
         uint32_t t0, t1, t2, t3;
+        if (wave == 1) fill_kw_rows(kw, p, len, nb, 0, lane);
         __syncthreads();
-        for (uint64_t c = 0; c < nb; c += 64) {
-            const uint64_t b = c + lane;
-            if (b < nb) {
-                uint32_t w[16];
-                load_block(w, p, len, b);
-                uint32_t* row = &kw[lane * kRow];
-#pragma unroll
-                for (int t = 0; t < 64; ++t) {
-                    uint32_t wt;
-                    if (t < 16) {
-                        wt = w[t];
-                    } else {
-                        wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) +
-                             w[t & 15];
-                        w[t & 15] = wt;
-                    }
-                    row[t] = K[t] + wt;
-                }
-            }
-            __syncthreads();
+        uint32_t buf = 0;
+        for (uint64_t c = 0; c < nb; c += 64, buf ^= 1) {
+            if (wave == 1) {
+                if (c + 64 < nb) fill_kw_rows(&kw[(buf ^ 1) * 64 * kRow], p, len, nb, c + 64, lane);
+            } else {
             const uint32_t cnt = (uint32_t)((nb - c) < 64 ? (nb - c) : 64);
-            // e-lanes read row j, a-lanes the ones row: a bit-select of byte
-            // offsets (no per-lane branch)
-            const uint32_t ones_off = 64 * kRow * 4;
+            // e-lanes read row j of this buffer, a-lanes the ones row: a
+            // bit-select of byte offsets (no per-lane branch)
+            const uint32_t ones_off = 128 * kRow * 4, buf_off = buf * 64 * kRow * 4;
             const uint4* r4 = reinterpret_cast<const uint4*>(
-                reinterpret_cast<const char*>(kw) + (M & ones_off));
+                reinterpret_cast<const char*>(kw) + ((M & ones_off) | (~M & buf_off)));
             uint4 v = r4[0], vn = r4[1];
             for (uint32_t j = 0; j < cnt; ++j) {
                 // the next row (clamped at the chunk end; its values are then
                 // not used) -- its first 32 B are read during groups 14-15
-                const uint32_t nrow_off = (j + 1 < cnt ? j + 1 : j) * kRow * 4;
+                const uint32_t nrow_off = buf_off + (j + 1 < cnt ? j + 1 : j) * kRow * 4;
                 const uint4* r4n = reinterpret_cast<const uint4*>(
                     reinterpret_cast<const char*>(kw) + ((M & ones_off) | (~M & nrow_off)));
                 uint4 vnn = r4[2];
@@ -389,8 +386,10 @@ __global__ __launch_bounds__(64) void k1_sha256_duo(SoloArgs a) {
                 }
                 r4 = r4n;
             }
+            }
             __syncthreads();
         }
+        if (wave == 1) continue;
         // tail: the e-lanes are done (H += X, X untouched so the a-lanes' last
         // Z reads raw e(64)); the a-lanes run rounds 62 and 63, then H += X.
         asm volatile("s_nop 1\n\t" RF_LAG_FIN("0x3", "a", "b", "c", "d")
@@ -473,7 +472,7 @@ hipError_t launch_sha_lanes(const LanesArgs& a, uint32_t grid, hipStream_t s) {
 hipError_t launch_sha_solo(const SoloArgs& a, bool duo, hipStream_t s) {
     if (a.n_order == 0) return hipSuccess;
     if (duo)
-        hipLaunchKernelGGL(k1_sha256_duo, dim3(a.n_order), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k1_sha256_duo, dim3(a.n_order), dim3(128), 0, s, a);
     else
         hipLaunchKernelGGL(k1_sha256_solo, dim3(a.n_order), dim3(64), 0, s, a);
     return hipGetLastError();
