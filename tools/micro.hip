@@ -118,6 +118,76 @@ __global__ __launch_bounds__(256) void k_op(uint32_t iters, uint32_t* out) {
     "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"                               \
     "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
 
+// orderings of the lag-2 step (OP 18..22)
+#define LAGV1(x0, x1, x2, x3, z, zn) \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t" \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t" \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t" \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[k]\n\t" \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t" \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t" \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"
+
+#define LAGV5(x0, x1, x2, x3, z, zn) \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[k]\n\t" \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t" \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t" \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t" \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t" \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t" \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"
+
+#define LAGV6(x0, x1, x2, x3, z, zn) \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[k]\n\t" \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t" \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t" \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t" \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t" \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t" \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"
+
+#define LAGV7(x0, x1, x2, x3, z, zn) \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[k]\n\t" \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t" \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t" \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t" \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t" \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t" \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"
+
+#define LAGV8(x0, x1, x2, x3, z, zn) \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t" \
+    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t" \
+    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t" \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t" \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[k]\n\t" \
+    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t" \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t" \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t" \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"
+
+// issue cost per instruction type: 64 independent instructions (8 chains)
+#define ICOST23(n) "v_alignbit_b32 %[r" n "], %[r" n "], %[r" n "], %[c]\n\t"
+#define ICOST24(n) "v_alignbit_b32 %[r" n "], %[r" n "], %[r" n "], 7\n\t"
+#define ICOST25(n) "v_bitop3_b32 %[r" n "], %[r" n "], %[c], %[e] bitop3:0x96\n\t"
+#define ICOST26(n) "v_add3_u32 %[r" n "], %[r" n "], %[c], %[e]\n\t"
+#define ICOST27(n) "v_xad_u32 %[r" n "], %[r" n "], %[c], %[e]\n\t"
+#define ICOST28(n) "v_add_u32 %[r" n "], %[r" n "], %[c]\n\t"
+#define ICOST29(n) "v_add_u32_dpp %[r" n "], %[c], %[r" n "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+#define ICOST30(n) "v_xor_b32 %[r" n "], %[r" n "], %[c]\n\t"
+#define ICOST31(n) "v_add_u32_e64 %[r" n "], %[r" n "], %[c]\n\t"
+#define ICOST32(n) "v_lshl_add_u32 %[r" n "], %[r" n "], 3, %[c]\n\t"
+#define ICOST33(n) "v_add_u32 %[r" n "], %[r" n "], %[r" n "]\n\t"
+#define ICOST34(n) "v_bitop3_b32 %[r" n "], %[r" n "], %[r" n "], %[c] bitop3:0x96\n\t"
+#define ICOST35(n) "v_mov_b32 %[r" n "], %[c]\n\t"
 // D: single-wave latency: one dependent chain per lane (grid 1 x 64), so
 // the time per instruction is the issue-to-dependent-issue latency.  OP 8/9
 // run the duo round (10 instructions) with DPP / with plain adds.
@@ -193,6 +263,62 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
                                      : [c] "{v61}"(c), [e] "{v62}"(s1));
                 }
             }
+            if (OP == 18 && (j & 3) == 0)
+                asm volatile(LAGV1("a", "b", "c", "d", "z", "y") LAGV1("d", "a", "b", "c", "y", "z")
+                             LAGV1("c", "d", "a", "b", "z", "y") LAGV1("b", "c", "d", "a", "y", "z")
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [y] "+v"(zy), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if (OP == 19 && (j & 3) == 0)
+                asm volatile(LAGV5("a", "b", "c", "d", "z", "y") LAGV5("d", "a", "b", "c", "y", "z")
+                             LAGV5("c", "d", "a", "b", "z", "y") LAGV5("b", "c", "d", "a", "y", "z")
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [y] "+v"(zy), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if (OP == 20 && (j & 3) == 0)
+                asm volatile(LAGV6("a", "b", "c", "d", "z", "y") LAGV6("d", "a", "b", "c", "y", "z")
+                             LAGV6("c", "d", "a", "b", "z", "y") LAGV6("b", "c", "d", "a", "y", "z")
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [y] "+v"(zy), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if (OP == 21 && (j & 3) == 0)
+                asm volatile(LAGV7("a", "b", "c", "d", "z", "y") LAGV7("d", "a", "b", "c", "y", "z")
+                             LAGV7("c", "d", "a", "b", "z", "y") LAGV7("b", "c", "d", "a", "y", "z")
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [y] "+v"(zy), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if (OP == 22 && (j & 3) == 0)
+                asm volatile(LAGV8("a", "b", "c", "d", "z", "y") LAGV8("d", "a", "b", "c", "y", "z")
+                             LAGV8("c", "d", "a", "b", "z", "y") LAGV8("b", "c", "d", "a", "y", "z")
+                             : [a] "+v"(r), [b] "+v"(x1), [c] "+v"(x2), [d] "+v"(x3), [z] "+v"(z),
+                               [y] "+v"(zy), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+                             : [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [m] "v"(m), [k] "v"(c));
+            if constexpr (OP == 23)
+                if (j == 0) asm volatile(I8(ICOST23) I8(ICOST23) I8(ICOST23) I8(ICOST23) I8(ICOST23) I8(ICOST23) I8(ICOST23) I8(ICOST23) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 24)
+                if (j == 0) asm volatile(I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 25)
+                if (j == 0) asm volatile(I8(ICOST25) I8(ICOST25) I8(ICOST25) I8(ICOST25) I8(ICOST25) I8(ICOST25) I8(ICOST25) I8(ICOST25) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 26)
+                if (j == 0) asm volatile(I8(ICOST26) I8(ICOST26) I8(ICOST26) I8(ICOST26) I8(ICOST26) I8(ICOST26) I8(ICOST26) I8(ICOST26) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 27)
+                if (j == 0) asm volatile(I8(ICOST27) I8(ICOST27) I8(ICOST27) I8(ICOST27) I8(ICOST27) I8(ICOST27) I8(ICOST27) I8(ICOST27) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 28)
+                if (j == 0) asm volatile(I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 29)
+                if (j == 0) asm volatile(I8(ICOST29) I8(ICOST29) I8(ICOST29) I8(ICOST29) I8(ICOST29) I8(ICOST29) I8(ICOST29) I8(ICOST29) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 30)
+                if (j == 0) asm volatile(I8(ICOST30) I8(ICOST30) I8(ICOST30) I8(ICOST30) I8(ICOST30) I8(ICOST30) I8(ICOST30) I8(ICOST30) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 31)
+                if (j == 0) asm volatile(I8(ICOST31) I8(ICOST31) I8(ICOST31) I8(ICOST31) I8(ICOST31) I8(ICOST31) I8(ICOST31) I8(ICOST31) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 32)
+                if (j == 0) asm volatile(I8(ICOST32) I8(ICOST32) I8(ICOST32) I8(ICOST32) I8(ICOST32) I8(ICOST32) I8(ICOST32) I8(ICOST32) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 33)
+                if (j == 0) asm volatile(I8(ICOST33) I8(ICOST33) I8(ICOST33) I8(ICOST33) I8(ICOST33) I8(ICOST33) I8(ICOST33) I8(ICOST33) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 34)
+                if (j == 0) asm volatile(I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 35)
+                if (j == 0) asm volatile(I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) : R8 : [c] "v"(c), [e] "v"(s1));
             if (OP == 10 && (j & 3) == 0)
                 asm volatile(LAG2("a", "b", "c", "d", "z", "y") LAG2("d", "a", "b", "c", "y", "z")
                              LAG2("c", "d", "a", "b", "z", "y") LAG2("b", "c", "d", "a", "y", "z")
@@ -210,7 +336,7 @@ struct LtArgs { int op; uint32_t iters; uint32_t* out; uint64_t* cyc; };
 static void run_lat(void* p) {
     auto* a = (LtArgs*)p;
 #define RF_LAT(N) case N: hipLaunchKernelGGL(k_lat<N>, dim3(1), dim3(64), 0, 0, a->iters, a->out, a->cyc); break;
-    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) RF_LAT(10) RF_LAT(11) RF_LAT(12) RF_LAT(13) RF_LAT(14) RF_LAT(15) RF_LAT(16) default: RF_LAT(17) }
+    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) RF_LAT(10) RF_LAT(11) RF_LAT(12) RF_LAT(13) RF_LAT(14) RF_LAT(15) RF_LAT(16) RF_LAT(17) RF_LAT(18) RF_LAT(19) RF_LAT(20) RF_LAT(21) RF_LAT(22) RF_LAT(23) RF_LAT(24) RF_LAT(25) RF_LAT(26) RF_LAT(27) RF_LAT(28) RF_LAT(29) RF_LAT(30) RF_LAT(31) RF_LAT(32) RF_LAT(33) RF_LAT(34) default: RF_LAT(35) }
 #undef RF_LAT
 }
 
