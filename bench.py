@@ -41,8 +41,12 @@ N_CU = 256
 VALU_LANE_OPS = N_CU * 4 * 32 * CLOCK_HZ      # int32 VALU lane-ops/s (= FP32 FMA rate)
 SHA_OPS_PER_BLOCK = 1464                        # canonical ops per 64-B block
 SHA_VALU_PEAK_GBS = VALU_LANE_OPS / SHA_OPS_PER_BLOCK * 64 / 1e9
-CHAIN_INSTR_PER_BLOCK = 64 * 11                 # two-lane round: 11 VALU issue slots
-WAVE_ISSUE_CYCLES = 4                           # one wave alone: 1 VALU / 4 cycles
+# A message's blocks are a serial chain (Merkle-Damgard).  One round's critical
+# path is 3 dependent VALU ops (rotate -> xor3 -> add3 into e/a); the
+# dependent-issue latency of one wave is 4 cycles (MI355X_MICROARCH.md,
+# "Dependent-chain latency"; tools/micro.py lat: 4-5).  So no implementation
+# can finish a message of B blocks in less than B * 64 * 3 * 4 cycles.
+CHAIN_CYCLES_PER_BLOCK = 64 * 3 * 4
 HBM_PEAK_GBS = 8000.0
 
 
@@ -167,8 +171,9 @@ def bench_sha(args, dist, ctx):
     dom_ms = float(np.mean(solo_ms if wave_mode else lanes_ms))
     dom_bytes = float(lens[ids].sum())
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    # skew-aware floor: the longest serial chain vs chip VALU throughput
-    t_chain = float(nblk[ids].max()) * CHAIN_INSTR_PER_BLOCK * WAVE_ISSUE_CYCLES / CLOCK_HZ
+    # skew-aware floor: the longest serial chain (critical-path latency) vs
+    # chip VALU throughput
+    t_chain = float(nblk[ids].max()) * CHAIN_CYCLES_PER_BLOCK / CLOCK_HZ
     t_valu = float(nblk[ids].sum()) * SHA_OPS_PER_BLOCK / VALU_LANE_OPS
     t_floor = max(t_chain, t_valu)
     peak = dom_bytes / t_floor / 1e9
@@ -177,8 +182,9 @@ def bench_sha(args, dist, ctx):
             "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": traffic,
             "traffic_source": tsrc, "traffic_over_algorithmic": (round(traffic / dom_bytes, 3)
                                                                  if traffic else None),
-            "peak_kind": "skew-aware: max(longest message chain at 11 VALU/round x 4 cyc/issue @2.4GHz,"
-                         " sum blocks x 1464 ops / INT32 VALU peak)",
+            "peak_kind": "skew-aware floor: max(longest message's blocks x 64 rounds x 3 dependent VALU"
+                         " x 4 cyc @2.4GHz (round critical path), sum blocks x 1464 ops / INT32 VALU peak)",
+            "floor_s": round(t_floor, 3), "chain_floor_s": round(t_chain, 3),
             "valu_peak_GBps": round(SHA_VALU_PEAK_GBS, 1),
             "frac_of_valu_peak": round(achieved / SHA_VALU_PEAK_GBS, 6),
             "launch_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes,
@@ -294,6 +300,14 @@ def bench_probe(args, dist, ctx):
     bpp = 32 + 8 * k + 1
     ach = n_probe * bpp / (dev_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic("k4_bloom_probe")
+    # Words one launch fetches: a present key (or a false positive) all k; an
+    # absent key stops at its first clear bit, so with a fraction f of the
+    # filter's bits set it fetches sum_{j<k} f^j on average.
+    f = float(np.bitwise_count(b.words()).sum()) / m
+    absent = n_probe - hits
+    reads = hits * k + absent * sum(f ** j for j in range(k))
+    gread_s = reads / (dev_ms * 1e-3) / 1e9
+    ceil = gather_ceiling(m // 8, n_probe // 4, k)
     res = {"workload": "bloomlive probe: n=%d keys (m=%d bits, %.1f MiB, k=%d), %d probes (50%% present)"
                        % (n_ins, m, m / 8 / 2**20, k, n_probe),
            "gprobes_per_s": dist.sum(n_probe) * args.probe_steps / t / 1e9,
@@ -301,15 +315,47 @@ def bench_probe(args, dist, ctx):
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_probe": bpp,
                         "traffic": traffic, "traffic_source": tsrc,
-                        "note": "filter fits the 256 MiB Infinity Cache at n=1e8; each random 8-B "
-                                "word read moves a 64-B line (traffic/launch ~ 5.7x algorithmic)"}}
+                        "note": "algorithmic bytes; each random 8-B word read moves a 64-B line, so the "
+                                "real bound is the random-gather rate (roofline_gather)"},
+           "roofline_gather": {"bound": "random 8-B gathers", "achieved": round(gread_s, 2),
+                               "peak": round(ceil, 2) if ceil else None, "unit": "G words/s",
+                               "frac": round(gread_s / ceil, 4) if ceil else None,
+                               "words_per_probe": round(reads / n_probe, 3), "filter_fill": round(f, 4),
+                               "peak_kind": "measured live: tools/micro.hip k_gather, k independent "
+                                            "random 8-B reads per thread over a table of the filter's size"}}
     for x in (keys, out, d_offs, d_lens):
         x.free()
     b.close()
     return res
 
 
+def gather_ceiling(table_bytes, n_threads, reads):
+    """Random 8-B gather rate (G words/s) of this GPU over a table of
+    `table_bytes`, from the diagnostic kernel in tools/_micro.so (built by
+    __graft_entry__.build()); None when that library is absent."""
+    import ctypes
+    so = os.path.join(ROOT, "tools", "_micro.so")
+    if not os.path.exists(so):
+        return None
+    L = ctypes.CDLL(so)
+    L.micro_gather.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+    L.micro_gather.restype = ctypes.c_float
+    r = 10 if reads >= 10 else 6 if reads >= 6 else 2
+    ms = L.micro_gather(int(table_bytes), int(n_threads), r, 1)
+    return n_threads * r / (ms * 1e-3) / 1e9 if ms > 0 else None
+
+
 # ----------------------------------------------------------- CPU baseline --
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(args, sha, dag):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
@@ -342,8 +388,27 @@ def cpu_baseline(args, sha, dag):
            "sample": "first %d files (%.2f GiB, largest %.2f GiB) of the same C2 set, oracle/oracle.c "
                      "scalar SHA-256, %d pthreads, largest-first" % (n, s_lens.sum() / GiB,
                                                                     s_lens.max() / GiB, threads),
-           "seconds": dt, "gpu_digests_match": match}
-    del arena
+           "seconds": dt, "gpu_digests_match": match, "cpu_model": cpu_model()}
+    # The same sample through OpenSSL's SHA-256 (hashlib; SHA-NI where the CPU
+    # has it -- what Go >= 1.21's crypto/sha256 uses), same threads, LPT order.
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    mv = memoryview(arena)
+
+    def one(i):
+        o, ln = int(s_offs[i]), int(s_lens[i])
+        return hashlib.sha256(mv[o:o + ln]).digest()
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        dig = list(ex.map(one, order.astype(np.int64).tolist()))
+    dt2 = time.perf_counter() - t0
+    ok2 = all(d == sha["_digests"][int(i)].tobytes() for d, i in zip(dig, order.astype(np.int64)))
+    res["openssl"] = {"value": float(s_lens.sum()) / dt2 / 1e9, "unit": "GB/s", "cores": threads,
+                      "kind": "library", "sample": "same files, hashlib/OpenSSL SHA-256, %d threads" % threads,
+                      "seconds": dt2, "gpu_digests_match": ok2,
+                      "sha_ni": "sha_ni" in open("/proc/cpuinfo").read()}
+    del mv, arena
     # C3 port: full recompute of a bounded sample DAG, 1 thread (Canonicalize is serial)
     if dag is not None:
         small = Dag1000(max(1, args.cpu_dag_samples), dag.P)
@@ -379,7 +444,7 @@ def main():
     ap.add_argument("--probe-keys", type=int, default=100_000_000)
     ap.add_argument("--probes", type=int, default=1_000_000_000)
     ap.add_argument("--probe-steps", type=int, default=3)
-    ap.add_argument("--cpu-sample-gib", type=float, default=8.0)
+    ap.add_argument("--cpu-sample-gib", type=float, default=20.0)
     ap.add_argument("--cpu-dag-samples", type=int, default=200)
     ap.add_argument("--skip", default="", help="comma list of: dag,probe,cpu")
     args = ap.parse_args()

@@ -10,9 +10,7 @@
 // Key = WD(d) = 00 05 || d (34 bytes).  (h1,h2) = mm3(key), (h3,h4) =
 // mm3(key || 0x01): both share the two 16-byte body blocks, so the body is
 // mixed once and finalised twice.  loc_i = (h[i%2] + i*h[2+((i+i%2)%4)/2])
-// mod m with an exact 64-bit Barrett reduction.  One lane per probe; all k
-// filter words are requested before any is tested (memory-level parallelism
-// instead of the reference's early exit).
+// mod m with an exact 64-bit Barrett reduction.  One lane per probe.
 #include "engine.h"
 
 namespace rf {
@@ -83,8 +81,13 @@ __device__ __forceinline__ void load_digest64(const uint8_t* d, uint64_t (&D)[4]
     D[0] = a.x; D[1] = a.y; D[2] = b.x; D[3] = b.y;
 }
 
-constexpr uint32_t kKMax = 16;
 
+// Fetch schedule: the k words are requested C at a time, and a key stops at
+// the first chunk that holds a clear bit (bloom.Test's early exit, batched for
+// memory-level parallelism).  The probe is bound by random 8-B gathers (one
+// 64-B line each, ~55 G/s on MI355X, tools/micro.py gather), so the fewer
+// words an absent key fetches, the faster; a present key always fetches k.
+template <int C>
 __global__ __launch_bounds__(256) void k4_bloom_probe(const uint64_t* __restrict__ words,
                                                       const uint64_t* __restrict__ len_dev,
                                                       uint64_t m, uint64_t mu, uint32_t k,
@@ -97,34 +100,18 @@ __global__ __launch_bounds__(256) void k4_bloom_probe(const uint64_t* __restrict
         load_digest64(d32 + 32 * i, D);
         base_hashes_wd(D, h);
         bool hit = true;
-        if (k <= kKMax) {
-            // all locations first (pure VALU), then two fetch phases: the first
-            // kPhase1 words decide most absent keys (a filter at its design
-            // load has ~half its bits set), the rest are fetched together only
-            // for the keys still alive.  Same answer as the sequential Test.
-            uint64_t loc[kKMax];
+        for (uint32_t j0 = 0; j0 < k && hit; j0 += C) {
+            uint64_t loc[C], w[C];
 #pragma unroll
-            for (uint32_t j = 0; j < kKMax; ++j) {
-                loc[j] = j < k ? mod_m(bloom_loc(h, j), m, mu) : 0;
-                if (j < k && loc[j] >= length) hit = false;
+            for (int c = 0; c < C; ++c) {
+                const uint32_t j = j0 + c;
+                loc[c] = j < k ? mod_m(bloom_loc(h, j), m, mu) : 0;
+                if (j < k && loc[c] >= length) hit = false;
             }
-            constexpr uint32_t kPhase1 = 2;
-            uint64_t w[kKMax];
 #pragma unroll
-            for (uint32_t j = 0; j < kPhase1; ++j) w[j] = (hit && j < k) ? words[loc[j] >> 6] : ~0ull;
+            for (int c = 0; c < C; ++c) w[c] = (hit && j0 + c < k) ? words[loc[c] >> 6] : ~0ull;
 #pragma unroll
-            for (uint32_t j = 0; j < kPhase1; ++j) hit = hit && ((w[j] >> (loc[j] & 63)) & 1ull);
-            if (hit && k > kPhase1) {
-#pragma unroll
-                for (uint32_t j = kPhase1; j < kKMax; ++j) w[j] = j < k ? words[loc[j] >> 6] : ~0ull;
-#pragma unroll
-                for (uint32_t j = kPhase1; j < kKMax; ++j) hit = hit && ((w[j] >> (loc[j] & 63)) & 1ull);
-            }
-        } else {
-            for (uint32_t j = 0; j < k && hit; ++j) {
-                const uint64_t loc = mod_m(bloom_loc(h, j), m, mu);
-                hit = loc < length && ((words[loc >> 6] >> (loc & 63)) & 1ull);
-            }
+            for (int c = 0; c < C; ++c) hit = hit && ((w[c] >> (loc[c] & 63)) & 1ull);
         }
         out[i] = hit ? 1 : 0;
     }
@@ -162,7 +149,9 @@ static uint32_t grid_for(uint64_t items) {
 hipError_t launch_bloom_probe(const BloomDev& b, const uint8_t* d32, uint64_t n, uint8_t* out,
                               hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k4_bloom_probe, dim3(grid_for(n)), dim3(256), 0, s, b.words, b.len_dev, b.m,
+    // one word at a time (tools/probe_sweep.py on MI355X, 1e9 probes, 1e8-key
+    // filter: C=1 111.6 ms, 2: 117.0, 3: 123.8, 4: 131.0, all 10: 183.6)
+    hipLaunchKernelGGL(k4_bloom_probe<1>, dim3(grid_for(n)), dim3(256), 0, s, b.words, b.len_dev, b.m,
                        barrett_mu(b.m), (uint32_t)b.k, d32, n, out);
     return hipGetLastError();
 }

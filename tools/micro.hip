@@ -188,6 +188,12 @@ __global__ __launch_bounds__(256) void k_op(uint32_t iters, uint32_t* out) {
 #define ICOST33(n) "v_add_u32 %[r" n "], %[r" n "], %[r" n "]\n\t"
 #define ICOST34(n) "v_bitop3_b32 %[r" n "], %[r" n "], %[r" n "], %[c] bitop3:0x96\n\t"
 #define ICOST35(n) "v_mov_b32 %[r" n "], %[c]\n\t"
+#define SADD8 "s_add_u32 %[s0], %[s0], %[sc]\n\t" "s_add_u32 %[s1], %[s1], %[sc]\n\t" "s_add_u32 %[s2], %[s2], %[sc]\n\t" "s_add_u32 %[s3], %[s3], %[sc]\n\t" \
+              "s_add_u32 %[s4], %[s4], %[sc]\n\t" "s_add_u32 %[s5], %[s5], %[sc]\n\t" "s_add_u32 %[s6], %[s6], %[sc]\n\t" "s_add_u32 %[s7], %[s7], %[sc]\n\t"
+#define VS_MIX(n) "v_add_u32 %[r" n "], %[r" n "], %[c]\n\t" "s_add_u32 %[s" n "], %[s" n "], %[sc]\n\t"
+#define VS_MIX3(n) "v_bitop3_b32 %[r" n "], %[r" n "], %[c], %[e] bitop3:0x96\n\t" "s_add_u32 %[s" n "], %[s" n "], %[sc]\n\t"
+#define S8 [s0] "+s"(sq[0]), [s1] "+s"(sq[1]), [s2] "+s"(sq[2]), [s3] "+s"(sq[3]), [s4] "+s"(sq[4]), \
+           [s5] "+s"(sq[5]), [s6] "+s"(sq[6]), [s7] "+s"(sq[7])
 // D: single-wave latency: one dependent chain per lane (grid 1 x 64), so
 // the time per instruction is the issue-to-dependent-issue latency.  OP 8/9
 // run the duo round (10 instructions) with DPP / with plain adds.
@@ -200,6 +206,10 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
     uint32_t q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) q[j] = r + j;
+    uint32_t sq[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sq[j] = __builtin_amdgcn_readfirstlane(iters + j);
+    const uint32_t sc = __builtin_amdgcn_readfirstlane(iters * 3);
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
     for (uint32_t i = 0; i < iters; ++i) {
 #pragma unroll
@@ -319,6 +329,14 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
                 if (j == 0) asm volatile(I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) I8(ICOST34) : R8 : [c] "v"(c), [e] "v"(s1));
             if constexpr (OP == 35)
                 if (j == 0) asm volatile(I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) I8(ICOST35) : R8 : [c] "v"(c), [e] "v"(s1));
+            if constexpr (OP == 36)
+                if (j == 0) asm volatile(SADD8 SADD8 SADD8 SADD8 SADD8 SADD8 SADD8 SADD8 : S8 : [sc] "s"(sc) : "scc");
+            if constexpr (OP == 37)
+                if (j == 0) asm volatile(I8(VS_MIX) I8(VS_MIX) I8(VS_MIX) I8(VS_MIX) I8(VS_MIX) I8(VS_MIX) I8(VS_MIX) I8(VS_MIX)
+                                         : R8, S8 : [c] "v"(c), [sc] "s"(sc) : "scc");
+            if constexpr (OP == 38)
+                if (j == 0) asm volatile(I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3)
+                                         : R8, S8 : [c] "v"(c), [e] "v"(s1), [sc] "s"(sc) : "scc");
             if (OP == 10 && (j & 3) == 0)
                 asm volatile(LAG2("a", "b", "c", "d", "z", "y") LAG2("d", "a", "b", "c", "y", "z")
                              LAG2("c", "d", "a", "b", "z", "y") LAG2("b", "c", "d", "a", "y", "z")
@@ -328,7 +346,7 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
         }
     }
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
-    out[threadIdx.x] = r ^ x1 ^ x2 ^ x3 ^ z ^ t0 ^ zy ^ t3 ^ q[0] ^ q[1] ^ q[2] ^ q[3] ^ q[4] ^ q[5] ^ q[6] ^ q[7];
+    out[threadIdx.x] = sq[0] ^ sq[1] ^ sq[2] ^ sq[3] ^ sq[4] ^ sq[5] ^ sq[6] ^ sq[7] ^ r ^ x1 ^ x2 ^ x3 ^ z ^ t0 ^ zy ^ t3 ^ q[0] ^ q[1] ^ q[2] ^ q[3] ^ q[4] ^ q[5] ^ q[6] ^ q[7];
     if (threadIdx.x == 0) *cyc = c1 - c0;
 }
 
@@ -336,7 +354,7 @@ struct LtArgs { int op; uint32_t iters; uint32_t* out; uint64_t* cyc; };
 static void run_lat(void* p) {
     auto* a = (LtArgs*)p;
 #define RF_LAT(N) case N: hipLaunchKernelGGL(k_lat<N>, dim3(1), dim3(64), 0, 0, a->iters, a->out, a->cyc); break;
-    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) RF_LAT(10) RF_LAT(11) RF_LAT(12) RF_LAT(13) RF_LAT(14) RF_LAT(15) RF_LAT(16) RF_LAT(17) RF_LAT(18) RF_LAT(19) RF_LAT(20) RF_LAT(21) RF_LAT(22) RF_LAT(23) RF_LAT(24) RF_LAT(25) RF_LAT(26) RF_LAT(27) RF_LAT(28) RF_LAT(29) RF_LAT(30) RF_LAT(31) RF_LAT(32) RF_LAT(33) RF_LAT(34) default: RF_LAT(35) }
+    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) RF_LAT(10) RF_LAT(11) RF_LAT(12) RF_LAT(13) RF_LAT(14) RF_LAT(15) RF_LAT(16) RF_LAT(17) RF_LAT(18) RF_LAT(19) RF_LAT(20) RF_LAT(21) RF_LAT(22) RF_LAT(23) RF_LAT(24) RF_LAT(25) RF_LAT(26) RF_LAT(27) RF_LAT(28) RF_LAT(29) RF_LAT(30) RF_LAT(31) RF_LAT(32) RF_LAT(33) RF_LAT(34) RF_LAT(35) RF_LAT(36) RF_LAT(37) default: RF_LAT(38) }
 #undef RF_LAT
 }
 
@@ -433,5 +451,74 @@ extern "C" float micro_loads(uint64_t stride, uint32_t nblk, uint32_t nlanes, in
     float ms = time_launch(run_loads, &a);
     hipFree(arena);
     hipFree(out);
+    return ms;
+}
+
+// ---------------------------------------------------------------------------
+// G: random 8-B gather ceiling (the K4 probe's access pattern without the
+// hashing): each thread reads R words at pseudo-random positions of a table
+// of nwords u64, all R requested before any is used (like the probe's
+// phase 2), and streams a 32-B key per thread from `keys` (nt or default).
+__device__ __forceinline__ uint64_t gmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ table, uint64_t nwords,
+                                                const uint4* __restrict__ keys, int key_mode, uint64_t n,
+                                                uint8_t* __restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t seed = i;
+        if (key_mode == 1) {
+            const uint4 a = keys[2 * i], b = keys[2 * i + 1];
+            seed ^= ((uint64_t)a.x << 32 | a.y) ^ b.z;
+        } else if (key_mode == 2) {
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            const v4u* kv = reinterpret_cast<const v4u*>(keys);
+            const v4u a = __builtin_nontemporal_load(&kv[2 * i]);
+            const v4u b = __builtin_nontemporal_load(&kv[2 * i + 1]);
+            seed ^= ((uint64_t)a.x << 32 | a.y) ^ b.z;
+        }
+        uint64_t w[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) w[j] = table[__umul64hi(gmix(seed * R + j), nwords)];
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc ^= w[j];
+        out[i] = (uint8_t)(acc & 1);
+    }
+}
+
+struct GArgs { const uint64_t* table; uint64_t nwords; const uint4* keys; int key_mode; uint64_t n; uint8_t* out; int r; };
+static void run_gather(void* p) {
+    auto* a = (GArgs*)p;
+    uint64_t g = (a->n + 255) / 256;
+    if (g > 16384) g = 16384;
+    if (a->r == 2)
+        hipLaunchKernelGGL(k_gather<2>, dim3((uint32_t)g), dim3(256), 0, 0, a->table, a->nwords, a->keys, a->key_mode, a->n, a->out);
+    else if (a->r == 6)
+        hipLaunchKernelGGL(k_gather<6>, dim3((uint32_t)g), dim3(256), 0, 0, a->table, a->nwords, a->keys, a->key_mode, a->n, a->out);
+    else
+        hipLaunchKernelGGL(k_gather<10>, dim3((uint32_t)g), dim3(256), 0, 0, a->table, a->nwords, a->keys, a->key_mode, a->n, a->out);
+}
+
+// Returns ms for n threads x r gathers from a table of table_bytes.
+extern "C" float micro_gather(uint64_t table_bytes, uint64_t n, int r, int key_mode) {
+    uint64_t* table;
+    uint4* keys = nullptr;
+    uint8_t* out;
+    if (hipMalloc(&table, table_bytes) != hipSuccess) return -2.f;
+    if (hipMalloc(&out, n) != hipSuccess) return -2.f;
+    if (key_mode && hipMalloc(&keys, 32 * n) != hipSuccess) return -2.f;
+    hipMemset(table, 0x5a, table_bytes);
+    if (keys) hipMemset(keys, 0x33, 32 * n);
+    GArgs a{table, table_bytes / 8, keys, key_mode, n, out, r};
+    float ms = time_launch(run_gather, &a);
+    hipFree(table);
+    hipFree(out);
+    if (keys) hipFree(keys);
     return ms;
 }

@@ -34,16 +34,28 @@ def main():
                  "indep8 bitop3 no-bank-conflict", "indep8 bitop3 bank-conflict",
                  "lag2 order V1", "lag2 order V5", "lag2 order V6", "lag2 order V7", "lag2 order V8",
                  "cost alignbit vshift", "cost alignbit imm", "cost bitop3 3v", "cost add3 3v", "cost xad 3v",
-                 "cost v_add vop2", "cost add_dpp", "cost v_xor vop2", "cost v_add e64", "cost lshl_add", "cost v_add same-reg", "cost bitop3 2reg", "cost v_mov"]
+                 "cost v_add vop2", "cost add_dpp", "cost v_xor vop2", "cost v_add e64", "cost lshl_add", "cost v_add same-reg", "cost bitop3 2reg", "cost v_mov",
+                 "cost s_add x64", "64 v_add + 64 s_add interleaved", "64 bitop3 + 64 s_add interleaved"]
     for op, name in enumerate(lat_names):
         iters = 1 << 17
         cyc = ctypes.c_uint64(0)
         ms = L.micro_lat(op, iters, ctypes.byref(cyc))
-        n = iters * 8 * (9 if op == 10 or 18 <= op <= 22 else 10 if op in (8, 9) else 8 if op >= 23 else 1)
+        n = iters * 8 * (9 if op == 10 or 18 <= op <= 22 else 10 if op in (8, 9) else 16 if op >= 37 else 8 if op >= 23 else 1)
         print("lat %-22s 1 wave  %.3f ms  %.2f ns/instr  memtime %.2f ticks/instr  %s"
               % (name, ms, ms * 1e6 / n, cyc.value / n, "(%.1f ns/round)" % (ms * 1e6 / (iters * 8)) if op >= 8 else ""),
               flush=True)
     if len(sys.argv) > 1 and sys.argv[1] == "lat":
+        return
+    L.micro_gather.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+    L.micro_gather.restype = ctypes.c_float
+    for tb in [171 * 2**20, 2 * 2**30]:
+        for r, km in [(10, 0), (10, 1), (10, 2), (6, 1), (2, 1)]:
+            n = 1 << 28
+            ms = L.micro_gather(tb, n, r, km)
+            print("gather table=%6.0f MiB reads/thread=%2d keys=%s  %.2f ms  %.2f G reads/s  %.2f G threads/s"
+                  % (tb / 2**20, r, ["none", "default", "nt"][km], ms, n * r / ms / 1e6, n / ms / 1e6),
+                  flush=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "gather":
         return
     names = ["v_add_u32", "v_alignbit_b32", "v_bitop3_b32", "v_add3_u32", "v_xor_b32", "v_perm_b32",
              "v_lshrrev_b32", "v_fma_f32"]
