@@ -617,7 +617,7 @@ struct rf_graph {
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
     DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_counts,
-        b_tmp_idx, b_tmp_dig;
+        b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
     uint32_t max_level_jobs = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -736,14 +736,19 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         uint8_t* t = tmpl.data() + job_off[i];
         const uint64_t len = d->tmpl_len[j];
         if (len) memcpy(t, d->blob + d->tmpl_off[j], len);
+        // the kernels OR digests into the holes: keep them zero
+        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) memset(t + d->hole_pos[h], 0, 32);
         t[len] = 0x80;
         const uint64_t bits = len * 8;
         uint8_t* e = t + 64ull * nblk[j];
         for (int b = 0; b < 8; ++b) e[-1 - b] = (uint8_t)(bits >> (8 * b));
     }
-    std::vector<uint32_t> cons_ptr(S + 1), cons_job(H);
+    std::vector<uint32_t> cons_ptr(S + 1), cons_job(2 * H);  // {internal job, level}
     for (uint32_t s = 0; s <= S; ++s) cons_ptr[s] = (uint32_t)cptr[s];
-    for (uint64_t c = 0; c < H; ++c) cons_job[c] = gr->ext2int[cjob[c]];
+    for (uint64_t c = 0; c < H; ++c) {
+        cons_job[2 * c] = gr->ext2int[cjob[c]];
+        cons_job[2 * c + 1] = level[cjob[c]];
+    }
     gr->hole_count = H;
     gr->tmpl_bytes = tb;
     // upload
@@ -760,25 +765,31 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     if ((e = up(gr->b_meta, meta.data(), 32ull * J)) != hipSuccess ||
         (e = up(gr->b_holes, holes.data(), 8ull * H)) != hipSuccess ||
         (e = up(gr->b_cons_ptr, cons_ptr.data(), 4ull * (S + 1))) != hipSuccess ||
-        (e = up(gr->b_cons_job, cons_job.data(), 4ull * H)) != hipSuccess ||
+        (e = up(gr->b_cons_job, cons_job.data(), 8ull * H)) != hipSuccess ||
         (e = up(gr->b_tmpl, tmpl.data(), tmpl.size())) != hipSuccess ||
         (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
         (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
         (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_counts.ensure(4ull * (L + 1))) != hipSuccess)
+        (e = gr->b_counts.ensure(4ull * (L + 1))) != hipSuccess ||
+        (e = gr->b_counts_last.ensure(4ull * (L + 1))) != hipSuccess ||
+        (e = up(gr->b_lvl_start, G.lvl_start.data(), 4ull * (L + 1))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
                     hipGetErrorString(e));
     HIPC(hipMemset(gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
     HIPC(hipMemset(gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
+    HIPC(hipMemset(gr->b_counts.p, 0, 4ull * (L + 1)));
+    HIPC(hipMemset(gr->b_counts_last.p, 0, 4ull * (L + 1)));
     G.meta = gr->b_meta.as<uint4>();
     G.holes = gr->b_holes.as<uint2>();
     G.cons_ptr = gr->b_cons_ptr.as<uint32_t>();
-    G.cons_job = gr->b_cons_job.as<uint32_t>();
+    G.cons = gr->b_cons_job.as<uint2>();
     G.tmpl = gr->b_tmpl.as<uint8_t>();
     G.slots = gr->b_slots.as<uint8_t>();
     G.dirty = gr->b_dirty.as<uint32_t>();
     G.list = gr->b_list.as<uint32_t>();
     G.counts = gr->b_counts.as<uint32_t>();
+    G.counts_last = gr->b_counts_last.as<uint32_t>();
+    G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
     HIPC(hipEventCreate(&gr->e0));
     HIPC(hipEventCreate(&gr->e1));
     guard.release();
@@ -791,7 +802,8 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
     if (gr->ctx) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
-                          &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_counts, &gr->b_tmp_idx,
+                          &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_counts, &gr->b_counts_last,
+                          &gr->b_lvl_start, &gr->b_tmp_idx,
                           &gr->b_tmp_dig})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
@@ -839,17 +851,17 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
     return RF_OK;
 }
 
-// The per-level launch sequence (2 kernels per level + 2 memsets) only reads
-// device-side counts, so it is fixed for a loaded graph: capture it once per
-// mode into a hipGraph and replay (kernel boundaries ~1.5 us instead of a host
-// launch each; MI355X_MICROARCH "boundary" / "graph-replay-floor").
+// The launch sequence (one kernel per level + a step-end kernel) only reads
+// device-side list lengths, so it is fixed for a loaded graph: capture it once
+// per mode into a hipGraph and replay (kernel boundaries ~1.5 us instead of a
+// host launch each; MI355X_MICROARCH "boundary" / "graph-replay-floor").  An
+// incremental step leaves the dirty set empty (each hashed job clears its
+// bit); a full one discards whatever set_slots queued.
 static int graph_enqueue(rf_graph* gr, int full, hipStream_t s) {
     GraphDev& G = gr->g;
-    const size_t dirty_bytes = 4ull * ((G.n_jobs + 31) / 32 + 1);
-    if (full) HIPC(hipMemsetAsync(G.dirty, 0xff, dirty_bytes, s));
-    HIPC(hipMemsetAsync(G.counts, 0, 4ull * (G.n_levels + 1), s));
     for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
-    HIPC(hipMemsetAsync(G.dirty, 0, dirty_bytes, s));
+    HIPC(launch_graph_step_end(G, full, s));
+    if (full) HIPC(hipMemsetAsync(G.dirty, 0, 4ull * ((G.n_jobs + 31) / 32 + 1), s));
     return RF_OK;
 }
 
@@ -899,7 +911,7 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
     if (int rc = graph_recompute_locked(gr, full, ctx->stream)) return rc;
     std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
     if (gr->g.n_levels)
-        HIPC(hipMemcpyAsync(counts.data(), gr->g.counts, 4ull * gr->g.n_levels,
+        HIPC(hipMemcpyAsync(counts.data(), gr->g.counts_last, 4ull * gr->g.n_levels,
                             hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
     uint64_t tot = 0;

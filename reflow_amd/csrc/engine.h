@@ -52,17 +52,20 @@ struct GraphDev {
     uint4* meta = nullptr;           // [2J]
     uint2* holes = nullptr;          // [H] {byte position, slot}
     uint32_t* cons_ptr = nullptr;    // [S+1] slot -> consumer jobs (internal ids)
-    uint32_t* cons_job = nullptr;    // [C]
-    uint8_t* tmpl = nullptr;         // padded templates
+    uint2* cons = nullptr;           // [C] {consumer job, its level}
+    uint8_t* tmpl = nullptr;         // padded templates, zero at the holes (read-only)
     uint8_t* slots = nullptr;        // [S][32] digest table
-    uint32_t* dirty = nullptr;       // [(J+31)/32] dirty bitset over internal ids
-    uint32_t* list = nullptr;        // [J] compacted dirty jobs of the current level
-    uint32_t* counts = nullptr;      // [L] jobs hashed per level
+    uint32_t* dirty = nullptr;       // [(J+31)/32] queued-this-step bitset over internal ids
+    uint32_t* list = nullptr;        // [J] per-level work lists (level l at lvl_start[l])
+    uint32_t* counts = nullptr;      // [L] list lengths (append cursors) of the current step
+    uint32_t* counts_last = nullptr; // [L] jobs hashed per level by the last recompute
+    uint32_t* lvl_start_dev = nullptr; // [L+1]
     std::vector<uint32_t> lvl_start; // host copy [L+1]
 };
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);
 hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s);
+hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);
 

@@ -8,170 +8,248 @@
 //
 // Data layout in HBM (DESIGN.md "Data layout"):
 //   tmpl      per job, its digest material with SHA padding already applied
-//             (64-B aligned, nblk*64 bytes); WD holes carry the 0x00 0x05
-//             prefix and 32 bytes that are rewritten from the slot table.
+//             (64-B aligned, nblk*64 bytes) and ZERO bytes at every hole; it is
+//             never written after load.
 //   meta      32-B job record (template offset, blocks, hole range, out slot,
 //             consumer range): two 16-B loads per job.
-//   holes     {byte position, slot} pairs.
+//   holes     {byte position, slot} pairs, sorted by position per job.
 //   slots     [S][32] digest table (node digests, physical keys, File IDs).
-//   dirty     bitset over jobs in level order.
+//   dirty     bitset over jobs in level order: "already queued this step".
+//   list      [J] per-level work lists; level l's list lives at lvl_start[l]
+//             (a level can never hold more dirty jobs than it has jobs).
 //   cons      slot -> consumer jobs (reverse edges for the frontier).
-// Per level: k3_compact turns the level's dirty bits into a dense job list,
-// then k2_hash gives each listed job one lane: patch holes from the slot
-// table, hash the padded template, write the slot and -- only if the digest
-// changed -- atomicOr the consumers' dirty bits (early cut-off).  A fused
-// per-workgroup compaction was measured 4x slower on the incremental step:
-// small, heavy levels (the wide K) got too few workgroups.
+// The frontier needs no compaction pass: whoever changes a slot (set_slots,
+// or a job whose digest changed -- early cut-off) sets its consumers' dirty
+// bits and appends the newly set ones to their levels' lists, one atomicAdd
+// per (wave, level).  One kernel per level then gives each listed job one
+// lane, which assembles the job's material block by block in a private LDS
+// ring (template block + digests OR-ed into the zero holes), hashes it and
+// propagates.  A level's jobs all depend only on lower levels, so a level's
+// list is complete when its kernel starts.
 #include "engine.h"
 #include "sha256_dev.h"
 
 namespace rf {
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(v, d, 64);
-        if (lane >= (uint32_t)d) v += t;
-    }
-    return v;
-}
-
-// Write the 32 digest bytes D (as 8 little-endian words) at byte `pos` of a
-// 4-B aligned buffer, preserving the neighbouring bytes.
-__device__ __forceinline__ void patch_digest(uint32_t* wb, uint32_t pos, const uint32_t (&D)[8]) {
-    const uint32_t w0 = pos >> 2, s = pos & 3;
-    if (s == 0) {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) wb[w0 + m] = D[m];
-    } else {
-        const uint32_t sh = 8 * s, keep = (1u << sh) - 1u;
-        wb[w0] = (wb[w0] & keep) | (D[0] << sh);
-#pragma unroll
-        for (int m = 1; m < 8; ++m) wb[w0 + m] = (D[m - 1] >> (32 - sh)) | (D[m] << sh);
-        wb[w0 + 8] = (wb[w0 + 8] & ~keep) | (D[7] >> (32 - sh));
-    }
-}
+constexpr uint32_t kLevelBlock = 256;
+constexpr uint32_t kRing = 33;  // words per lane: a 32-word ring + 1 (odd stride: no bank conflicts)
 
 struct LevelArgs {
     uint32_t s, e, lvl;  // internal job range of the level
     int full;
-    const uint4* meta;
-    const uint2* holes;
-    const uint32_t* cons_job;
-    uint8_t* tmpl;
+    const uint4* __restrict__ meta;
+    const uint2* __restrict__ holes;
+    const uint2* __restrict__ cons;          // {consumer job, its level}
+    const uint32_t* __restrict__ lvl_start;  // [L+1] on device
+    uint32_t n_levels;
+    const uint8_t* __restrict__ tmpl;
     uint8_t* slots;
     uint32_t* dirty;
+    uint32_t* list;
     uint32_t* counts;
 };
 
-__device__ __forceinline__ void hash_job(const LevelArgs& a, uint32_t p) {
-    const uint4 m0 = a.meta[2 * p], m1 = a.meta[2 * p + 1];
-    uint8_t* t = a.tmpl + 64ull * m0.x;
-    uint32_t* tw = reinterpret_cast<uint32_t*>(t);
-    // 1. patch holes from the slot table
-    for (uint32_t h = m0.z; h < m0.w; ++h) {
-        const uint2 hp = a.holes[h];
-        const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * hp.y);
-        const uint4 lo = src[0], hi = src[1];
-        const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        patch_digest(tw, hp.x, D);
+// Append the lanes' jobs j (need) at level lv to their levels' lists; one
+// atomicAdd per distinct level in the wave.  Called by every lane of the wave.
+__device__ __forceinline__ void append_jobs(uint32_t* list, uint32_t* counts, const uint32_t* ls,
+                                            bool need, uint32_t j, uint32_t lv) {
+    const uint32_t lane = __lane_id();
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint64_t mask = __ballot(need);
+    while (mask) {
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
+        const uint32_t lvl = __builtin_amdgcn_readfirstlane(__shfl(lv, leader, 64));
+        const bool mine = need && lv == lvl;
+        const uint64_t same = __ballot(mine);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&counts[lvl], (uint32_t)__popcll(same));
+        base = ls[lvl] + __shfl(base, leader, 64);
+        if (mine) {
+            list[base + (uint32_t)__popcll(same & lt)] = j;
+            need = false;
+        }
+        mask = __ballot(need);
     }
-    // 2. hash the padded template (full blocks only)
+}
+
+// Mark consumers [c, ce) of the lanes whose slot changed (c == ce otherwise)
+// dirty, queueing the newly dirty ones.  Wave-uniform loop.
+__device__ __forceinline__ void propagate(const uint2* __restrict__ cons, uint32_t* dirty, uint32_t* list,
+                                          uint32_t* counts, const uint32_t* ls, uint32_t c, uint32_t ce) {
+    while (__any(c < ce)) {
+        bool need = false;
+        uint2 jl = make_uint2(0, 0);
+        if (c < ce) {
+            jl = cons[c++];
+            const uint32_t bit = 1u << (jl.x & 31);
+            need = !(atomicOr(&dirty[jl.x >> 5], bit) & bit);
+        }
+        append_jobs(list, counts, ls, need, jl.x, jl.y);
+    }
+}
+
+// OR digest D (8 LE words) into the lane's ring at material byte `pos`; the
+// template holds zero bytes there, and the 00 05 prefix around it.
+__device__ __forceinline__ void or_digest(uint32_t* ring, uint32_t pos, const uint32_t (&D)[8]) {
+    const uint32_t x = pos >> 2, sh = 32 - 8 * (pos & 3);
+    uint32_t prev = 0;
+#pragma unroll
+    for (int m = 0; m < 9; ++m) {
+        const uint32_t cur = m < 8 ? D[m] : 0u;
+        const uint32_t v = (uint32_t)((((uint64_t)cur << 32) | prev) >> sh);
+        atomicOr(&ring[(x + m) & 31], v);
+        prev = cur;
+    }
+}
+
+__device__ __forceinline__ void ring_put(uint32_t* ring, uint32_t half, const uint4 (&t)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ring[half + 4 * q] = t[q].x;
+        ring[half + 4 * q + 1] = t[q].y;
+        ring[half + 4 * q + 2] = t[q].z;
+        ring[half + 4 * q + 3] = t[q].w;
+    }
+}
+
+// Hash job p; returns whether its slot changed (always true in full mode).
+// Software pipeline over blocks: while block b is compressed, the template
+// of block b+2 and the (at most two: holes are >= 32 B apart) holes that
+// start in block b+1 -- records and slot digests -- are in flight.
+__device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_t* ring, uint32_t& cb,
+                                         uint32_t& ce) {
+    const uint4 m0 = a.meta[2 * p], m1 = a.meta[2 * p + 1];
+    uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * m1.x);
+    uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
+    if (!a.full) {
+        olo = dst[0];
+        ohi = dst[1];
+    }
+    const uint4* __restrict__ T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
+    const uint32_t nb = m0.y, he = m0.w;
+    uint32_t hn = m0.z;  // first hole not yet applied
+    uint2 R[2];
+    uint4 DL[2], DH[2];
+    auto fetch_holes = [&]() {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            R[k] = hn + k < he ? a.holes[hn + k] : make_uint2(~0u, 0u);
+            const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * R[k].y);
+            DL[k] = src[0];
+            DH[k] = src[1];
+        }
+    };
+    fetch_holes();
+    uint4 t[4] = {T[0], T[1], T[2], T[3]};
+    ring_put(ring, 0, t);
+    if (nb > 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = T[4 + q];
+    }
     ShaState st;
     st.init();
-    const uint4* q = reinterpret_cast<const uint4*>(t);
-    for (uint32_t b = 0; b < m0.y; ++b) {
-        const uint4 r0 = q[4 * b], r1 = q[4 * b + 1], r2 = q[4 * b + 2], r3 = q[4 * b + 3];
-        uint32_t w[16] = {bswap32(r0.x), bswap32(r0.y), bswap32(r0.z), bswap32(r0.w),
-                          bswap32(r1.x), bswap32(r1.y), bswap32(r1.z), bswap32(r1.w),
-                          bswap32(r2.x), bswap32(r2.y), bswap32(r2.z), bswap32(r2.w),
-                          bswap32(r3.x), bswap32(r3.y), bswap32(r3.z), bswap32(r3.w)};
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t half = (b & 1) * 16;
+        if (b + 1 < nb) {
+            ring_put(ring, half ^ 16, t);
+            if (b + 2 < nb) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) t[q] = T[4 * (b + 2) + q];
+            }
+        }
+        // holes that start in block b (they may run into block b+1)
+        uint32_t used = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (R[k].x < 64 * (b + 1)) {
+                const uint32_t D[8] = {DL[k].x, DL[k].y, DL[k].z, DL[k].w, DH[k].x, DH[k].y, DH[k].z, DH[k].w};
+                or_digest(ring, R[k].x, D);
+                ++used;
+            }
+        }
+        if (used) {
+            hn += used;
+            fetch_holes();
+        }
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
         sha256_compress(st, w);
     }
     uint4 nlo, nhi;
     nlo.x = bswap32(st.h[0]); nlo.y = bswap32(st.h[1]); nlo.z = bswap32(st.h[2]); nlo.w = bswap32(st.h[3]);
     nhi.x = bswap32(st.h[4]); nhi.y = bswap32(st.h[5]); nhi.z = bswap32(st.h[6]); nhi.w = bswap32(st.h[7]);
-    // 3. store; propagate only on change (early cut-off)
-    uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * m1.x);
     bool changed = true;
-    if (!a.full) {
-        const uint4 olo = dst[0], ohi = dst[1];
+    if (!a.full)
         changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
                   (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
-    }
     if (changed) {
         dst[0] = nlo;
         dst[1] = nhi;
-        if (!a.full) {
-            for (uint32_t c = m1.y; c < m1.z; ++c) {
-                const uint32_t j = a.cons_job[c];
-                atomicOr(&a.dirty[j >> 5], 1u << (j & 31));
+    }
+    cb = m1.y;
+    ce = m1.z;
+    return changed;
+}
+
+// K2+K3, one level: every listed job (incremental) or every job of the level
+// (full).  Incremental: the job leaves the dirty set, and if its digest
+// changed its consumers join their levels' lists.
+__global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
+    __shared__ uint32_t ring_all[kLevelBlock * kRing];
+    uint32_t* ring = &ring_all[threadIdx.x * kRing];
+    const uint32_t n = a.full ? (a.e - a.s) : a.counts[a.lvl];
+    const uint32_t* lst = a.list + a.s;
+    for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t cb = 0, ce = 0;
+        if (i < n) {
+            const uint32_t p = a.full ? a.s + i : lst[i];
+            const bool changed = hash_job(a, p, ring, cb, ce);
+            if (!a.full) {
+                atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                if (!changed) ce = cb;
             }
         }
+        if (!a.full) propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, cb, ce);
     }
 }
 
-// K3: compact the dirty jobs of the level's range [s, e) into a dense global
-// list (wave popcount prefix, one atomic per wave) so K2 gets one full lane
-// per dirty job whatever the dirty density (2% on an incremental step).
-__global__ __launch_bounds__(256) void k3_compact(const uint32_t* __restrict__ dirty, uint32_t s,
-                                                  uint32_t e, uint32_t* __restrict__ list,
-                                                  uint32_t* __restrict__ counts, uint32_t lvl) {
-    const uint32_t w_lo = s >> 5, w_hi = (e + 31) >> 5;
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < (w_hi - w_lo); base += gridDim.x * blockDim.x) {
-        const uint32_t wi = w_lo + base + threadIdx.x;
-        uint32_t bits = 0;
-        if (wi < w_hi) {
-            bits = dirty[wi];
-            const uint32_t first = wi << 5;
-            if (first < s) bits &= ~0u << (s - first);
-            if (first + 32 > e) bits &= (e - first >= 32) ? ~0u : ((1u << (e - first)) - 1u);
-        }
-        const uint32_t c = __popc(bits);
-        const uint32_t incl = wave_incl_scan(c);
-        const uint32_t total = __shfl(incl, 63, 64);
-        uint32_t wbase = 0;
-        if (lane == 63 && total) wbase = atomicAdd(&counts[lvl], total);
-        wbase = __shfl(wbase, 63, 64);
-        uint32_t pos = wbase + incl - c;
-        while (bits) {
-            const uint32_t b = __ffs(bits) - 1;
-            bits &= bits - 1;
-            list[pos++] = (wi << 5) + b;
-        }
-    }
-}
-
-// K2: one lane per listed job of the level.
-__global__ __launch_bounds__(256) void k2_hash(LevelArgs a, const uint32_t* __restrict__ list) {
-    const uint32_t n = a.counts[a.lvl];
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        hash_job(a, list[i]);
-}
-
-// set_slots: write input digests, dirty their consumers when they changed.
+// set_slots: write input digests; a changed slot queues its consumers.
 __global__ __launch_bounds__(256) void k3_mark_slots(const uint32_t* __restrict__ sl,
                                                      const uint8_t* __restrict__ dig, uint32_t n,
-                                                     uint8_t* slots, const uint32_t* cons_ptr,
-                                                     const uint32_t* cons_job, uint32_t* dirty) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t s = sl[i];
-        const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
-        uint4* dst = reinterpret_cast<uint4*>(slots + 32ull * s);
-        const uint4 nlo = src[0], nhi = src[1], olo = dst[0], ohi = dst[1];
-        const bool changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) |
-                             (olo.w != nlo.w) | (ohi.x != nhi.x) | (ohi.y != nhi.y) |
-                             (ohi.z != nhi.z) | (ohi.w != nhi.w);
-        if (changed) {
-            dst[0] = nlo;
-            dst[1] = nhi;
-            for (uint32_t c = cons_ptr[s]; c < cons_ptr[s + 1]; ++c) {
-                const uint32_t j = cons_job[c];
-                atomicOr(&dirty[j >> 5], 1u << (j & 31));
+                                                     uint8_t* slots, const uint32_t* __restrict__ cons_ptr,
+                                                     const uint2* __restrict__ cons, uint32_t* dirty,
+                                                     uint32_t* list, uint32_t* counts,
+                                                     const uint32_t* __restrict__ ls) {
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t c = 0, ce = 0;
+        if (i < n) {
+            const uint32_t s = sl[i];
+            const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
+            uint4* dst = reinterpret_cast<uint4*>(slots + 32ull * s);
+            const uint4 nlo = src[0], nhi = src[1], olo = dst[0], ohi = dst[1];
+            const bool changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) |
+                                 (olo.w != nlo.w) | (ohi.x != nhi.x) | (ohi.y != nhi.y) |
+                                 (ohi.z != nhi.z) | (ohi.w != nhi.w);
+            if (changed) {
+                dst[0] = nlo;
+                dst[1] = nhi;
+                c = cons_ptr[s];
+                ce = cons_ptr[s + 1];
             }
         }
+        propagate(cons, dirty, list, counts, ls, c, ce);
+    }
+}
+
+// End of a recompute: record what each level hashed, reset the lists.
+__global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __restrict__ ls, uint32_t L,
+                            int full) {
+    for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
+        last[l] = full ? ls[l + 1] - ls[l] : counts[l];
+        counts[l] = 0;
     }
 }
 
@@ -208,18 +286,25 @@ hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, con
                                    uint32_t n, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k3_mark_slots, dim3(grid_for(n, 4096)), dim3(256), 0, s, slots, digests, n,
-                       g.slots, g.cons_ptr, g.cons_job, g.dirty);
+                       g.slots, g.cons_ptr, g.cons, g.dirty, g.list, g.counts, g.lvl_start_dev);
     return hipGetLastError();
 }
 
 hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s) {
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
-    const uint32_t words = ((e + 31) >> 5) - (b >> 5);
-    hipLaunchKernelGGL(k3_compact, dim3(grid_for(words, 2048)), dim3(256), 0, s, g.dirty, b, e, g.list,
-                       g.counts, lvl);
-    LevelArgs a{b, e, lvl, full, g.meta, g.holes, g.cons_job, g.tmpl, g.slots, g.dirty, g.counts};
-    hipLaunchKernelGGL(k2_hash, dim3(grid_for(e - b, 16384)), dim3(256), 0, s, a, g.list);
+    LevelArgs a{b, e, lvl, full, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
+                g.tmpl, g.slots, g.dirty, g.list, g.counts};
+    // incremental: the dirty count is only known on device; 1024 blocks (4
+    // per CU, all resident) cover any level's list with a grid-stride loop
+    const uint32_t grid = grid_for(e - b, full ? 16384u : 1024u);
+    hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s) {
+    hipLaunchKernelGGL(k3_step_end, dim3(1), dim3(256), 0, s, g.counts, g.counts_last, g.lvl_start_dev,
+                       g.n_levels, full);
     return hipGetLastError();
 }
 
