@@ -213,18 +213,21 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
 // (f = e(r-1), ..., d = a(r-3)) one round is
 //   e-lanes: e(r+1) = Z + Σ1(e) + Ch(e,f,g),  Z = h + K+W(r) + d
 //   a-lanes: a(r+1) = Z + Σ0(a) + Maj(a,b,c), Z = T1(r) = e(r+1) - d
-// i.e. the same  R = Z + S + F  on both halves (3 v_alignbit with per-lane
-// amounts + xor3; Maj(a,b,c) = Ch(a^c, b, c) via sel = X0 ^ (X2 & M)).  The
-// Z of the next step needs one cross-lane value that is already a step old
-// on both halves -- the partner's X0 (a(r-2) for the e-lane, e(r+2-2) for
-// the a-lane, two rounds behind) -- so it is
+// i.e. the same  R = Z + S + F  on both halves (Maj(a,b,c) = Ch(a^c, b, c)
+// via sel = X0 ^ (X2 & M)).  S = Σ is spread over a quad of lanes: lane q
+// of the quad rotates X0 by the q-th amount of its half (one v_alignbit with a
+// per-lane amount) and two quad_perm DPP xors give all of them the xor of the
+// three.  The Z of the next step needs one cross-lane value that is already a
+// step old on both halves -- the partner's X0 (a(r-2) for the e-lane, e(r+2-2)
+// for the a-lane, two rounds behind) -- so it is
 //   Zt = (X2 ^ M) + k      e: g + K+W(r+1)     a: -c   (k = 1)
 //   Z' = X0[lane^8] + Zt   one full-mask DPP add
-// 9 VALU per round and no instruction reads the result of the one before
-// it (a dependent VALU costs ~6-7 cycles against 4 for an independent one,
-// tools/micro.hip "lat").  Block boundaries: each half applies its own
-// feed-forward (bank-masked DPP adds) when it reaches round 0 of the next
-// block; the Z values that straddle the boundary read partner values from
+// 8 VALU per round (9 with three v_alignbit per lane: 327 -> 297 ms per 16 MiB
+// chain), every DPP source written >= 2 instructions earlier.  One wave issues
+// one instruction per ~4-5 cycles whatever the dependences (tools/micro.py
+// lat), so the instruction count per round is the chain's cost.
+// Block boundaries: each half applies its own feed-forward (bank-masked DPP
+// adds) when it reaches round 0 of the next block; the Z values that straddle the boundary read partner values from
 // before the partner's feed-forward and get per-block corrections
 // (c63/c64/c65 below).  A message starts from a zero raw state with
 // chaining value IV, so block 0 takes the same path as every other block.
@@ -234,15 +237,14 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
 // one asm block runs four steps and the compiler's pad after an asm block is
 // paid once per four rounds.
 #define RF_LAG_STEP(x0, x1, x2, x3, z, zn, k)                                              \
-    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[s1]\n\t"                                 \
-    "v_alignbit_b32 %[t1], %[" x0 "], %[" x0 "], %[s2]\n\t"                                 \
-    "v_alignbit_b32 %[t2], %[" x0 "], %[" x0 "], %[s3]\n\t"                                 \
-    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                        \
-    "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"                               \
-    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                       \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[sq]\n\t"                                 \
     "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[" k "]\n\t"                                    \
-    "v_add3_u32 %[" x3 "], %[" z "], %[t0], %[t3]\n\t"                                      \
-    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                        \
+    "v_xor_b32_dpp %[t1], %[t0], %[t0] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"  \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                       \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t" \
+    "v_xor_b32_dpp %[t1], %[t0], %[t1] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"  \
+    "v_add3_u32 %[" x3 "], %[" z "], %[t1], %[t3]\n\t"
 
 #define RF_LAG_GROUP                                        \
     RF_LAG_STEP("a", "b", "c", "d", "z", "y", "k1")         \
@@ -270,10 +272,10 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
     "v_add_u32_dpp %[h3], %[h3], %[" x3 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" bm "\n\t"
 
 #define RF_LAG_STATE [a] "+v"(Pa), [b] "+v"(Pb), [c] "+v"(Pc), [d] "+v"(Pd), [z] "+v"(Z), [y] "+v"(Y)
-#define RF_LAG_TMP [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+#define RF_LAG_TMP [t0] "=&v"(t0), [t1] "=&v"(t1), [t3] "=&v"(t3)
 #define RF_LAG_H [h0] "+v"(Hr0), [h1] "+v"(Hr1), [h2] "+v"(Hr2), [h3] "+v"(Hr3)
 #define RF_LAG_IN(k1v, k2v, k3v, k4v) \
-    [s1] "v"(sh1), [s2] "v"(sh2), [s3] "v"(sh3), [m] "v"(M), [k1] "v"(k1v), [k2] "v"(k2v), [k3] "v"(k3v), [k4] "v"(k4v)
+    [sq] "v"(shq), [m] "v"(M), [k1] "v"(k1v), [k2] "v"(k2v), [k3] "v"(k3v), [k4] "v"(k4v)
 
 namespace lag {
 constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
@@ -316,7 +318,11 @@ __global__ __launch_bounds__(128) void k1_sha256_duo(SoloArgs a) {
         if (lane < 4) ones[64 + lane] = 1u;
     }
     const bool elane = (lane & 8) == 0;
-    const uint32_t sh1 = elane ? 6 : 2, sh2 = elane ? 11 : 13, sh3 = elane ? 25 : 22;
+    // Σ over a quad: lane q (q = lane & 3 < 3) rotates by the q-th amount of
+    // its half (Σ1: 6 11 25, Σ0: 2 13 22); two quad_perm DPP xors give every
+    // lane of the quad the xor of all three (lane 3 of a quad is unused)
+    const uint32_t q3 = lane & 3;
+    const uint32_t shq = elane ? (q3 == 1 ? 11u : q3 == 2 ? 25u : 6u) : (q3 == 1 ? 13u : q3 == 2 ? 22u : 2u);
     const uint32_t M = elane ? 0u : ~0u;
     const uint32_t one = 1u, zero = 0u;
     for (uint32_t q = blockIdx.x; q < a.n_order; q += gridDim.x) {
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(128) void k1_sha256_duo(SoloArgs a) {
         uint32_t c63 = 0;
         uint32_t c64 = elane ? lag::IV[2] : 0u - lag::IV[4];
         uint32_t c65 = elane ? lag::IV[1] : 0u - lag::IV[3];
-        uint32_t t0, t1, t2, t3;
+        uint32_t t0, t1, t3;
         if (wave == 1) fill_kw_rows(kw, p, len, nb, 0, lane);
         __syncthreads();
         uint32_t buf = 0;
