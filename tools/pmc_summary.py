@@ -14,13 +14,15 @@ import csv
 import json
 import sys
 
-WIDE_STREAM = {"rf::k1_sha256_duo", "rf::k1_sha256_solo", "rf::k1_sha256_lanes"}
+WIDE_STREAM = {"rf::k1_sha256_duo", "rf::k1_sha256_solo", "rf::k1_sha256_lanes", "rf::k_gen_fill"}
 
 
 def load(path):
     agg = collections.defaultdict(lambda: [0, 0.0])
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"].split("(")[0]
+        k = k[5:] if k.startswith("void ") else k
+        k = k.split("<")[0]  # one entry per kernel template
         agg[k][0] += 1
         agg[k][1] += float(r["Counter_Value"])
     return agg
