@@ -136,6 +136,34 @@ int rf_fileset_digest_batch(rf_ctx *ctx, uint64_t n_sets, const uint64_t *set_gr
                             const uint64_t *group_entry, const char *const *paths,
                             const uint32_t *path_lens, const uint8_t *ids32, uint8_t *out32);
 
+/* ---- Fileset values as JSON (the assoc value, eval.go:1141 -> marshal
+ * eval.go:1961-1967 = json.Marshal + Repository.Put, repository.go:108-114) --
+ * A fileset TREE: node i's List = nodes list_child[list_ptr[i] .. list_ptr[i+1])
+ * (an empty range = nil or empty List: both omitted, `json:",omitempty"`);
+ * node i's Map = entries [entry_ptr[i], entry_ptr[i+1]) with path bytes,
+ * 32-B File ID and Size (executor.go:25-38).  JSON bytes follow Go 1.9/1.10
+ * encoding/json: {"List":[...],"Fileset":{"<path>":{"ID":"sha256:<hex>","Size":N}}},
+ * keys sorted bytewise, HTML-safe escaping, invalid UTF-8 -> �.  The ID's
+ * text form is grailbio/base digest's String() (unvendored: parity unpinned). */
+typedef struct {
+    uint64_t n_nodes;
+    const uint64_t *list_ptr;    /* [n_nodes+1] */
+    const uint32_t *list_child;  /* [list_ptr[n_nodes]] */
+    const uint64_t *entry_ptr;   /* [n_nodes+1] */
+    const char *const *paths;    /* [entries] */
+    const uint32_t *path_lens;   /* [entries] */
+    const uint8_t *ids32;        /* [entries][32] */
+    const int64_t *sizes;        /* [entries] */
+} rf_fileset_tree;
+/* json.Marshal of node `root` into out[cap]; *out_len = bytes needed (RF_EINVAL
+ * if cap is short).  Host-only (no device needed). */
+int rf_fileset_marshal_json(const rf_fileset_tree *t, uint32_t root, uint8_t *out, uint64_t cap,
+                            uint64_t *out_len);
+/* out32[i] = SHA256(json.Marshal(roots[i])): the value digests CacheWrite
+ * stores (eval.go:1141-1151); the hashes run on K1. */
+int rf_fileset_value_digest_batch(rf_ctx *ctx, const rf_fileset_tree *t, const uint32_t *roots,
+                                  uint64_t n, uint8_t *out32);
+
 /* ---- K2/K3: incremental digest DAG (Flow.Digest / CacheKeys) ------------
  * The host lowers a Flow graph (flow.go:653-802) into hash JOBS over digest
  * SLOTS.  Job j hashes a byte template (its digest material, flow.go:675-750

@@ -101,6 +101,10 @@ struct Fileset {
 
 // Fileset.Digest for many filesets in one device call.
 std::vector<Digest> FilesetDigests(Engine& e, const std::vector<const Fileset*>& v);
+// json.Marshal(Fileset) (eval.go:1961-1967; host code) and the value digests
+// CacheWrite stores under each cache key (SHA-256 on the GPU).
+std::string MarshalJSON(const Fileset& v);
+std::vector<Digest> FilesetValueDigests(Engine& e, const std::vector<const Fileset*>& v);
 
 // ---- flows -------------------------------------------------------------------
 enum Op : int {

@@ -9,6 +9,8 @@ What it restates (reference = LDuderino/reflow @ v0 under /root/reference):
   * digest framing  WD(d) = 0x00 0x05 || d          (grailbio/base/digest, not
     vendored; pinned by the goldens below)
   * Fileset.WriteDigest / Digest                   executor.go:205-233
+  * json.Marshal(Fileset) -> assoc value digest     executor.go:25-38, eval.go:1961-1967
+    (Go 1.9/1.10 encoding/json byte rules; digest JSON text unpinned)
   * Op.DigestString (stale table, OpData->"maxOp")  op_string.go:11-21
   * Flow.WriteDigest / Digest (V1 inline, V2 WD)   flow.go:653-750, writeN :909-913
   * Flow.PhysicalDigest / CacheKeys                flow.go:764-802
@@ -115,6 +117,96 @@ class OFileset:
 
     def digest(self) -> bytes:
         return sha256(self.material())
+
+    # json.Marshal(Fileset) (executor.go:25-38 struct tags; eval.go:1961-1967
+    # marshal -> Repository.Put: the assoc VALUE written under every cache key)
+    def json(self) -> bytes:
+        parts = []
+        if self.list:  # `json:",omitempty"`: nil and empty List both omitted
+            parts.append(b'"List":[' + b",".join(v.json() for v in self.list) + b"]")
+        if self.map:  # `json:"Fileset,omitempty"`
+            items = sorted(((_key_bytes(k), v) for k, v in self.map.items()), key=lambda kv: kv[0])
+            ents = []
+            for k, (fid, size) in items:
+                ents.append(go_json_string(k) + b':{"ID":' + go_json_string(digest_json_text(fid)) +
+                            b',"Size":' + str(int(size)).encode() + b"}")
+            parts.append(b'"Fileset":{' + b",".join(ents) + b"}")
+        return b"{" + b",".join(parts) + b"}"
+
+    def value_digest(self) -> bytes:
+        return sha256(self.json())
+
+
+def _key_bytes(k) -> bytes:
+    return k if isinstance(k, bytes) else k.encode("utf-8", "surrogateescape")
+
+
+def digest_json_text(d: bytes) -> bytes:
+    """digest.Digest's JSON text (grailbio/base/digest, NOT vendored: parity
+    unpinned) -- its String() form "sha256:<64 lowercase hex>"."""
+    assert len(d) == 32 and any(d), "zero digests have no pinned text form"
+    return b"sha256:" + d.hex().encode()
+
+
+_HEX = b"0123456789abcdef"
+
+
+def _utf8_len(s: bytes, i: int) -> int:
+    """Length of the valid UTF-8 sequence at s[i] (b >= 0x80), or 0 if invalid:
+    unicode/utf8.DecodeRuneInString's acceptance ranges."""
+    b0, n = s[i], len(s)
+
+    def cont(j, lo=0x80, hi=0xBF):
+        return j < n and lo <= s[j] <= hi
+    if 0xC2 <= b0 <= 0xDF:
+        return 2 if cont(i + 1) else 0
+    if 0xE0 <= b0 <= 0xEF:
+        lo, hi = (0xA0, 0xBF) if b0 == 0xE0 else (0x80, 0x9F) if b0 == 0xED else (0x80, 0xBF)
+        return 3 if cont(i + 1, lo, hi) and cont(i + 2) else 0
+    if 0xF0 <= b0 <= 0xF4:
+        lo, hi = (0x90, 0xBF) if b0 == 0xF0 else (0x80, 0x8F) if b0 == 0xF4 else (0x80, 0xBF)
+        return 4 if cont(i + 1, lo, hi) and cont(i + 2) and cont(i + 3) else 0
+    return 0
+
+
+def go_json_string(s: bytes) -> bytes:
+    """encoding/json encodeState.string(s, escapeHTML=true) as of Go 1.9/1.10
+    (.travis.yml:3-5): `"` `\\` -> backslash escapes; \\n \\r \\t short forms;
+    other bytes < 0x20 and < > & -> \\u00XX (lowercase hex; Go >= 1.22 writes
+    \\b \\f, not used here); invalid UTF-8 -> \\ufffd per bad byte; U+2028/2029 ->
+    \\u2028/\\u2029; everything else raw."""
+    out = bytearray(b'"')
+    i = 0
+    while i < len(s):
+        b = s[i]
+        if b < 0x80:
+            if b in (0x22, 0x5C):
+                out += bytes([0x5C, b])
+            elif b == 0x0A:
+                out += b"\\n"
+            elif b == 0x0D:
+                out += b"\\r"
+            elif b == 0x09:
+                out += b"\\t"
+            elif b < 0x20 or b in (0x3C, 0x3E, 0x26):
+                out += b"\\u00" + bytes([_HEX[b >> 4], _HEX[b & 15]])
+            else:
+                out.append(b)
+            i += 1
+            continue
+        n = _utf8_len(s, i)
+        if n == 0:
+            out += b"\\ufffd"
+            i += 1
+            continue
+        if s[i:i + n] in (b"\xe2\x80\xa8", b"\xe2\x80\xa9"):
+            out += b"\\u202" + bytes([_HEX[s[i + 2] - 0xA0]])
+            i += n
+            continue
+        out += s[i:i + n]
+        i += n
+    out += b'"'
+    return bytes(out)
 
 
 # --------------------------------------------------------------------------

@@ -32,6 +32,7 @@ EXPORTS = [
     "rf_malloc", "rf_free", "rf_memcpy_h2d", "rf_memcpy_d2h", "rf_memset_d", "rf_stream",
     "rf_timer_start", "rf_timer_stop", "rf_comm_unique_id", "rf_comm_init", "rf_comm_destroy",
     "rf_comm_allgather", "rf_comm_allreduce_or", "rf_memcpy_d2d", "rf_graph_gather_device",
+    "rf_fileset_marshal_json", "rf_fileset_value_digest_batch",
 ]
 
 
@@ -54,6 +55,74 @@ class GraphDesc(ctypes.Structure):
                 ("tmpl_len", ctypes.c_void_p), ("hole_ptr", ctypes.c_void_p),
                 ("hole_pos", ctypes.c_void_p), ("hole_slot", ctypes.c_void_p),
                 ("blob", ctypes.c_void_p), ("blob_len", ctypes.c_uint64)]
+
+
+class FilesetTree(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_uint64), ("list_ptr", ctypes.c_void_p),
+                ("list_child", ctypes.c_void_p), ("entry_ptr", ctypes.c_void_p),
+                ("paths", ctypes.c_void_p), ("path_lens", ctypes.c_void_p),
+                ("ids32", ctypes.c_void_p), ("sizes", ctypes.c_void_p)]
+
+
+class FilesetTreeBuilder:
+    """Flattens nested filesets into the rf_fileset_tree CSR form.  A fileset
+    is any object with .list (None or a list of filesets) and .map (None or a
+    dict path -> (id32, size)); add() returns its root node index."""
+
+    def __init__(self):
+        self.list_ptr, self.list_child, self.entry_ptr = [0], [], [0]
+        self.paths, self.ids, self.sizes = [], [], []
+        self._pending = []
+
+    def add(self, fs) -> int:
+        # nodes are numbered in pre-order; children lists refer forward
+        node = len(self.list_ptr) - 1
+        self.list_ptr.append(None)
+        self.entry_ptr.append(None)
+        for path, (id32, size) in (fs.map or {}).items():
+            self.paths.append(path.encode("utf-8", "surrogateescape") if isinstance(path, str) else path)
+            self.ids.append(bytes(id32))
+            self.sizes.append(int(size))
+        self.entry_ptr[node + 1] = len(self.paths)
+        kids = [self.add(c) for c in (fs.list or [])]
+        self._pending.append((node, kids))
+        return node
+
+    def struct(self):
+        n = len(self.list_ptr) - 1
+        children = dict(self._pending)
+        lp, lc = [0], []
+        for i in range(n):
+            lc.extend(children[i])
+            lp.append(len(lc))
+        # a node's entries are recorded before its children's (pre-order), so
+        # entry_ptr is already the CSR; list_ptr is rebuilt from the children
+        self._keep = dict(
+            lp=np.array(lp, dtype=np.uint64), lc=np.array(lc or [0], dtype=np.uint32),
+            ep=np.array(self.entry_ptr, dtype=np.uint64),
+            pb=[ctypes.create_string_buffer(p, max(len(p), 1)) for p in self.paths],
+            pl=np.array([len(p) for p in self.paths] or [0], dtype=np.uint32),
+            ids=np.frombuffer(b"".join(self.ids) or b"\0" * 32, dtype=np.uint8).copy(),
+            sz=np.array(self.sizes or [0], dtype=np.int64))
+        k = self._keep
+        k["pp"] = (ctypes.c_void_p * max(len(self.paths), 1))(*[ctypes.addressof(b) for b in k["pb"]])
+        return FilesetTree(n, _ptr(k["lp"]), _ptr(k["lc"]), _ptr(k["ep"]),
+                           ctypes.cast(k["pp"], ctypes.c_void_p), _ptr(k["pl"]), _ptr(k["ids"]),
+                           _ptr(k["sz"]))
+
+
+def fileset_marshal_json(fs) -> bytes:
+    """json.Marshal(Fileset) through the C-ABI (host code, no device)."""
+    b = FilesetTreeBuilder()
+    root = b.add(fs)
+    t = b.struct()
+    need = ctypes.c_uint64(0)
+    rc = lib().rf_fileset_marshal_json(ctypes.byref(t), root, None, 0, ctypes.byref(need))
+    if rc != RF_OK and need.value == 0:
+        _check(rc)
+    out = ctypes.create_string_buffer(max(need.value, 1))
+    _check(lib().rf_fileset_marshal_json(ctypes.byref(t), root, out, need.value, ctypes.byref(need)))
+    return out.raw[:need.value]
 
 
 class GraphStats(ctypes.Structure):
@@ -113,6 +182,8 @@ def lib():
             "rf_comm_allreduce_or": ([vp, vp, u64, vp], i32),
             "rf_memcpy_d2d": ([vp, vp, vp, u64], i32),
             "rf_graph_gather_device": ([vp, vp, u32, vp, vp], i32),
+            "rf_fileset_marshal_json": ([vp, u32, vp, u64, vp], i32),
+            "rf_fileset_value_digest_batch": ([vp, vp, vp, u64, vp], i32),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -239,6 +310,18 @@ class Context:
         _check(lib().rf_fileset_digest_batch(self._h, n, _ptr(sg), _ptr(ge), pp, _ptr(pl),
                                              _ptr(idb), _ptr(out)))
         return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+    def fileset_value_digests(self, sets):
+        """SHA256(json.Marshal(fs)) per fileset: CacheWrite's assoc values."""
+        if not sets:
+            return []
+        b = FilesetTreeBuilder()
+        roots = np.array([b.add(fs) for fs in sets], dtype=np.uint32)
+        t = b.struct()
+        out = np.zeros(32 * len(sets), dtype=np.uint8)
+        _check(lib().rf_fileset_value_digest_batch(self._h, ctypes.byref(t), _ptr(roots), len(sets),
+                                                   _ptr(out)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(len(sets))]
 
 
 class DeviceBuffer:

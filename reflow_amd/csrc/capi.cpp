@@ -609,6 +609,166 @@ extern "C" int rf_fileset_digest_batch(rf_ctx* ctx, uint64_t n_sets, const uint6
 }
 
 // ---------------------------------------------------------------------------
+// Fileset JSON: json.Marshal(Fileset) -> Repository.Put (eval.go:1961-1967),
+// the assoc value CacheWrite stores under every cache key (eval.go:1141).
+// Byte rules of Go 1.9/1.10 encoding/json (.travis.yml:3-5): struct fields
+// in declaration order with their tags (executor.go:25-38: "List" and
+// "Fileset", both omitempty, i.e. omitted when len == 0), map keys sorted
+// bytewise, strings escaped by encodeState.string with escapeHTML.
+static const char kHex[] = "0123456789abcdef";
+
+// Length of the valid UTF-8 sequence at s[i] (s[i] >= 0x80), 0 if invalid:
+// the acceptance ranges of unicode/utf8.DecodeRuneInString.
+static size_t utf8_seq(const uint8_t* s, size_t n, size_t i) {
+    const uint8_t b0 = s[i];
+    auto in = [&](size_t j, uint8_t lo, uint8_t hi) { return j < n && s[j] >= lo && s[j] <= hi; };
+    if (b0 >= 0xC2 && b0 <= 0xDF) return in(i + 1, 0x80, 0xBF) ? 2 : 0;
+    if (b0 >= 0xE0 && b0 <= 0xEF) {
+        const uint8_t lo = b0 == 0xE0 ? 0xA0 : 0x80, hi = b0 == 0xED ? 0x9F : 0xBF;
+        return in(i + 1, lo, hi) && in(i + 2, 0x80, 0xBF) ? 3 : 0;
+    }
+    if (b0 >= 0xF0 && b0 <= 0xF4) {
+        const uint8_t lo = b0 == 0xF0 ? 0x90 : 0x80, hi = b0 == 0xF4 ? 0x8F : 0xBF;
+        return in(i + 1, lo, hi) && in(i + 2, 0x80, 0xBF) && in(i + 3, 0x80, 0xBF) ? 4 : 0;
+    }
+    return 0;
+}
+
+static void json_string(std::string& o, const uint8_t* s, size_t n) {
+    o.push_back('"');
+    size_t i = 0;
+    while (i < n) {
+        const uint8_t b = s[i];
+        if (b < 0x80) {
+            switch (b) {
+                case '"': case '\\': o.push_back('\\'); o.push_back((char)b); break;
+                case '\n': o += "\\n"; break;
+                case '\r': o += "\\r"; break;
+                case '\t': o += "\\t"; break;
+                default:
+                    if (b < 0x20 || b == '<' || b == '>' || b == '&') {
+                        o += "\\u00";
+                        o.push_back(kHex[b >> 4]);
+                        o.push_back(kHex[b & 15]);
+                    } else {
+                        o.push_back((char)b);
+                    }
+            }
+            ++i;
+            continue;
+        }
+        const size_t len = utf8_seq(s, n, i);
+        if (len == 0) {  // utf8.RuneError of size 1: one replacement per bad byte
+            o += "\\ufffd";
+            ++i;
+        } else if (len == 3 && b == 0xE2 && s[i + 1] == 0x80 && (s[i + 2] == 0xA8 || s[i + 2] == 0xA9)) {
+            o += "\\u202";  // U+2028 / U+2029
+            o.push_back(kHex[s[i + 2] - 0xA0]);
+            i += 3;
+        } else {
+            o.append(reinterpret_cast<const char*>(s + i), len);
+            i += len;
+        }
+    }
+    o.push_back('"');
+}
+
+static int marshal_fileset(const rf_fileset_tree* t, uint32_t node, int depth, std::string& o,
+                           std::vector<uint64_t>& idx) {
+    if (node >= t->n_nodes) return fail(RF_EINVAL, "fileset node %u >= n_nodes %llu", node,
+                                        (unsigned long long)t->n_nodes);
+    if (depth > 4096) return fail(RF_EINVAL, "fileset tree deeper than 4096 (cycle?)");
+    const uint64_t lb = t->list_ptr[node], le = t->list_ptr[node + 1];
+    const uint64_t eb = t->entry_ptr[node], ee = t->entry_ptr[node + 1];
+    if (lb > le || eb > ee) return fail(RF_EINVAL, "fileset node %u: CSR not monotone", node);
+    o.push_back('{');
+    if (le > lb) {
+        o += "\"List\":[";
+        for (uint64_t c = lb; c < le; ++c) {
+            if (c > lb) o.push_back(',');
+            int rc = marshal_fileset(t, t->list_child[c], depth + 1, o, idx);
+            if (rc) return rc;
+        }
+        o.push_back(']');
+    }
+    if (ee > eb) {
+        if (le > lb) o.push_back(',');
+        o += "\"Fileset\":{";
+        const size_t base = idx.size();
+        for (uint64_t e = eb; e < ee; ++e) idx.push_back(e);
+        auto less = [&](uint64_t a, uint64_t b) {
+            const size_t la = t->path_lens[a], lb2 = t->path_lens[b];
+            const int c = memcmp(t->paths[a], t->paths[b], std::min(la, lb2));
+            return c < 0 || (c == 0 && la < lb2);
+        };
+        std::sort(idx.begin() + base, idx.end(), less);
+        for (size_t q = base; q < idx.size(); ++q) {
+            const uint64_t e = idx[q];
+            if (q > base && !less(idx[q - 1], e))
+                return fail(RF_EINVAL, "fileset node %u: duplicate map key", node);
+            const uint8_t* id = t->ids32 + 32 * e;
+            bool zero = true;
+            for (int k = 0; k < 32; ++k) zero &= id[k] == 0;
+            if (zero)  // digest.Digest's zero text form is grailbio/base's (unvendored)
+                return fail(RF_EINVAL, "fileset node %u: zero file ID has no pinned JSON form", node);
+            if (q > base) o.push_back(',');
+            json_string(o, reinterpret_cast<const uint8_t*>(t->paths[e]), t->path_lens[e]);
+            o += ":{\"ID\":\"sha256:";
+            for (int k = 0; k < 32; ++k) {
+                o.push_back(kHex[id[k] >> 4]);
+                o.push_back(kHex[id[k] & 15]);
+            }
+            o += "\",\"Size\":";
+            o += std::to_string((long long)t->sizes[e]);
+            o.push_back('}');
+        }
+        idx.resize(base);
+        o.push_back('}');
+    }
+    o.push_back('}');
+    return RF_OK;
+}
+
+static int check_tree(const rf_fileset_tree* t) {
+    ARG(t && t->list_ptr && t->entry_ptr, "null fileset tree");
+    const uint64_t nl = t->list_ptr[t->n_nodes], ne = t->entry_ptr[t->n_nodes];
+    ARG(nl == 0 || t->list_child, "null list_child");
+    ARG(ne == 0 || (t->paths && t->path_lens && t->ids32 && t->sizes), "null entry arrays");
+    return RF_OK;
+}
+
+extern "C" int rf_fileset_marshal_json(const rf_fileset_tree* t, uint32_t root, uint8_t* out,
+                                       uint64_t cap, uint64_t* out_len) {
+    int rc = check_tree(t);
+    if (rc) return rc;
+    ARG(out_len, "null out_len");
+    std::string o;
+    std::vector<uint64_t> idx;
+    if ((rc = marshal_fileset(t, root, 0, o, idx))) return rc;
+    *out_len = o.size();
+    if (o.size() > cap) return fail(RF_EINVAL, "output buffer too small: need %zu bytes", o.size());
+    if (!o.empty() && out) memcpy(out, o.data(), o.size());
+    return RF_OK;
+}
+
+extern "C" int rf_fileset_value_digest_batch(rf_ctx* ctx, const rf_fileset_tree* t, const uint32_t* roots,
+                                             uint64_t n, uint8_t* out32) {
+    ARG(ctx && (n == 0 || (roots && out32)), "null argument");
+    if (n == 0) return RF_OK;
+    int rc = check_tree(t);
+    if (rc) return rc;
+    std::string arena;
+    std::vector<uint64_t> offs(n), lens(n), idx;
+    for (uint64_t i = 0; i < n; ++i) {
+        offs[i] = arena.size();
+        if ((rc = marshal_fileset(t, roots[i], 0, arena, idx))) return rc;
+        lens[i] = arena.size() - offs[i];
+    }
+    return rf_sha256_arena(ctx, reinterpret_cast<const uint8_t*>(arena.data()), offs.data(), lens.data(),
+                           n, out32);
+}
+
+// ---------------------------------------------------------------------------
 // Digest DAG
 struct rf_graph {
     rf_ctx* ctx = nullptr;

@@ -81,5 +81,12 @@ struct BloomDev {
 hipError_t launch_bloom_probe(const BloomDev& b, const uint8_t* d32, uint64_t n, uint8_t* out,
                               hipStream_t s);
 hipError_t launch_bloom_add(const BloomDev& b, const uint8_t* d32, uint64_t n, hipStream_t s);
+// Repository.Collect: dead[n] flags, tile_count[bloom_collect_tiles(n)]
+// scratch; out_idx receives the dead indices ascending; nb2 = {n_dead,
+// dead_bytes} (u64, i64), zeroed by the caller.
+uint64_t bloom_collect_tiles(uint64_t n);
+hipError_t launch_bloom_collect(const BloomDev& b, const uint8_t* d32, const int64_t* sizes, uint64_t n,
+                                uint8_t* dead, uint32_t* tile_count, uint64_t* out_idx, uint64_t* nb2,
+                                hipStream_t s);
 
 }  // namespace rf

@@ -137,7 +137,138 @@ __global__ __launch_bounds__(256) void k4_bloom_add(unsigned long long* __restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// Repository.Collect (repository/file/repository.go:304-327): every object
+// whose digest the liveset does not contain is removed.  Batched over n
+// objects in three launches: (1) probe one tile of kTile objects per block,
+// write a dead flag per object and the tile's dead count and bytes; (2) one
+// block scans the tile counts; (3) each tile writes its dead indices at its
+// scanned offset, in ascending order (the reference removes in walk order).
+constexpr uint32_t kCollectBlock = 256, kCollectPer = 16, kTile = kCollectBlock * kCollectPer;
+
+__device__ __forceinline__ bool bloom_contains(const uint64_t* __restrict__ words, uint64_t length,
+                                               uint64_t m, uint64_t mu, uint32_t k, const uint8_t* d) {
+    uint64_t D[4], h[4];
+    load_digest64(d, D);
+    base_hashes_wd(D, h);
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint64_t loc = mod_m(bloom_loc(h, j), m, mu);
+        if (loc >= length || !((words[loc >> 6] >> (loc & 63)) & 1ull)) return false;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(kCollectBlock) void k4_collect_mark(
+    const uint64_t* __restrict__ words, const uint64_t* __restrict__ len_dev, uint64_t m, uint64_t mu,
+    uint32_t k, const uint8_t* __restrict__ d32, const int64_t* __restrict__ sizes, uint64_t n,
+    uint8_t* __restrict__ dead, uint32_t* __restrict__ tile_count, unsigned long long* __restrict__ bytes) {
+    __shared__ uint32_t s_cnt[kCollectBlock / 64];
+    __shared__ long long s_bytes[kCollectBlock / 64];
+    const uint64_t length = *len_dev;
+    const uint64_t base = (uint64_t)blockIdx.x * kTile;
+    uint32_t cnt = 0;
+    long long by = 0;
+#pragma unroll 4
+    for (uint32_t j = 0; j < kCollectPer; ++j) {
+        const uint64_t i = base + (uint64_t)j * kCollectBlock + threadIdx.x;
+        if (i < n) {
+            const bool d = !bloom_contains(words, length, m, mu, k, d32 + 32 * i);
+            dead[i] = d;
+            cnt += d;
+            if (d && sizes) by += sizes[i];
+        }
+    }
+    // wave sums, then the block's
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+        by += __shfl_xor(by, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_cnt[threadIdx.x >> 6] = cnt;
+        s_bytes[threadIdx.x >> 6] = by;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t c = 0;
+        long long b = 0;
+        for (uint32_t w = 0; w < kCollectBlock / 64; ++w) {
+            c += s_cnt[w];
+            b += s_bytes[w];
+        }
+        tile_count[blockIdx.x] = c;
+        if (b) atomicAdd(bytes, (unsigned long long)b);  // two's complement sum
+    }
+}
+
+// Exclusive scan of the tile counts by one block; total -> *n_dead.
+__global__ __launch_bounds__(1024) void k4_collect_scan(uint32_t* __restrict__ tile_count, uint64_t tiles,
+                                                        unsigned long long* __restrict__ n_dead) {
+    __shared__ unsigned long long s[1024];
+    const uint64_t per = (tiles + 1023) / 1024;
+    const uint64_t b = threadIdx.x * per, e = b + per < tiles ? b + per : tiles;
+    unsigned long long sum = 0;
+    for (uint64_t t = b; t < e; ++t) sum += tile_count[t];
+    s[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive
+        const unsigned long long v = threadIdx.x >= o ? s[threadIdx.x - o] : 0ull;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned long long run = s[threadIdx.x] - sum;
+    for (uint64_t t = b; t < e; ++t) {
+        const uint32_t c = tile_count[t];
+        tile_count[t] = (uint32_t)run;  // offsets fit: n_dead < 2^32 is checked on the host
+        run += c;
+    }
+    if (threadIdx.x == 1023) *n_dead = s[1023];
+}
+
+__global__ __launch_bounds__(kCollectBlock) void k4_collect_scatter(const uint8_t* __restrict__ dead,
+                                                                    const uint32_t* __restrict__ tile_off,
+                                                                    uint64_t n, uint64_t* __restrict__ out) {
+    __shared__ uint32_t s_w[kCollectBlock / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kTile;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t run = tile_off[blockIdx.x];
+    for (uint32_t j = 0; j < kCollectPer; ++j) {
+        const uint64_t i = base + (uint64_t)j * kCollectBlock + threadIdx.x;
+        const bool d = i < n && dead[i];
+        const uint64_t bal = __ballot(d);
+        if (lane == 0) s_w[wave] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (uint32_t w = 0; w < kCollectBlock / 64; ++w) {
+            before += w < wave ? s_w[w] : 0;
+            total += s_w[w];
+        }
+        if (d) out[run + before + (uint32_t)__popcll(bal & lt)] = i;
+        run += total;
+        __syncthreads();
+    }
+}
+
 static uint64_t barrett_mu(uint64_t m) { return m ? (~0ull) / m : 0; }
+
+hipError_t launch_bloom_collect(const BloomDev& b, const uint8_t* d32, const int64_t* sizes, uint64_t n,
+                                uint8_t* dead, uint32_t* tile_count, uint64_t* out_idx,
+                                uint64_t* n_dead_bytes2, hipStream_t s) {
+    // n_dead_bytes2 = {n_dead, dead_bytes}, zeroed by the caller
+    if (!n) return hipSuccess;
+    const uint64_t tiles = (n + kTile - 1) / kTile;
+    auto* nb = reinterpret_cast<unsigned long long*>(n_dead_bytes2);
+    hipLaunchKernelGGL(k4_collect_mark, dim3((uint32_t)tiles), dim3(kCollectBlock), 0, s, b.words,
+                       b.len_dev, b.m, barrett_mu(b.m), (uint32_t)b.k, d32, sizes, n, dead, tile_count,
+                       nb + 1);
+    hipLaunchKernelGGL(k4_collect_scan, dim3(1), dim3(1024), 0, s, tile_count, tiles, nb);
+    hipLaunchKernelGGL(k4_collect_scatter, dim3((uint32_t)tiles), dim3(kCollectBlock), 0, s, dead,
+                       tile_count, n, out_idx);
+    return hipGetLastError();
+}
+
+uint64_t bloom_collect_tiles(uint64_t n) { return (n + kTile - 1) / kTile; }
 
 static uint32_t grid_for(uint64_t items) {
     uint64_t g = (items + 255) / 256;

@@ -127,6 +127,66 @@ std::vector<Digest> FilesetDigests(Engine& e, const std::vector<const Fileset*>&
     return out;
 }
 
+// Fileset trees in the rf_fileset_tree CSR form (pre-order nodes; a node's
+// Map entries before its children's).
+namespace {
+struct TreeArrays {
+    std::vector<uint64_t> list_ptr{0}, entry_ptr{0};
+    std::vector<uint32_t> list_child;
+    std::vector<std::vector<uint32_t>> kids;
+    std::vector<const char*> paths;
+    std::vector<uint32_t> plen;
+    std::vector<uint8_t> ids;
+    std::vector<int64_t> sizes;
+    uint32_t add(const Fileset& f) {
+        const uint32_t node = (uint32_t)kids.size();
+        kids.emplace_back();
+        for (const auto& [path, file] : f.Map) {
+            paths.push_back(path.data());
+            plen.push_back((uint32_t)path.size());
+            ids.insert(ids.end(), file.ID.b.begin(), file.ID.b.end());
+            sizes.push_back(file.Size);
+        }
+        entry_ptr.push_back(paths.size());
+        if (f.List)
+            for (const Fileset& c : *f.List) {
+                const uint32_t k = add(c);
+                kids[node].push_back(k);
+            }
+        return node;
+    }
+    rf_fileset_tree tree() {
+        for (auto& k : kids) {
+            list_child.insert(list_child.end(), k.begin(), k.end());
+            list_ptr.push_back(list_child.size());
+        }
+        return rf_fileset_tree{kids.size(), list_ptr.data(), list_child.data(), entry_ptr.data(),
+                               paths.data(), plen.data(), ids.data(), sizes.data()};
+    }
+};
+}  // namespace
+
+std::string MarshalJSON(const Fileset& v) {
+    TreeArrays a;
+    const uint32_t root = a.add(v);
+    const rf_fileset_tree t = a.tree();
+    uint64_t need = 0;
+    if (rf_fileset_marshal_json(&t, root, nullptr, 0, &need) != RF_OK && need == 0) Check(RF_EINVAL);
+    std::string out(need, '\0');
+    Check(rf_fileset_marshal_json(&t, root, reinterpret_cast<uint8_t*>(out.data()), need, &need));
+    return out;
+}
+
+std::vector<Digest> FilesetValueDigests(Engine& e, const std::vector<const Fileset*>& v) {
+    TreeArrays a;
+    std::vector<uint32_t> roots;
+    for (const Fileset* f : v) roots.push_back(a.add(*f));
+    const rf_fileset_tree t = a.tree();
+    std::vector<Digest> out(v.size());
+    if (!v.empty()) Check(rf_fileset_value_digest_batch(e.ctx(), &t, roots.data(), roots.size(), out[0].b.data()));
+    return out;
+}
+
 // ---- flows ----------------------------------------------------------------------
 std::string DigestString(Op op) {
     static const char* names[] = {"OpExec", "OpIntern", "OpExtern", "OpGroupby", "OpMap",

@@ -80,6 +80,24 @@ static void TestValueDigest(Engine& e) {
     EXPECT(vlist.N() == 4, "N");
 }
 
+// CacheWrite's assoc value: json.Marshal(Fileset) (eval.go:1961-1967)
+static void TestValueJSON(Engine& e) {
+    Digester D(e);
+    File f1{D.FromString("foo"), 3}, f2{D.FromString("bar"), -1};
+    Fileset v1, vlist;
+    v1.Map = {{"foo", f1}, {"<b>", f2}};
+    vlist.List = std::vector<Fileset>{v1, Fileset{}};
+    const std::string want1 = "{\"Fileset\":{\"\\u003cb\\u003e\":{\"ID\":\"" + f2.ID.String() +
+                              "\",\"Size\":-1},\"foo\":{\"ID\":\"" + f1.ID.String() + "\",\"Size\":3}}}";
+    EXPECT(MarshalJSON(v1) == want1, "json got %s", MarshalJSON(v1).c_str());
+    EXPECT(MarshalJSON(vlist) == "{\"List\":[" + want1 + ",{}]}", "list json got %s",
+           MarshalJSON(vlist).c_str());
+    EXPECT(MarshalJSON(Fileset{}) == "{}", "empty");
+    auto d = FilesetValueDigests(e, {&v1, &vlist});
+    EXPECT(d[0] == D.FromBytes(want1), "value digest");
+    EXPECT(d[1] == D.FromBytes(MarshalJSON(vlist)), "list value digest");
+}
+
 static void TestDigestExec(Engine& e) {
     Digester D(e);
     FlowArena a;
@@ -175,6 +193,7 @@ int main() {
         TestDigestStability(e);
         TestCanonicalize(e);
         TestValueDigest(e);
+        TestValueJSON(e);
         TestDigestExec(e);
         TestCacheKeysAndIncremental(e);
         TestLiveset(e);

@@ -113,3 +113,10 @@ def json_to_flow(d):
         kw["hashv1"] = n.get("hashv1", False)
         nodes.append(OFlow(n["op"], [nodes[i] for i in n["deps"]], **kw))
     return nodes[d["root"]], nodes
+
+
+def json_to_fs_tree(d):
+    """Inverse of make_golden.fs_tree_to_json (byte paths)."""
+    return OFileset(list=None if d["list"] is None else [json_to_fs_tree(x) for x in d["list"]],
+                    map=None if d["map"] is None else
+                    {bytes.fromhex(p): (bytes.fromhex(f), s) for p, f, s in d["map"]})

@@ -17,6 +17,9 @@ verification value.  The fixtures are data: inputs and expected outputs.
                        material, digest
   flows.json           flow graphs (every op, V1/V2, Universe) -> digest,
                        physical digest, CacheKeys of every node
+  fileset_json.json    Fileset values (nested List + Map, adversarial path
+                       bytes) -> json.Marshal bytes, value digest (the assoc
+                       value CacheWrite stores; digest JSON text unpinned)
   murmur3.json         murmur3 x64_128 of WD keys and raw strings
   bloom.json           filters (m, k) -> per-key locations, filter words,
                        Contains answers, JSON/binary wire bytes
@@ -185,6 +188,45 @@ def gen_filesets():
     return {"cases": out}
 
 
+def fs_tree_to_json(v: OFileset):
+    """Byte-exact form for the JSON fixture: paths as hex (may be invalid UTF-8)."""
+    return {"list": None if v.list is None else [fs_tree_to_json(x) for x in v.list],
+            "map": None if v.map is None else
+            [[O._key_bytes(p).hex(), fid.hex(), size] for p, (fid, size) in v.map.items()]}
+
+
+# path bytes that exercise every escaping rule of encodeState.string
+JSON_PATHS = [b"a", b"", b"dir/file.fq.gz", b'q"uote', b"back\\slash", b"nl\n cr\r tab\t",
+              bytes(range(0x00, 0x20)), b"<html>&amp;", b"\x7f del", "é ü 日本".encode(),
+              "\u2028\u2029 sep".encode(), b"\xff\xfe bad", b"\xe2\x82 trunc", b"\xed\xa0\x80 surr",
+              b"\xf4\x90\x80\x80 >max", b"\xc0\xaf overlong", "\U0001F600 emoji".encode(),
+              "\ufffd real".encode(), b"A", b"B", b"a/b"]
+
+
+def gen_fileset_json():
+    rng = random.Random(0x150F)
+
+    def rid():
+        return bytes(rng.getrandbits(8) for _ in range(32))
+    flat = OFileset(map={p: (rid(), rng.choice([0, 1, -1, 123456789012, -(1 << 63), (1 << 63) - 1]))
+                         for p in JSON_PATHS})
+    sets = [("empty", OFileset()), ("empty list, empty map", OFileset(list=[], map={})),
+            ("escaping + order", flat),
+            ("single '.'", OFileset(map={".": (from_string("x"), 1)})),
+            ("list and map both", OFileset(list=[OFileset(map={"x": (rid(), 2)})], map={"y": (rid(), 3)})),
+            ("nested", OFileset(list=[OFileset(list=[flat, OFileset()]), OFileset(map={"z": (rid(), 0)})])),
+            ("vlist executor_test.go:77", vlist())]
+    for j in range(8):
+        kids = [OFileset(map={"s%d/%s" % (j, "x" * rng.randint(0, 40)) + str(t): (rid(), rng.randint(0, 1 << 40))
+                              for t in range(rng.randint(0, 30))}) for _ in range(rng.randint(0, 3))]
+        sets.append(("random %d" % j, OFileset(list=kids) if kids and rng.random() < 0.5 else
+                     (kids[0] if kids else OFileset(map={}))))
+    return {"note": "json.Marshal(Fileset), Go 1.9/1.10 encoding/json; ID text = sha256:<hex> "
+                    "(grailbio/base, unvendored: unpinned)",
+            "cases": [{"name": n, "value": fs_tree_to_json(v), "json": v.json().hex(),
+                       "value_digest": O.digest_string(v.value_digest())} for n, v in sets]}
+
+
 def flow_case(name, root, universe=b"", v1=False):
     nodes = topo(root)
     per = []
@@ -290,6 +332,7 @@ def main():
     write("c1_fileset.json", gen_c1())
     write("filesets.json", gen_filesets())
     write("flows.json", gen_flows())
+    write("fileset_json.json", gen_fileset_json())
     write("murmur3.json", gen_murmur3())
     write("bloom.json", gen_bloom())
 

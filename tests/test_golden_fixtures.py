@@ -22,7 +22,7 @@ import make_golden as MG  # noqa: E402
 from lowering import Lowerer  # noqa: E402
 
 FIXTURES = ["reference_kats.json", "sha256.json", "c1_fileset.json", "filesets.json", "flows.json",
-            "murmur3.json", "bloom.json"]
+            "murmur3.json", "bloom.json", "fileset_json.json"]
 
 
 def fileset_groups(v):
@@ -53,6 +53,7 @@ def test_reference_kats_reproduced():
 def test_fixtures_regenerate_identically():
     """make_golden.py is deterministic and the committed files are its output."""
     gens = {"sha256.json": MG.gen_sha256, "filesets.json": MG.gen_filesets, "flows.json": MG.gen_flows,
+            "fileset_json.json": MG.gen_fileset_json,
             "murmur3.json": MG.gen_murmur3, "bloom.json": MG.gen_bloom}
     for name, fn in gens.items():
         want = json.loads(json.dumps(fn(), sort_keys=True))
@@ -198,6 +199,25 @@ def test_gpu_c1_fixture(ctx):
     assert hashlib.sha256(ids.tobytes()).hexdigest() == d["ids_sha256"]
     group = [(MG.c1_path(i), ids[i].tobytes()) for i in range(d["n"])]
     assert O.digest_string(ctx.fileset_digest_batch([[group]])[0]) == d["fileset_digest"]
+
+
+def test_fileset_json_fixture_oracle_and_capi():
+    """json.Marshal bytes: the oracle re-derives them, and the C-ABI's host
+    marshaller (no device needed) reproduces them byte for byte."""
+    from reflow_amd import capi
+    for c in G.load("fileset_json.json")["cases"]:
+        v = G.json_to_fs_tree(c["value"])
+        assert v.json().hex() == c["json"], c["name"]
+        assert capi.fileset_marshal_json(v).hex() == c["json"], c["name"]
+        assert O.digest_string(O.sha256(bytes.fromhex(c["json"]))) == c["value_digest"]
+
+
+@pytest.mark.gpu
+def test_gpu_fileset_value_digests_fixture(ctx):
+    cases = G.load("fileset_json.json")["cases"]
+    got = ctx.fileset_value_digests([G.json_to_fs_tree(c["value"]) for c in cases])
+    for c, g in zip(cases, got):
+        assert O.digest_string(g) == c["value_digest"], c["name"]
 
 
 @pytest.mark.gpu
