@@ -234,6 +234,32 @@ int rf_bloom_add_device(rf_bloom *b, const void *d_digests32, uint64_t n, void *
 /* Read back m, k, length and the words (nwords = ceil(length/64) capacity). */
 int rf_bloom_params(rf_bloom *b, uint64_t *m, uint64_t *k, uint64_t *length, uint64_t *nwords);
 int rf_bloom_words(rf_bloom *b, uint64_t *words, uint64_t nwords);
+/* Wire formats out (liveset build side, POST /collect body): Go MarshalJSON
+ * {"m":M,"k":K,"b":"<base64.URLEncoding(BE64 len ‖ BE64 words)>"} (bloom.go:270-273,
+ * bitset.go:693-702) and WriteTo BE64 m ‖ BE64 k ‖ bitset (bloom.go:290-301).
+ * *out_len = bytes needed; RF_EINVAL if cap is short. */
+int rf_bloom_marshal_json(rf_bloom *b, uint8_t *out, uint64_t cap, uint64_t *out_len);
+int rf_bloom_marshal_binary(rf_bloom *b, uint8_t *out, uint64_t cap, uint64_t *out_len);
+/* Repository.Collect (repository/file/repository.go:304-327) over n objects:
+ * dead_idx[0 .. *n_dead) = the indices i, ascending, whose digest the liveset
+ * does not contain (the objects Collect removes); *dead_bytes (may be NULL) =
+ * the sum of their sizes (sizes may be NULL).  n < 2^32. */
+int rf_bloom_collect(rf_bloom *b, const uint8_t *digests32, const int64_t *sizes, uint64_t n,
+                     uint64_t *dead_idx, uint64_t *n_dead, int64_t *dead_bytes);
+/* Device-resident form: d_counts2 receives {n_dead (u64), dead_bytes (i64)}. */
+int rf_bloom_collect_device(rf_bloom *b, const void *d_digests32, const void *d_sizes, uint64_t n,
+                            void *d_dead_idx, void *d_counts2, void *stream);
+
+/* ---- K5: Canonicalize's flowMap (flow.go:814-843, flowMap.Get/Put :881-907) --
+ * canon[i] = min{ j : digests[j] == digests[i] } over n node digests.  With
+ * nodes numbered in the post-order of canonicalize's recursion (the order of
+ * its m.Put calls) this is the flow the reference's first Put registers: the
+ * canonical representative.  *n_unique = |{ i : canon[i] == i }|.  n <= 2^30. */
+int rf_dedup_digests(rf_ctx *ctx, const uint8_t *digests32, uint32_t n, uint32_t *canon,
+                     uint32_t *n_unique);
+/* Device-resident form (digests e.g. gathered from rf_graph slots). */
+int rf_dedup_digests_device(rf_ctx *ctx, const void *d_digests32, uint32_t n, void *d_canon,
+                            void *d_n_unique, void *stream);
 
 #ifdef __cplusplus
 }

@@ -329,6 +329,41 @@ class OFlow:
         return keys
 
 
+def canonicalize(root: OFlow, hashv1: bool = False, universe: bytes = b""):
+    """Flow.Canonicalize (flow.go:814-843) with flowMap.Get/Put (:881-907),
+    restated node for node: Get by the ORIGINAL node's digest before recursing,
+    copy + Config.Merge, canonicalize the deps (then the map flow, which
+    MapInit re-derives through the wrapped MapFunc right after the deps), Put
+    by the copy's digest (first Put wins).  Returns {id(original): original
+    whose copy is canonical for it}; copies are represented by their originals
+    (a copy's digest is its original's under the merged config)."""
+    m = {}       # digest -> original whose copy was Put
+    out = {}
+    memo = {}
+
+    def dig(f, v1):  # Flow.Digest is sync.Once-memoized per node (flow.go:653-664)
+        key = (id(f), v1)
+        if key not in memo:
+            memo[key] = f.digest(universe, v1)
+        return memo[key]
+
+    def rec(f):
+        hit = m.get(dig(f, f.hashv1))
+        if hit is not None:
+            out.setdefault(id(f), hit)
+            return hit
+        for d in f.deps:
+            rec(d)
+        if f.mapflow is not None:
+            rec(f.mapflow)
+        d = dig(f, f.hashv1 or hashv1)
+        got = m.setdefault(d, f)
+        out.setdefault(id(f), got)
+        return got
+    rec(root)
+    return out
+
+
 # --------------------------------------------------------------------------
 # values.WriteDigest subset (values/values.go:290-393) for the values golden
 # --------------------------------------------------------------------------

@@ -33,6 +33,8 @@ EXPORTS = [
     "rf_timer_start", "rf_timer_stop", "rf_comm_unique_id", "rf_comm_init", "rf_comm_destroy",
     "rf_comm_allgather", "rf_comm_allreduce_or", "rf_memcpy_d2d", "rf_graph_gather_device",
     "rf_fileset_marshal_json", "rf_fileset_value_digest_batch",
+    "rf_bloom_marshal_json", "rf_bloom_marshal_binary", "rf_bloom_collect", "rf_bloom_collect_device",
+    "rf_dedup_digests", "rf_dedup_digests_device",
 ]
 
 
@@ -184,6 +186,12 @@ def lib():
             "rf_graph_gather_device": ([vp, vp, u32, vp, vp], i32),
             "rf_fileset_marshal_json": ([vp, u32, vp, u64, vp], i32),
             "rf_fileset_value_digest_batch": ([vp, vp, vp, u64, vp], i32),
+            "rf_bloom_marshal_json": ([vp, vp, u64, vp], i32),
+            "rf_bloom_marshal_binary": ([vp, vp, u64, vp], i32),
+            "rf_bloom_collect": ([vp, vp, vp, u64, vp, vp, vp], i32),
+            "rf_bloom_collect_device": ([vp, vp, vp, u64, vp, vp, vp], i32),
+            "rf_dedup_digests": ([vp, vp, u32, vp, vp], i32),
+            "rf_dedup_digests_device": ([vp, vp, u32, vp, vp, vp], i32),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -310,6 +318,18 @@ class Context:
         _check(lib().rf_fileset_digest_batch(self._h, n, _ptr(sg), _ptr(ge), pp, _ptr(pl),
                                              _ptr(idb), _ptr(out)))
         return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+    def dedup_digests(self, digests: np.ndarray):
+        """Canonicalize's flowMap: (canon[i] = first index with digest i's value, n_unique)."""
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1)
+        n = len(d) // 32
+        canon = np.zeros(max(n, 1), dtype=np.uint32)
+        nu = ctypes.c_uint32(0)
+        _check(lib().rf_dedup_digests(self._h, _ptr(d), n, _ptr(canon), ctypes.byref(nu)))
+        return canon[:n], nu.value
+
+    def dedup_digests_device(self, d_digests, n, d_canon, d_n_unique, stream=None):
+        _check(lib().rf_dedup_digests_device(self._h, d_digests, n, d_canon, d_n_unique, stream))
 
     def fileset_value_digests(self, sets):
         """SHA256(json.Marshal(fs)) per fileset: CacheWrite's assoc values."""
@@ -550,6 +570,35 @@ class Bloom:
         out = np.zeros(nw, dtype=np.uint64)
         _check(lib().rf_bloom_words(self._h, _ptr(out) if nw else None, nw))
         return out
+
+    def _marshal(self, fn) -> bytes:
+        need = ctypes.c_uint64(0)
+        rc = fn(self._h, None, 0, ctypes.byref(need))
+        if rc != RF_OK and need.value == 0:
+            _check(rc)
+        out = ctypes.create_string_buffer(max(need.value, 1))
+        _check(fn(self._h, out, need.value, ctypes.byref(need)))
+        return out.raw[:need.value]
+
+    def marshal_json(self) -> bytes:
+        return self._marshal(lib().rf_bloom_marshal_json)
+
+    def marshal_binary(self) -> bytes:
+        return self._marshal(lib().rf_bloom_marshal_binary)
+
+    def collect(self, digests: np.ndarray, sizes=None):
+        """Repository.Collect over a batch: (ascending dead indices, dead bytes)."""
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1)
+        n = len(d) // 32
+        sz = None if sizes is None else np.ascontiguousarray(sizes, dtype=np.int64)
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        nd, nb = ctypes.c_uint64(0), ctypes.c_int64(0)
+        _check(lib().rf_bloom_collect(self._h, _ptr(d), _ptr(sz), n, _ptr(out), ctypes.byref(nd),
+                                      ctypes.byref(nb)))
+        return out[:nd.value], nb.value
+
+    def collect_device(self, d_digests, d_sizes, n, d_dead_idx, d_counts2, stream=None):
+        _check(lib().rf_bloom_collect_device(self._h, d_digests, d_sizes, n, d_dead_idx, d_counts2, stream))
 
     def close(self):
         if self._h:

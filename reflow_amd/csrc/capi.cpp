@@ -103,7 +103,7 @@ struct rf_ctx {
     int n_cu = 256;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    DevBuf d_arena, d_out, d_tmp;
+    DevBuf d_arena, d_out, d_tmp, d_tab, d_tab2, d_tab3;
     HostBuf h_stage;
     hipEvent_t t0 = nullptr, t1 = nullptr;
 };
@@ -1132,7 +1132,7 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
 struct rf_bloom {
     rf_ctx* ctx = nullptr;
     BloomDev b;
-    DevBuf words, len_dev, keys, out;
+    DevBuf words, len_dev, keys, out, sizes, dead, tiles, idx, nb;
 };
 
 static int bloom_make(rf_ctx* ctx, uint64_t m, uint64_t k, const uint64_t* words, uint64_t nwords,
@@ -1257,8 +1257,7 @@ extern "C" void rf_bloom_destroy(rf_bloom* bl) {
     DevGuard dg(bl->ctx->device);
     bl->words.release();
     bl->len_dev.release();
-    bl->keys.release();
-    bl->out.release();
+    for (DevBuf* d : {&bl->keys, &bl->out, &bl->sizes, &bl->dead, &bl->tiles, &bl->idx, &bl->nb}) d->release();
     delete bl;
 }
 
@@ -1324,5 +1323,153 @@ extern "C" int rf_bloom_words(rf_bloom* bl, uint64_t* words, uint64_t nwords) {
     ARG(nwords <= bl->b.nwords, "nwords exceeds filter capacity");
     DevGuard dg(bl->ctx->device);
     if (nwords) HIPC(hipMemcpy(words, bl->b.words, 8 * nwords, hipMemcpyDeviceToHost));
+    return RF_OK;
+}
+
+// ---- Liveset wire formats out (bloom.go:264-301, bitset.go:623-702) ----------
+// The bitset's words in its binary form: BE64 length ‖ BE64 words, with
+// wordsNeeded(length) words (bitset.go:628-640).
+static int bloom_bitset_bytes(rf_bloom* bl, std::vector<uint8_t>& o) {
+    uint64_t length = 0;
+    HIPC(hipMemcpy(&length, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
+    const uint64_t nw = (length + 63) / 64;
+    if (nw > bl->b.nwords) return fail(RF_EINVAL, "bitset length exceeds filter capacity");
+    std::vector<uint64_t> w(nw);
+    if (nw) HIPC(hipMemcpy(w.data(), bl->b.words, 8 * nw, hipMemcpyDeviceToHost));
+    auto put = [&](uint64_t v) {
+        for (int i = 7; i >= 0; --i) o.push_back((uint8_t)(v >> (8 * i)));
+    };
+    put(length);
+    for (uint64_t x : w) put(x);
+    return RF_OK;
+}
+
+static int copy_out(const std::vector<uint8_t>& o, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    ARG(out_len, "null out_len");
+    *out_len = o.size();
+    if (o.size() > cap) return fail(RF_EINVAL, "output buffer too small: need %zu bytes", o.size());
+    if (!o.empty() && out) memcpy(out, o.data(), o.size());
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_marshal_binary(rf_bloom* bl, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    ARG(bl, "null bloom");
+    DevGuard dg(bl->ctx->device);
+    std::vector<uint8_t> o;
+    for (uint64_t v : {bl->b.m, bl->b.k})  // WriteTo: BE64 m ‖ BE64 k ‖ bitset
+        for (int i = 7; i >= 0; --i) o.push_back((uint8_t)(v >> (8 * i)));
+    int rc = bloom_bitset_bytes(bl, o);
+    return rc ? rc : copy_out(o, out, cap, out_len);
+}
+
+extern "C" int rf_bloom_marshal_json(rf_bloom* bl, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    ARG(bl, "null bloom");
+    DevGuard dg(bl->ctx->device);
+    std::vector<uint8_t> bits;
+    int rc = bloom_bitset_bytes(bl, bits);
+    if (rc) return rc;
+    // json.Marshal(bloomFilterJSON{m, k, b}) with b's MarshalJSON =
+    // json.Marshal(base64.URLEncoding.EncodeToString(bits)) (padded; the
+    // alphabet needs no JSON escaping)
+    static const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+    std::string s = "{\"m\":" + std::to_string(bl->b.m) + ",\"k\":" + std::to_string(bl->b.k) + ",\"b\":\"";
+    size_t i = 0;
+    for (; i + 3 <= bits.size(); i += 3) {
+        const uint32_t v = (uint32_t)bits[i] << 16 | (uint32_t)bits[i + 1] << 8 | bits[i + 2];
+        s += A[v >> 18];
+        s += A[(v >> 12) & 63];
+        s += A[(v >> 6) & 63];
+        s += A[v & 63];
+    }
+    if (bits.size() - i == 1) {
+        const uint32_t v = (uint32_t)bits[i] << 16;
+        s += A[v >> 18];
+        s += A[(v >> 12) & 63];
+        s += "==";
+    } else if (bits.size() - i == 2) {
+        const uint32_t v = (uint32_t)bits[i] << 16 | (uint32_t)bits[i + 1] << 8;
+        s += A[v >> 18];
+        s += A[(v >> 12) & 63];
+        s += A[(v >> 6) & 63];
+        s += '=';
+    }
+    s += "\"}";
+    return copy_out(std::vector<uint8_t>(s.begin(), s.end()), out, cap, out_len);
+}
+
+// ---- Repository.Collect over a batch of objects (repository/file/repository.go:304-327)
+extern "C" int rf_bloom_collect_device(rf_bloom* bl, const void* d_digests32, const void* d_sizes, uint64_t n,
+                                       void* d_dead_idx, void* d_counts2, void* stream) {
+    ARG(bl && (n == 0 || (d_digests32 && d_dead_idx)) && d_counts2, "null argument");
+    ARG(n < (1ull << 32), "collect batch too large (n < 2^32)");
+    DevGuard dg(bl->ctx->device);
+    hipStream_t s = pick(bl->ctx, stream);
+    HIPC(hipMemsetAsync(d_counts2, 0, 16, s));
+    if (!n) return RF_OK;
+    HIPC(bl->dead.ensure(n));
+    HIPC(bl->tiles.ensure(4 * bloom_collect_tiles(n)));
+    HIPC(launch_bloom_collect(bl->b, static_cast<const uint8_t*>(d_digests32),
+                              static_cast<const int64_t*>(d_sizes), n, bl->dead.as<uint8_t>(),
+                              bl->tiles.as<uint32_t>(), static_cast<uint64_t*>(d_dead_idx),
+                              static_cast<uint64_t*>(d_counts2), s));
+    return RF_OK;
+}
+
+extern "C" int rf_bloom_collect(rf_bloom* bl, const uint8_t* digests32, const int64_t* sizes, uint64_t n,
+                                uint64_t* dead_idx, uint64_t* n_dead, int64_t* dead_bytes) {
+    ARG(bl && (n == 0 || (digests32 && dead_idx)) && n_dead, "null argument");
+    rf_ctx* ctx = bl->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    HIPC(bl->keys.ensure(32 * std::max<uint64_t>(n, 1)));
+    HIPC(bl->idx.ensure(8 * std::max<uint64_t>(n, 1)));
+    HIPC(bl->nb.ensure(16));
+    if (n) HIPC(hipMemcpyAsync(bl->keys.p, digests32, 32 * n, hipMemcpyHostToDevice, ctx->stream));
+    if (n && sizes) {
+        HIPC(bl->sizes.ensure(8 * n));
+        HIPC(hipMemcpyAsync(bl->sizes.p, sizes, 8 * n, hipMemcpyHostToDevice, ctx->stream));
+    }
+    int rc = rf_bloom_collect_device(bl, bl->keys.p, sizes ? bl->sizes.p : nullptr, n, bl->idx.p, bl->nb.p,
+                                     ctx->stream);
+    if (rc) return rc;
+    uint64_t nb[2] = {0, 0};
+    HIPC(hipMemcpyAsync(nb, bl->nb.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    if (nb[0]) HIPC(hipMemcpy(dead_idx, bl->idx.p, 8 * nb[0], hipMemcpyDeviceToHost));
+    *n_dead = nb[0];
+    if (dead_bytes) *dead_bytes = (int64_t)nb[1];
+    return RF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// K5: Canonicalize's flowMap (flow.go:814-843, flowMap.Get/Put :881-907)
+extern "C" int rf_dedup_digests_device(rf_ctx* ctx, const void* d_digests32, uint32_t n, void* d_canon,
+                                       void* d_n_unique, void* stream) {
+    ARG(ctx && d_n_unique && (n == 0 || (d_digests32 && d_canon)), "null argument");
+    ARG(n <= (1u << 30), "dedup batch too large (n <= 2^30)");
+    DevGuard dg(ctx->device);
+    HIPC(ctx->d_tab.ensure(4ull * dedup_table_slots(n)));
+    HIPC(ctx->d_tab2.ensure(4ull * std::max<uint32_t>(n, 1)));
+    HIPC(launch_dedup(static_cast<const uint8_t*>(d_digests32), n, ctx->d_tab.as<uint32_t>(),
+                      ctx->d_tab2.as<uint32_t>(), static_cast<uint32_t*>(d_canon),
+                      static_cast<uint32_t*>(d_n_unique), pick(ctx, stream)));
+    return RF_OK;
+}
+
+extern "C" int rf_dedup_digests(rf_ctx* ctx, const uint8_t* digests32, uint32_t n, uint32_t* canon,
+                                uint32_t* n_unique) {
+    ARG(ctx && n_unique && (n == 0 || (digests32 && canon)), "null argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    HIPC(ctx->d_arena.ensure(32ull * std::max<uint32_t>(n, 1)));
+    HIPC(ctx->d_tab3.ensure(4ull * std::max<uint32_t>(n, 1) + 64));
+    uint32_t* d_canon = ctx->d_tab3.as<uint32_t>();
+    uint32_t* d_nu = d_canon + std::max<uint32_t>(n, 1);
+    if (n) HIPC(hipMemcpyAsync(ctx->d_arena.p, digests32, 32ull * n, hipMemcpyHostToDevice, ctx->stream));
+    int rc = rf_dedup_digests_device(ctx, ctx->d_arena.p, n, d_canon, d_nu, ctx->stream);
+    if (rc) return rc;
+    if (n) HIPC(hipMemcpyAsync(canon, d_canon, 4ull * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipMemcpyAsync(n_unique, d_nu, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
     return RF_OK;
 }

@@ -89,4 +89,11 @@ hipError_t launch_bloom_collect(const BloomDev& b, const uint8_t* d32, const int
                                 uint8_t* dead, uint32_t* tile_count, uint64_t* out_idx, uint64_t* nb2,
                                 hipStream_t s);
 
+// ---- K5: digest-keyed hash table (Canonicalize's flowMap) --------------------
+uint32_t dedup_table_slots(uint32_t n);
+// canon[i] = min{j : dig[j] == dig[i]}; table [dedup_table_slots(n)] and
+// slot_of [n] are scratch; *n_unique = |{i : canon[i] == i}|.
+hipError_t launch_dedup(const uint8_t* dig, uint32_t n, uint32_t* table, uint32_t* slot_of, uint32_t* canon,
+                        uint32_t* n_unique, hipStream_t s);
+
 }  // namespace rf

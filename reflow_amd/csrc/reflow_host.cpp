@@ -519,15 +519,20 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
     Eval ev(e, U);
     ev.Add(croot);
     ev.Build();
-    // 3. flowMap.Put: first copy with a digest wins; deps re-pointed at it
-    //    (equal digests by construction, so digests do not change)
-    std::unordered_map<Digest, Flow*, DigestHash> m;
-    std::unordered_map<Flow*, Flow*> canon;
-    for (Flow* c : post) {
-        const Digest d = ev.FlowDigest(c);
-        auto it = m.find(d);
-        canon[c] = (it == m.end()) ? (m[d] = c) : it->second;
+    // 3. flowMap.Put: first copy with a digest wins (K5 on the device: the
+    //    smallest post-order index of each digest class); deps re-pointed at
+    //    it (equal digests by construction, so digests do not change)
+    std::vector<uint8_t> digs(32 * post.size());
+    for (size_t i = 0; i < post.size(); ++i) {
+        const Digest d = ev.FlowDigest(post[i]);
+        memcpy(&digs[32 * i], d.b.data(), 32);
     }
+    std::vector<uint32_t> first(post.size());
+    uint32_t n_unique = 0;
+    if (!post.empty())
+        Check(rf_dedup_digests(e.ctx(), digs.data(), (uint32_t)post.size(), first.data(), &n_unique));
+    std::unordered_map<Flow*, Flow*> canon;
+    for (size_t i = 0; i < post.size(); ++i) canon[post[i]] = post[first[i]];
     for (Flow* c : post) {
         for (Flow*& d : c->Deps) d = canon[d];
         if (c->MapFlow) c->MapFlow = canon[c->MapFlow];
