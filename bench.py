@@ -262,8 +262,45 @@ def bench_dag(args, dist, ctx, comm):
     ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
     res["roofline_full"] = {"bound": "valu", "achieved": round(ach, 2), "peak": round(SHA_VALU_PEAK_GBS, 1),
                             "unit": "GB/s", "frac": round(ach / SHA_VALU_PEAK_GBS, 4)}
+    res["canonicalize"] = bench_canon(ctx, g, dag)
     g.close()
     return res, dag
+
+
+def bench_canon(ctx, g, dag):
+    """K5: Canonicalize's flowMap over every node digest of the C3 DAG, as a
+    program that builds the shared reference-index chain (Intern -> Exec(bwa
+    index) -> Coerce) once per sample would hand it to Flow.Canonicalize: S
+    copies of those three nodes, then every other node, in construction order
+    (each kind reads only earlier ones)."""
+    ref = np.concatenate([dag.kinds[k].out_slot for k in ("R0", "R1", "R2")]).astype(np.uint32)
+    rest = [np.asarray(k.out_slot, dtype=np.uint32) for name, k in dag.kinds.items()
+            if name not in ("R0", "R1", "R2") and not name.startswith("p")]  # logical digests only
+    slots = np.concatenate([np.tile(ref, dag.S)] + rest)
+    n = len(slots)
+    d_idx = ctx.upload(slots)
+    d_dig, d_canon, d_nu = ctx.alloc(32 * n), ctx.alloc(4 * n), ctx.alloc(64)
+    g.gather_device(d_idx.ptr, n, d_dig.ptr, ctx.stream)
+    ctx.dedup_digests_device(d_dig.ptr, n, d_canon.ptr, d_nu.ptr)  # warm (allocates the table)
+    times = []
+    for _ in range(5):
+        ctx.timer_start()
+        ctx.dedup_digests_device(d_dig.ptr, n, d_canon.ptr, d_nu.ptr)
+        times.append(ctx.timer_stop())
+    nu = int(d_nu.to_numpy()[:4].view(np.uint32)[0])
+    canon = d_canon.to_numpy().view(np.uint32)
+    ms = float(np.median(times))
+    # every ref copy maps to the first; no other duplicates in the 1000align DAG
+    ok = nu == dag.n_nodes and n == dag.n_nodes + 3 * (dag.S - 1) and bool((canon[:3 * dag.S].reshape(dag.S, 3) == np.arange(3)).all())
+    # random accesses per node: insert = slot read + CAS (+ a 32-B compare read
+    # on a hit), resolve = one slot read -> ~3 random 4..32-B touches per node
+    res = {"workload": "dedup of %d node digests (C3 DAG + %d duplicated ref-index nodes)" % (n, 3 * (dag.S - 1)),
+           "ms": ms, "mnodes_per_s": n / (ms * 1e-3) / 1e6, "unique": nu, "parity_ok": ok,
+           "random_accesses_per_node": 3,
+           "achieved_g_accesses_per_s": round(3 * n / (ms * 1e-3) / 1e9, 2)}
+    for b in (d_idx, d_dig, d_canon, d_nu):
+        b.free()
+    return res
 
 
 # --------------------------------------------------------------- C5: probe --
@@ -309,10 +346,23 @@ def bench_probe(args, dist, ctx):
     reads = hits * k + absent * sum(f ** j for j in range(k))
     gread_s = reads / (dev_ms * 1e-3) / 1e9
     ceil = gather_ceiling(m // 8, n_probe // 4, k)
+    # Repository.Collect over the same 1e9 keys as repository objects: probe +
+    # ordered compaction of the dead ones (repository/file/repository.go:304-327)
+    d_dead, d_cnt = ctx.alloc(8 * n_probe), ctx.alloc(64)
+    b.collect_device(keys.ptr, None, n_probe, d_dead.ptr, d_cnt.ptr, ctx.stream)
+    ctx.timer_start()
+    b.collect_device(keys.ptr, None, n_probe, d_dead.ptr, d_cnt.ptr, ctx.stream)
+    coll_ms = ctx.timer_stop()
+    n_dead = int(d_cnt.to_numpy()[:8].view(np.uint64)[0])
+    d_dead.free()
+    d_cnt.free()
     res = {"workload": "bloomlive probe: n=%d keys (m=%d bits, %.1f MiB, k=%d), %d probes (50%% present)"
                        % (n_ins, m, m / 8 / 2**20, k, n_probe),
            "gprobes_per_s": dist.sum(n_probe) * args.probe_steps / t / 1e9,
            "device_ms": dev_ms, "add_ms": add_ms, "false_positive_rate": fp,
+           "collect": {"objects": n_probe, "dead": n_dead, "dead_matches_probe": n_dead == n_probe - hits,
+                       "ms": coll_ms, "g_objects_per_s": n_probe / (coll_ms * 1e-3) / 1e9,
+                       "overhead_vs_probe": round(coll_ms / dev_ms, 3)},
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_probe": bpp,
                         "traffic": traffic, "traffic_source": tsrc,

@@ -200,29 +200,34 @@ __global__ __launch_bounds__(kCollectBlock) void k4_collect_mark(
     }
 }
 
-// Exclusive scan of the tile counts by one block; total -> *n_dead.
+// Exclusive scan of the tile counts by one block, 1024 coalesced counts per
+// pass (wave scans by shuffles, wave totals through LDS, a running carry);
+// total -> *n_dead.
 __global__ __launch_bounds__(1024) void k4_collect_scan(uint32_t* __restrict__ tile_count, uint64_t tiles,
                                                         unsigned long long* __restrict__ n_dead) {
-    __shared__ unsigned long long s[1024];
-    const uint64_t per = (tiles + 1023) / 1024;
-    const uint64_t b = threadIdx.x * per, e = b + per < tiles ? b + per : tiles;
-    unsigned long long sum = 0;
-    for (uint64_t t = b; t < e; ++t) sum += tile_count[t];
-    s[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive
-        const unsigned long long v = threadIdx.x >= o ? s[threadIdx.x - o] : 0ull;
+    __shared__ uint32_t s_w[16];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long carry = 0;
+    for (uint64_t b = 0; b < tiles; b += 1024) {
+        const uint64_t t = b + threadIdx.x;
+        const uint32_t c = t < tiles ? tile_count[t] : 0u;
+        uint32_t x = c;  // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) s_w[wave] = x;
         __syncthreads();
-        s[threadIdx.x] += v;
+        uint32_t before = 0, total = 0;
+        for (uint32_t w = 0; w < 16; ++w) {
+            before += w < wave ? s_w[w] : 0u;
+            total += s_w[w];
+        }
+        if (t < tiles) tile_count[t] = (uint32_t)(carry + before + x - c);  // < 2^32: n < 2^32
+        carry += total;
         __syncthreads();
     }
-    unsigned long long run = s[threadIdx.x] - sum;
-    for (uint64_t t = b; t < e; ++t) {
-        const uint32_t c = tile_count[t];
-        tile_count[t] = (uint32_t)run;  // offsets fit: n_dead < 2^32 is checked on the host
-        run += c;
-    }
-    if (threadIdx.x == 1023) *n_dead = s[1023];
+    if (threadIdx.x == 0) *n_dead = carry;
 }
 
 __global__ __launch_bounds__(kCollectBlock) void k4_collect_scatter(const uint8_t* __restrict__ dead,
