@@ -201,6 +201,68 @@ def bench_sha(args, dist, ctx):
     return res
 
 
+# -------------------------------------------------- C1: reference config --
+C1_N, C1_LEN, C1_SEED = 4096, 262144, 0x5EED0001
+
+
+def c1_path(i):
+    return ("d%02d/f%04d.fq.gz" % (i // 64, i)).encode()
+
+
+def bench_c1(args, dist, ctx):
+    """configs[0], the reference's own CPU-runnable case, on the GPU: digest
+    1 GiB = 4096 x 256 KiB files (HBM-resident, File IDs on K1), the Fileset
+    digest of the 4096-entry map (executor.go:205-233; host material + K1,
+    File IDs read back), and CacheKeys of a ~10k-node 1000align DAG (K2 full
+    recompute).  Checked against the committed fixture tests/golden/c1_fileset.json."""
+    lens = np.full(C1_N, C1_LEN, dtype=np.uint64)
+    offs, arena_bytes = arena_layout(lens)
+    arena = ctx.alloc(arena_bytes)
+    d_offs, d_lens = ctx.upload(offs), ctx.upload(lens)
+    out = ctx.alloc(32 * C1_N)
+    ctx.gen_fill(arena.ptr, d_offs.ptr, d_lens.ptr, C1_N, C1_SEED, arena_bytes)
+    ctx.sync()
+    plan = ctx.sha_plan(offs, lens, 0)
+    plan.run(arena.ptr, out.ptr)
+    ctx.sync()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        plan.run(arena.ptr, out.ptr)
+    ctx.sync()
+    ids_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    ids = out.to_numpy().reshape(-1, 32)
+    fsd = ctx.fileset_digest_batch([[[(c1_path(i), ids[i].tobytes()) for i in range(C1_N)]]])[0]
+    fs_ms = (time.perf_counter() - t0) * 1e3
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "c1_fileset.json")))
+    ok = ("sha256:" + fsd.hex() == want["fileset_digest"] and
+          __import__("hashlib").sha256(ids.tobytes()).hexdigest() == want["ids_sha256"])
+    plan.close()
+    for b in (arena, d_offs, d_lens, out):
+        b.free()
+    # CacheKeys over a ~10k-node DAG (S*(14P+5) nodes at P=32)
+    small = Dag1000(22, 32)
+    a = small.arrays()
+    g = capi.Graph(ctx, a["n_slots"], a["out_slot"], a["tmpl_off"], a["tmpl_len"], a["hole_ptr"],
+                   a["hole_pos"], a["hole_slot"], a["blob"])
+    g.set_slots(small.file_slots, small.leaf_ids)
+    g.recompute(full=True)  # captures the hipGraph
+    ctx.timer_start()
+    for _ in range(reps):
+        g.recompute(full=True)
+    dag_ms = ctx.timer_stop() / reps
+    g.close()
+    return {"workload": "configs[0]: 4096 x 256 KiB files (1 GiB) -> File IDs + Fileset digest; CacheKeys "
+                        "of a %d-node 1000align DAG (%d jobs)" % (small.n_nodes, small.n_jobs),
+            "file_ids_ms": ids_ms, "file_ids_gbps": C1_N * C1_LEN / (ids_ms * 1e-3) / 1e9,
+            "fileset_digest_ms": fs_ms, "fixture_match": ok,
+            "dag_nodes": small.n_nodes, "dag_full_recompute_ms": dag_ms,
+            "total_ms": ids_ms + fs_ms + dag_ms,
+            "note": "4096 messages fill 64 waves: the per-file chain (4097 blocks, lane mode) bounds the "
+                    "file-ID time, not chip throughput"}
+
+
 # ------------------------------------------------------- C3: incremental --
 def bench_dag(args, dist, ctx, comm):
     S = args.dag_samples
@@ -356,10 +418,12 @@ def bench_probe(args, dist, ctx):
     n_dead = int(d_cnt.to_numpy()[:8].view(np.uint64)[0])
     d_dead.free()
     d_cnt.free()
+    assoc = bench_assoc(ctx, keys, n_ins, n_probe, hits)
     res = {"workload": "bloomlive probe: n=%d keys (m=%d bits, %.1f MiB, k=%d), %d probes (50%% present)"
                        % (n_ins, m, m / 8 / 2**20, k, n_probe),
            "gprobes_per_s": dist.sum(n_probe) * args.probe_steps / t / 1e9,
            "device_ms": dev_ms, "add_ms": add_ms, "false_positive_rate": fp,
+           "assoc": assoc,
            "collect": {"objects": n_probe, "dead": n_dead, "dead_matches_probe": n_dead == n_probe - hits,
                        "ms": coll_ms, "g_objects_per_s": n_probe / (coll_ms * 1e-3) / 1e9,
                        "overhead_vs_probe": round(coll_ms / dev_ms, 3)},
@@ -378,6 +442,42 @@ def bench_probe(args, dist, ctx):
         x.free()
     b.close()
     return res
+
+
+def bench_assoc(ctx, keys, n_ins, n_probe, hits):
+    """HBM assoc behind the probe (assoc.Assoc, assoc/assoc.go:26-38): the
+    n_ins inserted cache keys Put with values, then a Get of all n_probe keys
+    (the probe's positives resolve to values, the rest are NotExist)."""
+    a = capi.Assoc(ctx, capacity=n_ins)
+    vals = ctx.alloc(32 * n_ins)
+    v_off, v_len = ctx.upload(np.array([0], np.uint64)), ctx.upload(np.array([32 * n_ins], np.uint64))
+    ctx.gen_fill(vals.ptr, v_off.ptr, v_len.ptr, 1, 0x5EED0006, 32 * n_ins)
+    st = ctx.alloc(4 * n_ins)
+    ctx.sync()
+    v_off.free()
+    v_len.free()
+    t0 = time.perf_counter()
+    a.put_device(0, keys.ptr, vals.ptr, n_ins, st.ptr)
+    put_s = time.perf_counter() - t0
+    ok_put = not st.to_numpy(np.int32).any()
+    d_v, d_f = ctx.alloc(32 * n_probe), ctx.alloc(n_probe)
+    a.get_device(0, keys.ptr, n_probe, d_v.ptr, d_f.ptr)
+    ctx.timer_start()
+    a.get_device(0, keys.ptr, n_probe, d_v.ptr, d_f.ptr)
+    get_ms = ctx.timer_stop()
+    found = int(d_f.to_numpy().astype(np.int64).sum())
+    occ, cap = a.stats()
+    for b in (vals, st, d_v, d_f):
+        b.free()
+    a.close()
+    # bytes per Get: 32-B key read + a 4-B tag and a 32-B key compare (random)
+    # + a 32-B value read (random, hits) + 33-B result write
+    return {"workload": "Put %d keys (one batch), Get %d keys (%d present)" % (n_ins, n_probe, found),
+            "put_ms": put_s * 1e3, "put_mkeys_per_s": n_ins / put_s / 1e6, "put_ok": ok_put,
+            "get_ms": get_ms, "get_g_keys_per_s": n_probe / (get_ms * 1e-3) / 1e9,
+            "found_exact": found == (n_probe // 2) // n_ins * n_ins,  # every Put key, no false positive
+            "bloom_false_positives_resolved": hits - found,
+            "table_slots": cap, "occupied": occ}
 
 
 def gather_ceiling(table_bytes, n_threads, reads):
@@ -460,6 +560,24 @@ def cpu_baseline(args, sha, dag):
                       "seconds": dt2, "gpu_digests_match": ok2,
                       "sha_ni": "sha_ni" in open("/proc/cpuinfo").read()}
     del mv, arena
+    # configs[0] on the CPU port and OpenSSL (the reference's own CPU case)
+    c1l = np.full(C1_N, C1_LEN, dtype=np.uint64)
+    c1o, c1t = arena_layout(c1l, align=64)
+    c1a = np.zeros(c1t, dtype=np.uint8)
+    L.orc_fill_batch(C1_SEED, c1a.ctypes.data, c1o.ctypes.data, c1l.ctypes.data, C1_N, threads)
+    c1out = np.zeros((C1_N, 32), dtype=np.uint8)
+    t0 = time.perf_counter()
+    L.orc_sha256_batch(c1a.ctypes.data, c1o.ctypes.data, c1l.ctypes.data, C1_N, c1out.ctypes.data, threads)
+    c1_port = time.perf_counter() - t0
+    c1mv = memoryview(c1a)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda i: hashlib.sha256(c1mv[int(c1o[i]):int(c1o[i]) + C1_LEN]).digest(), range(C1_N)))
+    c1_ssl = time.perf_counter() - t0
+    res["c1"] = {"sample": "configs[0] in full: 4096 x 256 KiB", "port_ms": c1_port * 1e3,
+                 "port_gbps": C1_N * C1_LEN / c1_port / 1e9, "openssl_ms": c1_ssl * 1e3,
+                 "openssl_gbps": C1_N * C1_LEN / c1_ssl / 1e9, "cores": threads}
+    del c1mv, c1a
     # C3 port: full recompute of a bounded sample DAG, 1 thread (Canonicalize is serial)
     if dag is not None:
         small = Dag1000(max(1, args.cpu_dag_samples), dag.P)
@@ -497,7 +615,7 @@ def main():
     ap.add_argument("--probe-steps", type=int, default=3)
     ap.add_argument("--cpu-sample-gib", type=float, default=20.0)
     ap.add_argument("--cpu-dag-samples", type=int, default=200)
-    ap.add_argument("--skip", default="", help="comma list of: dag,probe,cpu")
+    ap.add_argument("--skip", default="", help="comma list of: c1,dag,probe,cpu")
     args = ap.parse_args()
     skip = set(filter(None, args.skip.split(",")))
 
@@ -509,6 +627,7 @@ def main():
         comm = capi.Comm(ctx, dist.world, dist.rank, uid)
 
     sha = bench_sha(args, dist, ctx)
+    c1 = None if "c1" in skip else bench_c1(args, dist, ctx)
     dag_res, dag = (None, None)
     if "dag" not in skip:
         dag_res, dag = bench_dag(args, dist, ctx, comm)
@@ -530,6 +649,7 @@ def main():
                        "parallelism": "files sharded per GPU (independent); RCCL only for DAG root digests"},
             "roofline": sha["roofline"],
             "cpu_baseline": cpu,
+            "c1": c1,
             "incremental": dag_res,
             "probe": probe,
         }

@@ -40,13 +40,15 @@ typedef enum {
     RF_EINTEGRITY = 3, /* errors.Integrity: digest mismatch on verify        */
     RF_EDEVICE = 4,    /* errors.Unavailable: HIP runtime / device failure   */
     RF_ENOMEM = 5,     /* errors.ResourcesExhausted: HBM or host allocation  */
-    RF_ENOTFOUND = 6   /* errors.NotExist                                     */
+    RF_ENOTFOUND = 6,  /* errors.NotExist                                     */
+    RF_EPRECONDITION = 7 /* errors.Precondition: assoc compare-and-set failed */
 } rf_status;
 
 typedef struct rf_ctx rf_ctx;
 typedef struct rf_sha_plan rf_sha_plan;
 typedef struct rf_graph rf_graph;
 typedef struct rf_bloom rf_bloom;
+typedef struct rf_assoc rf_assoc;
 
 /* ---- context ----------------------------------------------------------- */
 /* Bind a context to HIP device `device` (one process per GPU).  Replaces the
@@ -260,6 +262,36 @@ int rf_dedup_digests(rf_ctx *ctx, const uint8_t *digests32, uint32_t n, uint32_t
 /* Device-resident form (digests e.g. gathered from rf_graph slots). */
 int rf_dedup_digests_device(rf_ctx *ctx, const void *d_digests32, uint32_t n, void *d_canon,
                             void *d_n_unique, void *stream);
+
+/* ---- HBM assoc (assoc.Assoc, assoc/assoc.go:26-38) -----------------------
+ * A digest -> digest map per kind in HBM with the semantics of the in-memory
+ * assoc (test/testutil/assoc.go:34-56): the cache tier behind the probe, in
+ * front of DynamoDB (assoc/dydbassoc).  Batched. */
+int rf_assoc_new(rf_ctx *ctx, uint64_t capacity, rf_assoc **out);
+void rf_assoc_destroy(rf_assoc *a);
+/* Put, op i in batch order (ops on one key apply in index order): if
+ * expect32 (may be NULL) row i is nonzero and the current value differs,
+ * status[i] = RF_EPRECONDITION and nothing changes; else the value becomes
+ * vals32[i] (all-zero deletes) and status[i] = RF_OK. */
+int rf_assoc_put(rf_assoc *a, int kind, const uint8_t *expect32, const uint8_t *keys32,
+                 const uint8_t *vals32, uint64_t n, int32_t *status);
+/* Device-resident form (d_status: int32 per op); returns when applied. */
+int rf_assoc_put_device(rf_assoc *a, int kind, const void *d_expect32, const void *d_keys32,
+                        const void *d_vals32, uint64_t n, void *d_status);
+/* Get: found[i] = 1 and vals32[i] = the value, or found[i] = 0 (NotExist,
+ * vals32[i] zeroed). */
+int rf_assoc_get(rf_assoc *a, int kind, const uint8_t *keys32, uint64_t n, uint8_t *vals32,
+                 uint8_t *found);
+int rf_assoc_get_device(rf_assoc *a, int kind, const void *d_keys32, uint64_t n, void *d_vals32,
+                        void *d_found, void *stream);
+/* Abbreviated keys (dydbassoc.go:111-147, ID4 index + Digest.Expands): key i
+ * is given by its first nhex[i] hex digits (8..64) in keys32 row i.  status
+ * RF_OK with the expanded key and its value, RF_ENOTFOUND, or RF_EINVAL when
+ * more than one key matches. */
+int rf_assoc_get_abbrev(rf_assoc *a, int kind, const uint8_t *keys32, const uint8_t *nhex, uint64_t n,
+                        uint8_t *keys_out32, uint8_t *vals32, int32_t *status);
+/* Occupied slots (live + deleted keys) and table capacity. */
+int rf_assoc_stats(rf_assoc *a, uint64_t *occupied, uint64_t *capacity);
 
 #ifdef __cplusplus
 }

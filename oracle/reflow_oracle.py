@@ -364,6 +364,39 @@ def canonicalize(root: OFlow, hashv1: bool = False, universe: bytes = b""):
     return out
 
 
+class InmemoryAssoc:
+    """test/testutil/assoc.go:16-56 (NewInmemoryAssoc): (kind, key) -> value;
+    Put with a nonzero expect is a compare-and-set (errors.Precondition), a
+    zero value deletes; Get of a missing key is errors.NotExist.  Abbreviated
+    keys follow assoc/dydbassoc/dydbassoc.go:111-147 (ID4 narrowing, then
+    Digest.Expands = the full key's hex starts with the abbreviation's)."""
+    ZERO = bytes(32)
+
+    def __init__(self):
+        self.m = {}
+
+    def put(self, kind, expect, k, v):
+        key = (kind, k)
+        if expect is not None and expect != self.ZERO and self.m.get(key, self.ZERO) != expect:
+            return "precondition"
+        if v == self.ZERO:
+            self.m.pop(key, None)
+        else:
+            self.m[key] = v
+        return "ok"
+
+    def get(self, kind, k):
+        return self.m.get((kind, k))  # None = NotExist
+
+    def get_abbrev(self, kind, prefix_hex: str):
+        hits = [(k, v) for (kd, k), v in self.m.items() if kd == kind and k.hex().startswith(prefix_hex)]
+        if not hits:
+            return "notexist", None
+        if len(hits) > 1:
+            return "invalid", None  # "more than one key matched"
+        return "ok", hits[0]
+
+
 # --------------------------------------------------------------------------
 # values.WriteDigest subset (values/values.go:290-393) for the values golden
 # --------------------------------------------------------------------------

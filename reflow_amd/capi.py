@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libreflow_hip.so")
 
-RF_OK, RF_EINVAL, RF_EIO, RF_EINTEGRITY, RF_EDEVICE, RF_ENOMEM, RF_ENOTFOUND = range(7)
+RF_OK, RF_EINVAL, RF_EIO, RF_EINTEGRITY, RF_EDEVICE, RF_ENOMEM, RF_ENOTFOUND, RF_EPRECONDITION = range(8)
 RF_SHA_NO_SOLO = 1
 RF_SHA_ALL_SOLO = 2
 RF_SHA_ONE_LANE_CHAIN = 4
@@ -35,6 +35,8 @@ EXPORTS = [
     "rf_fileset_marshal_json", "rf_fileset_value_digest_batch",
     "rf_bloom_marshal_json", "rf_bloom_marshal_binary", "rf_bloom_collect", "rf_bloom_collect_device",
     "rf_dedup_digests", "rf_dedup_digests_device",
+    "rf_assoc_new", "rf_assoc_destroy", "rf_assoc_put", "rf_assoc_get", "rf_assoc_get_device",
+    "rf_assoc_get_abbrev", "rf_assoc_stats", "rf_assoc_put_device",
 ]
 
 
@@ -192,6 +194,13 @@ def lib():
             "rf_bloom_collect_device": ([vp, vp, vp, u64, vp, vp, vp], i32),
             "rf_dedup_digests": ([vp, vp, u32, vp, vp], i32),
             "rf_dedup_digests_device": ([vp, vp, u32, vp, vp, vp], i32),
+            "rf_assoc_new": ([vp, u64, vp], i32), "rf_assoc_destroy": ([vp], None),
+            "rf_assoc_put": ([vp, i32, vp, vp, vp, u64, vp], i32),
+            "rf_assoc_get": ([vp, i32, vp, u64, vp, vp], i32),
+            "rf_assoc_get_device": ([vp, i32, vp, u64, vp, vp, vp], i32),
+            "rf_assoc_get_abbrev": ([vp, i32, vp, vp, u64, vp, vp, vp], i32),
+            "rf_assoc_stats": ([vp, vp, vp], i32),
+            "rf_assoc_put_device": ([vp, i32, vp, vp, vp, u64, vp], i32),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -603,6 +612,64 @@ class Bloom:
     def close(self):
         if self._h:
             lib().rf_bloom_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Assoc:
+    """HBM assoc (assoc.Assoc with the in-memory assoc's semantics)."""
+
+    def __init__(self, ctx: Context, capacity=1024):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        _check(lib().rf_assoc_new(ctx.handle, capacity, ctypes.byref(self._h)))
+
+    def put(self, kind, keys, vals, expect=None) -> np.ndarray:
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        v = np.ascontiguousarray(vals, dtype=np.uint8).reshape(-1)
+        e = None if expect is None else np.ascontiguousarray(expect, dtype=np.uint8).reshape(-1)
+        n = len(k) // 32
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        _check(lib().rf_assoc_put(self._h, kind, _ptr(e), _ptr(k), _ptr(v), n, _ptr(st)))
+        return st[:n]
+
+    def get(self, kind, keys):
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = len(k) // 32
+        vals = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        found = np.zeros(max(n, 1), dtype=np.uint8)
+        _check(lib().rf_assoc_get(self._h, kind, _ptr(k), n, _ptr(vals), _ptr(found)))
+        return vals[:n], found[:n]
+
+    def put_device(self, kind, d_keys, d_vals, n, d_status, d_expect=None):
+        _check(lib().rf_assoc_put_device(self._h, kind, d_expect, d_keys, d_vals, n, d_status))
+
+    def get_device(self, kind, d_keys, n, d_vals, d_found, stream=None):
+        _check(lib().rf_assoc_get_device(self._h, kind, d_keys, n, d_vals, d_found, stream))
+
+    def get_abbrev(self, kind, keys, nhex):
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = len(k) // 32
+        nh = np.ascontiguousarray(nhex, dtype=np.uint8)
+        ko = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        vo = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        _check(lib().rf_assoc_get_abbrev(self._h, kind, _ptr(k), _ptr(nh), n, _ptr(ko), _ptr(vo), _ptr(st)))
+        return ko[:n], vo[:n], st[:n]
+
+    def stats(self):
+        o, c = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().rf_assoc_stats(self._h, ctypes.byref(o), ctypes.byref(c)))
+        return o.value, c.value
+
+    def close(self):
+        if self._h:
+            lib().rf_assoc_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):

@@ -1473,3 +1473,242 @@ extern "C" int rf_dedup_digests(rf_ctx* ctx, const uint8_t* digests32, uint32_t 
     HIPC(hipStreamSynchronize(ctx->stream));
     return RF_OK;
 }
+
+// ---------------------------------------------------------------------------
+// HBM assoc (assoc.Assoc, assoc/assoc.go:26-38; test/testutil/assoc.go:34-56)
+struct rf_assoc {
+    rf_ctx* ctx = nullptr;
+    uint32_t cap = 0;
+    DevBuf tag, keys, vals, count;                                   // the table
+    DevBuf b_keys, b_vals, b_exp, b_canon, b_aslot, b_cls, b_rem, b_next, b_cnt, b_status, b_found;  // batch scratch
+    AssocView view() {
+        return AssocView{tag.as<uint32_t>(), keys.as<uint4>(), vals.as<uint4>(), cap - 1, count.as<uint32_t>()};
+    }
+};
+
+static hipError_t assoc_alloc_table(rf_assoc* a, uint32_t cap, hipStream_t s) {
+    hipError_t e;
+    if ((e = a->tag.ensure(4ull * cap)) != hipSuccess || (e = a->keys.ensure(32ull * cap)) != hipSuccess ||
+        (e = a->vals.ensure(32ull * cap)) != hipSuccess || (e = a->count.ensure(64)) != hipSuccess)
+        return e;
+    a->cap = cap;
+    if ((e = hipMemsetAsync(a->tag.p, 0, 4ull * cap, s)) != hipSuccess) return e;
+    return hipMemsetAsync(a->count.p, 0, 4, s);
+}
+
+extern "C" int rf_assoc_new(rf_ctx* ctx, uint64_t capacity, rf_assoc** out) {
+    ARG(ctx && out, "null argument");
+    ARG(capacity < (1ull << 30), "assoc capacity too large");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    auto* a = new rf_assoc();
+    a->ctx = ctx;
+    uint32_t cap = 1024;
+    while (cap < 2 * capacity) cap <<= 1;
+    hipError_t e = assoc_alloc_table(a, cap, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        delete a;
+        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "assoc alloc: %s", hipGetErrorString(e));
+    }
+    *out = a;
+    return RF_OK;
+}
+
+extern "C" void rf_assoc_destroy(rf_assoc* a) {
+    if (!a) return;
+    DevGuard dg(a->ctx->device);
+    for (DevBuf* d : {&a->tag, &a->keys, &a->vals, &a->count, &a->b_keys, &a->b_vals, &a->b_exp, &a->b_canon,
+                      &a->b_aslot, &a->b_cls, &a->b_rem, &a->b_next, &a->b_cnt, &a->b_status, &a->b_found})
+        d->release();
+    delete a;
+}
+
+// keep the table at most half full after inserting up to `incoming` new keys
+static int assoc_reserve(rf_assoc* a, uint64_t incoming) {
+    rf_ctx* ctx = a->ctx;
+    uint32_t used = 0;
+    HIPC(hipMemcpyAsync(&used, a->count.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    const uint64_t need = (uint64_t)used + incoming;
+    if (2 * need <= a->cap) return RF_OK;
+    uint64_t cap = a->cap;
+    while (cap < 2 * need) cap <<= 1;
+    ARG(cap <= (1ull << 31), "assoc table would exceed 2^31 slots");
+    rf_assoc old;  // move the old table out
+    std::swap(old.tag, a->tag);
+    std::swap(old.keys, a->keys);
+    std::swap(old.vals, a->vals);
+    std::swap(old.count, a->count);
+    old.cap = a->cap;
+    HIPC(assoc_alloc_table(a, (uint32_t)cap, ctx->stream));
+    HIPC(launch_assoc_rehash(old.view(), old.cap, a->view(), ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    old.tag.release();
+    old.keys.release();
+    old.vals.release();
+    old.count.release();
+    return RF_OK;
+}
+
+// Put over device-resident keys / values / expects (d_status: int32 per op).
+static int assoc_put_locked(rf_assoc* a, int kind, const uint8_t* d_exp, const uint8_t* d_keys, const uint8_t* d_vals,
+                            uint64_t n, int32_t* d_status) {
+    rf_ctx* ctx = a->ctx;
+    hipStream_t s = ctx->stream;
+    int rc = assoc_reserve(a, n);
+    if (rc) return rc;
+    HIPC(a->b_canon.ensure(4 * n + 64));
+    HIPC(a->b_aslot.ensure(4 * n));
+    HIPC(a->b_cls.ensure(8 * n));
+    HIPC(a->b_rem.ensure(4 * n));
+    HIPC(a->b_next.ensure(4 * n));
+    HIPC(a->b_cnt.ensure(64));
+    // distinct keys of the batch (K5 dedup), then find-or-insert them
+    uint32_t* canon = a->b_canon.as<uint32_t>();
+    uint32_t* d_nu = canon + n;
+    HIPC(ctx->d_tab.ensure(4ull * dedup_table_slots((uint32_t)n)));
+    HIPC(ctx->d_tab2.ensure(4ull * n));
+    HIPC(launch_dedup(d_keys, (uint32_t)n, ctx->d_tab.as<uint32_t>(), ctx->d_tab2.as<uint32_t>(), canon, d_nu, s));
+    HIPC(launch_assoc_insert(a->view(), (uint32_t)kind, d_keys, canon, (uint32_t)n, a->b_aslot.as<uint32_t>(), s));
+    // ops in batch order per key: round r applies each key's r-th op
+    std::vector<uint32_t> iota(n);
+    std::iota(iota.begin(), iota.end(), 0u);
+    HIPC(hipMemcpyAsync(a->b_rem.p, iota.data(), 4 * n, hipMemcpyHostToDevice, s));
+    HIPC(hipMemsetAsync(a->b_cls.p, 0, 8 * n, s));
+    uint32_t* cnt = a->b_cnt.as<uint32_t>();  // cnt[0] = remaining, cnt[1] = next
+    uint32_t n_rem = (uint32_t)n;
+    HIPC(hipMemcpyAsync(cnt, &n_rem, 4, hipMemcpyHostToDevice, s));
+    uint32_t* rem = a->b_rem.as<uint32_t>();
+    uint32_t* next = a->b_next.as<uint32_t>();
+    for (uint32_t round = 1; n_rem; ++round) {
+        HIPC(hipMemsetAsync(cnt + 1, 0, 4, s));
+        HIPC(launch_assoc_round(a->view(), rem, cnt, n_rem, canon, (unsigned long long*)a->b_cls.p, round,
+                                a->b_aslot.as<uint32_t>(), d_exp, d_vals, d_status, next, cnt + 1, s));
+        HIPC(hipMemcpyAsync(&n_rem, cnt + 1, 4, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        HIPC(hipMemcpyAsync(cnt, cnt + 1, 4, hipMemcpyDeviceToDevice, s));
+        std::swap(rem, next);
+    }
+    return RF_OK;
+}
+
+extern "C" int rf_assoc_put_device(rf_assoc* a, int kind, const void* d_expect32, const void* d_keys32,
+                                   const void* d_vals32, uint64_t n, void* d_status) {
+    ARG(a && (n == 0 || (d_keys32 && d_vals32 && d_status)), "null argument");
+    ARG(kind >= 0 && kind < (1 << 30), "bad assoc kind");
+    ARG(n <= (1u << 30), "assoc batch too large");
+    if (!n) return RF_OK;
+    std::lock_guard<std::mutex> lk(a->ctx->mu);
+    DevGuard dg(a->ctx->device);
+    int rc = assoc_put_locked(a, kind, static_cast<const uint8_t*>(d_expect32), static_cast<const uint8_t*>(d_keys32),
+                              static_cast<const uint8_t*>(d_vals32), n, static_cast<int32_t*>(d_status));
+    if (rc) return rc;
+    HIPC(hipStreamSynchronize(a->ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_assoc_put(rf_assoc* a, int kind, const uint8_t* expect32, const uint8_t* keys32,
+                            const uint8_t* vals32, uint64_t n, int32_t* status) {
+    ARG(a && (n == 0 || (keys32 && vals32 && status)), "null argument");
+    ARG(kind >= 0 && kind < (1 << 30), "bad assoc kind");
+    ARG(n <= (1u << 30), "assoc batch too large");
+    if (!n) return RF_OK;
+    rf_ctx* ctx = a->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
+    HIPC(a->b_keys.ensure(32 * n));
+    HIPC(a->b_vals.ensure(32 * n));
+    HIPC(a->b_status.ensure(4 * n));
+    HIPC(hipMemcpyAsync(a->b_keys.p, keys32, 32 * n, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(a->b_vals.p, vals32, 32 * n, hipMemcpyHostToDevice, s));
+    if (expect32) {
+        HIPC(a->b_exp.ensure(32 * n));
+        HIPC(hipMemcpyAsync(a->b_exp.p, expect32, 32 * n, hipMemcpyHostToDevice, s));
+    }
+    int rc = assoc_put_locked(a, kind, expect32 ? a->b_exp.as<uint8_t>() : nullptr, a->b_keys.as<uint8_t>(),
+                              a->b_vals.as<uint8_t>(), n, a->b_status.as<int32_t>());
+    if (rc) return rc;
+    HIPC(hipMemcpyAsync(status, a->b_status.p, 4 * n, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    return RF_OK;
+}
+
+extern "C" int rf_assoc_get_device(rf_assoc* a, int kind, const void* d_keys32, uint64_t n, void* d_vals32,
+                                   void* d_found, void* stream) {
+    ARG(a && (n == 0 || (d_keys32 && d_vals32 && d_found)), "null argument");
+    DevGuard dg(a->ctx->device);
+    HIPC(launch_assoc_get(a->view(), (uint32_t)kind, static_cast<const uint8_t*>(d_keys32), n,
+                          static_cast<uint8_t*>(d_vals32), static_cast<uint8_t*>(d_found), pick(a->ctx, stream)));
+    return RF_OK;
+}
+
+extern "C" int rf_assoc_get(rf_assoc* a, int kind, const uint8_t* keys32, uint64_t n, uint8_t* vals32,
+                            uint8_t* found) {
+    ARG(a && (n == 0 || (keys32 && vals32 && found)), "null argument");
+    if (!n) return RF_OK;
+    rf_ctx* ctx = a->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    HIPC(a->b_keys.ensure(32 * n));
+    HIPC(a->b_vals.ensure(32 * n));
+    HIPC(a->b_found.ensure(n));
+    HIPC(hipMemcpyAsync(a->b_keys.p, keys32, 32 * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(launch_assoc_get(a->view(), (uint32_t)kind, a->b_keys.as<uint8_t>(), n, a->b_vals.as<uint8_t>(),
+                          a->b_found.as<uint8_t>(), ctx->stream));
+    HIPC(hipMemcpyAsync(vals32, a->b_vals.p, 32 * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipMemcpyAsync(found, a->b_found.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_assoc_get_abbrev(rf_assoc* a, int kind, const uint8_t* keys32, const uint8_t* nhex, uint64_t n,
+                                   uint8_t* keys_out32, uint8_t* vals32, int32_t* status) {
+    ARG(a && (n == 0 || (keys32 && nhex && keys_out32 && vals32 && status)), "null argument");
+    for (uint64_t i = 0; i < n; ++i) ARG(nhex[i] >= 8 && nhex[i] <= 64, "abbreviated keys need 8..64 hex digits (ID4)");
+    if (!n) return RF_OK;
+    rf_ctx* ctx = a->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
+    HIPC(a->b_keys.ensure(32 * 64 + 64));
+    HIPC(a->b_cnt.ensure(4 * 64 * 2));
+    uint32_t* cnt = a->b_cnt.as<uint32_t>();
+    for (uint64_t b = 0; b < n; b += 64) {
+        const uint32_t q = (uint32_t)std::min<uint64_t>(64, n - b);
+        HIPC(hipMemcpyAsync(a->b_keys.p, keys32 + 32 * b, 32 * q, hipMemcpyHostToDevice, s));
+        HIPC(hipMemcpyAsync(a->b_keys.as<uint8_t>() + 32 * 64, nhex + b, q, hipMemcpyHostToDevice, s));
+        HIPC(hipMemsetAsync(cnt, 0, 4 * 64, s));
+        HIPC(launch_assoc_abbrev(a->view(), (uint32_t)kind, a->cap, a->b_keys.as<uint8_t>(),
+                                 a->b_keys.as<uint8_t>() + 32 * 64, q, cnt, cnt + 64, s));
+        uint32_t h[128];
+        HIPC(hipMemcpyAsync(h, cnt, 4 * 128, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        for (uint32_t j = 0; j < q; ++j) {
+            const uint64_t i = b + j;
+            if (h[j] == 0) {
+                status[i] = RF_ENOTFOUND;
+            } else if (h[j] > 1) {
+                status[i] = RF_EINVAL;  // "more than one key matched" (dydbassoc.go:145-146)
+            } else {
+                HIPC(hipMemcpy(keys_out32 + 32 * i, a->keys.as<uint8_t>() + 32ull * h[64 + j], 32,
+                               hipMemcpyDeviceToHost));
+                HIPC(hipMemcpy(vals32 + 32 * i, a->vals.as<uint8_t>() + 32ull * h[64 + j], 32,
+                               hipMemcpyDeviceToHost));
+                status[i] = RF_OK;
+            }
+        }
+    }
+    return RF_OK;
+}
+
+extern "C" int rf_assoc_stats(rf_assoc* a, uint64_t* occupied, uint64_t* capacity) {
+    ARG(a, "null assoc");
+    DevGuard dg(a->ctx->device);
+    uint32_t used = 0;
+    HIPC(hipMemcpy(&used, a->count.p, 4, hipMemcpyDeviceToHost));
+    if (occupied) *occupied = used;
+    if (capacity) *capacity = a->cap;
+    return RF_OK;
+}

@@ -96,4 +96,25 @@ uint32_t dedup_table_slots(uint32_t n);
 hipError_t launch_dedup(const uint8_t* dig, uint32_t n, uint32_t* table, uint32_t* slot_of, uint32_t* canon,
                         uint32_t* n_unique, hipStream_t s);
 
+// HBM assoc (assoc.Assoc with test/testutil/assoc.go semantics)
+struct AssocView {
+    uint32_t* tag;
+    uint4* keys;
+    uint4* vals;
+    uint32_t mask;
+    uint32_t* count;
+};
+hipError_t launch_assoc_insert(const AssocView& t, uint32_t kind, const uint8_t* keys, const uint32_t* canon,
+                               uint32_t n, uint32_t* slot_of, hipStream_t s);
+hipError_t launch_assoc_round(const AssocView& t, const uint32_t* rem, const uint32_t* n_rem, uint32_t n_max,
+                              const uint32_t* canon, unsigned long long* cls, uint32_t round,
+                              const uint32_t* slot_of, const uint8_t* expect, const uint8_t* vals,
+                              int32_t* status, uint32_t* next, uint32_t* n_next, hipStream_t s);
+hipError_t launch_assoc_get(const AssocView& t, uint32_t kind, const uint8_t* keys, uint64_t n, uint8_t* vals,
+                            uint8_t* found, hipStream_t s);
+hipError_t launch_assoc_abbrev(const AssocView& t, uint32_t kind, uint32_t cap, const uint8_t* qkeys,
+                               const uint8_t* nhex, uint32_t q, uint32_t* matches, uint32_t* hit_slot,
+                               hipStream_t s);
+hipError_t launch_assoc_rehash(const AssocView& from, uint32_t cap_from, const AssocView& to, hipStream_t s);
+
 }  // namespace rf

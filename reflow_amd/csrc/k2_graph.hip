@@ -26,6 +26,8 @@
 // ring (template block + digests OR-ed into the zero holes), hashes it and
 // propagates.  A level's jobs all depend only on lower levels, so a level's
 // list is complete when its kernel starts.
+#include <cstdlib>
+
 #include "engine.h"
 #include "sha256_dev.h"
 
@@ -37,6 +39,7 @@ constexpr uint32_t kRing = 33;  // words per lane: a 32-word ring + 1 (odd strid
 struct LevelArgs {
     uint32_t s, e, lvl;  // internal job range of the level
     int full;
+    uint32_t dbg_twice;  // diagnostic: hash every block twice (RF_DBG_HASH2), result unchanged
     const uint4* __restrict__ meta;
     const uint2* __restrict__ holes;
     const uint2* __restrict__ cons;          // {consumer job, its level}
@@ -174,6 +177,14 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
+        if (a.dbg_twice) {
+            ShaState s2 = st;
+            uint32_t w2[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w2[i] = w[i] ^ (a.dbg_twice - 1);
+            sha256_compress(s2, w2);
+            st.h[0] ^= s2.h[0] & (a.dbg_twice - 1);
+        }
         sha256_compress(st, w);
     }
     uint4 nlo, nhi;
@@ -293,11 +304,16 @@ hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, con
 hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s) {
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
-    LevelArgs a{b, e, lvl, full, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
+    static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u : 0u;
+    LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
-    const uint32_t grid = grid_for(e - b, full ? 16384u : 1024u);
+    static const uint32_t inc_cap = [] {
+        const char* v = getenv("RF_INC_GRID");
+        return v ? (uint32_t)atoi(v) : 1024u;
+    }();
+    const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
     hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
     return hipGetLastError();
 }

@@ -98,4 +98,216 @@ hipError_t launch_dedup(const uint8_t* dig, uint32_t n, uint32_t* table, uint32_
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// HBM-resident assoc (assoc.Assoc, assoc/assoc.go:26-38) with the in-memory
+// implementation's semantics (test/testutil/assoc.go:34-56): (kind, key) ->
+// value; Put with a nonzero `expect` is a compare-and-set, a zero value
+// deletes.  Table: open addressing on the key's first 4 bytes, a tag word per
+// slot (0 empty, 1 being written, 2 + kind ready), keys and values 32 B each.
+// Deleted entries keep their slot with a zero value (Get: NotExist).
+constexpr uint32_t kTagEmpty = 0, kTagBusy = 1, kTagReady = 2;
+
+
+
+__device__ __forceinline__ bool key_eq(const uint4* k, const uint4& lo, const uint4& hi) {
+    const uint4 a = k[0], b = k[1];
+    return ((a.x ^ lo.x) | (a.y ^ lo.y) | (a.z ^ lo.z) | (a.w ^ lo.w) | (b.x ^ hi.x) | (b.y ^ hi.y) |
+            (b.z ^ hi.z) | (b.w ^ hi.w)) == 0;
+}
+
+// Insert (or find) the batch's DISTINCT keys (canon[i] == i): a busy slot is
+// some other key being written in this launch, so it is skipped, never waited on.
+__global__ __launch_bounds__(256) void k5_assoc_insert(AssocView t, uint32_t kind, const uint8_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ canon, uint32_t n,
+                                                       uint32_t* __restrict__ slot_of) {
+    const uint32_t ready = kTagReady + kind;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (canon[i] != i) continue;
+        const uint4* k = reinterpret_cast<const uint4*>(keys + 32ull * i);
+        const uint4 lo = k[0], hi = k[1];
+        uint32_t slot = lo.x & t.mask;
+        for (;;) {
+            uint32_t tg = __hip_atomic_load(&t.tag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (tg == kTagEmpty) {
+                tg = atomicCAS(&t.tag[slot], kTagEmpty, kTagBusy);
+                if (tg == kTagEmpty) {
+                    t.keys[2 * slot] = lo;
+                    t.keys[2 * slot + 1] = hi;
+                    t.vals[2 * slot] = make_uint4(0, 0, 0, 0);
+                    t.vals[2 * slot + 1] = make_uint4(0, 0, 0, 0);
+                    __hip_atomic_store(&t.tag[slot], ready, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicAdd(t.count, 1u);
+                    break;
+                }
+            }
+            if (tg == ready && key_eq(&t.keys[2 * slot], lo, hi)) break;
+            slot = (slot + 1) & t.mask;
+        }
+        slot_of[i] = slot;
+    }
+}
+
+__device__ __forceinline__ uint32_t assoc_find(const AssocView& t, uint32_t kind, const uint4& lo, const uint4& hi) {
+    const uint32_t ready = kTagReady + kind;
+    uint32_t slot = lo.x & t.mask;
+    for (;;) {
+        const uint32_t tg = t.tag[slot];
+        if (tg == kTagEmpty) return kEmpty;
+        if (tg == ready && key_eq(&t.keys[2 * slot], lo, hi)) return slot;
+        slot = (slot + 1) & t.mask;
+    }
+}
+
+// One round of a Put batch: every remaining op claims its key's class with
+// atomicMax((round << 32) | ~i) -- the smallest index of the class wins the
+// round -- then winners apply in index order across rounds.
+__global__ __launch_bounds__(256) void k5_assoc_claim(const uint32_t* __restrict__ rem, const uint32_t* __restrict__ n_rem,
+                                                      const uint32_t* __restrict__ canon,
+                                                      unsigned long long* __restrict__ cls, uint32_t round) {
+    const uint32_t n = *n_rem;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        const uint32_t i = rem[q];
+        atomicMax(&cls[canon[i]], ((unsigned long long)round << 32) | (unsigned long long)(~i));
+    }
+}
+
+__global__ __launch_bounds__(256) void k5_assoc_apply(AssocView t, const uint32_t* __restrict__ rem,
+                                                      const uint32_t* __restrict__ n_rem,
+                                                      const uint32_t* __restrict__ canon,
+                                                      const unsigned long long* __restrict__ cls, uint32_t round,
+                                                      const uint32_t* __restrict__ slot_of,
+                                                      const uint8_t* __restrict__ expect, const uint8_t* __restrict__ vals,
+                                                      int32_t* __restrict__ status, uint32_t* __restrict__ next,
+                                                      uint32_t* __restrict__ n_next) {
+    const uint32_t n = *n_rem;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        const uint32_t i = rem[q];
+        const uint32_t c = canon[i];
+        if (cls[c] != (((unsigned long long)round << 32) | (unsigned long long)(~i))) {
+            next[atomicAdd(n_next, 1u)] = i;  // a later op of the same key: next round
+            continue;
+        }
+        const uint32_t slot = slot_of[c];
+        uint4* v = &t.vals[2 * slot];
+        if (expect) {
+            const uint4* e = reinterpret_cast<const uint4*>(expect + 32ull * i);
+            const uint4 elo = e[0], ehi = e[1];
+            const bool nz = (elo.x | elo.y | elo.z | elo.w | ehi.x | ehi.y | ehi.z | ehi.w) != 0;
+            if (nz && !key_eq(v, elo, ehi)) {  // testutil/assoc.go:38-40
+                status[i] = 7;                 // RF_EPRECONDITION
+                continue;
+            }
+        }
+        const uint4* nv = reinterpret_cast<const uint4*>(vals + 32ull * i);
+        v[0] = nv[0];  // a zero value deletes (Get then reports NotExist)
+        v[1] = nv[1];
+        status[i] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k5_assoc_get(AssocView t, uint32_t kind, const uint8_t* __restrict__ keys,
+                                                    uint64_t n, uint8_t* __restrict__ vals, uint8_t* __restrict__ found) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4* k = reinterpret_cast<const uint4*>(keys + 32ull * i);
+        const uint4 lo = k[0], hi = k[1];
+        const uint32_t slot = assoc_find(t, kind, lo, hi);
+        uint4 a = make_uint4(0, 0, 0, 0), b = a;
+        if (slot != kEmpty) {
+            a = t.vals[2 * slot];
+            b = t.vals[2 * slot + 1];
+        }
+        uint4* o = reinterpret_cast<uint4*>(vals + 32ull * i);
+        o[0] = a;
+        o[1] = b;
+        found[i] = (a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w) != 0;
+    }
+}
+
+// Abbreviated keys (dydbassoc.go:111-147: the ID4 index narrows, Expands
+// decides): every live entry of the kind is compared with each of the q
+// queries' first nhex hex digits; per query, the number of matches and one
+// matching slot.
+__global__ __launch_bounds__(256) void k5_assoc_abbrev(AssocView t, uint32_t kind, uint32_t cap,
+                                                       const uint8_t* __restrict__ qkeys, const uint8_t* __restrict__ nhex,
+                                                       uint32_t q, uint32_t* __restrict__ matches,
+                                                       uint32_t* __restrict__ hit_slot) {
+    const uint32_t ready = kTagReady + kind;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += gridDim.x * blockDim.x) {
+        if (t.tag[s] != ready) continue;
+        const uint4 vlo = t.vals[2 * s], vhi = t.vals[2 * s + 1];
+        if ((vlo.x | vlo.y | vlo.z | vlo.w | vhi.x | vhi.y | vhi.z | vhi.w) == 0) continue;  // deleted
+        const uint8_t* key = reinterpret_cast<const uint8_t*>(&t.keys[2 * s]);
+        for (uint32_t j = 0; j < q; ++j) {
+            const uint32_t nh = nhex[j];
+            bool eq = true;
+            for (uint32_t b = 0; b < nh / 2 && eq; ++b) eq = key[b] == qkeys[32 * j + b];
+            if (eq && (nh & 1)) eq = (key[nh / 2] >> 4) == (qkeys[32 * j + nh / 2] >> 4);
+            if (eq) {
+                atomicAdd(&matches[j], 1u);
+                hit_slot[j] = s;
+            }
+        }
+    }
+}
+
+// Rehash every occupied slot into a larger (empty) table; keys are distinct.
+__global__ __launch_bounds__(256) void k5_assoc_rehash(AssocView from, uint32_t cap_from, AssocView to) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap_from; s += gridDim.x * blockDim.x) {
+        const uint32_t tg = from.tag[s];
+        if (tg < kTagReady) continue;
+        const uint4 lo = from.keys[2 * s], hi = from.keys[2 * s + 1];
+        uint32_t slot = lo.x & to.mask;
+        while (atomicCAS(&to.tag[slot], kTagEmpty, kTagBusy) != kTagEmpty) slot = (slot + 1) & to.mask;
+        to.keys[2 * slot] = lo;
+        to.keys[2 * slot + 1] = hi;
+        to.vals[2 * slot] = from.vals[2 * s];
+        to.vals[2 * slot + 1] = from.vals[2 * s + 1];
+        __hip_atomic_store(&to.tag[slot], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(to.count, 1u);
+    }
+}
+
+static uint32_t grid256(uint64_t n) {
+    uint64_t g = (n + 255) / 256;
+    return (uint32_t)(g < 1 ? 1 : g > 16384 ? 16384 : g);
+}
+
+hipError_t launch_assoc_insert(const AssocView& t, uint32_t kind, const uint8_t* keys, const uint32_t* canon,
+                               uint32_t n, uint32_t* slot_of, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k5_assoc_insert, dim3(grid256(n)), dim3(256), 0, s, t, kind, keys, canon, n, slot_of);
+    return hipGetLastError();
+}
+
+hipError_t launch_assoc_round(const AssocView& t, const uint32_t* rem, const uint32_t* n_rem, uint32_t n_max,
+                              const uint32_t* canon, unsigned long long* cls, uint32_t round,
+                              const uint32_t* slot_of, const uint8_t* expect, const uint8_t* vals,
+                              int32_t* status, uint32_t* next, uint32_t* n_next, hipStream_t s) {
+    if (!n_max) return hipSuccess;
+    hipLaunchKernelGGL(k5_assoc_claim, dim3(grid256(n_max)), dim3(256), 0, s, rem, n_rem, canon, cls, round);
+    hipLaunchKernelGGL(k5_assoc_apply, dim3(grid256(n_max)), dim3(256), 0, s, t, rem, n_rem, canon, cls, round,
+                       slot_of, expect, vals, status, next, n_next);
+    return hipGetLastError();
+}
+
+hipError_t launch_assoc_get(const AssocView& t, uint32_t kind, const uint8_t* keys, uint64_t n, uint8_t* vals,
+                            uint8_t* found, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k5_assoc_get, dim3(grid256(n)), dim3(256), 0, s, t, kind, keys, n, vals, found);
+    return hipGetLastError();
+}
+
+hipError_t launch_assoc_abbrev(const AssocView& t, uint32_t kind, uint32_t cap, const uint8_t* qkeys,
+                               const uint8_t* nhex, uint32_t q, uint32_t* matches, uint32_t* hit_slot,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k5_assoc_abbrev, dim3(grid256(cap)), dim3(256), 0, s, t, kind, cap, qkeys, nhex, q,
+                       matches, hit_slot);
+    return hipGetLastError();
+}
+
+hipError_t launch_assoc_rehash(const AssocView& from, uint32_t cap_from, const AssocView& to, hipStream_t s) {
+    hipLaunchKernelGGL(k5_assoc_rehash, dim3(grid256(cap_from)), dim3(256), 0, s, from, cap_from, to);
+    return hipGetLastError();
+}
+
 }  // namespace rf
