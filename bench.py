@@ -233,8 +233,12 @@ def bench_c1(args, dist, ctx):
     ids_ms = (time.perf_counter() - t0) / reps * 1e3
     t0 = time.perf_counter()
     ids = out.to_numpy().reshape(-1, 32)
-    fsd = ctx.fileset_digest_batch([[[(c1_path(i), ids[i].tobytes()) for i in range(C1_N)]]])[0]
-    fs_ms = (time.perf_counter() - t0) * 1e3
+    d2h_ms = (time.perf_counter() - t0) * 1e3
+    group = [[[(c1_path(i), ids[i].tobytes()) for i in range(C1_N)]]]  # harness-side argument building
+    ctx.fileset_digest_batch(group)
+    t0 = time.perf_counter()
+    fsd = ctx.fileset_digest_batch(group)[0]
+    fs_ms = (time.perf_counter() - t0) * 1e3 + d2h_ms
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "c1_fileset.json")))
     ok = ("sha256:" + fsd.hex() == want["fileset_digest"] and
           __import__("hashlib").sha256(ids.tobytes()).hexdigest() == want["ids_sha256"])
@@ -256,7 +260,9 @@ def bench_c1(args, dist, ctx):
     return {"workload": "configs[0]: 4096 x 256 KiB files (1 GiB) -> File IDs + Fileset digest; CacheKeys "
                         "of a %d-node 1000align DAG (%d jobs)" % (small.n_nodes, small.n_jobs),
             "file_ids_ms": ids_ms, "file_ids_gbps": C1_N * C1_LEN / (ids_ms * 1e-3) / 1e9,
-            "fileset_digest_ms": fs_ms, "fixture_match": ok,
+            "fileset_digest_ms": fs_ms, "fileset_digest_note": "File IDs read back + rf_fileset_digest_batch "
+            "(bytewise sort, material on the host, one %d-block message on the duo chain)" % ((C1_N * 49 + 9 + 63) // 64),
+            "fixture_match": ok,
             "dag_nodes": small.n_nodes, "dag_full_recompute_ms": dag_ms,
             "total_ms": ids_ms + fs_ms + dag_ms,
             "note": "4096 messages fill 64 waves: the per-file chain (4097 blocks, lane mode) bounds the "
@@ -438,9 +444,22 @@ def bench_probe(args, dist, ctx):
                                "words_per_probe": round(reads / n_probe, 3), "filter_fill": round(f, 4),
                                "peak_kind": "measured live: tools/micro.hip k_gather, k independent "
                                             "random 8-B reads per thread over a table of the filter's size"}}
+    # bounded sample for the CPU leg: the filter words and the first 2e7 probe keys
+    ns = min(n_probe, 20_000_000)
+    res["_cpu"] = {"words": b.words(), "length": b.params()[2], "m": m, "k": k,
+                   "keys": keys.to_numpy(count=32 * ns), "n": ns}
     for x in (keys, out, d_offs, d_lens):
         x.free()
     b.close()
+    # gather-bound kernels beside the probe, against the same live ceiling
+    if ceil:
+        a = res.get("assoc")
+        if a:
+            a["roofline_gather"] = {"achieved": round(3 * n_probe / (a["get_ms"] * 1e-3) / 1e9, 2), "peak": round(ceil, 2),
+                                    "unit": "G random accesses/s", "frac": round(3 * n_probe / (a["get_ms"] * 1e-3) / 1e9 / ceil, 3),
+                                    "accesses_per_get": "3 (tag, 32-B key compare, 32-B value on a hit; absent keys "
+                                                        "stop at an empty tag: 1-2)"}
+    res["_gather_ceiling"] = ceil
     return res
 
 
@@ -507,6 +526,42 @@ def cpu_model():
     return None
 
 
+def cpu_probe_and_tables(probe, canon_n=2_000_000):
+    """CPU legs of the probe / canonicalize / assoc rows: bloom Contains on the
+    same filter (oracle/oracle.c, bloom.Test order; 1 thread = bloomlive's
+    non-goroutine-safe Contains, and 16 threads), and Go-map-shaped dedup and
+    lookups (a Python dict over 32-B keys: the flowMap / in-memory assoc)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import reflow_oracle as O
+    L = O.lib()
+    c = probe["_cpu"]
+    words = np.ascontiguousarray(c["words"])
+    keys = np.ascontiguousarray(c["keys"])
+    out = np.zeros(c["n"], dtype=np.uint8)
+    r = {}
+    for th, n in ((1, min(c["n"], 2_000_000)), (16, c["n"])):
+        t0 = time.perf_counter()
+        L.orc_bloomlive_contains_batch(words.ctypes.data, int(c["length"]), int(c["m"]), int(c["k"]),
+                                       keys.ctypes.data, n, out.ctypes.data, th)
+        dt = time.perf_counter() - t0
+        r["probe_%dt" % th] = {"value": n / dt / 1e9, "unit": "G probes/s", "cores": th, "kind": "port",
+                               "sample": "%d probes of the configs[4] set against its filter" % n}
+    ks = [keys[32 * i:32 * i + 32].tobytes() for i in range(canon_n)]
+    t0 = time.perf_counter()
+    first = {}
+    for i, kk in enumerate(ks):
+        first.setdefault(kk, i)
+    dt = time.perf_counter() - t0
+    r["canonicalize"] = {"value": canon_n / dt / 1e6, "unit": "M nodes/s", "cores": 1, "kind": "port",
+                         "sample": "%d digests into a dict (flowMap.Put shape, flow.go:897-907)" % canon_n}
+    t0 = time.perf_counter()
+    hit = sum(1 for kk in ks if kk in first)
+    dt = time.perf_counter() - t0
+    r["assoc_get"] = {"value": canon_n / dt / 1e6, "unit": "M keys/s", "cores": 1, "kind": "port",
+                      "sample": "%d dict lookups (test/testutil/assoc.go:49-56 shape)" % canon_n, "hits": hit}
+    return r
+
+
 def cpu_baseline(args, sha, dag):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
@@ -536,6 +591,7 @@ def cpu_baseline(args, sha, dag):
     back[order.astype(np.int64)] = out
     match = bool((back == sha["_digests"][:n]).all())
     res = {"value": float(s_lens.sum()) / dt / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
+           "what": "SHA-256 of the C2 files (the headline metric's CPU leg)",
            "sample": "first %d files (%.2f GiB, largest %.2f GiB) of the same C2 set, oracle/oracle.c "
                      "scalar SHA-256, %d pthreads, largest-first" % (n, s_lens.sum() / GiB,
                                                                     s_lens.max() / GiB, threads),
@@ -635,6 +691,16 @@ def main():
     cpu = None
     if dist.rank == 0 and dist.world == 1 and "cpu" not in skip:
         cpu = cpu_baseline(args, sha, dag)
+        if probe is not None:
+            cpu.update(cpu_probe_and_tables(probe))
+    if probe is not None:
+        probe.pop("_cpu", None)
+        ceil = probe.pop("_gather_ceiling", None)
+        cn = (dag_res or {}).get("canonicalize")
+        if cn and ceil:
+            cn["roofline_gather"] = {"achieved": cn["achieved_g_accesses_per_s"], "peak": round(ceil, 2),
+                                     "unit": "G random accesses/s",
+                                     "frac": round(cn["achieved_g_accesses_per_s"] / ceil, 3)}
 
     if dist.rank == 0:
         line = {
