@@ -11,7 +11,10 @@
 //   Eval                      Flow.Digest / PhysicalDigest / CacheKeys /
 //                             Canonicalize (flow.go:653-843), lowered to
 //                             rf_graph jobs and computed by the HIP kernels
-//   Liveset                   bloomlive.T (internal/bloomlive/bloomlive.go)
+//   Liveset                   bloomlive.T (internal/bloomlive/bloomlive.go),
+//                             MarshalJSON, Repository.Collect
+//   Assoc                     assoc.Assoc (assoc/assoc.go) on the HBM table
+//   MarshalJSON               json.Marshal(Fileset), the CacheWrite value
 // Every digest is computed by libreflow_hip.so on the device.
 #pragma once
 
@@ -238,10 +241,40 @@ class Liveset {
     ~Liveset();
     void Add(const std::vector<Digest>& ds);
     std::vector<bool> Contains(const std::vector<Digest>& ds);
+    std::string MarshalJSON() const;  // bloomlive.go:38-41 (the Go wire form)
+    // Repository.Collect (repository/file/repository.go:304-327) over a batch
+    // of objects: indices (walk order) of the ones not in the liveset, and
+    // their total size.
+    std::pair<std::vector<uint64_t>, int64_t> Collect(const std::vector<Digest>& objs,
+                                                      const std::vector<int64_t>& sizes);
 
    private:
     explicit Liveset(rf_bloom* b) : b_(b) {}
     rf_bloom* b_ = nullptr;
 };
+
+// assoc.Assoc (assoc/assoc.go:26-38) on the HBM table, with the in-memory
+// implementation's semantics (test/testutil/assoc.go:34-56).  Single-key
+// calls mirror the Go interface (Put errors with RF_EPRECONDITION, Get with
+// RF_ENOTFOUND); the batch forms are what a shim coalesces them into.
+enum AssocKind : int { AssocFileset = 0 };
+class Assoc {
+   public:
+    explicit Assoc(Engine& e, uint64_t capacity = 1024);
+    ~Assoc();
+    Assoc(const Assoc&) = delete;
+    Assoc& operator=(const Assoc&) = delete;
+    void Put(AssocKind kind, const Digest& expect, const Digest& k, const Digest& v);
+    // returns (expanded key, value); an abbreviated key is given as its hex prefix
+    std::pair<Digest, Digest> Get(AssocKind kind, const Digest& k);
+    std::pair<Digest, Digest> GetAbbrev(AssocKind kind, const std::string& hex_prefix);
+    std::vector<int> PutBatch(AssocKind kind, const std::vector<Digest>& expect, const std::vector<Digest>& keys,
+                              const std::vector<Digest>& vals);
+    std::vector<std::optional<Digest>> GetBatch(AssocKind kind, const std::vector<Digest>& keys);
+
+   private:
+    rf_assoc* a_ = nullptr;
+};
+void Delete(Assoc& a, AssocKind kind, const Digest& k);  // assoc.go:40-43
 
 }  // namespace reflow

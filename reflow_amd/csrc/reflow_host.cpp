@@ -563,4 +563,84 @@ std::vector<bool> Liveset::Contains(const std::vector<Digest>& ds) {
     return std::vector<bool>(out.begin(), out.end());
 }
 
+std::string Liveset::MarshalJSON() const {
+    uint64_t n = 0;
+    rf_bloom_marshal_json(b_, nullptr, 0, &n);
+    std::string out(n, '\0');
+    Check(rf_bloom_marshal_json(b_, reinterpret_cast<uint8_t*>(out.data()), n, &n));
+    return out;
+}
+
+std::pair<std::vector<uint64_t>, int64_t> Liveset::Collect(const std::vector<Digest>& objs,
+                                                           const std::vector<int64_t>& sizes) {
+    std::vector<uint64_t> dead(objs.size() + 1);
+    uint64_t nd = 0;
+    int64_t bytes = 0;
+    if (!objs.empty())
+        Check(rf_bloom_collect(b_, objs[0].b.data(), sizes.empty() ? nullptr : sizes.data(), objs.size(),
+                               dead.data(), &nd, &bytes));
+    dead.resize(nd);
+    return {dead, bytes};
+}
+
+// ---- assoc -------------------------------------------------------------------
+Assoc::Assoc(Engine& e, uint64_t capacity) { Check(rf_assoc_new(e.ctx(), capacity, &a_)); }
+Assoc::~Assoc() {
+    if (a_) rf_assoc_destroy(a_);
+}
+
+std::vector<int> Assoc::PutBatch(AssocKind kind, const std::vector<Digest>& expect, const std::vector<Digest>& keys,
+                                 const std::vector<Digest>& vals) {
+    if (keys.size() != vals.size() || (!expect.empty() && expect.size() != keys.size()))
+        throw Error(RF_EINVAL, "assoc put: mismatched batch sizes");
+    std::vector<int32_t> st(keys.size());
+    if (!keys.empty())
+        Check(rf_assoc_put(a_, kind, expect.empty() ? nullptr : expect[0].b.data(), keys[0].b.data(),
+                           vals[0].b.data(), keys.size(), st.data()));
+    return std::vector<int>(st.begin(), st.end());
+}
+
+void Assoc::Put(AssocKind kind, const Digest& expect, const Digest& k, const Digest& v) {
+    const int st = PutBatch(kind, {expect}, {k}, {v})[0];
+    if (st == RF_EPRECONDITION)  // testutil/assoc.go:38-40: errors.Precondition
+        throw Error(RF_EPRECONDITION, "expected value " + expect.String() + ", have a different value");
+}
+
+std::vector<std::optional<Digest>> Assoc::GetBatch(AssocKind kind, const std::vector<Digest>& keys) {
+    std::vector<Digest> vals(keys.size());
+    std::vector<uint8_t> found(keys.size());
+    if (!keys.empty())
+        Check(rf_assoc_get(a_, kind, keys[0].b.data(), keys.size(), vals[0].b.data(), found.data()));
+    std::vector<std::optional<Digest>> out(keys.size());
+    for (size_t i = 0; i < keys.size(); ++i)
+        if (found[i]) out[i] = vals[i];
+    return out;
+}
+
+std::pair<Digest, Digest> Assoc::Get(AssocKind kind, const Digest& k) {
+    auto v = GetBatch(kind, {k})[0];
+    if (!v) throw Error(RF_ENOTFOUND, "key does not exist");  // testutil/assoc.go:51-54
+    return {k, *v};
+}
+
+std::pair<Digest, Digest> Assoc::GetAbbrev(AssocKind kind, const std::string& hex) {
+    if (hex.size() < 8 || hex.size() > 64) throw Error(RF_EINVAL, "abbreviated key needs 8..64 hex digits");
+    Digest q;
+    for (size_t i = 0; i < hex.size(); ++i) {
+        const char c = hex[i];
+        const int v = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : -1;
+        if (v < 0) throw Error(RF_EINVAL, "bad hex digit in abbreviated key");
+        q.b[i / 2] |= (uint8_t)(i % 2 ? v : v << 4);
+    }
+    const uint8_t nh = (uint8_t)hex.size();
+    Digest ko, vo;
+    int32_t st = 0;
+    Check(rf_assoc_get_abbrev(a_, kind, q.b.data(), &nh, 1, ko.b.data(), vo.b.data(), &st));
+    if (st == RF_ENOTFOUND) throw Error(RF_ENOTFOUND, "lookup " + hex + ": key does not exist");
+    if (st == RF_EINVAL) throw Error(RF_EINVAL, "lookup " + hex + ": more than one key matched");
+    return {ko, vo};
+}
+
+void Delete(Assoc& a, AssocKind kind, const Digest& k) { a.Put(kind, Digest{}, k, Digest{}); }
+
 }  // namespace reflow

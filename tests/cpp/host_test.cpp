@@ -6,7 +6,8 @@
 //   TestDigestExec        syntax/digest_test.go:13-29 (the evaluated flow chain)
 //   TestCacheKeys         flow.go:764-802 (physical key first)
 //   TestIncremental       SetFileID + Recompute == a fresh evaluation
-//   TestLiveset           bloomlive Contains over Add
+//   TestLiveset           bloomlive Contains over Add, MarshalJSON, Collect
+//   TestAssoc             assoc.Assoc: test/testutil/assoc.go semantics, abbreviations
 // Exit status 0 iff every check passes.
 #include <cstdio>
 #include <string>
@@ -185,6 +186,49 @@ static void TestLiveset(Engine& e) {
     for (bool b : got) EXPECT(b, "false negative");
     for (bool b : live.Contains(dout)) fp += b;
     EXPECT(fp < 20, "false positives %d", fp);
+    Liveset back = Liveset::FromJSON(e, live.MarshalJSON());
+    EXPECT(back.MarshalJSON() == live.MarshalJSON(), "JSON round trip");
+    std::vector<Digest> objs = din;
+    objs.insert(objs.end(), dout.begin(), dout.end());
+    auto [dead, bytes] = live.Collect(objs, std::vector<int64_t>(objs.size(), 2));
+    auto c = live.Contains(objs);
+    size_t j = 0;
+    for (size_t i = 0; i < objs.size(); ++i)
+        if (!c[i]) EXPECT(j < dead.size() && dead[j++] == i, "collect order at %zu", i);
+    EXPECT(j == dead.size() && bytes == 2 * (int64_t)dead.size() && dead.size() + fp == dout.size(),
+           "collect %zu dead", dead.size());
+}
+
+static void TestAssoc(Engine& e) {
+    Digester D(e);
+    Assoc a(e, 16);
+    Digest k1 = D.FromString("k1"), k2 = D.FromString("k2"), v1 = D.FromString("v1"), v2 = D.FromString("v2");
+    bool thrown = false;
+    try {
+        a.Get(AssocFileset, k1);
+    } catch (const Error& er) {
+        thrown = er.code == RF_ENOTFOUND;
+    }
+    EXPECT(thrown, "Get of a missing key is NotExist");
+    a.Put(AssocFileset, Digest{}, k1, v1);
+    EXPECT(a.Get(AssocFileset, k1).second == v1, "Get after Put");
+    thrown = false;
+    try {
+        a.Put(AssocFileset, v2, k1, v2);  // expect mismatch
+    } catch (const Error& er) {
+        thrown = er.code == RF_EPRECONDITION;
+    }
+    EXPECT(thrown && a.Get(AssocFileset, k1).second == v1, "CAS with a wrong expect is Precondition");
+    a.Put(AssocFileset, v1, k1, v2);  // CAS succeeds
+    EXPECT(a.Get(AssocFileset, k1).second == v2, "CAS");
+    a.Put(AssocFileset, Digest{}, k2, v1);
+    EXPECT(a.GetAbbrev(AssocFileset, k2.Hex().substr(0, 12)).first == k2, "abbreviated key expands");
+    Delete(a, AssocFileset, k1);
+    EXPECT(!a.GetBatch(AssocFileset, {k1})[0], "deleted");
+    // a batch that touches one key three times applies in order
+    auto st = a.PutBatch(AssocFileset, {Digest{}, v1, v2}, {k1, k1, k1}, {v1, v2, v1});
+    EXPECT(st[0] == RF_OK && st[1] == RF_OK && st[2] == RF_OK && a.Get(AssocFileset, k1).second == v1,
+           "batch order");
 }
 
 int main() {
@@ -197,6 +241,7 @@ int main() {
         TestDigestExec(e);
         TestCacheKeysAndIncremental(e);
         TestLiveset(e);
+        TestAssoc(e);
     } catch (const std::exception& ex) {
         fprintf(stderr, "exception: %s\n", ex.what());
         return 2;
