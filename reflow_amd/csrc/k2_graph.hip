@@ -115,25 +115,18 @@ __device__ __forceinline__ void ring_put(uint32_t* ring, uint32_t half, const ui
     }
 }
 
-// Hash job p; returns whether its slot changed (always true in full mode).
-// Software pipeline over blocks: while block b is compressed, the template
-// of block b+2 and the (at most two: holes are >= 32 B apart) holes that
-// start in block b+1 -- records and slot digests -- are in flight.
-__device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_t* ring, uint32_t& cb,
-                                         uint32_t& ce) {
-    const uint4 m0 = a.meta[2 * p], m1 = a.meta[2 * p + 1];
-    uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * m1.x);
-    uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
-    if (!a.full) {
-        olo = dst[0];
-        ohi = dst[1];
-    }
-    const uint4* __restrict__ T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
-    const uint32_t nb = m0.y, he = m0.w;
-    uint32_t hn = m0.z;  // first hole not yet applied
+// Assembles a job's material block by block in the lane's LDS ring (a
+// template block with the slot digests OR-ed into its zero holes).  Software
+// pipeline: while block b is consumed, the template of block b+2 and the (at
+// most two: holes are >= 32 B apart) holes that start in block b+1 -- records
+// and slot digests -- are in flight.
+struct MatCursor {
+    const uint4* __restrict__ T;
+    uint32_t nb, he, hn;
     uint2 R[2];
-    uint4 DL[2], DH[2];
-    auto fetch_holes = [&]() {
+    uint4 DL[2], DH[2], t[4];
+
+    __device__ __forceinline__ void fetch_holes(const LevelArgs& a) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             R[k] = hn + k < he ? a.holes[hn + k] : make_uint2(~0u, 0u);
@@ -141,17 +134,22 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
             DL[k] = src[0];
             DH[k] = src[1];
         }
-    };
-    fetch_holes();
-    uint4 t[4] = {T[0], T[1], T[2], T[3]};
-    ring_put(ring, 0, t);
-    if (nb > 1) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = T[4 + q];
     }
-    ShaState st;
-    st.init();
-    for (uint32_t b = 0; b < nb; ++b) {
+    __device__ __forceinline__ void begin(const LevelArgs& a, const uint4& m0, uint32_t* ring) {
+        T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
+        nb = m0.y;
+        he = m0.w;
+        hn = m0.z;  // first hole not yet applied
+        fetch_holes(a);
+        t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
+        ring_put(ring, 0, t);
+        if (nb > 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[q] = T[4 + q];
+        }
+    }
+    // the 16 big-endian words of block b (blocks taken in order)
+    __device__ __forceinline__ void block(const LevelArgs& a, uint32_t b, uint32_t* ring, uint32_t (&w)[16]) {
         const uint32_t half = (b & 1) * 16;
         if (b + 1 < nb) {
             ring_put(ring, half ^ 16, t);
@@ -172,11 +170,74 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
         }
         if (used) {
             hn += used;
-            fetch_holes();
+            fetch_holes(a);
         }
-        uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
+    }
+};
+
+// Store the digest into its slot if it changed (always in full mode).
+__device__ __forceinline__ bool finish_job(const LevelArgs& a, const uint4& m1, const ShaState& st) {
+    uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * m1.x);
+    uint4 nlo, nhi;
+    nlo.x = bswap32(st.h[0]); nlo.y = bswap32(st.h[1]); nlo.z = bswap32(st.h[2]); nlo.w = bswap32(st.h[3]);
+    nhi.x = bswap32(st.h[4]); nhi.y = bswap32(st.h[5]); nhi.z = bswap32(st.h[6]); nhi.w = bswap32(st.h[7]);
+    bool changed = true;
+    if (!a.full) {
+        const uint4 olo = dst[0], ohi = dst[1];
+        changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                  (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
+    }
+    if (changed) {
+        dst[0] = nlo;
+        dst[1] = nhi;
+    }
+    return changed;
+}
+
+// As finish_job, with the old digest already loaded (incremental mode).
+__device__ __forceinline__ bool finish_job_pre(const LevelArgs& a, const uint4& m1, const ShaState& st,
+                                               const uint4& olo, const uint4& ohi) {
+    uint4 nlo, nhi;
+    nlo.x = bswap32(st.h[0]); nlo.y = bswap32(st.h[1]); nlo.z = bswap32(st.h[2]); nlo.w = bswap32(st.h[3]);
+    nhi.x = bswap32(st.h[4]); nhi.y = bswap32(st.h[5]); nhi.z = bswap32(st.h[6]); nhi.w = bswap32(st.h[7]);
+    const bool changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                         (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
+    if (changed) {
+        uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * m1.x);
+        dst[0] = nlo;
+        dst[1] = nhi;
+    }
+    return changed;
+}
+
+// propagate() with the first two reverse edges already in registers.
+__device__ __forceinline__ void propagate_pre(const LevelArgs& a, uint32_t c, uint32_t ce, const uint2 (&pre)[2]) {
+    for (int k = 0; k < 2; ++k) {
+        bool need = false;
+        const uint2 jl = pre[k];
+        if (c < ce) {
+            ++c;
+            const uint32_t bit = 1u << (jl.x & 31);
+            need = !(atomicOr(&a.dirty[jl.x >> 5], bit) & bit);
+        }
+        append_jobs(a.list, a.counts, a.lvl_start, need, jl.x, jl.y);
+    }
+    propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, c, ce);
+}
+
+// Hash job p in one lane; returns whether its slot changed.
+__device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_t* ring, uint32_t& cb,
+                                         uint32_t& ce) {
+    const uint4 m0 = a.meta[2 * p], m1 = a.meta[2 * p + 1];
+    MatCursor cur;
+    cur.begin(a, m0, ring);
+    ShaState st;
+    st.init();
+    for (uint32_t b = 0; b < cur.nb; ++b) {
+        uint32_t w[16];
+        cur.block(a, b, ring, w);
         if (a.dbg_twice) {
             ShaState s2 = st;
             uint32_t w2[16];
@@ -187,20 +248,9 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
         }
         sha256_compress(st, w);
     }
-    uint4 nlo, nhi;
-    nlo.x = bswap32(st.h[0]); nlo.y = bswap32(st.h[1]); nlo.z = bswap32(st.h[2]); nlo.w = bswap32(st.h[3]);
-    nhi.x = bswap32(st.h[4]); nhi.y = bswap32(st.h[5]); nhi.z = bswap32(st.h[6]); nhi.w = bswap32(st.h[7]);
-    bool changed = true;
-    if (!a.full)
-        changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
-                  (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
-    if (changed) {
-        dst[0] = nlo;
-        dst[1] = nhi;
-    }
     cb = m1.y;
     ce = m1.z;
-    return changed;
+    return finish_job(a, m1, st);
 }
 
 // K2+K3, one level: every listed job (incremental) or every job of the level
@@ -223,6 +273,116 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
             }
         }
         if (!a.full) propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, cb, ce);
+    }
+}
+
+// Incremental levels are latency-bound (a level's dirty jobs fill a few
+// hundred waves, one per SIMD): a lane-per-job hash costs ~1400 issued
+// instructions per block on one wave (~3 us).  Here a workgroup of two waves
+// splits that work for 64 jobs: the producer wave assembles each job's next
+// block and expands its message schedule (K[t]+W[t], 64 words) into a
+// double-buffered LDS row per job, while the chain wave runs the 64 rounds of
+// the current block from LDS (14 instructions per round: ~910 per block).
+// One workgroup barrier per block; the chain then stores, clears the queued
+// bit and propagates like k2_level.
+constexpr uint32_t kPcRow = 68;  // words per K+W row: 16-B reads of 64 rows hit distinct banks
+
+__device__ __forceinline__ void kw_expand_store(uint32_t (&w)[16], uint4* row) {
+    constexpr uint32_t K[64] = RF_SHA_K;
+#pragma unroll
+    for (int t4 = 0; t4 < 16; ++t4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = 4 * t4 + u;
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+                w[t & 15] = wt;
+            }
+            v[u] = K[t] + wt;
+        }
+        row[t4] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+__device__ __forceinline__ void compress_kw(ShaState& s, const uint4* row) {
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+    uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+    for (int t4 = 0; t4 < 16; ++t4) {
+        const uint4 v = row[t4];
+        const uint32_t kv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t t1 = add3v(h + kv[u], bsig1(e), ch(e, f, g));
+            h = g; g = f; f = e; e = d + t1;
+            const uint32_t an = add3v(t1, bsig0(a), maj(a, b, c));
+            d = c; c = b; b = a; a = an;
+        }
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
+__global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t kw[2 * 64 * kPcRow];
+    __shared__ uint32_t ring_all[64 * kRing];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 chain, 1 producer
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t* ring = &ring_all[lane * kRing];
+    const uint32_t n = a.counts[a.lvl];
+    const uint32_t* lst = a.list + a.s;
+    for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+        const uint32_t i = base + lane;
+        const bool has = i < n;
+        const uint32_t p = has ? lst[i] : 0u;
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        if (has) {
+            m0 = a.meta[2 * p];
+            m1 = a.meta[2 * p + 1];
+        }
+        // both waves read the same records: the same block count for the loop
+        uint32_t maxnb = m0.y;
+        for (int o = 32; o > 0; o >>= 1) maxnb = max(maxnb, (uint32_t)__shfl_xor((int)maxnb, o, 64));
+        maxnb = __builtin_amdgcn_readfirstlane(maxnb);
+        MatCursor cur;
+        ShaState st;
+        st.init();
+        uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
+        uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+        if (wave == 1 && has) cur.begin(a, m0, ring);
+        if (wave == 0 && has) {  // the chain wave waits for block 0 anyway: fetch what finishing needs
+            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+            olo = od[0];
+            ohi = od[1];
+            if (m1.y < m1.z) pre[0] = a.cons[m1.y];
+            if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+        }
+        for (uint32_t it = 0; it <= maxnb; ++it) {
+            if (wave == 1) {
+                if (it < m0.y) {  // block it of this lane's job -> buffer it & 1
+                    uint32_t w[16];
+                    cur.block(a, it, ring, w);
+                    kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
+                }
+            } else if (it >= 1 && it - 1 < m0.y) {  // block it-1 from buffer (it-1) & 1
+                compress_kw(st, reinterpret_cast<const uint4*>(&kw[(((it - 1) & 1) * 64 + lane) * kPcRow]));
+            }
+            __syncthreads();
+        }
+        if (wave == 0) {
+            uint32_t cb = 0, ce = 0;
+            if (has) {
+                const bool changed = finish_job_pre(a, m1, st, olo, ohi);
+                atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                cb = m1.y;
+                ce = changed ? m1.z : m1.y;
+            }
+            propagate_pre(a, cb, ce, pre);
+        }
     }
 }
 
@@ -313,6 +473,13 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         const char* v = getenv("RF_INC_GRID");
         return v ? (uint32_t)atoi(v) : 1024u;
     }();
+    static const bool lanes_only = getenv("RF_K2_LANES") != nullptr;  // diagnostic: lane-per-job hashing
+    if (!full && !lanes_only) {
+        uint64_t g = (e - b + 63) / 64;
+        if (g > 2048) g = 2048;
+        hipLaunchKernelGGL(k2_level_pc, dim3((uint32_t)g), dim3(128), 0, s, a);
+        return hipGetLastError();
+    }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
     hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
     return hipGetLastError();
