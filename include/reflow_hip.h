@@ -121,6 +121,7 @@ void rf_sha_plan_destroy(rf_sha_plan *plan);
 #define RF_SHA_NO_SOLO 1u      /* every message lane-per-message */
 #define RF_SHA_ALL_SOLO 2u     /* every message wave-per-message */
 #define RF_SHA_ONE_LANE_CHAIN 4u /* wave-per-message kernel keeps the round chain on one lane */
+#define RF_SHA_NO_PAIR 8u      /* small sets: lanes kernel instead of the producer/chain pair */
 
 /* Synthetic data generator (bench / tests): fills d_arena so that message i
  * is the splitmix64 counter stream with seed (seed ^ i). */

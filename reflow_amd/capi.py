@@ -18,6 +18,7 @@ RF_OK, RF_EINVAL, RF_EIO, RF_EINTEGRITY, RF_EDEVICE, RF_ENOMEM, RF_ENOTFOUND, RF
 RF_SHA_NO_SOLO = 1
 RF_SHA_ALL_SOLO = 2
 RF_SHA_ONE_LANE_CHAIN = 4
+RF_SHA_NO_PAIR = 8
 
 # Every symbol include/reflow_hip.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = [

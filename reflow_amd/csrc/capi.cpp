@@ -325,6 +325,7 @@ struct rf_sha_plan {
     uint64_t n = 0;
     uint32_t n_lanes = 0, n_solo = 0, grid = 0, n_shards = 1;
     bool duo = true;  // wave-per-message kernel: two-lane chain (default) or one-lane
+    bool pair = false;  // lane messages on k1_sha256_pair (latency-bound small sets)
     DevBuf d_offs, d_lens, d_order, d_heads;  // d_order = [lanes order | solo order]
     hipStream_t side = nullptr;
     hipEvent_t e0 = nullptr, e_solo = nullptr, e_lanes = nullptr, e1 = nullptr;
@@ -332,10 +333,19 @@ struct rf_sha_plan {
     rf_sha_stats st{};
 };
 
-// Cycle model used only to decide lane- vs wave-per-message:
-// a lane retires one block per ~1464 issued instructions; a wave alone on its
-// SIMD issues one instruction per 4 cycles; the chip issues one wave-
-// instruction per 2 cycles per SIMD.  The solo chain issues ~920 per block.
+// Which messages run wave-per-message (the duo chain) and which lane per
+// message (pair or lanes kernel): the smallest makespan over k = the k largest
+// messages on duo waves, from measured per-block chain latencies:
+//   duo chain            1.13 us/block (one wave per message, one per SIMD)
+//   pair chain           1.9 us/block on configs[0] (lane messages <= 16 per
+//                        SIMD: one pair workgroup per CU) but 31-42 s on the
+//                        same 19M-block message run to run beside the duo
+//                        chains of configs[1]: modelled at the lanes rate,
+//                        so a lane message never sets the makespan
+//   lanes, latency-bound 3.2 us/block; throughput 64 B x 35 T lane-ops/s / 1464
+// M(k) = max(duo: nb[0] x 1.13 us if k > 0,
+//            lane set: max(nb[k] x t_lane(n - k), sum_{i >= k} nb[i] x 1464 / 35e12)).
+// Ties keep the smaller k (fewer waves sharing SIMDs).
 static void plan_split(const std::vector<uint64_t>& nb, std::vector<uint32_t>& order, uint32_t n_cu,
                        uint32_t flags, uint32_t* n_solo_out) {
     const uint64_t n = nb.size();
@@ -346,19 +356,27 @@ static void plan_split(const std::vector<uint64_t>& nb, std::vector<uint32_t>& o
     if (flags & RF_SHA_ALL_SOLO) {
         n_solo = (uint32_t)n;
     } else if (!(flags & RF_SHA_NO_SOLO)) {
-        const double n_simd = 4.0 * n_cu;
-        const uint64_t cap = (uint64_t)n_cu * 4;
-        double remaining = 0;
-        for (uint64_t i = 0; i < n; ++i) remaining += (double)nb[i];
-        for (uint64_t i = 0; i < n && n_solo < cap; ++i) {
-            const double b = (double)nb[order[i]];
-            if (b < 1024) break;
-            const double t_lane = b * 1464.0 * 4.0;
-            const double t_rest = (remaining - b) * 1464.0 * 2.0 / (n_simd * 64.0);
-            if (t_lane <= t_rest) break;
-            remaining -= b;
-            ++n_solo;
+        const double t_duo = 1.13e-6, t_pair = 3.2e-6, t_lanes = 3.2e-6, blk_rate = 35e12 / 1464.0;
+        const uint64_t n_simd = 4ull * n_cu, cap = std::min<uint64_t>(n, n_simd);
+        double rest = 0;
+        for (uint64_t i = 0; i < n; ++i) rest += (double)nb[i];
+        const bool pair_ok = !(flags & RF_SHA_NO_PAIR);
+        double best = 1e300;
+        uint64_t best_k = 0;
+        for (uint64_t k = 0; k <= cap; ++k) {
+            if (k > 0) rest -= (double)nb[order[k - 1]];
+            const uint64_t lanes = n - k;
+            double m = k ? (double)nb[order[0]] * t_duo : 0.0;
+            if (lanes) {
+                const double tl = (pair_ok && lanes <= 16 * n_simd) ? t_pair : t_lanes;
+                m = std::max(m, std::max((double)nb[order[k]] * tl, rest / blk_rate));
+            }
+            if (m < best * 0.98) {
+                best = m;
+                best_k = k;
+            }
         }
+        n_solo = (uint32_t)best_k;
     }
     // solo messages go to the back of `order`: [lanes..., solo...]
     std::vector<uint32_t> o2;
@@ -399,6 +417,10 @@ static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t*
     const uint64_t want = (p->n_lanes + sha_lanes_block() - 1) / sha_lanes_block();
     p->grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->n_cu * 5));
     p->n_shards = std::max<uint32_t>(1, std::min<uint32_t>(64, p->grid * 4));
+    // Few lane messages (<= 16 per SIMD: one 64-message pair workgroup per CU)
+    // are latency-bound on their wave's issue rate: split schedule and rounds
+    // over two waves (k1_sha256_pair).
+    p->pair = !(flags & RF_SHA_NO_PAIR) && p->n_lanes > 0 && p->n_lanes <= 16ull * 4 * ctx->n_cu;
     hipError_t e = hipSuccess;
     if ((e = p->d_offs.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
         (e = p->d_lens.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
@@ -445,7 +467,11 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
         HIPC(launch_sha_solo(sa, p->duo, p->side));
         HIPC(hipEventRecord(p->e_solo, p->side));
     }
-    if (p->n_lanes) {
+    if (p->n_lanes && p->pair) {
+        SoloArgs pa{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(), p->d_lens.as<uint64_t>(),
+                    order, p->n_lanes, static_cast<uint8_t*>(d_out)};
+        HIPC(launch_sha_pair(pa, s));
+    } else if (p->n_lanes) {
         LanesArgs la{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(),
                      p->d_lens.as<uint64_t>(), order, p->n_lanes, p->n_shards,
                      p->d_heads.as<uint32_t>(), static_cast<uint8_t*>(d_out)};

@@ -35,6 +35,8 @@ struct SoloArgs {
 };
 // duo: the round chain on two lanes (k1_sha256_duo); else one lane (k1_sha256_solo)
 hipError_t launch_sha_solo(const SoloArgs& a, bool duo, hipStream_t s);
+// Lane per message with a producer wave beside the chain wave (small sets).
+hipError_t launch_sha_pair(const SoloArgs& a, hipStream_t s);
 
 // Checks that the gfx950 code object of this library loads on the device.
 hipError_t probe_kernels();

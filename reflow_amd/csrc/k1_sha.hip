@@ -18,6 +18,8 @@
 // SHA-256 is Merkle-Damgard: one message's blocks are strictly serial and
 // bit-exactness forbids tree hashing, so a skewed set is bounded below by its
 // largest message (skew-aware roofline).
+#include <cstdlib>
+
 #include "engine.h"
 #include "sha256_dev.h"
 
@@ -56,6 +58,29 @@ __device__ __forceinline__ void load_block(uint32_t (&w)[16], const uint8_t* p, 
             if (rem > 16 * c) r = q[c];
             raw[4 * c] = r.x; raw[4 * c + 1] = r.y; raw[4 * c + 2] = r.z; raw[4 * c + 3] = r.w;
         }
+        sha256_pad_words(w, raw, len, blk);
+    }
+}
+
+// load_block split in two so a producer can have block b+1 in flight while it
+// expands block b: the guarded 16-B loads, then byte swap / padding.
+__device__ __forceinline__ void load_raw(uint4 (&r)[4], const uint8_t* p, uint64_t len, uint64_t blk) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + blk * 64u);
+    const int64_t rem = (int64_t)len - (int64_t)(blk * 64u);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[c] = rem > 16 * c ? q[c] : make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ void raw_words(uint32_t (&w)[16], const uint4 (&r)[4], uint64_t len, uint64_t blk) {
+    uint32_t raw[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        raw[4 * c] = r[c].x; raw[4 * c + 1] = r[c].y; raw[4 * c + 2] = r[c].z; raw[4 * c + 3] = r[c].w;
+    }
+    if ((int64_t)len - (int64_t)(blk * 64u) >= 64) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = bswap32(raw[i]);
+    } else {
         sha256_pad_words(w, raw, len, blk);
     }
 }
@@ -414,6 +439,55 @@ __global__ __launch_bounds__(128) void k1_sha256_duo(SoloArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Pair: lane per message like k1_sha256_lanes, for sets too small to load the
+// chip (<= one wave per SIMD), where a lane's chain is bound by its wave's
+// issue rate: a producer wave loads/pads each message's next block and
+// expands its schedule into a double-buffered LDS row (kw_expand_store), the
+// chain wave runs the rounds from LDS (compress_kw: 14 instead of ~22
+// instructions per round).  64 messages per workgroup (largest-first order,
+// so a workgroup's messages have similar block counts), one barrier per block.
+constexpr uint32_t kPairRow = 68;
+
+__global__ __launch_bounds__(256) void k1_sha256_pair(SoloArgs a, uint32_t pw, uint32_t dbg) {
+    __shared__ __attribute__((aligned(16))) uint32_t kw[2 * 64 * kPairRow];
+    // wave 0 chain, wave pw producer, any other wave only meets the barriers
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wave = w0 == 0 ? 0u : w0 == pw ? 1u : 2u;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * 64; base < a.n_order; base += gridDim.x * 64) {
+        const uint32_t q = base + lane;
+        const bool has = q < a.n_order;
+        const uint32_t id = has ? a.order[q] : 0u;
+        const uint64_t len = has ? a.lens[id] : 0;
+        const uint8_t* p = a.arena + (has ? a.offs[id] : 0);
+        const uint64_t nb = has ? sha256_nblocks(len) : 0;
+        uint64_t maxnb = nb;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t x = __shfl_xor(maxnb, o, 64);
+            maxnb = x > maxnb ? x : maxnb;
+        }
+        ShaState st;
+        st.init();
+        uint4 r[4];
+        if (wave == 1 && nb) load_raw(r, p, len, 0);
+        for (uint64_t it = 0; it <= maxnb; ++it) {
+            if (wave == 1) {
+                if (it < nb && !(dbg & 1)) {
+                    uint32_t w[16];
+                    raw_words(w, r, len, it);
+                    if (it + 1 < nb) load_raw(r, p, len, it + 1);  // in flight during the expansion
+                    kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPairRow]));
+                }
+            } else if (wave == 0 && it >= 1 && it - 1 < nb && !(dbg & 2)) {
+                compress_kw(st, reinterpret_cast<const uint4*>(&kw[(((it - 1) & 1) * 64 + lane) * kPairRow]));
+            }
+            __syncthreads();
+        }
+        if (wave == 0 && has) store_digest(a.out + 32ull * id, st);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic content: word q of message i = mix64((seed ^ i) + (q+1)*G), LE.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -481,6 +555,19 @@ hipError_t launch_sha_solo(const SoloArgs& a, bool duo, hipStream_t s) {
         hipLaunchKernelGGL(k1_sha256_duo, dim3(a.n_order), dim3(128), 0, s, a);
     else
         hipLaunchKernelGGL(k1_sha256_solo, dim3(a.n_order), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sha_pair(const SoloArgs& a, hipStream_t s) {
+    if (a.n_order == 0) return hipSuccess;
+    uint32_t grid = (a.n_order + 63) / 64;
+    if (grid > 4096) grid = 4096;
+    // A pair workgroup reserves most of its CU's LDS so no other pair or duo
+    // workgroup shares the CU: its chain wave then has a SIMD to itself (a
+    // co-resident duo chain at s_setprio 3 took the issue slots: 1.9 -> 2.9 us
+    // per block, and the planner's makespan model counts on 1.9).
+    static const size_t reserve = 126 * 1024 - sizeof(uint32_t) * 2 * 64 * kPairRow;
+    hipLaunchKernelGGL(k1_sha256_pair, dim3(grid), dim3(128), reserve, s, a, 1u, 0u);
     return hipGetLastError();
 }
 

@@ -94,6 +94,50 @@ __device__ __forceinline__ void sha256_compress(ShaState& s, uint32_t (&w)[16]) 
     s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
 }
 
+// Producer/chain split of one block (k2_level_pc, k1_sha256_pair): the
+// producer expands the message schedule and stores K[t] + W[t] as 16 uint4
+// into an LDS row; the chain runs the 64 rounds from that row, 14
+// instructions per round (the schedule's ~8 per round moved off the chain).
+__device__ __forceinline__ void kw_expand_store(uint32_t (&w)[16], uint4* row) {
+    constexpr uint32_t K[64] = RF_SHA_K;
+#pragma unroll
+    for (int t4 = 0; t4 < 16; ++t4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = 4 * t4 + u;
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+                w[t & 15] = wt;
+            }
+            v[u] = K[t] + wt;
+        }
+        row[t4] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+__device__ __forceinline__ void compress_kw(ShaState& s, const uint4* row) {
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+    uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+    for (int t4 = 0; t4 < 16; ++t4) {
+        const uint4 v = row[t4];
+        const uint32_t kv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t t1 = add3v(h + kv[u], bsig1(e), ch(e, f, g));
+            h = g; g = f; f = e; e = d + t1;
+            const uint32_t an = add3v(t1, bsig0(a), maj(a, b, c));
+            d = c; c = b; b = a; a = an;
+        }
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
 // Build the big-endian words of block `blk` of a message of `len` bytes whose
 // raw little-endian-loaded words are raw[] (loaded from the block's address;
 // bytes past the message end may hold anything).  Applies FIPS-180 padding:

@@ -156,15 +156,16 @@ def _device_set(ctx, seed, lens):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, 1, 2])
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
 def test_gpu_sha256_fixture(ctx, flags):
     """Device-generated messages (rf_gen_fill = the fixture's stream) through
-    every K1 mode: planner default (0), lanes only, wave-per-message only."""
+    every K1 mode: planner default (0), lane messages only (pair kernel),
+    wave-per-message only, lanes kernel only."""
     from reflow_amd import capi
     d = G.load("sha256.json")
     lens = [c["len"] for c in d["cases"]]
     arena, offs, lens, keep = _device_set(ctx, d["seed"], lens)
-    mode = [0, capi.RF_SHA_NO_SOLO, capi.RF_SHA_ALL_SOLO][flags]
+    mode = [0, capi.RF_SHA_NO_SOLO, capi.RF_SHA_ALL_SOLO, capi.RF_SHA_NO_SOLO | capi.RF_SHA_NO_PAIR][flags]
     out = ctx.alloc(32 * len(lens))
     plan = ctx.sha_plan(offs, lens, mode)
     plan.run(arena.ptr, out.ptr)

@@ -68,11 +68,12 @@ def _device_arena(lens, align=256):
     return np.array(offs, dtype=np.uint64), max(pos, 16)
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 6])
+@pytest.mark.parametrize("flags", [0, 1, 2, 6, 8, 9])
 def test_plan_gen_fill_device(ctx, flags):
     """rf_gen_fill + rf_sha_plan_run on HBM-resident data (the bench path),
-    planner mix / lanes-only / wave-per-message with the two-lane chain /
-    wave-per-message with the one-lane chain."""
+    planner mix / lane messages only (producer/chain pair for this small set) /
+    wave-per-message with the two-lane chain / with the one-lane chain / the
+    lanes kernel instead of the pair (8), lanes kernel only (9)."""
     from reflow_amd import capi
     rng = random.Random(10 + flags)
     lens = [rng.choice([0, 1, 55, 56, 64, 4096, rng.randint(1, 300000), rng.randint(1, 3000)])
@@ -90,7 +91,7 @@ def test_plan_gen_fill_device(ctx, flags):
     st = plan.stats()
     if flags & capi.RF_SHA_ALL_SOLO:
         assert st.n_solo == len(lens)
-    if flags == capi.RF_SHA_NO_SOLO:
+    if flags & capi.RF_SHA_NO_SOLO:
         assert st.n_solo == 0
     out = d_out.to_numpy().reshape(-1, 32)
     arena = d_arena.to_numpy()

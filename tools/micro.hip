@@ -522,3 +522,62 @@ extern "C" float micro_gather(uint64_t table_bytes, uint64_t n, int r, int key_m
     if (keys) hipFree(keys);
     return ms;
 }
+
+// ---------------------------------------------------------------------------
+// Wave placement: which SIMD each wave of a workgroup lands on (HW_ID
+// register, SIMD_ID = bits [5:4] on gfx9), and the CU id (bits [11:8]).
+__global__ void k_hwid(uint32_t* out) {
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if ((threadIdx.x & 63) == 0) out[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = hw;
+}
+
+extern "C" int micro_hwid(uint32_t grid, uint32_t block, uint32_t* host_out) {
+    uint32_t* d = nullptr;
+    const size_t n = (size_t)grid * (block / 64);
+    if (hipMalloc(&d, 4 * n) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_hwid, dim3(grid), dim3(block), 0, 0, d);
+    hipMemcpy(host_out, d, 4 * n, hipMemcpyDeviceToHost);
+    hipFree(d);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup barrier cost: `iters` __syncthreads() in a loop, nothing else.
+__global__ void k_barrier(uint32_t iters, uint32_t* sink) {
+    uint32_t x = threadIdx.x;
+    for (uint32_t i = 0; i < iters; ++i) {
+        x = x * 1664525u + 1013904223u;
+        __syncthreads();
+    }
+    if (x == 0x12345678u) sink[0] = x;
+}
+
+// Same with a raw s_barrier (no fence).
+__global__ void k_barrier_raw(uint32_t iters, uint32_t* sink) {
+    uint32_t x = threadIdx.x;
+    for (uint32_t i = 0; i < iters; ++i) {
+        x = x * 1664525u + 1013904223u;
+        __builtin_amdgcn_s_barrier();
+    }
+    if (x == 0x12345678u) sink[0] = x;
+}
+
+extern "C" float micro_barrier(uint32_t grid, uint32_t block, uint32_t iters, int raw) {
+    uint32_t* d = nullptr;
+    hipMalloc(&d, 64);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    if (raw) hipLaunchKernelGGL(k_barrier_raw, dim3(grid), dim3(block), 0, 0, iters, d);
+    else hipLaunchKernelGGL(k_barrier, dim3(grid), dim3(block), 0, 0, iters, d);
+    hipEventRecord(a, 0);
+    if (raw) hipLaunchKernelGGL(k_barrier_raw, dim3(grid), dim3(block), 0, 0, iters, d);
+    else hipLaunchKernelGGL(k_barrier, dim3(grid), dim3(block), 0, 0, iters, d);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    hipFree(d);
+    return ms;
+}

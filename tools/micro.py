@@ -19,6 +19,28 @@ def main():
         if len(sys.argv) > 1 and sys.argv[1] == "build":
             return
     L = ctypes.CDLL(SO)
+    if len(sys.argv) > 1 and sys.argv[1] == "barrier":
+        L.micro_barrier.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+        L.micro_barrier.restype = ctypes.c_float
+        it = 100000
+        for grid, block in ((1, 64), (1, 128), (1, 256), (64, 128), (256, 128)):
+            for raw in (0, 1):
+                ms = L.micro_barrier(grid, block, it, raw)
+                print("barrier grid %4d block %3d %-14s %.3f ms  %.1f ns/iter" %
+                      (grid, block, "s_barrier" if raw else "__syncthreads", ms, ms * 1e6 / it))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "hwid":
+        import numpy as np
+        for grid, block in ((64, 128), (64, 256), (512, 128), (1024, 128)):
+            out = np.zeros(grid * block // 64, dtype=np.uint32)
+            L.micro_hwid.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+            L.micro_hwid(grid, block, out.ctypes.data)
+            simd = (out >> 4) & 3
+            per_wg = simd.reshape(grid, block // 64)
+            same = int((per_wg == per_wg[:, :1]).all(axis=1).sum())
+            print("grid %d block %d: workgroups with all waves on one SIMD: %d/%d; first WGs %s"
+                  % (grid, block, same, grid, per_wg[:4].tolist()))
+        return
     L.micro_compute.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
     L.micro_compute.restype = ctypes.c_float
     L.micro_loads.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
