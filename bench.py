@@ -444,10 +444,12 @@ def bench_probe(args, dist, ctx):
                                "words_per_probe": round(reads / n_probe, 3), "filter_fill": round(f, 4),
                                "peak_kind": "measured live: tools/micro.hip k_gather, k independent "
                                             "random 8-B reads per thread over a table of the filter's size"}}
-    # bounded sample for the CPU leg: the filter words and the first 2e7 probe keys
-    ns = min(n_probe, 20_000_000)
-    res["_cpu"] = {"words": b.words(), "length": b.params()[2], "m": m, "k": k,
-                   "keys": keys.to_numpy(count=32 * ns), "n": ns}
+    # bounded sample for the CPU leg (rank 0, N=1): the filter words and the
+    # first 2e7 probe keys
+    if dist.world == 1 and "cpu" not in args.skip:
+        ns = min(n_probe, 20_000_000)
+        res["_cpu"] = {"words": b.words(), "length": b.params()[2], "m": m, "k": k,
+                       "keys": keys.to_numpy(count=32 * ns), "n": ns}
     for x in (keys, out, d_offs, d_lens):
         x.free()
     b.close()
@@ -691,7 +693,7 @@ def main():
     cpu = None
     if dist.rank == 0 and dist.world == 1 and "cpu" not in skip:
         cpu = cpu_baseline(args, sha, dag)
-        if probe is not None:
+        if probe is not None and "_cpu" in probe:
             cpu.update(cpu_probe_and_tables(probe))
     if probe is not None:
         probe.pop("_cpu", None)

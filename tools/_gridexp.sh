@@ -1,2 +1,6 @@
 set -e
-timeout -k 10 300 python -u bench.py --sha-gib 0.25 --dag-samples 200 --skip cpu,dag,probe 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['c1']['file_ids_ms'], d['c1']['fixture_match'])"
+for r in 0 40 82; do
+  export RF_K2_RESERVE=$r
+  echo "reserve $r KiB"
+  timeout -k 10 120 python tools/dag_probe.py --dag-steps 50 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['mnodes_per_s'])"
+done
