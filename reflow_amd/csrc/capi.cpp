@@ -802,6 +802,7 @@ struct rf_graph {
     std::vector<int64_t> producer;   // slot -> external job or -1
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
+    DevBuf b_stamps;
     DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_counts,
         b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
@@ -877,6 +878,24 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     if (q.size() != J) return fail(RF_EINVAL, "job graph has a cycle (%zu of %u jobs ordered)", q.size(), J);
     uint32_t L = 0;
     for (uint32_t j = 0; j < J; ++j) L = std::max(L, level[j] + 1);
+    // Fused chains (k2_level_pc): job j's fusion target is a consumer k whose
+    // material has exactly one hole -- j's digest -- so k depends on nothing
+    // else and can be hashed right after j, in the same lane, without being
+    // queued.  Its reverse edge is moved to the end of j's consumer range.
+    std::vector<int64_t> fuse(J, -1);
+    std::vector<uint8_t> fused_target(J, 0);
+    for (uint32_t j = 0; j < J; ++j) {
+        const uint32_t s = d->out_slot[j];
+        for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
+            const uint32_t k = cjob[c];
+            if (d->hole_ptr[k + 1] - d->hole_ptr[k] == 1 && !fused_target[k]) {
+                fuse[j] = k;
+                fused_target[k] = 1;
+                std::swap(cjob[c], cjob[cptr[s + 1] - 1]);
+                break;
+            }
+        }
+    }
     // internal order: level ascending, blocks descending (similar lanes per wave)
     std::vector<uint32_t> perm(J);
     std::iota(perm.begin(), perm.end(), 0u);
@@ -912,6 +931,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         m[4] = s;
         m[5] = (uint32_t)cptr[s];
         m[6] = (uint32_t)cptr[s + 1];
+        m[7] = fuse[j] >= 0 ? gr->ext2int[(uint32_t)fuse[j]] : 0xffffffffu;
         tb += 64ull * nblk[j];
         gr->total_blocks += nblk[j];
     }
@@ -936,6 +956,9 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         cons_job[2 * c + 1] = level[cjob[c]];
     }
     gr->hole_count = H;
+    gr->g.inc_level.assign(L, 0);
+    for (uint32_t j = 0; j < J; ++j)
+        if (!fused_target[j]) gr->g.inc_level[level[j]] = 1;
     gr->tmpl_bytes = tb;
     // upload
     GraphDev& G = gr->g;
@@ -976,6 +999,11 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     G.counts = gr->b_counts.as<uint32_t>();
     G.counts_last = gr->b_counts_last.as<uint32_t>();
     G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
+    if (getenv("RF_K2_STAMPS")) {  // diagnostic: per-phase times of workgroup 0 of each level
+        HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
+        HIPC(hipMemset(gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
+        G.stamps = static_cast<unsigned long long*>(gr->b_stamps.p);
+    }
     HIPC(hipEventCreate(&gr->e0));
     HIPC(hipEventCreate(&gr->e1));
     guard.release();
@@ -1096,12 +1124,24 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
     DevGuard dg(ctx->device);
     if (int rc = graph_recompute_locked(gr, full, ctx->stream)) return rc;
     std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
-    if (gr->g.n_levels)
-        HIPC(hipMemcpyAsync(counts.data(), gr->g.counts_last, 4ull * gr->g.n_levels,
+    if (gr->g.n_levels)  // [L]: jobs hashed inside fused chains
+        HIPC(hipMemcpyAsync(counts.data(), gr->g.counts_last, 4ull * (gr->g.n_levels + 1),
                             hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
     uint64_t tot = 0;
-    for (uint32_t l = 0; l < gr->g.n_levels; ++l) tot += counts[l];
+    for (uint32_t l = 0; l <= gr->g.n_levels; ++l) tot += counts[l];
+    if (gr->g.stamps && !full) {  // diagnostic print: per level, chain wave then producer wave
+        std::vector<unsigned long long> st(128ull * gr->g.n_levels);
+        HIPC(hipMemcpy(st.data(), gr->g.stamps, 8 * st.size(), hipMemcpyDeviceToHost));
+        for (uint32_t l = 0; l < gr->g.n_levels; ++l)
+            for (int w = 0; w < 2; ++w) {
+                const unsigned long long* x = &st[128ull * l + 64 * w];
+                if (!x[0]) continue;
+                fprintf(stderr, "[stamps] level %u wave %d:", l, w);
+                for (int k = 1; k < 64 && x[k]; ++k) fprintf(stderr, " %.2f", (x[k] - x[k - 1]) * 0.01);
+                fprintf(stderr, " (us)\n");
+            }
+    }
     gr->last_recomputed = tot;
     if (out_recomputed) *out_recomputed = tot;
     return RF_OK;

@@ -50,7 +50,8 @@ struct GraphDev {
     // jobs in internal (level) order
     // job record, 32 B, one pair of 16-B loads per job:
     //   meta[2j]   = {template offset / 64, blocks, hole_begin, hole_end}
-    //   meta[2j+1] = {out slot, consumer_begin, consumer_end, 0}
+    //   meta[2j+1] = {out slot, consumer_begin, consumer_end, fusion target or ~0}
+    //   (the fusion target's reverse edge is the last of the range)
     uint4* meta = nullptr;           // [2J]
     uint2* holes = nullptr;          // [H] {byte position, slot}
     uint32_t* cons_ptr = nullptr;    // [S+1] slot -> consumer jobs (internal ids)
@@ -59,10 +60,12 @@ struct GraphDev {
     uint8_t* slots = nullptr;        // [S][32] digest table
     uint32_t* dirty = nullptr;       // [(J+31)/32] queued-this-step bitset over internal ids
     uint32_t* list = nullptr;        // [J] per-level work lists (level l at lvl_start[l])
-    uint32_t* counts = nullptr;      // [L] list lengths (append cursors) of the current step
-    uint32_t* counts_last = nullptr; // [L] jobs hashed per level by the last recompute
+    uint32_t* counts = nullptr;      // [L+1] list lengths (append cursors); [L] = fused jobs hashed
+    uint32_t* counts_last = nullptr; // [L+1] jobs hashed per level by the last recompute; [L] fused
     uint32_t* lvl_start_dev = nullptr; // [L+1]
     std::vector<uint32_t> lvl_start; // host copy [L+1]
+    std::vector<uint8_t> inc_level;  // [L] level has jobs that can be queued (not all fusion targets)
+    unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
 };
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);

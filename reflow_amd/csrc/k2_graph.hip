@@ -50,6 +50,7 @@ struct LevelArgs {
     uint32_t* dirty;
     uint32_t* list;
     uint32_t* counts;
+    unsigned long long* stamps;  // diagnostic (RF_K2_STAMPS): phase times of workgroup 0, else null
 };
 
 // Append the lanes' jobs j (need) at level lv to their levels' lists; one
@@ -120,32 +121,47 @@ __device__ __forceinline__ void ring_put(uint32_t* ring, uint32_t half, const ui
 // pipeline: while block b is consumed, the template of block b+2 and the (at
 // most two: holes are >= 32 B apart) holes that start in block b+1 -- records
 // and slot digests -- are in flight.
+struct PendingHole {
+    uint2 r;  // (material byte, slot), or ~0 past the job's last hole
+    uint4 lo, hi;
+};
+
 struct MatCursor {
+    // holes hn .. hn+3 in flight: a block applies at most two (holes are >= 32 B
+    // apart), so each hole's record -> slot digest chain is issued at least one
+    // whole block before its own block
     const uint4* __restrict__ T;
     uint32_t nb, he, hn;
-    uint2 R[2];
-    uint4 DL[2], DH[2], t[4];
+    PendingHole q0, q1, q2, q3;
+    uint4 t[4];
+    uint32_t fslot = ~0u;  // a slot whose new digest is handed over in registers (fused chains)
+    uint4 flo, fhi;
 
-    __device__ __forceinline__ void fetch_holes(const LevelArgs& a) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            R[k] = hn + k < he ? a.holes[hn + k] : make_uint2(~0u, 0u);
-            const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * R[k].y);
-            DL[k] = src[0];
-            DH[k] = src[1];
-        }
+    __device__ __forceinline__ void fetch(const LevelArgs& a, PendingHole& q, uint32_t h) const {
+        q.r = h < he ? a.holes[h] : make_uint2(~0u, 0u);
+        const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * (q.r.y == ~0u ? 0u : q.r.y));
+        q.lo = src[0];
+        q.hi = src[1];
+    }
+    __device__ __forceinline__ void apply(uint32_t* ring, const PendingHole& q) const {
+        const bool f = q.r.y == fslot;
+        const uint4 lo = f ? flo : q.lo, hi = f ? fhi : q.hi;
+        const uint32_t D[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        or_digest(ring, q.r.x, D);
     }
     __device__ __forceinline__ void begin(const LevelArgs& a, const uint4& m0, uint32_t* ring) {
         T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
         nb = m0.y;
         he = m0.w;
         hn = m0.z;  // first hole not yet applied
-        fetch_holes(a);
+        fetch(a, q0, hn);
+        fetch(a, q1, hn + 1);
+        fetch(a, q2, hn + 2);
+        fetch(a, q3, hn + 3);
         t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
         ring_put(ring, 0, t);
         if (nb > 1) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) t[q] = T[4 + q];
+            t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
         }
     }
     // the 16 big-endian words of block b (blocks taken in order)
@@ -154,23 +170,28 @@ struct MatCursor {
         if (b + 1 < nb) {
             ring_put(ring, half ^ 16, t);
             if (b + 2 < nb) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) t[q] = T[4 * (b + 2) + q];
+                const uint4* s = T + 4 * (b + 2);
+                t[0] = s[0]; t[1] = s[1]; t[2] = s[2]; t[3] = s[3];
             }
         }
         // holes that start in block b (they may run into block b+1)
-        uint32_t used = 0;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (R[k].x < 64 * (b + 1)) {
-                const uint32_t D[8] = {DL[k].x, DL[k].y, DL[k].z, DL[k].w, DH[k].x, DH[k].y, DH[k].z, DH[k].w};
-                or_digest(ring, R[k].x, D);
-                ++used;
+        const uint32_t lim = 64 * (b + 1);
+        if (q0.r.x < lim) {
+            apply(ring, q0);
+            if (q1.r.x < lim) {
+                apply(ring, q1);
+                q0 = q2;
+                q1 = q3;
+                hn += 2;
+                fetch(a, q2, hn + 2);
+                fetch(a, q3, hn + 3);
+            } else {
+                q0 = q1;
+                q1 = q2;
+                q2 = q3;
+                hn += 1;
+                fetch(a, q3, hn + 3);
             }
-        }
-        if (used) {
-            hn += used;
-            fetch_holes(a);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
@@ -287,9 +308,23 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
 // bit and propagates like k2_level.
 constexpr uint32_t kPcRow = 68;  // words per K+W row: 16-B reads of 64 rows hit distinct banks
 
+// Fused chains: a job whose only input is one job's digest, and which that
+// job names as its fusion target (meta[2j+1].w, rf_graph_load), is never
+// queued; whoever hashes its producer hashes it next, in the same lane, as
+// soon as the producer's digest changed -- no level barrier between them (the
+// 1000align pair chain Exec -> Coerce -> K -> ... is ten such jobs deep).  The
+// producer's new digest reaches the fused job's material through LDS.
+#define RF_STAMP(k)                                                                        \
+    do {                                                                                   \
+        if (a.stamps && blockIdx.x == 0 && lane == 0 && (k) < 64)                          \
+            a.stamps[128 * a.lvl + 64 * wave + (k)] = __builtin_amdgcn_s_memrealtime();    \
+    } while (0)
+
 __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t kw[2 * 64 * kPcRow];
     __shared__ uint32_t ring_all[64 * kRing];
+    __shared__ uint4 s_dig[64][2];   // the last job's new digest (raw words)
+    __shared__ uint32_t s_next[64];  // the lane's next (fused) job, or ~0
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 chain, 1 producer
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* ring = &ring_all[lane * kRing];
@@ -297,51 +332,87 @@ __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
     const uint32_t* lst = a.list + a.s;
     for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
         const uint32_t i = base + lane;
-        const bool has = i < n;
-        const uint32_t p = has ? lst[i] : 0u;
-        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-        if (has) {
-            m0 = a.meta[2 * p];
-            m1 = a.meta[2 * p + 1];
-        }
-        // both waves read the same records: the same block count for the loop
-        uint32_t maxnb = m0.y;
-        for (int o = 32; o > 0; o >>= 1) maxnb = max(maxnb, (uint32_t)__shfl_xor((int)maxnb, o, 64));
-        maxnb = __builtin_amdgcn_readfirstlane(maxnb);
-        MatCursor cur;
-        ShaState st;
-        st.init();
-        uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
-        uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
-        if (wave == 1 && has) cur.begin(a, m0, ring);
-        if (wave == 0 && has) {  // the chain wave waits for block 0 anyway: fetch what finishing needs
-            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
-            olo = od[0];
-            ohi = od[1];
-            if (m1.y < m1.z) pre[0] = a.cons[m1.y];
-            if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
-        }
-        for (uint32_t it = 0; it <= maxnb; ++it) {
-            if (wave == 1) {
-                if (it < m0.y) {  // block it of this lane's job -> buffer it & 1
-                    uint32_t w[16];
-                    cur.block(a, it, ring, w);
-                    kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
-                }
-            } else if (it >= 1 && it - 1 < m0.y) {  // block it-1 from buffer (it-1) & 1
-                compress_kw(st, reinterpret_cast<const uint4*>(&kw[(((it - 1) & 1) * 64 + lane) * kPcRow]));
-            }
-            __syncthreads();
-        }
-        if (wave == 0) {
-            uint32_t cb = 0, ce = 0;
+        bool has = i < n;
+        uint32_t p = has ? lst[i] : 0u;
+        uint32_t fslot = ~0u;  // the previous job's out slot (fused hand-over)
+        uint32_t sk = 0;
+        // both waves hold the same per-lane job, so this loop is uniform
+        while (__any(has)) {
+            RF_STAMP(sk); ++sk;
+            uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
             if (has) {
-                const bool changed = finish_job_pre(a, m1, st, olo, ohi);
-                atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
-                cb = m1.y;
-                ce = changed ? m1.z : m1.y;
+                m0 = a.meta[2 * p];
+                m1 = a.meta[2 * p + 1];
             }
-            propagate_pre(a, cb, ce, pre);
+            uint32_t maxnb = m0.y;
+            for (int o = 32; o > 0; o >>= 1) maxnb = max(maxnb, (uint32_t)__shfl_xor((int)maxnb, o, 64));
+            maxnb = __builtin_amdgcn_readfirstlane(maxnb);
+            MatCursor cur;
+            ShaState st;
+            st.init();
+            uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
+            uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+            if (wave == 1 && has) {
+                cur.fslot = fslot;
+                if (fslot != ~0u) {
+                    cur.flo = s_dig[lane][0];
+                    cur.fhi = s_dig[lane][1];
+                }
+                cur.begin(a, m0, ring);
+            }
+            if (wave == 0 && has) {  // the chain wave waits for block 0 anyway: fetch what finishing needs
+                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+                olo = od[0];
+                ohi = od[1];
+                if (m1.y < m1.z) pre[0] = a.cons[m1.y];
+                if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+            }
+            for (uint32_t it = 0; it <= maxnb; ++it) {
+                if (wave == 1) {
+                    if (it < m0.y) {  // block it of this lane's job -> buffer it & 1
+                        uint32_t w[16];
+                        cur.block(a, it, ring, w);
+                        kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
+                    }
+                } else if (it >= 1 && it - 1 < m0.y) {  // block it-1 from buffer (it-1) & 1
+                    compress_kw(st, reinterpret_cast<const uint4*>(&kw[(((it - 1) & 1) * 64 + lane) * kPcRow]));
+                }
+                __syncthreads();
+                RF_STAMP(sk); ++sk;
+            }
+            if (wave == 0) {
+                uint32_t cb = 0, ce = 0, next = ~0u;
+                if (has) {
+                    const bool changed = finish_job_pre(a, m1, st, olo, ohi);
+                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                    cb = m1.y;
+                    ce = m1.y;
+                    if (changed) {
+                        // the fusion target's edge is the last of the range
+                        const bool fuse = m1.w != ~0u;
+                        ce = fuse ? m1.z - 1 : m1.z;
+                        if (fuse) {
+                            next = m1.w;
+                            s_dig[lane][0] = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
+                                                        bswap32(st.h[3]));
+                            s_dig[lane][1] = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]),
+                                                        bswap32(st.h[7]));
+                        }
+                    }
+                }
+                propagate_pre(a, cb, ce, pre);
+                s_next[lane] = next;
+                const uint64_t fb = __ballot(next != ~0u);
+                if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));  // fused jobs hashed
+            }
+            const uint32_t out_slot = m1.x;
+            RF_STAMP(sk); ++sk;
+            __syncthreads();
+            const uint32_t nx = s_next[lane];
+            fslot = has ? out_slot : ~0u;
+            has = nx != ~0u;
+            p = has ? nx : 0u;
+            __syncthreads();  // s_next / s_dig are rewritten by the next job's finish
         }
     }
 }
@@ -378,8 +449,9 @@ __global__ __launch_bounds__(256) void k3_mark_slots(const uint32_t* __restrict_
 // End of a recompute: record what each level hashed, reset the lists.
 __global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __restrict__ ls, uint32_t L,
                             int full) {
-    for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
-        last[l] = full ? ls[l + 1] - ls[l] : counts[l];
+    // counts[L]: jobs hashed inside fused chains (never queued)
+    for (uint32_t l = threadIdx.x; l <= L; l += blockDim.x) {
+        last[l] = l == L ? (full ? 0u : counts[L]) : full ? ls[l + 1] - ls[l] : counts[l];
         counts[l] = 0;
     }
 }
@@ -426,15 +498,15 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     if (e <= b) return hipSuccess;
     static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u : 0u;
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
         const char* v = getenv("RF_INC_GRID");
         return v ? (uint32_t)atoi(v) : 1024u;
     }();
-    static const bool lanes_only = getenv("RF_K2_LANES") != nullptr;  // diagnostic: lane-per-job hashing
-    if (!full && !lanes_only) {
+    if (!full) {
+        if (!g.inc_level[lvl]) return hipSuccess;  // every job of the level is a fusion target
         uint64_t g = (e - b + 63) / 64;
         if (g > 2048) g = 2048;
         hipLaunchKernelGGL(k2_level_pc, dim3((uint32_t)g), dim3(128), 0, s, a);
