@@ -127,18 +127,23 @@ struct PendingHole {
 };
 
 struct MatCursor {
-    // holes hn .. hn+3 in flight: a block applies at most two (holes are >= 32 B
-    // apart), so each hole's record -> slot digest chain is issued at least one
-    // whole block before its own block
+    // holes hn .. hn+3 in flight with their slot digests, and the records of
+    // hn+4 and hn+5: a block applies at most two holes (they are >= 32 B apart),
+    // so a record arrives a block before its digest load is issued, and the
+    // digest a block before it is applied
     const uint4* __restrict__ T;
     uint32_t nb, he, hn;
     PendingHole q0, q1, q2, q3;
+    uint2 r4, r5;
     uint4 t[4];
     uint32_t fslot = ~0u;  // a slot whose new digest is handed over in registers (fused chains)
     uint4 flo, fhi;
 
-    __device__ __forceinline__ void fetch(const LevelArgs& a, PendingHole& q, uint32_t h) const {
-        q.r = h < he ? a.holes[h] : make_uint2(~0u, 0u);
+    __device__ __forceinline__ uint2 record(const LevelArgs& a, uint32_t h) const {
+        return h < he ? a.holes[h] : make_uint2(~0u, 0u);
+    }
+    __device__ __forceinline__ void digest(const LevelArgs& a, PendingHole& q, const uint2& r) const {
+        q.r = r;
         const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * (q.r.y == ~0u ? 0u : q.r.y));
         q.lo = src[0];
         q.hi = src[1];
@@ -154,15 +159,32 @@ struct MatCursor {
         nb = m0.y;
         he = m0.w;
         hn = m0.z;  // first hole not yet applied
-        fetch(a, q0, hn);
-        fetch(a, q1, hn + 1);
-        fetch(a, q2, hn + 2);
-        fetch(a, q3, hn + 3);
+        digest(a, q0, record(a, hn));
+        digest(a, q1, record(a, hn + 1));
+        digest(a, q2, record(a, hn + 2));
+        digest(a, q3, record(a, hn + 3));
+        r4 = record(a, hn + 4);
+        r5 = record(a, hn + 5);
         t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
         ring_put(ring, 0, t);
         if (nb > 1) {
             t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
         }
+    }
+    // begin() for a fused job: its one hole reads the slot handed over in
+    // registers, and its first two template blocks and hole record were
+    // prefetched while its producer was hashed
+    __device__ __forceinline__ void begin_pre(const uint4& m0, const uint4* __restrict__ tmpl, const uint4 (&nt)[8],
+                                              const uint2& nr, uint32_t* ring) {
+        T = tmpl + 4ull * m0.x;
+        nb = m0.y;
+        he = m0.w;
+        hn = m0.z;
+        q0.r = nr;
+        q1.r = q2.r = q3.r = r4 = r5 = make_uint2(~0u, 0u);
+        t[0] = nt[0]; t[1] = nt[1]; t[2] = nt[2]; t[3] = nt[3];
+        ring_put(ring, 0, t);
+        t[0] = nt[4]; t[1] = nt[5]; t[2] = nt[6]; t[3] = nt[7];
     }
     // the 16 big-endian words of block b (blocks taken in order)
     __device__ __forceinline__ void block(const LevelArgs& a, uint32_t b, uint32_t* ring, uint32_t (&w)[16]) {
@@ -183,14 +205,18 @@ struct MatCursor {
                 q0 = q2;
                 q1 = q3;
                 hn += 2;
-                fetch(a, q2, hn + 2);
-                fetch(a, q3, hn + 3);
+                digest(a, q2, r4);
+                digest(a, q3, r5);
+                r4 = record(a, hn + 4);
+                r5 = record(a, hn + 5);
             } else {
                 q0 = q1;
                 q1 = q2;
                 q2 = q3;
                 hn += 1;
-                fetch(a, q3, hn + 3);
+                digest(a, q3, r4);
+                r4 = r5;
+                r5 = record(a, hn + 5);
             }
         }
 #pragma unroll
@@ -306,6 +332,15 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
 // the current block from LDS (14 instructions per round: ~910 per block).
 // One workgroup barrier per block; the chain then stores, clears the queued
 // bit and propagates like k2_level.
+// Workgroup barrier for LDS hand-overs only.  __syncthreads() is a release /
+// acquire fence as well, which waits for every outstanding global load and
+// store of the wave (s_waitcnt vmcnt(0)): each block would then wait out the
+// HBM latency of the template and hole loads just issued for later blocks.
+// Nothing here is passed between the two waves through global memory.
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 constexpr uint32_t kPcRow = 68;  // words per K+W row: 16-B reads of 64 rows hit distinct banks
 
 // Fused chains: a job whose only input is one job's digest, and which that
@@ -336,13 +371,31 @@ __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
         uint32_t p = has ? lst[i] : 0u;
         uint32_t fslot = ~0u;  // the previous job's out slot (fused hand-over)
         uint32_t sk = 0;
+        // the fusion target's meta, first template blocks, hole record (producer)
+        // and old digest + first reverse edges (chain), prefetched while its
+        // producer is hashed: a fused job starts without a dependent HBM chain
+        uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0;
+        uint4 nt[8];
+        uint2 nr = make_uint2(0, 0);
+        uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
         // both waves hold the same per-lane job, so this loop is uniform
         while (__any(has)) {
             RF_STAMP(sk); ++sk;
+            const bool fused = fslot != ~0u;
             uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
             if (has) {
-                m0 = a.meta[2 * p];
-                m1 = a.meta[2 * p + 1];
+                if (fused) {
+                    m0 = nm0;
+                    m1 = nm1;
+                } else {
+                    m0 = a.meta[2 * p];
+                    m1 = a.meta[2 * p + 1];
+                }
+            }
+            const bool nfu = has && m1.w != ~0u;
+            if (nfu) {
+                nm0 = a.meta[2ull * m1.w];
+                nm1 = a.meta[2ull * m1.w + 1];
             }
             uint32_t maxnb = m0.y;
             for (int o = 32; o > 0; o >>= 1) maxnb = max(maxnb, (uint32_t)__shfl_xor((int)maxnb, o, 64));
@@ -354,18 +407,34 @@ __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
             uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
             if (wave == 1 && has) {
                 cur.fslot = fslot;
-                if (fslot != ~0u) {
+                if (fused) {
                     cur.flo = s_dig[lane][0];
                     cur.fhi = s_dig[lane][1];
+                    cur.begin_pre(m0, reinterpret_cast<const uint4*>(a.tmpl), nt, nr, ring);
+                } else {
+                    cur.begin(a, m0, ring);
                 }
-                cur.begin(a, m0, ring);
             }
             if (wave == 0 && has) {  // the chain wave waits for block 0 anyway: fetch what finishing needs
-                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
-                olo = od[0];
-                ohi = od[1];
-                if (m1.y < m1.z) pre[0] = a.cons[m1.y];
-                if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+                if (fused) {
+                    olo = nolo;
+                    ohi = nohi;
+                    pre[0] = npre[0];
+                    pre[1] = npre[1];
+                } else {
+                    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+                    olo = od[0];
+                    ohi = od[1];
+                    if (m1.y < m1.z) pre[0] = a.cons[m1.y];
+                    if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+                }
+                if (nfu) {
+                    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
+                    nolo = od[0];
+                    nohi = od[1];
+                    if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
+                    if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
+                }
             }
             for (uint32_t it = 0; it <= maxnb; ++it) {
                 if (wave == 1) {
@@ -374,10 +443,18 @@ __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
                         cur.block(a, it, ring, w);
                         kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
                     }
+                    if (it == 0 && nfu) {
+                        const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
+                        nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
+                        if (nm0.y > 1) {
+                            nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
+                        }
+                        nr = a.holes[nm0.z];
+                    }
                 } else if (it >= 1 && it - 1 < m0.y) {  // block it-1 from buffer (it-1) & 1
                     compress_kw(st, reinterpret_cast<const uint4*>(&kw[(((it - 1) & 1) * 64 + lane) * kPcRow]));
                 }
-                __syncthreads();
+                lds_barrier();
                 RF_STAMP(sk); ++sk;
             }
             if (wave == 0) {
@@ -407,12 +484,12 @@ __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
             }
             const uint32_t out_slot = m1.x;
             RF_STAMP(sk); ++sk;
-            __syncthreads();
+            lds_barrier();
             const uint32_t nx = s_next[lane];
             fslot = has ? out_slot : ~0u;
             has = nx != ~0u;
             p = has ? nx : 0u;
-            __syncthreads();  // s_next / s_dig are rewritten by the next job's finish
+            lds_barrier();  // s_next / s_dig are rewritten by the next job's finish
         }
     }
 }
