@@ -231,16 +231,26 @@ def bench_c1(args, dist, ctx):
         plan.run(arena.ptr, out.ptr)
     ctx.sync()
     ids_ms = (time.perf_counter() - t0) / reps * 1e3
+    # Fileset digest over the IDs where K1 left them (rf_fileset_digest_device:
+    # path material from the host, IDs placed on the device); the paths are
+    # marshalled once, outside the timed region
+    fp = ctx.fileset_paths([[[c1_path(i) for i in range(C1_N)]]])
+    fp.digest_device(out.ptr)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fsd = fp.digest_device(out.ptr)[0]
+    fs_ms = (time.perf_counter() - t0) / reps * 1e3
+    # the host-ID form (IDs read back, rf_fileset_digest_batch), for comparison
     t0 = time.perf_counter()
     ids = out.to_numpy().reshape(-1, 32)
     d2h_ms = (time.perf_counter() - t0) * 1e3
     group = [[[(c1_path(i), ids[i].tobytes()) for i in range(C1_N)]]]  # harness-side argument building
     ctx.fileset_digest_batch(group)
     t0 = time.perf_counter()
-    fsd = ctx.fileset_digest_batch(group)[0]
-    fs_ms = (time.perf_counter() - t0) * 1e3 + d2h_ms
+    fsd_host = ctx.fileset_digest_batch(group)[0]
+    fs_host_ms = (time.perf_counter() - t0) * 1e3 + d2h_ms
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "c1_fileset.json")))
-    ok = ("sha256:" + fsd.hex() == want["fileset_digest"] and
+    ok = ("sha256:" + fsd.hex() == want["fileset_digest"] and fsd_host == fsd and
           __import__("hashlib").sha256(ids.tobytes()).hexdigest() == want["ids_sha256"])
     plan.close()
     for b in (arena, d_offs, d_lens, out):
@@ -260,8 +270,9 @@ def bench_c1(args, dist, ctx):
     return {"workload": "configs[0]: 4096 x 256 KiB files (1 GiB) -> File IDs + Fileset digest; CacheKeys "
                         "of a %d-node 1000align DAG (%d jobs)" % (small.n_nodes, small.n_jobs),
             "file_ids_ms": ids_ms, "file_ids_gbps": C1_N * C1_LEN / (ids_ms * 1e-3) / 1e9,
-            "fileset_digest_ms": fs_ms, "fileset_digest_note": "File IDs read back + rf_fileset_digest_batch "
-            "(bytewise sort, material on the host, one %d-block message on the duo chain)" % ((C1_N * 49 + 9 + 63) // 64),
+            "fileset_digest_ms": fs_ms, "fileset_digest_note": "rf_fileset_digest_device: bytewise sort and path "
+            "material on the host, IDs placed from HBM, one %d-block message on the duo chain" % ((C1_N * 49 + 9 + 63) // 64),
+            "fileset_digest_host_ids_ms": fs_host_ms,
             "fixture_match": ok,
             "dag_nodes": small.n_nodes, "dag_full_recompute_ms": dag_ms,
             "total_ms": ids_ms + fs_ms + dag_ms,

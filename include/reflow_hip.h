@@ -138,6 +138,14 @@ int rf_gen_fill(rf_ctx *ctx, void *d_arena, const uint64_t *d_offs, const uint64
 int rf_fileset_digest_batch(rf_ctx *ctx, uint64_t n_sets, const uint64_t *set_group,
                             const uint64_t *group_entry, const char *const *paths,
                             const uint32_t *path_lens, const uint8_t *ids32, uint8_t *out32);
+/* As rf_fileset_digest_batch with the File IDs resident in HBM (d_ids32[e],
+ * e.g. the out32 of an rf_sha_plan_run over the installed files): no ID
+ * readback; the IDs are placed into the material on the device and only the
+ * set digests return (Executor.install -> Fileset.Digest,
+ * local/executor.go:514-557 + executor.go:205-233). */
+int rf_fileset_digest_device(rf_ctx *ctx, uint64_t n_sets, const uint64_t *set_group,
+                             const uint64_t *group_entry, const char *const *paths,
+                             const uint32_t *path_lens, const void *d_ids32, uint8_t *out32);
 
 /* ---- Fileset values as JSON (the assoc value, eval.go:1141 -> marshal
  * eval.go:1961-1967 = json.Marshal + Repository.Put, repository.go:108-114) --

@@ -25,6 +25,7 @@ EXPORTS = [
     "rf_init", "rf_destroy", "rf_last_error", "rf_device_count", "rf_sync", "rf_version",
     "rf_sha256_batch", "rf_sha256_arena", "rf_sha_plan_create", "rf_sha_plan_run",
     "rf_sha_plan_stats", "rf_sha_plan_destroy", "rf_gen_fill", "rf_fileset_digest_batch",
+    "rf_fileset_digest_device",
     "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
     "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
@@ -141,6 +142,34 @@ class GraphStats(ctypes.Structure):
 _lib = None
 
 
+class FilesetPaths:
+    """Argument arrays of rf_fileset_digest_device, built once: sets is a list
+    of filesets, each a list of groups (a Map is one group), each a list of
+    paths; File ID of entry e = d_ids32[e] (flattened order)."""
+
+    def __init__(self, ctx, sets):
+        self.ctx = ctx
+        set_group, group_entry, paths = [0], [0], []
+        for groups in sets:
+            for g in groups:
+                paths.extend(p.encode() if isinstance(p, str) else p for p in g)
+                group_entry.append(len(paths))
+            set_group.append(len(group_entry) - 1)
+        self.n = len(sets)
+        self.n_entries = len(paths)
+        self.sg = np.array(set_group, dtype=np.uint64)
+        self.ge = np.array(group_entry, dtype=np.uint64)
+        self._pb = [ctypes.create_string_buffer(p, max(len(p), 1)) for p in paths]
+        self.pp = (ctypes.c_void_p * max(len(paths), 1))(*[ctypes.addressof(b) for b in self._pb])
+        self.pl = np.array([len(p) for p in paths] or [0], dtype=np.uint32)
+
+    def digest_device(self, d_ids32) -> list:
+        out = np.zeros(32 * self.n, dtype=np.uint8)
+        _check(lib().rf_fileset_digest_device(self.ctx._h, self.n, _ptr(self.sg), _ptr(self.ge), self.pp,
+                                              _ptr(self.pl), d_ids32, _ptr(out)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(self.n)]
+
+
 def lib():
     """Load libreflow_hip.so.  Raises if it was not built (no fallback)."""
     global _lib
@@ -161,6 +190,7 @@ def lib():
             "rf_sha_plan_stats": ([vp, vp], i32), "rf_sha_plan_destroy": ([vp], None),
             "rf_gen_fill": ([vp, vp, vp, vp, u64, u64, u64, vp], i32),
             "rf_fileset_digest_batch": ([vp, u64, vp, vp, vp, vp, vp, vp], i32),
+            "rf_fileset_digest_device": ([vp, u64, vp, vp, vp, vp, vp, vp], i32),
             "rf_graph_load": ([vp, vp, vp], i32), "rf_graph_destroy": ([vp], None),
             "rf_graph_set_slots": ([vp, vp, vp, u32], i32),
             "rf_graph_set_slots_device": ([vp, vp, vp, u32, vp], i32),
@@ -328,6 +358,11 @@ class Context:
         _check(lib().rf_fileset_digest_batch(self._h, n, _ptr(sg), _ptr(ge), pp, _ptr(pl),
                                              _ptr(idb), _ptr(out)))
         return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+    def fileset_paths(self, sets):
+        """Marshals the paths of `sets` once (groups of paths; entry e = the
+        e-th path in order) for repeated digests with device-resident IDs."""
+        return FilesetPaths(self, sets)
 
     def dedup_digests(self, digests: np.ndarray):
         """Canonicalize's flowMap: (canon[i] = first index with digest i's value, n_unique)."""

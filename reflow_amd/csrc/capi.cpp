@@ -103,7 +103,7 @@ struct rf_ctx {
     int n_cu = 256;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    DevBuf d_arena, d_out, d_tmp, d_tab, d_tab2, d_tab3;
+    DevBuf d_arena, d_out, d_tmp, d_tab, d_tab2, d_tab3, d_place;
     HostBuf h_stage;
     hipEvent_t t0 = nullptr, t1 = nullptr;
 };
@@ -593,27 +593,43 @@ extern "C" int rf_gen_fill(rf_ctx* ctx, void* d_arena, const uint64_t* d_offs,
 
 // ---------------------------------------------------------------------------
 // Fileset digest (executor.go:205-233)
-extern "C" int rf_fileset_digest_batch(rf_ctx* ctx, uint64_t n_sets, const uint64_t* set_group,
-                                       const uint64_t* group_entry, const char* const* paths,
-                                       const uint32_t* path_lens, const uint8_t* ids32,
-                                       uint8_t* out32) {
-    ARG(ctx && set_group && out32, "null argument");
-    if (n_sets == 0) return RF_OK;
+//
+// Material of set s = Σ over its groups, entries sorted bytewise (sort.Strings):
+// path ‖ 0x00 0x05 ‖ id, written straight into the packed host stage (sets at
+// 64-B aligned offsets).  With ids32 == nullptr the ID bytes are left for the
+// device (k_place_ids): *place gets (material byte, entry) per entry.
+static int fileset_material(rf_ctx* ctx, uint64_t n_sets, const uint64_t* set_group, const uint64_t* group_entry,
+                            const char* const* paths, const uint32_t* path_lens, const uint8_t* ids32,
+                            std::vector<uint64_t>& offs, std::vector<uint64_t>& lens, uint64_t& arena_bytes,
+                            std::vector<uint64_t>* place_off, std::vector<uint32_t>* place_entry) {
     const uint64_t n_groups = set_group[n_sets];
     ARG(n_groups == 0 || group_entry, "null group_entry");
     const uint64_t n_entries = n_groups ? group_entry[n_groups] : 0;
-    ARG(n_entries == 0 || (paths && path_lens && ids32), "null entries");
-    std::vector<uint64_t> offs(n_sets), lens(n_sets);
-    std::vector<uint32_t> idx;
-    std::vector<uint8_t> mat;
-    // material of set s = Σ over its groups, entries sorted bytewise:
-    // path ‖ 0x00 0x05 ‖ id
-    std::vector<uint8_t> arena;
+    ARG(n_entries == 0 || (paths && path_lens), "null entries");
+    offs.assign(n_sets, 0);
+    lens.assign(n_sets, 0);
+    uint64_t pos = 0;
     for (uint64_t s = 0; s < n_sets; ++s) {
         ARG(set_group[s] <= set_group[s + 1], "set_group not monotone");
-        offs[s] = arena.size();
+        uint64_t len = 0;
         for (uint64_t gi = set_group[s]; gi < set_group[s + 1]; ++gi) {
             ARG(group_entry[gi] <= group_entry[gi + 1], "group_entry not monotone");
+            for (uint64_t e = group_entry[gi]; e < group_entry[gi + 1]; ++e) {
+                ARG(paths[e] || path_lens[e] == 0, "null path");
+                len += path_lens[e] + 34ull;
+            }
+        }
+        offs[s] = pos;
+        lens[s] = len;
+        pos += (len + 63) & ~63ull;
+    }
+    arena_bytes = pos;
+    HIPC(ctx->h_stage.ensure(pos + 64));
+    uint8_t* out = ctx->h_stage.bytes();
+    std::vector<uint32_t> idx;
+    for (uint64_t s = 0; s < n_sets; ++s) {
+        uint64_t w = offs[s];
+        for (uint64_t gi = set_group[s]; gi < set_group[s + 1]; ++gi) {
             idx.resize(group_entry[gi + 1] - group_entry[gi]);
             std::iota(idx.begin(), idx.end(), (uint32_t)group_entry[gi]);
             std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
@@ -622,16 +638,78 @@ extern "C" int rf_fileset_digest_batch(rf_ctx* ctx, uint64_t n_sets, const uint6
                 return c < 0 || (c == 0 && la < lb);
             });
             for (uint32_t e : idx) {
-                arena.insert(arena.end(), paths[e], paths[e] + path_lens[e]);
-                arena.push_back(0x00);
-                arena.push_back(0x05);
-                arena.insert(arena.end(), ids32 + 32ull * e, ids32 + 32ull * e + 32);
+                if (path_lens[e]) memcpy(out + w, paths[e], path_lens[e]);
+                w += path_lens[e];
+                out[w++] = 0x00;
+                out[w++] = 0x05;
+                if (ids32) {
+                    memcpy(out + w, ids32 + 32ull * e, 32);
+                } else {
+                    place_off->push_back(w);
+                    place_entry->push_back(e);
+                }
+                w += 32;
             }
         }
-        lens[s] = arena.size() - offs[s];
     }
-    if (arena.empty()) arena.push_back(0);
-    return rf_sha256_arena(ctx, arena.data(), offs.data(), lens.data(), n_sets, out32);
+    return RF_OK;
+}
+
+extern "C" int rf_fileset_digest_batch(rf_ctx* ctx, uint64_t n_sets, const uint64_t* set_group,
+                                       const uint64_t* group_entry, const char* const* paths,
+                                       const uint32_t* path_lens, const uint8_t* ids32,
+                                       uint8_t* out32) {
+    ARG(ctx && set_group && out32, "null argument");
+    if (n_sets == 0) return RF_OK;
+    ARG(set_group[n_sets] == 0 || group_entry, "null group_entry");
+    ARG(set_group[n_sets] == 0 || group_entry[set_group[n_sets]] == 0 || ids32, "null ids32");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard g(ctx->device);
+    std::vector<uint64_t> offs, lens;
+    uint64_t arena_bytes = 0;
+    int rc = fileset_material(ctx, n_sets, set_group, group_entry, paths, path_lens, ids32, offs, lens,
+                              arena_bytes, nullptr, nullptr);
+    if (rc) return rc;
+    return sha_host_packed(ctx, offs, lens, arena_bytes, out32);
+}
+
+extern "C" int rf_fileset_digest_device(rf_ctx* ctx, uint64_t n_sets, const uint64_t* set_group,
+                                        const uint64_t* group_entry, const char* const* paths,
+                                        const uint32_t* path_lens, const void* d_ids32, uint8_t* out32) {
+    ARG(ctx && set_group && out32, "null argument");
+    if (n_sets == 0) return RF_OK;
+    ARG(set_group[n_sets] == 0 || group_entry, "null group_entry");
+    ARG(set_group[n_sets] == 0 || group_entry[set_group[n_sets]] == 0 || d_ids32, "null d_ids32");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard g(ctx->device);
+    std::vector<uint64_t> offs, lens, place_off;
+    std::vector<uint32_t> place_entry;
+    uint64_t arena_bytes = 0;
+    int rc = fileset_material(ctx, n_sets, set_group, group_entry, paths, path_lens, nullptr, offs, lens,
+                              arena_bytes, &place_off, &place_entry);
+    if (rc) return rc;
+    const uint64_t n = n_sets, np = place_off.size();
+    HIPC(ctx->d_arena.ensure(arena_bytes + 64));
+    HIPC(ctx->d_out.ensure(32 * n));
+    HIPC(ctx->d_place.ensure(12 * np + 16));
+    HIPC(hipMemcpyAsync(ctx->d_arena.p, ctx->h_stage.p, arena_bytes, hipMemcpyHostToDevice, ctx->stream));
+    uint64_t* d_off = ctx->d_place.as<uint64_t>();
+    uint32_t* d_ent = reinterpret_cast<uint32_t*>(d_off + np);
+    HIPC(hipMemcpyAsync(d_off, place_off.data(), 8 * np, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(hipMemcpyAsync(d_ent, place_entry.data(), 4 * np, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(launch_place_ids(ctx->d_arena.as<uint8_t>(), d_off, d_ent, np, static_cast<const uint8_t*>(d_ids32),
+                          ctx->stream));
+    rf_sha_plan* p = nullptr;
+    rc = plan_create_nolock(ctx, offs.data(), lens.data(), n, 0, &p);
+    if (rc) return rc;
+    rc = plan_run_locked(p, ctx->d_arena.p, ctx->d_out.p, ctx->stream);
+    if (rc == RF_OK) {
+        hipError_t e = hipMemcpyAsync(out32, ctx->d_out.p, 32 * n, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) rc = fail(RF_EDEVICE, "fileset digest: %s", hipGetErrorString(e));
+    }
+    rf_sha_plan_destroy(p);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------

@@ -41,6 +41,8 @@ hipError_t launch_sha_pair(const SoloArgs& a, hipStream_t s);
 // Checks that the gfx950 code object of this library loads on the device.
 hipError_t probe_kernels();
 
+hipError_t launch_place_ids(uint8_t* arena, const uint64_t* mat_off, const uint32_t* entry, uint64_t n,
+                            const uint8_t* ids32, hipStream_t s);
 hipError_t launch_gen_fill(uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n,
                            uint64_t seed, uint64_t arena_bytes, hipStream_t s);
 

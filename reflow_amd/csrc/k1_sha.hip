@@ -582,4 +582,24 @@ hipError_t launch_gen_fill(uint8_t* arena, const uint64_t* offs, const uint64_t*
     return hipGetLastError();
 }
 
+// Fileset digest with device-resident File IDs: entry i's 32 ID bytes go to
+// byte mat_off[i] of the material arena (one thread per byte; the material
+// positions are unaligned: path lengths vary).
+__global__ __launch_bounds__(256) void k_place_ids(uint8_t* __restrict__ arena, const uint64_t* __restrict__ mat_off,
+                                                   const uint32_t* __restrict__ entry, uint64_t n,
+                                                   const uint8_t* __restrict__ ids32) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 32 * n) return;
+    const uint64_t i = t >> 5, b = t & 31;
+    arena[mat_off[i] + b] = ids32[32ull * entry[i] + b];
+}
+
+hipError_t launch_place_ids(uint8_t* arena, const uint64_t* mat_off, const uint32_t* entry, uint64_t n,
+                            const uint8_t* ids32, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t grid = (32 * n + 255) / 256;
+    hipLaunchKernelGGL(k_place_ids, dim3((uint32_t)grid), dim3(256), 0, s, arena, mat_off, entry, n, ids32);
+    return hipGetLastError();
+}
+
 }  // namespace rf

@@ -130,6 +130,33 @@ def test_fileset_random(ctx):
     assert ctx.fileset_digest_batch(sets) == want
 
 
+def test_fileset_device_ids(ctx):
+    """rf_fileset_digest_device (IDs in HBM, placed into the material on the
+    device) == rf_fileset_digest_batch == oracle, incl. empty sets/groups and
+    unaligned path lengths."""
+    rng = random.Random(9)
+    sets, flat_ids, want = [], [], []
+    for k in range(40):
+        groups = []
+        for _ in range(rng.randint(0, 3)):
+            g = [("d%d/%s%d" % (rng.randint(0, 5), "x" * rng.randint(0, 70), j),
+                  bytes(rng.getrandbits(8) for _ in range(32))) for j in range(rng.randint(0, 40))]
+            groups.append(g)
+        sets.append(groups)
+        fs = O.OFileset(list=[O.OFileset(map={p: (d, 0) for p, d in g}) for g in groups])
+        want.append(fs.digest())
+        flat_ids.extend(d for g in groups for _, d in g)
+    host = ctx.fileset_digest_batch(sets)
+    fp = ctx.fileset_paths([[[p for p, _ in g] for g in groups] for groups in sets])
+    d_ids = ctx.upload(np.frombuffer(b"".join(flat_ids) or b"\0" * 32, dtype=np.uint8).copy())
+    try:
+        dev = fp.digest_device(d_ids.ptr)
+    finally:
+        d_ids.free()
+    assert host == want
+    assert dev == want
+
+
 # ---------------------------------------------------------- digest DAG --
 def _load(ctx, low):
     from reflow_amd import capi
