@@ -122,6 +122,7 @@ void rf_sha_plan_destroy(rf_sha_plan *plan);
 #define RF_SHA_ALL_SOLO 2u     /* every message wave-per-message */
 #define RF_SHA_ONE_LANE_CHAIN 4u /* wave-per-message kernel keeps the round chain on one lane */
 #define RF_SHA_NO_PAIR 8u      /* small sets: lanes kernel instead of the producer/chain pair */
+#define RF_SHA_NO_OCTO 16u     /* small sets: no eight-per-wave two-lane chains (pair or lanes) */
 
 /* Synthetic data generator (bench / tests): fills d_arena so that message i
  * is the splitmix64 counter stream with seed (seed ^ i). */

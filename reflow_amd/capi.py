@@ -19,6 +19,7 @@ RF_SHA_NO_SOLO = 1
 RF_SHA_ALL_SOLO = 2
 RF_SHA_ONE_LANE_CHAIN = 4
 RF_SHA_NO_PAIR = 8
+RF_SHA_NO_OCTO = 16
 
 # Every symbol include/reflow_hip.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = [

@@ -326,6 +326,7 @@ struct rf_sha_plan {
     uint32_t n_lanes = 0, n_solo = 0, grid = 0, n_shards = 1;
     bool duo = true;  // wave-per-message kernel: two-lane chain (default) or one-lane
     bool pair = false;  // lane messages on k1_sha256_pair (latency-bound small sets)
+    bool octo = false;  // ... or on k1_sha256_octo (eight per wave, two-lane chain)
     DevBuf d_offs, d_lens, d_order, d_heads;  // d_order = [lanes order | solo order]
     hipStream_t side = nullptr;
     hipEvent_t e0 = nullptr, e_solo = nullptr, e_lanes = nullptr, e1 = nullptr;
@@ -342,6 +343,8 @@ struct rf_sha_plan {
 //                        same 19M-block message run to run beside the duo
 //                        chains of configs[1]: modelled at the lanes rate,
 //                        so a lane message never sets the makespan
+//   octo chain           1.3 us/block (eight messages per wave; sets of <= 4
+//                        messages per SIMD, so the chain waves do not share)
 //   lanes, latency-bound 3.2 us/block; throughput 64 B x 35 T lane-ops/s / 1464
 // M(k) = max(duo: nb[0] x 1.13 us if k > 0,
 //            lane set: max(nb[k] x t_lane(n - k), sum_{i >= k} nb[i] x 1464 / 35e12)).
@@ -356,11 +359,13 @@ static void plan_split(const std::vector<uint64_t>& nb, std::vector<uint32_t>& o
     if (flags & RF_SHA_ALL_SOLO) {
         n_solo = (uint32_t)n;
     } else if (!(flags & RF_SHA_NO_SOLO)) {
-        const double t_duo = 1.13e-6, t_pair = 3.2e-6, t_lanes = 3.2e-6, blk_rate = 35e12 / 1464.0;
+        const double t_duo = 1.13e-6, t_octo = 1.3e-6, t_pair = 3.2e-6, t_lanes = 3.2e-6,
+                     blk_rate = 35e12 / 1464.0;
         const uint64_t n_simd = 4ull * n_cu, cap = std::min<uint64_t>(n, n_simd);
         double rest = 0;
         for (uint64_t i = 0; i < n; ++i) rest += (double)nb[i];
         const bool pair_ok = !(flags & RF_SHA_NO_PAIR);
+        const bool octo_ok = !(flags & RF_SHA_NO_OCTO);
         double best = 1e300;
         uint64_t best_k = 0;
         for (uint64_t k = 0; k <= cap; ++k) {
@@ -368,7 +373,9 @@ static void plan_split(const std::vector<uint64_t>& nb, std::vector<uint32_t>& o
             const uint64_t lanes = n - k;
             double m = k ? (double)nb[order[0]] * t_duo : 0.0;
             if (lanes) {
-                const double tl = (pair_ok && lanes <= 16 * n_simd) ? t_pair : t_lanes;
+                const double tl = (octo_ok && lanes <= 4 * n_simd)   ? t_octo
+                                  : (pair_ok && lanes <= 16 * n_simd) ? t_pair
+                                                                      : t_lanes;
                 m = std::max(m, std::max((double)nb[order[k]] * tl, rest / blk_rate));
             }
             if (m < best * 0.98) {
@@ -421,6 +428,9 @@ static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t*
     // are latency-bound on their wave's issue rate: split schedule and rounds
     // over two waves (k1_sha256_pair).
     p->pair = !(flags & RF_SHA_NO_PAIR) && p->n_lanes > 0 && p->n_lanes <= 16ull * 4 * ctx->n_cu;
+    // Up to 4 lane messages per SIMD: eight per wave on the two-lane chain
+    // (k1_sha256_octo), 8 instead of 14 chain instructions per round.
+    p->octo = !(flags & RF_SHA_NO_OCTO) && p->n_lanes > 0 && p->n_lanes <= 4ull * 4 * ctx->n_cu;
     hipError_t e = hipSuccess;
     if ((e = p->d_offs.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
         (e = p->d_lens.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
@@ -467,7 +477,11 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
         HIPC(launch_sha_solo(sa, p->duo, p->side));
         HIPC(hipEventRecord(p->e_solo, p->side));
     }
-    if (p->n_lanes && p->pair) {
+    if (p->n_lanes && p->octo) {
+        SoloArgs oa{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(), p->d_lens.as<uint64_t>(),
+                    order, p->n_lanes, static_cast<uint8_t*>(d_out)};
+        HIPC(launch_sha_octo(oa, s));
+    } else if (p->n_lanes && p->pair) {
         SoloArgs pa{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(), p->d_lens.as<uint64_t>(),
                     order, p->n_lanes, static_cast<uint8_t*>(d_out)};
         HIPC(launch_sha_pair(pa, s));

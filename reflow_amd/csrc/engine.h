@@ -37,6 +37,8 @@ struct SoloArgs {
 hipError_t launch_sha_solo(const SoloArgs& a, bool duo, hipStream_t s);
 // Lane per message with a producer wave beside the chain wave (small sets).
 hipError_t launch_sha_pair(const SoloArgs& a, hipStream_t s);
+// Eight messages per wave on the duo's two-lane chain (small sets).
+hipError_t launch_sha_octo(const SoloArgs& a, hipStream_t s);
 
 // Checks that the gfx950 code object of this library loads on the device.
 hipError_t probe_kernels();

@@ -261,15 +261,17 @@ __global__ __launch_bounds__(64) void k1_sha256_solo(SoloArgs a) {
 // the old X3's register), so after four steps the mapping is back in place;
 // one asm block runs four steps and the compiler's pad after an asm block is
 // paid once per four rounds.
-#define RF_LAG_STEP(x0, x1, x2, x3, z, zn, k)                                              \
-    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[sq]\n\t"                                 \
-    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[" k "]\n\t"                                    \
-    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                        \
-    "v_xor_b32_dpp %[t1], %[t0], %[t0] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"  \
-    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                       \
-    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t" \
-    "v_xor_b32_dpp %[t1], %[t0], %[t1] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"  \
+#define RF_LAG_STEP_P(x0, x1, x2, x3, z, zn, k, P1, P2, PART)                              \
+    "v_alignbit_b32 %[t0], %[" x0 "], %[" x0 "], %[sq]\n\t"                                  \
+    "v_xad_u32 %[" zn "], %[" x2 "], %[m], %[" k "]\n\t"                                     \
+    "v_bitop3_b32 %[t3], %[" x0 "], %[" x2 "], %[m] bitop3:0x78\n\t"                         \
+    "v_xor_b32_dpp %[t1], %[t0], %[t0] " P1 " row_mask:0xf bank_mask:0xf\n\t"                \
+    "v_bitop3_b32 %[t3], %[t3], %[" x1 "], %[" x2 "] bitop3:0xca\n\t"                        \
+    "v_add_u32_dpp %[" zn "], %[" x0 "], %[" zn "] " PART " row_mask:0xf bank_mask:0xf\n\t"  \
+    "v_xor_b32_dpp %[t1], %[t0], %[t1] " P2 " row_mask:0xf bank_mask:0xf\n\t"                \
     "v_add3_u32 %[" x3 "], %[" z "], %[t1], %[t3]\n\t"
+#define RF_LAG_STEP(x0, x1, x2, x3, z, zn, k) \
+    RF_LAG_STEP_P(x0, x1, x2, x3, z, zn, k, "quad_perm:[1,2,0,3]", "quad_perm:[2,0,1,3]", "row_ror:8")
 
 #define RF_LAG_GROUP                                        \
     RF_LAG_STEP("a", "b", "c", "d", "z", "y", "k1")         \
@@ -316,14 +318,15 @@ constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
 // (v_subrev_u32_dpp does not permute the operand one would expect; the
 // negation goes through a temporary and a plain DPP move, t0 being free after
 // the group's last step.)
-#define RF_LAG_CORR                                                                          \
-    "v_sub_u32 %[t0], %[zero], %[h0]\n\t"                                                    \
-    "v_add_u32_dpp %[c63], %[h3], %[h3] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"            \
-    "v_mov_b32_dpp %[c63], %[one] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n\t"        \
-    "v_mov_b32_dpp %[c64], %[h2] row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                   \
-    "v_mov_b32_dpp %[c64], %[t0] row_ror:8 row_mask:0xf bank_mask:0xc\n\t"                   \
-    "v_mov_b32_dpp %[c65], %[h1] row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                   \
-    "v_sub_u32_dpp %[c65], %[zero], %[h3] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n\t"
+#define RF_LAG_CORR_P(PART, BE, BA)                                                            \
+    "v_sub_u32 %[t0], %[zero], %[h0]\n\t"                                                      \
+    "v_add_u32_dpp %[c63], %[h3], %[h3] " PART " row_mask:0xf bank_mask:0xf\n\t"               \
+    "v_mov_b32_dpp %[c63], %[one] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" BA "\n\t"       \
+    "v_mov_b32_dpp %[c64], %[h2] " PART " row_mask:0xf bank_mask:" BE "\n\t"                   \
+    "v_mov_b32_dpp %[c64], %[t0] " PART " row_mask:0xf bank_mask:" BA "\n\t"                   \
+    "v_mov_b32_dpp %[c65], %[h1] " PART " row_mask:0xf bank_mask:" BE "\n\t"                   \
+    "v_sub_u32_dpp %[c65], %[zero], %[h3] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" BA "\n\t"
+#define RF_LAG_CORR RF_LAG_CORR_P("row_ror:8", "0x3", "0xc")
 
 // Two waves: wave 0 runs the chain, wave 1 expands the next 64 blocks'
 // K+W rows into the other half of a double buffer meanwhile (one barrier per
@@ -434,6 +437,160 @@ __global__ __launch_bounds__(128) void k1_sha256_duo(SoloArgs a) {
             uint4 o;
             o.x = bswap32(Hr0); o.y = bswap32(Hr1); o.z = bswap32(Hr2); o.w = bswap32(Hr3);
             reinterpret_cast<uint4*>(a.out + 32ull * id)[lane == 0 ? 1 : 0] = o;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Octo: the duo's two-lane lagged chain for eight messages per wave (sets that
+// leave the chip mostly idle, e.g. configs[0]'s 4096 files: 512 chain waves at
+// 8 instructions per round instead of 64-message pair waves at 14).  Lanes
+// 8f..8f+7 run message f: 8f..8f+3 the e-half, 8f+4..8f+7 the a-half.  Every
+// lane of a quad ends a round with the full Σ (positions 0..2 rotate by the
+// half's three amounts, position 3 repeats position 0's; quad_perm [1,2,0,1]
+// then [2,0,1,2] xor them together), so the partner's X0 can come from the
+// mirrored lane of the half-row (row_half_mirror: i <-> 7-i) and the halves'
+// feed-forwards select banks 0x5 (e) / 0xa (a).
+// The producer wave expands the K+W rows one lane per (message, block), in
+// chunks of eight blocks per message, double-buffered; rows are block-major
+// (message f's row of block j at (buf*8 + j)*8 + f) so the eight rows one
+// ds_read_b128 reads sit 68 words apart, in disjoint banks.
+// A message's digest is its chaining value after the group 0 of block nb --
+// the block after its last, where both halves have applied the final
+// feed-forward; the wave runs that group 0 for its longest message after the
+// loop.  Shorter messages of the wave keep hashing rows nobody wrote (their
+// lanes' results are never stored again).
+#define RF_OCT_STEP(x0, x1, x2, x3, z, zn, k) \
+    RF_LAG_STEP_P(x0, x1, x2, x3, z, zn, k, "quad_perm:[1,2,0,1]", "quad_perm:[2,0,1,2]", "row_half_mirror")
+#define RF_OCT_GROUP                                        \
+    RF_OCT_STEP("a", "b", "c", "d", "z", "y", "k1")         \
+    RF_OCT_STEP("d", "a", "b", "c", "y", "z", "k2")         \
+    RF_OCT_STEP("c", "d", "a", "b", "z", "y", "k3")         \
+    RF_OCT_STEP("b", "c", "d", "a", "y", "z", "k4")
+#define RF_OCT_GROUP0                                        \
+    "s_nop 1\n\t" RF_LAG_FF("0x5", "a", "b", "c", "d")       \
+    "v_add_u32 %[z], %[z], %[kw0]\n\t"                       \
+    RF_OCT_STEP("a", "b", "c", "d", "z", "y", "k1")          \
+    RF_OCT_STEP("d", "a", "b", "c", "y", "z", "k2")          \
+    RF_LAG_FF("0xa", "c", "d", "a", "b")                     \
+    RF_OCT_STEP("c", "d", "a", "b", "z", "y", "k3")          \
+    RF_OCT_STEP("b", "c", "d", "a", "y", "z", "k4")          \
+    RF_LAG_CORR_P("row_half_mirror", "0x5", "0xa")
+
+// Producer lane l: block c + (l & 7) of message l >> 3 into its row of buffer kwb.
+__device__ __forceinline__ void fill_oct_row(uint32_t* kwb, const uint8_t* p, uint64_t len, uint64_t nb,
+                                             uint64_t c, uint32_t lane) {
+    const uint32_t jj = lane & 7;
+    const uint64_t b = c + jj;
+    if (b >= nb) return;
+    uint32_t w[16];
+    load_block(w, p, len, b);
+    kw_expand_store(w, reinterpret_cast<uint4*>(&kwb[(jj * 8 + (lane >> 3)) * kRow]));
+}
+
+constexpr uint32_t kOctChunk = 8;
+
+__global__ __launch_bounds__(128) void k1_sha256_octo(SoloArgs a) {
+    // two buffers of 8 blocks x 8 messages, then the a-lanes' k row
+    __shared__ __attribute__((aligned(16))) uint32_t kw[129 * kRow];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t* const ones = &kw[128 * kRow];
+    if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        ones[lane] = lane ? 1u : 0u;
+        if (lane < 4) ones[64 + lane] = 1u;
+    }
+    const uint32_t f = lane >> 3;
+    const bool elane = (lane & 4) == 0;
+    const uint32_t q3 = lane & 3;
+    const uint32_t shq = elane ? (q3 == 1 ? 11u : q3 == 2 ? 25u : 6u) : (q3 == 1 ? 13u : q3 == 2 ? 22u : 2u);
+    const uint32_t M = elane ? 0u : ~0u;
+    const uint32_t one = 1u, zero = 0u;
+    const uint32_t n_groups = (a.n_order + 7) / 8;
+    for (uint32_t q = blockIdx.x; q < n_groups; q += gridDim.x) {
+        const uint32_t qi = 8 * q + f;
+        const bool has = qi < a.n_order;
+        const uint32_t id = has ? a.order[qi] : 0u;
+        const uint64_t len = has ? a.lens[id] : 0;
+        const uint8_t* p = a.arena + (has ? a.offs[id] : 0);
+        const uint64_t nb = has ? sha256_nblocks(len) : 0;
+        uint64_t maxnb = nb;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t x = __shfl_xor(maxnb, o, 64);
+            maxnb = x > maxnb ? x : maxnb;
+        }
+        uint32_t Hr0 = elane ? lag::IV[4] : lag::IV[0], Hr1 = elane ? lag::IV[5] : lag::IV[1];
+        uint32_t Hr2 = elane ? lag::IV[6] : lag::IV[2], Hr3 = elane ? lag::IV[7] : lag::IV[3];
+        uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
+        uint32_t Z = elane ? lag::IV[7] + lag::IV[3] : 0u, Y = 0;
+        uint32_t c63 = 0;
+        uint32_t c64 = elane ? lag::IV[2] : 0u - lag::IV[4];
+        uint32_t c65 = elane ? lag::IV[1] : 0u - lag::IV[3];
+        uint32_t t0, t1, t3;
+        uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+        uint4 v = make_uint4(0, 0, 0, 0), vn = v;
+        if (wave == 1) fill_oct_row(kw, p, len, nb, 0, lane);
+        __syncthreads();
+        uint32_t buf = 0;
+        for (uint64_t c = 0; c < maxnb; c += kOctChunk, buf ^= 1) {
+            if (wave == 1) {
+                if (c + kOctChunk < maxnb) fill_oct_row(&kw[(buf ^ 1) * 64 * kRow], p, len, nb, c + kOctChunk, lane);
+            } else {
+                const uint32_t cnt = (uint32_t)((maxnb - c) < kOctChunk ? (maxnb - c) : kOctChunk);
+                // e-lanes read their message's rows, a-lanes the ones row
+                const uint32_t ones_off = 128 * kRow * 4, buf_off = (buf * 64 + f) * kRow * 4;
+                const uint4* r4 = reinterpret_cast<const uint4*>(
+                    reinterpret_cast<const char*>(kw) + ((M & ones_off) | (~M & buf_off)));
+                v = r4[0];
+                vn = r4[1];
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    const uint32_t nrow_off = buf_off + (j + 1 < cnt ? j + 1 : j) * 8 * kRow * 4;
+                    const uint4* r4n = reinterpret_cast<const uint4*>(
+                        reinterpret_cast<const char*>(kw) + ((M & ones_off) | (~M & nrow_off)));
+                    uint4 vnn = r4[2];
+                    {
+                        const uint32_t k1 = v.y + c64, k2 = v.z + c65;
+                        asm volatile(RF_OCT_GROUP0
+                                     : RF_LAG_STATE, RF_LAG_TMP, RF_LAG_H,
+                                       [c63] "=&v"(c63), [c64] "+v"(c64), [c65] "+v"(c65)
+                                     : RF_LAG_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one),
+                                       [zero] "v"(zero));
+                    }
+                    if (c + j == nb) {  // message done: its final chaining value
+                        D0 = Hr0; D1 = Hr1; D2 = Hr2; D3 = Hr3;
+                    }
+                    v = vn;
+                    vn = vnn;
+#pragma unroll
+                    for (int g = 1; g < 16; ++g) {
+                        vnn = g < 14 ? r4[g + 2] : r4n[g - 14];
+                        const uint32_t k4 = g == 15 ? c63 : vn.x;
+                        asm volatile(RF_OCT_GROUP : RF_LAG_STATE, RF_LAG_TMP : RF_LAG_IN(v.y, v.z, v.w, k4));
+                        v = vn;
+                        vn = vnn;
+                    }
+                    r4 = r4n;
+                }
+            }
+            __syncthreads();
+        }
+        if (wave == 1) continue;
+        {
+            const uint32_t k1 = v.y + c64, k2 = v.z + c65;
+            asm volatile(RF_OCT_GROUP0
+                         : RF_LAG_STATE, RF_LAG_TMP, RF_LAG_H,
+                           [c63] "=&v"(c63), [c64] "+v"(c64), [c65] "+v"(c65)
+                         : RF_LAG_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one), [zero] "v"(zero));
+        }
+        if (nb == maxnb) {
+            D0 = Hr0; D1 = Hr1; D2 = Hr2; D3 = Hr3;
+        }
+        // lane 8f (e) holds H4..H7, lane 8f+4 (a) H0..H3
+        if (has && (lane & 3) == 0) {
+            uint4 o;
+            o.x = bswap32(D0); o.y = bswap32(D1); o.z = bswap32(D2); o.w = bswap32(D3);
+            reinterpret_cast<uint4*>(a.out + 32ull * id)[elane ? 1 : 0] = o;
         }
     }
 }
@@ -568,6 +725,18 @@ hipError_t launch_sha_pair(const SoloArgs& a, hipStream_t s) {
     // per block, and the planner's makespan model counts on 1.9).
     static const size_t reserve = 126 * 1024 - sizeof(uint32_t) * 2 * 64 * kPairRow;
     hipLaunchKernelGGL(k1_sha256_pair, dim3(grid), dim3(128), reserve, s, a, 1u, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_sha_octo(const SoloArgs& a, hipStream_t s) {
+    if (a.n_order == 0) return hipSuccess;
+    uint32_t grid = (a.n_order + 7) / 8;
+    if (grid > 8192) grid = 8192;
+    static const size_t reserve = [] {
+        const char* v = getenv("RF_OCTO_LDS_KB");
+        return v ? (size_t)atoi(v) * 1024 : (size_t)0;
+    }();
+    hipLaunchKernelGGL(k1_sha256_octo, dim3(grid), dim3(128), reserve, s, a);
     return hipGetLastError();
 }
 

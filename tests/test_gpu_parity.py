@@ -68,12 +68,13 @@ def _device_arena(lens, align=256):
     return np.array(offs, dtype=np.uint64), max(pos, 16)
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 6, 8, 9])
+@pytest.mark.parametrize("flags", [0, 1, 2, 6, 16, 17, 24, 25])
 def test_plan_gen_fill_device(ctx, flags):
-    """rf_gen_fill + rf_sha_plan_run on HBM-resident data (the bench path),
-    planner mix / lane messages only (producer/chain pair for this small set) /
-    wave-per-message with the two-lane chain / with the one-lane chain / the
-    lanes kernel instead of the pair (8), lanes kernel only (9)."""
+    """rf_gen_fill + rf_sha_plan_run on HBM-resident data (the bench path):
+    planner mix (lane set on eight-per-wave octo chains for this small set) /
+    lane messages only (octo: groups of eight with lengths 0 .. 2 MB) /
+    wave-per-message with the two-lane chain (2) / with the one-lane chain (6) /
+    the producer/chain pair instead of octo (16, 17) / the lanes kernel (24, 25)."""
     from reflow_amd import capi
     rng = random.Random(10 + flags)
     lens = [rng.choice([0, 1, 55, 56, 64, 4096, rng.randint(1, 300000), rng.randint(1, 3000)])

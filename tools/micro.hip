@@ -337,6 +337,16 @@ __global__ __launch_bounds__(64) void k_lat(uint32_t iters, uint32_t* out, uint6
             if constexpr (OP == 38)
                 if (j == 0) asm volatile(I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3) I8(VS_MIX3)
                                          : R8, S8 : [c] "v"(c), [e] "v"(s1), [sc] "s"(sc) : "scc");
+            // EXEC-masked copies of cost v_add vop2 / cost alignbit imm: does a
+            // wave with only lanes 0..15 (or lane 0) active issue faster?
+            if constexpr (OP == 39 || OP == 40 || OP == 41 || OP == 42) {
+                if (j == 0 && threadIdx.x < ((OP == 39 || OP == 41) ? 16u : 1u)) {
+                    if constexpr (OP == 39 || OP == 40)
+                        asm volatile(I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) I8(ICOST28) : R8 : [c] "v"(c), [e] "v"(s1));
+                    else
+                        asm volatile(I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) I8(ICOST24) : R8 : [c] "v"(c), [e] "v"(s1));
+                }
+            }
             if (OP == 10 && (j & 3) == 0)
                 asm volatile(LAG2("a", "b", "c", "d", "z", "y") LAG2("d", "a", "b", "c", "y", "z")
                              LAG2("c", "d", "a", "b", "z", "y") LAG2("b", "c", "d", "a", "y", "z")
@@ -354,7 +364,7 @@ struct LtArgs { int op; uint32_t iters; uint32_t* out; uint64_t* cyc; };
 static void run_lat(void* p) {
     auto* a = (LtArgs*)p;
 #define RF_LAT(N) case N: hipLaunchKernelGGL(k_lat<N>, dim3(1), dim3(64), 0, 0, a->iters, a->out, a->cyc); break;
-    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) RF_LAT(10) RF_LAT(11) RF_LAT(12) RF_LAT(13) RF_LAT(14) RF_LAT(15) RF_LAT(16) RF_LAT(17) RF_LAT(18) RF_LAT(19) RF_LAT(20) RF_LAT(21) RF_LAT(22) RF_LAT(23) RF_LAT(24) RF_LAT(25) RF_LAT(26) RF_LAT(27) RF_LAT(28) RF_LAT(29) RF_LAT(30) RF_LAT(31) RF_LAT(32) RF_LAT(33) RF_LAT(34) RF_LAT(35) RF_LAT(36) RF_LAT(37) default: RF_LAT(38) }
+    switch (a->op) { RF_LAT(0) RF_LAT(1) RF_LAT(2) RF_LAT(3) RF_LAT(4) RF_LAT(5) RF_LAT(6) RF_LAT(7) RF_LAT(8) RF_LAT(9) RF_LAT(10) RF_LAT(11) RF_LAT(12) RF_LAT(13) RF_LAT(14) RF_LAT(15) RF_LAT(16) RF_LAT(17) RF_LAT(18) RF_LAT(19) RF_LAT(20) RF_LAT(21) RF_LAT(22) RF_LAT(23) RF_LAT(24) RF_LAT(25) RF_LAT(26) RF_LAT(27) RF_LAT(28) RF_LAT(29) RF_LAT(30) RF_LAT(31) RF_LAT(32) RF_LAT(33) RF_LAT(34) RF_LAT(35) RF_LAT(36) RF_LAT(37) RF_LAT(38) RF_LAT(39) RF_LAT(40) RF_LAT(41) default: RF_LAT(42) }
 #undef RF_LAT
 }
 

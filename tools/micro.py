@@ -57,12 +57,13 @@ def main():
                  "lag2 order V1", "lag2 order V5", "lag2 order V6", "lag2 order V7", "lag2 order V8",
                  "cost alignbit vshift", "cost alignbit imm", "cost bitop3 3v", "cost add3 3v", "cost xad 3v",
                  "cost v_add vop2", "cost add_dpp", "cost v_xor vop2", "cost v_add e64", "cost lshl_add", "cost v_add same-reg", "cost bitop3 2reg", "cost v_mov",
-                 "cost s_add x64", "64 v_add + 64 s_add interleaved", "64 bitop3 + 64 s_add interleaved"]
+                 "cost s_add x64", "64 v_add + 64 s_add interleaved", "64 bitop3 + 64 s_add interleaved",
+                 "cost v_add exec16", "cost v_add exec1", "cost alignbit exec16", "cost alignbit exec1"]
     for op, name in enumerate(lat_names):
         iters = 1 << 17
         cyc = ctypes.c_uint64(0)
         ms = L.micro_lat(op, iters, ctypes.byref(cyc))
-        n = iters * 8 * (9 if op == 10 or 18 <= op <= 22 else 10 if op in (8, 9) else 16 if op >= 37 else 8 if op >= 23 else 1)
+        n = iters * 8 * (9 if op == 10 or 18 <= op <= 22 else 10 if op in (8, 9) else 8 if op >= 39 else 16 if op >= 37 else 8 if op >= 23 else 1)
         print("lat %-22s 1 wave  %.3f ms  %.2f ns/instr  memtime %.2f ticks/instr  %s"
               % (name, ms, ms * 1e6 / n, cyc.value / n, "(%.1f ns/round)" % (ms * 1e6 / (iters * 8)) if op >= 8 else ""),
               flush=True)
