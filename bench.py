@@ -276,8 +276,8 @@ def bench_c1(args, dist, ctx):
             "fixture_match": ok,
             "dag_nodes": small.n_nodes, "dag_full_recompute_ms": dag_ms,
             "total_ms": ids_ms + fs_ms + dag_ms,
-            "note": "4096 messages fill 64 waves: the per-file chain (4097 blocks, lane mode) bounds the "
-                    "file-ID time, not chip throughput"}
+            "note": "4096 messages on 512 k1_sha256_octo chain waves (eight files per wave): the per-file "
+                    "chain (4097 blocks x ~1.2 us) bounds the file-ID time, not chip throughput"}
 
 
 # ------------------------------------------------------- C3: incremental --

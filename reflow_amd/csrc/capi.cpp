@@ -106,6 +106,7 @@ struct rf_ctx {
     DevBuf d_arena, d_out, d_tmp, d_tab, d_tab2, d_tab3, d_place;
     HostBuf h_stage;
     hipEvent_t t0 = nullptr, t1 = nullptr;
+    rf_sha_plan* tplan = nullptr;  // one-shot batches (transient_plan)
 };
 
 struct DevGuard {
@@ -160,7 +161,12 @@ extern "C" void rf_destroy(rf_ctx* ctx) {
     ctx->d_arena.release();
     ctx->d_out.release();
     ctx->d_tmp.release();
+    ctx->d_tab.release();
+    ctx->d_tab2.release();
+    ctx->d_tab3.release();
+    ctx->d_place.release();
     ctx->h_stage.release();
+    rf_sha_plan_destroy(ctx->tplan);
     if (ctx->t0) (void)hipEventDestroy(ctx->t0);
     if (ctx->t1) (void)hipEventDestroy(ctx->t1);
     (void)hipStreamDestroy(ctx->stream);
@@ -394,13 +400,14 @@ static void plan_split(const std::vector<uint64_t>& nb, std::vector<uint32_t>& o
     *n_solo_out = n_solo;
 }
 
-static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens, uint64_t n,
-                              uint32_t flags, rf_sha_plan** out) {
-    ARG(ctx && out, "null argument");
+extern "C" void rf_sha_plan_destroy(rf_sha_plan* p);
+
+// Fills plan p for (offs, lens): host-side split, device copies of the
+// offsets/lengths/order (buffers only grow), stream and events created once.
+static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const uint64_t* lens, uint64_t n,
+                      uint32_t flags) {
     ARG(n == 0 || (offs && lens), "null offs/lens");
     ARG(n < 0xffffffffull, "too many messages");
-    *out = nullptr;
-    DevGuard g(ctx->device);
     std::vector<uint64_t> nb(n);
     uint64_t total_blocks = 0, max_blocks = 0, total_bytes = 0;
     for (uint64_t i = 0; i < n; ++i) {
@@ -410,9 +417,10 @@ static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t*
         max_blocks = std::max(max_blocks, nb[i]);
         total_bytes += lens[i];
     }
-    auto* p = new rf_sha_plan();
     p->ctx = ctx;
     p->n = n;
+    p->ran = false;
+    p->st = rf_sha_stats{};
     std::vector<uint32_t> order;
     uint32_t n_solo = 0;
     plan_split(nb, order, (uint32_t)ctx->n_cu, flags, &n_solo);
@@ -435,27 +443,47 @@ static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t*
     if ((e = p->d_offs.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
         (e = p->d_lens.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
         (e = p->d_order.ensure(4 * std::max<uint64_t>(n, 1))) != hipSuccess ||
-        (e = p->d_heads.ensure(4 * 64)) != hipSuccess) {
-        delete p;
+        (e = p->d_heads.ensure(4 * 64)) != hipSuccess)
         return fail(RF_ENOMEM, "plan alloc: %s", hipGetErrorString(e));
-    }
     if (n) {
         HIPC(hipMemcpy(p->d_offs.p, offs, 8 * n, hipMemcpyHostToDevice));
         HIPC(hipMemcpy(p->d_lens.p, lens, 8 * n, hipMemcpyHostToDevice));
         HIPC(hipMemcpy(p->d_order.p, order.data(), 4 * n, hipMemcpyHostToDevice));
     }
-    HIPC(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
-    HIPC(hipEventCreate(&p->e0));
-    HIPC(hipEventCreate(&p->e_solo));
-    HIPC(hipEventCreate(&p->e_lanes));
-    HIPC(hipEventCreate(&p->e1));
+    if (!p->side) HIPC(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+    for (hipEvent_t* ev : {&p->e0, &p->e_solo, &p->e_lanes, &p->e1})
+        if (!*ev) HIPC(hipEventCreate(ev));
     p->st.n_msgs = n;
     p->st.n_solo = n_solo;
     p->st.total_blocks = total_blocks;
     p->st.max_blocks = max_blocks;
     p->st.total_bytes = total_bytes;
+    return RF_OK;
+}
+
+static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens, uint64_t n,
+                              uint32_t flags, rf_sha_plan** out) {
+    ARG(ctx && out, "null argument");
+    *out = nullptr;
+    DevGuard g(ctx->device);
+    auto* p = new rf_sha_plan();
+    const int rc = plan_setup(ctx, p, offs, lens, n, flags);
+    if (rc) {
+        rf_sha_plan_destroy(p);
+        return rc;
+    }
     *out = p;
     return RF_OK;
+}
+
+// The context's own plan for one-shot batches (rf_sha256_batch/arena, the
+// Fileset digests): its stream, events and device buffers are created once
+// (a fresh plan costs ~4 ms of stream/event/allocation setup per call).
+static int transient_plan(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens, uint64_t n,
+                          rf_sha_plan** out) {
+    if (!ctx->tplan) ctx->tplan = new rf_sha_plan();
+    *out = ctx->tplan;
+    return plan_setup(ctx, ctx->tplan, offs, lens, n, 0);
 }
 
 extern "C" int rf_sha_plan_create(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens,
@@ -554,7 +582,7 @@ static int sha_host_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
     HIPC(hipMemcpyAsync(ctx->d_arena.p, ctx->h_stage.p, arena_bytes, hipMemcpyHostToDevice,
                         ctx->stream));
     rf_sha_plan* p = nullptr;
-    int rc = plan_create_nolock(ctx, offs.data(), lens.data(), n, 0, &p);
+    int rc = transient_plan(ctx, offs.data(), lens.data(), n, &p);
     if (rc) return rc;
     rc = plan_run_locked(p, ctx->d_arena.p, ctx->d_out.p, ctx->stream);
     if (rc == RF_OK) {
@@ -562,7 +590,6 @@ static int sha_host_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
         if (e != hipSuccess) rc = fail(RF_EDEVICE, "sha256 batch: %s", hipGetErrorString(e));
     }
-    rf_sha_plan_destroy(p);
     return rc;
 }
 
@@ -714,7 +741,7 @@ extern "C" int rf_fileset_digest_device(rf_ctx* ctx, uint64_t n_sets, const uint
     HIPC(launch_place_ids(ctx->d_arena.as<uint8_t>(), d_off, d_ent, np, static_cast<const uint8_t*>(d_ids32),
                           ctx->stream));
     rf_sha_plan* p = nullptr;
-    rc = plan_create_nolock(ctx, offs.data(), lens.data(), n, 0, &p);
+    rc = transient_plan(ctx, offs.data(), lens.data(), n, &p);
     if (rc) return rc;
     rc = plan_run_locked(p, ctx->d_arena.p, ctx->d_out.p, ctx->stream);
     if (rc == RF_OK) {
@@ -722,7 +749,6 @@ extern "C" int rf_fileset_digest_device(rf_ctx* ctx, uint64_t n_sets, const uint
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
         if (e != hipSuccess) rc = fail(RF_EDEVICE, "fileset digest: %s", hipGetErrorString(e));
     }
-    rf_sha_plan_destroy(p);
     return rc;
 }
 
