@@ -67,7 +67,9 @@ def pmc_traffic(kernel):
     v = d.get("rf::" + kernel)
     if not v:
         return None, None
-    return v["traffic_bytes_per_launch"], os.path.relpath(paths[-1], ROOT)
+    # the bench prices the kernel's largest launch (the mean over dispatches
+    # would mix in small launches of other workloads)
+    return v.get("traffic_bytes_largest_launch", v["traffic_bytes_per_launch"]), os.path.relpath(paths[-1], ROOT)
 
 
 class Dist:
@@ -79,7 +81,17 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            # gloo prints "[Gloo] Rank r is connected ..." on the C-level
+            # stdout: keep stdout for the one JSON line (send it to stderr)
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                dist.barrier()
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
         if n_gpus != self.world and self.world > 1:
             log("warning: --gpus %d but WORLD_SIZE %d" % (n_gpus, self.world))
@@ -110,6 +122,15 @@ class Dist:
         obj = [b]
         self.dist.broadcast_object_list(obj, src=0)
         return obj[0]
+
+    def all_gather_bytes(self, arr):
+        """Host all-gather over gloo (the exchange when no RCCL communicator
+        could be created)."""
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy())
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return np.concatenate([o.numpy() for o in out])
 
 
 def timed_steps(dist, ctx, fn, steps, warmup):
@@ -316,9 +337,13 @@ def bench_dag(args, dist, ctx, comm):
         state["v"] ^= 1
         g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
         g.recompute_async(False, ctx.stream)
-        if comm is not None:  # boundary digests (per-sample roots) to every rank
+        if dist.world > 1:  # boundary digests (per-sample roots) to every rank
             g.gather_device(d_roots_idx.ptr, len(roots), d_local.ptr, ctx.stream)
-            comm.allgather(d_local.ptr, d_gather.ptr, 32 * len(roots), ctx.stream)
+            if comm is not None:
+                comm.allgather(d_local.ptr, d_gather.ptr, 32 * len(roots), ctx.stream)
+            else:  # no RCCL communicator (see main): same exchange through the host
+                ctx.sync()
+                dist.all_gather_bytes(d_local.to_numpy())
 
     steps = args.dag_steps
     t = timed_steps(dist, ctx, step, steps, 2)
@@ -689,11 +714,19 @@ def main():
     skip = set(filter(None, args.skip.split(",")))
 
     dist = Dist(args.gpus)
-    ctx = capi.Context(dist.local)
-    comm = None
+    device = dist.local
+    share = os.environ.get("RF_BENCH_SHARE_GPU") == "1"
+    if share:  # rehearsal of the N-rank path on a box with fewer GPUs (never the driver's run)
+        device = dist.local % max(capi.device_count(), 1)
+    ctx = capi.Context(device)
+    comm, exchange = None, "none (1 rank)"
     if dist.world > 1:
-        uid = dist.bcast_bytes(capi.Comm.unique_id() if dist.rank == 0 else None)
-        comm = capi.Comm(ctx, dist.world, dist.rank, uid)
+        if share:
+            exchange = "gloo host all-gather (RF_BENCH_SHARE_GPU: RCCL needs one GPU per rank)"
+        else:
+            uid = dist.bcast_bytes(capi.Comm.unique_id() if dist.rank == 0 else None)
+            comm = capi.Comm(ctx, dist.world, dist.rank, uid)
+            exchange = "RCCL all-gather over xGMI"
 
     sha = bench_sha(args, dist, ctx)
     c1 = None if "c1" in skip else bench_c1(args, dist, ctx)
@@ -725,7 +758,8 @@ def main():
             "config": {"workload": "configs[1]: 64 GiB FASTQ/BAM-like Fileset per GPU, %d files 4 KiB-2 GiB "
                                    "(98%% log-uniform 4 KiB-1 MiB, 2%% 64 MiB-2 GiB), SHA-256 of every file"
                                    % sha["files"],
-                       "parallelism": "files sharded per GPU (independent); RCCL only for DAG root digests"},
+                       "parallelism": "files sharded per GPU (independent); RCCL only for DAG root digests",
+                       "exchange": exchange},
             "roofline": sha["roofline"],
             "cpu_baseline": cpu,
             "c1": c1,

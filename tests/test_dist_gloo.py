@@ -31,10 +31,11 @@ def _worker(rank, world, port, q):
     mx = d.max(1.0 + rank)
     sm = d.sum(10.0 * (rank + 1))
     uid = d.bcast_bytes(b"U" * 128 if rank == 0 else None)
+    ag = d.all_gather_bytes(np.full(3, 7 + rank, dtype=np.uint8)).tolist()  # root-digest exchange without RCCL
     seed = 0x5EED0004 + rank
     lens = c2_sizes(total_bytes=1 << 30, seed=seed)
     dag = Dag1000(3, 4, seed=0x5EED0003 + 1000003 * rank)
-    q.put((rank, mx, sm, uid, int(lens.sum()), lens[:8].tolist(), dag.leaf_ids[:2].tobytes()))
+    q.put((rank, mx, sm, uid, int(lens.sum()), lens[:8].tolist(), dag.leaf_ids[:2].tobytes(), ag))
     d.dist.destroy_process_group()
 
 
@@ -50,7 +51,8 @@ def test_gloo_world2_bench_dist():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, mx0, sm0, uid0, b0, l0, ids0), (r1, mx1, sm1, uid1, b1, l1, ids1) = res
+    (r0, mx0, sm0, uid0, b0, l0, ids0, ag0), (r1, mx1, sm1, uid1, b1, l1, ids1, ag1) = res
+    assert ag0 == ag1 == [7, 7, 7, 8, 8, 8]  # rank order
     assert mx0 == mx1 == 2.0  # max over ranks
     assert sm0 == sm1 == 30.0  # whole-job aggregate
     assert uid0 == uid1 == b"U" * 128  # RCCL id reaches every rank

@@ -14,17 +14,22 @@ import csv
 import json
 import sys
 
-WIDE_STREAM = {"rf::k1_sha256_duo", "rf::k1_sha256_solo", "rf::k1_sha256_lanes", "rf::k_gen_fill"}
+WIDE_STREAM = {"rf::k1_sha256_duo", "rf::k1_sha256_octo", "rf::k1_sha256_solo", "rf::k1_sha256_lanes", "rf::k_gen_fill"}
 
 
 def load(path):
-    agg = collections.defaultdict(lambda: [0, 0.0])
-    for r in csv.DictReader(open(path)):
+    """kernel -> [dispatches, total KiB, largest dispatch's KiB]"""
+    per = collections.defaultdict(float)
+    for i, r in enumerate(csv.DictReader(open(path))):
         k = r["Kernel_Name"].split("(")[0]
         k = k[5:] if k.startswith("void ") else k
         k = k.split("<")[0]  # one entry per kernel template
+        per[(k, r.get("Dispatch_Id", i))] += float(r["Counter_Value"])
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+    for (k, _), v in per.items():
         agg[k][0] += 1
-        agg[k][1] += float(r["Counter_Value"])
+        agg[k][1] += v
+        agg[k][2] = max(agg[k][2], v)
     return agg
 
 
@@ -33,19 +38,23 @@ def main():
     F, W = load(f), load(w)
     res = {}
     for k in sorted(set(F) | set(W)):
-        nf, vf = F.get(k, [0, 0.0])
-        nw, vw = W.get(k, [0, 0.0])
+        nf, vf, mf = F.get(k, [0, 0.0, 0.0])
+        nw, vw, mw = W.get(k, [0, 0.0, 0.0])
         fb = vf / max(nf, 1) * 1024
         wb = vw / max(nw, 1) * 1024
         corr = 2.0 if k in WIDE_STREAM else 1.0
+        # the mean mixes a kernel's big launches with its small ones (e.g. the
+        # duo chain runs the 64 GiB set and configs[0]'s Fileset material):
+        # the largest dispatch is the one a bench roofline prices
         res[k] = {"calls": nf, "fetch_bytes_raw": fb, "fetch_bytes_corrected": fb * corr,
                   "fetch_correction": corr, "write_bytes": wb,
-                  "traffic_bytes_per_launch": fb * corr + wb}
+                  "traffic_bytes_per_launch": fb * corr + wb,
+                  "traffic_bytes_largest_launch": (mf * corr + mw) * 1024}
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
-        print("%-36s traffic/launch %.4e B (fetch raw %.4e x%.0f, write %.4e)"
-              % (k, v["traffic_bytes_per_launch"], v["fetch_bytes_raw"], v["fetch_correction"],
-                 v["write_bytes"]))
+        print("%-36s traffic/launch %.4e B, largest launch %.4e B (fetch raw %.4e x%.0f, write %.4e)"
+              % (k, v["traffic_bytes_per_launch"], v["traffic_bytes_largest_launch"], v["fetch_bytes_raw"],
+                 v["fetch_correction"], v["write_bytes"]))
 
 
 if __name__ == "__main__":
