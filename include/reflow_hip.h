@@ -49,6 +49,7 @@ typedef struct rf_sha_plan rf_sha_plan;
 typedef struct rf_graph rf_graph;
 typedef struct rf_bloom rf_bloom;
 typedef struct rf_assoc rf_assoc;
+typedef struct rf_install rf_install;
 
 /* ---- context ----------------------------------------------------------- */
 /* Bind a context to HIP device `device` (one process per GPU).  Replaces the
@@ -147,6 +148,31 @@ int rf_fileset_digest_batch(rf_ctx *ctx, uint64_t n_sets, const uint64_t *set_gr
 int rf_fileset_digest_device(rf_ctx *ctx, uint64_t n_sets, const uint64_t *set_group,
                              const uint64_t *group_entry, const char *const *paths,
                              const uint32_t *path_lens, const void *d_ids32, uint8_t *out32);
+
+/* ---- Executor.install: walk + read + digest a tree into a Fileset ----------
+ * Replaces local/executor.go:514-557 (install: walker loop, <=60 concurrent
+ * repo.Install calls, Fileset{Map} assembly) over internal/walker/walker.go:33-99
+ * and repository/file/repository.go:50-63 (ID = SHA256(contents)).  Walk
+ * semantics are the walker's: os.Stat follows symlinks, a path that does not
+ * exist (ENOENT, e.g. a dangling link) is skipped, directory entries are
+ * visited in bytewise-sorted, depth-first pre-order; every non-directory
+ * entry is read and digested (one K1 batch per <= 8 GiB chunk).  Entry i has
+ * relpath = filepath.Rel(root, path) ("." when root is a file), ID and Size =
+ * the Stat size (executor.go:525).  A missing root gives n = 0 and the digest
+ * of the empty Fileset.  Errors: RF_EIO for stat/readdir/open/read failures
+ * (the walker's w.Err(), Install's error) and for a file whose size changed
+ * between the walk and the read.  The optional symlink replacement of
+ * executor.go:544-552 stays with the caller (it only uses the IDs returned).
+ * rf_install_info: entry count, total relpath bytes, and
+ * Fileset{Map: relpath -> File}.Digest() (executor.go:205-233).
+ * rf_install_entries: caller-allocated paths (path_bytes), path_offs (n+1),
+ * ids32 (32n), sizes (n), in walk order; any of them may be NULL. */
+int rf_install_dir(rf_ctx *ctx, const char *root, rf_install **out);
+int rf_install_info(const rf_install *in, uint64_t *n_entries, uint64_t *path_bytes,
+                    uint8_t fileset_digest32[32]);
+int rf_install_entries(const rf_install *in, char *paths, uint64_t *path_offs, uint8_t *ids32,
+                       int64_t *sizes);
+void rf_install_destroy(rf_install *in);
 
 /* ---- Fileset values as JSON (the assoc value, eval.go:1141 -> marshal
  * eval.go:1961-1967 = json.Marshal + Repository.Put, repository.go:108-114) --

@@ -6,6 +6,7 @@
 //   Digest / WriteDigest      grailbio/base/digest (00 05 || sha256)
 //   Digester                  reflow.Digester (flow.go:36), batched on the GPU
 //   File / Fileset            executor.go:25-38, WriteDigest :214-233
+//   Install                   Executor.install (local/executor.go:514-557)
 //   Op / Config / Flow        flow.go:40-301, Op.DigestString op_string.go:15-21
 //   flow::Exec/Intern/...     test/flow/constructor.go:17-74
 //   Eval                      Flow.Digest / PhysicalDigest / CacheKeys /
@@ -108,6 +109,11 @@ std::vector<Digest> FilesetDigests(Engine& e, const std::vector<const Fileset*>&
 // CacheWrite stores under each cache key (SHA-256 on the GPU).
 std::string MarshalJSON(const Fileset& v);
 std::vector<Digest> FilesetValueDigests(Engine& e, const std::vector<const Fileset*>& v);
+// Executor.install (local/executor.go:514-557): walk `path` like
+// internal/walker (symlinks followed, missing paths skipped, sorted
+// depth-first), digest every file on the GPU -> Fileset{Map: relpath -> File}.
+// *digest (optional) receives the Fileset's digest computed alongside.
+Fileset Install(Engine& e, const std::string& path, Digest* digest = nullptr);
 
 // ---- flows -------------------------------------------------------------------
 enum Op : int {

@@ -9,6 +9,7 @@ What it restates (reference = LDuderino/reflow @ v0 under /root/reference):
   * digest framing  WD(d) = 0x00 0x05 || d          (grailbio/base/digest, not
     vendored; pinned by the goldens below)
   * Fileset.WriteDigest / Digest                   executor.go:205-233
+  * Executor.install over walker.Scan               local/executor.go:514-557, internal/walker/walker.go:33-99
   * json.Marshal(Fileset) -> assoc value digest     executor.go:25-38, eval.go:1961-1967
     (Go 1.9/1.10 encoding/json byte rules; digest JSON text unpinned)
   * Op.DigestString (stale table, OpData->"maxOp")  op_string.go:11-21
@@ -135,6 +136,35 @@ class OFileset:
 
     def value_digest(self) -> bytes:
         return sha256(self.json())
+
+
+def install_dir(root):
+    """Executor.install (local/executor.go:514-557) over walker.Scan
+    (internal/walker/walker.go:33-99): os.Stat follows links and ENOENT skips
+    the path (:39-43); directories expand to their bytewise-sorted names,
+    prepended to the todo list (:48-55, readDirNames :88-99), so the order is
+    depth-first pre-order; every non-directory is Install-ed (ID =
+    SHA256(contents), repository/file/repository.go:50-63) with Size = the
+    Stat size (executor.go:525) under relpath = filepath.Rel(root, path).
+    Returns ([(relpath bytes, id32, size)] in walk order, Fileset digest)."""
+    root = os.fsencode(root)
+    ents = []
+    todo = [(root, b".")]
+    while todo:
+        path, rel = todo.pop(0)
+        try:
+            st = os.stat(path)
+        except FileNotFoundError:
+            continue
+        if (st.st_mode & 0o170000) == 0o040000:  # S_ISDIR
+            names = sorted(os.listdir(path))
+            todo = [(path + b"/" + nm, nm if rel == b"." else rel + b"/" + nm) for nm in names] + todo
+            continue
+        with open(path, "rb") as f:
+            data = f.read()
+        ents.append((rel, sha256(data), st.st_size))
+    material = b"".join(r + WD(i) for r, i, _ in sorted(ents, key=lambda e: e[0]))
+    return ents, sha256(material)
 
 
 def _key_bytes(k) -> bytes:

@@ -26,7 +26,8 @@ EXPORTS = [
     "rf_init", "rf_destroy", "rf_last_error", "rf_device_count", "rf_sync", "rf_version",
     "rf_sha256_batch", "rf_sha256_arena", "rf_sha_plan_create", "rf_sha_plan_run",
     "rf_sha_plan_stats", "rf_sha_plan_destroy", "rf_gen_fill", "rf_fileset_digest_batch",
-    "rf_fileset_digest_device",
+    "rf_fileset_digest_device", "rf_install_dir", "rf_install_info", "rf_install_entries",
+    "rf_install_destroy",
     "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
     "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
@@ -192,6 +193,10 @@ def lib():
             "rf_gen_fill": ([vp, vp, vp, vp, u64, u64, u64, vp], i32),
             "rf_fileset_digest_batch": ([vp, u64, vp, vp, vp, vp, vp, vp], i32),
             "rf_fileset_digest_device": ([vp, u64, vp, vp, vp, vp, vp, vp], i32),
+            "rf_install_dir": ([vp, ctypes.c_char_p, vp], i32),
+            "rf_install_info": ([vp, vp, vp, vp], i32),
+            "rf_install_entries": ([vp, vp, vp, vp, vp], i32),
+            "rf_install_destroy": ([vp], None),
             "rf_graph_load": ([vp, vp, vp], i32), "rf_graph_destroy": ([vp], None),
             "rf_graph_set_slots": ([vp, vp, vp, u32], i32),
             "rf_graph_set_slots_device": ([vp, vp, vp, u32, vp], i32),
@@ -333,6 +338,31 @@ class Context:
     def gen_fill(self, d_arena, d_offs, d_lens, n, seed, arena_bytes, stream=None):
         _check(lib().rf_gen_fill(self._h, d_arena, d_offs, d_lens, n, seed & (2**64 - 1),
                                  arena_bytes, stream))
+
+    # ---- Executor.install -------------------------------------------------
+    def install_dir(self, root):
+        """rf_install_dir: walk `root` (walker.go semantics), digest every file
+        on the GPU.  Returns (entries, fileset_digest32) with entries a list of
+        (relpath bytes, id32, size) in walk order (local/executor.go:514-557)."""
+        h = ctypes.c_void_p()
+        r = root.encode() if isinstance(root, str) else root
+        _check(lib().rf_install_dir(self._h, r, ctypes.byref(h)))
+        try:
+            n, pb = ctypes.c_uint64(0), ctypes.c_uint64(0)
+            fs = np.zeros(32, dtype=np.uint8)
+            _check(lib().rf_install_info(h, ctypes.byref(n), ctypes.byref(pb), _ptr(fs)))
+            n, pb = n.value, pb.value
+            paths = np.zeros(max(pb, 1), dtype=np.uint8)
+            offs = np.zeros(n + 1, dtype=np.uint64)
+            ids = np.zeros(max(32 * n, 1), dtype=np.uint8)
+            sizes = np.zeros(max(n, 1), dtype=np.int64)
+            _check(lib().rf_install_entries(h, _ptr(paths), _ptr(offs), _ptr(ids), _ptr(sizes)))
+        finally:
+            lib().rf_install_destroy(h)
+        pbytes = paths.tobytes()
+        ents = [(pbytes[int(offs[i]):int(offs[i + 1])], ids[32 * i:32 * i + 32].tobytes(), int(sizes[i]))
+                for i in range(n)]
+        return ents, fs.tobytes()
 
     # ---- Fileset --------------------------------------------------------
     def fileset_digest_batch(self, sets):

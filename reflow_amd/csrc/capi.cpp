@@ -8,7 +8,14 @@
 // computed by a HIP kernel; a missing device or code object is RF_EDEVICE.
 #include <hip/hip_runtime.h>
 
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -16,6 +23,7 @@
 #include <mutex>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -751,6 +759,189 @@ extern "C" int rf_fileset_digest_device(rf_ctx* ctx, uint64_t n_sets, const uint
     }
     return rc;
 }
+
+// ---------------------------------------------------------------------------
+// Executor.install (local/executor.go:514-557): walk a tree the way
+// internal/walker/walker.go:33-99 does, digest every non-directory entry
+// (repository/file/repository.go:50-63: ID = SHA256(contents)) and build
+// Fileset{Map: relpath -> File{ID, Size}}.
+//   * os.Stat semantics: symlinks are followed; ENOENT (e.g. a dangling link)
+//     skips the entry (walker.go:40-43); any other stat/readdir error fails.
+//   * directory entries sorted bytewise (readDirNames, walker.go:88-99),
+//     depth-first pre-order (children prepended to the todo list, :52-55).
+//   * relpath = filepath.Rel(root, path): "." for a root that is a file.
+//   * Size = the Stat size (executor.go:525 takes w.Info().Size()).
+// Files are read by a pool of host threads (<= 60, the DigestLimiter of
+// local/executor.go:41) straight into the pinned stage, in chunks of at most
+// kInstallChunk bytes, and each chunk is one K1 batch.
+struct rf_install {
+    std::vector<std::string> rel;
+    std::vector<std::string> full;
+    std::vector<int64_t> sizes;
+    std::vector<uint8_t> ids;
+    uint8_t fileset[32];
+};
+
+static constexpr uint64_t kInstallChunk = 8ull << 30;
+
+static int install_walk(const std::string& path, const std::string& rel, rf_install* in) {
+    struct stat st;
+    if (::stat(path.c_str(), &st) != 0) {
+        if (errno == ENOENT) return RF_OK;
+        return fail(RF_EIO, "stat %s: %s", path.c_str(), strerror(errno));
+    }
+    if (!S_ISDIR(st.st_mode)) {
+        in->full.push_back(path);
+        in->rel.push_back(rel);
+        in->sizes.push_back((int64_t)st.st_size);
+        return RF_OK;
+    }
+    DIR* d = ::opendir(path.c_str());
+    if (!d) return fail(RF_EIO, "open %s: %s", path.c_str(), strerror(errno));
+    std::vector<std::string> names;
+    errno = 0;
+    while (struct dirent* de = ::readdir(d)) {
+        if (strcmp(de->d_name, ".") && strcmp(de->d_name, "..")) names.emplace_back(de->d_name);
+        errno = 0;
+    }
+    const int rerr = errno;
+    ::closedir(d);
+    if (rerr) return fail(RF_EIO, "readdir %s: %s", path.c_str(), strerror(rerr));
+    std::sort(names.begin(), names.end());  // char_traits<char>: bytewise (unsigned) order
+    for (const std::string& nm : names) {
+        int rc = install_walk(path + "/" + nm, rel == "." ? nm : rel + "/" + nm, in);
+        if (rc) return rc;
+    }
+    return RF_OK;
+}
+
+// Read file f (expected `want` bytes) into dst; the content must not have
+// changed size since the walk's stat.
+static bool install_read(const std::string& f, uint8_t* dst, uint64_t want, std::string& err) {
+    const int fd = ::open(f.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+        err = "open " + f + ": " + strerror(errno);
+        return false;
+    }
+    uint64_t got = 0;
+    for (;;) {
+        uint8_t probe;
+        uint8_t* p = got < want ? dst + got : &probe;
+        const size_t ask = got < want ? (size_t)std::min<uint64_t>(want - got, 1ull << 30) : 1;
+        const ssize_t r = ::read(fd, p, ask);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            err = "read " + f + ": " + strerror(errno);
+            ::close(fd);
+            return false;
+        }
+        if (r == 0) break;
+        got += (uint64_t)r;
+        if (got > want) break;
+    }
+    ::close(fd);
+    if (got != want) {
+        err = "file " + f + " changed size while it was digested";
+        return false;
+    }
+    return true;
+}
+
+extern "C" int rf_install_dir(rf_ctx* ctx, const char* root, rf_install** out) {
+    ARG(ctx && root && out, "null argument");
+    *out = nullptr;
+    std::unique_ptr<rf_install> in(new rf_install());
+    int rc = install_walk(root, ".", in.get());
+    if (rc) return rc;
+    const uint64_t n = in->rel.size();
+    in->ids.assign(32 * n, 0);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard g(ctx->device);
+    for (uint64_t c0 = 0; c0 < n;) {
+        // chunk [c0, c1): walk order, at most kInstallChunk bytes (or one file)
+        uint64_t c1 = c0, pos = 0;
+        std::vector<uint64_t> offs, lens;
+        while (c1 < n) {
+            const uint64_t len = (uint64_t)in->sizes[c1];
+            const uint64_t alen = (len + 63) & ~63ull;
+            if (c1 > c0 && pos + alen > kInstallChunk) break;
+            offs.push_back(pos);
+            lens.push_back(len);
+            pos += alen;
+            ++c1;
+        }
+        HIPC(ctx->h_stage.ensure(pos + 64));
+        uint8_t* stage = ctx->h_stage.bytes();
+        std::atomic<uint64_t> next{c0};
+        std::mutex emu;
+        std::string first_err;
+        auto worker = [&]() {
+            for (uint64_t i; (i = next.fetch_add(1)) < c1;) {
+                std::string err;
+                if (!install_read(in->full[i], stage + offs[i - c0], lens[i - c0], err)) {
+                    std::lock_guard<std::mutex> el(emu);
+                    if (first_err.empty()) first_err = err;
+                }
+            }
+        };
+        const uint64_t hw = std::max(1u, std::thread::hardware_concurrency());
+        const uint64_t nt = std::min<uint64_t>({60, hw, c1 - c0});
+        std::vector<std::thread> pool;
+        for (uint64_t t = 1; t < nt; ++t) pool.emplace_back(worker);
+        worker();
+        for (auto& t : pool) t.join();
+        if (!first_err.empty()) return fail(RF_EIO, "%s", first_err.c_str());
+        rc = sha_host_packed(ctx, offs, lens, pos, in->ids.data() + 32 * c0);
+        if (rc) return rc;
+        c0 = c1;
+    }
+    // Fileset{Map}.Digest: one set, one group, all entries
+    std::vector<const char*> paths(n);
+    std::vector<uint32_t> plen(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        paths[i] = in->rel[i].data();
+        plen[i] = (uint32_t)in->rel[i].size();
+    }
+    const uint64_t set_group[2] = {0, 1}, group_entry[2] = {0, n};
+    std::vector<uint64_t> offs, lens;
+    uint64_t arena_bytes = 0;
+    rc = fileset_material(ctx, 1, set_group, group_entry, paths.data(), plen.data(), in->ids.data(), offs, lens,
+                          arena_bytes, nullptr, nullptr);
+    if (rc) return rc;
+    rc = sha_host_packed(ctx, offs, lens, arena_bytes, in->fileset);
+    if (rc) return rc;
+    *out = in.release();
+    return RF_OK;
+}
+
+extern "C" int rf_install_info(const rf_install* in, uint64_t* n_entries, uint64_t* path_bytes,
+                               uint8_t fileset_digest32[32]) {
+    ARG(in, "null install");
+    uint64_t pb = 0;
+    for (const std::string& r : in->rel) pb += r.size();
+    if (n_entries) *n_entries = in->rel.size();
+    if (path_bytes) *path_bytes = pb;
+    if (fileset_digest32) memcpy(fileset_digest32, in->fileset, 32);
+    return RF_OK;
+}
+
+extern "C" int rf_install_entries(const rf_install* in, char* paths, uint64_t* path_offs, uint8_t* ids32,
+                                  int64_t* sizes) {
+    ARG(in, "null install");
+    const uint64_t n = in->rel.size();
+    uint64_t w = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (path_offs) path_offs[i] = w;
+        if (paths && !in->rel[i].empty()) memcpy(paths + w, in->rel[i].data(), in->rel[i].size());
+        w += in->rel[i].size();
+    }
+    if (path_offs) path_offs[n] = w;
+    if (ids32 && n) memcpy(ids32, in->ids.data(), 32 * n);
+    if (sizes && n) memcpy(sizes, in->sizes.data(), 8 * n);
+    return RF_OK;
+}
+
+extern "C" void rf_install_destroy(rf_install* in) { delete in; }
 
 // ---------------------------------------------------------------------------
 // Fileset JSON: json.Marshal(Fileset) -> Repository.Put (eval.go:1961-1967),

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <functional>
+#include <memory>
 #include <unordered_set>
 
 namespace reflow {
@@ -125,6 +126,29 @@ std::vector<Digest> FilesetDigests(Engine& e, const std::vector<const Fileset*>&
         Check(rf_fileset_digest_batch(e.ctx(), v.size(), set_group.data(), group_entry.data(),
                                       paths.data(), plen.data(), ids.data(), out[0].b.data()));
     return out;
+}
+
+Fileset Install(Engine& e, const std::string& path, Digest* digest) {
+    rf_install* in = nullptr;
+    Check(rf_install_dir(e.ctx(), path.c_str(), &in));
+    std::unique_ptr<rf_install, void (*)(rf_install*)> guard(in, rf_install_destroy);
+    uint64_t n = 0, pb = 0;
+    Digest fs;
+    Check(rf_install_info(in, &n, &pb, fs.b.data()));
+    std::string paths(pb, '\0');
+    std::vector<uint64_t> offs(n + 1);
+    std::vector<uint8_t> ids(32 * n);
+    std::vector<int64_t> sizes(n);
+    Check(rf_install_entries(in, paths.data(), offs.data(), ids.data(), sizes.data()));
+    Fileset v;
+    for (uint64_t i = 0; i < n; ++i) {
+        File f;
+        memcpy(f.ID.b.data(), ids.data() + 32 * i, 32);
+        f.Size = sizes[i];
+        v.Map.emplace(paths.substr(offs[i], offs[i + 1] - offs[i]), f);
+    }
+    if (digest) *digest = fs;
+    return v;
 }
 
 // Fileset trees in the rf_fileset_tree CSR form (pre-order nodes; a node's

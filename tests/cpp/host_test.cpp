@@ -9,6 +9,9 @@
 //   TestLiveset           bloomlive Contains over Add, MarshalJSON, Collect
 //   TestAssoc             assoc.Assoc: test/testutil/assoc.go semantics, abbreviations
 // Exit status 0 iff every check passes.
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <string>
 
@@ -231,6 +234,44 @@ static void TestAssoc(Engine& e) {
            "batch order");
 }
 
+// Executor.install (local/executor.go:514-557): the executor_test.go:86-88
+// single-file result, and a small tree whose Fileset digest must equal
+// FilesetDigests over the returned Map.
+static void TestInstall(Engine& e) {
+    char tmpl[] = "/tmp/rf_install_XXXXXX";
+    const std::string d = mkdtemp(tmpl);
+    auto put = [](const std::string& p, const std::string& b) {
+        FILE* f = fopen(p.c_str(), "wb");
+        if (f) {
+            fwrite(b.data(), 1, b.size(), f);
+            fclose(f);
+        }
+    };
+    put(d + "/out", "foobar\n");
+    Digester dg(e);
+    Fileset one_file = Install(e, d + "/out");
+    EXPECT(one_file.Map.size() == 1 && one_file.Map.count(".") &&
+               one_file.Map["."].ID == dg.FromString("foobar\n") && one_file.Map["."].Size == 7,
+           "install single file -> \".\"");
+    mkdir((d + "/t").c_str(), 0755);
+    mkdir((d + "/t/a").c_str(), 0755);
+    put(d + "/t/a/b", "ab");
+    put(d + "/t/a-b", std::string(70000, 'x'));
+    put(d + "/t/z", "");
+    Digest fsd;
+    Fileset t = Install(e, d + "/t", &fsd);
+    EXPECT(t.Map.size() == 3 && t.Map["a-b"].Size == 70000 && t.Map["a/b"].ID == dg.FromString("ab"),
+           "install tree entries");
+    EXPECT(fsd == FilesetDigests(e, {&t})[0], "install fileset digest");
+    unlink((d + "/t/a/b").c_str());
+    unlink((d + "/t/a-b").c_str());
+    unlink((d + "/t/z").c_str());
+    rmdir((d + "/t/a").c_str());
+    rmdir((d + "/t").c_str());
+    unlink((d + "/out").c_str());
+    rmdir(d.c_str());
+}
+
 int main() {
     try {
         Engine e(0);
@@ -242,6 +283,7 @@ int main() {
         TestCacheKeysAndIncremental(e);
         TestLiveset(e);
         TestAssoc(e);
+        TestInstall(e);
     } catch (const std::exception& ex) {
         fprintf(stderr, "exception: %s\n", ex.what());
         return 2;
