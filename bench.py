@@ -273,6 +273,8 @@ def bench_c1(args, dist, ctx):
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "c1_fileset.json")))
     ok = ("sha256:" + fsd.hex() == want["fileset_digest"] and fsd_host == fsd and
           __import__("hashlib").sha256(ids.tobytes()).hexdigest() == want["ids_sha256"])
+    inst = (bench_c1_install(ctx, arena, offs, fsd, cpu_leg=dist.world == 1 and "cpu" not in args.skip)
+            if "install" not in args.skip and dist.rank == 0 else None)
     plan.close()
     for b in (arena, d_offs, d_lens, out):
         b.free()
@@ -297,8 +299,53 @@ def bench_c1(args, dist, ctx):
             "fixture_match": ok,
             "dag_nodes": small.n_nodes, "dag_full_recompute_ms": dag_ms,
             "total_ms": ids_ms + fs_ms + dag_ms,
+            "install": inst,
             "note": "4096 messages on 512 k1_sha256_octo chain waves (eight files per wave): the per-file "
                     "chain (4097 blocks x ~1.2 us) bounds the file-ID time, not chip throughput"}
+
+
+def bench_c1_install(ctx, arena, offs, want_fsd, cpu_leg=False):
+    """configs[0] from files: the same 4096 x 256 KiB contents written as a
+    tree d%02d/f%04d.fq.gz, then Executor.install over it (rf_install_dir:
+    walk, read on <=60 host threads into pinned memory, H2D, K1, Fileset
+    digest) -- page-cache-warm reads, so storage speed is not measured."""
+    import shutil
+    import tempfile
+    host = arena.to_numpy()
+    root = tempfile.mkdtemp(prefix="rf_c1_")
+    try:
+        for i in range(C1_N):
+            p = os.path.join(root, c1_path(i).decode())
+            os.makedirs(os.path.dirname(p), exist_ok=True)
+            with open(p, "wb") as f:
+                f.write(host[int(offs[i]):int(offs[i]) + C1_LEN].tobytes())
+        del host
+        ctx.install_dir(root)  # warm-up (stage allocation, plan)
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ents, fsd = ctx.install_dir(root)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        res = {"what": "rf_install_dir over the configs[0] tree on local disk (page cache warm)",
+               "ms": ms, "gbps": C1_N * C1_LEN / (ms * 1e-3) / 1e9, "entries": len(ents),
+               "fileset_digest_match": fsd == want_fsd}
+        if cpu_leg:  # the same install on the host: read + hashlib (OpenSSL) SHA-256, 16 threads
+            import hashlib
+            from concurrent.futures import ThreadPoolExecutor
+            paths = [os.path.join(root, c1_path(i).decode()) for i in range(C1_N)]
+
+            def one(p):
+                with open(p, "rb") as f:
+                    return hashlib.sha256(f.read()).digest()
+            with ThreadPoolExecutor(16) as ex:
+                t0 = time.perf_counter()
+                cpu_ids = list(ex.map(one, paths))
+                cms = (time.perf_counter() - t0) * 1e3
+            res["cpu_openssl_16t"] = {"ms": cms, "gbps": C1_N * C1_LEN / (cms * 1e-3) / 1e9, "cores": 16,
+                                      "ids_match": cpu_ids == [e[1] for e in ents]}
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return res
 
 
 # ------------------------------------------------------- C3: incremental --
@@ -709,7 +756,7 @@ def main():
     ap.add_argument("--probe-steps", type=int, default=3)
     ap.add_argument("--cpu-sample-gib", type=float, default=20.0)
     ap.add_argument("--cpu-dag-samples", type=int, default=200)
-    ap.add_argument("--skip", default="", help="comma list of: c1,dag,probe,cpu")
+    ap.add_argument("--skip", default="", help="comma list of: c1,install,dag,probe,cpu")
     args = ap.parse_args()
     skip = set(filter(None, args.skip.split(",")))
 
