@@ -14,8 +14,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cerrno>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -581,14 +583,12 @@ extern "C" void rf_sha_plan_destroy(rf_sha_plan* p) {
 
 // Host-buffer batch: pack into pinned staging with 64-B aligned starts,
 // upload, plan, run, download.
-static int sha_host_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
-                           const std::vector<uint64_t>& lens, uint64_t arena_bytes,
-                           uint8_t* out32) {
+// The packed messages already in ctx->d_arena (queued on ctx->stream): plan,
+// run, download.
+static int sha_device_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
+                             const std::vector<uint64_t>& lens, uint8_t* out32) {
     const uint64_t n = lens.size();
-    HIPC(ctx->d_arena.ensure(arena_bytes + 64));
     HIPC(ctx->d_out.ensure(32 * n));
-    HIPC(hipMemcpyAsync(ctx->d_arena.p, ctx->h_stage.p, arena_bytes, hipMemcpyHostToDevice,
-                        ctx->stream));
     rf_sha_plan* p = nullptr;
     int rc = transient_plan(ctx, offs.data(), lens.data(), n, &p);
     if (rc) return rc;
@@ -599,6 +599,15 @@ static int sha_host_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
         if (e != hipSuccess) rc = fail(RF_EDEVICE, "sha256 batch: %s", hipGetErrorString(e));
     }
     return rc;
+}
+
+static int sha_host_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
+                           const std::vector<uint64_t>& lens, uint64_t arena_bytes,
+                           uint8_t* out32) {
+    HIPC(ctx->d_arena.ensure(arena_bytes + 64));
+    HIPC(hipMemcpyAsync(ctx->d_arena.p, ctx->h_stage.p, arena_bytes, hipMemcpyHostToDevice,
+                        ctx->stream));
+    return sha_device_packed(ctx, offs, lens, out32);
 }
 
 extern "C" int rf_sha256_batch(rf_ctx* ctx, const uint8_t* const* msgs, const uint64_t* lens,
@@ -783,10 +792,14 @@ struct rf_install {
 };
 
 static constexpr uint64_t kInstallChunk = 8ull << 30;
+static constexpr uint64_t kInstallSeg = 32ull << 20;
 
-static int install_walk(const std::string& path, const std::string& rel, rf_install* in) {
+// Entry `name` of the directory open as dfd (or the root path itself when
+// dfd == AT_FDCWD); stat relative to the directory fd (no full path walk).
+static int install_walk(int dfd, const std::string& name, const std::string& path, const std::string& rel,
+                        rf_install* in) {
     struct stat st;
-    if (::stat(path.c_str(), &st) != 0) {
+    if (::fstatat(dfd, name.c_str(), &st, 0) != 0) {
         if (errno == ENOENT) return RF_OK;
         return fail(RF_EIO, "stat %s: %s", path.c_str(), strerror(errno));
     }
@@ -796,23 +809,37 @@ static int install_walk(const std::string& path, const std::string& rel, rf_inst
         in->sizes.push_back((int64_t)st.st_size);
         return RF_OK;
     }
-    DIR* d = ::opendir(path.c_str());
-    if (!d) return fail(RF_EIO, "open %s: %s", path.c_str(), strerror(errno));
-    std::vector<std::string> names;
+    const int fd = ::openat(dfd, name.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    DIR* d = fd >= 0 ? ::fdopendir(fd) : nullptr;
+    if (!d) {
+        const int e = errno;
+        if (fd >= 0) ::close(fd);
+        return fail(RF_EIO, "open %s: %s", path.c_str(), strerror(e));
+    }
+    std::vector<std::pair<std::string, unsigned char>> names;
     errno = 0;
     while (struct dirent* de = ::readdir(d)) {
-        if (strcmp(de->d_name, ".") && strcmp(de->d_name, "..")) names.emplace_back(de->d_name);
+        if (strcmp(de->d_name, ".") && strcmp(de->d_name, "..")) names.emplace_back(de->d_name, de->d_type);
         errno = 0;
     }
-    const int rerr = errno;
-    ::closedir(d);
-    if (rerr) return fail(RF_EIO, "readdir %s: %s", path.c_str(), strerror(rerr));
-    std::sort(names.begin(), names.end());  // char_traits<char>: bytewise (unsigned) order
-    for (const std::string& nm : names) {
-        int rc = install_walk(path + "/" + nm, rel == "." ? nm : rel + "/" + nm, in);
-        if (rc) return rc;
+    int rc = errno ? fail(RF_EIO, "readdir %s: %s", path.c_str(), strerror(errno)) : RF_OK;
+    // char_traits<char>: bytewise (unsigned) order
+    std::sort(names.begin(), names.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (size_t i = 0; rc == RF_OK && i < names.size(); ++i) {
+        const std::string& nm = names[i].first;
+        std::string cpath = path + "/" + nm, crel = rel == "." ? nm : rel + "/" + nm;
+        if (names[i].second == DT_REG) {
+            // a regular file (not a link): its Stat size is taken by the
+            // parallel pass in rf_install_dir (-1 = pending)
+            in->full.push_back(std::move(cpath));
+            in->rel.push_back(std::move(crel));
+            in->sizes.push_back(-1);
+        } else {  // directories, links and unknown types: stat (follows links)
+            rc = install_walk(::dirfd(d), nm, cpath, crel, in);
+        }
     }
-    return RF_OK;
+    ::closedir(d);
+    return rc;
 }
 
 // Read file f (expected `want` bytes) into dst; the content must not have
@@ -851,8 +878,57 @@ extern "C" int rf_install_dir(rf_ctx* ctx, const char* root, rf_install** out) {
     ARG(ctx && root && out, "null argument");
     *out = nullptr;
     std::unique_ptr<rf_install> in(new rf_install());
-    int rc = install_walk(root, ".", in.get());
+    // RF_INSTALL_TIMING=1: phase times on stderr (diagnostic)
+    const bool timing = getenv("RF_INSTALL_TIMING") != nullptr;
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_begin = now();
+    int rc = install_walk(AT_FDCWD, root, root, ".", in.get());
     if (rc) return rc;
+    {
+        // Stat sizes of the regular files the walk did not stat, in parallel;
+        // one removed since the readdir is skipped, as the walker's Stat would
+        std::vector<uint64_t> pend;
+        for (uint64_t i = 0; i < in->sizes.size(); ++i)
+            if (in->sizes[i] < 0) pend.push_back(i);
+        std::vector<int> err(pend.size(), 0);
+        std::atomic<uint64_t> nx{0};
+        auto st_worker = [&]() {
+            for (uint64_t k; (k = nx.fetch_add(1)) < pend.size();) {
+                struct stat st;
+                if (::stat(in->full[pend[k]].c_str(), &st) == 0)
+                    in->sizes[pend[k]] = (int64_t)st.st_size;
+                else
+                    err[k] = errno;
+            }
+        };
+        const uint64_t hw = std::max(1u, std::thread::hardware_concurrency());
+        const uint64_t nt = std::min<uint64_t>({60, hw, pend.size() / 64 + 1});
+        std::vector<std::thread> pool;
+        for (uint64_t t = 1; t < nt; ++t) pool.emplace_back(st_worker);
+        st_worker();
+        for (auto& t : pool) t.join();
+        bool drop = false;
+        for (uint64_t k = 0; k < pend.size(); ++k) {
+            if (err[k] == ENOENT) {
+                drop = true;
+            } else if (err[k]) {
+                return fail(RF_EIO, "stat %s: %s", in->full[pend[k]].c_str(), strerror(err[k]));
+            }
+        }
+        if (drop) {  // rare: compact out the vanished entries (sizes still -1)
+            uint64_t w = 0;
+            for (uint64_t i = 0; i < in->sizes.size(); ++i) {
+                if (in->sizes[i] < 0) continue;
+                in->full[w] = std::move(in->full[i]);
+                in->rel[w] = std::move(in->rel[i]);
+                in->sizes[w++] = in->sizes[i];
+            }
+            in->full.resize(w);
+            in->rel.resize(w);
+            in->sizes.resize(w);
+        }
+    }
+    const double t_walk = now();
     const uint64_t n = in->rel.size();
     in->ids.assign(32 * n, 0);
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -871,27 +947,74 @@ extern "C" int rf_install_dir(rf_ctx* ctx, const char* root, rf_install** out) {
             ++c1;
         }
         HIPC(ctx->h_stage.ensure(pos + 64));
+        HIPC(ctx->d_arena.ensure(pos + 64));
         uint8_t* stage = ctx->h_stage.bytes();
-        std::atomic<uint64_t> next{c0};
+        // segments of >= kInstallSeg bytes (consecutive files): the H2D copy of
+        // a segment is queued as soon as its last file is read, overlapping
+        // the reads of the next ones (files are claimed in order)
+        std::vector<uint64_t> seg_first{0};
+        for (uint64_t i = 0, acc = 0; i < c1 - c0; ++i) {
+            acc += (lens[i] + 63) & ~63ull;
+            if (acc >= kInstallSeg && i + 1 < c1 - c0) {
+                seg_first.push_back(i + 1);
+                acc = 0;
+            }
+        }
+        seg_first.push_back(c1 - c0);
+        const uint64_t nseg = seg_first.size() - 1;
+        std::vector<uint64_t> seg_of(c1 - c0);
+        std::unique_ptr<std::atomic<uint64_t>[]> left(new std::atomic<uint64_t>[nseg]);
+        for (uint64_t sg = 0; sg < nseg; ++sg) {
+            left[sg] = seg_first[sg + 1] - seg_first[sg];
+            for (uint64_t i = seg_first[sg]; i < seg_first[sg + 1]; ++i) seg_of[i] = sg;
+        }
+        std::atomic<uint64_t> next{0};
         std::mutex emu;
+        std::condition_variable cv;
         std::string first_err;
         auto worker = [&]() {
-            for (uint64_t i; (i = next.fetch_add(1)) < c1;) {
+            for (uint64_t i; (i = next.fetch_add(1)) < c1 - c0;) {
                 std::string err;
-                if (!install_read(in->full[i], stage + offs[i - c0], lens[i - c0], err)) {
+                if (!install_read(in->full[c0 + i], stage + offs[i], lens[i], err)) {
                     std::lock_guard<std::mutex> el(emu);
                     if (first_err.empty()) first_err = err;
+                }
+                if (left[seg_of[i]].fetch_sub(1) == 1) {
+                    std::lock_guard<std::mutex> el(emu);
+                    cv.notify_all();
                 }
             }
         };
         const uint64_t hw = std::max(1u, std::thread::hardware_concurrency());
         const uint64_t nt = std::min<uint64_t>({60, hw, c1 - c0});
         std::vector<std::thread> pool;
-        for (uint64_t t = 1; t < nt; ++t) pool.emplace_back(worker);
-        worker();
+        for (uint64_t t = 0; t < nt; ++t) pool.emplace_back(worker);
+        hipError_t he = hipSuccess;
+        for (uint64_t sg = 0; sg < nseg; ++sg) {  // this thread queues the copies, in order
+            {
+                std::unique_lock<std::mutex> el(emu);
+                cv.wait(el, [&] { return left[sg].load() == 0; });
+            }
+            const uint64_t b0 = offs[seg_first[sg]];
+            const uint64_t b1 = seg_first[sg + 1] < c1 - c0 ? offs[seg_first[sg + 1]] : pos;
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->d_arena.as<uint8_t>() + b0, stage + b0, b1 - b0, hipMemcpyHostToDevice,
+                                    ctx->stream);
+        }
         for (auto& t : pool) t.join();
-        if (!first_err.empty()) return fail(RF_EIO, "%s", first_err.c_str());
-        rc = sha_host_packed(ctx, offs, lens, pos, in->ids.data() + 32 * c0);
+        if (timing) {
+            const double tr = now();
+            (void)hipStreamSynchronize(ctx->stream);
+            fprintf(stderr, "[install] walk %.2f ms, reads done %.2f ms, copies done %.2f ms (%llu files, %llu threads)\n",
+                    t_walk - t_begin, tr - t_begin, now() - t_begin, (unsigned long long)(c1 - c0),
+                    (unsigned long long)nt);
+        }
+        if (!first_err.empty()) {
+            (void)hipStreamSynchronize(ctx->stream);
+            return fail(RF_EIO, "%s", first_err.c_str());
+        }
+        HIPC(he);
+        rc = sha_device_packed(ctx, offs, lens, in->ids.data() + 32 * c0);
         if (rc) return rc;
         c0 = c1;
     }
@@ -908,8 +1031,10 @@ extern "C" int rf_install_dir(rf_ctx* ctx, const char* root, rf_install** out) {
     rc = fileset_material(ctx, 1, set_group, group_entry, paths.data(), plen.data(), in->ids.data(), offs, lens,
                           arena_bytes, nullptr, nullptr);
     if (rc) return rc;
+    const double t_ids = now();
     rc = sha_host_packed(ctx, offs, lens, arena_bytes, in->fileset);
     if (rc) return rc;
+    if (timing) fprintf(stderr, "[install] ids %.2f ms, fileset digest %.2f ms\n", t_ids - t_begin, now() - t_begin);
     *out = in.release();
     return RF_OK;
 }
