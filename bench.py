@@ -573,6 +573,23 @@ def bench_assoc(ctx, keys, n_ins, n_probe, hits):
     occ, cap = a.stats()
     for b in (vals, st, d_v, d_f):
         b.free()
+    # Eval.lookup for a batch of nodes (rf_assoc_lookup, host API): CacheKeys
+    # [physical (absent), logical (an inserted key)] per node, precise read
+    # repair writes the found value under the physical key
+    n_nodes = min(2_000_000, n_ins)
+    logical = keys.to_numpy(count=32 * n_nodes).reshape(n_nodes, 32)
+    physical = np.random.default_rng(0x5EED0007).integers(0, 256, size=(n_nodes, 32), dtype=np.uint8)
+    node_keys = np.stack([physical, logical], axis=1).reshape(-1)
+    ptr = np.arange(0, 2 * n_nodes + 1, 2, dtype=np.uint64)
+    t0 = time.perf_counter()
+    which, _ = a.lookup(0, node_keys, ptr, repair=2)
+    lk_s = time.perf_counter() - t0
+    _, f2 = a.get(0, physical)  # repaired: the physical keys now resolve
+    lookup = {"workload": "%d nodes x 2 cache keys (physical absent, logical present), precise read repair"
+                          % n_nodes,
+              "ms": lk_s * 1e3, "m_nodes_per_s": n_nodes / lk_s / 1e6,
+              "hits_on_logical": int((which == 1).sum()), "repaired": int(f2.astype(np.int64).sum()),
+              "note": "host API: keys H2D, one Get batch, first-hit select on the device, repair Put batch"}
     a.close()
     # bytes per Get: 32-B key read + a 4-B tag and a 32-B key compare (random)
     # + a 32-B value read (random, hits) + 33-B result write
@@ -581,7 +598,7 @@ def bench_assoc(ctx, keys, n_ins, n_probe, hits):
             "get_ms": get_ms, "get_g_keys_per_s": n_probe / (get_ms * 1e-3) / 1e9,
             "found_exact": found == (n_probe // 2) // n_ins * n_ins,  # every Put key, no false positive
             "bloom_false_positives_resolved": hits - found,
-            "table_slots": cap, "occupied": occ}
+            "table_slots": cap, "occupied": occ, "lookup": lookup}
 
 
 def gather_ceiling(table_bytes, n_threads, reads):

@@ -326,6 +326,19 @@ int rf_assoc_get_device(rf_assoc *a, int kind, const void *d_keys32, uint64_t n,
  * more than one key matches. */
 int rf_assoc_get_abbrev(rf_assoc *a, int kind, const uint8_t *keys32, const uint8_t *nhex, uint64_t n,
                         uint8_t *keys_out32, uint8_t *vals32, int32_t *status);
+/* Eval.lookup's assoc step for a batch of nodes (eval.go:1172-1258): node i's
+ * cache keys (CacheKeys order, most to least concrete) are keys32 rows
+ * [key_ptr[i], key_ptr[i+1]); which[i] = index of the first key whose Get finds
+ * a value (vals32[i] = that value, the Fileset id), or -1 (vals32[i] zeroed).
+ * All keys go in one Get batch (the batching the TODO at eval.go:1199-1201
+ * asks for).  repair: 0 none; 1 = the reference's read repair, Put(zero
+ * expect) of the found value under every other key of the node
+ * (eval.go:1247-1258); 2 = precise read repair, only under the keys that were
+ * missing.  Repairs apply as one Put batch in node order, then key order.  The
+ * fileset unmarshal / missing-file checks (repository I/O) stay with the
+ * caller. */
+int rf_assoc_lookup(rf_assoc *a, int kind, const uint8_t *keys32, const uint64_t *key_ptr, uint64_t n_nodes,
+                    int repair, int32_t *which, uint8_t *vals32);
 /* Occupied slots (live + deleted keys) and table capacity. */
 int rf_assoc_stats(rf_assoc *a, uint64_t *occupied, uint64_t *capacity);
 

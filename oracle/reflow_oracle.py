@@ -427,6 +427,30 @@ class InmemoryAssoc:
         return "ok", hits[0]
 
 
+def assoc_lookup(assoc, kind, node_keys, repair=0):
+    """Eval.lookup's assoc part for a batch of nodes (eval.go:1172-1258):
+    keys are tried in CacheKeys order and the first Get that finds a value
+    wins (which = its index, -1 if none).  repair 1 = the reference's blind
+    read repair, Put(zero expect, key, fsid) for every other key of the node
+    (eval.go:1247-1258); repair 2 = precise read repair (the TODO at
+    eval.go:1199-1201): only the node's keys that were missing.  Nodes apply
+    their repairs in node order, keys in order.  (The fileset unmarshal and
+    repository missing-file checks are repository I/O and stay with the caller.)"""
+    res = []
+    for keys in node_keys:
+        got = [assoc.get(kind, k) for k in keys]
+        which = next((j for j, v in enumerate(got) if v is not None), -1)
+        res.append((which, got[which] if which >= 0 else bytes(32), got))
+    if repair:
+        for keys, (which, val, got) in zip(node_keys, res):
+            if which < 0:
+                continue
+            for j, k in enumerate(keys):
+                if j != which and (repair == 1 or got[j] is None):
+                    assoc.put(kind, None, k, val)
+    return [(w, v) for w, v, _ in res]
+
+
 # --------------------------------------------------------------------------
 # values.WriteDigest subset (values/values.go:290-393) for the values golden
 # --------------------------------------------------------------------------

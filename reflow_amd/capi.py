@@ -38,7 +38,7 @@ EXPORTS = [
     "rf_comm_allgather", "rf_comm_allreduce_or", "rf_memcpy_d2d", "rf_graph_gather_device",
     "rf_fileset_marshal_json", "rf_fileset_value_digest_batch",
     "rf_bloom_marshal_json", "rf_bloom_marshal_binary", "rf_bloom_collect", "rf_bloom_collect_device",
-    "rf_dedup_digests", "rf_dedup_digests_device",
+    "rf_dedup_digests", "rf_dedup_digests_device", "rf_assoc_lookup",
     "rf_assoc_new", "rf_assoc_destroy", "rf_assoc_put", "rf_assoc_get", "rf_assoc_get_device",
     "rf_assoc_get_abbrev", "rf_assoc_stats", "rf_assoc_put_device",
 ]
@@ -234,6 +234,7 @@ def lib():
             "rf_assoc_new": ([vp, u64, vp], i32), "rf_assoc_destroy": ([vp], None),
             "rf_assoc_put": ([vp, i32, vp, vp, vp, u64, vp], i32),
             "rf_assoc_get": ([vp, i32, vp, u64, vp, vp], i32),
+            "rf_assoc_lookup": ([vp, i32, vp, vp, u64, i32, vp, vp], i32),
             "rf_assoc_get_device": ([vp, i32, vp, u64, vp, vp, vp], i32),
             "rf_assoc_get_abbrev": ([vp, i32, vp, vp, u64, vp, vp, vp], i32),
             "rf_assoc_stats": ([vp, vp, vp], i32),
@@ -712,6 +713,18 @@ class Assoc:
         found = np.zeros(max(n, 1), dtype=np.uint8)
         _check(lib().rf_assoc_get(self._h, kind, _ptr(k), n, _ptr(vals), _ptr(found)))
         return vals[:n], found[:n]
+
+    def lookup(self, kind, keys, key_ptr, repair=0):
+        """rf_assoc_lookup: keys (rows of 32 B) grouped per node by key_ptr
+        (n_nodes + 1 offsets).  Returns (which int32 per node, values)."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        kp = np.ascontiguousarray(key_ptr, dtype=np.uint64)
+        n = len(kp) - 1
+        which = np.zeros(max(n, 1), dtype=np.int32)
+        vals = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        _check(lib().rf_assoc_lookup(self._h, kind, _ptr(k) if len(k) else None, _ptr(kp), n, repair,
+                                     _ptr(which), _ptr(vals)))
+        return which[:n], vals[:n]
 
     def put_device(self, kind, d_keys, d_vals, n, d_status, d_expect=None):
         _check(lib().rf_assoc_put_device(self._h, kind, d_expect, d_keys, d_vals, n, d_status))

@@ -2163,6 +2163,76 @@ extern "C" int rf_assoc_get(rf_assoc* a, int kind, const uint8_t* keys32, uint64
     return RF_OK;
 }
 
+// Eval.lookup over a batch of nodes (eval.go:1172-1258): one Get batch over
+// every node's cache keys (the BatchGetItem the TODO at eval.go:1199-1201
+// asks for), first hit per node selected on the device, then the read
+// repair as one Put batch in node order.
+extern "C" int rf_assoc_lookup(rf_assoc* a, int kind, const uint8_t* keys32, const uint64_t* key_ptr, uint64_t n_nodes,
+                               int repair, int32_t* which, uint8_t* vals32) {
+    ARG(a && key_ptr && (n_nodes == 0 || (which && vals32)), "null argument");
+    ARG(repair >= 0 && repair <= 2, "repair must be 0, 1 or 2");
+    ARG(kind >= 0 && kind < (1 << 30), "bad assoc kind");
+    if (!n_nodes) return RF_OK;
+    ARG(key_ptr[0] == 0, "key_ptr[0] must be 0");
+    for (uint64_t i = 0; i < n_nodes; ++i) ARG(key_ptr[i] <= key_ptr[i + 1], "key_ptr not monotone");
+    const uint64_t nk = key_ptr[n_nodes];
+    ARG(nk == 0 || keys32, "null keys");
+    ARG(nk <= (1u << 30), "lookup batch too large");
+    rf_ctx* ctx = a->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
+    // scratch: keys + per-key values (b_keys, b_vals), found per key, the
+    // node CSR and per-node outputs (b_exp region)
+    HIPC(a->b_keys.ensure(32 * nk + 32));
+    HIPC(a->b_vals.ensure(32 * nk + 32));
+    HIPC(a->b_found.ensure(nk + 16));
+    const uint64_t off_which = (8 * (n_nodes + 1) + 15) & ~15ull, off_out = (off_which + 4 * n_nodes + 15) & ~15ull;
+    HIPC(a->b_exp.ensure(off_out + 32 * n_nodes));
+    uint64_t* d_ptr = a->b_exp.as<uint64_t>();
+    int32_t* d_which = reinterpret_cast<int32_t*>(a->b_exp.as<uint8_t>() + off_which);
+    uint8_t* d_out = a->b_exp.as<uint8_t>() + off_out;
+    if (nk) HIPC(hipMemcpyAsync(a->b_keys.p, keys32, 32 * nk, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(d_ptr, key_ptr, 8 * (n_nodes + 1), hipMemcpyHostToDevice, s));
+    HIPC(launch_assoc_get(a->view(), (uint32_t)kind, a->b_keys.as<uint8_t>(), nk, a->b_vals.as<uint8_t>(),
+                          a->b_found.as<uint8_t>(), s));
+    HIPC(launch_assoc_select(a->b_found.as<uint8_t>(), a->b_vals.as<uint8_t>(), d_ptr, n_nodes, d_which, d_out, s));
+    HIPC(hipMemcpyAsync(which, d_which, 4 * n_nodes, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(vals32, d_out, 32 * n_nodes, hipMemcpyDeviceToHost, s));
+    std::vector<uint8_t> found;
+    if (repair == 2) {
+        found.resize(nk);
+        if (nk) HIPC(hipMemcpyAsync(found.data(), a->b_found.p, nk, hipMemcpyDeviceToHost, s));
+    }
+    HIPC(hipStreamSynchronize(s));
+    if (!repair) return RF_OK;
+    // read repair: Put(zero expect, key, fsid) per other key of a hit node,
+    // node order then key order (eval.go:1247-1258; precise: missing keys only)
+    std::vector<uint8_t> rk, rv;
+    rk.reserve(32 * nk);
+    rv.reserve(32 * nk);
+    for (uint64_t i = 0; i < n_nodes; ++i) {
+        if (which[i] < 0) continue;
+        for (uint64_t k = key_ptr[i]; k < key_ptr[i + 1]; ++k) {
+            if ((int64_t)(k - key_ptr[i]) == which[i] || (repair == 2 && found[k])) continue;
+            rk.insert(rk.end(), keys32 + 32 * k, keys32 + 32 * k + 32);
+            rv.insert(rv.end(), vals32 + 32 * i, vals32 + 32 * i + 32);
+        }
+    }
+    const uint64_t nr = rk.size() / 32;
+    if (!nr) return RF_OK;
+    HIPC(a->b_keys.ensure(32 * nr));
+    HIPC(a->b_vals.ensure(32 * nr));
+    HIPC(a->b_status.ensure(4 * nr));
+    HIPC(hipMemcpyAsync(a->b_keys.p, rk.data(), 32 * nr, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(a->b_vals.p, rv.data(), 32 * nr, hipMemcpyHostToDevice, s));
+    int rc = assoc_put_locked(a, kind, nullptr, a->b_keys.as<uint8_t>(), a->b_vals.as<uint8_t>(), nr,
+                              a->b_status.as<int32_t>());
+    if (rc) return rc;
+    HIPC(hipStreamSynchronize(s));
+    return RF_OK;
+}
+
 extern "C" int rf_assoc_get_abbrev(rf_assoc* a, int kind, const uint8_t* keys32, const uint8_t* nhex, uint64_t n,
                                    uint8_t* keys_out32, uint8_t* vals32, int32_t* status) {
     ARG(a && (n == 0 || (keys32 && nhex && keys_out32 && vals32 && status)), "null argument");

@@ -121,6 +121,8 @@ hipError_t launch_assoc_round(const AssocView& t, const uint32_t* rem, const uin
                               int32_t* status, uint32_t* next, uint32_t* n_next, hipStream_t s);
 hipError_t launch_assoc_get(const AssocView& t, uint32_t kind, const uint8_t* keys, uint64_t n, uint8_t* vals,
                             uint8_t* found, hipStream_t s);
+hipError_t launch_assoc_select(const uint8_t* found, const uint8_t* vals, const uint64_t* key_ptr, uint64_t n,
+                              int32_t* which, uint8_t* out, hipStream_t s);
 hipError_t launch_assoc_abbrev(const AssocView& t, uint32_t kind, uint32_t cap, const uint8_t* qkeys,
                                const uint8_t* nhex, uint32_t q, uint32_t* matches, uint32_t* hit_slot,
                                hipStream_t s);

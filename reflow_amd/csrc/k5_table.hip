@@ -223,6 +223,32 @@ __global__ __launch_bounds__(256) void k5_assoc_get(AssocView t, uint32_t kind, 
     }
 }
 
+// Eval.lookup for a batch of nodes (eval.go:1202-1221): node i's cache keys
+// are [key_ptr[i], key_ptr[i+1]) of a k5_assoc_get batch in CacheKeys order;
+// the first key found wins.  One lane per node.
+__global__ __launch_bounds__(256) void k5_assoc_select(const uint8_t* __restrict__ found,
+                                                       const uint8_t* __restrict__ vals,
+                                                       const uint64_t* __restrict__ key_ptr, uint64_t n,
+                                                       int32_t* __restrict__ which, uint8_t* __restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = key_ptr[i], e = key_ptr[i + 1];
+        int32_t w = -1;
+        uint4 lo = make_uint4(0, 0, 0, 0), hi = lo;
+        for (uint64_t k = b; k < e; ++k)
+            if (found[k]) {
+                w = (int32_t)(k - b);
+                const uint4* v = reinterpret_cast<const uint4*>(vals + 32ull * k);
+                lo = v[0];
+                hi = v[1];
+                break;
+            }
+        which[i] = w;
+        uint4* o = reinterpret_cast<uint4*>(out + 32ull * i);
+        o[0] = lo;
+        o[1] = hi;
+    }
+}
+
 // Abbreviated keys (dydbassoc.go:111-147: the ID4 index narrows, Expands
 // decides): every live entry of the kind is compared with each of the q
 // queries' first nhex hex digits; per query, the number of matches and one
@@ -294,6 +320,13 @@ hipError_t launch_assoc_get(const AssocView& t, uint32_t kind, const uint8_t* ke
                             uint8_t* found, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k5_assoc_get, dim3(grid256(n)), dim3(256), 0, s, t, kind, keys, n, vals, found);
+    return hipGetLastError();
+}
+
+hipError_t launch_assoc_select(const uint8_t* found, const uint8_t* vals, const uint64_t* key_ptr, uint64_t n,
+                              int32_t* which, uint8_t* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k5_assoc_select, dim3(grid256(n)), dim3(256), 0, s, found, vals, key_ptr, n, which, out);
     return hipGetLastError();
 }
 

@@ -112,3 +112,44 @@ def test_assoc_abbrev_expansion(ctx):
         if want == "ok":
             assert ko[j].tobytes() == hit[0] and vo[j].tobytes() == hit[1]
     a.close()
+
+
+def _lookup_case(rng, n_nodes, pool, vals):
+    """Nodes with 0..3 cache keys (CacheKeys gives 1-2; 0 and 3 are edges),
+    keys shared between nodes (synonyms), some keys present."""
+    node_keys = [[rng.choice(pool) for _ in range(rng.choice([0, 1, 2, 2, 2, 3]))] for _ in range(n_nodes)]
+    preset = [(k, rng.choice(vals)) for k in rng.sample(pool, len(pool) // 3)]
+    return node_keys, preset
+
+
+@pytest.mark.parametrize("repair", [0, 1, 2])
+def test_assoc_lookup_matches_oracle(ctx, repair):
+    """Eval.lookup's assoc step (eval.go:1172-1258) for a batch of nodes: first
+    hit in key order wins; blind (1) or precise (2) read repair; the table
+    after the batch equals the oracle's, key for key."""
+    from reflow_amd import capi
+    rng = random.Random(40 + repair)
+    pool = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(400)]
+    vals = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(40)]
+    a = capi.Assoc(ctx, capacity=64)
+    ref = O.InmemoryAssoc()
+    for rnd in range(3):  # repairs of one batch feed the next
+        node_keys, preset = _lookup_case(rng, 700, pool, vals)
+        if rnd == 0:
+            for k, v in preset:
+                ref.put(0, None, k, v)
+            st = a.put(0, np.frombuffer(b"".join(k for k, _ in preset), np.uint8),
+                       np.frombuffer(b"".join(v for _, v in preset), np.uint8))
+            assert (st == 0).all()
+        want = O.assoc_lookup(ref, 0, node_keys, repair)
+        flat = b"".join(k for ks in node_keys for k in ks)
+        ptr = np.cumsum([0] + [len(ks) for ks in node_keys]).astype(np.uint64)
+        which, got = a.lookup(0, np.frombuffer(flat, np.uint8), ptr, repair)
+        assert [int(w) for w in which] == [w for w, _ in want]
+        assert [g.tobytes() for g in got] == [v for _, v in want]
+    allk = np.frombuffer(b"".join(pool), np.uint8)
+    gv, gf = a.get(0, allk)
+    for i, k in enumerate(pool):
+        r = ref.get(0, k)
+        assert (r is not None) == bool(gf[i]) and (r is None or gv[i].tobytes() == r)
+
