@@ -277,6 +277,11 @@ class Assoc {
     std::vector<int> PutBatch(AssocKind kind, const std::vector<Digest>& expect, const std::vector<Digest>& keys,
                               const std::vector<Digest>& vals);
     std::vector<std::optional<Digest>> GetBatch(AssocKind kind, const std::vector<Digest>& keys);
+    // Eval.lookup's assoc step for many nodes (eval.go:1172-1258): per node,
+    // the index of its first cache key with a value (-1: none) and the value;
+    // repair 0 none, 1 blind (the reference), 2 precise (missing keys only)
+    std::vector<std::pair<int, Digest>> Lookup(AssocKind kind, const std::vector<std::vector<Digest>>& node_keys,
+                                               int repair);
 
    private:
     rf_assoc* a_ = nullptr;

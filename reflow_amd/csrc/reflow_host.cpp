@@ -630,6 +630,28 @@ void Assoc::Put(AssocKind kind, const Digest& expect, const Digest& k, const Dig
         throw Error(RF_EPRECONDITION, "expected value " + expect.String() + ", have a different value");
 }
 
+std::vector<std::pair<int, Digest>> Assoc::Lookup(AssocKind kind, const std::vector<std::vector<Digest>>& node_keys,
+                                                  int repair) {
+    std::vector<uint64_t> ptr{0};
+    std::vector<uint8_t> flat;
+    for (const auto& ks : node_keys) {
+        for (const Digest& k : ks) flat.insert(flat.end(), k.b.begin(), k.b.end());
+        ptr.push_back(ptr.back() + ks.size());
+    }
+    const size_t n = node_keys.size();
+    std::vector<int32_t> which(n);
+    std::vector<uint8_t> vals(32 * n);
+    std::vector<std::pair<int, Digest>> out(n);
+    if (!n) return out;
+    Check(rf_assoc_lookup(a_, (int)kind, flat.empty() ? nullptr : flat.data(), ptr.data(), n, repair, which.data(),
+                          vals.data()));
+    for (size_t i = 0; i < n; ++i) {
+        out[i].first = which[i];
+        memcpy(out[i].second.b.data(), vals.data() + 32 * i, 32);
+    }
+    return out;
+}
+
 std::vector<std::optional<Digest>> Assoc::GetBatch(AssocKind kind, const std::vector<Digest>& keys) {
     std::vector<Digest> vals(keys.size());
     std::vector<uint8_t> found(keys.size());

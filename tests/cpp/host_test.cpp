@@ -232,6 +232,14 @@ static void TestAssoc(Engine& e) {
     auto st = a.PutBatch(AssocFileset, {Digest{}, v1, v2}, {k1, k1, k1}, {v1, v2, v1});
     EXPECT(st[0] == RF_OK && st[1] == RF_OK && st[2] == RF_OK && a.Get(AssocFileset, k1).second == v1,
            "batch order");
+    // Eval.lookup (eval.go:1202-1258): physical key absent, logical present ->
+    // which = 1; precise read repair fills the physical key
+    Digester dg(e);
+    const Digest phys = dg.FromString("physical"), logi = dg.FromString("logical");
+    a.Put(AssocFileset, Digest{}, logi, v2);
+    auto lk = a.Lookup(AssocFileset, {{phys, logi}, {}}, 2);
+    EXPECT(lk[0].first == 1 && lk[0].second == v2 && lk[1].first == -1, "lookup first hit");
+    EXPECT(a.Get(AssocFileset, phys).second == v2, "precise read repair");
 }
 
 // Executor.install (local/executor.go:514-557): the executor_test.go:86-88
