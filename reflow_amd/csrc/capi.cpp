@@ -1390,9 +1390,24 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         cons_job[2 * c + 1] = level[cjob[c]];
     }
     gr->hole_count = H;
+    // 1: the level has queueable jobs (k2_level_pc<2>); 2: they average at
+    // least RF_K2_WIDE blocks (default 8; 0 = never), so the producer's
+    // assembly + expansion outlasts the chain's rounds (k2_level_pc<3>)
     gr->g.inc_level.assign(L, 0);
-    for (uint32_t j = 0; j < J; ++j)
-        if (!fused_target[j]) gr->g.inc_level[level[j]] = 1;
+    {
+        static const uint64_t wide = [] {
+            const char* v = getenv("RF_K2_WIDE");
+            return v ? (uint64_t)strtoull(v, nullptr, 10) : 8ull;
+        }();
+        std::vector<uint64_t> qj(L, 0), qb(L, 0);
+        for (uint32_t j = 0; j < J; ++j)
+            if (!fused_target[j]) {
+                qj[level[j]] += 1;
+                qb[level[j]] += nblk[j];
+            }
+        for (uint32_t l = 0; l < L; ++l)
+            if (qj[l]) gr->g.inc_level[l] = (wide && qb[l] >= wide * qj[l]) ? 2 : 1;
+    }
     gr->tmpl_bytes = tb;
     // upload
     GraphDev& G = gr->g;

@@ -351,16 +351,27 @@ constexpr uint32_t kPcRow = 68;  // words per K+W row: 16-B reads of 64 rows hit
 // producer's new digest reaches the fused job's material through LDS.
 #define RF_STAMP(k)                                                                        \
     do {                                                                                   \
-        if (a.stamps && blockIdx.x == 0 && lane == 0 && (k) < 64)                          \
+        if (a.stamps && blockIdx.x == 0 && lane == 0 && wave < 2 && (k) < 64)             \
             a.stamps[128 * a.lvl + 64 * wave + (k)] = __builtin_amdgcn_s_memrealtime();    \
     } while (0)
 
-__global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
+// kW = 2: chain + producer.  kW = 3 (levels of long jobs, e.g. the
+// per-sample OpK with 18 blocks, where the producer's ~2.4 us per block
+// exceeded the chain's ~1.9 us): the producer only assembles each block and
+// hands its 16 big-endian words through LDS (wbuf) to an expander wave, which
+// writes the K+W row a block later; the chain lags two blocks.
+constexpr uint32_t kWRow = 20;  // words per assembled-block row: 16-B accesses of 16 lanes hit distinct banks
+
+template <uint32_t kW>
+__global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
+    static_assert(kW == 2 || kW == 3, "chain + producer (+ expander)");
+    constexpr uint32_t lag = kW - 1;  // iterations between a block's assembly and its rounds
     __shared__ __attribute__((aligned(16))) uint32_t kw[2 * 64 * kPcRow];
+    __shared__ __attribute__((aligned(16))) uint32_t wbuf[kW == 3 ? 2 * 64 * kWRow : 4];
     __shared__ uint32_t ring_all[64 * kRing];
     __shared__ uint4 s_dig[64][2];   // the last job's new digest (raw words)
     __shared__ uint32_t s_next[64];  // the lane's next (fused) job, or ~0
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 chain, 1 producer
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 chain, 1 producer, 2 expander
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* ring = &ring_all[lane * kRing];
     const uint32_t n = a.counts[a.lvl];
@@ -436,12 +447,19 @@ __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
                     if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
                 }
             }
-            for (uint32_t it = 0; it <= maxnb; ++it) {
+            for (uint32_t it = 0; it < maxnb + lag; ++it) {
                 if (wave == 1) {
                     if (it < m0.y) {  // block it of this lane's job -> buffer it & 1
                         uint32_t w[16];
                         cur.block(a, it, ring, w);
-                        kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
+                        if (kW == 2) {
+                            kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
+                        } else {
+                            uint4* row = reinterpret_cast<uint4*>(&wbuf[((it & 1) * 64 + lane) * kWRow]);
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                row[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+                        }
                     }
                     if (it == 0 && nfu) {
                         const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
@@ -451,45 +469,64 @@ __global__ __launch_bounds__(128) void k2_level_pc(LevelArgs a) {
                         }
                         nr = a.holes[nm0.z];
                     }
-                } else if (it >= 1 && it - 1 < m0.y) {  // block it-1 from buffer (it-1) & 1
-                    compress_kw(st, reinterpret_cast<const uint4*>(&kw[(((it - 1) & 1) * 64 + lane) * kPcRow]));
+                } else if (kW == 3 && wave == 2) {
+                    if (it >= 1 && it - 1 < m0.y) {  // expand block it-1: wbuf -> kw, buffer (it-1) & 1
+                        const uint32_t bb = (it - 1) & 1;
+                        const uint4* row = reinterpret_cast<const uint4*>(&wbuf[(bb * 64 + lane) * kWRow]);
+                        uint32_t w[16];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint4 v = row[q];
+                            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+                        }
+                        kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(bb * 64 + lane) * kPcRow]));
+                    }
+                } else if (wave == 0 && it >= lag && it - lag < m0.y) {  // block it-lag from buffer (it-lag) & 1
+                    compress_kw(st, reinterpret_cast<const uint4*>(&kw[(((it - lag) & 1) * 64 + lane) * kPcRow]));
                 }
                 lds_barrier();
                 RF_STAMP(sk); ++sk;
             }
+            // Hand-over first, frontier second: the chain wave stores the digest
+            // and passes a fused target's digest through s_dig / s_next, then
+            // runs the frontier atomics (each a returning HBM round trip) while
+            // the producer already assembles and expands the target's block 0.
+            // No second barrier: s_next / s_dig are rewritten only at the next
+            // job's finish, after the block loop's barriers, and the producer
+            // reads them before its first one.
+            bool changed = false;
             if (wave == 0) {
-                uint32_t cb = 0, ce = 0, next = ~0u;
+                uint32_t next = ~0u;
                 if (has) {
-                    const bool changed = finish_job_pre(a, m1, st, olo, ohi);
-                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
-                    cb = m1.y;
-                    ce = m1.y;
-                    if (changed) {
-                        // the fusion target's edge is the last of the range
-                        const bool fuse = m1.w != ~0u;
-                        ce = fuse ? m1.z - 1 : m1.z;
-                        if (fuse) {
-                            next = m1.w;
-                            s_dig[lane][0] = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
-                                                        bswap32(st.h[3]));
-                            s_dig[lane][1] = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]),
-                                                        bswap32(st.h[7]));
-                        }
+                    changed = finish_job_pre(a, m1, st, olo, ohi);
+                    if (changed && m1.w != ~0u) {
+                        next = m1.w;
+                        s_dig[lane][0] = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
+                                                    bswap32(st.h[3]));
+                        s_dig[lane][1] = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]),
+                                                    bswap32(st.h[7]));
                     }
                 }
-                propagate_pre(a, cb, ce, pre);
                 s_next[lane] = next;
-                const uint64_t fb = __ballot(next != ~0u);
-                if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));  // fused jobs hashed
             }
-            const uint32_t out_slot = m1.x;
             RF_STAMP(sk); ++sk;
             lds_barrier();
             const uint32_t nx = s_next[lane];
-            fslot = has ? out_slot : ~0u;
+            if (wave == 0) {
+                uint32_t cb = 0, ce = 0;
+                if (has) {
+                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                    cb = m1.y;
+                    // the fusion target's edge is the last of the range
+                    ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
+                }
+                propagate_pre(a, cb, ce, pre);
+                const uint64_t fb = __ballot(nx != ~0u);
+                if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));  // fused jobs hashed
+            }
+            fslot = has ? m1.x : ~0u;
             has = nx != ~0u;
             p = has ? nx : 0u;
-            lds_barrier();  // s_next / s_dig are rewritten by the next job's finish
         }
     }
 }
@@ -584,9 +621,12 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }();
     if (!full) {
         if (!g.inc_level[lvl]) return hipSuccess;  // every job of the level is a fusion target
-        uint64_t g = (e - b + 63) / 64;
-        if (g > 2048) g = 2048;
-        hipLaunchKernelGGL(k2_level_pc, dim3((uint32_t)g), dim3(128), 0, s, a);
+        uint64_t wg = (e - b + 63) / 64;
+        if (wg > 2048) wg = 2048;
+        if (g.inc_level[lvl] == 2)
+            hipLaunchKernelGGL(k2_level_pc<3>, dim3((uint32_t)wg), dim3(192), 0, s, a);
+        else
+            hipLaunchKernelGGL(k2_level_pc<2>, dim3((uint32_t)wg), dim3(128), 0, s, a);
         return hipGetLastError();
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
