@@ -385,7 +385,9 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
         // the fusion target's meta, first template blocks, hole record (producer)
         // and old digest + first reverse edges (chain), prefetched while its
         // producer is hashed: a fused job starts without a dependent HBM chain
-        uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0;
+        // nnm: the target's own fusion target's meta, fetched a job ahead, so a
+        // fused job's successor record never costs an HBM round trip on its block 0
+        uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
         uint4 nt[8];
         uint2 nr = make_uint2(0, 0);
         uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
@@ -398,13 +400,15 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
                 if (fused) {
                     m0 = nm0;
                     m1 = nm1;
+                    nm0 = nnm0;  // = meta[m1.w], valid when m1.w != ~0
+                    nm1 = nnm1;
                 } else {
                     m0 = a.meta[2 * p];
                     m1 = a.meta[2 * p + 1];
                 }
             }
             const bool nfu = has && m1.w != ~0u;
-            if (nfu) {
+            if (nfu && !fused) {
                 nm0 = a.meta[2ull * m1.w];
                 nm1 = a.meta[2ull * m1.w + 1];
             }
@@ -445,7 +449,15 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
                     nohi = od[1];
                     if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
                     if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
+                    if (nm1.w != ~0u) {
+                        nnm0 = a.meta[2ull * nm1.w];
+                        nnm1 = a.meta[2ull * nm1.w + 1];
+                    }
                 }
+            }
+            if (kW == 3 && wave == 2 && nfu && nm1.w != ~0u) {  // the expander needs m0.y of every job too
+                nnm0 = a.meta[2ull * nm1.w];
+                nnm1 = a.meta[2ull * nm1.w + 1];
             }
             for (uint32_t it = 0; it < maxnb + lag; ++it) {
                 if (wave == 1) {
@@ -468,6 +480,10 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
                             nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
                         }
                         nr = a.holes[nm0.z];
+                        if (nm1.w != ~0u) {
+                            nnm0 = a.meta[2ull * nm1.w];
+                            nnm1 = a.meta[2ull * nm1.w + 1];
+                        }
                     }
                 } else if (kW == 3 && wave == 2) {
                     if (it >= 1 && it - 1 < m0.y) {  // expand block it-1: wbuf -> kw, buffer (it-1) & 1
