@@ -1433,6 +1433,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         (e = up(gr->b_lvl_start, G.lvl_start.data(), 4ull * (L + 1))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
                     hipGetErrorString(e));
+    HIPC(gr->b_holes.ensure(8));  // k2's record loads read element 0 unconditionally
     HIPC(hipMemset(gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
     HIPC(hipMemset(gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
     HIPC(hipMemset(gr->b_counts.p, 0, 4ull * (L + 1)));

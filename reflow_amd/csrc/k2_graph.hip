@@ -139,8 +139,12 @@ struct MatCursor {
     uint32_t fslot = ~0u;  // a slot whose new digest is handed over in registers (fused chains)
     uint4 flo, fhi;
 
+    // unconditional load (index 0 past the job's holes; the hole array always
+    // has an element), so independent record loads issue back to back with no
+    // branch forcing a wait between them
     __device__ __forceinline__ uint2 record(const LevelArgs& a, uint32_t h) const {
-        return h < he ? a.holes[h] : make_uint2(~0u, 0u);
+        const uint2 v = a.holes[h < he ? h : 0u];
+        return h < he ? v : make_uint2(~0u, 0u);
     }
     __device__ __forceinline__ void digest(const LevelArgs& a, PendingHole& q, const uint2& r) const {
         q.r = r;
@@ -159,13 +163,16 @@ struct MatCursor {
         nb = m0.y;
         he = m0.w;
         hn = m0.z;  // first hole not yet applied
-        digest(a, q0, record(a, hn));
-        digest(a, q1, record(a, hn + 1));
-        digest(a, q2, record(a, hn + 2));
-        digest(a, q3, record(a, hn + 3));
+        // all six records first, then the four digest loads: one HBM round
+        // trip each way instead of four dependent record -> digest pairs
+        const uint2 r0 = record(a, hn), r1 = record(a, hn + 1), r2 = record(a, hn + 2), r3 = record(a, hn + 3);
         r4 = record(a, hn + 4);
         r5 = record(a, hn + 5);
         t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
+        digest(a, q0, r0);
+        digest(a, q1, r1);
+        digest(a, q2, r2);
+        digest(a, q3, r3);
         ring_put(ring, 0, t);
         if (nb > 1) {
             t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
