@@ -4,23 +4,30 @@
     python bench.py --gpus N --steps K --warmup W
 
 Primary line (value): SHA-256 digest GB/s of configs[1], the 64 GiB
-FASTQ/BAM-like skewed Fileset (4 KiB-2 GiB files), HBM-resident, on each GPU
-(weak scaling: every rank digests its own 64 GiB set).  A step = one
-rf_sha_plan_run over the whole set (all File IDs of the Fileset).
+FASTQ/BAM-like skewed Fileset (4 KiB-2 GiB files), HBM-resident, per GPU.
+A step = one rf_sha_plan_run over the whole set: every File ID, by the K1
+planner's legs -- the longest chains on the host leg (SHA-NI threads fed by
+chunked D2H; the reference's <=60-goroutine digest pool), the rest on the GPU
+kernels (duo / octo / pair / lanes), split by a makespan model.  With N ranks
+the global Fileset is N configs[1]-distributed sets (seeds 0x5EED0004+g),
+sharded LPT by size over the ranks (weak scaling: 64 GiB per GPU; N = 8 is
+configs[3]'s 512 GiB).
 
 Secondary, in the same JSON line:
-  "incremental"  configs[2]: 10M-node 1000align DAG, 1% of leaf File IDs
-                 changed per step -> K3 frontier + K2 recompute (Mnodes/s of
-                 dirty nodes, and effective graph nodes/s); RCCL all-gather of
-                 the per-rank root digests when N > 1.
-  "probe"        configs[4]: 1e9 bloomlive probes against a 1e8-key filter.
-  "cpu_baseline" the oracle's C port on the host cores (rank 0, N=1).
-
-The only process-wide runtime is the engine's own (libreflow_hip.so); torch is
-used only for torch.distributed (gloo, CPU) to bootstrap RCCL and to take the
-max over ranks.
+  "roofline"          the dominant GPU kernel of the hybrid run vs the
+                      skew-aware floor; "roofline_gpu_only": k1_sha256_duo on
+                      the GPU-only plan (one run); "host_leg": the SHA-NI leg
+  "c1"                configs[0] (the reference's CPU case) on the GPU
+  "incremental"       configs[2]: 10M-node 1000align DAG, 1% of leaf File
+                      IDs changed per step (K3 frontier + K2), dirty blocks
+  "probe"             configs[4]: 1e9 probes against the 1e8-key filter
+                      (171 MiB, MALL-resident) and a 1.2e9-key one (2 GiB)
+  "cpu_baseline"      host-core legs on the GPU box (rank 0, N = 1)
+A --budget-s guard skips optional sections (recorded as skipped) so the run
+ends in time even on a slow box; the JSON line is printed last.
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -44,32 +51,50 @@ SHA_VALU_PEAK_GBS = VALU_LANE_OPS / SHA_OPS_PER_BLOCK * 64 / 1e9
 # A message's blocks are a serial chain (Merkle-Damgard).  One round's critical
 # path is 3 dependent VALU ops (rotate -> xor3 -> add3 into e/a); the
 # dependent-issue latency of one wave is 4 cycles (MI355X_MICROARCH.md,
-# "Dependent-chain latency"; tools/micro.py lat: 4-5).  So no implementation
-# can finish a message of B blocks in less than B * 64 * 3 * 4 cycles.
+# "Dependent-chain latency"; tools/micro.py lat: 4-5).  So no GPU
+# implementation can finish a message of B blocks in less than B*64*3*4 cycles.
 CHAIN_CYCLES_PER_BLOCK = 64 * 3 * 4
 HBM_PEAK_GBS = 8000.0
+T_START = time.perf_counter()
 
 
 def log(*a):
-    print("[bench]", *a, file=sys.stderr, flush=True)
+    print("[bench %6.1fs]" % (time.perf_counter() - T_START), *a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
-    --pmc FETCH_SIZE/WRITE_SIZE summary (tools/pmc_summary.py, corrected as
-    MI355X_MICROARCH.md prescribes), or None.  The PMC passes run the same
-    default workloads as this script."""
+class Budget:
+    """Skips optional sections whose estimated cost would overrun --budget-s
+    (the driver kills a bench at its own limit, and a killed run prints
+    nothing)."""
+
+    def __init__(self, seconds):
+        self.seconds = seconds
+        self.skipped = []
+
+    def allow(self, name, est_s):
+        left = self.seconds - (time.perf_counter() - T_START)
+        if est_s > left:
+            self.skipped.append({"section": name, "estimate_s": est_s, "left_s": round(left, 1)})
+            log("SKIP %s: estimated %.0f s, %.0f s left in the budget" % (name, est_s, left))
+            return False
+        return True
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 --pmc
+    FETCH_SIZE/WRITE_SIZE pass (tools/pmc_summary.py, corrected as
+    MI355X_MICROARCH.md prescribes) -- only when that pass ran this same
+    workload (its "workload" key); None otherwise.  PMC counters cannot be read
+    inside this process."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
-    if not paths:
-        return None, None
-    d = json.load(open(paths[-1]))
-    v = d.get("rf::" + kernel)
-    if not v:
-        return None, None
-    # the bench prices the kernel's largest launch (the mean over dispatches
-    # would mix in small launches of other workloads)
-    return v.get("traffic_bytes_largest_launch", v["traffic_bytes_per_launch"]), os.path.relpath(paths[-1], ROOT)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        d = json.load(open(path))
+        if d.get("workload") != workload:
+            continue
+        v = d.get("rf::" + kernel)
+        if v:
+            return v.get("traffic_bytes_largest_launch", v["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
 class Dist:
@@ -77,7 +102,6 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -100,21 +124,19 @@ class Dist:
         if self.world > 1:
             self.dist.barrier()
 
-    def max(self, x):
+    def _reduce(self, x, op):
         if self.world == 1:
             return x
         import torch
         t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
 
+    def max(self, x):
+        return x if self.world == 1 else self._reduce(x, self.dist.ReduceOp.MAX)
+
     def sum(self, x):
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return x if self.world == 1 else self._reduce(x, self.dist.ReduceOp.SUM)
 
     def bcast_bytes(self, b):
         if self.world == 1:
@@ -140,10 +162,8 @@ def timed_steps(dist, ctx, fn, steps, warmup):
     dist.barrier()
     ctx.sync()
     t0 = time.perf_counter()
-    for i in range(steps):
+    for _ in range(steps):
         fn()
-        if steps > 2:
-            pass
     ctx.sync()
     dist.barrier()
     t1 = time.perf_counter()
@@ -151,10 +171,57 @@ def timed_steps(dist, ctx, fn, steps, warmup):
 
 
 # ---------------------------------------------------------------- C2: SHA --
-def bench_sha(args, dist, ctx):
-    seed = 0x5EED0002 if dist.world == 1 else 0x5EED0004 + dist.rank
+def shard_lpt(sizes, world):
+    """LPT by size: files largest first, each to the least-loaded rank.
+    Returns the owner rank of every file."""
+    order = np.argsort(-sizes.astype(np.int64), kind="stable")
+    load = np.zeros(world, dtype=np.float64)
+    owner = np.zeros(len(sizes), dtype=np.int64)
+    for i in order:
+        r = int(np.argmin(load))
+        owner[i] = r
+        load[r] += float(sizes[i])
+    return owner
+
+
+def rank_sizes(args, dist):
+    """This rank's files.  N = 1: configs[1] itself.  N > 1: the global Fileset
+    of N configs[1]-distributed sets (seeds 0x5EED0004 + g), LPT-sharded."""
     total = int(args.sha_gib * GiB)
-    lens = c2_sizes(total_bytes=total, seed=seed)
+    if dist.world == 1:
+        return c2_sizes(total_bytes=total, seed=0x5EED0002), 0x5EED0002, None
+    sets = [c2_sizes(total_bytes=total, seed=0x5EED0004 + g) for g in range(dist.world)]
+    allsz = np.concatenate(sets)
+    owner = shard_lpt(allsz, dist.world)
+    mine = allsz[owner == dist.rank]
+    glob_info = {"files": int(len(allsz)), "bytes": int(allsz.sum()),
+                 "rank_bytes_max_over_min": float(np.bincount(owner, weights=allsz.astype(np.float64)).max()
+                                                  / max(np.bincount(owner, weights=allsz.astype(np.float64)).min(), 1))}
+    return mine, 0x5EED0004 + 0x100 * dist.rank, glob_info
+
+
+def kernel_roofline(name, lens, ids, ms):
+    """achieved = the kernel's file bytes / its HIP-event time; peak = the
+    skew-aware floor of its message set (the longest chain's critical path,
+    or the chip's VALU throughput)."""
+    nblk = (lens.astype(np.int64) + 9 + 63) // 64
+    b = float(lens[ids].sum())
+    t_chain = float(nblk[ids].max()) * CHAIN_CYCLES_PER_BLOCK / CLOCK_HZ
+    t_valu = float(nblk[ids].sum()) * SHA_OPS_PER_BLOCK / VALU_LANE_OPS
+    t_floor = max(t_chain, t_valu)
+    ach = b / (ms * 1e-3) / 1e9
+    peak = b / t_floor / 1e9
+    return {"bound": "valu", "kernel": name, "achieved": round(ach, 3), "peak": round(peak, 3), "unit": "GB/s",
+            "frac": round(ach / peak, 4),
+            "peak_kind": "skew-aware floor: max(longest message's blocks x 64 rounds x 3 dependent VALU x 4 cyc "
+                         "@2.4GHz, sum blocks x 1464 ops / INT32 VALU peak)",
+            "floor_s": round(t_floor, 4), "chain_floor_s": round(t_chain, 4),
+            "frac_of_valu_peak": round(ach / SHA_VALU_PEAK_GBS, 6), "launch_ms": round(ms, 3),
+            "bytes_per_launch": b, "messages": int(len(ids)), "critical_chain_blocks": int(nblk[ids].max())}
+
+
+def bench_sha(args, dist, ctx, budget):
+    lens, seed, glob_info = rank_sizes(args, dist)
     offs, arena_bytes = arena_layout(lens)
     arena = ctx.alloc(arena_bytes)
     d_offs, d_lens = ctx.upload(offs), ctx.upload(lens)
@@ -163,61 +230,90 @@ def bench_sha(args, dist, ctx):
     ctx.sync()
     plan = ctx.sha_plan(offs, lens, 0)
     st = plan.stats()
-    log("C2: %d files, %.1f GiB, %d wave-per-message, max file %.2f GiB"
-        % (len(lens), lens.sum() / GiB, st.n_solo, lens.max() / GiB))
-    solo_ms, lanes_ms = [], []
+    log("C2: %d files, %.1f GiB, largest %.2f GiB: %d on the host leg (%.1f GiB, %d threads), %d duo, %d lane"
+        % (len(lens), lens.sum() / GiB, lens.max() / GiB, st.n_host, st.host_bytes / GiB, st.host_threads,
+           st.n_solo, len(lens) - st.n_host - st.n_solo))
+    rec = {"solo": [], "lanes": [], "host": [], "total": []}
 
     def step():
         plan.run(arena.ptr, out.ptr)
-        s = plan.stats()  # synchronises: per-kernel HIP-event times of this run
-        solo_ms.append(s.last_ms_solo)
-        lanes_ms.append(s.last_ms_lanes)
-        log("  sha step: total %.1f ms (solo %.1f, lanes %.1f)" % (s.last_ms_total, s.last_ms_solo,
-                                                                    s.last_ms_lanes))
+        s = plan.stats()  # synchronises: per-leg times of this run
+        rec["solo"].append(s.last_ms_solo)
+        rec["lanes"].append(s.last_ms_lanes)
+        rec["host"].append(s.last_ms_host)
+        rec["total"].append(s.last_ms_total)
 
     t = timed_steps(dist, ctx, step, args.steps, args.warmup)
-    solo_ms, lanes_ms = solo_ms[args.warmup:], lanes_ms[args.warmup:]
+    for k in rec:
+        rec[k] = rec[k][args.warmup:]
+    log("  hybrid: %.1f ms/step (host leg %.1f ms, duo %.1f ms, lanes %.1f ms)"
+        % (t / args.steps * 1e3, np.mean(rec["host"]), np.mean(rec["solo"]), np.mean(rec["lanes"])))
     bytes_all = dist.sum(float(lens.sum())) * args.steps
-    gbs = bytes_all / t / 1e9
-    # roofline of the dominant kernel (the longer of solo / lanes)
-    order = np.argsort(-lens.astype(np.int64), kind="stable")
-    solo_ids = order[:st.n_solo]
-    lane_ids = order[st.n_solo:]
     nblk = (lens.astype(np.int64) + 9 + 63) // 64
-    # dominant kernel: the one that holds the largest message (its chain is the
-    # critical path); wave-per-message runs k1_sha256_duo by default
-    wave_mode = st.n_solo > 0
-    dom = "k1_sha256_duo" if wave_mode else "k1_sha256_lanes"
-    ids = solo_ids if wave_mode else lane_ids
-    dom_ms = float(np.mean(solo_ms if wave_mode else lanes_ms))
-    dom_bytes = float(lens[ids].sum())
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    # skew-aware floor: the longest serial chain (critical-path latency) vs
-    # chip VALU throughput
-    t_chain = float(nblk[ids].max()) * CHAIN_CYCLES_PER_BLOCK / CLOCK_HZ
-    t_valu = float(nblk[ids].sum()) * SHA_OPS_PER_BLOCK / VALU_LANE_OPS
-    t_floor = max(t_chain, t_valu)
-    peak = dom_bytes / t_floor / 1e9
-    traffic, tsrc = pmc_traffic(dom)
-    roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
-            "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-            "traffic_source": tsrc, "traffic_over_algorithmic": (round(traffic / dom_bytes, 3)
-                                                                 if traffic else None),
-            "peak_kind": "skew-aware floor: max(longest message's blocks x 64 rounds x 3 dependent VALU"
-                         " x 4 cyc @2.4GHz (round critical path), sum blocks x 1464 ops / INT32 VALU peak)",
-            "floor_s": round(t_floor, 3), "chain_floor_s": round(t_chain, 3),
-            "valu_peak_GBps": round(SHA_VALU_PEAK_GBS, 1),
-            "frac_of_valu_peak": round(achieved / SHA_VALU_PEAK_GBS, 6),
-            "launch_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes,
-            "critical_chain_blocks": int(nblk[ids].max())}
-    res = dict(value=gbs, ms_per_step=t / args.steps * 1e3, roofline=roof,
-               files=int(len(lens)), bytes_per_gpu=int(lens.sum()), n_solo=int(st.n_solo),
-               lanes_ms=float(np.mean(lanes_ms)) if lanes_ms else 0.0)
-    # keep digests of a host-checkable sample for the cpu_baseline cross-check
+    order = np.argsort(-nblk, kind="stable")
+    h, k = int(st.n_host), int(st.n_solo)
+    host_ids, solo_ids, lane_ids = order[:h], order[h:h + k], order[h + k:]
+    legs = []
+    if k:
+        legs.append(("k1_sha256_duo", solo_ids, float(np.mean(rec["solo"]))))
+    if len(lane_ids):
+        n_simd = 4 * N_CU
+        lk = "k1_sha256_octo" if len(lane_ids) <= 4 * n_simd else "k1_sha256_pair" if len(lane_ids) <= 16 * n_simd \
+            else "k1_sha256_lanes"
+        legs.append((lk, lane_ids, float(np.mean(rec["lanes"]))))
+    dom = max(legs, key=lambda x: x[2]) if legs else None
+    roof = kernel_roofline(*dom) if dom else None
+    workload = ("configs[1]: %.1f GiB Fileset per GPU, %d files 4 KiB-2 GiB (98%% log-uniform 4 KiB-1 MiB, "
+                "2%% 64 MiB-2 GiB), SHA-256 of every file" % (lens.sum() / GiB, len(lens)))
+    if roof:
+        traffic, tsrc = pmc_traffic(roof["kernel"], workload)
+        roof["traffic"] = traffic
+        roof["traffic_source"] = tsrc or "not measured in this process (rocprofv3 --pmc needs its own pass)"
+        roof["legs"] = {name: {"ms": round(ms, 3), "messages": int(len(ids)), "bytes": float(lens[ids].sum())}
+                        for name, ids, ms in legs}
+    hb = float(lens[host_ids].sum()) if h else 0.0
+    host_ms = float(np.mean(rec["host"])) if h else 0.0
+    thr, core_rate, sha_ext = ctx.host_info()
+    host_leg = None
+    if h:
+        per_thread = hb / (host_ms * 1e-3) / st.host_threads / 1e9
+        host_leg = {"threads": int(st.host_threads), "files": h, "bytes": hb, "ms": round(host_ms, 2),
+                    "gbps": round(hb / (host_ms * 1e-3) / 1e9, 3), "per_thread_gbps": round(per_thread, 3),
+                    "core_sha_ni_gbps": round(core_rate / 1e9, 3),
+                    "frac_of_core_rate": round(per_thread / (core_rate / 1e9), 3) if core_rate else None,
+                    "largest_file_gib": round(float(lens[host_ids].max()) / GiB, 3),
+                    "feed": "D2H in 8 MiB chunks per thread, double-buffered (PCIe), from the HBM-resident set",
+                    "why": "one file is one serial chain: a SHA-NI core runs it ~40x faster than a GPU wave"}
+    res = dict(value=bytes_all / t / 1e9, ms_per_step=t / args.steps * 1e3, roofline=roof, host_leg=host_leg,
+               files=int(len(lens)), bytes_per_gpu=int(lens.sum()), workload=workload, glob=glob_info,
+               split={"host": h, "duo": k, "lanes": int(len(lane_ids))},
+               step_ms={kk: round(float(np.mean(v)), 3) for kk, v in rec.items()})
+    # GPU-only plan (no host leg), one run: the duo chain's roofline on the
+    # same set (the chain-bound floor the host leg exists for)
+    if args.gpu_only_run and budget.allow("gpu_only_duo", 45):
+        p2 = ctx.sha_plan(offs, lens, capi.RF_SHA_NO_HOST)
+        out2 = ctx.alloc(32 * len(lens))
+        t0 = time.perf_counter()
+        p2.run(arena.ptr, out2.ptr)
+        s2 = p2.stats()
+        wall = time.perf_counter() - t0
+        o2 = np.argsort(-nblk, kind="stable")
+        duo_ids = o2[:int(s2.n_solo)]
+        r2 = kernel_roofline("k1_sha256_duo", lens, duo_ids, s2.last_ms_solo) if s2.n_solo else None
+        if r2:
+            tr2, ts2 = pmc_traffic("k1_sha256_duo", workload)
+            r2["traffic"], r2["traffic_source"] = tr2, ts2 or "not measured in this process"
+        same = bool((out2.to_numpy() == out.to_numpy()).all())
+        res["roofline_gpu_only"] = r2
+        res["gpu_only"] = {"gbps": float(lens.sum()) / wall / 1e9, "ms": wall * 1e3, "duo_files": int(s2.n_solo),
+                           "digests_equal_hybrid": same}
+        log("  GPU-only plan: %.1f s (duo %.1f s), digests equal: %s" % (wall, s2.last_ms_solo / 1e3, same))
+        p2.close()
+        out2.free()
     res["_digests"] = out.to_numpy().reshape(-1, 32)
-    res["_lens"], res["_seed"] = lens, seed
+    res["_lens"], res["_seed"], res["_arena"], res["_offs"] = lens, seed, arena, offs
     plan.close()
-    for b in (arena, d_offs, d_lens, out):
+    for b in (d_offs, d_lens, out):
         b.free()
     return res
 
@@ -230,12 +326,13 @@ def c1_path(i):
     return ("d%02d/f%04d.fq.gz" % (i // 64, i)).encode()
 
 
-def bench_c1(args, dist, ctx):
-    """configs[0], the reference's own CPU-runnable case, on the GPU: digest
-    1 GiB = 4096 x 256 KiB files (HBM-resident, File IDs on K1), the Fileset
-    digest of the 4096-entry map (executor.go:205-233; host material + K1,
-    File IDs read back), and CacheKeys of a ~10k-node 1000align DAG (K2 full
-    recompute).  Checked against the committed fixture tests/golden/c1_fileset.json."""
+def bench_c1(args, dist, ctx, budget):
+    """configs[0], the reference's own CPU-runnable case, on the GPU: File IDs
+    of 1 GiB = 4096 x 256 KiB files (HBM-resident, GPU kernels: octo chains),
+    the Fileset digest of the 4096-entry map (executor.go:205-233: one 3137-
+    block material, IDs placed from HBM; the planner gives the one long chain
+    to the host leg), and CacheKeys of a ~10k-node 1000align DAG (K2 full
+    recompute).  Checked against tests/golden/c1_fileset.json."""
     lens = np.full(C1_N, C1_LEN, dtype=np.uint64)
     offs, arena_bytes = arena_layout(lens)
     arena = ctx.alloc(arena_bytes)
@@ -244,6 +341,7 @@ def bench_c1(args, dist, ctx):
     ctx.gen_fill(arena.ptr, d_offs.ptr, d_lens.ptr, C1_N, C1_SEED, arena_bytes)
     ctx.sync()
     plan = ctx.sha_plan(offs, lens, 0)
+    st = plan.stats()
     plan.run(arena.ptr, out.ptr)
     ctx.sync()
     reps = 5
@@ -252,33 +350,22 @@ def bench_c1(args, dist, ctx):
         plan.run(arena.ptr, out.ptr)
     ctx.sync()
     ids_ms = (time.perf_counter() - t0) / reps * 1e3
-    # Fileset digest over the IDs where K1 left them (rf_fileset_digest_device:
-    # path material from the host, IDs placed on the device); the paths are
-    # marshalled once, outside the timed region
     fp = ctx.fileset_paths([[[c1_path(i) for i in range(C1_N)]]])
     fp.digest_device(out.ptr)
     t0 = time.perf_counter()
     for _ in range(reps):
         fsd = fp.digest_device(out.ptr)[0]
     fs_ms = (time.perf_counter() - t0) / reps * 1e3
-    # the host-ID form (IDs read back, rf_fileset_digest_batch), for comparison
-    t0 = time.perf_counter()
     ids = out.to_numpy().reshape(-1, 32)
-    d2h_ms = (time.perf_counter() - t0) * 1e3
-    group = [[[(c1_path(i), ids[i].tobytes()) for i in range(C1_N)]]]  # harness-side argument building
-    ctx.fileset_digest_batch(group)
-    t0 = time.perf_counter()
-    fsd_host = ctx.fileset_digest_batch(group)[0]
-    fs_host_ms = (time.perf_counter() - t0) * 1e3 + d2h_ms
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "c1_fileset.json")))
-    ok = ("sha256:" + fsd.hex() == want["fileset_digest"] and fsd_host == fsd and
-          __import__("hashlib").sha256(ids.tobytes()).hexdigest() == want["ids_sha256"])
-    inst = (bench_c1_install(ctx, arena, offs, fsd, cpu_leg=dist.world == 1 and "cpu" not in args.skip)
-            if "install" not in args.skip and dist.rank == 0 else None)
+    ok = ("sha256:" + fsd.hex() == want["fileset_digest"] and
+          hashlib.sha256(ids.tobytes()).hexdigest() == want["ids_sha256"])
+    inst = None
+    if "install" not in args.skip and dist.rank == 0 and budget.allow("c1_install", 20):
+        inst = bench_c1_install(ctx, arena, offs, fsd, cpu_leg=dist.world == 1 and "cpu" not in args.skip)
     plan.close()
     for b in (arena, d_offs, d_lens, out):
         b.free()
-    # CacheKeys over a ~10k-node DAG (S*(14P+5) nodes at P=32)
     small = Dag1000(22, 32)
     a = small.arrays()
     g = capi.Graph(ctx, a["n_slots"], a["out_slot"], a["tmpl_off"], a["tmpl_len"], a["hole_ptr"],
@@ -293,15 +380,11 @@ def bench_c1(args, dist, ctx):
     return {"workload": "configs[0]: 4096 x 256 KiB files (1 GiB) -> File IDs + Fileset digest; CacheKeys "
                         "of a %d-node 1000align DAG (%d jobs)" % (small.n_nodes, small.n_jobs),
             "file_ids_ms": ids_ms, "file_ids_gbps": C1_N * C1_LEN / (ids_ms * 1e-3) / 1e9,
-            "fileset_digest_ms": fs_ms, "fileset_digest_note": "rf_fileset_digest_device: bytewise sort and path "
-            "material on the host, IDs placed from HBM, one %d-block message on the duo chain" % ((C1_N * 49 + 9 + 63) // 64),
-            "fileset_digest_host_ids_ms": fs_host_ms,
-            "fixture_match": ok,
-            "dag_nodes": small.n_nodes, "dag_full_recompute_ms": dag_ms,
-            "total_ms": ids_ms + fs_ms + dag_ms,
-            "install": inst,
-            "note": "4096 messages on 512 k1_sha256_octo chain waves (eight files per wave): the per-file "
-                    "chain (4097 blocks x ~1.2 us) bounds the file-ID time, not chip throughput"}
+            "file_ids_split": {"host": int(st.n_host), "duo": int(st.n_solo),
+                               "lanes": int(C1_N - st.n_host - st.n_solo)},
+            "fileset_digest_ms": fs_ms,
+            "fixture_match": ok, "dag_nodes": small.n_nodes, "dag_full_recompute_ms": dag_ms,
+            "total_ms": ids_ms + fs_ms + dag_ms, "install": inst}
 
 
 def bench_c1_install(ctx, arena, offs, want_fsd, cpu_leg=False):
@@ -329,34 +412,33 @@ def bench_c1_install(ctx, arena, offs, want_fsd, cpu_leg=False):
         res = {"what": "rf_install_dir over the configs[0] tree on local disk (page cache warm)",
                "ms": ms, "gbps": C1_N * C1_LEN / (ms * 1e-3) / 1e9, "entries": len(ents),
                "fileset_digest_match": fsd == want_fsd}
-        if cpu_leg:  # the same install on the host: read + hashlib (OpenSSL) SHA-256, 16 threads
-            import hashlib
+        if cpu_leg:  # the same install on the host: read + hashlib (OpenSSL) SHA-256
             from concurrent.futures import ThreadPoolExecutor
             paths = [os.path.join(root, c1_path(i).decode()) for i in range(C1_N)]
+            threads = ctx.host_info()[0] or 1
 
             def one(p):
                 with open(p, "rb") as f:
                     return hashlib.sha256(f.read()).digest()
-            with ThreadPoolExecutor(16) as ex:
+            with ThreadPoolExecutor(threads) as ex:
                 t0 = time.perf_counter()
                 cpu_ids = list(ex.map(one, paths))
                 cms = (time.perf_counter() - t0) * 1e3
-            res["cpu_openssl_16t"] = {"ms": cms, "gbps": C1_N * C1_LEN / (cms * 1e-3) / 1e9, "cores": 16,
-                                      "ids_match": cpu_ids == [e[1] for e in ents]}
+            res["cpu_openssl"] = {"ms": cms, "gbps": C1_N * C1_LEN / (cms * 1e-3) / 1e9, "cores": threads,
+                                  "ids_match": cpu_ids == [e[1] for e in ents]}
     finally:
         shutil.rmtree(root, ignore_errors=True)
     return res
 
 
 # ------------------------------------------------------- C3: incremental --
-def bench_dag(args, dist, ctx, comm):
+def bench_dag(args, dist, ctx, comm, budget):
     S = args.dag_samples
     t0 = time.perf_counter()
     dag = Dag1000(S, args.dag_pairs, seed=0x5EED0003 + 1000003 * dist.rank)
     a = dag.arrays()
     g = capi.Graph(ctx, a["n_slots"], a["out_slot"], a["tmpl_off"], a["tmpl_len"], a["hole_ptr"],
                    a["hole_pos"], a["hole_slot"], a["blob"])
-    del a
     g.set_slots(dag.file_slots, dag.leaf_ids)
     log("C3: %d nodes, %d jobs built+loaded in %.1f s" % (dag.n_nodes, dag.n_jobs, time.perf_counter() - t0))
     g.recompute(full=True)  # first call also captures the hipGraphs (host work): untimed
@@ -388,7 +470,7 @@ def bench_dag(args, dist, ctx, comm):
             g.gather_device(d_roots_idx.ptr, len(roots), d_local.ptr, ctx.stream)
             if comm is not None:
                 comm.allgather(d_local.ptr, d_gather.ptr, 32 * len(roots), ctx.stream)
-            else:  # no RCCL communicator (see main): same exchange through the host
+            else:
                 ctx.sync()
                 dist.all_gather_bytes(d_local.to_numpy())
 
@@ -408,14 +490,16 @@ def bench_dag(args, dist, ctx, comm):
            "full_recompute_ms": full_ms,
            "full_recompute_mnodes_per_s": dag.n_nodes / (full_ms * 1e-3) / 1e6,
            "levels": g.stats().n_levels}
-    # full-recompute roofline (VALU): all template blocks hashed
     st = g.stats()
     ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
     res["roofline_full"] = {"bound": "valu", "achieved": round(ach, 2), "peak": round(SHA_VALU_PEAK_GBS, 1),
                             "unit": "GB/s", "frac": round(ach / SHA_VALU_PEAK_GBS, 4)}
     res["canonicalize"] = bench_canon(ctx, g, dag)
+    # the configs[2] CPU legs need the host arrays (rank 0, N = 1)
+    res["_cpu"] = {"a": a, "dag": dag, "slots": slots, "old": old, "new": new,
+                   "gpu_dirty_jobs": int(n_dirty_jobs)} if dist.world == 1 else None
     g.close()
-    return res, dag
+    return res
 
 
 def bench_canon(ctx, g, dag):
@@ -441,10 +525,8 @@ def bench_canon(ctx, g, dag):
     nu = int(d_nu.to_numpy()[:4].view(np.uint32)[0])
     canon = d_canon.to_numpy().view(np.uint32)
     ms = float(np.median(times))
-    # every ref copy maps to the first; no other duplicates in the 1000align DAG
-    ok = nu == dag.n_nodes and n == dag.n_nodes + 3 * (dag.S - 1) and bool((canon[:3 * dag.S].reshape(dag.S, 3) == np.arange(3)).all())
-    # random accesses per node: insert = slot read + CAS (+ a 32-B compare read
-    # on a hit), resolve = one slot read -> ~3 random 4..32-B touches per node
+    ok = nu == dag.n_nodes and n == dag.n_nodes + 3 * (dag.S - 1) and bool(
+        (canon[:3 * dag.S].reshape(dag.S, 3) == np.arange(3)).all())
     res = {"workload": "dedup of %d node digests (C3 DAG + %d duplicated ref-index nodes)" % (n, 3 * (dag.S - 1)),
            "ms": ms, "mnodes_per_s": n / (ms * 1e-3) / 1e6, "unique": nu, "parity_ok": ok,
            "random_accesses_per_node": 3,
@@ -455,21 +537,34 @@ def bench_canon(ctx, g, dag):
 
 
 # --------------------------------------------------------------- C5: probe --
-def bench_probe(args, dist, ctx):
-    n_ins, n_probe = args.probe_keys, args.probes
+def probe_case(ctx, dist, n_ins, n_probe, steps, seed):
+    """Filter of n_ins keys (bloom.NewWithEstimates(n, 0.001), eval.go:838-843)
+    and n_probe probes: the inserted keys repeated to half the batch, then
+    fresh keys.  Keys generated on the device."""
     m = int(math.ceil(-1 * float(n_ins) * math.log(0.001) / math.pow(math.log(2), 2)))
     k = int(math.ceil(math.log(2) * float(m) / float(n_ins)))
-    keys = ctx.alloc(32 * n_probe)
-    # probes: [inserted keys x (n_probe/2n_ins)] ++ [fresh]; generated on device
     half = n_probe // 2
+    # rows [0, n_ins): the inserted keys.  n_ins <= half: probes = the inserted
+    # keys repeated to half the batch, then fresh keys; else probes = the last
+    # `half` inserted keys, then fresh keys after them.
     lens = np.array([32 * n_ins, 32 * (n_probe - half)], dtype=np.uint64)
-    offs = np.array([0, 32 * half], dtype=np.uint64)
+    if n_ins <= half:
+        rows, offs = n_probe, np.array([0, 32 * half], dtype=np.uint64)
+    else:
+        rows, offs = n_ins + n_probe - half, np.array([0, 32 * n_ins], dtype=np.uint64)
+    keys = ctx.alloc(32 * rows)
     d_offs, d_lens = ctx.upload(offs), ctx.upload(lens)
-    ctx.gen_fill(keys.ptr, d_offs.ptr, d_lens.ptr, 2, 0x5EED0005 + dist.rank, 32 * n_probe)
+    ctx.gen_fill(keys.ptr, d_offs.ptr, d_lens.ptr, 2, seed, 32 * rows)
     ctx.sync()
-    rep = half // n_ins
-    for r in range(1, rep):
-        capi._check(capi.lib().rf_memcpy_d2d(ctx.handle, keys.ptr + 32 * n_ins * r, keys.ptr, 32 * n_ins))
+    if n_ins <= half:
+        rep = half // n_ins
+        for r in range(1, rep):
+            capi._check(capi.lib().rf_memcpy_d2d(ctx.handle, keys.ptr + 32 * n_ins * r, keys.ptr, 32 * n_ins))
+        present = rep * n_ins
+        probe_ptr = keys.ptr
+    else:
+        present = half
+        probe_ptr = keys.ptr + 32 * (n_ins - half)
     b = capi.Bloom.new(ctx, m, k)
     ctx.timer_start()
     b.add_device(keys.ptr, n_ins, ctx.stream)
@@ -477,26 +572,49 @@ def bench_probe(args, dist, ctx):
     out = ctx.alloc(n_probe)
 
     def step():
-        b.probe_device(keys.ptr, n_probe, out.ptr, ctx.stream)
+        b.probe_device(probe_ptr, n_probe, out.ptr, ctx.stream)
 
-    t = timed_steps(dist, ctx, step, args.probe_steps, 1)
+    t = timed_steps(dist, ctx, step, steps, 1)
     ctx.timer_start()
     step()
     dev_ms = ctx.timer_stop()
-    hits = int(out.to_numpy().astype(np.int64).sum())
-    fresh = n_probe - rep * n_ins
-    fp = (hits - rep * n_ins) / max(fresh, 1)
+    o_np = out.to_numpy()
+    hits = int(o_np.astype(np.int64).sum())
+    no_false_negative = bool(o_np[:present].all())  # every inserted key's probe says "contains"
+    del o_np
+    fresh = n_probe - present
+    fp = (hits - present) / max(fresh, 1)
     bpp = 32 + 8 * k + 1
     ach = n_probe * bpp / (dev_ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic("k4_bloom_probe")
-    # Words one launch fetches: a present key (or a false positive) all k; an
-    # absent key stops at its first clear bit, so with a fraction f of the
-    # filter's bits set it fetches sum_{j<k} f^j on average.
     f = float(np.bitwise_count(b.words()).sum()) / m
     absent = n_probe - hits
     reads = hits * k + absent * sum(f ** j for j in range(k))
     gread_s = reads / (dev_ms * 1e-3) / 1e9
     ceil = gather_ceiling(m // 8, n_probe // 4, k)
+    res = {"workload": "bloomlive probe: n=%d keys (m=%d bits, %.1f MiB, k=%d), %d probes (%.0f%% present)"
+                       % (n_ins, m, m / 8 / 2**20, k, n_probe, 100.0 * present / n_probe),
+           "gprobes_per_s": dist.sum(n_probe) * steps / t / 1e9,
+           "device_ms": dev_ms, "add_ms": add_ms, "false_positive_rate": fp,
+           "no_false_negatives": no_false_negative, "present": present,
+           "false_positives": hits - present,
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_probe": bpp,
+                        "note": "algorithmic bytes; each random 8-B word read moves a 64-B line, so the "
+                                "real bound is the random-gather rate (roofline_gather)"},
+           "roofline_gather": {"bound": "random 8-B gathers", "achieved": round(gread_s, 2),
+                               "peak": round(ceil, 2) if ceil else None, "unit": "G words/s",
+                               "frac": round(gread_s / ceil, 4) if ceil else None,
+                               "words_per_probe": round(reads / n_probe, 3), "filter_fill": round(f, 4),
+                               "peak_kind": "measured live: tools/micro.hip k_gather, k independent "
+                                            "random 8-B reads per thread over a table of the filter's size"}}
+    return res, {"keys": keys, "probe_ptr": probe_ptr, "out": out, "bloom": b, "hits": hits, "m": m, "k": k,
+                 "extra": (d_offs, d_lens), "ceil": ceil, "present": present}
+
+
+def bench_probe(args, dist, ctx, budget):
+    n_ins, n_probe = args.probe_keys, args.probes
+    res, h = probe_case(ctx, dist, n_ins, n_probe, args.probe_steps, 0x5EED0005 + dist.rank)
+    keys, out, b, hits = h["keys"], h["out"], h["bloom"], h["hits"]
     # Repository.Collect over the same 1e9 keys as repository objects: probe +
     # ordered compaction of the dead ones (repository/file/repository.go:304-327)
     d_dead, d_cnt = ctx.alloc(8 * n_probe), ctx.alloc(64)
@@ -507,44 +625,37 @@ def bench_probe(args, dist, ctx):
     n_dead = int(d_cnt.to_numpy()[:8].view(np.uint64)[0])
     d_dead.free()
     d_cnt.free()
-    assoc = bench_assoc(ctx, keys, n_ins, n_probe, hits)
-    res = {"workload": "bloomlive probe: n=%d keys (m=%d bits, %.1f MiB, k=%d), %d probes (50%% present)"
-                       % (n_ins, m, m / 8 / 2**20, k, n_probe),
-           "gprobes_per_s": dist.sum(n_probe) * args.probe_steps / t / 1e9,
-           "device_ms": dev_ms, "add_ms": add_ms, "false_positive_rate": fp,
-           "assoc": assoc,
-           "collect": {"objects": n_probe, "dead": n_dead, "dead_matches_probe": n_dead == n_probe - hits,
-                       "ms": coll_ms, "g_objects_per_s": n_probe / (coll_ms * 1e-3) / 1e9,
-                       "overhead_vs_probe": round(coll_ms / dev_ms, 3)},
-           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_probe": bpp,
-                        "traffic": traffic, "traffic_source": tsrc,
-                        "note": "algorithmic bytes; each random 8-B word read moves a 64-B line, so the "
-                                "real bound is the random-gather rate (roofline_gather)"},
-           "roofline_gather": {"bound": "random 8-B gathers", "achieved": round(gread_s, 2),
-                               "peak": round(ceil, 2) if ceil else None, "unit": "G words/s",
-                               "frac": round(gread_s / ceil, 4) if ceil else None,
-                               "words_per_probe": round(reads / n_probe, 3), "filter_fill": round(f, 4),
-                               "peak_kind": "measured live: tools/micro.hip k_gather, k independent "
-                                            "random 8-B reads per thread over a table of the filter's size"}}
-    # bounded sample for the CPU leg (rank 0, N=1): the filter words and the
-    # first 2e7 probe keys
+    res["collect"] = {"objects": n_probe, "dead": n_dead, "dead_matches_probe": n_dead == n_probe - hits,
+                      "ms": coll_ms, "g_objects_per_s": n_probe / (coll_ms * 1e-3) / 1e9,
+                      "overhead_vs_probe": round(coll_ms / res["device_ms"], 3)}
+    res["assoc"] = bench_assoc(ctx, keys, n_ins, n_probe, hits)
+    ceil = h["ceil"]
+    if ceil and res["assoc"]:
+        a = res["assoc"]
+        ga = 3 * n_probe / (a["get_ms"] * 1e-3) / 1e9
+        a["roofline_gather"] = {"achieved": round(ga, 2), "peak": round(ceil, 2), "unit": "G random accesses/s",
+                                "frac": round(ga / ceil, 3),
+                                "accesses_per_get": "3 (tag, 32-B key compare, 32-B value on a hit; absent keys "
+                                                    "stop at an empty tag: 1-2)"}
+    # bounded sample for the CPU leg (rank 0, N = 1): the filter words and
+    # the first 2e7 probe keys
     if dist.world == 1 and "cpu" not in args.skip:
         ns = min(n_probe, 20_000_000)
-        res["_cpu"] = {"words": b.words(), "length": b.params()[2], "m": m, "k": k,
+        res["_cpu"] = {"words": b.words(), "length": b.params()[2], "m": h["m"], "k": h["k"],
                        "keys": keys.to_numpy(count=32 * ns), "n": ns}
-    for x in (keys, out, d_offs, d_lens):
+    for x in (keys, out) + h["extra"]:
         x.free()
     b.close()
-    # gather-bound kernels beside the probe, against the same live ceiling
-    if ceil:
-        a = res.get("assoc")
-        if a:
-            a["roofline_gather"] = {"achieved": round(3 * n_probe / (a["get_ms"] * 1e-3) / 1e9, 2), "peak": round(ceil, 2),
-                                    "unit": "G random accesses/s", "frac": round(3 * n_probe / (a["get_ms"] * 1e-3) / 1e9 / ceil, 3),
-                                    "accesses_per_get": "3 (tag, 32-B key compare, 32-B value on a hit; absent keys "
-                                                        "stop at an empty tag: 1-2)"}
     res["_gather_ceiling"] = ceil
+    # SURVEY §8(d) C5 second case: n = 1.2e9 keys -> m = 17.25 G bits (2.0 GiB):
+    # larger than the 256 MB MALL, so the gathers go to HBM
+    if args.probe_big_keys and budget.allow("probe_2gib_filter", 25):
+        rb, hb = probe_case(ctx, dist, args.probe_big_keys, n_probe, args.probe_steps, 0x5EED0015 + dist.rank)
+        for x in (hb["keys"], hb["out"]) + hb["extra"]:
+            x.free()
+        hb["bloom"].close()
+        res["filter_2gib"] = rb
+        log("  probe 2 GiB filter: %.2f G probes/s (171 MiB: %.2f)" % (rb["gprobes_per_s"], res["gprobes_per_s"]))
     return res
 
 
@@ -573,9 +684,6 @@ def bench_assoc(ctx, keys, n_ins, n_probe, hits):
     occ, cap = a.stats()
     for b in (vals, st, d_v, d_f):
         b.free()
-    # Eval.lookup for a batch of nodes (rf_assoc_lookup, host API): CacheKeys
-    # [physical (absent), logical (an inserted key)] per node, precise read
-    # repair writes the found value under the physical key
     n_nodes = min(2_000_000, n_ins)
     logical = keys.to_numpy(count=32 * n_nodes).reshape(n_nodes, 32)
     physical = np.random.default_rng(0x5EED0007).integers(0, 256, size=(n_nodes, 32), dtype=np.uint8)
@@ -584,19 +692,17 @@ def bench_assoc(ctx, keys, n_ins, n_probe, hits):
     t0 = time.perf_counter()
     which, _ = a.lookup(0, node_keys, ptr, repair=2)
     lk_s = time.perf_counter() - t0
-    _, f2 = a.get(0, physical)  # repaired: the physical keys now resolve
+    _, f2 = a.get(0, physical)
     lookup = {"workload": "%d nodes x 2 cache keys (physical absent, logical present), precise read repair"
                           % n_nodes,
               "ms": lk_s * 1e3, "m_nodes_per_s": n_nodes / lk_s / 1e6,
               "hits_on_logical": int((which == 1).sum()), "repaired": int(f2.astype(np.int64).sum()),
               "note": "host API: keys H2D, one Get batch, first-hit select on the device, repair Put batch"}
     a.close()
-    # bytes per Get: 32-B key read + a 4-B tag and a 32-B key compare (random)
-    # + a 32-B value read (random, hits) + 33-B result write
     return {"workload": "Put %d keys (one batch), Get %d keys (%d present)" % (n_ins, n_probe, found),
             "put_ms": put_s * 1e3, "put_mkeys_per_s": n_ins / put_s / 1e6, "put_ok": ok_put,
             "get_ms": get_ms, "get_g_keys_per_s": n_probe / (get_ms * 1e-3) / 1e9,
-            "found_exact": found == (n_probe // 2) // n_ins * n_ins,  # every Put key, no false positive
+            "found_exact": found == (n_probe // 2) // n_ins * n_ins,
             "bloom_false_positives_resolved": hits - found,
             "table_slots": cap, "occupied": occ, "lookup": lookup}
 
@@ -631,8 +737,8 @@ def cpu_model():
 def cpu_probe_and_tables(probe, canon_n=2_000_000):
     """CPU legs of the probe / canonicalize / assoc rows: bloom Contains on the
     same filter (oracle/oracle.c, bloom.Test order; 1 thread = bloomlive's
-    non-goroutine-safe Contains, and 16 threads), and Go-map-shaped dedup and
-    lookups (a Python dict over 32-B keys: the flowMap / in-memory assoc)."""
+    non-goroutine-safe Contains, and the host leg's thread count), and
+    Go-map-shaped dedup and lookups (a Python dict over 32-B keys)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import reflow_oracle as O
     L = O.lib()
@@ -641,7 +747,8 @@ def cpu_probe_and_tables(probe, canon_n=2_000_000):
     keys = np.ascontiguousarray(c["keys"])
     out = np.zeros(c["n"], dtype=np.uint8)
     r = {}
-    for th, n in ((1, min(c["n"], 2_000_000)), (16, c["n"])):
+    th_n = cpu_threads()
+    for th, n in ((1, min(c["n"], 2_000_000)), (th_n, c["n"])):
         t0 = time.perf_counter()
         L.orc_bloomlive_contains_batch(words.ctypes.data, int(c["length"]), int(c["m"]), int(c["k"]),
                                        keys.ctypes.data, n, out.ctypes.data, th)
@@ -664,61 +771,74 @@ def cpu_probe_and_tables(probe, canon_n=2_000_000):
     return r
 
 
-def cpu_baseline(args, sha, dag):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ctypes
+def cpu_threads():
+    """min(60, the CPU share): DigestLimiter (local/executor.go:41) on the
+    cores this process may use -- the same width as the host leg."""
+    ctx_threads = int(os.environ.get("RF_BENCH_CPU_THREADS", "0"))
+    if ctx_threads:
+        return ctx_threads
+    share = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            share = min(share, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(60, share))
 
+
+def cpu_baseline(args, sha, dag_res, budget):
+    """The headline's CPU leg: OpenSSL SHA-256 (hashlib; SHA-NI, what Go >= 1.21
+    crypto/sha256 uses) over the WHOLE configs[1] set on min(60, CPU share)
+    threads, LPT order; the oracle's scalar C port (~Go 1.9/1.10 speed class)
+    on a bounded sample; configs[0]; configs[2] on its own DAG and change set
+    (1 thread: Canonicalize is serial)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import reflow_oracle as O  # the oracle: cpu_baseline leg only
-    L = O.lib()
-    threads = min(16, os.cpu_count() or 1)
-    lens = sha["_lens"]
-    # bounded sample of the same workload: files in generation order up to the
-    # byte budget (the same skewed mix, big files included)
-    budget = int(args.cpu_sample_gib * GiB)
-    csum = np.cumsum(lens.astype(np.int64))
-    n = int(np.searchsorted(csum, budget)) + 1
-    n = min(n, len(lens))
-    s_lens = lens[:n].copy()
-    s_offs, total = arena_layout(s_lens, align=64)
-    arena = np.zeros(total, dtype=np.uint8)
-    L.orc_fill_batch(sha["_seed"], arena.ctypes.data, s_offs.ctypes.data, s_lens.ctypes.data, n, threads)
-    out = np.zeros((n, 32), dtype=np.uint8)
-    order = np.argsort(-s_lens.astype(np.int64), kind="stable").astype(np.uint64)  # LPT
-    o_offs, o_lens = s_offs[order].copy(), s_lens[order].copy()
-    t0 = time.perf_counter()
-    L.orc_sha256_batch(arena.ctypes.data, o_offs.ctypes.data, o_lens.ctypes.data, n, out.ctypes.data,
-                       threads)
-    dt = time.perf_counter() - t0
-    back = np.empty_like(out)
-    back[order.astype(np.int64)] = out
-    match = bool((back == sha["_digests"][:n]).all())
-    res = {"value": float(s_lens.sum()) / dt / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
-           "what": "SHA-256 of the C2 files (the headline metric's CPU leg)",
-           "sample": "first %d files (%.2f GiB, largest %.2f GiB) of the same C2 set, oracle/oracle.c "
-                     "scalar SHA-256, %d pthreads, largest-first" % (n, s_lens.sum() / GiB,
-                                                                    s_lens.max() / GiB, threads),
-           "seconds": dt, "gpu_digests_match": match, "cpu_model": cpu_model()}
-    # The same sample through OpenSSL's SHA-256 (hashlib; SHA-NI where the CPU
-    # has it -- what Go >= 1.21's crypto/sha256 uses), same threads, LPT order.
-    import hashlib
     from concurrent.futures import ThreadPoolExecutor
-    mv = memoryview(arena)
+    L = O.lib()
+    threads = cpu_threads()
+    lens, offs = sha["_lens"], sha["_offs"]
+    res = {"cores": threads, "cpu_model": cpu_model(), "sha_ni": "sha_ni" in open("/proc/cpuinfo").read()}
+    # the set itself, copied out of HBM (not timed)
+    t0 = time.perf_counter()
+    host = sha["_arena"].to_numpy()
+    log("cpu: copied the %.1f GiB set to host memory in %.1f s" % (host.nbytes / GiB, time.perf_counter() - t0))
+    mv = memoryview(host)
+    order = np.argsort(-lens.astype(np.int64), kind="stable")
 
     def one(i):
-        o, ln = int(s_offs[i]), int(s_lens[i])
+        o, ln = int(offs[i]), int(lens[i])
         return hashlib.sha256(mv[o:o + ln]).digest()
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
-        dig = list(ex.map(one, order.astype(np.int64).tolist()))
-    dt2 = time.perf_counter() - t0
-    ok2 = all(d == sha["_digests"][int(i)].tobytes() for d, i in zip(dig, order.astype(np.int64)))
-    res["openssl"] = {"value": float(s_lens.sum()) / dt2 / 1e9, "unit": "GB/s", "cores": threads,
-                      "kind": "library", "sample": "same files, hashlib/OpenSSL SHA-256, %d threads" % threads,
-                      "seconds": dt2, "gpu_digests_match": ok2,
-                      "sha_ni": "sha_ni" in open("/proc/cpuinfo").read()}
-    del mv, arena
-    # configs[0] on the CPU port and OpenSSL (the reference's own CPU case)
+        dig = list(ex.map(one, order.tolist()))
+    dt = time.perf_counter() - t0
+    ok = all(d == sha["_digests"][int(i)].tobytes() for d, i in zip(dig, order))
+    res.update({"value": float(lens.sum()) / dt / 1e9, "unit": "GB/s", "kind": "library",
+                "what": "SHA-256 of every configs[1] file, hashlib/OpenSSL (SHA-NI), LPT order",
+                "sample": "the whole configs[1] set (%d files, %.1f GiB)" % (len(lens), lens.sum() / GiB),
+                "seconds": dt, "gpu_digests_match": ok})
+    # scalar port on a bounded sample (files in generation order up to the budget)
+    budget_b = int(args.cpu_sample_gib * GiB)
+    n = min(int(np.searchsorted(np.cumsum(lens.astype(np.int64)), budget_b)) + 1, len(lens))
+    s_lens = np.ascontiguousarray(lens[:n])
+    s_offs = np.ascontiguousarray(offs[:n])
+    s_order = np.argsort(-s_lens.astype(np.int64), kind="stable").astype(np.uint64)
+    o_offs, o_lens = np.ascontiguousarray(s_offs[s_order]), np.ascontiguousarray(s_lens[s_order])
+    out = np.zeros((n, 32), dtype=np.uint8)
+    t0 = time.perf_counter()
+    L.orc_sha256_batch(host.ctypes.data, o_offs.ctypes.data, o_lens.ctypes.data, n, out.ctypes.data, threads)
+    dt = time.perf_counter() - t0
+    back = np.empty_like(out)
+    back[s_order.astype(np.int64)] = out
+    res["port"] = {"value": float(s_lens.sum()) / dt / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
+                   "sample": "first %d files (%.2f GiB, largest %.2f GiB) of configs[1], oracle/oracle.c scalar "
+                             "SHA-256, largest-first" % (n, s_lens.sum() / GiB, s_lens.max() / GiB),
+                   "seconds": dt, "gpu_digests_match": bool((back == sha["_digests"][:n]).all())}
+    del mv, host
+    # configs[0]: port and OpenSSL
     c1l = np.full(C1_N, C1_LEN, dtype=np.uint64)
     c1o, c1t = arena_layout(c1l, align=64)
     c1a = np.zeros(c1t, dtype=np.uint8)
@@ -736,46 +856,63 @@ def cpu_baseline(args, sha, dag):
                  "port_gbps": C1_N * C1_LEN / c1_port / 1e9, "openssl_ms": c1_ssl * 1e3,
                  "openssl_gbps": C1_N * C1_LEN / c1_ssl / 1e9, "cores": threads}
     del c1mv, c1a
-    # C3 port: full recompute of a bounded sample DAG, 1 thread (Canonicalize is serial)
-    if dag is not None:
-        small = Dag1000(max(1, args.cpu_dag_samples), dag.P)
-        a = small.arrays()
-        order = np.zeros(small.n_jobs, dtype=np.uint64)
-        # topological order = kinds in construction order (each kind only reads earlier ones)
-        order[:] = np.arange(small.n_jobs, dtype=np.uint64)
-        slots = np.zeros((small.n_slots, 32), dtype=np.uint8)
-        slots[small.file_slots] = small.leaf_ids
+    # configs[2] on the CPU: the same 10M-node DAG and change set, 1 thread
+    c = (dag_res or {}).get("_cpu")
+    if c is not None and budget.allow("cpu_dag", 40):
+        og = O.OGraph(c["a"])
+        og.set_inputs(c["dag"].file_slots, c["dag"].leaf_ids)
         t0 = time.perf_counter()
-        L.orc_graph_eval(small.n_jobs, order.ctypes.data, a["out_slot"].ctypes.data,
-                         a["tmpl_off"].ctypes.data, a["tmpl_len"].ctypes.data, a["hole_ptr"].ctypes.data,
-                         a["hole_pos"].ctypes.data, a["hole_slot"].ctypes.data, a["blob"].ctypes.data,
-                         slots.ctypes.data)
-        dt = time.perf_counter() - t0
-        res["dag"] = {"value": small.n_nodes / dt / 1e6, "unit": "Mnodes/s (full recompute)", "cores": 1,
-                      "kind": "port", "sample": "1000align DAG S=%d P=%d (%d nodes, %d jobs), "
-                      "oracle/oracle.c orc_graph_eval" % (small.S, small.P, small.n_nodes, small.n_jobs),
-                      "seconds": dt}
-    _ = ctypes
+        og.full()
+        full_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        hashed = og.update(c["slots"], c["new"])
+        inc_s = time.perf_counter() - t0
+        blocks = og.last_blocks()
+        n_nodes = c["dag"].n_nodes
+        res["dag_full"] = {"value": n_nodes / full_s / 1e6, "unit": "M graph nodes/s", "cores": 1, "kind": "port",
+                           "what": "every digest recomputed, the reference's behaviour per Eval (flow.go:653-664 "
+                                   "memoises per *Flow node only)",
+                           "sample": "configs[2] in full: %d nodes / %d jobs, oracle/oracle.c orc_graph_full"
+                                     % (n_nodes, c["dag"].n_jobs), "seconds": full_s}
+        res["dag_incremental"] = {"value": (c["gpu_dirty_jobs"] - len(np.unique(c["slots"] // 2))) / inc_s / 1e6,
+                                  "unit": "M dirty nodes/s", "cores": 1, "kind": "port",
+                                  "sample": "configs[2] in full, the bench's own change set (1%% of leaf File IDs): "
+                                            "%d jobs / %d blocks re-hashed (oracle/oracle.c orc_graph_update)"
+                                            % (hashed, blocks),
+                                  "seconds": inc_s, "jobs_equal_gpu": hashed == c["gpu_dirty_jobs"]}
+        if dag_res is not None:
+            dag_res["dirty_blocks_per_step"] = int(blocks)
+            ops = blocks * SHA_OPS_PER_BLOCK
+            dag_res["roofline_incremental"] = {
+                "bound": "valu", "achieved_tops": round(ops / (dag_res["device_ms_per_step"] * 1e-3) / 1e12, 3),
+                "peak_tops": round(VALU_LANE_OPS / 1e12, 1),
+                "frac": round(ops / (dag_res["device_ms_per_step"] * 1e-3) / VALU_LANE_OPS, 4),
+                "note": "dirty blocks x 1464 ops per step / device time; the step is latency-bound (fused "
+                        "chains of dependent jobs), not throughput-bound"}
+        og.close()
     return res
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sha-gib", type=float, default=64.0)
     ap.add_argument("--dag-samples", type=int, default=22075)  # ~10M nodes at P=32
     ap.add_argument("--dag-pairs", type=int, default=32)
     ap.add_argument("--dag-steps", type=int, default=20)
     ap.add_argument("--probe-keys", type=int, default=100_000_000)
+    ap.add_argument("--probe-big-keys", type=int, default=1_200_000_000)
     ap.add_argument("--probes", type=int, default=1_000_000_000)
     ap.add_argument("--probe-steps", type=int, default=3)
-    ap.add_argument("--cpu-sample-gib", type=float, default=20.0)
-    ap.add_argument("--cpu-dag-samples", type=int, default=200)
+    ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
+    ap.add_argument("--gpu-only-run", type=int, default=1, help="one GPU-only run (duo roofline)")
+    ap.add_argument("--budget-s", type=float, default=420.0)
     ap.add_argument("--skip", default="", help="comma list of: c1,install,dag,probe,cpu")
     args = ap.parse_args()
-    skip = set(filter(None, args.skip.split(",")))
+    args.skip = set(filter(None, args.skip.split(",")))
+    budget = Budget(args.budget_s)
 
     dist = Dist(args.gpus)
     device = dist.local
@@ -792,15 +929,15 @@ def main():
             comm = capi.Comm(ctx, dist.world, dist.rank, uid)
             exchange = "RCCL all-gather over xGMI"
 
-    sha = bench_sha(args, dist, ctx)
-    c1 = None if "c1" in skip else bench_c1(args, dist, ctx)
-    dag_res, dag = (None, None)
-    if "dag" not in skip:
-        dag_res, dag = bench_dag(args, dist, ctx, comm)
-    probe = None if "probe" in skip else bench_probe(args, dist, ctx)
+    sha = bench_sha(args, dist, ctx, budget)
+    c1 = bench_c1(args, dist, ctx, budget) if "c1" not in args.skip and budget.allow("c1", 15) else None
+    dag_res = None
+    if "dag" not in args.skip and budget.allow("dag", 40):
+        dag_res = bench_dag(args, dist, ctx, comm, budget)
+    probe = bench_probe(args, dist, ctx, budget) if "probe" not in args.skip and budget.allow("probe", 30) else None
     cpu = None
-    if dist.rank == 0 and dist.world == 1 and "cpu" not in skip:
-        cpu = cpu_baseline(args, sha, dag)
+    if dist.rank == 0 and dist.world == 1 and "cpu" not in args.skip and budget.allow("cpu", 60):
+        cpu = cpu_baseline(args, sha, dag_res, budget)
         if probe is not None and "_cpu" in probe:
             cpu.update(cpu_probe_and_tables(probe))
     if probe is not None:
@@ -811,24 +948,37 @@ def main():
             cn["roofline_gather"] = {"achieved": cn["achieved_g_accesses_per_s"], "peak": round(ceil, 2),
                                      "unit": "G random accesses/s",
                                      "frac": round(cn["achieved_g_accesses_per_s"] / ceil, 3)}
+    if dag_res is not None:
+        dag_res.pop("_cpu", None)
+    sha["_arena"].free()
 
     if dist.rank == 0:
+        workload = sha["workload"]
+        if dist.world > 1:
+            workload = ("configs[3] weak-scaled: the global Fileset = %d configs[1]-distributed sets (%d files, "
+                        "%.0f GiB), LPT-sharded by size: %.1f GiB / %d files on rank 0"
+                        % (dist.world, sha["glob"]["files"], sha["glob"]["bytes"] / GiB,
+                           sha["bytes_per_gpu"] / GiB, sha["files"]))
         line = {
             "metric": "SHA-256 digest GB/s + incremental cache-key recompute Mnodes/s, 1/2/4/8 GPU",
             "value": round(sha["value"], 4), "unit": "GB/s", "n_gpus": dist.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(sha["ms_per_step"], 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 content generated in HBM)",
-            "config": {"workload": "configs[1]: 64 GiB FASTQ/BAM-like Fileset per GPU, %d files 4 KiB-2 GiB "
-                                   "(98%% log-uniform 4 KiB-1 MiB, 2%% 64 MiB-2 GiB), SHA-256 of every file"
-                                   % sha["files"],
-                       "parallelism": "files sharded per GPU (independent); RCCL only for DAG root digests",
-                       "exchange": exchange},
+            "config": {"workload": workload,
+                       "parallelism": "files sharded per GPU (LPT by size); per GPU: host leg (SHA-NI threads) + "
+                                      "GPU kernels split by the K1 planner; RCCL only for DAG root digests",
+                       "exchange": exchange, "split_rank0": sha["split"], "step_ms_rank0": sha["step_ms"]},
             "roofline": sha["roofline"],
+            "host_leg": sha["host_leg"],
+            "roofline_gpu_only": sha.get("roofline_gpu_only"),
+            "gpu_only": sha.get("gpu_only"),
             "cpu_baseline": cpu,
             "c1": c1,
             "incremental": dag_res,
             "probe": probe,
+            "budget": {"seconds": args.budget_s, "skipped": budget.skipped,
+                       "elapsed_s": round(time.perf_counter() - T_START, 1)},
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

@@ -18,9 +18,15 @@
  *   - A digest is 32 raw SHA-256 bytes.  WD(d) = 0x00 0x05 || d (34 bytes) is
  *     the grailbio/base/digest.WriteDigest framing the reference hashes.
  *
- * The product path is the HIP path only: if the gfx950 code object cannot be
+ * The product path is the HIP path: if the gfx950 code object cannot be
  * loaded or no device is present, rf_init fails with RF_EDEVICE -- there is
- * no CPU fallback behind this ABI.
+ * no CPU fallback behind this ABI.  The one place host cores hash is the K1
+ * planner's host leg (rf_set_host_threads): a scheduled part of a batch, not
+ * a fallback -- the longest SHA-256 chains of a skewed batch, which a host
+ * core with SHA-NI runs ~40x faster than one GPU wave, go to a pool of host
+ * threads (the reference's <=60-goroutine digest pool, local/executor.go:41)
+ * while the GPU kernels hash the rest.  It needs a device like every other
+ * call, and rf_set_host_threads(ctx, 0) pins every message to the GPU.
  */
 #ifndef REFLOW_HIP_H
 #define REFLOW_HIP_H
@@ -63,6 +69,17 @@ int rf_sync(rf_ctx *ctx);
 /* Version string, e.g. "reflow-hip 0.1 gfx950". */
 const char *rf_version(void);
 
+/* K1 host leg width: n >= 1 threads, 0 = none (every message on the GPU
+ * kernels), -1 = default min(60, CPU share): 60 is the reference's
+ * DigestLimiter (local/executor.go:41), the share the smaller of the affinity
+ * mask and the cgroup cpu.max quota, divided by LOCAL_WORLD_SIZE (ranks per
+ * node); RF_HOST_THREADS overrides the default.  Without the x86 SHA
+ * extensions the host leg is off whatever n is. */
+int rf_set_host_threads(rf_ctx *ctx, int n);
+/* Host leg threads in effect, one core's measured SHA-NI rate (bytes/s; 0 if
+ * unavailable) and whether the CPU has the SHA extensions. */
+int rf_host_info(rf_ctx *ctx, int *threads, double *core_bytes_per_s, int *sha_ext);
+
 /* ---- device memory and timing -------------------------------------------
  * The engine owns its HIP runtime; callers (the cgo shim, bench.py, tests)
  * allocate HBM through these so no second runtime enters the process. */
@@ -103,8 +120,13 @@ int rf_sha256_arena(rf_ctx *ctx, const uint8_t *arena, const uint64_t *offs, con
                     uint64_t n, uint8_t *out32);
 
 /* Device-resident form.  A plan is built once from host-side offsets and
- * lengths (it orders messages largest-first and decides which messages run
- * wave-per-message); rf_sha_plan_run then digests messages already in HBM.
+ * lengths: it orders messages largest-first and splits them by a makespan
+ * model over the legs -- the host leg (the largest messages, SHA-NI threads,
+ * bytes streamed D2H in 8 MiB chunks), wave-per-message duo chains, and the
+ * lane-per-message kernels; rf_sha_plan_run then digests messages already in
+ * HBM.  The GPU legs are queued asynchronously on `stream`; with a host leg
+ * the call returns once the host threads are done (their digests' upload and
+ * scatter into out queued on `stream`).
  * Requirements: offs[i] % 16 == 0.  out is n*32 bytes of device memory. */
 int rf_sha_plan_create(rf_ctx *ctx, const uint64_t *offs, const uint64_t *lens, uint64_t n,
                        uint32_t flags, rf_sha_plan **out);
@@ -115,6 +137,9 @@ typedef struct {
     uint64_t max_blocks;         /* critical path of the largest message       */
     uint64_t total_bytes;
     float last_ms_lanes, last_ms_solo, last_ms_total; /* HIP-event times of the last run */
+    float last_ms_host;          /* wall time of the last run's host leg         */
+    uint32_t host_threads;       /* host leg threads (0: no host leg)            */
+    uint64_t n_host, host_bytes; /* messages / bytes on the host leg             */
 } rf_sha_stats;
 int rf_sha_plan_stats(rf_sha_plan *plan, rf_sha_stats *out);
 void rf_sha_plan_destroy(rf_sha_plan *plan);
@@ -124,6 +149,8 @@ void rf_sha_plan_destroy(rf_sha_plan *plan);
 #define RF_SHA_ONE_LANE_CHAIN 4u /* wave-per-message kernel keeps the round chain on one lane */
 #define RF_SHA_NO_PAIR 8u      /* small sets: lanes kernel instead of the producer/chain pair */
 #define RF_SHA_NO_OCTO 16u     /* small sets: no eight-per-wave two-lane chains (pair or lanes) */
+#define RF_SHA_ALL_HOST 32u    /* every message on the host leg (needs SHA-NI and host threads) */
+#define RF_SHA_NO_HOST 64u     /* no host leg: every message on the GPU kernels */
 
 /* Synthetic data generator (bench / tests): fills d_arena so that message i
  * is the splitmix64 counter stream with seed (seed ^ i). */

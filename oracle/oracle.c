@@ -157,6 +157,71 @@ static void *fill_worker(void *p) {
     return NULL;
 }
 
+/* SHA-256 of stream `seed` of `len` bytes without materialising it: 1 MiB
+ * chunks generated and compressed in turn (configs[1] files reach 2 GiB). */
+void orc_stream_sha256(uint64_t seed, uint64_t len, uint8_t out[32]) {
+    enum { CH = 1 << 20 };
+    static __thread uint8_t *buf = NULL;
+    if (!buf) buf = (uint8_t *)malloc(CH + 128);
+    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint64_t done = 0;
+    for (;;) {
+        const uint64_t n = len - done < CH ? len - done : CH;
+        for (uint64_t q = 0; 8 * q < n; ++q) {
+            uint64_t v = mix64(seed + (done / 8 + q + 1) * 0x9E3779B97F4A7C15ULL);
+            memcpy(buf + 8 * q, &v, 8);
+        }
+        if (n == CH) {
+            for (uint64_t b = 0; b < CH / 64; ++b) sha256_compress(st, buf + 64 * b);
+            done += CH;  /* len a multiple of CH: the next pass pads an empty tail */
+            continue;
+        }
+        /* last (partial) chunk: whole blocks, then the padded tail */
+        const uint64_t full = n / 64, rem = n - 64 * full;
+        for (uint64_t b = 0; b < full; ++b) sha256_compress(st, buf + 64 * b);
+        uint8_t tail[128];
+        memset(tail, 0, sizeof tail);
+        if (rem) memcpy(tail, buf + 64 * full, rem);
+        tail[rem] = 0x80;
+        const uint64_t tl = (rem + 9 <= 64) ? 64 : 128, bits = len * 8;
+        for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+        sha256_compress(st, tail);
+        if (tl == 128) sha256_compress(st, tail + 64);
+        break;
+    }
+    for (int i = 0; i < 8; ++i) {
+        out[4 * i] = (uint8_t)(st[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(st[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(st[i] >> 8);
+        out[4 * i + 3] = (uint8_t)st[i];
+    }
+}
+
+typedef struct {
+    uint64_t seed; const uint64_t *lens; uint64_t n; uint8_t *out; int tid, nth;
+} stream_job;
+
+static void *stream_worker(void *p) {
+    stream_job *j = (stream_job *)p;
+    for (uint64_t i = (uint64_t)j->tid; i < j->n; i += (uint64_t)j->nth)
+        orc_stream_sha256(j->seed ^ i, j->lens[i], j->out + 32 * i);
+    return NULL;
+}
+
+/* out[i] = SHA-256 of message i = stream (seed ^ i) of lens[i] bytes. */
+void orc_stream_sha256_batch(uint64_t seed, const uint64_t *lens, uint64_t n, uint8_t *out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    stream_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (stream_job){seed, lens, n, out, t, nthreads};
+        pthread_create(&th[t], NULL, stream_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
 /* message i = stream (seed ^ i), the layout rf_gen_fill produces on device. */
 void orc_fill_batch(uint64_t seed, uint8_t *arena, const uint64_t *offs, const uint64_t *lens,
                     uint64_t n, int nthreads) {
@@ -198,6 +263,154 @@ void orc_graph_eval(uint64_t n_jobs, const uint64_t *order, const uint32_t *out_
         orc_sha256(buf, len, slots32 + 32ull * out_slot[j]);
     }
     free(buf);
+}
+
+/* ------------------------------------------------------------------ */
+/* Incremental recompute (the CPU port of rf_graph_set_slots +          */
+/* rf_graph_recompute): after input slots change, their consumers are   */
+/* re-hashed in topological order; a job whose digest did not change    */
+/* does not dirty its own consumers (early cut-off).  The reference has */
+/* no incremental form -- Flow.Digest is memoized per *Flow node and    */
+/* every Eval recomputes every digest (flow.go:653-664, 814-843) -- so  */
+/* this is the CPU statement of the same dirty-closure work the GPU     */
+/* path does, used as the checker of its dirty counts and as the        */
+/* single-thread CPU leg of configs[2].  The caller keeps the arrays.   */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint64_t n_jobs, n_slots;
+    const uint32_t *out_slot, *tmpl_len, *hole_pos, *hole_slot;
+    const uint64_t *tmpl_off, *hole_ptr;
+    const uint8_t *blob;
+    uint32_t *topo;      /* topological position of each job */
+    uint64_t *cptr;      /* slot -> consumer jobs (CSR)      */
+    uint32_t *cjob;
+    uint8_t *queued;     /* job already in the heap          */
+    uint32_t *heap;      /* min-heap of topo positions       */
+    uint32_t *job_at;    /* topo position -> job             */
+    uint8_t *buf;
+    uint64_t cap;
+    uint64_t last_blocks; /* SHA-256 blocks hashed by the last update */
+} orc_graph;
+
+orc_graph *orc_graph_new(uint64_t n_jobs, uint64_t n_slots, const uint32_t *out_slot, const uint64_t *tmpl_off,
+                         const uint32_t *tmpl_len, const uint64_t *hole_ptr, const uint32_t *hole_pos,
+                         const uint32_t *hole_slot, const uint8_t *blob) {
+    orc_graph *g = (orc_graph *)calloc(1, sizeof *g);
+    g->n_jobs = n_jobs; g->n_slots = n_slots; g->out_slot = out_slot; g->tmpl_off = tmpl_off;
+    g->tmpl_len = tmpl_len; g->hole_ptr = hole_ptr; g->hole_pos = hole_pos; g->hole_slot = hole_slot;
+    g->blob = blob;
+    const uint64_t H = n_jobs ? hole_ptr[n_jobs] : 0;
+    g->cptr = (uint64_t *)calloc(n_slots + 1, 8);
+    g->cjob = (uint32_t *)malloc(4 * (H + 1));
+    for (uint64_t h = 0; h < H; ++h) g->cptr[hole_slot[h] + 1]++;
+    for (uint64_t s = 0; s < n_slots; ++s) g->cptr[s + 1] += g->cptr[s];
+    uint64_t *fill = (uint64_t *)malloc(8 * (n_slots + 1));
+    memcpy(fill, g->cptr, 8 * (n_slots + 1));
+    for (uint64_t j = 0; j < n_jobs; ++j)
+        for (uint64_t h = hole_ptr[j]; h < hole_ptr[j + 1]; ++h) g->cjob[fill[hole_slot[h]]++] = (uint32_t)j;
+    /* Kahn over jobs: in-degree = holes whose slot some job writes */
+    int64_t *producer = (int64_t *)malloc(8 * (n_slots + 1));
+    for (uint64_t s = 0; s < n_slots; ++s) producer[s] = -1;
+    for (uint64_t j = 0; j < n_jobs; ++j) producer[out_slot[j]] = (int64_t)j;
+    uint32_t *indeg = (uint32_t *)calloc(n_jobs + 1, 4);
+    for (uint64_t j = 0; j < n_jobs; ++j)
+        for (uint64_t h = hole_ptr[j]; h < hole_ptr[j + 1]; ++h)
+            if (producer[hole_slot[h]] >= 0) indeg[j]++;
+    g->job_at = (uint32_t *)malloc(4 * (n_jobs + 1));
+    g->topo = (uint32_t *)malloc(4 * (n_jobs + 1));
+    uint64_t qh = 0, qt = 0;
+    for (uint64_t j = 0; j < n_jobs; ++j)
+        if (!indeg[j]) g->job_at[qt++] = (uint32_t)j;
+    while (qh < qt) {
+        const uint32_t j = g->job_at[qh++];
+        const uint32_t s = out_slot[j];
+        for (uint64_t c = g->cptr[s]; c < g->cptr[s + 1]; ++c)
+            if (--indeg[g->cjob[c]] == 0) g->job_at[qt++] = g->cjob[c];
+    }
+    for (uint64_t i = 0; i < qt; ++i) g->topo[g->job_at[i]] = (uint32_t)i;
+    free(fill); free(producer); free(indeg);
+    g->queued = (uint8_t *)calloc(n_jobs + 1, 1);
+    g->heap = (uint32_t *)malloc(4 * (n_jobs + 1));
+    return g;
+}
+
+void orc_graph_free(orc_graph *g) {
+    if (!g) return;
+    free(g->cptr); free(g->cjob); free(g->job_at); free(g->topo); free(g->queued); free(g->heap); free(g->buf);
+    free(g);
+}
+
+static void heap_push(uint32_t *h, uint64_t *n, uint32_t v) {
+    uint64_t i = (*n)++;
+    while (i && h[(i - 1) / 2] > v) { h[i] = h[(i - 1) / 2]; i = (i - 1) / 2; }
+    h[i] = v;
+}
+
+static uint32_t heap_pop(uint32_t *h, uint64_t *n) {
+    const uint32_t top = h[0], v = h[--(*n)];
+    uint64_t i = 0;
+    for (;;) {
+        uint64_t c = 2 * i + 1;
+        if (c >= *n) break;
+        if (c + 1 < *n && h[c + 1] < h[c]) ++c;
+        if (h[c] >= v) break;
+        h[i] = h[c]; i = c;
+    }
+    h[i] = v;
+    return top;
+}
+
+/* Write n changed input slots into slots32 and re-derive their dependents;
+ * returns the number of jobs hashed. */
+uint64_t orc_graph_update(orc_graph *g, uint8_t *slots32, const uint32_t *changed, const uint8_t *digests32,
+                          uint64_t n) {
+    uint64_t hn = 0, hashed = 0;
+    g->last_blocks = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t s = changed[i];
+        memcpy(slots32 + 32ull * s, digests32 + 32 * i, 32);
+        for (uint64_t c = g->cptr[s]; c < g->cptr[s + 1]; ++c) {
+            const uint32_t k = g->cjob[c];
+            if (!g->queued[k]) { g->queued[k] = 1; heap_push(g->heap, &hn, g->topo[k]); }
+        }
+    }
+    uint8_t d[32];
+    while (hn) {
+        const uint32_t j = g->job_at[heap_pop(g->heap, &hn)];
+        g->queued[j] = 0;
+        const uint32_t len = g->tmpl_len[j];
+        if (len > g->cap) { g->cap = 2 * (uint64_t)len + 64; g->buf = (uint8_t *)realloc(g->buf, g->cap); }
+        memcpy(g->buf, g->blob + g->tmpl_off[j], len);
+        for (uint64_t h = g->hole_ptr[j]; h < g->hole_ptr[j + 1]; ++h)
+            memcpy(g->buf + g->hole_pos[h], slots32 + 32ull * g->hole_slot[h], 32);
+        orc_sha256(g->buf, len, d);
+        ++hashed;
+        g->last_blocks += ((uint64_t)len + 9 + 63) / 64;
+        uint8_t *o = slots32 + 32ull * g->out_slot[j];
+        if (!memcmp(o, d, 32)) continue;  /* early cut-off */
+        memcpy(o, d, 32);
+        const uint32_t s = g->out_slot[j];
+        for (uint64_t c = g->cptr[s]; c < g->cptr[s + 1]; ++c) {
+            const uint32_t k = g->cjob[c];
+            if (!g->queued[k]) { g->queued[k] = 1; heap_push(g->heap, &hn, g->topo[k]); }
+        }
+    }
+    return hashed;
+}
+
+uint64_t orc_graph_last_blocks(const orc_graph *g) { return g->last_blocks; }
+
+/* Full recompute in topological order (every job once). */
+void orc_graph_full(orc_graph *g, uint8_t *slots32) {
+    for (uint64_t q = 0; q < g->n_jobs; ++q) {
+        const uint32_t j = g->job_at[q];
+        const uint32_t len = g->tmpl_len[j];
+        if (len > g->cap) { g->cap = 2 * (uint64_t)len + 64; g->buf = (uint8_t *)realloc(g->buf, g->cap); }
+        memcpy(g->buf, g->blob + g->tmpl_off[j], len);
+        for (uint64_t h = g->hole_ptr[j]; h < g->hole_ptr[j + 1]; ++h)
+            memcpy(g->buf + g->hole_pos[h], slots32 + 32ull * g->hole_slot[h], 32);
+        orc_sha256(g->buf, len, slots32 + 32ull * g->out_slot[j]);
+    }
 }
 
 /* ------------------------------------------------------------------ */

@@ -31,6 +31,8 @@ import os
 import struct
 import subprocess
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
@@ -62,9 +64,61 @@ def lib():
         L.orc_bloomlive_add_batch.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p,
                                               ctypes.c_uint64]
         L.orc_fill_batch.argtypes = [ctypes.c_uint64, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_int]
+        L.orc_stream_sha256.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u8p]
+        L.orc_stream_sha256_batch.argtypes = [ctypes.c_uint64, u8p, ctypes.c_uint64, u8p, ctypes.c_int]
+        L.orc_graph_new.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u8p, u8p, u8p, u8p, u8p, u8p, u8p]
+        L.orc_graph_new.restype = ctypes.c_void_p
+        L.orc_graph_free.argtypes = [ctypes.c_void_p]
+        L.orc_graph_update.argtypes = [ctypes.c_void_p, u8p, u8p, u8p, ctypes.c_uint64]
+        L.orc_graph_update.restype = ctypes.c_uint64
+        L.orc_graph_full.argtypes = [ctypes.c_void_p, u8p]
+        L.orc_graph_last_blocks.argtypes = [ctypes.c_void_p]
+        L.orc_graph_last_blocks.restype = ctypes.c_uint64
         L.orc_graph_eval.argtypes = [ctypes.c_uint64, u8p, u8p, u8p, u8p, u8p, u8p, u8p, u8p, u8p]
         _LIB = L
     return _LIB
+
+
+class OGraph:
+    """The oracle's job graph (orc_graph_*): full and incremental recompute
+    over rf_graph_desc-shaped arrays (a dict as Dag1000.arrays() returns)."""
+
+    def __init__(self, a):
+        self._a = {k: (np.ascontiguousarray(v) if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+        self._blob = np.frombuffer(a["blob"], dtype=np.uint8) if isinstance(a["blob"], (bytes, bytearray)) \
+            else np.ascontiguousarray(a["blob"], dtype=np.uint8)
+        k = self._a
+        self.n_slots = int(k["n_slots"])
+        self.slots = np.zeros((max(self.n_slots, 1), 32), dtype=np.uint8)
+        hp = np.ascontiguousarray(k["hole_pos"], dtype=np.uint32)
+        hs = np.ascontiguousarray(k["hole_slot"], dtype=np.uint32)
+        self._keep = (hp, hs)
+        self._h = lib().orc_graph_new(len(k["out_slot"]), self.n_slots, k["out_slot"].ctypes.data,
+                                      k["tmpl_off"].ctypes.data, k["tmpl_len"].ctypes.data,
+                                      k["hole_ptr"].ctypes.data, hp.ctypes.data if len(hp) else None,
+                                      hs.ctypes.data if len(hs) else None, self._blob.ctypes.data)
+
+    def set_inputs(self, slots, digests):
+        self.slots[np.asarray(slots, dtype=np.int64)] = np.asarray(digests, dtype=np.uint8).reshape(-1, 32)
+
+    def full(self):
+        lib().orc_graph_full(self._h, self.slots.ctypes.data)
+
+    def update(self, slots, digests) -> int:
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1)
+        return int(lib().orc_graph_update(self._h, self.slots.ctypes.data, s.ctypes.data, d.ctypes.data, len(s)))
+
+    def last_blocks(self) -> int:
+        return int(lib().orc_graph_last_blocks(self._h))
+
+    def close(self):
+        if self._h:
+            lib().orc_graph_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 def _buf(b: bytes):

@@ -20,6 +20,8 @@ RF_SHA_ALL_SOLO = 2
 RF_SHA_ONE_LANE_CHAIN = 4
 RF_SHA_NO_PAIR = 8
 RF_SHA_NO_OCTO = 16
+RF_SHA_ALL_HOST = 32
+RF_SHA_NO_HOST = 64
 
 # Every symbol include/reflow_hip.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = [
@@ -41,6 +43,7 @@ EXPORTS = [
     "rf_dedup_digests", "rf_dedup_digests_device", "rf_assoc_lookup",
     "rf_assoc_new", "rf_assoc_destroy", "rf_assoc_put", "rf_assoc_get", "rf_assoc_get_device",
     "rf_assoc_get_abbrev", "rf_assoc_stats", "rf_assoc_put_device",
+    "rf_set_host_threads", "rf_host_info",
 ]
 
 
@@ -54,7 +57,9 @@ class ShaStats(ctypes.Structure):
     _fields_ = [("n_msgs", ctypes.c_uint64), ("n_solo", ctypes.c_uint64),
                 ("total_blocks", ctypes.c_uint64), ("max_blocks", ctypes.c_uint64),
                 ("total_bytes", ctypes.c_uint64), ("last_ms_lanes", ctypes.c_float),
-                ("last_ms_solo", ctypes.c_float), ("last_ms_total", ctypes.c_float)]
+                ("last_ms_solo", ctypes.c_float), ("last_ms_total", ctypes.c_float),
+                ("last_ms_host", ctypes.c_float), ("host_threads", ctypes.c_uint32),
+                ("n_host", ctypes.c_uint64), ("host_bytes", ctypes.c_uint64)]
 
 
 class GraphDesc(ctypes.Structure):
@@ -239,6 +244,8 @@ def lib():
             "rf_assoc_get_abbrev": ([vp, i32, vp, vp, u64, vp, vp, vp], i32),
             "rf_assoc_stats": ([vp, vp, vp], i32),
             "rf_assoc_put_device": ([vp, i32, vp, vp, vp, u64, vp], i32),
+            "rf_set_host_threads": ([vp, i32], i32),
+            "rf_host_info": ([vp, vp, vp, vp], i32),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -264,12 +271,27 @@ def device_count():
 
 
 class Context:
-    """One rf_ctx bound to one HIP device (one process per GPU)."""
+    """One rf_ctx bound to one HIP device (one process per GPU).
 
-    def __init__(self, device=0):
+    host_threads: width of K1's host leg (rf_set_host_threads): None keeps the
+    library default (min(60, CPU share)), 0 pins every message to the GPU
+    kernels -- what the kernel parity tests use."""
+
+    def __init__(self, device=0, host_threads=None):
         self._h = ctypes.c_void_p()
         _check(lib().rf_init(device, ctypes.byref(self._h)))
         self.device = device
+        if host_threads is not None:
+            self.set_host_threads(host_threads)
+
+    def set_host_threads(self, n):
+        _check(lib().rf_set_host_threads(self._h, -1 if n is None else int(n)))
+
+    def host_info(self):
+        """(threads, one core's SHA-NI bytes/s, has SHA extensions)."""
+        t, r, e = ctypes.c_int(0), ctypes.c_double(0), ctypes.c_int(0)
+        _check(lib().rf_host_info(self._h, ctypes.byref(t), ctypes.byref(r), ctypes.byref(e)))
+        return t.value, r.value, bool(e.value)
 
     def close(self):
         if self._h:

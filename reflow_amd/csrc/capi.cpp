@@ -31,6 +31,8 @@
 #include <rccl/rccl.h>
 
 #include "engine.h"
+#include "host_leg.h"
+#include "host_sha.h"
 #include "reflow_hip.h"
 
 using namespace rf;
@@ -117,7 +119,26 @@ struct rf_ctx {
     HostBuf h_stage;
     hipEvent_t t0 = nullptr, t1 = nullptr;
     rf_sha_plan* tplan = nullptr;  // one-shot batches (transient_plan)
+    int host_threads = -1;         // K1 host leg: -1 default width, 0 none
+    HostPool* pool = nullptr;      // created on first use
 };
+
+// Host-leg width of a context (0 when the CPU has no SHA extensions).
+static unsigned ctx_host_threads(rf_ctx* ctx) {
+    if (!host_sha_available()) return 0;
+    return ctx->host_threads < 0 ? host_default_threads() : (unsigned)ctx->host_threads;
+}
+
+static HostPool* ctx_pool(rf_ctx* ctx) {
+    const unsigned n = ctx_host_threads(ctx);
+    if (!n) return nullptr;
+    if (ctx->pool && ctx->pool->size() != n) {
+        delete ctx->pool;
+        ctx->pool = nullptr;
+    }
+    if (!ctx->pool) ctx->pool = new HostPool(ctx->device, n);
+    return ctx->pool;
+}
 
 struct DevGuard {
     explicit DevGuard(int d) { (void)hipSetDevice(d); }
@@ -177,6 +198,7 @@ extern "C" void rf_destroy(rf_ctx* ctx) {
     ctx->d_place.release();
     ctx->h_stage.release();
     rf_sha_plan_destroy(ctx->tplan);
+    delete ctx->pool;
     if (ctx->t0) (void)hipEventDestroy(ctx->t0);
     if (ctx->t1) (void)hipEventDestroy(ctx->t1);
     (void)hipStreamDestroy(ctx->stream);
@@ -187,6 +209,24 @@ extern "C" int rf_sync(rf_ctx* ctx) {
     ARG(ctx, "null ctx");
     DevGuard g(ctx->device);
     HIPC(hipStreamSynchronize(ctx->stream));
+    return RF_OK;
+}
+
+extern "C" int rf_set_host_threads(rf_ctx* ctx, int n) {
+    ARG(ctx, "null ctx");
+    ARG(n >= -1 && n <= 1024, "host threads must be -1 (default), 0 (none) or 1..1024");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->host_threads = n;
+    delete ctx->pool;
+    ctx->pool = nullptr;
+    return RF_OK;
+}
+
+extern "C" int rf_host_info(rf_ctx* ctx, int* threads, double* core_bytes_per_s, int* sha_ext) {
+    ARG(ctx, "null ctx");
+    if (threads) *threads = (int)ctx_host_threads(ctx);
+    if (core_bytes_per_s) *core_bytes_per_s = host_sha_rate();
+    if (sha_ext) *sha_ext = host_sha_available() ? 1 : 0;
     return RF_OK;
 }
 
@@ -339,20 +379,26 @@ extern "C" int rf_comm_allreduce_or(rf_comm* c, void* d_words, uint64_t nwords, 
 struct rf_sha_plan {
     rf_ctx* ctx = nullptr;
     uint64_t n = 0;
-    uint32_t n_lanes = 0, n_solo = 0, grid = 0, n_shards = 1;
+    uint32_t n_lanes = 0, n_solo = 0, n_host = 0, grid = 0, n_shards = 1;
     bool duo = true;  // wave-per-message kernel: two-lane chain (default) or one-lane
     bool pair = false;  // lane messages on k1_sha256_pair (latency-bound small sets)
     bool octo = false;  // ... or on k1_sha256_octo (eight per wave, two-lane chain)
     DevBuf d_offs, d_lens, d_order, d_heads;  // d_order = [lanes order | solo order]
+    // host leg: messages hashed by the context's HostPool, largest first;
+    // their digests go to HBM through h_dig -> d_dig -> scatter into out32
+    std::vector<HostTask> host;
+    DevBuf d_host_ids, d_host_dig;
+    HostBuf h_host_dig;
+    hipEvent_t e_hcopy = nullptr;
+    bool hcopy_pending = false;
+    float last_ms_host = 0.f;
     hipStream_t side = nullptr;
     hipEvent_t e0 = nullptr, e_solo = nullptr, e_lanes = nullptr, e1 = nullptr;
     bool ran = false;
     rf_sha_stats st{};
 };
 
-// Which messages run wave-per-message (the duo chain) and which lane per
-// message (pair or lanes kernel): the smallest makespan over k = the k largest
-// messages on duo waves, from measured per-block chain latencies:
+// Measured per-block chain latencies of the GPU legs:
 //   duo chain            1.13 us/block (one wave per message, one per SIMD)
 //   pair chain           1.9 us/block on configs[0] (lane messages <= 16 per
 //                        SIMD: one pair workgroup per CU) but 31-42 s on the
@@ -362,62 +408,149 @@ struct rf_sha_plan {
 //   octo chain           1.3 us/block (eight messages per wave; sets of <= 4
 //                        messages per SIMD, so the chain waves do not share)
 //   lanes, latency-bound 3.2 us/block; throughput 64 B x 35 T lane-ops/s / 1464
-// M(k) = max(duo: nb[0] x 1.13 us if k > 0,
-//            lane set: max(nb[k] x t_lane(n - k), sum_{i >= k} nb[i] x 1464 / 35e12)).
-// Ties keep the smaller k (fewer waves sharing SIMDs).
-static void plan_split(const std::vector<uint64_t>& nb, std::vector<uint32_t>& order, uint32_t n_cu,
-                       uint32_t flags, uint32_t* n_solo_out) {
+// For the size-sorted messages nbs[h..n) (blocks, descending; suf = suffix
+// sums) the GPU makespan of putting the k largest on duo waves is
+//   M(k) = max(duo: nbs[h] x 1.13 us if k > 0,
+//              lane set: max(nbs[h+k] x t_lane(n-h-k), suf[h+k] x 1464 / 35e12))
+// minimised over k <= #SIMDs; ties keep the smaller k.
+static double gpu_model(const std::vector<uint64_t>& nbs, const std::vector<double>& suf, uint64_t h,
+                        uint32_t n_cu, uint32_t flags, uint64_t* k_out) {
+    const double t_duo = 1.13e-6, t_octo = 1.3e-6, t_pair = 3.2e-6, t_lanes = 3.2e-6, blk_rate = 35e12 / 1464.0;
+    const uint64_t n = nbs.size();
+    *k_out = 0;
+    if (h >= n) return 0.0;
+    const uint64_t cnt = n - h;
+    if (flags & RF_SHA_ALL_SOLO) {
+        *k_out = cnt;
+        return (double)nbs[h] * t_duo;
+    }
+    const uint64_t n_simd = 4ull * n_cu;
+    const uint64_t cap = (flags & RF_SHA_NO_SOLO) ? 0 : std::min<uint64_t>(cnt, n_simd);
+    const bool pair_ok = !(flags & RF_SHA_NO_PAIR), octo_ok = !(flags & RF_SHA_NO_OCTO);
+    double best = 1e300;
+    for (uint64_t k = 0; k <= cap; ++k) {
+        const uint64_t lanes = cnt - k;
+        double m = k ? (double)nbs[h] * t_duo : 0.0;
+        if (lanes) {
+            const double tl = (octo_ok && lanes <= 4 * n_simd)   ? t_octo
+                              : (pair_ok && lanes <= 16 * n_simd) ? t_pair
+                                                                  : t_lanes;
+            m = std::max(m, std::max((double)nbs[h + k] * tl, suf[h + k] / blk_rate));
+        }
+        if (m < best * 0.98) {
+            best = m;
+            *k_out = k;
+        }
+    }
+    return best;
+}
+
+// The host leg's inputs to the split: threads, the per-thread SHA-NI rate
+// (bytes/s, measured on this machine) and, for messages resident in HBM,
+// the D2H link rate every host-leg byte crosses.
+struct HostModel {
+    unsigned threads = 0;
+    double rate = 0.0;
+    double link = 0.0;  // 0: messages already in host memory
+};
+
+// Which messages go to the host leg (the h largest) and how the rest split
+// over the GPU kernels.  The host leg's makespan for the h largest messages
+// is list scheduling in LPT order over `threads` threads (what the pool's
+// shared largest-first queue does), each message costing len/rate plus a
+// fixed 100 us (its first D2H chunk / queue hop), bounded below by the link;
+// plus 100 us to wake the pool.  host(h) grows with h, gpu(h) shrinks, so
+// the best h sits at their crossing; the smallest h reaching the best
+// makespan (2% margin) wins, so the GPU keeps every message the host leg
+// would not finish sooner.
+static void plan_split(const std::vector<uint64_t>& nb, const uint64_t* lens, std::vector<uint32_t>& order,
+                       uint32_t n_cu, uint32_t flags, const HostModel& hm, uint32_t* n_host_out,
+                       uint32_t* n_solo_out) {
     const uint64_t n = nb.size();
     order.resize(n);
     std::iota(order.begin(), order.end(), 0u);
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return nb[a] > nb[b]; });
-    uint32_t n_solo = 0;
-    if (flags & RF_SHA_ALL_SOLO) {
-        n_solo = (uint32_t)n;
-    } else if (!(flags & RF_SHA_NO_SOLO)) {
-        const double t_duo = 1.13e-6, t_octo = 1.3e-6, t_pair = 3.2e-6, t_lanes = 3.2e-6,
-                     blk_rate = 35e12 / 1464.0;
-        const uint64_t n_simd = 4ull * n_cu, cap = std::min<uint64_t>(n, n_simd);
-        double rest = 0;
-        for (uint64_t i = 0; i < n; ++i) rest += (double)nb[i];
-        const bool pair_ok = !(flags & RF_SHA_NO_PAIR);
-        const bool octo_ok = !(flags & RF_SHA_NO_OCTO);
-        double best = 1e300;
-        uint64_t best_k = 0;
-        for (uint64_t k = 0; k <= cap; ++k) {
-            if (k > 0) rest -= (double)nb[order[k - 1]];
-            const uint64_t lanes = n - k;
-            double m = k ? (double)nb[order[0]] * t_duo : 0.0;
-            if (lanes) {
-                const double tl = (octo_ok && lanes <= 4 * n_simd)   ? t_octo
-                                  : (pair_ok && lanes <= 16 * n_simd) ? t_pair
-                                                                      : t_lanes;
-                m = std::max(m, std::max((double)nb[order[k]] * tl, rest / blk_rate));
+    std::vector<uint64_t> nbs(n);
+    std::vector<double> suf(n + 1, 0.0);
+    for (uint64_t i = 0; i < n; ++i) nbs[i] = nb[order[i]];
+    for (uint64_t i = n; i-- > 0;) suf[i] = suf[i + 1] + (double)nbs[i];
+    uint64_t h = 0;
+    const bool host_ok = hm.threads > 0 && hm.rate > 0 && !(flags & RF_SHA_NO_HOST);
+    if (host_ok && (flags & RF_SHA_ALL_HOST)) {
+        h = n;
+    } else if (host_ok && n) {
+        std::vector<double> host_t(n + 1, 0.0);
+        std::vector<double> load(hm.threads, 0.0);  // min-heap of thread loads (s)
+        double maxload = 0, bytes = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            std::pop_heap(load.begin(), load.end(), std::greater<double>());
+            load.back() += (double)lens[order[i]] / hm.rate + 100e-6;
+            maxload = std::max(maxload, load.back());
+            std::push_heap(load.begin(), load.end(), std::greater<double>());
+            bytes += (double)lens[order[i]];
+            host_t[i + 1] = std::max(maxload, hm.link > 0 ? bytes / hm.link : 0.0) + 100e-6;
+        }
+        std::vector<double> gmemo(n + 1, -1.0);
+        auto gpu_t = [&](uint64_t x) {
+            if (gmemo[x] < 0) {
+                uint64_t k;
+                gmemo[x] = gpu_model(nbs, suf, x, n_cu, flags, &k);
             }
+            return gmemo[x];
+        };
+        // smallest x with host_t[x] >= gpu_t(x) (true at x = n, gpu_t(n) = 0)
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (host_t[mid] >= gpu_t(mid)) hi = mid; else lo = mid + 1;
+        }
+        const uint64_t x0 = lo;
+        double best = gpu_t(0);
+        uint64_t best_h = 0;
+        for (uint64_t c : {x0 > 0 ? x0 - 1 : 0, x0}) {
+            const double m = std::max(host_t[c], gpu_t(c));
             if (m < best * 0.98) {
                 best = m;
-                best_k = k;
+                best_h = c;
             }
         }
-        n_solo = (uint32_t)best_k;
+        // the smallest h with the same makespan (gpu_t is a step function
+        // of h: below the crossing the host leg only adds threads' work)
+        if (best_h > 0 && host_t[best_h] < gpu_t(best_h)) {
+            const double target = gpu_t(best_h);
+            uint64_t a = 0, b = best_h;
+            while (a < b) {
+                const uint64_t mid = (a + b) / 2;
+                if (gpu_t(mid) <= target) b = mid; else a = mid + 1;
+            }
+            best_h = a;
+        }
+        h = best_h;
     }
-    // solo messages go to the back of `order`: [lanes..., solo...]
+    uint64_t k = 0;
+    gpu_model(nbs, suf, h, n_cu, flags, &k);
+    // order = [host (largest first)..., lanes..., solo...]
     std::vector<uint32_t> o2;
     o2.reserve(n);
-    for (uint64_t i = n_solo; i < n; ++i) o2.push_back(order[i]);
-    for (uint64_t i = 0; i < n_solo; ++i) o2.push_back(order[i]);
+    for (uint64_t i = 0; i < h; ++i) o2.push_back(order[i]);
+    for (uint64_t i = h + k; i < n; ++i) o2.push_back(order[i]);
+    for (uint64_t i = h; i < h + k; ++i) o2.push_back(order[i]);
     order.swap(o2);
-    *n_solo_out = n_solo;
+    *n_host_out = (uint32_t)h;
+    *n_solo_out = (uint32_t)k;
 }
 
 extern "C" void rf_sha_plan_destroy(rf_sha_plan* p);
 
 // Fills plan p for (offs, lens): host-side split, device copies of the
 // offsets/lengths/order (buffers only grow), stream and events created once.
+// host_resident: the messages will be in host memory at run time (no D2H in
+// the host leg's cost).
 static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const uint64_t* lens, uint64_t n,
-                      uint32_t flags) {
+                      uint32_t flags, bool host_resident) {
     ARG(n == 0 || (offs && lens), "null offs/lens");
     ARG(n < 0xffffffffull, "too many messages");
+    ARG(!((flags & RF_SHA_ALL_HOST) && (flags & RF_SHA_NO_HOST)), "RF_SHA_ALL_HOST with RF_SHA_NO_HOST");
     std::vector<uint64_t> nb(n);
     uint64_t total_blocks = 0, max_blocks = 0, total_bytes = 0;
     for (uint64_t i = 0; i < n; ++i) {
@@ -427,16 +560,26 @@ static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const u
         max_blocks = std::max(max_blocks, nb[i]);
         total_bytes += lens[i];
     }
+    HostModel hm;
+    hm.threads = (flags & RF_SHA_NO_HOST) ? 0u : ctx_host_threads(ctx);
+    if ((flags & RF_SHA_ALL_HOST) && hm.threads == 0)
+        return fail(RF_EINVAL, "RF_SHA_ALL_HOST: the host leg is off (no SHA extensions, or 0 host threads)");
+    // per-thread rate with all threads busy: 0.9 x one core alone
+    hm.rate = hm.threads ? 0.9 * host_sha_rate() : 0.0;
+    hm.link = host_resident ? 0.0 : 40e9;  // PCIe Gen5 x16 D2H, sustained
     p->ctx = ctx;
     p->n = n;
     p->ran = false;
     p->st = rf_sha_stats{};
     std::vector<uint32_t> order;
-    uint32_t n_solo = 0;
-    plan_split(nb, order, (uint32_t)ctx->n_cu, flags, &n_solo);
+    uint32_t n_solo = 0, n_host = 0;
+    plan_split(nb, lens, order, (uint32_t)ctx->n_cu, flags, hm, &n_host, &n_solo);
+    p->n_host = n_host;
     p->n_solo = n_solo;
     p->duo = !(flags & RF_SHA_ONE_LANE_CHAIN);
-    p->n_lanes = (uint32_t)(n - n_solo);
+    p->n_lanes = (uint32_t)(n - n_solo - n_host);
+    p->host.resize(n_host);
+    for (uint32_t i = 0; i < n_host; ++i) p->host[i] = HostTask{order[i], offs[order[i]], lens[order[i]]};
     // The lanes kernel is persistent: enough 256-thread blocks for every lane
     // message, capped at 5 blocks per CU (its VGPR-limited residency).
     const uint64_t want = (p->n_lanes + sha_lanes_block() - 1) / sha_lanes_block();
@@ -449,22 +592,37 @@ static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const u
     // Up to 4 lane messages per SIMD: eight per wave on the two-lane chain
     // (k1_sha256_octo), 8 instead of 14 chain instructions per round.
     p->octo = !(flags & RF_SHA_NO_OCTO) && p->n_lanes > 0 && p->n_lanes <= 4ull * 4 * ctx->n_cu;
+    const uint64_t n_gpu = n - n_host;
     hipError_t e = hipSuccess;
     if ((e = p->d_offs.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
         (e = p->d_lens.ensure(8 * std::max<uint64_t>(n, 1))) != hipSuccess ||
-        (e = p->d_order.ensure(4 * std::max<uint64_t>(n, 1))) != hipSuccess ||
-        (e = p->d_heads.ensure(4 * 64)) != hipSuccess)
+        (e = p->d_order.ensure(4 * std::max<uint64_t>(n_gpu, 1))) != hipSuccess ||
+        (e = p->d_heads.ensure(4 * 64)) != hipSuccess ||
+        (e = p->d_host_ids.ensure(4 * std::max<uint64_t>(n_host, 1))) != hipSuccess ||
+        (e = p->d_host_dig.ensure(32 * std::max<uint64_t>(n_host, 1))) != hipSuccess)
         return fail(RF_ENOMEM, "plan alloc: %s", hipGetErrorString(e));
+    if (p->hcopy_pending) {  // a previous run's digest upload still reads h_host_dig
+        HIPC(hipEventSynchronize(p->e_hcopy));
+        p->hcopy_pending = false;
+    }
+    HIPC(p->h_host_dig.ensure(32 * std::max<uint64_t>(n_host, 1)));
     if (n) {
         HIPC(hipMemcpy(p->d_offs.p, offs, 8 * n, hipMemcpyHostToDevice));
         HIPC(hipMemcpy(p->d_lens.p, lens, 8 * n, hipMemcpyHostToDevice));
-        HIPC(hipMemcpy(p->d_order.p, order.data(), 4 * n, hipMemcpyHostToDevice));
+        if (n_gpu) HIPC(hipMemcpy(p->d_order.p, order.data() + n_host, 4 * n_gpu, hipMemcpyHostToDevice));
+        if (n_host) HIPC(hipMemcpy(p->d_host_ids.p, order.data(), 4 * n_host, hipMemcpyHostToDevice));
     }
     if (!p->side) HIPC(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
     for (hipEvent_t* ev : {&p->e0, &p->e_solo, &p->e_lanes, &p->e1})
         if (!*ev) HIPC(hipEventCreate(ev));
+    if (!p->e_hcopy) HIPC(hipEventCreateWithFlags(&p->e_hcopy, hipEventDisableTiming));
+    uint64_t host_bytes = 0;
+    for (const HostTask& t : p->host) host_bytes += t.len;
     p->st.n_msgs = n;
     p->st.n_solo = n_solo;
+    p->st.n_host = n_host;
+    p->st.host_bytes = host_bytes;
+    p->st.host_threads = n_host ? hm.threads : 0;
     p->st.total_blocks = total_blocks;
     p->st.max_blocks = max_blocks;
     p->st.total_bytes = total_bytes;
@@ -477,7 +635,7 @@ static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t*
     *out = nullptr;
     DevGuard g(ctx->device);
     auto* p = new rf_sha_plan();
-    const int rc = plan_setup(ctx, p, offs, lens, n, flags);
+    const int rc = plan_setup(ctx, p, offs, lens, n, flags, false);
     if (rc) {
         rf_sha_plan_destroy(p);
         return rc;
@@ -489,11 +647,12 @@ static int plan_create_nolock(rf_ctx* ctx, const uint64_t* offs, const uint64_t*
 // The context's own plan for one-shot batches (rf_sha256_batch/arena, the
 // Fileset digests): its stream, events and device buffers are created once
 // (a fresh plan costs ~4 ms of stream/event/allocation setup per call).
+// The messages of these batches sit in host memory (the pinned stage).
 static int transient_plan(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens, uint64_t n,
                           rf_sha_plan** out) {
     if (!ctx->tplan) ctx->tplan = new rf_sha_plan();
     *out = ctx->tplan;
-    return plan_setup(ctx, ctx->tplan, offs, lens, n, 0);
+    return plan_setup(ctx, ctx->tplan, offs, lens, n, 0, true);
 }
 
 extern "C" int rf_sha_plan_create(rf_ctx* ctx, const uint64_t* offs, const uint64_t* lens,
@@ -503,10 +662,15 @@ extern "C" int rf_sha_plan_create(rf_ctx* ctx, const uint64_t* offs, const uint6
     return plan_create_nolock(ctx, offs, lens, n, flags, out);
 }
 
-static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hipStream_t s) {
+// GPU legs are queued asynchronously on s (and the plan's side stream); the
+// host leg runs on the context's pool meanwhile and this call returns when
+// it is done, with the upload + scatter of its digests queued on s.  The
+// host leg reads h_arena (host memory) when given, else d_arena via D2H.
+static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hipStream_t s,
+                           const uint8_t* h_arena = nullptr) {
     HIPC(hipEventRecord(p->e0, s));
-    HIPC(hipMemsetAsync(p->d_heads.p, 0, 4 * 64, s));
     const uint32_t* order = p->d_order.as<uint32_t>();
+    if (p->n_lanes) HIPC(hipMemsetAsync(p->d_heads.p, 0, 4 * 64, s));
     if (p->n_solo) {
         HIPC(hipStreamWaitEvent(p->side, p->e0, 0));
         SoloArgs sa{static_cast<const uint8_t*>(d_arena), p->d_offs.as<uint64_t>(),
@@ -530,6 +694,26 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
         HIPC(launch_sha_lanes(la, p->grid, s));
     }
     HIPC(hipEventRecord(p->e_lanes, s));
+    p->last_ms_host = 0.f;
+    if (p->n_host) {
+        HostPool* pool = ctx_pool(p->ctx);
+        if (!pool) return fail(RF_EINVAL, "plan has a host leg but the context's host leg is off");
+        if (p->hcopy_pending) {
+            HIPC(hipEventSynchronize(p->e_hcopy));
+            p->hcopy_pending = false;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        std::string err;
+        if (!host_leg_run(*pool, p->host.data(), p->n_host, h_arena ? nullptr : static_cast<const uint8_t*>(d_arena),
+                          h_arena, p->e0, p->h_host_dig.bytes(), &err))
+            return fail(RF_EDEVICE, "%s", err.c_str());
+        p->last_ms_host = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        HIPC(hipMemcpyAsync(p->d_host_dig.p, p->h_host_dig.p, 32ull * p->n_host, hipMemcpyHostToDevice, s));
+        HIPC(hipEventRecord(p->e_hcopy, s));
+        p->hcopy_pending = true;
+        HIPC(launch_scatter_digests(static_cast<uint8_t*>(d_out), p->d_host_ids.as<uint32_t>(),
+                                    p->d_host_dig.as<uint8_t>(), p->n_host, s));
+    }
     if (p->n_solo) HIPC(hipStreamWaitEvent(s, p->e_solo, 0));
     HIPC(hipEventRecord(p->e1, s));
     p->ran = true;
@@ -560,6 +744,7 @@ extern "C" int rf_sha_plan_stats(rf_sha_plan* p, rf_sha_stats* out) {
         } else {
             p->st.last_ms_solo = 0.f;
         }
+        p->st.last_ms_host = p->last_ms_host;
     }
     *out = p->st;
     return RF_OK;
@@ -567,32 +752,38 @@ extern "C" int rf_sha_plan_stats(rf_sha_plan* p, rf_sha_stats* out) {
 
 extern "C" void rf_sha_plan_destroy(rf_sha_plan* p) {
     if (!p) return;
-    DevGuard g(p->ctx->device);
-    if (p->side) {
-        (void)hipStreamSynchronize(p->side);
-        (void)hipStreamDestroy(p->side);
+    if (p->ctx) {
+        DevGuard g(p->ctx->device);
+        if (p->side) {
+            (void)hipStreamSynchronize(p->side);
+            (void)hipStreamDestroy(p->side);
+        }
+        if (p->hcopy_pending) (void)hipEventSynchronize(p->e_hcopy);
+        for (hipEvent_t ev : {p->e0, p->e_solo, p->e_lanes, p->e1, p->e_hcopy})
+            if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {p->e0, p->e_solo, p->e_lanes, p->e1})
-        if (ev) (void)hipEventDestroy(ev);
     p->d_offs.release();
     p->d_lens.release();
     p->d_order.release();
     p->d_heads.release();
+    p->d_host_ids.release();
+    p->d_host_dig.release();
+    p->h_host_dig.release();
     delete p;
 }
 
-// Host-buffer batch: pack into pinned staging with 64-B aligned starts,
-// upload, plan, run, download.
 // The packed messages already in ctx->d_arena (queued on ctx->stream): plan,
-// run, download.
-static int sha_device_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
-                             const std::vector<uint64_t>& lens, uint8_t* out32) {
+// run, download.  h_arena: the same bytes in host memory, for the host leg.
+static int sha_device_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs, const std::vector<uint64_t>& lens,
+                             uint8_t* out32, const uint8_t* h_arena, rf_sha_plan* planned = nullptr) {
     const uint64_t n = lens.size();
     HIPC(ctx->d_out.ensure(32 * n));
-    rf_sha_plan* p = nullptr;
-    int rc = transient_plan(ctx, offs.data(), lens.data(), n, &p);
-    if (rc) return rc;
-    rc = plan_run_locked(p, ctx->d_arena.p, ctx->d_out.p, ctx->stream);
+    rf_sha_plan* p = planned;
+    if (!p) {
+        int rc = transient_plan(ctx, offs.data(), lens.data(), n, &p);
+        if (rc) return rc;
+    }
+    int rc = plan_run_locked(p, ctx->d_arena.p, ctx->d_out.p, ctx->stream, h_arena);
     if (rc == RF_OK) {
         hipError_t e = hipMemcpyAsync(out32, ctx->d_out.p, 32 * n, hipMemcpyDeviceToHost, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -601,13 +792,37 @@ static int sha_device_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
     return rc;
 }
 
+// Host-buffer batch packed in the pinned stage: plan first, upload only the
+// bytes of the messages the GPU legs hash (runs of consecutive GPU messages),
+// run, download.
 static int sha_host_packed(rf_ctx* ctx, const std::vector<uint64_t>& offs,
                            const std::vector<uint64_t>& lens, uint64_t arena_bytes,
                            uint8_t* out32) {
+    const uint64_t n = lens.size();
     HIPC(ctx->d_arena.ensure(arena_bytes + 64));
-    HIPC(hipMemcpyAsync(ctx->d_arena.p, ctx->h_stage.p, arena_bytes, hipMemcpyHostToDevice,
-                        ctx->stream));
-    return sha_device_packed(ctx, offs, lens, out32);
+    rf_sha_plan* p = nullptr;
+    int rc = transient_plan(ctx, offs.data(), lens.data(), n, &p);
+    if (rc) return rc;
+    if (p->n_host == 0) {
+        HIPC(hipMemcpyAsync(ctx->d_arena.p, ctx->h_stage.p, arena_bytes, hipMemcpyHostToDevice, ctx->stream));
+    } else if (p->n_host < n) {
+        std::vector<uint8_t> on_host(n, 0);
+        for (const HostTask& t : p->host) on_host[t.id] = 1;
+        for (uint64_t i = 0; i < n;) {
+            if (on_host[i]) {
+                ++i;
+                continue;
+            }
+            uint64_t j = i;
+            while (j + 1 < n && !on_host[j + 1]) ++j;
+            const uint64_t b0 = offs[i], b1 = offs[j] + lens[j];
+            if (b1 > b0)
+                HIPC(hipMemcpyAsync(ctx->d_arena.as<uint8_t>() + b0, ctx->h_stage.bytes() + b0, b1 - b0,
+                                    hipMemcpyHostToDevice, ctx->stream));
+            i = j + 1;
+        }
+    }
+    return sha_device_packed(ctx, offs, lens, out32, ctx->h_stage.bytes(), p);
 }
 
 extern "C" int rf_sha256_batch(rf_ctx* ctx, const uint8_t* const* msgs, const uint64_t* lens,
@@ -1014,7 +1229,7 @@ extern "C" int rf_install_dir(rf_ctx* ctx, const char* root, rf_install** out) {
             return fail(RF_EIO, "%s", first_err.c_str());
         }
         HIPC(he);
-        rc = sha_device_packed(ctx, offs, lens, in->ids.data() + 32 * c0);
+        rc = sha_device_packed(ctx, offs, lens, in->ids.data() + 32 * c0, ctx->h_stage.bytes());
         if (rc) return rc;
         c0 = c1;
     }

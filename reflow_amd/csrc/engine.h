@@ -40,6 +40,10 @@ hipError_t launch_sha_pair(const SoloArgs& a, hipStream_t s);
 // Eight messages per wave on the duo's two-lane chain (small sets).
 hipError_t launch_sha_octo(const SoloArgs& a, hipStream_t s);
 
+// out32[ids[i]] = digs32[i] (the host leg's digests into the plan's output).
+hipError_t launch_scatter_digests(uint8_t* out32, const uint32_t* ids, const uint8_t* digs32, uint64_t n,
+                                  hipStream_t s);
+
 // Checks that the gfx950 code object of this library loads on the device.
 hipError_t probe_kernels();
 

@@ -694,6 +694,23 @@ __global__ __launch_bounds__(256) void k_gen_fill(uint8_t* arena, const uint64_t
     }
 }
 
+// The host leg's digests into the plan's output rows: one 16-B half per lane.
+__global__ __launch_bounds__(256) void k_scatter_digests(uint8_t* __restrict__ out, const uint32_t* __restrict__ ids,
+                                                         const uint8_t* __restrict__ digs, uint64_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * n) return;
+    const uint64_t i = t >> 1, half = t & 1;
+    reinterpret_cast<uint4*>(out + 32ull * ids[i])[half] = reinterpret_cast<const uint4*>(digs + 32 * i)[half];
+}
+
+hipError_t launch_scatter_digests(uint8_t* out32, const uint32_t* ids, const uint8_t* digs32, uint64_t n,
+                                  hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t grid = (2 * n + 255) / 256;
+    hipLaunchKernelGGL(k_scatter_digests, dim3((uint32_t)grid), dim3(256), 0, s, out32, ids, digs32, n);
+    return hipGetLastError();
+}
+
 uint32_t sha_lanes_block() { return kLanesBlock; }
 
 hipError_t probe_kernels() {

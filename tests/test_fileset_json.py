@@ -120,7 +120,7 @@ def test_capi_marshal_rejects_duplicates_and_zero_ids():
 @pytest.mark.gpu
 def test_gpu_value_digests_random():
     from reflow_amd import capi
-    ctx = capi.Context(0)
+    ctx = capi.Context(0, host_threads=0)
     rng = random.Random(0x7A1)
     sets = [_random_tree(rng) for _ in range(200)]
     # plus a large value: a 20k-file Map (JSON ~2 MB, one long K1 message)

@@ -140,7 +140,7 @@ def test_bloom_fixture_oracle():
 @pytest.fixture(scope="module")
 def ctx():
     from reflow_amd import capi
-    c = capi.Context(0)
+    c = capi.Context(0, host_threads=0)
     yield c
     c.close()
 

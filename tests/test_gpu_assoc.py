@@ -16,7 +16,7 @@ ZERO = bytes(32)
 @pytest.fixture(scope="module")
 def ctx():
     from reflow_amd import capi
-    c = capi.Context(0)
+    c = capi.Context(0, host_threads=0)
     yield c
     c.close()
 

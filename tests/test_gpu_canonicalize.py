@@ -66,7 +66,7 @@ def test_oracle_canonicalize_reference_shape():
 @pytest.fixture(scope="module")
 def ctx():
     from reflow_amd import capi
-    c = capi.Context(0)
+    c = capi.Context(0, host_threads=0)
     yield c
     c.close()
 

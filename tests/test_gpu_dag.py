@@ -17,7 +17,7 @@ PHYS = {"pR1": "R1", "pE1": "E1", "pE2": "E2", "pE3": "E3", "pES": "ES", "pXS": 
 @pytest.fixture(scope="module")
 def ctx():
     from reflow_amd import capi
-    c = capi.Context(0)
+    c = capi.Context(0, host_threads=0)
     yield c
     c.close()
 

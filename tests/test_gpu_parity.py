@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def ctx():
     from reflow_amd import capi
-    c = capi.Context(0)
+    c = capi.Context(0, host_threads=0)
     yield c
     c.close()
 

@@ -78,7 +78,7 @@ def test_oracle_missing_root_and_order(tmp_path):
 @pytest.fixture(scope="module")
 def ctx():
     from reflow_amd import capi
-    c = capi.Context(0)
+    c = capi.Context(0, host_threads=0)
     yield c
     c.close()
 
