@@ -218,7 +218,7 @@ class Eval {
         std::vector<std::pair<uint32_t, uint32_t>> holes;  // (byte pos, slot)
         uint32_t out;
     };
-    void material(const Flow* f, bool v1, std::string& out, std::vector<std::pair<uint32_t, uint32_t>>& holes);
+    void material(const Flow* f, std::string& out, std::vector<std::pair<uint32_t, uint32_t>>& holes);
     void fileset_material(const Fileset& v, std::string& out,
                           std::vector<std::pair<uint32_t, uint32_t>>& holes);
     uint32_t lower(const Flow* f);

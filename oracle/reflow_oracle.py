@@ -336,20 +336,29 @@ class OFlow:
         self.err = kw.get("err", False)
 
     # Flow.WriteDigest (flow.go:675-750)
-    def material(self, universe: bytes = b"", v1=False) -> bytes:
-        v1 = v1 or self.hashv1
+    def material(self, universe: bytes = b"", merged=False) -> bytes:
+        """Each node's OWN Config.HashV1 decides whether its deps are inlined
+        (dep.WriteDigest) or written as WD(dep.Digest()) (flow.go:692-697);
+        an inlined dep then follows its own config in turn.  `merged` says
+        this node is a Canonicalize copy under Config{HashV1: true}
+        (flow.go:820-823: f.Copy() + Config.Merge): its Deps (and OpRequirements'
+        dep) are canonical copies merged the same way, and so is its MapFlow
+        (MapInit through the canonicalizing MapFunc wrapper, :828-835); its
+        Parent is not -- Copy keeps the pointer and canonicalize never visits
+        it -- so the Parent writes with its own config (flow.go:680-685)."""
+        v1 = self.hashv1 or merged
         w = [universe]
         if self.op == OP["OpRequirements"]:
-            return universe + self.deps[0].material(universe, v1)
+            return universe + self.deps[0].material(universe, merged)
         if self.parent is not None:
-            return universe + self.parent.material(universe, v1)
+            return universe + self.parent.material(universe, False)
         for d in self.deps:
-            w.append(d.material(universe, v1) if v1 else WD(d.digest(universe, v1)))
+            w.append(d.material(universe, merged) if v1 else WD(d.digest(universe, merged)))
         w.append(op_digest_string(self.op).encode())
-        w.append(self.params(universe, v1))
+        w.append(self.params(universe, merged))
         return b"".join(w)
 
-    def params(self, universe, v1) -> bytes:
+    def params(self, universe, merged) -> bytes:
         op = self.op
         if op in (OP["OpIntern"], OP["OpExtern"]):
             return self.url.encode()
@@ -358,7 +367,7 @@ class OFlow:
         if op == OP["OpGroupby"]:
             return self.re.encode()
         if op == OP["OpMap"]:
-            return self.mapflow.material(universe, v1)
+            return self.mapflow.material(universe, merged)
         if op == OP["OpCollect"]:
             return self.re.encode() + self.repl.encode()
         if op == OP["OpVal"]:
@@ -381,8 +390,8 @@ class OFlow:
             out += writeN(-idx if is_out else idx)
         return out
 
-    def digest(self, universe: bytes = b"", v1=False) -> bytes:
-        return sha256(self.material(universe, v1))
+    def digest(self, universe: bytes = b"", merged=False) -> bytes:
+        return sha256(self.material(universe, merged))
 
     # Flow.PhysicalDigest (flow.go:764-792); None == zero digest
     def physical_material(self):
@@ -404,12 +413,12 @@ class OFlow:
         return None if m is None else sha256(m)
 
     # Flow.CacheKeys (flow.go:796-802)
-    def cache_keys(self, universe: bytes = b"", v1=False):
+    def cache_keys(self, universe: bytes = b"", merged=False):
         keys = []
         p = self.physical_digest()
         if p is not None:
             keys.append(p)
-        keys.append(self.digest(universe, v1))
+        keys.append(self.digest(universe, merged))
         return keys
 
 
@@ -425,14 +434,14 @@ def canonicalize(root: OFlow, hashv1: bool = False, universe: bytes = b""):
     out = {}
     memo = {}
 
-    def dig(f, v1):  # Flow.Digest is sync.Once-memoized per node (flow.go:653-664)
-        key = (id(f), v1)
+    def dig(f, merged):  # Flow.Digest is sync.Once-memoized per node (flow.go:653-664)
+        key = (id(f), merged)
         if key not in memo:
-            memo[key] = f.digest(universe, v1)
+            memo[key] = f.digest(universe, merged)
         return memo[key]
 
     def rec(f):
-        hit = m.get(dig(f, f.hashv1))
+        hit = m.get(dig(f, False))  # the original node's own digest
         if hit is not None:
             out.setdefault(id(f), hit)
             return hit
@@ -440,7 +449,7 @@ def canonicalize(root: OFlow, hashv1: bool = False, universe: bytes = b""):
             rec(d)
         if f.mapflow is not None:
             rec(f.mapflow)
-        d = dig(f, f.hashv1 or hashv1)
+        d = dig(f, hashv1)  # the copy's, Config merged
         got = m.setdefault(d, f)
         out.setdefault(id(f), got)
         return got

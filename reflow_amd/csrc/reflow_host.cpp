@@ -332,22 +332,24 @@ void Eval::fileset_material(const Fileset& v, std::string& out,
     }
 }
 
-// Flow.WriteDigest (flow.go:675-750) with WD(dep.Digest()) as holes.
-void Eval::material(const Flow* f, bool v1, std::string& out,
-                    std::vector<std::pair<uint32_t, uint32_t>>& holes) {
-    v1 = v1 || f->config.HashV1;
+// Flow.WriteDigest (flow.go:675-750) with WD(dep.Digest()) as holes.  Each
+// node's own Config.HashV1 decides whether its deps are inlined (flow.go:
+// 692-697); an inlined dep follows its own config in turn, and so does a
+// Parent (Canonicalize merges the config into the copies it makes, never
+// into f.Parent: flow.go:818-843).
+void Eval::material(const Flow* f, std::string& out, std::vector<std::pair<uint32_t, uint32_t>>& holes) {
     out += U_;
     if (f->op == OpRequirements) {
-        material(f->Deps.at(0), v1, out, holes);
+        material(f->Deps.at(0), out, holes);
         return;
     }
     if (f->Parent) {
-        material(f->Parent, v1, out, holes);
+        material(f->Parent, out, holes);
         return;
     }
     for (const Flow* d : f->Deps) {
-        if (v1) {
-            material(d, v1, out, holes);
+        if (f->config.HashV1) {
+            material(d, out, holes);
         } else {
             const uint32_t s = lower(d);
             out.push_back('\0');
@@ -362,7 +364,7 @@ void Eval::material(const Flow* f, bool v1, std::string& out,
     case OpExtern: out += f->URL; break;
     case OpExec: exec_suffix(f, out); break;
     case OpGroupby: out += f->Re; break;
-    case OpMap: material(f->MapFlow, v1, out, holes); break;
+    case OpMap: material(f->MapFlow, out, holes); break;
     case OpCollect: out += f->Re; out += f->Repl; break;
     case OpVal:
         if (f->Err) throw Error(RF_EINVAL, "error OpVal digests are random (flow.go:722-731)");
@@ -387,7 +389,7 @@ uint32_t Eval::lower(const Flow* f) {
     auto it = logical_.find(f);
     if (it != logical_.end()) return it->second;
     Job j;
-    material(f, false, j.tmpl, j.holes);
+    material(f, j.tmpl, j.holes);
     j.out = new_slot();
     logical_[f] = j.out;
     jobs_.push_back(std::move(j));

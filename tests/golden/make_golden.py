@@ -102,7 +102,7 @@ def values_map():
 def check_reference_kats():
     got = {
         "flow_test.go:34": O.digest_string(stable_flow().digest()),
-        "flow_test.go:33": O.digest_string(stable_flow().digest(v1=True)),
+        "flow_test.go:33": O.digest_string(stable_flow().digest(merged=True)),
         "executor_test.go:77": O.digest_string(vlist().digest()),
         "syntax/digest_test.go:25": O.digest_string(syntax_exec_chain().digest()),
         "values/digest_test.go:28": O.digest_string(O.sha256(values_map())),
@@ -238,6 +238,20 @@ def flow_case(name, root, universe=b"", v1=False):
     return {"name": name, "universe": universe.decode(), "v1": v1, "flow": flow_to_json(root), "nodes": per}
 
 
+def mixed_config_flows():
+    """(name, root, universe, merged): flows whose nodes carry different
+    HashV1 configs; tests/test_oracle_golden.py pins their bytes by hand."""
+    c = OFlow("OpIntern", url="s3://mix")
+    b_v2 = OFlow("OpCoerce", [c], flow_digest=from_string("b"))
+    a_v1 = OFlow("OpExec", [b_v2], image="img", cmd="cmd", argmap=[(False, 0)], hashv1=True)
+    p_v2 = OFlow("OpCoerce", [c], flow_digest=from_string("p"))
+    k_v1 = OFlow("OpK", [c], flow_digest=from_string("k"), parent=p_v2, hashv1=True)
+    return [("HashV1 node over a V2 dep", a_v1, b"", False),
+            ("V2 node over a HashV1 dep", OFlow("OpMerge", [a_v1]), b"", False),
+            ("HashV1 node whose Parent is V2", k_v1, b"", False),
+            ("Canonicalize(HashV1) copy whose Parent is V2, Universe", OFlow("OpMerge", [k_v1]), b"U", True)]
+
+
 def gen_flows():
     from flowgen import random_dag
     cases = [flow_case("TestDigestStability V2 (flow_test.go:34)", stable_flow()),
@@ -256,6 +270,10 @@ def gen_flows():
     edge = OFlow("OpMerge", [ext, OFlow("OpPullup", [ex])])
     cases.append(flow_case("edge ops", edge))
     cases.append(flow_case("edge ops, Universe", edge, universe=b"U"))
+    # HashV1 is each node's OWN config (flow.go:692-697); Canonicalize merges
+    # it into the copies it makes, never into a Parent (flow.go:818-843)
+    for name, root, u, merged in mixed_config_flows():
+        cases.append(flow_case(name, root, universe=u, v1=merged))
     for seed, u in [(101, b""), (102, b"universe-x"), (103, b"")]:
         root, _ = random_dag(seed, n=40)
         cases.append(flow_case("random_dag seed %d" % seed, root, universe=u))

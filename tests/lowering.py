@@ -77,19 +77,22 @@ class Lowerer:
                 out.append(b"\x00\x05" + fid)
         return out
 
-    def _material(self, f: OFlow, v1: bool):
-        v1 = v1 or f.hashv1
+    def _material(self, f: OFlow, merged: bool):
+        """Flow.WriteDigest (flow.go:675-750) with WD(dep.Digest()) as holes:
+        the node's own HashV1 (or the Canonicalize merge) decides inlining;
+        the Parent keeps its own config (see reflow_oracle.OFlow.material)."""
+        v1 = merged or f.hashv1
         U = self.U
         if f.op == OP["OpRequirements"]:
-            return [U] + self._material(f.deps[0], v1)
+            return [U] + self._material(f.deps[0], merged)
         if f.parent is not None:
-            return [U] + self._material(f.parent, v1)
+            return [U] + self._material(f.parent, False)
         out = [U]
         for d in f.deps:
             if v1:
-                out += self._material(d, v1)
+                out += self._material(d, merged)
             else:
-                out += self._wd_hole(self.lower(d))
+                out += self._wd_hole(self.lower(d, merged))
         out.append(op_digest_string(f.op).encode())
         op = f.op
         if op in (OP["OpIntern"], OP["OpExtern"]):
@@ -99,7 +102,7 @@ class Lowerer:
         elif op == OP["OpGroupby"]:
             out.append(f.re.encode())
         elif op == OP["OpMap"]:
-            out += self._material(f.mapflow, v1)
+            out += self._material(f.mapflow, merged)
         elif op == OP["OpCollect"]:
             out.append(f.re.encode() + f.repl.encode())
         elif op == OP["OpVal"]:
@@ -125,11 +128,12 @@ class Lowerer:
         self.L.jobs.append((slot, mat, holes))
 
     def lower(self, f: OFlow, v1=False) -> int:
-        """Logical digest slot of f (jobs for its deps are emitted first)."""
-        key = id(f)
+        """Logical digest slot of f (jobs for its deps are emitted first);
+        v1 = f is a Canonicalize copy under Config{HashV1: true}."""
+        key = (id(f), bool(v1))
         if key in self.L.logical:
             return self.L.logical[key]
-        pieces = self._material(f, v1)
+        pieces = self._material(f, bool(v1))
         slot = self.L.new_slot()
         self.L.logical[key] = slot
         self._emit(slot, pieces)

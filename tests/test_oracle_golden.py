@@ -43,7 +43,7 @@ def test_stable_v2():
 def test_stable_v1_after_canonicalize():
     # Canonicalize(Config{HashV1: true}) merges HashV1 into every node,
     # including the re-initialized MapFlow (flow.go:814-843).
-    assert O.digest_string(stable_flow().digest(v1=True)) == STABLE_V1
+    assert O.digest_string(stable_flow().digest(merged=True)) == STABLE_V1
 
 
 def test_value_digest_vlist():
@@ -155,3 +155,40 @@ def test_bloom_roundtrip_oracle():
 def test_estimate_parameters_c5():
     # n = 1e8, p = 0.001
     assert O.estimate_parameters(10**8, 0.001) == (1437758757, 10)
+
+
+def test_hashv1_is_each_nodes_own_config():
+    """flow.go:692-697 reads f.Config.HashV1 of the node being written: a V1
+    node inlines a V2 dep's material, and that dep then writes ITS deps as
+    WD(digest); a Parent writes with its own config (Canonicalize merges the
+    config into copies, never into f.Parent, flow.go:818-843).  Bytes derived
+    by hand from the flow.go grammar with hashlib, not the oracle's recursion;
+    the same flows are fixture cases (make_golden.mixed_config_flows) that the
+    GPU path is checked against in test_golden_fixtures.py."""
+    import hashlib
+    import struct
+
+    import make_golden as MG
+
+    def H(b):
+        return hashlib.sha256(b).digest()
+
+    def WD(d):
+        return b"\x00\x05" + d
+
+    cases = {name: (root, u, merged) for name, root, u, merged in MG.mixed_config_flows()}
+    c_mat = b"OpIntern" + b"s3://mix"
+    b_mat = WD(H(c_mat)) + b"OpCoerce" + WD(H(b"b"))            # V2: dep as WD(digest)
+    a_mat = b_mat + b"OpExec" + b"img" + b"cmd" + struct.pack("<q", 0)  # V1: dep inlined
+    root, u, merged = cases["HashV1 node over a V2 dep"]
+    assert root.digest(u, merged) == H(a_mat)
+    root, u, merged = cases["V2 node over a HashV1 dep"]
+    assert root.digest(u, merged) == H(WD(H(a_mat)) + b"OpMerge")
+    p_mat = WD(H(c_mat)) + b"OpCoerce" + WD(H(b"p"))
+    root, u, merged = cases["HashV1 node whose Parent is V2"]
+    assert root.digest(u, merged) == H(p_mat)                   # U = "": Parent's own material
+    root, u, merged = cases["Canonicalize(HashV1) copy whose Parent is V2, Universe"]
+    U = b"U"
+    p_mat_u = U + WD(H(U + c_mat)) + b"OpCoerce" + WD(H(b"p"))
+    k_mat_u = U + p_mat_u                                       # Parent-forwarded: U written again
+    assert merged and root.digest(u, merged) == H(U + k_mat_u + b"OpMerge")  # merged copy inlines its dep
