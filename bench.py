@@ -262,7 +262,7 @@ def bench_sha(args, dist, ctx, budget):
             else "k1_sha256_lanes"
         legs.append((lk, lane_ids, float(np.mean(rec["lanes"]))))
     dom = max(legs, key=lambda x: x[2]) if legs else None
-    roof = kernel_roofline(*dom) if dom else None
+    roof = kernel_roofline(dom[0], lens, dom[1], dom[2]) if dom else None
     workload = ("configs[1]: %.1f GiB Fileset per GPU, %d files 4 KiB-2 GiB (98%% log-uniform 4 KiB-1 MiB, "
                 "2%% 64 MiB-2 GiB), SHA-256 of every file" % (lens.sum() / GiB, len(lens)))
     if roof:

@@ -702,10 +702,13 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
             HIPC(hipEventSynchronize(p->e_hcopy));
             p->hcopy_pending = false;
         }
+        // the arena's bytes are written once the work queued on s before e0
+        // is done (a host-side wait: see HostPool::Stage on stream-side waits)
+        if (!h_arena) HIPC(hipEventSynchronize(p->e0));
         const auto t0 = std::chrono::steady_clock::now();
         std::string err;
         if (!host_leg_run(*pool, p->host.data(), p->n_host, h_arena ? nullptr : static_cast<const uint8_t*>(d_arena),
-                          h_arena, p->e0, p->h_host_dig.bytes(), &err))
+                          h_arena, p->h_host_dig.bytes(), &err))
             return fail(RF_EDEVICE, "%s", err.c_str());
         p->last_ms_host = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         HIPC(hipMemcpyAsync(p->d_host_dig.p, p->h_host_dig.p, 32ull * p->n_host, hipMemcpyHostToDevice, s));

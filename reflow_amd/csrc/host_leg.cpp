@@ -8,11 +8,31 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 
 #include "host_sha.h"
 
 namespace rf {
+
+uint64_t host_chunk_bytes() {
+    static const uint64_t c = [] {
+        const char* v = getenv("RF_HOST_CHUNK_MB");
+        const uint64_t mb = v ? (uint64_t)std::max(1, atoi(v)) : 8ull;
+        return mb << 20;
+    }();
+    return c;
+}
+
+// RF_HOST_LEG_TIMING=1: per-run totals of the host threads' time waiting for
+// D2H chunks and hashing (stderr; diagnostic).
+static bool leg_timing() {
+    static const bool on = getenv("RF_HOST_LEG_TIMING") != nullptr;
+    return on;
+}
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // CPUs the cgroup (v2 cpu.max, or v1 cfs quota) lets this process use; 0 = no limit.
 static unsigned cgroup_cpus() {
@@ -61,14 +81,14 @@ HostPool::~HostPool() {
     cv_.notify_all();
     for (auto& t : th_) t.join();
     (void)hipSetDevice(device_);
-    for (Stage& s : stages_) {
-        if (s.s) (void)hipStreamSynchronize(s.s);
+    for (Stage& s : stages_)
         for (int i = 0; i < 2; ++i) {
+            if (s.s[i]) {
+                (void)hipStreamSynchronize(s.s[i]);
+                (void)hipStreamDestroy(s.s[i]);
+            }
             if (s.buf[i]) (void)hipHostFree(s.buf[i]);
-            if (s.ev[i]) (void)hipEventDestroy(s.ev[i]);
         }
-        if (s.s) (void)hipStreamDestroy(s.s);
-    }
 }
 
 void HostPool::loop(unsigned w) {
@@ -105,40 +125,44 @@ void HostPool::run(const std::function<void(unsigned)>& fn) {
 hipError_t HostPool::stage(unsigned w, Stage** out) {
     Stage& s = stages_[w];
     *out = &s;
-    if (s.s) return hipSuccess;
+    if (s.buf[1]) return hipSuccess;
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking)) != hipSuccess) return e;
     for (int i = 0; i < 2; ++i) {
-        if ((e = hipEventCreateWithFlags(&s.ev[i], hipEventDisableTiming)) != hipSuccess) return e;
+        if (!s.s[i] && (e = hipStreamCreateWithFlags(&s.s[i], hipStreamNonBlocking)) != hipSuccess) return e;
+        if (s.buf[i]) continue;
         void* p = nullptr;
-        if ((e = hipHostMalloc(&p, kHostChunk, hipHostMallocDefault)) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&p, host_chunk_bytes(), hipHostMallocDefault)) != hipSuccess) return e;
         s.buf[i] = static_cast<uint8_t*>(p);
     }
     return hipSuccess;
 }
 
 // One message resident in HBM: chunk c+1's D2H is queued before chunk c is
-// hashed, so the copy engine and the core overlap.
-static hipError_t hash_device_message(HostPool::Stage* st, const uint8_t* src, uint64_t len, uint8_t* out32) {
+// hashed, so the copy engine and the core overlap.  wait/hash (optional)
+// accumulate the seconds spent waiting for chunks and hashing.
+static hipError_t hash_device_message(HostPool::Stage* st, const uint8_t* src, uint64_t len, uint8_t* out32,
+                                      double* wait, double* hash) {
+    const uint64_t C = host_chunk_bytes();
     uint32_t h[8];
     host_sha_init(h);
-    const uint64_t nch = len ? (len + kHostChunk - 1) / kHostChunk : 0;
+    const uint64_t nch = len ? (len + C - 1) / C : 0;
     auto issue = [&](uint64_t c) -> hipError_t {
-        const uint64_t off = c * kHostChunk, sz = std::min(kHostChunk, len - off);
-        hipError_t e = hipMemcpyAsync(st->buf[c & 1], src + off, sz, hipMemcpyDeviceToHost, st->s);
-        return e == hipSuccess ? hipEventRecord(st->ev[c & 1], st->s) : e;
+        const uint64_t off = c * C, sz = std::min(C, len - off);
+        return hipMemcpyAsync(st->buf[c & 1], src + off, sz, hipMemcpyDeviceToHost, st->s[c & 1]);
     };
     hipError_t e = hipSuccess;
     if (nch) e = issue(0);
     for (uint64_t c = 0; c < nch && e == hipSuccess; ++c) {
         if (c + 1 < nch && (e = issue(c + 1)) != hipSuccess) break;
-        if ((e = hipEventSynchronize(st->ev[c & 1])) != hipSuccess) break;
-        const uint64_t sz = std::min(kHostChunk, len - c * kHostChunk);
-        if (c + 1 < nch) {
-            host_sha_blocks(h, st->buf[c & 1], sz / 64);
-        } else {
-            host_sha_blocks(h, st->buf[c & 1], sz / 64);
-            host_sha_final(h, st->buf[c & 1] + (sz & ~63ull), sz & 63, len, out32);
+        const double t0 = wait ? now_s() : 0;
+        if ((e = hipStreamSynchronize(st->s[c & 1])) != hipSuccess) break;
+        const double t1 = wait ? now_s() : 0;
+        const uint64_t sz = std::min(C, len - c * C);
+        host_sha_blocks(h, st->buf[c & 1], sz / 64);
+        if (c + 1 == nch) host_sha_final(h, st->buf[c & 1] + (sz & ~63ull), sz & 63, len, out32);
+        if (wait) {
+            *wait += t1 - t0;
+            *hash += now_s() - t1;
         }
     }
     if (e == hipSuccess && nch == 0) host_sha_final(h, nullptr, 0, 0, out32);
@@ -146,15 +170,18 @@ static hipError_t hash_device_message(HostPool::Stage* st, const uint8_t* src, u
 }
 
 bool host_leg_run(HostPool& pool, const HostTask* tasks, uint64_t n, const uint8_t* d_arena,
-                  const uint8_t* h_arena, hipEvent_t wait_ev, uint8_t* out32, std::string* err) {
+                  const uint8_t* h_arena, uint8_t* out32, std::string* err) {
     std::atomic<uint64_t> next{0};
     std::atomic<bool> bad{false};
     std::mutex emu;
+    const bool timing = leg_timing();
+    std::vector<double> tw(pool.size(), 0.0), th(pool.size(), 0.0), tt(pool.size(), 0.0);
+    const double t_run = timing ? now_s() : 0;
     pool.run([&](unsigned w) {
+        const double t_start = timing ? now_s() : 0;
         HostPool::Stage* st = nullptr;
         if (d_arena) {
-            hipError_t e = pool.stage(w, &st);
-            if (e == hipSuccess && wait_ev) e = hipStreamWaitEvent(st->s, wait_ev, 0);
+            const hipError_t e = pool.stage(w, &st);
             if (e != hipSuccess) {
                 std::lock_guard<std::mutex> lk(emu);
                 if (!bad.exchange(true)) *err = std::string("host leg stage: ") + hipGetErrorString(e);
@@ -167,13 +194,29 @@ bool host_leg_run(HostPool& pool, const HostTask* tasks, uint64_t n, const uint8
                 host_sha256(h_arena + t.off, t.len, out32 + 32 * i);
                 continue;
             }
-            const hipError_t e = hash_device_message(st, d_arena + t.off, t.len, out32 + 32 * i);
+            const hipError_t e = hash_device_message(st, d_arena + t.off, t.len, out32 + 32 * i,
+                                                     timing ? &tw[w] : nullptr, timing ? &th[w] : nullptr);
             if (e != hipSuccess) {
                 std::lock_guard<std::mutex> lk(emu);
                 if (!bad.exchange(true)) *err = std::string("host leg D2H: ") + hipGetErrorString(e);
             }
         }
+        if (timing) tt[w] = now_s() - t_start;
     });
+    if (timing) {
+        double sw = 0, sh = 0, mx = 0;
+        for (unsigned w = 0; w < pool.size(); ++w) {
+            sw += tw[w];
+            sh += th[w];
+            mx = std::max(mx, tt[w]);
+        }
+        uint64_t bytes = 0;
+        for (uint64_t i = 0; i < n; ++i) bytes += tasks[i].len;
+        fprintf(stderr, "[host leg] %u threads, %llu msgs, %.2f GB: wall %.1f ms, slowest thread %.1f ms; "
+                        "sum wait %.1f ms, sum hash %.1f ms (%.2f GB/s per hashing thread)\n",
+                pool.size(), (unsigned long long)n, bytes / 1e9, (now_s() - t_run) * 1e3, mx * 1e3, sw * 1e3,
+                sh * 1e3, sh > 0 ? bytes / sh / 1e9 : 0.0);
+    }
     return !bad.load();
 }
 

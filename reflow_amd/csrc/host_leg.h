@@ -17,8 +17,9 @@
 
 namespace rf {
 
-// D2H chunk of one host thread (a multiple of 64: whole SHA-256 blocks).
-constexpr uint64_t kHostChunk = 8ull << 20;
+// D2H chunk of one host thread (a multiple of 64: whole SHA-256 blocks);
+// RF_HOST_CHUNK_MB overrides it (tuning experiments).
+uint64_t host_chunk_bytes();
 
 // Default host-leg width: min(60, the process's CPU share).  60 is the
 // reference's DigestLimiter (local/executor.go:41); the share is the smaller
@@ -29,9 +30,16 @@ unsigned host_default_threads();
 
 class HostPool {
    public:
-    struct Stage {  // per-thread D2H staging, created on first use
-        hipStream_t s = nullptr;
-        hipEvent_t ev[2] = {nullptr, nullptr};
+    // Per-thread D2H staging, created on first use: one stream per buffer,
+    // waited on with hipStreamSynchronize.  Not events: hipEventRecord (and
+    // hipStreamWaitEvent) put marker/barrier packets into a hardware queue,
+    // and with 4 HW queues per process (GPU_MAX_HW_QUEUES) a worker stream
+    // shares one with the GPU legs' streams, so the marker completes only
+    // after the duo kernel queued before it -- measured: every host thread
+    // stalled for the whole 1.9 s duo run (tools/d2h_probe3.hip: event waits
+    // 1000 ms behind a 1 s kernel, stream syncs 29 ms for 1 GiB).
+    struct Stage {
+        hipStream_t s[2] = {nullptr, nullptr};
         uint8_t* buf[2] = {nullptr, nullptr};
     };
     HostPool(int device, unsigned n);
@@ -66,10 +74,10 @@ struct HostTask {
 
 // out32[i] = SHA256(task i), tasks claimed in array order (callers sort them
 // largest first: list scheduling in LPT order).  Exactly one of d_arena (HBM:
-// chunked D2H after wait_ev) and h_arena (host memory) is non-null.
-// Returns false with *err set on a HIP failure.
+// chunked D2H; the caller has waited until its bytes are written) and h_arena
+// (host memory) is non-null.  Returns false with *err set on a HIP failure.
 bool host_leg_run(HostPool& pool, const HostTask* tasks, uint64_t n, const uint8_t* d_arena,
-                  const uint8_t* h_arena, hipEvent_t wait_ev, uint8_t* out32, std::string* err);
+                  const uint8_t* h_arena, uint8_t* out32, std::string* err);
 
 // Streaming absorb with a carry block: feeds len bytes at p into midstate st
 // whose pending partial block is carry[0 .. *carry_len).
