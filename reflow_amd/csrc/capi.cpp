@@ -445,21 +445,26 @@ static double gpu_model(const std::vector<uint64_t>& nbs, const std::vector<doub
     return best;
 }
 
-// The host leg's inputs to the split: threads, the per-thread SHA-NI rate
-// (bytes/s, measured on this machine) and, for messages resident in HBM,
-// the D2H link rate every host-leg byte crosses.
+// The host leg's inputs to the split: its slots (threads x interleaved
+// lanes), one slot's SHA-NI rate (bytes/s: a core's measured rate with
+// `ways` messages interleaved, divided among them) and, for messages resident
+// in HBM, the D2H link rate every host-leg byte crosses.
 struct HostModel {
-    unsigned threads = 0;
+    unsigned slots = 0;
     double rate = 0.0;
     double link = 0.0;  // 0: messages already in host memory
 };
 
+// Sustained D2H rate the host leg's copies reach on the MI355X box (PCIe
+// Gen5 x16; tools/host_leg_probe.py all-host runs).
+static constexpr double kD2HLink = 52e9;
+
 // Which messages go to the host leg (the h largest) and how the rest split
 // over the GPU kernels.  The host leg's makespan for the h largest messages
-// is list scheduling in LPT order over `threads` threads (what the pool's
-// shared largest-first queue does), each message costing len/rate plus a
-// fixed 100 us (its first D2H chunk / queue hop), bounded below by the link;
-// plus 100 us to wake the pool.  host(h) grows with h, gpu(h) shrinks, so
+// is list scheduling in LPT order over its slots (what the pool's shared
+// largest-first queue does), each message costing len/rate plus a fixed
+// 20 us (its first D2H chunk / queue hop), bounded below by the link; plus
+// 100 us to wake the pool.  host(h) grows with h, gpu(h) shrinks, so
 // the best h sits at their crossing; the smallest h reaching the best
 // makespan (2% margin) wins, so the GPU keeps every message the host leg
 // would not finish sooner.
@@ -475,16 +480,16 @@ static void plan_split(const std::vector<uint64_t>& nb, const uint64_t* lens, st
     for (uint64_t i = 0; i < n; ++i) nbs[i] = nb[order[i]];
     for (uint64_t i = n; i-- > 0;) suf[i] = suf[i + 1] + (double)nbs[i];
     uint64_t h = 0;
-    const bool host_ok = hm.threads > 0 && hm.rate > 0 && !(flags & RF_SHA_NO_HOST);
+    const bool host_ok = hm.slots > 0 && hm.rate > 0 && !(flags & RF_SHA_NO_HOST);
     if (host_ok && (flags & RF_SHA_ALL_HOST)) {
         h = n;
     } else if (host_ok && n) {
         std::vector<double> host_t(n + 1, 0.0);
-        std::vector<double> load(hm.threads, 0.0);  // min-heap of thread loads (s)
+        std::vector<double> load(hm.slots, 0.0);  // min-heap of slot loads (s)
         double maxload = 0, bytes = 0;
         for (uint64_t i = 0; i < n; ++i) {
             std::pop_heap(load.begin(), load.end(), std::greater<double>());
-            load.back() += (double)lens[order[i]] / hm.rate + 100e-6;
+            load.back() += (double)lens[order[i]] / hm.rate + 20e-6;
             maxload = std::max(maxload, load.back());
             std::push_heap(load.begin(), load.end(), std::greater<double>());
             bytes += (double)lens[order[i]];
@@ -561,12 +566,13 @@ static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const u
         total_bytes += lens[i];
     }
     HostModel hm;
-    hm.threads = (flags & RF_SHA_NO_HOST) ? 0u : ctx_host_threads(ctx);
-    if ((flags & RF_SHA_ALL_HOST) && hm.threads == 0)
+    const unsigned threads = (flags & RF_SHA_NO_HOST) ? 0u : ctx_host_threads(ctx);
+    if ((flags & RF_SHA_ALL_HOST) && threads == 0)
         return fail(RF_EINVAL, "RF_SHA_ALL_HOST: the host leg is off (no SHA extensions, or 0 host threads)");
-    // per-thread rate with all threads busy: 0.9 x one core alone
-    hm.rate = hm.threads ? 0.9 * host_sha_rate() : 0.0;
-    hm.link = host_resident ? 0.0 : 40e9;  // PCIe Gen5 x16 D2H, sustained
+    const int ways = host_ways();
+    hm.slots = threads * (unsigned)ways;
+    hm.rate = threads ? host_sha_rate(ways) / ways : 0.0;
+    hm.link = host_resident ? 0.0 : kD2HLink;
     p->ctx = ctx;
     p->n = n;
     p->ran = false;
@@ -622,7 +628,7 @@ static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const u
     p->st.n_solo = n_solo;
     p->st.n_host = n_host;
     p->st.host_bytes = host_bytes;
-    p->st.host_threads = n_host ? hm.threads : 0;
+    p->st.host_threads = n_host ? threads : 0;
     p->st.total_blocks = total_blocks;
     p->st.max_blocks = max_blocks;
     p->st.total_bytes = total_bytes;

@@ -82,12 +82,13 @@ HostPool::~HostPool() {
     for (auto& t : th_) t.join();
     (void)hipSetDevice(device_);
     for (Stage& s : stages_)
-        for (int i = 0; i < 2; ++i) {
-            if (s.s[i]) {
-                (void)hipStreamSynchronize(s.s[i]);
-                (void)hipStreamDestroy(s.s[i]);
+        for (LaneStage& l : s.lane) {
+            if (l.s) {
+                (void)hipStreamSynchronize(l.s);
+                (void)hipStreamDestroy(l.s);
             }
-            if (s.buf[i]) (void)hipHostFree(s.buf[i]);
+            for (uint8_t* b : l.buf)
+                if (b) (void)hipHostFree(b);
         }
 }
 
@@ -122,52 +123,43 @@ void HostPool::run(const std::function<void(unsigned)>& fn) {
     job_ = nullptr;
 }
 
-hipError_t HostPool::stage(unsigned w, Stage** out) {
+hipError_t HostPool::stage(unsigned w, int ways, Stage** out) {
     Stage& s = stages_[w];
     *out = &s;
-    if (s.buf[1]) return hipSuccess;
     hipError_t e;
-    for (int i = 0; i < 2; ++i) {
-        if (!s.s[i] && (e = hipStreamCreateWithFlags(&s.s[i], hipStreamNonBlocking)) != hipSuccess) return e;
-        if (s.buf[i]) continue;
-        void* p = nullptr;
-        if ((e = hipHostMalloc(&p, host_chunk_bytes(), hipHostMallocDefault)) != hipSuccess) return e;
-        s.buf[i] = static_cast<uint8_t*>(p);
+    for (int k = 0; k < ways; ++k) {
+        LaneStage& l = s.lane[k];
+        if (!l.s && (e = hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking)) != hipSuccess) return e;
+        for (uint8_t*& b : l.buf) {
+            if (b) continue;
+            void* p = nullptr;
+            if ((e = hipHostMalloc(&p, host_chunk_bytes(), hipHostMallocDefault)) != hipSuccess) return e;
+            b = static_cast<uint8_t*>(p);
+        }
     }
     return hipSuccess;
 }
 
-// One message resident in HBM: chunk c+1's D2H is queued before chunk c is
-// hashed, so the copy engine and the core overlap.  wait/hash (optional)
-// accumulate the seconds spent waiting for chunks and hashing.
-static hipError_t hash_device_message(HostPool::Stage* st, const uint8_t* src, uint64_t len, uint8_t* out32,
-                                      double* wait, double* hash) {
-    const uint64_t C = host_chunk_bytes();
-    uint32_t h[8];
-    host_sha_init(h);
-    const uint64_t nch = len ? (len + C - 1) / C : 0;
-    auto issue = [&](uint64_t c) -> hipError_t {
-        const uint64_t off = c * C, sz = std::min(C, len - off);
-        return hipMemcpyAsync(st->buf[c & 1], src + off, sz, hipMemcpyDeviceToHost, st->s[c & 1]);
-    };
-    hipError_t e = hipSuccess;
-    if (nch) e = issue(0);
-    for (uint64_t c = 0; c < nch && e == hipSuccess; ++c) {
-        if (c + 1 < nch && (e = issue(c + 1)) != hipSuccess) break;
-        const double t0 = wait ? now_s() : 0;
-        if ((e = hipStreamSynchronize(st->s[c & 1])) != hipSuccess) break;
-        const double t1 = wait ? now_s() : 0;
-        const uint64_t sz = std::min(C, len - c * C);
-        host_sha_blocks(h, st->buf[c & 1], sz / 64);
-        if (c + 1 == nch) host_sha_final(h, st->buf[c & 1] + (sz & ~63ull), sz & 63, len, out32);
-        if (wait) {
-            *wait += t1 - t0;
-            *hash += now_s() - t1;
-        }
-    }
-    if (e == hipSuccess && nch == 0) host_sha_final(h, nullptr, 0, 0, out32);
-    return e;
+int host_ways() {
+    static const int w = [] {
+        const char* v = getenv("RF_HOST_WAYS");
+        return v ? std::min(4, std::max(1, atoi(v))) : 2;
+    }();
+    return w;
 }
+
+namespace {
+// One message in flight on a host thread.  Its bytes come in chunks of C
+// (from the message start, so every chunk but the last is whole blocks):
+// from HBM through the lane's double buffer, or straight from host memory.
+struct Lane {
+    bool active = false, ready = false;
+    uint64_t task = 0, len = 0, nch = 0, c = 0, pos = 0;
+    int buf = 0;
+    const uint8_t* src = nullptr;
+    uint32_t st[8];
+};
+}  // namespace
 
 bool host_leg_run(HostPool& pool, const HostTask* tasks, uint64_t n, const uint8_t* d_arena,
                   const uint8_t* h_arena, uint8_t* out32, std::string* err) {
@@ -175,31 +167,105 @@ bool host_leg_run(HostPool& pool, const HostTask* tasks, uint64_t n, const uint8
     std::atomic<bool> bad{false};
     std::mutex emu;
     const bool timing = leg_timing();
+    const int W = host_ways();
+    const uint64_t C = host_chunk_bytes();
     std::vector<double> tw(pool.size(), 0.0), th(pool.size(), 0.0), tt(pool.size(), 0.0);
     const double t_run = timing ? now_s() : 0;
+    auto fail_with = [&](const char* what, hipError_t e) {
+        std::lock_guard<std::mutex> lk(emu);
+        if (!bad.exchange(true)) *err = std::string(what) + hipGetErrorString(e);
+    };
     pool.run([&](unsigned w) {
         const double t_start = timing ? now_s() : 0;
         HostPool::Stage* st = nullptr;
         if (d_arena) {
-            const hipError_t e = pool.stage(w, &st);
-            if (e != hipSuccess) {
-                std::lock_guard<std::mutex> lk(emu);
-                if (!bad.exchange(true)) *err = std::string("host leg stage: ") + hipGetErrorString(e);
+            const hipError_t e = pool.stage(w, W, &st);
+            if (e != hipSuccess) return fail_with("host leg stage: ", e);
+        }
+        Lane L[4];
+        auto chunk_len = [&](const Lane& x) { return std::min(C, x.len - x.c * C); };
+        auto data = [&](const Lane& x, int k) -> const uint8_t* {
+            return h_arena ? x.src + x.c * C : st->lane[k].buf[x.buf];
+        };
+        auto issue = [&](Lane& x, int k, uint64_t c, int b) -> bool {
+            const uint64_t off = c * C;
+            const hipError_t e = hipMemcpyAsync(st->lane[k].buf[b], x.src + off, std::min(C, x.len - off),
+                                                hipMemcpyDeviceToHost, st->lane[k].s);
+            if (e != hipSuccess) fail_with("host leg D2H: ", e);
+            return e == hipSuccess;
+        };
+        // next message into lane slot k (zero-length ones finish on the spot)
+        auto claim = [&](int k) {
+            Lane& x = L[k];
+            x.active = false;
+            for (uint64_t i; !bad.load(std::memory_order_relaxed) && (i = next.fetch_add(1)) < n;) {
+                x.task = i;
+                x.len = tasks[i].len;
+                x.src = (h_arena ? h_arena : d_arena) + tasks[i].off;
+                host_sha_init(x.st);
+                if (!x.len) {
+                    host_sha_final(x.st, nullptr, 0, 0, out32 + 32 * i);
+                    continue;
+                }
+                x.nch = (x.len + C - 1) / C;
+                x.c = x.pos = 0;
+                x.buf = 0;
+                x.ready = h_arena != nullptr;
+                if (!h_arena && !issue(x, k, 0, 0)) return;
+                x.active = true;
                 return;
             }
-        }
-        for (uint64_t i; !bad.load(std::memory_order_relaxed) && (i = next.fetch_add(1)) < n;) {
-            const HostTask& t = tasks[i];
-            if (h_arena) {
-                host_sha256(h_arena + t.off, t.len, out32 + 32 * i);
-                continue;
+        };
+        for (int k = 0; k < W; ++k) claim(k);
+        for (;;) {
+            int idx[4], na = 0;
+            for (int k = 0; k < W; ++k)
+                if (L[k].active) idx[na++] = k;
+            if (!na || bad.load(std::memory_order_relaxed)) break;
+            // chunks not yet waited on: wait, then queue the lane's next chunk
+            // into the buffer its previous chunk has left
+            for (int a = 0; a < na; ++a) {
+                Lane& x = L[idx[a]];
+                if (x.ready) continue;
+                const double t0 = timing ? now_s() : 0;
+                const hipError_t e = hipStreamSynchronize(st->lane[idx[a]].s);
+                if (timing) tw[w] += now_s() - t0;
+                if (e != hipSuccess) return fail_with("host leg D2H: ", e);
+                x.ready = true;
+                if (x.c + 1 < x.nch && !issue(x, idx[a], x.c + 1, x.buf ^ 1)) return;
             }
-            const hipError_t e = hash_device_message(st, d_arena + t.off, t.len, out32 + 32 * i,
-                                                     timing ? &tw[w] : nullptr, timing ? &th[w] : nullptr);
-            if (e != hipSuccess) {
-                std::lock_guard<std::mutex> lk(emu);
-                if (!bad.exchange(true)) *err = std::string("host leg D2H: ") + hipGetErrorString(e);
+            // whole blocks every active lane has left in its current chunk
+            uint64_t m = ~0ull;
+            for (int a = 0; a < na; ++a) {
+                const Lane& x = L[idx[a]];
+                m = std::min(m, (chunk_len(x) - x.pos) / 64);
             }
+            const double t1 = timing ? now_s() : 0;
+            if (m) {
+                uint32_t* sp[4];
+                const uint8_t* pp[4];
+                for (int a = 0; a < na; ++a) {
+                    sp[a] = L[idx[a]].st;
+                    pp[a] = data(L[idx[a]], idx[a]) + L[idx[a]].pos;
+                }
+                host_sha_blocks_multi(na, sp, pp, m);
+                for (int a = 0; a < na; ++a) L[idx[a]].pos += 64 * m;
+            }
+            for (int a = 0; a < na; ++a) {
+                Lane& x = L[idx[a]];
+                const uint64_t cl = chunk_len(x);
+                if (cl - x.pos >= 64) continue;  // blocks left in this chunk
+                if (x.c + 1 < x.nch) {           // on to the next chunk (its copy is queued)
+                    ++x.c;
+                    x.pos = 0;
+                    x.buf ^= 1;
+                    x.ready = h_arena != nullptr;
+                } else {  // the tail: pad, finish, take the next message
+                    host_sha_final(x.st, data(x, idx[a]) + x.pos, cl - x.pos, x.len, out32 + 32 * x.task);
+                    claim(idx[a]);
+                }
+            }
+            if (timing) th[w] += now_s() - t1;
         }
         if (timing) tt[w] = now_s() - t_start;
     });
@@ -212,9 +278,9 @@ bool host_leg_run(HostPool& pool, const HostTask* tasks, uint64_t n, const uint8
         }
         uint64_t bytes = 0;
         for (uint64_t i = 0; i < n; ++i) bytes += tasks[i].len;
-        fprintf(stderr, "[host leg] %u threads, %llu msgs, %.2f GB: wall %.1f ms, slowest thread %.1f ms; "
+        fprintf(stderr, "[host leg] %u threads x %d ways, %llu msgs, %.2f GB: wall %.1f ms, slowest thread %.1f ms; "
                         "sum wait %.1f ms, sum hash %.1f ms (%.2f GB/s per hashing thread)\n",
-                pool.size(), (unsigned long long)n, bytes / 1e9, (now_s() - t_run) * 1e3, mx * 1e3, sw * 1e3,
+                pool.size(), W, (unsigned long long)n, bytes / 1e9, (now_s() - t_run) * 1e3, mx * 1e3, sw * 1e3,
                 sh * 1e3, sh > 0 ? bytes / sh / 1e9 : 0.0);
     }
     return !bad.load();

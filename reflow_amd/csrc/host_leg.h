@@ -38,9 +38,16 @@ class HostPool {
     // after the duo kernel queued before it -- measured: every host thread
     // stalled for the whole 1.9 s duo run (tools/d2h_probe3.hip: event waits
     // 1000 ms behind a 1 s kernel, stream syncs 29 ms for 1 GiB).
-    struct Stage {
-        hipStream_t s[2] = {nullptr, nullptr};
+    // One per interleaved message ("lane") of a thread: a stream and two
+    // buffers (chunk c+1's D2H lands in one while chunk c is hashed from the
+    // other; one stream suffices because c+1 is queued only after c is
+    // waited on).
+    struct LaneStage {
+        hipStream_t s = nullptr;
         uint8_t* buf[2] = {nullptr, nullptr};
+    };
+    struct Stage {
+        LaneStage lane[4];
     };
     HostPool(int device, unsigned n);
     ~HostPool();
@@ -49,8 +56,8 @@ class HostPool {
     unsigned size() const { return n_; }
     // fn(w) once on every worker w in [0, size()); returns when all returned.
     void run(const std::function<void(unsigned)>& fn);
-    // worker w's staging (call from worker w)
-    hipError_t stage(unsigned w, Stage** out);
+    // worker w's staging for `ways` lanes (call from worker w)
+    hipError_t stage(unsigned w, int ways, Stage** out);
 
    private:
     void loop(unsigned w);
@@ -71,6 +78,12 @@ struct HostTask {
     uint64_t off;   // byte offset in the arena
     uint64_t len;
 };
+
+// Messages one host thread hashes at once, interleaved (host_sha_blocks_multi):
+// RF_HOST_WAYS, default 2 -- on the MI355X box two SHA-NI chains per core
+// already out-run the PCIe D2H share of a thread, and fewer lanes keep the
+// longest message's own chain fast (DESIGN.md §5 "K1 host leg").
+int host_ways();
 
 // out32[i] = SHA256(task i), tasks claimed in array order (callers sort them
 // largest first: list scheduling in LPT order).  Exactly one of d_arena (HBM:

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <vector>
 
 namespace rf {
@@ -93,6 +94,67 @@ __attribute__((target("sha,sse4.1,ssse3"))) void ni_blocks(uint32_t st[8], const
 #undef RF_NI_ROUNDS
 #undef RF_NI_SCHED
 
+// N interleaved chains: the same rounds and schedule as ni_blocks, each
+// statement issued for every chain before the next, so N independent
+// sha256rnds2 are in flight.  State kept in locals (written back once):
+// through the caller's memory every round would add store-forwarding latency.
+template <int N>
+__attribute__((target("sha,sse4.1,ssse3"))) void ni_multi(uint32_t* const* st, const uint8_t* const* p,
+                                                         uint64_t nblocks) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bll, 0x0405060700010203ll);
+    __m128i abef[N], cdgh[N];
+    const uint8_t* q[N];
+#pragma GCC unroll 4
+    for (int i = 0; i < N; ++i) {
+        __m128i t = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(st[i])), 0xB1);
+        __m128i c = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(st[i] + 4)), 0x1B);
+        abef[i] = _mm_alignr_epi8(t, c, 8);
+        cdgh[i] = _mm_blend_epi16(c, t, 0xF0);
+        q[i] = p[i];
+    }
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        __m128i a0[N], c0[N], m[N][4];
+#pragma GCC unroll 4
+        for (int i = 0; i < N; ++i) {
+            a0[i] = abef[i];
+            c0[i] = cdgh[i];
+#pragma GCC unroll 4
+            for (int j = 0; j < 4; ++j)
+                m[i][j] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(q[i] + 64 * b + 16 * j)),
+                                           bswap);
+        }
+#pragma GCC unroll 16
+        for (int g = 0; g < 16; ++g) {
+#pragma GCC unroll 4
+            for (int i = 0; i < N; ++i) {
+                if (g >= 4) {
+                    __m128i& x = m[i][g & 3];
+                    x = _mm_sha256msg2_epu32(
+                        _mm_add_epi32(_mm_sha256msg1_epu32(x, m[i][(g + 1) & 3]),
+                                      _mm_alignr_epi8(m[i][(g + 3) & 3], m[i][(g + 2) & 3], 4)),
+                        m[i][(g + 3) & 3]);
+                }
+                __m128i kw = _mm_add_epi32(m[i][g & 3], _mm_load_si128(reinterpret_cast<const __m128i*>(&kK[4 * g])));
+                cdgh[i] = _mm_sha256rnds2_epu32(cdgh[i], abef[i], kw);
+                kw = _mm_shuffle_epi32(kw, 0x0E);
+                abef[i] = _mm_sha256rnds2_epu32(abef[i], cdgh[i], kw);
+            }
+        }
+#pragma GCC unroll 4
+        for (int i = 0; i < N; ++i) {
+            abef[i] = _mm_add_epi32(abef[i], a0[i]);
+            cdgh[i] = _mm_add_epi32(cdgh[i], c0[i]);
+        }
+    }
+#pragma GCC unroll 4
+    for (int i = 0; i < N; ++i) {
+        const __m128i t = _mm_shuffle_epi32(abef[i], 0x1B);
+        const __m128i c = _mm_shuffle_epi32(cdgh[i], 0xB1);
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(st[i]), _mm_blend_epi16(t, c, 0xF0));
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(st[i] + 4), _mm_alignr_epi8(c, t, 8));
+    }
+}
+
 }  // namespace
 
 bool host_sha_available() {
@@ -110,6 +172,17 @@ void host_sha_init(uint32_t st[8]) { memcpy(st, kIV, sizeof kIV); }
 
 void host_sha_blocks(uint32_t st[8], const uint8_t* p, uint64_t nblocks) {
     if (nblocks) ni_blocks(st, p, nblocks);
+}
+
+void host_sha_blocks_multi(int n, uint32_t* const* st, const uint8_t* const* p, uint64_t nblocks) {
+    if (!nblocks) return;
+    switch (n) {
+        case 1: ni_blocks(st[0], p[0], nblocks); break;
+        case 2: ni_multi<2>(st, p, nblocks); break;
+        case 3: ni_multi<3>(st, p, nblocks); break;
+        case 4: ni_multi<4>(st, p, nblocks); break;
+        default: break;
+    }
 }
 
 void host_sha_final(uint32_t st[8], const uint8_t* tail, uint64_t tail_len, uint64_t total_len,
@@ -137,25 +210,31 @@ void host_sha256(const uint8_t* p, uint64_t len, uint8_t out32[32]) {
     host_sha_final(st, p + 64 * nb, len - 64 * nb, len, out32);
 }
 
-double host_sha_rate() {
-    static const double rate = [] {
-        if (!host_sha_available()) return 0.0;
-        std::vector<uint8_t> buf(8u << 20);
-        for (size_t i = 0; i < buf.size(); ++i) buf[i] = (uint8_t)(i * 131u + (i >> 11));
-        uint32_t st[8];
-        double best = 1e30;
-        for (int r = 0; r < 3; ++r) {
-            host_sha_init(st);
-            const auto t0 = std::chrono::steady_clock::now();
-            host_sha_blocks(st, buf.data(), buf.size() / 64);
-            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            best = std::min(best, dt);
-        }
-        volatile uint32_t sink = st[0];
-        (void)sink;
-        return (double)buf.size() / best;
-    }();
-    return rate;
+double host_sha_rate(int ways) {
+    static double cache[5] = {-1, -1, -1, -1, -1};
+    static std::mutex mu;
+    if (ways < 1 || ways > 4) return 0.0;
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache[ways] >= 0) return cache[ways];
+    if (!host_sha_available()) return cache[ways] = 0.0;
+    std::vector<uint8_t> buf(8u << 20);
+    for (size_t i = 0; i < buf.size(); ++i) buf[i] = (uint8_t)(i * 131u + (i >> 11));
+    const uint64_t per = buf.size() / 64 / ways;
+    uint32_t st[4][8];
+    uint32_t* sp[4] = {st[0], st[1], st[2], st[3]};
+    const uint8_t* pp[4];
+    for (int i = 0; i < ways; ++i) pp[i] = buf.data() + 64 * per * i;
+    double best = 1e30;
+    for (int r = 0; r < 3; ++r) {
+        for (int i = 0; i < ways; ++i) host_sha_init(st[i]);
+        const auto t0 = std::chrono::steady_clock::now();
+        host_sha_blocks_multi(ways, sp, pp, per);
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        best = std::min(best, dt);
+    }
+    volatile uint32_t sink = st[0][0];
+    (void)sink;
+    return cache[ways] = (double)(64 * per * ways) / best;
 }
 
 }  // namespace rf

@@ -22,13 +22,20 @@ bool host_sha_available();
 void host_sha_init(uint32_t st[8]);
 // nblocks whole 64-byte blocks from st (a midstate), no padding.
 void host_sha_blocks(uint32_t st[8], const uint8_t* p, uint64_t nblocks);
+// n (1..4) independent messages at once: nblocks whole blocks of each, p[i]
+// into midstate st[i].  One SHA-NI chain is bound by sha256rnds2's latency
+// (32 dependent per block); interleaving n chains fills the pipeline
+// (measured on the MI355X box's EPYC 9575F, one core: 2.44 / 3.53 / 4.19 /
+// 4.31 GB/s for n = 1..4, tools/shani_ilp.cpp).
+void host_sha_blocks_multi(int n, uint32_t* const* st, const uint8_t* const* p, uint64_t nblocks);
 // Pads and finishes a message: `tail` holds its last (total_len % 64) bytes
 // (tail_len < 64), everything before has gone through host_sha_blocks.
 void host_sha_final(uint32_t st[8], const uint8_t* tail, uint64_t tail_len, uint64_t total_len,
                     uint8_t out32[32]);
 // One whole message.
 void host_sha256(const uint8_t* p, uint64_t len, uint8_t out32[32]);
-// Measured bytes/s of one core on this machine (8 MiB, best of 3; cached).
-double host_sha_rate();
+// Measured bytes/s of one core on this machine with `ways` interleaved
+// messages (8 MiB in total, best of 3; cached per ways in 1..4).
+double host_sha_rate(int ways = 1);
 
 }  // namespace rf

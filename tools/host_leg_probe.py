@@ -47,7 +47,7 @@ if os.environ.get("PROBE_C2"):
     ctx.sync()
     ctx.set_host_threads(None)
     for name, flags in [("c2 all-host", capi.RF_SHA_ALL_HOST), ("c2 hybrid", 0), ("c2 all-host", capi.RF_SHA_ALL_HOST),
-                        ("c2 hybrid", 0)]:
+                        ("c2 hybrid", 0), ("c2 hybrid", 0)]:
         plan = ctx.sha_plan(offs, lens, flags)
         t0 = time.perf_counter()
         plan.run(arena.ptr, out.ptr)
