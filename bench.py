@@ -690,14 +690,16 @@ def bench_assoc(ctx, keys, n_ins, n_probe, hits):
     node_keys = np.stack([physical, logical], axis=1).reshape(-1)
     ptr = np.arange(0, 2 * n_nodes + 1, 2, dtype=np.uint64)
     t0 = time.perf_counter()
-    which, _ = a.lookup(0, node_keys, ptr, repair=2)
+    which, fsids, kf, _ = a.lookup(0, node_keys, ptr)
+    a.repair(0, node_keys, ptr, which, fsids, kf)  # precise; every fsid taken as verified
     lk_s = time.perf_counter() - t0
     _, f2 = a.get(0, physical)
     lookup = {"workload": "%d nodes x 2 cache keys (physical absent, logical present), precise read repair"
                           % n_nodes,
               "ms": lk_s * 1e3, "m_nodes_per_s": n_nodes / lk_s / 1e6,
               "hits_on_logical": int((which == 1).sum()), "repaired": int(f2.astype(np.int64).sum()),
-              "note": "host API: keys H2D, one Get batch, first-hit select on the device, repair Put batch"}
+              "note": "host API: keys H2D, one Get batch, first-hit select on the device (rf_assoc_lookup), "
+                      "then the precise repair Put batch (rf_assoc_repair)"}
     a.close()
     return {"workload": "Put %d keys (one batch), Get %d keys (%d present)" % (n_ins, n_probe, found),
             "put_ms": put_s * 1e3, "put_mkeys_per_s": n_ins / put_s / 1e6, "put_ok": ok_put,

@@ -353,19 +353,28 @@ int rf_assoc_get_device(rf_assoc *a, int kind, const void *d_keys32, uint64_t n,
  * more than one key matches. */
 int rf_assoc_get_abbrev(rf_assoc *a, int kind, const uint8_t *keys32, const uint8_t *nhex, uint64_t n,
                         uint8_t *keys_out32, uint8_t *vals32, int32_t *status);
-/* Eval.lookup's assoc step for a batch of nodes (eval.go:1172-1258): node i's
- * cache keys (CacheKeys order, most to least concrete) are keys32 rows
- * [key_ptr[i], key_ptr[i+1]); which[i] = index of the first key whose Get finds
- * a value (vals32[i] = that value, the Fileset id), or -1 (vals32[i] zeroed).
- * All keys go in one Get batch (the batching the TODO at eval.go:1199-1201
- * asks for).  repair: 0 none; 1 = the reference's read repair, Put(zero
- * expect) of the found value under every other key of the node
- * (eval.go:1247-1258); 2 = precise read repair, only under the keys that were
- * missing.  Repairs apply as one Put batch in node order, then key order.  The
- * fileset unmarshal / missing-file checks (repository I/O) stay with the
- * caller. */
+/* Eval.lookup's assoc step for a batch of nodes (eval.go:1172-1220), read
+ * only: node i's cache keys (CacheKeys order, most to least concrete) are
+ * keys32 rows [key_ptr[i], key_ptr[i+1]); all of them go in one Get batch (the
+ * batching the TODO at eval.go:1199-1201 asks for).  which[i] = index within
+ * the node of its first key with a value (vals32[i] = that value, the Fileset
+ * id), or -1 (vals32[i] zeroed).  key_found / key_vals32 (either may be NULL):
+ * per key, found and value -- the later candidates the caller tries when the
+ * first fsid does not unmarshal (eval.go:1210-1218 moves on to the next key).
+ * Nothing is written: read repair waits for the caller's checks
+ * (rf_assoc_repair). */
 int rf_assoc_lookup(rf_assoc *a, int kind, const uint8_t *keys32, const uint64_t *key_ptr, uint64_t n_nodes,
-                    int repair, int32_t *which, uint8_t *vals32);
+                    int32_t *which, uint8_t *vals32, uint8_t *key_found, uint8_t *key_vals32);
+/* Read repair after the caller's checks (eval.go:1227-1258): node i takes part
+ * iff which[i] >= 0 -- the key whose fsid unmarshalled and whose files all
+ * exist (missing(), and not an empty value under RecomputeEmpty); the caller
+ * sets which[i] = -1 for every other node.  Put(zero expect, key, vals32[i])
+ * under every other key of the node (the reference's blind write-back), or,
+ * with key_found (rf_assoc_lookup's) given, only under the keys that were
+ * missing (precise read repair, the TODO at eval.go:1199-1201).  One Put
+ * batch, node order then key order. */
+int rf_assoc_repair(rf_assoc *a, int kind, const uint8_t *keys32, const uint64_t *key_ptr, uint64_t n_nodes,
+                    const int32_t *which, const uint8_t *vals32, const uint8_t *key_found);
 /* Occupied slots (live + deleted keys) and table capacity. */
 int rf_assoc_stats(rf_assoc *a, uint64_t *occupied, uint64_t *capacity);
 

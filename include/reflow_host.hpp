@@ -23,6 +23,7 @@
 #include <cstring>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <map>
 #include <optional>
 #include <string>
@@ -277,11 +278,18 @@ class Assoc {
     std::vector<int> PutBatch(AssocKind kind, const std::vector<Digest>& expect, const std::vector<Digest>& keys,
                               const std::vector<Digest>& vals);
     std::vector<std::optional<Digest>> GetBatch(AssocKind kind, const std::vector<Digest>& keys);
-    // Eval.lookup's assoc step for many nodes (eval.go:1172-1258): per node,
-    // the index of its first cache key with a value (-1: none) and the value;
-    // repair 0 none, 1 blind (the reference), 2 precise (missing keys only)
+    // Eval.lookup's assoc step for many nodes (eval.go:1172-1258), batched:
+    // one Get over every node's cache keys; per node the first key (CacheKeys
+    // order) with a value that `usable` accepts -- the caller's unmarshal of
+    // the fsid; eval.go:1210-1218 moves on to the next key when it fails --
+    // or -1.  Then read repair (0 none, 1 blind as the reference, 2 precise:
+    // missing keys only) for the nodes whose value `verified` passes (the
+    // missing()/RecomputeEmpty checks of eval.go:1227-1246); null callbacks
+    // accept everything.
+    using FsidCheck = std::function<bool(size_t node, const Digest& fsid)>;
     std::vector<std::pair<int, Digest>> Lookup(AssocKind kind, const std::vector<std::vector<Digest>>& node_keys,
-                                               int repair);
+                                               int repair, const FsidCheck& usable = nullptr,
+                                               const FsidCheck& verified = nullptr);
 
    private:
     rf_assoc* a_ = nullptr;

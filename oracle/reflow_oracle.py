@@ -490,28 +490,51 @@ class InmemoryAssoc:
         return "ok", hits[0]
 
 
-def assoc_lookup(assoc, kind, node_keys, repair=0):
-    """Eval.lookup's assoc part for a batch of nodes (eval.go:1172-1258):
-    keys are tried in CacheKeys order and the first Get that finds a value
-    wins (which = its index, -1 if none).  repair 1 = the reference's blind
-    read repair, Put(zero expect, key, fsid) for every other key of the node
-    (eval.go:1247-1258); repair 2 = precise read repair (the TODO at
-    eval.go:1199-1201): only the node's keys that were missing.  Nodes apply
-    their repairs in node order, keys in order.  (The fileset unmarshal and
-    repository missing-file checks are repository I/O and stay with the caller.)"""
+def assoc_lookup(assoc, kind, node_keys):
+    """The Gets of Eval.lookup's key loop for a batch of nodes (eval.go:1202-1209),
+    all against the table as it is before the batch: per node (which, value,
+    per-key values) with which = the first key that has a value (-1 if none)."""
     res = []
     for keys in node_keys:
         got = [assoc.get(kind, k) for k in keys]
         which = next((j for j, v in enumerate(got) if v is not None), -1)
         res.append((which, got[which] if which >= 0 else bytes(32), got))
+    return res
+
+
+def assoc_repair(assoc, kind, node_keys, which, vals, got=None):
+    """Read repair (eval.go:1247-1258) of the nodes with which >= 0, in node
+    order: Put(zero expect, key, value) under every other key (blind, the
+    reference), or with got (per-key Get results) only under the keys that
+    were missing (precise, the TODO at eval.go:1199-1201)."""
+    for i, keys in enumerate(node_keys):
+        if which[i] < 0:
+            continue
+        for j, k in enumerate(keys):
+            if j != which[i] and (got is None or got[i][j] is None):
+                assoc.put(kind, None, k, vals[i])
+
+
+def eval_lookup(assoc, kind, node_keys, repair=0, usable=None, verified=None):
+    """Eval.lookup (eval.go:1172-1258) for a batch of nodes: keys in CacheKeys
+    order; a key counts if Get finds a value that `usable(node, fsid)` accepts
+    (the unmarshal, :1210-1218 -- otherwise the loop goes on to the next key);
+    read repair (1 blind, 2 precise) only for nodes whose value passes
+    `verified(node, fsid)` (missing() / RecomputeEmpty, :1227-1246).  Returns
+    [(which, fsid)] (-1 and zero when no key counts)."""
+    snap = assoc_lookup(assoc, kind, node_keys)
+    out, which, vals, got = [], [], [], []
+    for i, (_, _, g) in enumerate(snap):
+        w = next((j for j, v in enumerate(g) if v is not None and (usable is None or usable(i, v))), -1)
+        v = g[w] if w >= 0 else bytes(32)
+        out.append((w, v))
+        ok = w >= 0 and (verified is None or verified(i, v))
+        which.append(w if ok else -1)
+        vals.append(v)
+        got.append(g)
     if repair:
-        for keys, (which, val, got) in zip(node_keys, res):
-            if which < 0:
-                continue
-            for j, k in enumerate(keys):
-                if j != which and (repair == 1 or got[j] is None):
-                    assoc.put(kind, None, k, val)
-    return [(w, v) for w, v, _ in res]
+        assoc_repair(assoc, kind, node_keys, which, vals, got if repair == 2 else None)
+    return out
 
 
 # --------------------------------------------------------------------------

@@ -43,7 +43,7 @@ EXPORTS = [
     "rf_dedup_digests", "rf_dedup_digests_device", "rf_assoc_lookup",
     "rf_assoc_new", "rf_assoc_destroy", "rf_assoc_put", "rf_assoc_get", "rf_assoc_get_device",
     "rf_assoc_get_abbrev", "rf_assoc_stats", "rf_assoc_put_device",
-    "rf_set_host_threads", "rf_host_info",
+    "rf_set_host_threads", "rf_host_info", "rf_assoc_repair",
 ]
 
 
@@ -239,7 +239,8 @@ def lib():
             "rf_assoc_new": ([vp, u64, vp], i32), "rf_assoc_destroy": ([vp], None),
             "rf_assoc_put": ([vp, i32, vp, vp, vp, u64, vp], i32),
             "rf_assoc_get": ([vp, i32, vp, u64, vp, vp], i32),
-            "rf_assoc_lookup": ([vp, i32, vp, vp, u64, i32, vp, vp], i32),
+            "rf_assoc_lookup": ([vp, i32, vp, vp, u64, vp, vp, vp, vp], i32),
+            "rf_assoc_repair": ([vp, i32, vp, vp, u64, vp, vp, vp], i32),
             "rf_assoc_get_device": ([vp, i32, vp, u64, vp, vp, vp], i32),
             "rf_assoc_get_abbrev": ([vp, i32, vp, vp, u64, vp, vp, vp], i32),
             "rf_assoc_stats": ([vp, vp, vp], i32),
@@ -736,17 +737,31 @@ class Assoc:
         _check(lib().rf_assoc_get(self._h, kind, _ptr(k), n, _ptr(vals), _ptr(found)))
         return vals[:n], found[:n]
 
-    def lookup(self, kind, keys, key_ptr, repair=0):
-        """rf_assoc_lookup: keys (rows of 32 B) grouped per node by key_ptr
-        (n_nodes + 1 offsets).  Returns (which int32 per node, values)."""
+    def lookup(self, kind, keys, key_ptr):
+        """rf_assoc_lookup (read only): keys (rows of 32 B) grouped per node by
+        key_ptr (n_nodes + 1 offsets).  Returns (which int32 per node, values,
+        found per key, value per key)."""
         k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
         kp = np.ascontiguousarray(key_ptr, dtype=np.uint64)
-        n = len(kp) - 1
+        n, nk = len(kp) - 1, len(k) // 32
         which = np.zeros(max(n, 1), dtype=np.int32)
         vals = np.zeros((max(n, 1), 32), dtype=np.uint8)
-        _check(lib().rf_assoc_lookup(self._h, kind, _ptr(k) if len(k) else None, _ptr(kp), n, repair,
-                                     _ptr(which), _ptr(vals)))
-        return which[:n], vals[:n]
+        kf = np.zeros(max(nk, 1), dtype=np.uint8)
+        kv = np.zeros((max(nk, 1), 32), dtype=np.uint8)
+        _check(lib().rf_assoc_lookup(self._h, kind, _ptr(k) if len(k) else None, _ptr(kp), n, _ptr(which),
+                                     _ptr(vals), _ptr(kf), _ptr(kv)))
+        return which[:n], vals[:n], kf[:nk], kv[:nk]
+
+    def repair(self, kind, keys, key_ptr, which, vals, key_found=None):
+        """rf_assoc_repair: read repair of the nodes with which >= 0 (blind, or
+        precise with key_found)."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        kp = np.ascontiguousarray(key_ptr, dtype=np.uint64)
+        w = np.ascontiguousarray(which, dtype=np.int32)
+        v = np.ascontiguousarray(vals, dtype=np.uint8).reshape(-1)
+        kf = None if key_found is None else np.ascontiguousarray(key_found, dtype=np.uint8)
+        _check(lib().rf_assoc_repair(self._h, kind, _ptr(k) if len(k) else None, _ptr(kp), len(kp) - 1, _ptr(w),
+                                     _ptr(v), _ptr(kf) if kf is not None and len(kf) else None))
 
     def put_device(self, kind, d_keys, d_vals, n, d_status, d_expect=None):
         _check(lib().rf_assoc_put_device(self._h, kind, d_expect, d_keys, d_vals, n, d_status))

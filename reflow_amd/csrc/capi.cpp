@@ -173,6 +173,13 @@ extern "C" int rf_init(int device, rf_ctx** out) {
     e = probe_kernels();
     if (e != hipSuccess)
         return fail(RF_EDEVICE, "gfx950 code object not loadable: %s", hipGetErrorString(e));
+    // device-form calls take per-call scratch from the default pool in stream
+    // order; keep freed blocks pooled for the next call instead of unmapping
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+        uint64_t keep = ~0ull;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
     rf_ctx* ctx = new rf_ctx();
     ctx->device = device;
     ctx->n_cu = prop.multiProcessorCount;
@@ -1018,12 +1025,13 @@ struct rf_install {
 static constexpr uint64_t kInstallChunk = 8ull << 30;
 static constexpr uint64_t kInstallSeg = 32ull << 20;
 
-// Entry `name` of the directory open as dfd (or the root path itself when
-// dfd == AT_FDCWD); stat relative to the directory fd (no full path walk).
-static int install_walk(int dfd, const std::string& name, const std::string& path, const std::string& rel,
-                        rf_install* in) {
+// Entry `path` (stat follows links, as os.Stat).  A directory is read,
+// sorted and closed before its children are visited, so the walk holds one
+// directory open at a time whatever the depth (walker.Scan closes each
+// directory after Readdirnames too).
+static int install_walk(const std::string& path, const std::string& rel, rf_install* in, int depth = 0) {
     struct stat st;
-    if (::fstatat(dfd, name.c_str(), &st, 0) != 0) {
+    if (::stat(path.c_str(), &st) != 0) {
         if (errno == ENOENT) return RF_OK;
         return fail(RF_EIO, "stat %s: %s", path.c_str(), strerror(errno));
     }
@@ -1033,37 +1041,33 @@ static int install_walk(int dfd, const std::string& name, const std::string& pat
         in->sizes.push_back((int64_t)st.st_size);
         return RF_OK;
     }
-    const int fd = ::openat(dfd, name.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
-    DIR* d = fd >= 0 ? ::fdopendir(fd) : nullptr;
-    if (!d) {
-        const int e = errno;
-        if (fd >= 0) ::close(fd);
-        return fail(RF_EIO, "open %s: %s", path.c_str(), strerror(e));
-    }
+    if (depth > 4096) return fail(RF_EIO, "walk %s: directory nesting deeper than 4096 (link cycle?)", path.c_str());
+    DIR* d = ::opendir(path.c_str());
+    if (!d) return fail(RF_EIO, "open %s: %s", path.c_str(), strerror(errno));
     std::vector<std::pair<std::string, unsigned char>> names;
     errno = 0;
     while (struct dirent* de = ::readdir(d)) {
         if (strcmp(de->d_name, ".") && strcmp(de->d_name, "..")) names.emplace_back(de->d_name, de->d_type);
         errno = 0;
     }
-    int rc = errno ? fail(RF_EIO, "readdir %s: %s", path.c_str(), strerror(errno)) : RF_OK;
+    const int rerr = errno;
+    ::closedir(d);
+    if (rerr) return fail(RF_EIO, "readdir %s: %s", path.c_str(), strerror(rerr));
     // char_traits<char>: bytewise (unsigned) order
     std::sort(names.begin(), names.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-    for (size_t i = 0; rc == RF_OK && i < names.size(); ++i) {
-        const std::string& nm = names[i].first;
+    for (const auto& [nm, type] : names) {
         std::string cpath = path + "/" + nm, crel = rel == "." ? nm : rel + "/" + nm;
-        if (names[i].second == DT_REG) {
+        if (type == DT_REG) {
             // a regular file (not a link): its Stat size is taken by the
             // parallel pass in rf_install_dir (-1 = pending)
             in->full.push_back(std::move(cpath));
             in->rel.push_back(std::move(crel));
             in->sizes.push_back(-1);
-        } else {  // directories, links and unknown types: stat (follows links)
-            rc = install_walk(::dirfd(d), nm, cpath, crel, in);
+        } else if (int rc = install_walk(cpath, crel, in, depth + 1)) {  // dirs, links, unknown: stat
+            return rc;
         }
     }
-    ::closedir(d);
-    return rc;
+    return RF_OK;
 }
 
 // Read file f (expected `want` bytes) into dst; the content must not have
@@ -1106,7 +1110,7 @@ extern "C" int rf_install_dir(rf_ctx* ctx, const char* root, rf_install** out) {
     const bool timing = getenv("RF_INSTALL_TIMING") != nullptr;
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_begin = now();
-    int rc = install_walk(AT_FDCWD, root, root, ".", in.get());
+    int rc = install_walk(root, ".", in.get());
     if (rc) return rc;
     {
         // Stat sizes of the regular files the walk did not stat, in parallel;
@@ -1895,7 +1899,9 @@ static int bloom_make(rf_ctx* ctx, uint64_t m, uint64_t k, const uint64_t* words
         return fail(RF_ENOMEM, "bloom alloc: %s", hipGetErrorString(e));
     }
     HIPC(hipMemset(bl->words.p, 0, 8 * cap));
-    if (nwords && words) HIPC(hipMemcpy(bl->words.p, words, 8 * nwords, hipMemcpyHostToDevice));
+    // the bitset holds exactly wordsNeeded(length) words (bitset.go:89-94,
+    // ReadFrom); words past them stay zero, as extendSetMaybe exposes them
+    if (need && words) HIPC(hipMemcpy(bl->words.p, words, 8 * need, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(bl->len_dev.p, &length, 8, hipMemcpyHostToDevice));
     bl->b.m = m;
     bl->b.k = k;
@@ -2146,12 +2152,17 @@ extern "C" int rf_bloom_collect_device(rf_bloom* bl, const void* d_digests32, co
     hipStream_t s = pick(bl->ctx, stream);
     HIPC(hipMemsetAsync(d_counts2, 0, 16, s));
     if (!n) return RF_OK;
-    HIPC(bl->dead.ensure(n));
-    HIPC(bl->tiles.ensure(4 * bloom_collect_tiles(n)));
-    HIPC(launch_bloom_collect(bl->b, static_cast<const uint8_t*>(d_digests32),
-                              static_cast<const int64_t*>(d_sizes), n, bl->dead.as<uint8_t>(),
-                              bl->tiles.as<uint32_t>(), static_cast<uint64_t*>(d_dead_idx),
-                              static_cast<uint64_t*>(d_counts2), s));
+    // per-call scratch in stream order (see dedup_on_stream)
+    void *dead = nullptr, *tiles = nullptr;
+    HIPC(hipMallocAsync(&dead, n, s));
+    hipError_t e = hipMallocAsync(&tiles, 4 * bloom_collect_tiles(n), s);
+    if (e == hipSuccess)
+        e = launch_bloom_collect(bl->b, static_cast<const uint8_t*>(d_digests32), static_cast<const int64_t*>(d_sizes),
+                                 n, static_cast<uint8_t*>(dead), static_cast<uint32_t*>(tiles),
+                                 static_cast<uint64_t*>(d_dead_idx), static_cast<uint64_t*>(d_counts2), s);
+    if (tiles) (void)hipFreeAsync(tiles, s);
+    (void)hipFreeAsync(dead, s);
+    if (e != hipSuccess) return fail(RF_EDEVICE, "collect: %s", hipGetErrorString(e));
     return RF_OK;
 }
 
@@ -2183,17 +2194,30 @@ extern "C" int rf_bloom_collect(rf_bloom* bl, const uint8_t* digests32, const in
 
 // ---------------------------------------------------------------------------
 // K5: Canonicalize's flowMap (flow.go:814-843, flowMap.Get/Put :881-907)
+// Scratch of a device-form call lives in stream order on the caller's
+// stream (hipMallocAsync / hipFreeAsync): calls on different streams or
+// threads never share it (the context's scratch buffers are only for the
+// host forms, which run under ctx->mu on ctx->stream).
+static int dedup_on_stream(const void* d_digests32, uint32_t n, void* d_canon, void* d_n_unique, hipStream_t s) {
+    void *tab = nullptr, *slot_of = nullptr;
+    HIPC(hipMallocAsync(&tab, 4ull * dedup_table_slots(n), s));
+    hipError_t e = hipMallocAsync(&slot_of, 4ull * std::max<uint32_t>(n, 1), s);
+    if (e == hipSuccess)
+        e = launch_dedup(static_cast<const uint8_t*>(d_digests32), n, static_cast<uint32_t*>(tab),
+                         static_cast<uint32_t*>(slot_of), static_cast<uint32_t*>(d_canon),
+                         static_cast<uint32_t*>(d_n_unique), s);
+    if (slot_of) (void)hipFreeAsync(slot_of, s);
+    (void)hipFreeAsync(tab, s);
+    if (e != hipSuccess) return fail(RF_EDEVICE, "dedup: %s", hipGetErrorString(e));
+    return RF_OK;
+}
+
 extern "C" int rf_dedup_digests_device(rf_ctx* ctx, const void* d_digests32, uint32_t n, void* d_canon,
                                        void* d_n_unique, void* stream) {
     ARG(ctx && d_n_unique && (n == 0 || (d_digests32 && d_canon)), "null argument");
     ARG(n <= (1u << 30), "dedup batch too large (n <= 2^30)");
     DevGuard dg(ctx->device);
-    HIPC(ctx->d_tab.ensure(4ull * dedup_table_slots(n)));
-    HIPC(ctx->d_tab2.ensure(4ull * std::max<uint32_t>(n, 1)));
-    HIPC(launch_dedup(static_cast<const uint8_t*>(d_digests32), n, ctx->d_tab.as<uint32_t>(),
-                      ctx->d_tab2.as<uint32_t>(), static_cast<uint32_t*>(d_canon),
-                      static_cast<uint32_t*>(d_n_unique), pick(ctx, stream)));
-    return RF_OK;
+    return dedup_on_stream(d_digests32, n, d_canon, d_n_unique, pick(ctx, stream));
 }
 
 extern "C" int rf_dedup_digests(rf_ctx* ctx, const uint8_t* digests32, uint32_t n, uint32_t* canon,
@@ -2206,8 +2230,10 @@ extern "C" int rf_dedup_digests(rf_ctx* ctx, const uint8_t* digests32, uint32_t 
     uint32_t* d_canon = ctx->d_tab3.as<uint32_t>();
     uint32_t* d_nu = d_canon + std::max<uint32_t>(n, 1);
     if (n) HIPC(hipMemcpyAsync(ctx->d_arena.p, digests32, 32ull * n, hipMemcpyHostToDevice, ctx->stream));
-    int rc = rf_dedup_digests_device(ctx, ctx->d_arena.p, n, d_canon, d_nu, ctx->stream);
-    if (rc) return rc;
+    HIPC(ctx->d_tab.ensure(4ull * dedup_table_slots(n)));
+    HIPC(ctx->d_tab2.ensure(4ull * std::max<uint32_t>(n, 1)));
+    HIPC(launch_dedup(ctx->d_arena.as<uint8_t>(), n, ctx->d_tab.as<uint32_t>(), ctx->d_tab2.as<uint32_t>(), d_canon,
+                      d_nu, ctx->stream));
     if (n) HIPC(hipMemcpyAsync(canon, d_canon, 4ull * n, hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipMemcpyAsync(n_unique, d_nu, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
@@ -2219,6 +2245,10 @@ extern "C" int rf_dedup_digests(rf_ctx* ctx, const uint8_t* digests32, uint32_t 
 struct rf_assoc {
     rf_ctx* ctx = nullptr;
     uint32_t cap = 0;
+    // the last Get launched on a caller's stream (rf_assoc_get_device): a
+    // rehash frees the old table only after it
+    hipEvent_t e_reader = nullptr;
+    bool reader_pending = false;
     DevBuf tag, keys, vals, count;                                   // the table
     DevBuf b_keys, b_vals, b_exp, b_canon, b_aslot, b_cls, b_rem, b_next, b_cnt, b_status, b_found;  // batch scratch
     AssocView view() {
@@ -2258,6 +2288,10 @@ extern "C" int rf_assoc_new(rf_ctx* ctx, uint64_t capacity, rf_assoc** out) {
 extern "C" void rf_assoc_destroy(rf_assoc* a) {
     if (!a) return;
     DevGuard dg(a->ctx->device);
+    if (a->e_reader) {
+        if (a->reader_pending) (void)hipEventSynchronize(a->e_reader);
+        (void)hipEventDestroy(a->e_reader);
+    }
     for (DevBuf* d : {&a->tag, &a->keys, &a->vals, &a->count, &a->b_keys, &a->b_vals, &a->b_exp, &a->b_canon,
                       &a->b_aslot, &a->b_cls, &a->b_rem, &a->b_next, &a->b_cnt, &a->b_status, &a->b_found})
         d->release();
@@ -2284,6 +2318,10 @@ static int assoc_reserve(rf_assoc* a, uint64_t incoming) {
     HIPC(assoc_alloc_table(a, (uint32_t)cap, ctx->stream));
     HIPC(launch_assoc_rehash(old.view(), old.cap, a->view(), ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
+    if (a->reader_pending) {  // a device-form Get on another stream may still read the old table
+        HIPC(hipEventSynchronize(a->e_reader));
+        a->reader_pending = false;
+    }
     old.tag.release();
     old.keys.release();
     old.vals.release();
@@ -2378,9 +2416,16 @@ extern "C" int rf_assoc_put(rf_assoc* a, int kind, const uint8_t* expect32, cons
 extern "C" int rf_assoc_get_device(rf_assoc* a, int kind, const void* d_keys32, uint64_t n, void* d_vals32,
                                    void* d_found, void* stream) {
     ARG(a && (n == 0 || (d_keys32 && d_vals32 && d_found)), "null argument");
+    std::lock_guard<std::mutex> lk(a->ctx->mu);  // no Put may swap the table meanwhile
     DevGuard dg(a->ctx->device);
+    hipStream_t s = pick(a->ctx, stream);
     HIPC(launch_assoc_get(a->view(), (uint32_t)kind, static_cast<const uint8_t*>(d_keys32), n,
-                          static_cast<uint8_t*>(d_vals32), static_cast<uint8_t*>(d_found), pick(a->ctx, stream)));
+                          static_cast<uint8_t*>(d_vals32), static_cast<uint8_t*>(d_found), s));
+    if (s != a->ctx->stream) {  // Puts run on ctx->stream, ordered after it already
+        if (!a->e_reader) HIPC(hipEventCreateWithFlags(&a->e_reader, hipEventDisableTiming));
+        HIPC(hipEventRecord(a->e_reader, s));
+        a->reader_pending = true;
+    }
     return RF_OK;
 }
 
@@ -2403,21 +2448,24 @@ extern "C" int rf_assoc_get(rf_assoc* a, int kind, const uint8_t* keys32, uint64
     return RF_OK;
 }
 
-// Eval.lookup over a batch of nodes (eval.go:1172-1258): one Get batch over
+// Eval.lookup over a batch of nodes (eval.go:1172-1220): one Get batch over
 // every node's cache keys (the BatchGetItem the TODO at eval.go:1199-1201
-// asks for), first hit per node selected on the device, then the read
-// repair as one Put batch in node order.
-extern "C" int rf_assoc_lookup(rf_assoc* a, int kind, const uint8_t* keys32, const uint64_t* key_ptr, uint64_t n_nodes,
-                               int repair, int32_t* which, uint8_t* vals32) {
-    ARG(a && key_ptr && (n_nodes == 0 || (which && vals32)), "null argument");
-    ARG(repair >= 0 && repair <= 2, "repair must be 0, 1 or 2");
-    ARG(kind >= 0 && kind < (1 << 30), "bad assoc kind");
-    if (!n_nodes) return RF_OK;
+// asks for), first hit per node selected on the device.  Read only.
+static int check_key_ptr(const uint64_t* key_ptr, uint64_t n_nodes) {
     ARG(key_ptr[0] == 0, "key_ptr[0] must be 0");
     for (uint64_t i = 0; i < n_nodes; ++i) ARG(key_ptr[i] <= key_ptr[i + 1], "key_ptr not monotone");
+    ARG(key_ptr[n_nodes] <= (1u << 30), "lookup batch too large");
+    return RF_OK;
+}
+
+extern "C" int rf_assoc_lookup(rf_assoc* a, int kind, const uint8_t* keys32, const uint64_t* key_ptr, uint64_t n_nodes,
+                               int32_t* which, uint8_t* vals32, uint8_t* key_found, uint8_t* key_vals32) {
+    ARG(a && key_ptr && (n_nodes == 0 || (which && vals32)), "null argument");
+    ARG(kind >= 0 && kind < (1 << 30), "bad assoc kind");
+    if (!n_nodes) return RF_OK;
+    if (int rc = check_key_ptr(key_ptr, n_nodes)) return rc;
     const uint64_t nk = key_ptr[n_nodes];
     ARG(nk == 0 || keys32, "null keys");
-    ARG(nk <= (1u << 30), "lookup batch too large");
     rf_ctx* ctx = a->ctx;
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
@@ -2439,28 +2487,39 @@ extern "C" int rf_assoc_lookup(rf_assoc* a, int kind, const uint8_t* keys32, con
     HIPC(launch_assoc_select(a->b_found.as<uint8_t>(), a->b_vals.as<uint8_t>(), d_ptr, n_nodes, d_which, d_out, s));
     HIPC(hipMemcpyAsync(which, d_which, 4 * n_nodes, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(vals32, d_out, 32 * n_nodes, hipMemcpyDeviceToHost, s));
-    std::vector<uint8_t> found;
-    if (repair == 2) {
-        found.resize(nk);
-        if (nk) HIPC(hipMemcpyAsync(found.data(), a->b_found.p, nk, hipMemcpyDeviceToHost, s));
-    }
+    if (key_found && nk) HIPC(hipMemcpyAsync(key_found, a->b_found.p, nk, hipMemcpyDeviceToHost, s));
+    if (key_vals32 && nk) HIPC(hipMemcpyAsync(key_vals32, a->b_vals.p, 32 * nk, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    if (!repair) return RF_OK;
-    // read repair: Put(zero expect, key, fsid) per other key of a hit node,
-    // node order then key order (eval.go:1247-1258; precise: missing keys only)
+    return RF_OK;
+}
+
+// Read repair of the nodes the caller verified (eval.go:1227-1258): Put(zero
+// expect) of the node's value under its other keys (blind) or under the ones
+// the Get found missing (precise), as one Put batch in node order, key order.
+extern "C" int rf_assoc_repair(rf_assoc* a, int kind, const uint8_t* keys32, const uint64_t* key_ptr, uint64_t n_nodes,
+                               const int32_t* which, const uint8_t* vals32, const uint8_t* key_found) {
+    ARG(a && key_ptr && (n_nodes == 0 || (which && vals32)), "null argument");
+    ARG(kind >= 0 && kind < (1 << 30), "bad assoc kind");
+    if (!n_nodes) return RF_OK;
+    if (int rc = check_key_ptr(key_ptr, n_nodes)) return rc;
+    const uint64_t nk = key_ptr[n_nodes];
+    ARG(nk == 0 || keys32, "null keys");
     std::vector<uint8_t> rk, rv;
-    rk.reserve(32 * nk);
-    rv.reserve(32 * nk);
     for (uint64_t i = 0; i < n_nodes; ++i) {
         if (which[i] < 0) continue;
+        ARG((uint64_t)which[i] < key_ptr[i + 1] - key_ptr[i], "which[i] past the node's keys");
         for (uint64_t k = key_ptr[i]; k < key_ptr[i + 1]; ++k) {
-            if ((int64_t)(k - key_ptr[i]) == which[i] || (repair == 2 && found[k])) continue;
+            if ((int64_t)(k - key_ptr[i]) == which[i] || (key_found && key_found[k])) continue;
             rk.insert(rk.end(), keys32 + 32 * k, keys32 + 32 * k + 32);
             rv.insert(rv.end(), vals32 + 32 * i, vals32 + 32 * i + 32);
         }
     }
     const uint64_t nr = rk.size() / 32;
     if (!nr) return RF_OK;
+    rf_ctx* ctx = a->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
     HIPC(a->b_keys.ensure(32 * nr));
     HIPC(a->b_vals.ensure(32 * nr));
     HIPC(a->b_status.ensure(4 * nr));

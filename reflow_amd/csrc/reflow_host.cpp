@@ -633,24 +633,41 @@ void Assoc::Put(AssocKind kind, const Digest& expect, const Digest& k, const Dig
 }
 
 std::vector<std::pair<int, Digest>> Assoc::Lookup(AssocKind kind, const std::vector<std::vector<Digest>>& node_keys,
-                                                  int repair) {
+                                                  int repair, const FsidCheck& usable, const FsidCheck& verified) {
+    if (repair < 0 || repair > 2) throw Error(RF_EINVAL, "repair must be 0, 1 or 2");
     std::vector<uint64_t> ptr{0};
     std::vector<uint8_t> flat;
     for (const auto& ks : node_keys) {
         for (const Digest& k : ks) flat.insert(flat.end(), k.b.begin(), k.b.end());
         ptr.push_back(ptr.back() + ks.size());
     }
-    const size_t n = node_keys.size();
-    std::vector<int32_t> which(n);
-    std::vector<uint8_t> vals(32 * n);
-    std::vector<std::pair<int, Digest>> out(n);
+    const size_t n = node_keys.size(), nk = ptr.back();
+    std::vector<std::pair<int, Digest>> out(n, {-1, Digest{}});
     if (!n) return out;
-    Check(rf_assoc_lookup(a_, (int)kind, flat.empty() ? nullptr : flat.data(), ptr.data(), n, repair, which.data(),
-                          vals.data()));
+    std::vector<int32_t> which(n);
+    std::vector<uint8_t> vals(32 * n), found(nk + 1), kvals(32 * nk + 32);
+    Check(rf_assoc_lookup(a_, (int)kind, flat.empty() ? nullptr : flat.data(), ptr.data(), n, which.data(),
+                          vals.data(), found.data(), kvals.data()));
+    // per node: the first found key whose fsid the caller can use
+    std::vector<int32_t> rep(n, -1);
+    std::vector<uint8_t> rvals(32 * n, 0);
     for (size_t i = 0; i < n; ++i) {
-        out[i].first = which[i];
-        memcpy(out[i].second.b.data(), vals.data() + 32 * i, 32);
+        for (uint64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+            if (!found[k]) continue;
+            Digest v;
+            memcpy(v.b.data(), kvals.data() + 32 * k, 32);
+            if (usable && !usable(i, v)) continue;
+            out[i] = {(int)(k - ptr[i]), v};
+            break;
+        }
+        if (out[i].first >= 0 && (!verified || verified(i, out[i].second))) {
+            rep[i] = out[i].first;
+            memcpy(rvals.data() + 32 * i, out[i].second.b.data(), 32);
+        }
     }
+    if (repair)
+        Check(rf_assoc_repair(a_, (int)kind, flat.empty() ? nullptr : flat.data(), ptr.data(), n, rep.data(),
+                              rvals.data(), repair == 2 ? found.data() : nullptr));
     return out;
 }
 

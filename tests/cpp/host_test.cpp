@@ -240,6 +240,10 @@ static void TestAssoc(Engine& e) {
     auto lk = a.Lookup(AssocFileset, {{phys, logi}, {}}, 2);
     EXPECT(lk[0].first == 1 && lk[0].second == v2 && lk[1].first == -1, "lookup first hit");
     EXPECT(a.Get(AssocFileset, phys).second == v2, "precise read repair");
+    // a node whose files are missing (verified = false) is not repaired
+    const Digest other = dg.FromString("other key");
+    lk = a.Lookup(AssocFileset, {{other, logi}}, 1, nullptr, [](size_t, const Digest&) { return false; });
+    EXPECT(lk[0].first == 1 && !a.GetBatch(AssocFileset, {other})[0], "no repair of an unverified node");
 }
 
 // Executor.install (local/executor.go:514-557): the executor_test.go:86-88

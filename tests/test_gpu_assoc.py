@@ -114,6 +114,11 @@ def test_assoc_abbrev_expansion(ctx):
     a.close()
 
 
+def capi_assoc(ctx, capacity):
+    from reflow_amd import capi
+    return capi.Assoc(ctx, capacity=capacity)
+
+
 def _lookup_case(rng, n_nodes, pool, vals):
     """Nodes with 0..3 cache keys (CacheKeys gives 1-2; 0 and 3 are edges),
     keys shared between nodes (synonyms), some keys present."""
@@ -124,14 +129,17 @@ def _lookup_case(rng, n_nodes, pool, vals):
 
 @pytest.mark.parametrize("repair", [0, 1, 2])
 def test_assoc_lookup_matches_oracle(ctx, repair):
-    """Eval.lookup's assoc step (eval.go:1172-1258) for a batch of nodes: first
-    hit in key order wins; blind (1) or precise (2) read repair; the table
-    after the batch equals the oracle's, key for key."""
-    from reflow_amd import capi
+    """Eval.lookup's assoc step (eval.go:1172-1258) for a batch of nodes: one
+    Get batch (rf_assoc_lookup, read only); the caller's unmarshal rejects some
+    fsids (the next found key wins, :1210-1218) and its missing() check fails
+    some nodes; rf_assoc_repair then writes blind (1) or precise (2) repairs
+    for the verified nodes only.  The table after each batch equals the
+    oracle's, key for key."""
     rng = random.Random(40 + repair)
     pool = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(400)]
     vals = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(40)]
-    a = capi.Assoc(ctx, capacity=64)
+    bad = set(vals[:6])          # fsids that do not unmarshal
+    a = capi_assoc(ctx, 64)
     ref = O.InmemoryAssoc()
     for rnd in range(3):  # repairs of one batch feed the next
         node_keys, preset = _lookup_case(rng, 700, pool, vals)
@@ -141,12 +149,27 @@ def test_assoc_lookup_matches_oracle(ctx, repair):
             st = a.put(0, np.frombuffer(b"".join(k for k, _ in preset), np.uint8),
                        np.frombuffer(b"".join(v for _, v in preset), np.uint8))
             assert (st == 0).all()
-        want = O.assoc_lookup(ref, 0, node_keys, repair)
+        unverified = set(rng.sample(range(700), 60))  # nodes whose files are missing
+        want = O.eval_lookup(ref, 0, node_keys, repair, usable=lambda i, v: v not in bad,
+                             verified=lambda i, v: i not in unverified)
         flat = b"".join(k for ks in node_keys for k in ks)
         ptr = np.cumsum([0] + [len(ks) for ks in node_keys]).astype(np.uint64)
-        which, got = a.lookup(0, np.frombuffer(flat, np.uint8), ptr, repair)
-        assert [int(w) for w in which] == [w for w, _ in want]
-        assert [g.tobytes() for g in got] == [v for _, v in want]
+        kb = np.frombuffer(flat, np.uint8)
+        which, got, kf, kv = a.lookup(0, kb, ptr)
+        # the caller's key loop over the per-key results
+        w2, v2, rep = [], [], []
+        for i, ks in enumerate(node_keys):
+            w = next((j for j in range(len(ks)) if kf[ptr[i] + j] and kv[ptr[i] + j].tobytes() not in bad), -1)
+            v = kv[ptr[i] + w].tobytes() if w >= 0 else ZERO
+            w2.append(w)
+            v2.append(v)
+            rep.append(w if w >= 0 and i not in unverified else -1)
+        assert list(zip(w2, v2)) == want
+        first = [next((j for j in range(len(ks)) if kf[ptr[i] + j]), -1) for i, ks in enumerate(node_keys)]
+        assert [int(x) for x in which] == first
+        if repair:
+            a.repair(0, kb, ptr, rep, np.frombuffer(b"".join(v2), np.uint8).reshape(-1, 32),
+                     kf if repair == 2 else None)
     allk = np.frombuffer(b"".join(pool), np.uint8)
     gv, gf = a.get(0, allk)
     for i, k in enumerate(pool):

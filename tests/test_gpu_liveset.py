@@ -118,3 +118,28 @@ def test_marshal_golden_fixture(ctx):
         assert b.marshal_json().decode() == c["json"]
         assert hashlib.sha256(b.marshal_binary()).hexdigest() == c["binary_sha256"]
         b.close()
+
+
+def test_load_ignores_words_past_length(ctx):
+    """A bitset holds exactly wordsNeeded(length) words (bitset.go:89-94,
+    ReadFrom): words a caller passes beyond them must not surface when Add
+    grows the length (extendSetMaybe exposes zero words).  Checked against the
+    oracle's Add from the truncated words."""
+    from reflow_amd import capi
+    rng = np.random.default_rng(11)
+    m, k = 4096, 3
+    length = 1000                       # 16 words needed
+    words = rng.integers(0, 2**63, size=(m + 63) // 64, dtype=np.uint64)  # junk past word 16
+    b = capi.Bloom.load(ctx, m, k, words, length)
+    keys = rng.integers(0, 256, size=32 * 200, dtype=np.uint8)
+    b.add(keys)
+    want = np.zeros((m + 63) // 64, dtype=np.uint64)
+    need = (length + 63) // 64
+    want[:need] = words[:need]
+    ln = np.array([length], dtype=np.uint64)
+    O.lib().orc_bloomlive_add_batch(want.ctypes.data, ln.ctypes.data, m, k, keys.tobytes(), 200)
+    got = b.words()
+    assert b.params()[2] == int(ln[0])
+    nw = (int(ln[0]) + 63) // 64
+    assert (got[:nw] == want[:nw]).all()
+    b.close()

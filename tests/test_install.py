@@ -121,3 +121,17 @@ def test_gpu_install_unreadable_file_fails(ctx, tmp_path):
     with pytest.raises(capi.RfError) as e:
         ctx.install_dir(str(tmp_path))
     assert e.value.code == capi.RF_EIO
+
+
+@pytest.mark.gpu
+def test_gpu_install_deep_tree(ctx, tmp_path):
+    """A tree nested 300 directories deep (the walk holds one directory open at
+    a time, as walker.Scan does), with a file at every level."""
+    d = str(tmp_path)
+    p = d
+    for i in range(300):
+        p = os.path.join(p, "n%03d" % i)
+        _write(os.path.join(p, "f"), b"level %d" % i)
+    ents, fs = ctx.install_dir(d)
+    w_ents, w_fs = O.install_dir(d)
+    assert ents == w_ents and fs == w_fs and len(ents) == 300
