@@ -152,6 +152,36 @@ void rf_sha_plan_destroy(rf_sha_plan *plan);
 #define RF_SHA_ALL_HOST 32u    /* every message on the host leg (needs SHA-NI and host threads) */
 #define RF_SHA_NO_HOST 64u     /* no host leg: every message on the GPU kernels */
 
+/* ---- Streaming SHA-256 (Digester.NewWriter: an io.Writer whose state carries
+ * across Write calls) for many streams at once -------------------------------
+ * Repository.Put hashes an io.Reader as it copies it (repository/file/
+ * repository.go:237-264; s3's Put through a TeeReader, repository/s3/s3.go:
+ * 120-147): the shim feeds each upload's chunks here as they arrive, so no
+ * upload is buffered whole.  Per stream the carried partial block plus its
+ * chunks give whole blocks, hashed from the stream's midstate -- the largest
+ * on the host leg (in place), the rest by k1_sha256_resume on the GPU, by a
+ * makespan model like a K1 plan.  flags: 0, RF_SHA_ALL_HOST or
+ * RF_SHA_NO_HOST (every segment on k1_sha256_resume). */
+typedef struct rf_sha_streams rf_sha_streams;
+int rf_sha_streams_open(rf_ctx *ctx, uint64_t n_streams, uint32_t flags, rf_sha_streams **out);
+void rf_sha_streams_close(rf_sha_streams *s);
+/* Write chunk i to stream ids[i]; chunks of one stream apply in batch order. */
+int rf_sha_streams_write(rf_sha_streams *s, const uint64_t *ids, const uint8_t *const *chunks,
+                         const uint64_t *lens, uint64_t n);
+/* out32[i] = Digest() of stream ids[i] (distinct ids); the stream restarts empty. */
+int rf_sha_streams_digest(rf_sha_streams *s, const uint64_t *ids, uint64_t n, uint8_t *out32);
+/* Bytes written to stream id since its last digest (Put's returned size). */
+int rf_sha_streams_len(rf_sha_streams *s, uint64_t id, uint64_t *len);
+/* Integrity check (ReadFrom / WriteTo re-digest, repository/file/repository.go:
+ * 126-166, 212): status[i] = RF_OK or RF_EINTEGRITY (digest of stream ids[i] vs
+ * want32[i]); returns RF_EINTEGRITY if any differs (errors.Integrity).  The
+ * streams restart empty. */
+int rf_sha_streams_verify(rf_sha_streams *s, const uint64_t *ids, const uint8_t *want32, uint64_t n,
+                          int32_t *status);
+/* The same for whole messages: status[i] for SHA256(msg i) vs want32[i]. */
+int rf_sha256_verify(rf_ctx *ctx, const uint8_t *const *msgs, const uint64_t *lens, uint64_t n,
+                     const uint8_t *want32, int32_t *status);
+
 /* Synthetic data generator (bench / tests): fills d_arena so that message i
  * is the splitmix64 counter stream with seed (seed ^ i). */
 int rf_gen_fill(rf_ctx *ctx, void *d_arena, const uint64_t *d_offs, const uint64_t *d_lens,
@@ -275,6 +305,17 @@ typedef struct {
     float last_ms;
 } rf_graph_stats;
 int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
+
+/* Eval.dirty (eval.go:874-887) for every node of a Flow graph at once:
+ * dirty[i] = 1 iff no_cache_extern and node i is an OpExtern (is_extern[i])
+ * or one of its Deps is dirty -- Deps only ("dirty considers only visible
+ * nodes": not MapFlow, Parent or continuations).  Eval.todo consults it under
+ * NoCacheExtern to skip a node's cache lookup (eval.go:910).  Node i's deps
+ * are deps[dep_ptr[i] .. dep_ptr[i+1]).  The closure runs on the GPU (K3
+ * reachability over reverse edges, one launch per level); the reference's
+ * per-node recursion has no memo. */
+int rf_flow_dirty(rf_ctx *ctx, uint64_t n, const uint64_t *dep_ptr, const uint32_t *deps,
+                  const uint8_t *is_extern, int no_cache_extern, uint8_t *dirty);
 
 /* ---- K4: bloomlive / assoc probe (bloom.go:182-190, bloomlive.go:30-36) --
  * Filters cache-key lookups before Assoc.Get (eval.go:1202-1220) and serves

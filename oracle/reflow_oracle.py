@@ -422,6 +422,21 @@ class OFlow:
         return keys
 
 
+def eval_dirty(f: OFlow, no_cache_extern: bool, memo=None) -> bool:
+    """Eval.dirty (eval.go:874-887), restated: false unless NoCacheExtern; an
+    OpExtern is dirty; otherwise dirty iff a Dep is (Deps only -- not MapFlow
+    or Parent).  `memo` caches per node (the reference recomputes; the answer
+    is the same)."""
+    if not no_cache_extern:
+        return False
+    if memo is None:
+        memo = {}
+    k = id(f)
+    if k not in memo:
+        memo[k] = f.op == OP["OpExtern"] or any(eval_dirty(d, True, memo) for d in f.deps)
+    return memo[k]
+
+
 def canonicalize(root: OFlow, hashv1: bool = False, universe: bytes = b""):
     """Flow.Canonicalize (flow.go:814-843) with flowMap.Get/Put (:881-907),
     restated node for node: Get by the ORIGINAL node's digest before recursing,

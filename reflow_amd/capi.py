@@ -44,6 +44,8 @@ EXPORTS = [
     "rf_assoc_new", "rf_assoc_destroy", "rf_assoc_put", "rf_assoc_get", "rf_assoc_get_device",
     "rf_assoc_get_abbrev", "rf_assoc_stats", "rf_assoc_put_device",
     "rf_set_host_threads", "rf_host_info", "rf_assoc_repair",
+    "rf_sha_streams_open", "rf_sha_streams_close", "rf_sha_streams_write", "rf_sha_streams_digest",
+    "rf_sha_streams_len", "rf_sha_streams_verify", "rf_sha256_verify", "rf_flow_dirty",
 ]
 
 
@@ -246,6 +248,13 @@ def lib():
             "rf_assoc_stats": ([vp, vp, vp], i32),
             "rf_assoc_put_device": ([vp, i32, vp, vp, vp, u64, vp], i32),
             "rf_set_host_threads": ([vp, i32], i32),
+            "rf_sha_streams_open": ([vp, u64, u32, vp], i32), "rf_sha_streams_close": ([vp], None),
+            "rf_sha_streams_write": ([vp, vp, vp, vp, u64], i32),
+            "rf_sha_streams_digest": ([vp, vp, u64, vp], i32),
+            "rf_sha_streams_len": ([vp, u64, vp], i32),
+            "rf_sha_streams_verify": ([vp, vp, vp, u64, vp], i32),
+            "rf_sha256_verify": ([vp, vp, vp, u64, vp, vp], i32),
+            "rf_flow_dirty": ([vp, u64, vp, vp, vp, i32, vp], i32),
             "rf_host_info": ([vp, vp, vp, vp], i32),
         }
         for name, (args, res) in sigs.items():
@@ -356,6 +365,33 @@ class Context:
         _check(lib().rf_sha256_arena(self._h, _ptr(arena), _ptr(offs), _ptr(lens), n, _ptr(out)))
         return out
 
+    def sha256_verify(self, msgs, want):
+        """(rc, status per message) of rf_sha256_verify."""
+        n = len(msgs)
+        bufs = [ctypes.create_string_buffer(bytes(m), max(len(m), 1)) for m in msgs]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in bufs])
+        lens = np.array([len(m) for m in msgs] or [0], dtype=np.uint64)
+        w = np.frombuffer(b"".join(want) or bytes(32), dtype=np.uint8).copy()
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        rc = lib().rf_sha256_verify(self._h, ptrs, _ptr(lens), n, _ptr(w), _ptr(st))
+        if rc not in (RF_OK, RF_EINTEGRITY):
+            _check(rc)
+        return rc, st[:n]
+
+    def flow_dirty(self, dep_ptr, deps, is_extern, no_cache_extern=True):
+        """rf_flow_dirty: Eval.dirty of every node (bool array)."""
+        dp = np.ascontiguousarray(dep_ptr, dtype=np.uint64)
+        dv = np.ascontiguousarray(deps, dtype=np.uint32)
+        ex = np.ascontiguousarray(is_extern, dtype=np.uint8)
+        n = len(dp) - 1
+        out = np.zeros(max(n, 1), dtype=np.uint8)
+        _check(lib().rf_flow_dirty(self._h, n, _ptr(dp), _ptr(dv) if len(dv) else None, _ptr(ex),
+                                   1 if no_cache_extern else 0, _ptr(out)))
+        return out[:n].astype(bool)
+
+    def sha_streams(self, n, flags=0):
+        return ShaStreams(self, n, flags)
+
     def sha_plan(self, offs, lens, flags=0):
         return ShaPlan(self, offs, lens, flags)
 
@@ -442,6 +478,58 @@ class Context:
         _check(lib().rf_fileset_value_digest_batch(self._h, ctypes.byref(t), _ptr(roots), len(sets),
                                                    _ptr(out)))
         return [out[32 * i:32 * i + 32].tobytes() for i in range(len(sets))]
+
+
+class ShaStreams:
+    """rf_sha_streams: n streaming SHA-256 writers (Digester.NewWriter)."""
+
+    def __init__(self, ctx, n, flags=0):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        _check(lib().rf_sha_streams_open(ctx.handle, n, flags, ctypes.byref(self._h)))
+
+    def write(self, ids, chunks):
+        """chunks[i] (bytes) to stream ids[i], in order."""
+        n = len(ids)
+        if n == 0:
+            return
+        bufs = [ctypes.create_string_buffer(bytes(c), max(len(c), 1)) for c in chunks]
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        lens = np.array([len(c) for c in chunks], dtype=np.uint64)
+        idv = np.ascontiguousarray(ids, dtype=np.uint64)
+        _check(lib().rf_sha_streams_write(self._h, _ptr(idv), ptrs, _ptr(lens), n))
+
+    def digest(self, ids):
+        idv = np.ascontiguousarray(ids, dtype=np.uint64)
+        out = np.zeros(32 * max(len(idv), 1), dtype=np.uint8)
+        _check(lib().rf_sha_streams_digest(self._h, _ptr(idv), len(idv), _ptr(out)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(len(idv))]
+
+    def length(self, i):
+        n = ctypes.c_uint64(0)
+        _check(lib().rf_sha_streams_len(self._h, i, ctypes.byref(n)))
+        return n.value
+
+    def verify(self, ids, want):
+        """(rc, status per stream): rc RF_OK or RF_EINTEGRITY."""
+        idv = np.ascontiguousarray(ids, dtype=np.uint64)
+        w = np.frombuffer(b"".join(want), dtype=np.uint8).copy()
+        st = np.zeros(max(len(idv), 1), dtype=np.int32)
+        rc = lib().rf_sha_streams_verify(self._h, _ptr(idv), _ptr(w), len(idv), _ptr(st))
+        if rc not in (RF_OK, RF_EINTEGRITY):
+            _check(rc)
+        return rc, st[:len(idv)]
+
+    def close(self):
+        if self._h:
+            lib().rf_sha_streams_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class DeviceBuffer:

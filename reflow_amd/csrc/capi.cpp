@@ -32,16 +32,17 @@
 
 #include "engine.h"
 #include "host_leg.h"
+#include "ctx.h"
 #include "host_sha.h"
 #include "reflow_hip.h"
 
 using namespace rf;
 
 // ---------------------------------------------------------------------------
-// errors
+// errors (declared in ctx.h)
 static thread_local std::string g_err;
 
-static int fail(int code, const char* fmt, ...) {
+int rf::fail(int code, const char* fmt, ...) {
     char buf[1024];
     va_list ap;
     va_start(ap, fmt);
@@ -51,98 +52,8 @@ static int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIPC(x)                                                                              \
-    do {                                                                                     \
-        hipError_t e_ = (x);                                                                 \
-        if (e_ != hipSuccess) return fail(RF_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
-    } while (0)
-
-#define ARG(cond, msg)                                   \
-    do {                                                 \
-        if (!(cond)) return fail(RF_EINVAL, "%s", msg); \
-    } while (0)
-
 extern "C" const char* rf_last_error(void) { return g_err.c_str(); }
-extern "C" const char* rf_version(void) { return "reflow-hip 0.1 gfx950"; }
-
-// ---------------------------------------------------------------------------
-// device buffers
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t n) {
-        if (n <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(n, 4096);
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) cap = want;
-        return e;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    template <class T>
-    T* as() const { return static_cast<T*>(p); }
-};
-
-struct HostBuf {  // pinned staging
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t n) {
-        if (n <= cap) return hipSuccess;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(n, 1 << 16);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-        if (e == hipSuccess) cap = want;
-        return e;
-    }
-    void release() {
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
-};
-
-struct rf_ctx {
-    int device = 0;
-    int n_cu = 256;
-    hipStream_t stream = nullptr;
-    std::mutex mu;
-    DevBuf d_arena, d_out, d_tmp, d_tab, d_tab2, d_tab3, d_place;
-    HostBuf h_stage;
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    rf_sha_plan* tplan = nullptr;  // one-shot batches (transient_plan)
-    int host_threads = -1;         // K1 host leg: -1 default width, 0 none
-    HostPool* pool = nullptr;      // created on first use
-};
-
-// Host-leg width of a context (0 when the CPU has no SHA extensions).
-static unsigned ctx_host_threads(rf_ctx* ctx) {
-    if (!host_sha_available()) return 0;
-    return ctx->host_threads < 0 ? host_default_threads() : (unsigned)ctx->host_threads;
-}
-
-static HostPool* ctx_pool(rf_ctx* ctx) {
-    const unsigned n = ctx_host_threads(ctx);
-    if (!n) return nullptr;
-    if (ctx->pool && ctx->pool->size() != n) {
-        delete ctx->pool;
-        ctx->pool = nullptr;
-    }
-    if (!ctx->pool) ctx->pool = new HostPool(ctx->device, n);
-    return ctx->pool;
-}
-
-struct DevGuard {
-    explicit DevGuard(int d) { (void)hipSetDevice(d); }
-};
+extern "C" const char* rf_version(void) { return "reflow-hip 0.2 gfx950"; }
 
 extern "C" int rf_device_count(int* n) {
     ARG(n, "null out");
@@ -237,9 +148,6 @@ extern "C" int rf_host_info(rf_ctx* ctx, int* threads, double* core_bytes_per_s,
     return RF_OK;
 }
 
-static hipStream_t pick(rf_ctx* ctx, void* stream) {
-    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-}
 
 // ---------------------------------------------------------------------------
 // device memory / timing

@@ -1,0 +1,118 @@
+// ctx.h -- internal: the context object behind rf_ctx* and the helpers the
+// C-ABI translation units share (error reporting, device/pinned buffers).
+// Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+
+#include "host_leg.h"
+#include "host_sha.h"
+#include "reflow_hip.h"
+
+namespace rf {
+// Sets the thread-local rf_last_error() message; returns code.
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+}  // namespace rf
+
+#define HIPC(x)                                                                                  \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) return rf::fail(RF_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+#define ARG(cond, msg)                                       \
+    do {                                                     \
+        if (!(cond)) return rf::fail(RF_EINVAL, "%s", msg); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// device buffers
+using rf::HostPool;
+using rf::host_sha_available;
+using rf::host_default_threads;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostBuf {  // pinned staging
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1 << 16);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
+};
+
+struct rf_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    DevBuf d_arena, d_out, d_tmp, d_tab, d_tab2, d_tab3, d_place;
+    HostBuf h_stage;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    rf_sha_plan* tplan = nullptr;  // one-shot batches (transient_plan)
+    int host_threads = -1;         // K1 host leg: -1 default width, 0 none
+    HostPool* pool = nullptr;      // created on first use
+};
+
+// Host-leg width of a context (0 when the CPU has no SHA extensions).
+inline unsigned ctx_host_threads(rf_ctx* ctx) {
+    if (!host_sha_available()) return 0;
+    return ctx->host_threads < 0 ? host_default_threads() : (unsigned)ctx->host_threads;
+}
+
+inline HostPool* ctx_pool(rf_ctx* ctx) {
+    const unsigned n = ctx_host_threads(ctx);
+    if (!n) return nullptr;
+    if (ctx->pool && ctx->pool->size() != n) {
+        delete ctx->pool;
+        ctx->pool = nullptr;
+    }
+    if (!ctx->pool) ctx->pool = new HostPool(ctx->device, n);
+    return ctx->pool;
+}
+
+
+struct DevGuard {
+    explicit DevGuard(int d) { (void)hipSetDevice(d); }
+};
+
+inline hipStream_t pick(rf_ctx* ctx, void* stream) {
+    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}

@@ -40,6 +40,17 @@ hipError_t launch_sha_pair(const SoloArgs& a, hipStream_t s);
 // Eight messages per wave on the duo's two-lane chain (small sets).
 hipError_t launch_sha_octo(const SoloArgs& a, hipStream_t s);
 
+// Streaming SHA-256 (rf_sha_streams): segment i = nblocks[i] whole blocks at
+// arena + offs[i] (16-B aligned) fed into midstate mid[8i..8i+7] in place.
+struct ResumeArgs {
+    const uint8_t* arena;
+    const uint64_t* offs;
+    const uint64_t* nblocks;
+    uint32_t* mid;
+    uint32_t n;
+};
+hipError_t launch_sha_resume(const ResumeArgs& a, hipStream_t s);
+
 // out32[ids[i]] = digs32[i] (the host leg's digests into the plan's output).
 hipError_t launch_scatter_digests(uint8_t* out32, const uint32_t* ids, const uint8_t* digs32, uint64_t n,
                                   hipStream_t s);
@@ -81,6 +92,11 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipSt
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);
+
+// K3 reachability (Eval.dirty): one frontier level; bits = marked set,
+// next/n_next = the newly marked nodes (n_next zeroed by the caller).
+hipError_t launch_reach_step(const uint32_t* front, uint32_t n_front, const uint64_t* cons_ptr, const uint32_t* cons,
+                             uint32_t* bits, uint32_t* next, uint32_t* n_next, hipStream_t s);
 
 hipError_t launch_or_reduce(const uint64_t* gathered, uint64_t nwords, int nranks, uint64_t* out,
                             hipStream_t s);

@@ -694,6 +694,37 @@ __global__ __launch_bounds__(256) void k_gen_fill(uint8_t* arena, const uint64_t
     }
 }
 
+// Streaming: lane per segment, whole blocks from a carried midstate (the
+// Writer state of Digester.NewWriter between Write calls).  Segments come
+// largest first, so a wave's lanes run similar block counts.
+__global__ __launch_bounds__(256) void k1_sha256_resume(ResumeArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    ShaState st;
+    uint4* m4 = reinterpret_cast<uint4*>(a.mid + 8ull * i);
+    const uint4 lo = m4[0], hi = m4[1];
+    st.h[0] = lo.x; st.h[1] = lo.y; st.h[2] = lo.z; st.h[3] = lo.w;
+    st.h[4] = hi.x; st.h[5] = hi.y; st.h[6] = hi.z; st.h[7] = hi.w;
+    const uint4* q = reinterpret_cast<const uint4*>(a.arena + a.offs[i]);
+    const uint64_t nb = a.nblocks[i];
+    for (uint64_t b = 0; b < nb; ++b, q += 4) {
+        const uint4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
+        uint32_t w[16] = {bswap32(r0.x), bswap32(r0.y), bswap32(r0.z), bswap32(r0.w),
+                          bswap32(r1.x), bswap32(r1.y), bswap32(r1.z), bswap32(r1.w),
+                          bswap32(r2.x), bswap32(r2.y), bswap32(r2.z), bswap32(r2.w),
+                          bswap32(r3.x), bswap32(r3.y), bswap32(r3.z), bswap32(r3.w)};
+        sha256_compress(st, w);
+    }
+    m4[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+    m4[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+}
+
+hipError_t launch_sha_resume(const ResumeArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k1_sha256_resume, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 // The host leg's digests into the plan's output rows: one 16-B half per lane.
 __global__ __launch_bounds__(256) void k_scatter_digests(uint8_t* __restrict__ out, const uint32_t* __restrict__ ids,
                                                          const uint8_t* __restrict__ digs, uint64_t n) {
