@@ -1,7 +1,8 @@
 """GPU parity: every kernel, called through the C-ABI, against the oracle.
 
 Bar: bit-exact (integer/byte work).  Sizes are chosen so the oracle finishes
-in seconds; full-size properties are covered in test_gpu_scale.py.
+in seconds; full-size properties are in test_gpu_scale.py (configs[2],
+configs[4]) and test_gpu_hybrid.py (configs[1] against its fixture).
 """
 import random
 
