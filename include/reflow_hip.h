@@ -306,6 +306,49 @@ typedef struct {
 } rf_graph_stats;
 int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
 
+/* ---- One DAG over many GPUs ---------------------------------
+ * Each rank loads its PIECE of the global job graph (rf_graph_load on a local
+ * desc: its own jobs plus replicated ones, slots renumbered locally) and
+ * attaches its place in the partition: EXPORTS (local slots other ranks
+ * read; export i of rank r has boundary id r * max_export + i, max_export the
+ * same on every rank) and IMPORTS (local input slots fed from another rank's
+ * boundary id).  rf_graph_recompute_part runs bulk-synchronous supersteps:
+ * local recompute; an OR all-reduce of the bitset of exports changed since
+ * they were last sent (RCCL has no bitwise OR: all-gather + local OR); an
+ * all-gather of the export digests; changed imports written and their local
+ * consumers queued; until no export changed (one exchange when no rank
+ * imports, e.g. 1000align split by sample with the shared reference-index
+ * chain replicated).  Transport: comm (RCCL over xGMI) or fn, a host
+ * all-gather (recv[r*bytes ..] = rank r's send; 0 = ok) for ranks without
+ * RCCL (tests on gloo, ranks sharing a GPU). */
+typedef struct {
+    int nranks, rank;
+    uint32_t max_export;
+    uint32_t n_export;
+    const uint32_t *export_slot;
+    uint32_t n_import;
+    const uint32_t *import_slot;
+    const uint32_t *import_bid;
+    int any_import; /* some rank imports something (the same on every rank) */
+} rf_graph_part;
+typedef int (*rf_host_allgather_fn)(void *user, const void *send, void *recv, uint64_t bytes);
+int rf_graph_set_part(rf_graph *g, const rf_graph_part *p);
+int rf_graph_recompute_part(rf_graph *g, rf_comm *comm, rf_host_allgather_fn fn, void *user, int full,
+                            uint64_t *out_recomputed);
+/* The last exchange's gathered export digests (device, [nranks*max_export][32],
+ * boundary-id order) and the supersteps the last recompute took. */
+int rf_graph_part_gathered(rf_graph *g, const void **d_digests32, uint64_t *n, uint64_t *supersteps);
+/* Host-only splitter: rank `rank`'s piece of a global desc, owner[j] = the
+ * rank that hashes job j (-1: every rank, e.g. the shared reference index).
+ * The piece's desc arrays are owned by the piece (its blob is the global
+ * blob, not copied); global_of_local maps its slots back. */
+typedef struct rf_graph_piece rf_graph_piece;
+int rf_graph_split(const rf_graph_desc *global, int nranks, int rank, const int32_t *owner, rf_graph_piece **out);
+void rf_graph_piece_free(rf_graph_piece *p);
+int rf_graph_piece_desc(const rf_graph_piece *p, rf_graph_desc *out);
+int rf_graph_piece_part(const rf_graph_piece *p, rf_graph_part *out);
+int rf_graph_piece_slots(const rf_graph_piece *p, const uint32_t **global_of_local, uint32_t *n);
+
 /* Eval.dirty (eval.go:874-887) for every node of a Flow graph at once:
  * dirty[i] = 1 iff no_cache_extern and node i is an OpExtern (is_extern[i])
  * or one of its Deps is dirty -- Deps only ("dirty considers only visible

@@ -46,6 +46,8 @@ EXPORTS = [
     "rf_set_host_threads", "rf_host_info", "rf_assoc_repair",
     "rf_sha_streams_open", "rf_sha_streams_close", "rf_sha_streams_write", "rf_sha_streams_digest",
     "rf_sha_streams_len", "rf_sha_streams_verify", "rf_sha256_verify", "rf_flow_dirty",
+    "rf_graph_set_part", "rf_graph_recompute_part", "rf_graph_part_gathered", "rf_graph_split",
+    "rf_graph_piece_free", "rf_graph_piece_desc", "rf_graph_piece_part", "rf_graph_piece_slots",
 ]
 
 
@@ -138,6 +140,83 @@ def fileset_marshal_json(fs) -> bytes:
     out = ctypes.create_string_buffer(max(need.value, 1))
     _check(lib().rf_fileset_marshal_json(ctypes.byref(t), root, out, need.value, ctypes.byref(need)))
     return out.raw[:need.value]
+
+
+class GraphPart(ctypes.Structure):
+    _fields_ = [("nranks", ctypes.c_int), ("rank", ctypes.c_int), ("max_export", ctypes.c_uint32),
+                ("n_export", ctypes.c_uint32), ("export_slot", ctypes.c_void_p),
+                ("n_import", ctypes.c_uint32), ("import_slot", ctypes.c_void_p),
+                ("import_bid", ctypes.c_void_p), ("any_import", ctypes.c_int)]
+
+
+# int (*)(void *user, const void *send, void *recv, uint64_t bytes)
+HOST_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+
+
+def host_allgather_fn(allgather, nranks):
+    """Wraps allgather(bytes) -> [bytes per rank] (e.g. torch.distributed
+    gloo) as the library's host all-gather callback."""
+    def fn(user, send, recv, nbytes):
+        try:
+            parts = allgather(ctypes.string_at(send, nbytes))
+            assert len(parts) == nranks and all(len(p) == nbytes for p in parts)
+            ctypes.memmove(recv, b"".join(parts), nranks * nbytes)
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the library as a failure
+            import traceback
+            traceback.print_exc()
+            return 1
+    return HOST_ALLGATHER(fn)
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    c = {np.uint32: ctypes.c_uint32, np.uint64: ctypes.c_uint64}[dtype]
+    return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(c)), shape=(n,)).copy()
+
+
+class GraphPiece:
+    """rf_graph_split (host only): rank `rank`'s piece of a global job graph
+    given as rf_graph_desc arrays (a dict like Dag1000.arrays()); owner[j] =
+    the rank hashing job j, -1 = every rank.  Attributes: desc (the piece's
+    arrays, templates in the global blob), part (exports / imports / boundary
+    ids), global_of_local."""
+
+    def __init__(self, arrays, nranks, rank, owner):
+        k = {n: np.ascontiguousarray(arrays[n], dtype=dt) for n, dt in
+             (("out_slot", np.uint32), ("tmpl_off", np.uint64), ("tmpl_len", np.uint32),
+              ("hole_ptr", np.uint64), ("hole_pos", np.uint32), ("hole_slot", np.uint32))}
+        blob = arrays["blob"]
+        self.blob = np.frombuffer(bytes(blob), np.uint8) if isinstance(blob, (bytes, bytearray)) \
+            else np.ascontiguousarray(blob, dtype=np.uint8)
+        own = np.ascontiguousarray(owner, dtype=np.int32)
+        d = GraphDesc(len(k["out_slot"]), int(arrays["n_slots"]), _ptr(k["out_slot"]), _ptr(k["tmpl_off"]),
+                      _ptr(k["tmpl_len"]), _ptr(k["hole_ptr"]), _ptr(k["hole_pos"]) if len(k["hole_pos"]) else None,
+                      _ptr(k["hole_slot"]) if len(k["hole_slot"]) else None, _ptr(self.blob), len(self.blob))
+        h = ctypes.c_void_p()
+        _check(lib().rf_graph_split(ctypes.byref(d), nranks, rank, _ptr(own), ctypes.byref(h)))
+        try:
+            ld = GraphDesc()
+            _check(lib().rf_graph_piece_desc(h, ctypes.byref(ld)))
+            J = ld.n_jobs
+            hp = _arr(ld.hole_ptr, J + 1, np.uint64)
+            H = int(hp[-1]) if J else 0
+            self.desc = dict(n_slots=ld.n_slots, out_slot=_arr(ld.out_slot, J, np.uint32),
+                             tmpl_off=_arr(ld.tmpl_off, J, np.uint64), tmpl_len=_arr(ld.tmpl_len, J, np.uint32),
+                             hole_ptr=hp, hole_pos=_arr(ld.hole_pos, H, np.uint32),
+                             hole_slot=_arr(ld.hole_slot, H, np.uint32), blob=self.blob)
+            pt = GraphPart()
+            _check(lib().rf_graph_piece_part(h, ctypes.byref(pt)))
+            self.part = dict(nranks=pt.nranks, rank=pt.rank, max_export=pt.max_export,
+                             export_slot=_arr(pt.export_slot, pt.n_export, np.uint32),
+                             import_slot=_arr(pt.import_slot, pt.n_import, np.uint32),
+                             import_bid=_arr(pt.import_bid, pt.n_import, np.uint32), any_import=bool(pt.any_import))
+            gp, gn = ctypes.c_void_p(), ctypes.c_uint32()
+            _check(lib().rf_graph_piece_slots(h, ctypes.byref(gp), ctypes.byref(gn)))
+            self.global_of_local = _arr(gp, gn.value, np.uint32)
+        finally:
+            lib().rf_graph_piece_free(h)
 
 
 class GraphStats(ctypes.Structure):
@@ -255,6 +334,12 @@ def lib():
             "rf_sha_streams_verify": ([vp, vp, vp, u64, vp], i32),
             "rf_sha256_verify": ([vp, vp, vp, u64, vp, vp], i32),
             "rf_flow_dirty": ([vp, u64, vp, vp, vp, i32, vp], i32),
+            "rf_graph_set_part": ([vp, vp], i32),
+            "rf_graph_recompute_part": ([vp, vp, vp, vp, i32, vp], i32),
+            "rf_graph_part_gathered": ([vp, vp, vp, vp], i32),
+            "rf_graph_split": ([vp, i32, i32, vp, vp], i32), "rf_graph_piece_free": ([vp], None),
+            "rf_graph_piece_desc": ([vp, vp], i32), "rf_graph_piece_part": ([vp, vp], i32),
+            "rf_graph_piece_slots": ([vp, vp, vp], i32),
             "rf_host_info": ([vp, vp, vp, vp], i32),
         }
         for name, (args, res) in sigs.items():
@@ -683,6 +768,39 @@ class Graph:
         s = GraphStats()
         _check(lib().rf_graph_stats_get(self._h, ctypes.byref(s)))
         return s
+
+    @classmethod
+    def from_arrays(cls, ctx, a):
+        return cls(ctx, a["n_slots"], a["out_slot"], a["tmpl_off"], a["tmpl_len"], a["hole_ptr"], a["hole_pos"],
+                   a["hole_slot"], a["blob"])
+
+    def set_part(self, part):
+        """part: dict(nranks, rank, max_export, export_slot, import_slot,
+        import_bid, any_import) (GraphPiece.part)."""
+        ex = np.ascontiguousarray(part["export_slot"], dtype=np.uint32)
+        im = np.ascontiguousarray(part["import_slot"], dtype=np.uint32)
+        ib = np.ascontiguousarray(part["import_bid"], dtype=np.uint32)
+        p = GraphPart(part["nranks"], part["rank"], part["max_export"], len(ex), _ptr(ex) if len(ex) else None,
+                      len(im), _ptr(im) if len(im) else None, _ptr(ib) if len(ib) else None,
+                      1 if part.get("any_import", True) else 0)
+        _check(lib().rf_graph_set_part(self._h, ctypes.byref(p)))
+
+    def recompute_part(self, comm=None, allgather=None, nranks=1, full=False) -> int:
+        """Superstep recompute across ranks: comm (Comm, RCCL) or allgather
+        (bytes -> [bytes per rank], a host transport)."""
+        fn = host_allgather_fn(allgather, nranks) if allgather is not None else None
+        self._fn = fn  # alive during the call
+        n = ctypes.c_uint64(0)
+        _check(lib().rf_graph_recompute_part(self._h, comm._h if comm is not None else None,
+                                             ctypes.cast(fn, ctypes.c_void_p) if fn is not None else None, None,
+                                             1 if full else 0, ctypes.byref(n)))
+        return n.value
+
+    def part_gathered(self):
+        """(device pointer of the gathered export digests, count, supersteps)."""
+        p, n, st = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().rf_graph_part_gathered(self._h, ctypes.byref(p), ctypes.byref(n), ctypes.byref(st)))
+        return p.value, n.value, st.value
 
     def close(self):
         if self._h:

@@ -33,6 +33,7 @@
 #include "engine.h"
 #include "host_leg.h"
 #include "ctx.h"
+#include "graph_internal.h"
 #include "host_sha.h"
 #include "reflow_hip.h"
 
@@ -1366,22 +1367,6 @@ extern "C" int rf_fileset_value_digest_batch(rf_ctx* ctx, const rf_fileset_tree*
 
 // ---------------------------------------------------------------------------
 // Digest DAG
-struct rf_graph {
-    rf_ctx* ctx = nullptr;
-    GraphDev g;
-    std::vector<int64_t> producer;   // slot -> external job or -1
-    std::vector<uint32_t> ext2int;   // external job id -> internal
-    bool initialized = false;
-    DevBuf b_stamps;
-    DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_counts,
-        b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
-    uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
-    uint32_t max_level_jobs = 0;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    hipGraphExec_t exec_inc = nullptr, exec_full = nullptr;
-    bool timed = false;
-};
-
 extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out) {
     ARG(ctx && d && out, "null argument");
     *out = nullptr;
@@ -1610,6 +1595,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         if (gr->e1) (void)hipEventDestroy(gr->e1);
         if (gr->exec_inc) (void)hipGraphExecDestroy(gr->exec_inc);
         if (gr->exec_full) (void)hipGraphExecDestroy(gr->exec_full);
+        graph_part_release(gr);
     }
     delete gr;
 }
@@ -1683,7 +1669,7 @@ static int graph_capture(rf_graph* gr, int full, hipGraphExec_t* out) {
     return RF_OK;
 }
 
-static int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
+int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
     if (!gr->initialized) full = 1;
     hipGraphExec_t& ex = full ? gr->exec_full : gr->exec_inc;
     if (!ex && gr->g.n_levels)

@@ -92,6 +92,13 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipSt
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);
+// Partitioned DAG exchange: pack changed exports (bits at bit0 + i), test the
+// reduced bitset, apply changed imports (queues their local consumers).
+hipError_t launch_part_pack(const uint32_t* export_slot, uint32_t n, const uint8_t* slots, uint8_t* snap,
+                            uint8_t* send, uint32_t* bits, uint32_t bit0, hipStream_t s);
+hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, uint32_t* flag, hipStream_t s);
+hipError_t launch_part_apply(const GraphDev& g, const uint32_t* import_slot, const uint32_t* import_bid, uint32_t n,
+                             const uint32_t* bits, const uint8_t* gather, hipStream_t s);
 
 // K3 reachability (Eval.dirty): one frontier level; bits = marked set,
 // next/n_next = the newly marked nodes (n_next zeroed by the caller).

@@ -1,0 +1,45 @@
+// graph_internal.h -- internal: the object behind rf_graph* (digest DAG on
+// one device), shared by capi.cpp (load, recompute) and partition.cpp
+// (multi-GPU pieces).  Not part of the public ABI.
+#pragma once
+#include <vector>
+
+#include "ctx.h"
+#include "engine.h"
+
+// A loaded piece's place in a partitioned DAG (partition.cpp).
+struct GraphPart {
+    int nranks = 1, rank = 0;
+    uint32_t max_export = 0, n_export = 0, n_import = 0;
+    bool any_import = true;   // some rank imports (else one exchange ends a step)
+    uint64_t nwords = 0;      // u64 words of the boundary bitset (nranks * max_export bits)
+    DevBuf d_export_slot, d_import_slot, d_import_bid;
+    DevBuf d_snap;            // [n_export][32] export digests as last sent
+    DevBuf d_send;            // [max_export][32]
+    DevBuf d_gather;          // [nranks][max_export][32]
+    DevBuf d_bits, d_bits_g;  // boundary bitset; gathered copies (host transport OR)
+    DevBuf d_flag;
+    HostBuf h_buf;            // host transport staging
+    uint64_t last_supersteps = 0;
+};
+
+struct rf_graph {
+    rf_ctx* ctx = nullptr;
+    rf::GraphDev g;
+    std::vector<int64_t> producer;   // slot -> external job or -1
+    std::vector<uint32_t> ext2int;   // external job id -> internal
+    bool initialized = false;
+    DevBuf b_stamps;
+    DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_counts,
+        b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
+    uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
+    uint32_t max_level_jobs = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipGraphExec_t exec_inc = nullptr, exec_full = nullptr;
+    bool timed = false;
+    GraphPart* part = nullptr;  // multi-GPU partition (rf_graph_set_part), else null
+};
+
+
+int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s);
+void graph_part_release(rf_graph* gr);

@@ -583,6 +583,71 @@ __global__ __launch_bounds__(256) void k3_mark_slots(const uint32_t* __restrict_
     }
 }
 
+// ---- partitioned DAG exchange (partition.cpp) --------------------------------
+// Exports whose digest changed since last sent: their bit (bit0 + i) in the
+// boundary bitset, the snapshot updated, the digest into the send block.
+__global__ __launch_bounds__(256) void k_part_pack(const uint32_t* __restrict__ export_slot, uint32_t n,
+                                                   const uint8_t* __restrict__ slots, uint8_t* snap, uint8_t* send,
+                                                   uint32_t* bits, uint32_t bit0) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4* src = reinterpret_cast<const uint4*>(slots + 32ull * export_slot[i]);
+    uint4* sn = reinterpret_cast<uint4*>(snap + 32ull * i);
+    const uint4 lo = src[0], hi = src[1], olo = sn[0], ohi = sn[1];
+    const bool changed = (olo.x != lo.x) | (olo.y != lo.y) | (olo.z != lo.z) | (olo.w != lo.w) |
+                         (ohi.x != hi.x) | (ohi.y != hi.y) | (ohi.z != hi.z) | (ohi.w != hi.w);
+    if (changed) {
+        const uint32_t b = bit0 + i;
+        atomicOr(&bits[b >> 5], 1u << (b & 31));
+        sn[0] = lo;
+        sn[1] = hi;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(send + 32ull * i);
+    dst[0] = lo;
+    dst[1] = hi;
+}
+
+// flag = any bit set in the (OR-reduced) bitset.
+__global__ __launch_bounds__(256) void k_part_any(const uint64_t* __restrict__ bits, uint64_t nwords, uint32_t* flag) {
+    uint64_t v = 0;
+    for (uint64_t i = threadIdx.x; i < nwords; i += blockDim.x) v |= bits[i];
+    const int any = __syncthreads_or(v != 0);
+    if (threadIdx.x == 0) flag[0] = any ? 1u : 0u;
+}
+
+// Imports whose boundary bit is set: the gathered digest into the slot; a
+// changed slot queues its local consumers (as k3_mark_slots).
+__global__ __launch_bounds__(256) void k_part_apply(const uint32_t* __restrict__ import_slot,
+                                                    const uint32_t* __restrict__ import_bid, uint32_t n,
+                                                    const uint32_t* __restrict__ bits,
+                                                    const uint8_t* __restrict__ gather, uint8_t* slots,
+                                                    const uint32_t* __restrict__ cons_ptr,
+                                                    const uint2* __restrict__ cons, uint32_t* dirty, uint32_t* list,
+                                                    uint32_t* counts, const uint32_t* __restrict__ ls) {
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t c = 0, ce = 0;
+        if (i < n) {
+            const uint32_t b = import_bid[i];
+            if ((bits[b >> 5] >> (b & 31)) & 1u) {
+                const uint32_t s = import_slot[i];
+                const uint4* src = reinterpret_cast<const uint4*>(gather + 32ull * b);
+                uint4* dst = reinterpret_cast<uint4*>(slots + 32ull * s);
+                const uint4 nlo = src[0], nhi = src[1], olo = dst[0], ohi = dst[1];
+                const bool changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                                     (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
+                if (changed) {
+                    dst[0] = nlo;
+                    dst[1] = nhi;
+                    c = cons_ptr[s];
+                    ce = cons_ptr[s + 1];
+                }
+            }
+        }
+        propagate(cons, dirty, list, counts, ls, c, ce);
+    }
+}
+
 // End of a recompute: record what each level hashed, reset the lists.
 __global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __restrict__ ls, uint32_t L,
                             int full) {
@@ -654,6 +719,27 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
     hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_pack(const uint32_t* export_slot, uint32_t n, const uint8_t* slots, uint8_t* snap,
+                            uint8_t* send, uint32_t* bits, uint32_t bit0, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_part_pack, dim3((n + 255) / 256), dim3(256), 0, s, export_slot, n, slots, snap, send, bits,
+                       bit0);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, uint32_t* flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_part_any, dim3(1), dim3(256), 0, s, bits, nwords, flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_apply(const GraphDev& g, const uint32_t* import_slot, const uint32_t* import_bid, uint32_t n,
+                             const uint32_t* bits, const uint8_t* gather, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_part_apply, dim3(grid_for(n, 4096)), dim3(256), 0, s, import_slot, import_bid, n, bits,
+                       gather, g.slots, g.cons_ptr, g.cons, g.dirty, g.list, g.counts, g.lvl_start_dev);
     return hipGetLastError();
 }
 

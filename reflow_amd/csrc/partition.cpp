@@ -1,0 +1,333 @@
+// partition.cpp -- one digest DAG over many GPUs: the host
+// splitter (rf_graph_split: a rank's piece of a global job graph), the
+// partition attached to a loaded piece (rf_graph_set_part) and the
+// superstep recompute across ranks (rf_graph_recompute_part).
+//
+// Protocol (bulk-synchronous supersteps, no global level agreement needed):
+//   1. every rank recomputes its piece (K3 frontier + K2 levels);
+//   2. each rank sets, in a bitset over all ranks' export slots (boundary id
+//      = owner rank * max_export + export index), the bits of its exports
+//      whose digest changed since they were last sent; the bitsets are
+//      OR-reduced over the ranks (RCCL has no bitwise OR: all-gather + a
+//      local OR kernel, rf_comm_allreduce_or);
+//   3. no bit set anywhere: done.  Else every rank all-gathers the export
+//      digests, writes each changed import into its slot and queues the
+//      slot's local consumers (k3_mark_slots' compare-and-queue), and the
+//      next superstep recomputes them.
+// The global graph is a DAG, so this reaches the same digests as a
+// single-rank recompute; a partition by 1000align sample (the shared
+// reference-index chain replicated) has no imports and ends after one
+// exchange.  Transport: an rf_comm (RCCL over xGMI, device buffers) or a host
+// all-gather callback (gloo in tests / ranks sharing a GPU).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <vector>
+
+#include "ctx.h"
+#include "engine.h"
+#include "graph_internal.h"
+
+using namespace rf;
+
+// ---------------------------------------------------------------------------
+// host splitter
+struct rf_graph_piece {
+    std::vector<uint32_t> out_slot, tmpl_len, hole_pos, hole_slot;
+    std::vector<uint64_t> tmpl_off, hole_ptr;
+    const uint8_t* blob = nullptr;
+    uint64_t blob_len = 0;
+    std::vector<uint32_t> global_of_local;  // local slot -> global slot
+    std::vector<uint32_t> export_slot, import_slot, import_bid;
+    uint32_t max_export = 0;
+    int nranks = 1, rank = 0;
+    bool any_import = false;
+};
+
+extern "C" int rf_graph_split(const rf_graph_desc* d, int nranks, int rank, const int32_t* owner,
+                              rf_graph_piece** out) {
+    ARG(d && owner && out, "null argument");
+    ARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank");
+    *out = nullptr;
+    const uint32_t J = d->n_jobs, S = d->n_slots;
+    ARG(J == 0 || (d->out_slot && d->tmpl_off && d->tmpl_len && d->hole_ptr), "null job arrays");
+    const uint64_t H = J ? d->hole_ptr[J] : 0;
+    ARG(H == 0 || (d->hole_pos && d->hole_slot), "null hole arrays");
+    std::vector<int64_t> producer(S, -1);
+    for (uint32_t j = 0; j < J; ++j) {
+        ARG(owner[j] >= -1 && owner[j] < nranks, "owner out of range (-1 = every rank)");
+        if (d->out_slot[j] >= S) return fail(RF_EINVAL, "job %u: out_slot out of range", j);
+        if (producer[d->out_slot[j]] >= 0) return fail(RF_EINVAL, "slot %u written twice", d->out_slot[j]);
+        producer[d->out_slot[j]] = j;
+        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h)
+            if (d->hole_slot[h] >= S) return fail(RF_EINVAL, "job %u: hole slot out of range", j);
+    }
+    // exports of every rank (deterministic order: by slot), so boundary ids agree
+    std::vector<std::vector<uint32_t>> exports(nranks);
+    {
+        std::vector<uint8_t> is_export(S, 0);
+        for (uint32_t k = 0; k < J; ++k)
+            for (uint64_t h = d->hole_ptr[k]; h < d->hole_ptr[k + 1]; ++h) {
+                const int64_t p = producer[d->hole_slot[h]];
+                if (p < 0 || owner[p] < 0) continue;  // input, or replicated: no exchange
+                // read on a rank that does not hash it: every rank if k is replicated
+                if (owner[k] != owner[p]) is_export[d->hole_slot[h]] = 1;
+            }
+        for (uint32_t s = 0; s < S; ++s)
+            if (is_export[s]) exports[owner[producer[s]]].push_back(s);
+    }
+    auto* pc = new rf_graph_piece();
+    std::unique_ptr<rf_graph_piece> guard(pc);
+    pc->nranks = nranks;
+    pc->rank = rank;
+    for (const auto& e : exports) pc->max_export = std::max<uint32_t>(pc->max_export, (uint32_t)e.size());
+    std::vector<uint32_t> bid_of(S, ~0u);
+    for (int r = 0; r < nranks; ++r)
+        for (uint32_t i = 0; i < exports[r].size(); ++i) bid_of[exports[r][i]] = (uint32_t)r * pc->max_export + i;
+    // local jobs (global order) and the slots they touch, renumbered densely
+    std::vector<uint32_t> local_of(S, ~0u);
+    std::vector<uint8_t> used(S, 0);
+    std::vector<uint32_t> jobs;
+    for (uint32_t j = 0; j < J; ++j)
+        if (owner[j] == -1 || owner[j] == rank) {
+            jobs.push_back(j);
+            used[d->out_slot[j]] = 1;
+            for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) used[d->hole_slot[h]] = 1;
+        }
+    for (uint32_t s = 0; s < S; ++s)
+        if (used[s]) {
+            local_of[s] = (uint32_t)pc->global_of_local.size();
+            pc->global_of_local.push_back(s);
+        }
+    pc->hole_ptr.push_back(0);
+    for (uint32_t j : jobs) {
+        pc->out_slot.push_back(local_of[d->out_slot[j]]);
+        pc->tmpl_off.push_back(d->tmpl_off[j]);
+        pc->tmpl_len.push_back(d->tmpl_len[j]);
+        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) {
+            pc->hole_pos.push_back(d->hole_pos[h]);
+            pc->hole_slot.push_back(local_of[d->hole_slot[h]]);
+        }
+        pc->hole_ptr.push_back(pc->hole_pos.size());
+    }
+    pc->blob = d->blob;
+    pc->blob_len = d->blob_len;
+    for (uint32_t s : exports[rank]) pc->export_slot.push_back(local_of[s]);
+    pc->any_import = false;
+    for (uint32_t k = 0; k < J && !pc->any_import; ++k)  // does any rank import anything?
+        for (uint64_t h = d->hole_ptr[k]; h < d->hole_ptr[k + 1]; ++h) {
+            const int64_t p = producer[d->hole_slot[h]];
+            if (p >= 0 && owner[p] >= 0 && owner[k] != owner[p]) {
+                pc->any_import = true;
+                break;
+            }
+        }
+    // imports: slots this piece reads that another rank's job produces
+    for (uint32_t ls = 0; ls < pc->global_of_local.size(); ++ls) {
+        const uint32_t s = pc->global_of_local[ls];
+        const int64_t p = producer[s];
+        if (p >= 0 && owner[p] >= 0 && owner[p] != rank) {
+            pc->import_slot.push_back(ls);
+            pc->import_bid.push_back(bid_of[s]);
+        }
+    }
+    *out = guard.release();
+    return RF_OK;
+}
+
+extern "C" void rf_graph_piece_free(rf_graph_piece* pc) { delete pc; }
+
+extern "C" int rf_graph_piece_desc(const rf_graph_piece* pc, rf_graph_desc* o) {
+    ARG(pc && o, "null argument");
+    o->n_jobs = (uint32_t)pc->out_slot.size();
+    o->n_slots = (uint32_t)pc->global_of_local.size();
+    o->out_slot = pc->out_slot.data();
+    o->tmpl_off = pc->tmpl_off.data();
+    o->tmpl_len = pc->tmpl_len.data();
+    o->hole_ptr = pc->hole_ptr.data();
+    o->hole_pos = pc->hole_pos.data();
+    o->hole_slot = pc->hole_slot.data();
+    o->blob = pc->blob;
+    o->blob_len = pc->blob_len;
+    return RF_OK;
+}
+
+extern "C" int rf_graph_piece_part(const rf_graph_piece* pc, rf_graph_part* o) {
+    ARG(pc && o, "null argument");
+    o->nranks = pc->nranks;
+    o->rank = pc->rank;
+    o->max_export = pc->max_export;
+    o->n_export = (uint32_t)pc->export_slot.size();
+    o->export_slot = pc->export_slot.data();
+    o->n_import = (uint32_t)pc->import_slot.size();
+    o->import_slot = pc->import_slot.data();
+    o->import_bid = pc->import_bid.data();
+    o->any_import = pc->any_import ? 1 : 0;
+    return RF_OK;
+}
+
+extern "C" int rf_graph_piece_slots(const rf_graph_piece* pc, const uint32_t** global_of_local, uint32_t* n) {
+    ARG(pc && global_of_local && n, "null argument");
+    *global_of_local = pc->global_of_local.data();
+    *n = (uint32_t)pc->global_of_local.size();
+    return RF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// a loaded piece's partition and the superstep recompute
+void graph_part_release(rf_graph* gr) {
+    GraphPart* P = gr->part;
+    if (!P) return;
+    for (DevBuf* b : {&P->d_export_slot, &P->d_import_slot, &P->d_import_bid, &P->d_snap, &P->d_send, &P->d_gather,
+                      &P->d_bits, &P->d_bits_g, &P->d_flag})
+        b->release();
+    P->h_buf.release();
+    delete P;
+    gr->part = nullptr;
+}
+
+extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
+    ARG(gr && p, "null argument");
+    ARG(p->nranks >= 1 && p->rank >= 0 && p->rank < p->nranks, "bad rank");
+    ARG(p->n_export <= p->max_export, "n_export > max_export");
+    ARG(p->n_export == 0 || p->export_slot, "null export_slot");
+    ARG(p->n_import == 0 || (p->import_slot && p->import_bid), "null import arrays");
+    ARG((uint64_t)p->nranks * p->max_export < (1ull << 32), "boundary too large");
+    for (uint32_t i = 0; i < p->n_export; ++i) {
+        if (p->export_slot[i] >= gr->g.n_slots) return fail(RF_EINVAL, "export slot %u out of range", p->export_slot[i]);
+        if (gr->producer[p->export_slot[i]] < 0)
+            return fail(RF_EINVAL, "export slot %u is not produced by this piece", p->export_slot[i]);
+    }
+    for (uint32_t i = 0; i < p->n_import; ++i) {
+        if (p->import_slot[i] >= gr->g.n_slots) return fail(RF_EINVAL, "import slot %u out of range", p->import_slot[i]);
+        if (gr->producer[p->import_slot[i]] >= 0)
+            return fail(RF_EINVAL, "import slot %u is produced by this piece", p->import_slot[i]);
+        if (p->import_bid[i] >= (uint64_t)p->nranks * p->max_export || p->import_bid[i] / p->max_export == (uint32_t)p->rank)
+            return fail(RF_EINVAL, "import %u: boundary id %u is not another rank's export", i, p->import_bid[i]);
+    }
+    rf_ctx* ctx = gr->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    graph_part_release(gr);
+    auto* P = new GraphPart();
+    gr->part = P;
+    P->nranks = p->nranks;
+    P->rank = p->rank;
+    P->max_export = p->max_export;
+    P->n_export = p->n_export;
+    P->n_import = p->n_import;
+    P->any_import = p->any_import != 0;
+    P->nwords = ((uint64_t)p->nranks * p->max_export + 63) / 64;
+    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
+        hipError_t e = b.ensure(std::max<size_t>(bytes, 64));
+        return e != hipSuccess || !bytes ? e : hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
+    };
+    const uint64_t blk = 32ull * std::max<uint32_t>(p->max_export, 1);
+    hipError_t e;
+    if ((e = up(P->d_export_slot, p->export_slot, 4ull * p->n_export)) != hipSuccess ||
+        (e = up(P->d_import_slot, p->import_slot, 4ull * p->n_import)) != hipSuccess ||
+        (e = up(P->d_import_bid, p->import_bid, 4ull * p->n_import)) != hipSuccess ||
+        (e = P->d_snap.ensure(32ull * std::max<uint32_t>(p->n_export, 1))) != hipSuccess ||
+        (e = P->d_send.ensure(blk)) != hipSuccess || (e = P->d_gather.ensure(blk * p->nranks)) != hipSuccess ||
+        (e = P->d_bits.ensure(8 * std::max<uint64_t>(P->nwords, 1))) != hipSuccess ||
+        (e = P->d_bits_g.ensure(8 * std::max<uint64_t>(P->nwords, 1) * p->nranks)) != hipSuccess ||
+        (e = P->d_flag.ensure(64)) != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "partition alloc: %s", hipGetErrorString(e));
+    // nothing sent yet: every export counts as changed at the first exchange
+    HIPC(hipMemset(P->d_snap.p, 0, 32ull * std::max<uint32_t>(p->n_export, 1)));
+    return RF_OK;
+}
+
+// OR of the ranks' boundary bitsets, in place in d_bits.
+static int part_or(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn, void* user, hipStream_t s) {
+    GraphPart* P = gr->part;
+    const uint64_t nb = 8 * P->nwords;
+    if (P->nranks == 1 || !nb) return RF_OK;
+    if (comm) return rf_comm_allreduce_or(comm, P->d_bits.p, P->nwords, s);
+    HIPC(P->h_buf.ensure(nb * (P->nranks + 1)));
+    uint64_t* h = reinterpret_cast<uint64_t*>(P->h_buf.bytes());
+    HIPC(hipMemcpyAsync(h, P->d_bits.p, nb, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (fn(user, h, h + P->nwords, nb)) return fail(RF_EDEVICE, "host all-gather (boundary bitset) failed");
+    for (int r = 0; r < P->nranks; ++r)
+        for (uint64_t w = 0; w < P->nwords; ++w) h[w] |= h[P->nwords * (r + 1) + w];
+    HIPC(hipMemcpyAsync(P->d_bits.p, h, nb, hipMemcpyHostToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+    return RF_OK;
+}
+
+// All-gather of the export blocks ([max_export][32] per rank) into d_gather.
+static int part_gather(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn, void* user, hipStream_t s) {
+    GraphPart* P = gr->part;
+    const uint64_t blk = 32ull * P->max_export;
+    if (!blk) return RF_OK;
+    if (P->nranks == 1) {
+        HIPC(hipMemcpyAsync(P->d_gather.p, P->d_send.p, blk, hipMemcpyDeviceToDevice, s));
+        return RF_OK;
+    }
+    if (comm) return rf_comm_allgather(comm, P->d_send.p, P->d_gather.p, blk, s);
+    HIPC(P->h_buf.ensure(blk * (P->nranks + 1)));
+    uint8_t* h = P->h_buf.bytes();
+    HIPC(hipMemcpyAsync(h, P->d_send.p, blk, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (fn(user, h, h + blk, blk)) return fail(RF_EDEVICE, "host all-gather (boundary digests) failed");
+    HIPC(hipMemcpyAsync(P->d_gather.p, h + blk, blk * P->nranks, hipMemcpyHostToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+    return RF_OK;
+}
+
+static int part_counts(rf_graph* gr, hipStream_t s, uint64_t* tot) {
+    std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
+    if (gr->g.n_levels)
+        HIPC(hipMemcpyAsync(counts.data(), gr->g.counts_last, 4ull * (gr->g.n_levels + 1), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    for (uint32_t c : counts) *tot += c;
+    return RF_OK;
+}
+
+extern "C" int rf_graph_recompute_part(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn, void* user, int full,
+                                       uint64_t* out_recomputed) {
+    ARG(gr && gr->part, "graph has no partition (rf_graph_set_part)");
+    GraphPart* P = gr->part;
+    ARG(P->nranks == 1 || comm || fn, "several ranks need an rf_comm or a host all-gather");
+    rf_ctx* ctx = gr->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    hipStream_t s = ctx->stream;
+    uint64_t tot = 0, steps = 0;
+    for (;;) {
+        if (int rc = graph_recompute_locked(gr, steps == 0 ? full : 0, s)) return rc;
+        ++steps;
+        if (out_recomputed)
+            if (int rc = part_counts(gr, s, &tot)) return rc;
+        if (!P->nwords) break;  // no rank exports anything: the pieces are independent
+        HIPC(hipMemsetAsync(P->d_bits.p, 0, 8 * P->nwords, s));
+        HIPC(launch_part_pack(P->d_export_slot.as<uint32_t>(), P->n_export, gr->g.slots, P->d_snap.as<uint8_t>(),
+                              P->d_send.as<uint8_t>(), P->d_bits.as<uint32_t>(), (uint32_t)P->rank * P->max_export, s));
+        if (int rc = part_or(gr, comm, fn, user, s)) return rc;
+        if (P->any_import) {  // a changed import may change exports again: one more superstep
+            uint32_t flag = 0;
+            HIPC(launch_part_any(P->d_bits.as<uint64_t>(), P->nwords, P->d_flag.as<uint32_t>(), s));
+            HIPC(hipMemcpyAsync(&flag, P->d_flag.p, 4, hipMemcpyDeviceToHost, s));
+            HIPC(hipStreamSynchronize(s));
+            if (!flag) break;
+        }
+        if (int rc = part_gather(gr, comm, fn, user, s)) return rc;
+        if (!P->any_import) break;  // exports observed, nobody consumes them
+        HIPC(launch_part_apply(gr->g, P->d_import_slot.as<uint32_t>(), P->d_import_bid.as<uint32_t>(), P->n_import,
+                               P->d_bits.as<uint32_t>(), P->d_gather.as<uint8_t>(), s));
+    }
+    P->last_supersteps = steps;
+    if (out_recomputed) *out_recomputed = tot;
+    return RF_OK;
+}
+
+extern "C" int rf_graph_part_gathered(rf_graph* gr, const void** d_digests32, uint64_t* n, uint64_t* supersteps) {
+    ARG(gr && gr->part, "graph has no partition");
+    if (d_digests32) *d_digests32 = gr->part->d_gather.p;
+    if (n) *n = (uint64_t)gr->part->nranks * gr->part->max_export;
+    if (supersteps) *supersteps = gr->part->last_supersteps;
+    return RF_OK;
+}

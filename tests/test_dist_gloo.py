@@ -1,9 +1,13 @@
-"""Multi-rank host logic of bench.py on the CPU (gloo, world_size 2).
+"""Multi-rank host logic on the CPU (gloo, world_size 2).
 
 The GPU data path (RCCL inside libreflow_hip.so) cannot run here; these tests
 cover what every rank does around it: rendezvous on 127.0.0.1, barrier,
-max-over-ranks timing, the RCCL unique-id broadcast, and that ranks get
-disjoint weak-scaling shards (distinct seeds -> distinct files / DAGs)."""
+max-over-ranks timing, the RCCL unique-id broadcast, the LPT sharding of the
+global Fileset, and -- the partitioned DAG -- the product's splitter
+(rf_graph_split, host code in libreflow_hip.so) with the superstep exchange
+protocol of rf_graph_recompute_part (boundary-bitset OR all-reduce +
+all-gather of boundary digests over gloo), each rank's local recompute done by
+the oracle, checked slot for slot against a single-rank recompute."""
 import os
 import socket
 
@@ -32,10 +36,13 @@ def _worker(rank, world, port, q):
     sm = d.sum(10.0 * (rank + 1))
     uid = d.bcast_bytes(b"U" * 128 if rank == 0 else None)
     ag = d.all_gather_bytes(np.full(3, 7 + rank, dtype=np.uint8)).tolist()  # root-digest exchange without RCCL
-    seed = 0x5EED0004 + rank
-    lens = c2_sizes(total_bytes=1 << 30, seed=seed)
+    class A:
+        sha_gib = 1.0
+    lens, _, glob = bench.rank_sizes(A, d)  # LPT shard of the global Fileset
+    allsz = np.concatenate([c2_sizes(total_bytes=1 << 30, seed=0x5EED0004 + g) for g in range(world)])
     dag = Dag1000(3, 4, seed=0x5EED0003 + 1000003 * rank)
-    q.put((rank, mx, sm, uid, int(lens.sum()), lens[:8].tolist(), dag.leaf_ids[:2].tobytes(), ag))
+    q.put((rank, mx, sm, uid, int(lens.sum()), sorted(lens.tolist()), dag.leaf_ids[:2].tobytes(), ag,
+           glob["files"], int(allsz.sum()), sorted(allsz.tolist())))
     d.dist.destroy_process_group()
 
 
@@ -51,20 +58,84 @@ def test_gloo_world2_bench_dist():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, mx0, sm0, uid0, b0, l0, ids0, ag0), (r1, mx1, sm1, uid1, b1, l1, ids1, ag1) = res
+    (r0, mx0, sm0, uid0, b0, l0, ids0, ag0, n0, tot0, all0), (r1, mx1, sm1, uid1, b1, l1, ids1, ag1, n1, tot1, _) = res
     assert ag0 == ag1 == [7, 7, 7, 8, 8, 8]  # rank order
     assert mx0 == mx1 == 2.0  # max over ranks
     assert sm0 == sm1 == 30.0  # whole-job aggregate
     assert uid0 == uid1 == b"U" * 128  # RCCL id reaches every rank
-    assert b0 == b1 == 1 << 30  # equal per-rank work (weak scaling)
-    assert l0 != l1 and ids0 != ids1  # disjoint shards
+    # the LPT shards partition the global Fileset and balance its bytes
+    assert sorted(l0 + l1) == all0 and b0 + b1 == tot0 and n0 == n1 == len(all0)
+    assert abs(b0 - b1) <= max(l0 + l1)
+    assert ids0 != ids1  # per-rank DAG seeds differ
 
 
-def test_or_allreduce_semantics():
-    """rf_comm_allreduce_or = all-gather + OR (RCCL has no bitwise OR); the
-    CPU restatement over 4 simulated ranks."""
-    rng = np.random.default_rng(0)
-    ranks = [rng.integers(0, 2**63, size=17, dtype=np.uint64) for _ in range(4)]
-    gathered = np.stack(ranks)
-    want = ranks[0] | ranks[1] | ranks[2] | ranks[3]
-    assert (np.bitwise_or.reduce(gathered, axis=0) == want).all()
+def _part_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as dist
+
+    import partition_case as PC
+    from reflow_amd import capi
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(b):
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        return [o.numpy().tobytes() for o in out]
+
+    dag, arrays, owner, root_slot, tail_slot = PC.global_case(S=6, P=4, nranks=world)
+    piece = capi.GraphPiece(arrays, world, rank, owner)
+    ids = dag.leaf_ids.copy()
+    state, steps1 = PC.superstep_oracle(piece, dag, ids, allgather)
+    first = state["og"].slots[:len(piece.global_of_local)].copy()
+    # change 1/3 of the leaf files, including ones of every sample
+    rng = np.random.default_rng(3)
+    pick = np.sort(rng.choice(len(dag.file_slots), size=len(dag.file_slots) // 3, replace=False))
+    new = ids.copy()
+    new[pick] = rng.integers(0, 256, size=(len(pick), 32), dtype=np.uint8)
+    state, steps2 = PC.superstep_oracle(piece, dag, new, allgather, changed=(dag.file_slots[pick], new[pick]),
+                                        state=state)
+    second = state["og"].slots[:len(piece.global_of_local)].copy()
+    q.put((rank, piece.global_of_local.tolist(), first.tobytes(), second.tobytes(), steps1, steps2,
+           len(piece.part["import_slot"]), len(piece.part["export_slot"]), piece.part["any_import"]))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_partitioned_dag():
+    """One DAG over 2 ranks: every rank's local slots equal the single-rank
+    recompute, before and after an incremental change, and the change crosses
+    ranks twice (global root on rank 0, its consumer on rank 1)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import partition_case as PC
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_part_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dag, arrays, owner, root_slot, tail_slot = PC.global_case(S=6, P=4, nranks=2)
+    want1 = PC.global_digests(dag, arrays, dag.leaf_ids)
+    rng = np.random.default_rng(3)
+    pick = np.sort(rng.choice(len(dag.file_slots), size=len(dag.file_slots) // 3, replace=False))
+    new = dag.leaf_ids.copy()
+    new[pick] = rng.integers(0, 256, size=(len(pick), 32), dtype=np.uint8)
+    want2 = PC.global_digests(dag, arrays, new)
+    covered = set()
+    for rank, g, first, second, steps1, steps2, n_imp, n_exp, any_imp in res:
+        g = np.array(g)
+        assert (np.frombuffer(first, np.uint8).reshape(-1, 32) == want1[g]).all(), rank
+        assert (np.frombuffer(second, np.uint8).reshape(-1, 32) == want2[g]).all(), rank
+        assert any_imp and n_imp > 0 and n_exp > 0
+        assert steps2 >= 3  # sample roots -> global root (rank 0) -> tail (rank 1) -> quiet
+        covered |= set(g.tolist())
+    assert covered == set(range(arrays["n_slots"]))  # every slot lives on some rank
