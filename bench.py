@@ -40,7 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from reflow_amd import capi  # noqa: E402
-from reflow_amd.workloads import Dag1000, GiB, arena_layout, c2_sizes  # noqa: E402
+from reflow_amd.workloads import Dag1000, GiB, PartitionedDag1000, arena_layout, c2_sizes  # noqa: E402
 
 # ---- hardware constants (MI355X_MICROARCH.md) ------------------------------
 CLOCK_HZ = 2.4e9
@@ -433,30 +433,48 @@ def bench_c1_install(ctx, arena, offs, want_fsd, cpu_leg=False):
 
 # ------------------------------------------------------- C3: incremental --
 def bench_dag(args, dist, ctx, comm, budget):
-    S = args.dag_samples
+    """configs[2] at N = 1 (one 10M-node DAG); configs[3] at N > 1: ONE global
+    DAG of N x 12.5M nodes (100M at N = 8), partitioned by sample subtree
+    (workloads.PartitionedDag1000) and recomputed with
+    rf_graph_recompute_part's supersteps (boundary bitset OR + boundary
+    digest all-gather over RCCL)."""
     t0 = time.perf_counter()
-    dag = Dag1000(S, args.dag_pairs, seed=0x5EED0003 + 1000003 * dist.rank)
-    a = dag.arrays()
-    g = capi.Graph(ctx, a["n_slots"], a["out_slot"], a["tmpl_off"], a["tmpl_len"], a["hole_ptr"],
-                   a["hole_pos"], a["hole_slot"], a["blob"])
+    part = None
+    if dist.world > 1:
+        S = args.c4_samples
+        part = PartitionedDag1000(S, args.dag_pairs, dist.world, dist.rank)
+        dag, a = part.dag, part.desc
+    else:
+        S = args.dag_samples
+        dag = Dag1000(S, args.dag_pairs)
+        a = dag.arrays()
+    n_nodes = part.n_nodes if part is not None else dag.n_nodes
+    g = capi.Graph.from_arrays(ctx, a)
     g.set_slots(dag.file_slots, dag.leaf_ids)
-    log("C3: %d nodes, %d jobs built+loaded in %.1f s" % (dag.n_nodes, dag.n_jobs, time.perf_counter() - t0))
-    g.recompute(full=True)  # first call also captures the hipGraphs (host work): untimed
+    log("C3: %d nodes, %d jobs built+loaded in %.1f s" % (n_nodes, len(a["out_slot"]), time.perf_counter() - t0))
+    if part is not None:
+        g.set_part(part.part)
+        ag = None
+        if comm is None:  # RF_BENCH_SHARE_GPU rehearsal: gloo host transport
+            ag = lambda b: [x.tobytes() for x in np.split(dist.all_gather_bytes(np.frombuffer(b, np.uint8)), dist.world)]  # noqa: E731,E501
+
+        def recompute(full):
+            return g.recompute_part(comm=comm, allgather=ag, nranks=dist.world, full=full)
+    else:
+        recompute = lambda full: g.recompute(full=full)  # noqa: E731
+    recompute(True)  # first call also captures the hipGraphs (host work): untimed
+    dist.barrier()
     ctx.timer_start()
-    g.recompute(full=True)
+    recompute(True)
     full_ms = ctx.timer_stop()
     slots, old, new = dag.change_set(0.01)
     d_slots = ctx.upload(slots)
     d_old, d_new = ctx.upload(old), ctx.upload(new)
-    roots = dag.kinds["XS"].out_slot
-    d_roots_idx = ctx.upload(roots)
-    d_gather = ctx.alloc(32 * len(roots) * max(dist.world, 1))
-    d_local = ctx.alloc(32 * len(roots))
     # one counted step to learn the dirty-set size
     g.set_slots(slots, new)
-    n_dirty_jobs = g.recompute(full=False)
+    n_dirty_jobs = recompute(False)
     g.set_slots(slots, old)
-    g.recompute(full=False)
+    recompute(False)
     pairs = np.unique(slots // 2)
     n_dirty_nodes = n_dirty_jobs - len(pairs)  # minus the pE1 physical keys
     state = {"v": 0}
@@ -465,14 +483,10 @@ def bench_dag(args, dist, ctx, comm, budget):
         ver = d_new if state["v"] == 0 else d_old
         state["v"] ^= 1
         g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
-        g.recompute_async(False, ctx.stream)
-        if dist.world > 1:  # boundary digests (per-sample roots) to every rank
-            g.gather_device(d_roots_idx.ptr, len(roots), d_local.ptr, ctx.stream)
-            if comm is not None:
-                comm.allgather(d_local.ptr, d_gather.ptr, 32 * len(roots), ctx.stream)
-            else:
-                ctx.sync()
-                dist.all_gather_bytes(d_local.to_numpy())
+        if part is not None:
+            recompute(False)
+        else:
+            g.recompute_async(False, ctx.stream)
 
     steps = args.dag_steps
     t = timed_steps(dist, ctx, step, steps, 2)
@@ -481,14 +495,22 @@ def bench_dag(args, dist, ctx, comm, budget):
         step()
     dev_ms = ctx.timer_stop() / steps
     total_dirty_nodes = dist.sum(n_dirty_nodes) * steps
-    res = {"workload": "1000align DAG S=%d P=%d per GPU, 1%% leaf File IDs toggled per step" % (S, args.dag_pairs),
-           "nodes_per_gpu": dag.n_nodes, "jobs_per_gpu": dag.n_jobs,
+    if part is not None:
+        wl = ("configs[3]: one 1000align DAG of %d samples x P=%d (%d nodes), partitioned by sample subtree "
+              "over %d ranks (%d samples each; shared reference chain replicated; per-rank Merge tree; global root "
+              "on rank 0), 1%% leaf File IDs toggled per step on every rank; supersteps %d"
+              % (S * dist.world, args.dag_pairs, dist.sum(n_nodes), dist.world, S,
+                 g.part_gathered()[2]))
+    else:
+        wl = "configs[2]: 1000align DAG S=%d P=%d, 1%% leaf File IDs toggled per step" % (S, args.dag_pairs)
+    res = {"workload": wl,
+           "nodes_per_gpu": n_nodes, "jobs_per_gpu": len(a["out_slot"]),
            "dirty_nodes_per_step": int(n_dirty_nodes), "dirty_jobs_per_step": int(n_dirty_jobs),
            "ms_per_step": t / steps * 1e3, "device_ms_per_step": dev_ms,
            "mnodes_per_s": total_dirty_nodes / t / 1e6,
-           "effective_mnodes_per_s": dist.sum(dag.n_nodes) * steps / t / 1e6,
+           "effective_mnodes_per_s": dist.sum(n_nodes) * steps / t / 1e6,
            "full_recompute_ms": full_ms,
-           "full_recompute_mnodes_per_s": dag.n_nodes / (full_ms * 1e-3) / 1e6,
+           "full_recompute_mnodes_per_s": n_nodes / (full_ms * 1e-3) / 1e6,
            "levels": g.stats().n_levels}
     st = g.stats()
     ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
@@ -903,6 +925,8 @@ def main():
     ap.add_argument("--sha-gib", type=float, default=64.0)
     ap.add_argument("--dag-samples", type=int, default=22075)  # ~10M nodes at P=32
     ap.add_argument("--dag-pairs", type=int, default=32)
+    ap.add_argument("--c4-samples", type=int, default=27594,
+                    help="samples per rank at N > 1 (12.5M nodes: the global DAG is 100M nodes at N = 8)")
     ap.add_argument("--dag-steps", type=int, default=20)
     ap.add_argument("--probe-keys", type=int, default=100_000_000)
     ap.add_argument("--probe-big-keys", type=int, default=1_200_000_000)
@@ -969,7 +993,8 @@ def main():
             "data": "synthetic (splitmix64 content generated in HBM)",
             "config": {"workload": workload,
                        "parallelism": "files sharded per GPU (LPT by size); per GPU: host leg (SHA-NI threads) + "
-                                      "GPU kernels split by the K1 planner; RCCL only for DAG root digests",
+                                      "GPU kernels split by the K1 planner; DAG partitioned by sample subtree, "
+                                      "RCCL only for its boundary exchange",
                        "exchange": exchange, "split_rank0": sha["split"], "step_ms_rank0": sha["step_ms"]},
             "roofline": sha["roofline"],
             "host_leg": sha["host_leg"],

@@ -96,7 +96,8 @@ hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32
 // reduced bitset, apply changed imports (queues their local consumers).
 hipError_t launch_part_pack(const uint32_t* export_slot, uint32_t n, const uint8_t* slots, uint8_t* snap,
                             uint8_t* send, uint32_t* bits, uint32_t bit0, hipStream_t s);
-hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, uint32_t* flag, hipStream_t s);
+hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, const uint32_t* import_bid, uint32_t n_import,
+                           uint32_t* flag, hipStream_t s);
 hipError_t launch_part_apply(const GraphDev& g, const uint32_t* import_slot, const uint32_t* import_bid, uint32_t n,
                              const uint32_t* bits, const uint8_t* gather, hipStream_t s);
 

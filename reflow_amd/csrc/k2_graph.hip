@@ -607,12 +607,27 @@ __global__ __launch_bounds__(256) void k_part_pack(const uint32_t* __restrict__ 
     dst[1] = hi;
 }
 
-// flag = any bit set in the (OR-reduced) bitset.
-__global__ __launch_bounds__(256) void k_part_any(const uint64_t* __restrict__ bits, uint64_t nwords, uint32_t* flag) {
+// flag[0] = any bit set in the (OR-reduced) bitset; flag[1] = any of this
+// rank's imports has its bit set (else its next superstep has nothing to do).
+__global__ __launch_bounds__(256) void k_part_any(const uint64_t* __restrict__ bits, uint64_t nwords,
+                                                  const uint32_t* __restrict__ import_bid, uint32_t n_import,
+                                                  uint32_t* flag) {
     uint64_t v = 0;
     for (uint64_t i = threadIdx.x; i < nwords; i += blockDim.x) v |= bits[i];
     const int any = __syncthreads_or(v != 0);
-    if (threadIdx.x == 0) flag[0] = any ? 1u : 0u;
+    bool mine = false;
+    if (any) {
+        const uint32_t* b32 = reinterpret_cast<const uint32_t*>(bits);
+        for (uint32_t i = threadIdx.x; i < n_import && !mine; i += blockDim.x) {
+            const uint32_t b = import_bid[i];
+            mine = (b32[b >> 5] >> (b & 31)) & 1u;
+        }
+    }
+    const int my = __syncthreads_or(mine);
+    if (threadIdx.x == 0) {
+        flag[0] = any ? 1u : 0u;
+        flag[1] = my ? 1u : 0u;
+    }
 }
 
 // Imports whose boundary bit is set: the gathered digest into the slot; a
@@ -730,8 +745,9 @@ hipError_t launch_part_pack(const uint32_t* export_slot, uint32_t n, const uint8
     return hipGetLastError();
 }
 
-hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, uint32_t* flag, hipStream_t s) {
-    hipLaunchKernelGGL(k_part_any, dim3(1), dim3(256), 0, s, bits, nwords, flag);
+hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, const uint32_t* import_bid, uint32_t n_import,
+                           uint32_t* flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_part_any, dim3(1), dim3(256), 0, s, bits, nwords, import_bid, n_import, flag);
     return hipGetLastError();
 }
 

@@ -297,27 +297,33 @@ extern "C" int rf_graph_recompute_part(rf_graph* gr, rf_comm* comm, rf_host_allg
     DevGuard dg(ctx->device);
     hipStream_t s = ctx->stream;
     uint64_t tot = 0, steps = 0;
+    bool run = true;  // this rank has new inputs for the superstep
     for (;;) {
-        if (int rc = graph_recompute_locked(gr, steps == 0 ? full : 0, s)) return rc;
+        if (run) {
+            if (int rc = graph_recompute_locked(gr, steps == 0 ? full : 0, s)) return rc;
+            if (out_recomputed)
+                if (int rc = part_counts(gr, s, &tot)) return rc;
+        }
         ++steps;
-        if (out_recomputed)
-            if (int rc = part_counts(gr, s, &tot)) return rc;
         if (!P->nwords) break;  // no rank exports anything: the pieces are independent
         HIPC(hipMemsetAsync(P->d_bits.p, 0, 8 * P->nwords, s));
         HIPC(launch_part_pack(P->d_export_slot.as<uint32_t>(), P->n_export, gr->g.slots, P->d_snap.as<uint8_t>(),
                               P->d_send.as<uint8_t>(), P->d_bits.as<uint32_t>(), (uint32_t)P->rank * P->max_export, s));
         if (int rc = part_or(gr, comm, fn, user, s)) return rc;
         if (P->any_import) {  // a changed import may change exports again: one more superstep
-            uint32_t flag = 0;
-            HIPC(launch_part_any(P->d_bits.as<uint64_t>(), P->nwords, P->d_flag.as<uint32_t>(), s));
-            HIPC(hipMemcpyAsync(&flag, P->d_flag.p, 4, hipMemcpyDeviceToHost, s));
+            uint32_t flag[2] = {0, 0};
+            HIPC(launch_part_any(P->d_bits.as<uint64_t>(), P->nwords, P->d_import_bid.as<uint32_t>(), P->n_import,
+                                 P->d_flag.as<uint32_t>(), s));
+            HIPC(hipMemcpyAsync(flag, P->d_flag.p, 8, hipMemcpyDeviceToHost, s));
             HIPC(hipStreamSynchronize(s));
-            if (!flag) break;
+            if (!flag[0]) break;
+            run = flag[1] != 0;
         }
         if (int rc = part_gather(gr, comm, fn, user, s)) return rc;
         if (!P->any_import) break;  // exports observed, nobody consumes them
-        HIPC(launch_part_apply(gr->g, P->d_import_slot.as<uint32_t>(), P->d_import_bid.as<uint32_t>(), P->n_import,
-                               P->d_bits.as<uint32_t>(), P->d_gather.as<uint8_t>(), s));
+        if (run)
+            HIPC(launch_part_apply(gr->g, P->d_import_slot.as<uint32_t>(), P->d_import_bid.as<uint32_t>(),
+                                   P->n_import, P->d_bits.as<uint32_t>(), P->d_gather.as<uint8_t>(), s));
     }
     P->last_supersteps = steps;
     if (out_recomputed) *out_recomputed = tot;

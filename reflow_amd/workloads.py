@@ -130,18 +130,21 @@ class Dag1000:
     PAIR_KINDS = ["V1", "V2", "C1", "C2", "E1", "C3", "K1", "C4", "E2", "C5", "K2", "C6", "E3", "C7"]
     SAMPLE_KINDS = ["KS", "CS1", "ES", "CS2", "XS"]
 
-    def __init__(self, S: int, P: int = 32, seed=0x5EED0003):
-        self.S, self.P, self.seed = S, P, seed
+    def __init__(self, S: int, P: int = 32, seed=0x5EED0003, sample0=0):
+        """sample0: global index of this DAG's first sample -- Dag1000(S,
+        sample0=r*S) is samples [r*S, (r+1)*S) of the global Dag1000 with the
+        same seed, node for node (rank r's piece of a partitioned DAG)."""
+        self.S, self.P, self.seed, self.sample0 = S, P, seed, sample0
         self.Q = S * P
         self.n_nodes = 3 + self.Q * 14 + S * 5
         self._build()
 
     # deterministic "previous run" values
     def file_id(self, i):  # File ID of leaf file i (2 per pair)
-        return _h(b"file:%d:%d" % (self.seed, i))
+        return _h(b"file:%d:%d" % (self.seed, i + 2 * self.P * self.sample0))
 
-    def out_id(self, tag, i):  # output File ID of exec instance i
-        return _h(b"out:%s:%d:%d" % (tag, self.seed, i))
+    def out_id(self, tag, i):  # output File ID of exec instance i (per pair; "es" per sample)
+        return _h(b"out:%s:%d:%d" % (tag, self.seed, i + (self.sample0 if tag == b"es" else self.P * self.sample0)))
 
     def _ids(self, fn, n):
         return np.frombuffer(b"".join(fn(i) for i in range(n)), dtype=np.uint8).reshape(n, 32)
@@ -158,9 +161,9 @@ class Dag1000:
             return np.arange(b, b + n, dtype=np.uint32)
 
         q = np.arange(Q)
-        s_of_q = q // P
+        s_of_q = q // P + self.sample0
         p_of_q = q % P
-        sidx = np.arange(S)
+        sidx = np.arange(S) + self.sample0
 
         # shared
         k = _Kind("R0", b"OpIntern" + REF_URL, 1)
@@ -417,3 +420,88 @@ class Dag1000:
             for name, f in zip(self.SAMPLE_KINDS, [ks, cs1, es, cs2, xs]):
                 T[name].append(f)
         return T
+
+
+# --------------------------------------------------------------------- C4 --
+def merge_tmpl(k):
+    """A Merge over k deps (the shape of KS: k WD holes, "OpK", FD_MERGE)."""
+    return WD0 * k + b"OpK" + b"\x00\x05" + FD_MERGE
+
+
+def append_jobs(a, jobs):
+    """Append jobs to rf_graph_desc arrays: jobs = [(tmpl bytes, [(pos,
+    slot)...])], each given the next fresh output slot.  Returns (arrays,
+    out slots)."""
+    blob = bytearray(np.asarray(a["blob"], dtype=np.uint8).tobytes())
+    while len(blob) % 16:
+        blob.append(0)
+    n = int(a["n_slots"])
+    offs, lens, hp, pos, sl, outs = [], [], [], [], [], []
+    h = int(a["hole_ptr"][-1])
+    for tmpl, holes in jobs:
+        offs.append(len(blob))
+        lens.append(len(tmpl))
+        blob += tmpl + bytes((-len(tmpl)) % 16)
+        h += len(holes)
+        hp.append(h)
+        pos += [p for p, _ in holes]
+        sl += [x for _, x in holes]
+        outs.append(n)
+        n += 1
+    out = dict(n_slots=n,
+               out_slot=np.concatenate([a["out_slot"], np.array(outs, np.uint32)]).astype(np.uint32),
+               tmpl_off=np.concatenate([a["tmpl_off"], np.array(offs, np.uint64)]).astype(np.uint64),
+               tmpl_len=np.concatenate([a["tmpl_len"], np.array(lens, np.uint32)]).astype(np.uint32),
+               hole_ptr=np.concatenate([a["hole_ptr"], np.array(hp, np.uint64)]).astype(np.uint64),
+               hole_pos=np.concatenate([a["hole_pos"], np.array(pos, np.uint32)]).astype(np.uint32),
+               hole_slot=np.concatenate([a["hole_slot"], np.array(sl, np.uint32)]).astype(np.uint32),
+               blob=np.frombuffer(bytes(blob), dtype=np.uint8))
+    return out, np.array(outs, dtype=np.uint32)
+
+
+def merge_tree(a, leaves, fanin=32):
+    """Fan-in-`fanin` Merge tree over `leaves` slots, appended to arrays a.
+    Returns (arrays, root slot, [tree slots in job order])."""
+    cur, made = np.asarray(leaves, dtype=np.uint32), []
+    while len(cur) > 1:
+        jobs = [(merge_tmpl(len(g)), [(34 * j + 2, int(x)) for j, x in enumerate(g)])
+                for g in (cur[i:i + fanin] for i in range(0, len(cur), fanin))]
+        a, cur = append_jobs(a, jobs)
+        made.append(cur)
+    return a, int(cur[0]), (np.concatenate(made) if made else np.zeros(0, np.uint32))
+
+
+class PartitionedDag1000:
+    """configs[3]'s DAG, one rank's piece: the global 1000align DAG has
+    nranks*S samples and rank r owns samples [r*S, (r+1)*S) -- SURVEY §8(e):
+    partition by sample subtree, the shared reference-index chain replicated
+    on every rank, the global root on rank 0.  Each rank merges its sample
+    roots (XS) with a fan-in-32 Merge tree into a rank root; rank 0's global
+    root merges the rank roots (its own locally, the others imported: one
+    boundary digest per rank, so the exchange per step is nranks bits + 32*
+    nranks bytes).  desc: this piece's rf_graph_desc arrays; part: its
+    rf_graph_part (exports = the rank root on ranks > 0, boundary id = rank).
+    Slot layout: the rank's Dag1000 slots, then its tree slots, then (rank 0)
+    the import slots of ranks 1.. and the global root."""
+
+    def __init__(self, S, P, nranks, rank, seed=0x5EED0003, fanin=32):
+        self.nranks, self.rank = nranks, rank
+        self.dag = Dag1000(S, P, seed, sample0=rank * S)
+        a = self.dag.arrays()
+        a, self.rank_root, self.tree_slots = merge_tree(a, self.dag.kinds["XS"].out_slot, fanin)
+        self.import_slot = np.zeros(0, np.uint32)
+        self.global_root = None
+        if rank == 0 and nranks > 1:
+            base = int(a["n_slots"])
+            self.import_slot = np.arange(base, base + nranks - 1, dtype=np.uint32)
+            a["n_slots"] = base + nranks - 1
+            holes = [self.rank_root] + self.import_slot.tolist()
+            a, outs = append_jobs(a, [(merge_tmpl(nranks), [(34 * j + 2, x) for j, x in enumerate(holes)])])
+            self.global_root = int(outs[0])
+        self.desc = a
+        self.n_nodes = self.dag.n_nodes + len(self.tree_slots) + (1 if self.global_root is not None else 0)
+        ex = np.array([self.rank_root] if rank > 0 else [], dtype=np.uint32)
+        self.part = dict(nranks=nranks, rank=rank, max_export=1 if nranks > 1 else 0, export_slot=ex,
+                         import_slot=self.import_slot,
+                         import_bid=np.arange(1, nranks, dtype=np.uint32) if rank == 0 else np.zeros(0, np.uint32),
+                         any_import=nranks > 1)

@@ -1,18 +1,23 @@
 """Test helper: a global job graph partitioned over ranks.
 
-A 1000align DAG (reflow_amd.workloads.Dag1000) split by sample, the shared
+global_case: a 1000align DAG (reflow_amd.workloads.Dag1000) split by
+sample with rf_graph_split, the shared
 reference-index chain replicated (owner -1), plus two jobs that make the
 exchange real: a global root Merge over every sample's Extern (owned by rank
 0, so it imports every other rank's sample roots) and a consumer of that root
 owned by the last rank (so a change crosses ranks twice: two supersteps).
+global_c4: configs[3]'s DAG as bench.py lays it out per rank
+(workloads.PartitionedDag1000), with the map from each piece to it.
 
 superstep_oracle() runs the protocol of rf_graph_recompute_part with the
 oracle (reflow_oracle.OGraph) as each rank's local engine -- test
 infrastructure for the CPU checks of the splitter and the exchange."""
+import threading
+
 import numpy as np
 
 import reflow_oracle as O
-from reflow_amd.workloads import Dag1000
+from reflow_amd.workloads import Dag1000, append_jobs, merge_tmpl, merge_tree
 
 WD0 = b"\x00\x05" + bytes(32)
 
@@ -54,6 +59,16 @@ def global_case(S=6, P=4, nranks=2):
     return dag, out, owner, root_slot, tail_slot
 
 
+def piece_inputs(piece, dag, file_ids, pick=None):
+    """(local slots, IDs) of a GraphPiece's leaf files among global file
+    indices `pick` (default all)."""
+    g2l = {int(s): i for i, s in enumerate(piece.global_of_local)}
+    ks = range(len(dag.file_slots)) if pick is None else pick
+    mine = [k for k in ks if int(dag.file_slots[k]) in g2l]
+    return (np.array([g2l[int(dag.file_slots[k])] for k in mine], np.uint32),
+            file_ids[mine] if len(mine) else np.zeros((0, 32), np.uint8))
+
+
 def global_digests(dag, arrays, file_ids):
     g = O.OGraph(arrays)
     g.set_inputs(dag.file_slots, file_ids)
@@ -63,26 +78,110 @@ def global_digests(dag, arrays, file_ids):
     return d
 
 
-def superstep_oracle(piece, dag, file_ids, allgather, changed=None, state=None):
+SHARED = ("R0", "R1", "R2", "pR1")
+
+
+class ThreadGather:
+    """All-gather between threads of one process (ranks as threads)."""
+
+    def __init__(self, n):
+        self.n, self.bar, self.buf = n, threading.Barrier(n, timeout=120), [None] * n
+
+    def fn(self, rank):
+        def allgather(b):
+            self.buf[rank] = b
+            self.bar.wait()
+            out = list(self.buf)
+            self.bar.wait()
+            return out
+        return allgather
+
+
+def run_threads(nranks, body):
+    """body(rank, allgather) on nranks threads; returns the results by rank
+    (re-raises the first failure)."""
+    tg = ThreadGather(nranks)
+    res, errs = [None] * nranks, []
+
+    def main(r):
+        try:
+            res[r] = body(r, tg.fn(r))
+        except BaseException as e:  # noqa: BLE001
+            errs.append((r, e))
+            tg.bar.abort()
+
+    th = [threading.Thread(target=main, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    if errs:
+        raise errs[0][1]
+    return res
+
+
+def global_c4(S, P, nranks, seed=0x5EED0003, fanin=32):
+    """The whole configs[3] DAG that PartitionedDag1000(S, P, nranks, r)
+    pieces: Dag1000(nranks*S) + per-rank Merge trees + the global root.
+    Returns (G, arrays, owner, rank roots, rank tree slots, global root)."""
+    G = Dag1000(S * nranks, P, seed)
+    a = G.arrays()
+    roots, trees = [], []
+    for r in range(nranks):
+        a, root, tree = merge_tree(a, G.kinds["XS"].out_slot[r * S:(r + 1) * S], fanin)
+        roots.append(root)
+        trees.append(tree)
+    groot = None
+    if nranks > 1:
+        a, outs = append_jobs(a, [(merge_tmpl(nranks), [(34 * j + 2, x) for j, x in enumerate(roots)])])
+        groot = int(outs[0])
+    owner = []
+    for name, kk in G.kinds.items():
+        if name in SHARED:
+            owner.append(np.full(kk.count, -1))
+        elif kk.count == G.Q:
+            owner.append(np.arange(kk.count) // (P * S))
+        else:
+            owner.append(np.arange(kk.count) // S)
+    for r in range(nranks):
+        owner.append(np.full(len(trees[r]), r))
+    if groot is not None:
+        owner.append([0])
+    return G, a, np.concatenate(owner).astype(np.int32), roots, trees, groot
+
+
+def c4_local_to_global(piece, G, roots, trees, groot):
+    """Global slot of every slot of a PartitionedDag1000 piece."""
+    d, r = piece.dag, piece.rank
+    m = np.full(int(piece.desc["n_slots"]), -1, dtype=np.int64)
+    m[d.file_slots] = G.file_slots[2 * d.Q * r:2 * d.Q * (r + 1)]
+    for name, kk in d.kinds.items():
+        off = 0 if name in SHARED else r * kk.count
+        m[kk.out_slot] = G.kinds[name].out_slot[off:off + kk.count]
+    m[piece.tree_slots] = trees[r]
+    if piece.global_root is not None:
+        m[piece.import_slot] = roots[1:]
+        m[piece.global_root] = groot
+    assert (m >= 0).all()
+    return m
+
+
+def superstep_oracle(desc, part, allgather, inputs=None, changed=None, state=None):
     """Rank's side of rf_graph_recompute_part with the oracle as local engine.
-    allgather(bytes) -> [bytes per rank].  First call (state None): load +
-    full; later calls: `changed` = (global file slots, new IDs).  Returns
-    (state, supersteps)."""
-    part, g2l = piece.part, {int(gs): i for i, gs in enumerate(piece.global_of_local)}
+    allgather(bytes) -> [bytes per rank].  First call (state None): inputs =
+    (local slots, IDs) loaded, full recompute; later calls: `changed` = (local
+    slots, new IDs).  Returns (state, supersteps)."""
     nr, me, mx = part["nranks"], part["rank"], part["max_export"]
     if state is None:
-        og = O.OGraph(piece.desc)
-        local_files = [(g2l[int(s)], file_ids[k]) for k, s in enumerate(dag.file_slots) if int(s) in g2l]
-        if local_files:
-            og.set_inputs([s for s, _ in local_files], np.stack([d for _, d in local_files]))
+        og = O.OGraph(desc)
+        if inputs is not None and len(inputs[0]):
+            og.set_inputs(inputs[0], inputs[1])
         og.full()
         state = {"og": og, "snap": np.zeros((len(part["export_slot"]), 32), np.uint8)}
     else:
         og = state["og"]
-        sl, ids = changed
-        loc = [(g2l[int(s)], ids[k]) for k, s in enumerate(sl) if int(s) in g2l]
-        if loc:
-            og.update([s for s, _ in loc], np.stack([d for _, d in loc]))
+        if changed is not None and len(changed[0]):
+            og.update(changed[0], changed[1])
     steps = 0
     nbits = nr * mx
     while True:

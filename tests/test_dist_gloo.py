@@ -90,15 +90,15 @@ def _part_worker(rank, world, port, q):
     dag, arrays, owner, root_slot, tail_slot = PC.global_case(S=6, P=4, nranks=world)
     piece = capi.GraphPiece(arrays, world, rank, owner)
     ids = dag.leaf_ids.copy()
-    state, steps1 = PC.superstep_oracle(piece, dag, ids, allgather)
+    state, steps1 = PC.superstep_oracle(piece.desc, piece.part, allgather, inputs=PC.piece_inputs(piece, dag, ids))
     first = state["og"].slots[:len(piece.global_of_local)].copy()
     # change 1/3 of the leaf files, including ones of every sample
     rng = np.random.default_rng(3)
     pick = np.sort(rng.choice(len(dag.file_slots), size=len(dag.file_slots) // 3, replace=False))
     new = ids.copy()
     new[pick] = rng.integers(0, 256, size=(len(pick), 32), dtype=np.uint8)
-    state, steps2 = PC.superstep_oracle(piece, dag, new, allgather, changed=(dag.file_slots[pick], new[pick]),
-                                        state=state)
+    state, steps2 = PC.superstep_oracle(piece.desc, piece.part, allgather,
+                                        changed=PC.piece_inputs(piece, dag, new, pick), state=state)
     second = state["og"].slots[:len(piece.global_of_local)].copy()
     q.put((rank, piece.global_of_local.tolist(), first.tobytes(), second.tobytes(), steps1, steps2,
            len(piece.part["import_slot"]), len(piece.part["export_slot"]), piece.part["any_import"]))

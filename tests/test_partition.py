@@ -1,0 +1,81 @@
+"""configs[3]'s partitioned DAG on the CPU: the per-rank pieces
+bench.py builds (workloads.PartitionedDag1000: samples [r*S, (r+1)*S), the
+shared reference chain replicated, per-rank Merge tree, global root on rank
+0) together compute exactly the digests of the one global DAG, slot for slot,
+through the superstep exchange of rf_graph_recompute_part (ranks as threads,
+the oracle as each rank's local engine); and rf_graph_split of that global
+DAG (the library's splitter) finds the same boundary."""
+import numpy as np
+import pytest
+
+import partition_case as PC
+from reflow_amd import capi
+from reflow_amd.workloads import Dag1000, PartitionedDag1000
+
+
+def test_sample0_slices_the_global_dag():
+    G = Dag1000(6, 3)
+    for r in range(3):
+        d = Dag1000(2, 3, sample0=2 * r)
+        assert (d.leaf_ids == G.leaf_ids[12 * r:12 * (r + 1)]).all()
+        a, ga = d.arrays(), G.arrays()
+        for name in ("E1", "ES", "pE2", "pXS"):
+            k, gk = d.kinds[name], G.kinds[name]
+            gi = np.arange(k.count) + r * k.count
+            for i in range(k.count):
+                j = int(np.nonzero(a["out_slot"] == k.out_slot[i])[0][0])
+                gj = int(np.nonzero(ga["out_slot"] == gk.out_slot[gi[i]])[0][0])
+                assert bytes(a["blob"][a["tmpl_off"][j]:a["tmpl_off"][j] + a["tmpl_len"][j]]) == \
+                    bytes(ga["blob"][ga["tmpl_off"][gj]:ga["tmpl_off"][gj] + ga["tmpl_len"][gj]])
+
+
+@pytest.mark.parametrize("nranks,S,P,fanin", [(2, 5, 3, 32), (3, 40, 4, 8), (4, 9, 2, 4)])
+def test_c4_pieces_equal_global_dag(nranks, S, P, fanin):
+    G, ga, owner, roots, trees, groot = PC.global_c4(S, P, nranks, fanin=fanin)
+    rng = np.random.default_rng(nranks)
+    nf = len(G.file_slots)
+    ids = [G.leaf_ids.copy()]
+    picks = []
+    for frac, ranks in ((0.01, range(nranks)), (0.2, range(1, nranks))):  # then: rank 0's samples unchanged
+        pick = np.sort(rng.choice([k for k in range(nf) if k // (2 * P * S) in ranks], size=max(1, int(nf * frac)),
+                                  replace=False))
+        new = ids[-1].copy()
+        new[pick] = rng.integers(0, 256, size=(len(pick), 32), dtype=np.uint8)
+        ids.append(new)
+        picks.append(pick)
+    wants = [PC.global_digests(G, ga, x) for x in ids]
+
+    def body(r, ag):
+        pc = PartitionedDag1000(S, P, nranks, r, fanin=fanin)
+        m = PC.c4_local_to_global(pc, G, roots, trees, groot)
+        f0 = 2 * pc.dag.Q * r
+        out = []
+        st, n = PC.superstep_oracle(pc.desc, pc.part, ag, inputs=(pc.dag.file_slots, ids[0][f0:f0 + 2 * pc.dag.Q]))
+        out.append((st["og"].slots[:len(m)].copy(), n))
+        for pick, x in zip(picks, ids[1:]):
+            mine = pick[(pick >= f0) & (pick < f0 + 2 * pc.dag.Q)]
+            st, n = PC.superstep_oracle(pc.desc, pc.part, ag, changed=(pc.dag.file_slots[mine - f0], x[mine]),
+                                        state=st)
+            out.append((st["og"].slots[:len(m)].copy(), n))
+        st["og"].close()
+        return m, out
+
+    res = PC.run_threads(nranks, body)
+    for r, (m, out) in enumerate(res):
+        for step, ((slots, n), want) in enumerate(zip(out, wants)):
+            assert (slots == want[m]).all(), (r, step)
+            assert n == 2  # rank roots -> global root, then quiet
+    assert (wants[2][groot] != wants[1][groot]).any()  # rank 0 saw only imported changes
+
+
+def test_split_finds_the_same_boundary():
+    nranks, S, P = 3, 10, 2
+    G, ga, owner, roots, trees, groot = PC.global_c4(S, P, nranks, fanin=4)
+    for r in range(nranks):
+        piece = capi.GraphPiece(ga, nranks, r, owner)
+        pc = PartitionedDag1000(S, P, nranks, r, fanin=4)
+        gl = piece.global_of_local
+        assert sorted(gl[piece.part["export_slot"]].tolist()) == ([roots[r]] if r else [])
+        assert sorted(gl[piece.part["import_slot"]].tolist()) == (sorted(roots[1:]) if r == 0 else [])
+        assert len(piece.desc["out_slot"]) == len(pc.desc["out_slot"])
+        assert piece.part["any_import"]
