@@ -529,10 +529,10 @@ static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const u
     }
     HIPC(p->h_host_dig.ensure(32 * std::max<uint64_t>(n_host, 1)));
     if (n) {
-        HIPC(hipMemcpy(p->d_offs.p, offs, 8 * n, hipMemcpyHostToDevice));
-        HIPC(hipMemcpy(p->d_lens.p, lens, 8 * n, hipMemcpyHostToDevice));
-        if (n_gpu) HIPC(hipMemcpy(p->d_order.p, order.data() + n_host, 4 * n_gpu, hipMemcpyHostToDevice));
-        if (n_host) HIPC(hipMemcpy(p->d_host_ids.p, order.data(), 4 * n_host, hipMemcpyHostToDevice));
+        HIPC(sync_copy(ctx, p->d_offs.p, offs, 8 * n, hipMemcpyHostToDevice));
+        HIPC(sync_copy(ctx, p->d_lens.p, lens, 8 * n, hipMemcpyHostToDevice));
+        if (n_gpu) HIPC(sync_copy(ctx, p->d_order.p, order.data() + n_host, 4 * n_gpu, hipMemcpyHostToDevice));
+        if (n_host) HIPC(sync_copy(ctx, p->d_host_ids.p, order.data(), 4 * n_host, hipMemcpyHostToDevice));
     }
     if (!p->side) HIPC(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
     for (hipEvent_t* ev : {&p->e0, &p->e_solo, &p->e_lanes, &p->e1})
@@ -1538,7 +1538,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
         hipError_t e = b.ensure(std::max<size_t>(bytes, 64));
         if (e != hipSuccess) return e;
-        return bytes ? hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
+        return bytes ? sync_copy(ctx, b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
     };
     hipError_t e;
     if ((e = up(gr->b_meta, meta.data(), 32ull * J)) != hipSuccess ||
@@ -1555,10 +1555,10 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
                     hipGetErrorString(e));
     HIPC(gr->b_holes.ensure(8));  // k2's record loads read element 0 unconditionally
-    HIPC(hipMemset(gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
-    HIPC(hipMemset(gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
-    HIPC(hipMemset(gr->b_counts.p, 0, 4ull * (L + 1)));
-    HIPC(hipMemset(gr->b_counts_last.p, 0, 4ull * (L + 1)));
+    HIPC(sync_memset(ctx, gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
+    HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
+    HIPC(sync_memset(ctx, gr->b_counts.p, 0, 4ull * (L + 1)));
+    HIPC(sync_memset(ctx, gr->b_counts_last.p, 0, 4ull * (L + 1)));
     G.meta = gr->b_meta.as<uint4>();
     G.holes = gr->b_holes.as<uint2>();
     G.cons_ptr = gr->b_cons_ptr.as<uint32_t>();
@@ -1572,7 +1572,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
     if (getenv("RF_K2_STAMPS")) {  // diagnostic: per-phase times of workgroup 0 of each level
         HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
-        HIPC(hipMemset(gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
+        HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
         G.stamps = static_cast<unsigned long long*>(gr->b_stamps.p);
     }
     HIPC(hipEventCreate(&gr->e0));
@@ -1704,7 +1704,7 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
     for (uint32_t l = 0; l <= gr->g.n_levels; ++l) tot += counts[l];
     if (gr->g.stamps && !full) {  // diagnostic print: per level, chain wave then producer wave
         std::vector<unsigned long long> st(128ull * gr->g.n_levels);
-        HIPC(hipMemcpy(st.data(), gr->g.stamps, 8 * st.size(), hipMemcpyDeviceToHost));
+        HIPC(sync_copy(ctx, st.data(), gr->g.stamps, 8 * st.size(), hipMemcpyDeviceToHost));
         for (uint32_t l = 0; l < gr->g.n_levels; ++l)
             for (int w = 0; w < 2; ++w) {
                 const unsigned long long* x = &st[128ull * l + 64 * w];
@@ -1792,11 +1792,11 @@ static int bloom_make(rf_ctx* ctx, uint64_t m, uint64_t k, const uint64_t* words
         delete bl;
         return fail(RF_ENOMEM, "bloom alloc: %s", hipGetErrorString(e));
     }
-    HIPC(hipMemset(bl->words.p, 0, 8 * cap));
+    HIPC(sync_memset(ctx, bl->words.p, 0, 8 * cap));
     // the bitset holds exactly wordsNeeded(length) words (bitset.go:89-94,
     // ReadFrom); words past them stay zero, as extendSetMaybe exposes them
-    if (need && words) HIPC(hipMemcpy(bl->words.p, words, 8 * need, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(bl->len_dev.p, &length, 8, hipMemcpyHostToDevice));
+    if (need && words) HIPC(sync_copy(ctx, bl->words.p, words, 8 * need, hipMemcpyHostToDevice));
+    HIPC(sync_copy(ctx, bl->len_dev.p, &length, 8, hipMemcpyHostToDevice));
     bl->b.m = m;
     bl->b.k = k;
     bl->b.length = length;
@@ -1950,7 +1950,7 @@ extern "C" int rf_bloom_params(rf_bloom* bl, uint64_t* m, uint64_t* k, uint64_t*
     ARG(bl, "null bloom");
     DevGuard dg(bl->ctx->device);
     uint64_t len = 0;
-    HIPC(hipMemcpy(&len, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
+    HIPC(sync_copy(bl->ctx, &len, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
     if (m) *m = bl->b.m;
     if (k) *k = bl->b.k;
     if (length) *length = len;
@@ -1962,7 +1962,7 @@ extern "C" int rf_bloom_words(rf_bloom* bl, uint64_t* words, uint64_t nwords) {
     ARG(bl && (nwords == 0 || words), "null argument");
     ARG(nwords <= bl->b.nwords, "nwords exceeds filter capacity");
     DevGuard dg(bl->ctx->device);
-    if (nwords) HIPC(hipMemcpy(words, bl->b.words, 8 * nwords, hipMemcpyDeviceToHost));
+    if (nwords) HIPC(sync_copy(bl->ctx, words, bl->b.words, 8 * nwords, hipMemcpyDeviceToHost));
     return RF_OK;
 }
 
@@ -1971,11 +1971,11 @@ extern "C" int rf_bloom_words(rf_bloom* bl, uint64_t* words, uint64_t nwords) {
 // wordsNeeded(length) words (bitset.go:628-640).
 static int bloom_bitset_bytes(rf_bloom* bl, std::vector<uint8_t>& o) {
     uint64_t length = 0;
-    HIPC(hipMemcpy(&length, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
+    HIPC(sync_copy(bl->ctx, &length, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
     const uint64_t nw = (length + 63) / 64;
     if (nw > bl->b.nwords) return fail(RF_EINVAL, "bitset length exceeds filter capacity");
     std::vector<uint64_t> w(nw);
-    if (nw) HIPC(hipMemcpy(w.data(), bl->b.words, 8 * nw, hipMemcpyDeviceToHost));
+    if (nw) HIPC(sync_copy(bl->ctx, w.data(), bl->b.words, 8 * nw, hipMemcpyDeviceToHost));
     auto put = [&](uint64_t v) {
         for (int i = 7; i >= 0; --i) o.push_back((uint8_t)(v >> (8 * i)));
     };
@@ -2080,7 +2080,7 @@ extern "C" int rf_bloom_collect(rf_bloom* bl, const uint8_t* digests32, const in
     uint64_t nb[2] = {0, 0};
     HIPC(hipMemcpyAsync(nb, bl->nb.p, 16, hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
-    if (nb[0]) HIPC(hipMemcpy(dead_idx, bl->idx.p, 8 * nb[0], hipMemcpyDeviceToHost));
+    if (nb[0]) HIPC(sync_copy(bl->ctx, dead_idx, bl->idx.p, 8 * nb[0], hipMemcpyDeviceToHost));
     *n_dead = nb[0];
     if (dead_bytes) *dead_bytes = (int64_t)nb[1];
     return RF_OK;
@@ -2455,9 +2455,9 @@ extern "C" int rf_assoc_get_abbrev(rf_assoc* a, int kind, const uint8_t* keys32,
             } else if (h[j] > 1) {
                 status[i] = RF_EINVAL;  // "more than one key matched" (dydbassoc.go:145-146)
             } else {
-                HIPC(hipMemcpy(keys_out32 + 32 * i, a->keys.as<uint8_t>() + 32ull * h[64 + j], 32,
+                HIPC(sync_copy(ctx, keys_out32 + 32 * i, a->keys.as<uint8_t>() + 32ull * h[64 + j], 32,
                                hipMemcpyDeviceToHost));
-                HIPC(hipMemcpy(vals32 + 32 * i, a->vals.as<uint8_t>() + 32ull * h[64 + j], 32,
+                HIPC(sync_copy(ctx, vals32 + 32 * i, a->vals.as<uint8_t>() + 32ull * h[64 + j], 32,
                                hipMemcpyDeviceToHost));
                 status[i] = RF_OK;
             }
@@ -2470,7 +2470,7 @@ extern "C" int rf_assoc_stats(rf_assoc* a, uint64_t* occupied, uint64_t* capacit
     ARG(a, "null assoc");
     DevGuard dg(a->ctx->device);
     uint32_t used = 0;
-    HIPC(hipMemcpy(&used, a->count.p, 4, hipMemcpyDeviceToHost));
+    HIPC(sync_copy(a->ctx, &used, a->count.p, 4, hipMemcpyDeviceToHost));
     if (occupied) *occupied = used;
     if (capacity) *capacity = a->cap;
     return RF_OK;

@@ -109,6 +109,22 @@ inline HostPool* ctx_pool(rf_ctx* ctx) {
 }
 
 
+// Blocking copy / memset on the context's own (non-blocking) stream, never
+// the legacy null stream: a legacy-stream operation is ordered after every
+// stream of the device, and HIP refuses it (hipErrorStreamCaptureImplicit)
+// while another thread captures a hipGraph -- several contexts in one
+// process (ranks as threads, a server's concurrent callers) must not.
+inline hipError_t sync_copy(rf_ctx* c, void* dst, const void* src, size_t n, hipMemcpyKind k) {
+    if (!n) return hipSuccess;
+    hipError_t e = hipMemcpyAsync(dst, src, n, k, c->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(c->stream);
+}
+inline hipError_t sync_memset(rf_ctx* c, void* dst, int v, size_t n) {
+    if (!n) return hipSuccess;
+    hipError_t e = hipMemsetAsync(dst, v, n, c->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(c->stream);
+}
+
 struct DevGuard {
     explicit DevGuard(int d) { (void)hipSetDevice(d); }
 };

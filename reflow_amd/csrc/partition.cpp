@@ -222,7 +222,7 @@ extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
     P->nwords = ((uint64_t)p->nranks * p->max_export + 63) / 64;
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
         hipError_t e = b.ensure(std::max<size_t>(bytes, 64));
-        return e != hipSuccess || !bytes ? e : hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
+        return e != hipSuccess || !bytes ? e : sync_copy(ctx, b.p, src, bytes, hipMemcpyHostToDevice);
     };
     const uint64_t blk = 32ull * std::max<uint32_t>(p->max_export, 1);
     hipError_t e;
@@ -236,7 +236,7 @@ extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
         (e = P->d_flag.ensure(64)) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "partition alloc: %s", hipGetErrorString(e));
     // nothing sent yet: every export counts as changed at the first exchange
-    HIPC(hipMemset(P->d_snap.p, 0, 32ull * std::max<uint32_t>(p->n_export, 1)));
+    HIPC(sync_memset(ctx, P->d_snap.p, 0, 32ull * std::max<uint32_t>(p->n_export, 1)));
     return RF_OK;
 }
 
