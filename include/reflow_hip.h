@@ -406,7 +406,11 @@ int rf_bloom_collect_device(rf_bloom *b, const void *d_digests32, const void *d_
  * canonical representative.  *n_unique = |{ i : canon[i] == i }|.  n <= 2^30. */
 int rf_dedup_digests(rf_ctx *ctx, const uint8_t *digests32, uint32_t n, uint32_t *canon,
                      uint32_t *n_unique);
-/* Device-resident form (digests e.g. gathered from rf_graph slots). */
+/* Device-resident form (digests e.g. gathered from rf_graph slots), on
+ * `stream`.  *d_n_unique (uint32) gets the class count; its bit 31 set means
+ * the batch hit the kernel's probe bound (65536 slots of linear probing at
+ * load <= 1/2: not reachable for SHA-256 digests) and the result
+ * must not be used -- rf_dedup_digests returns RF_EDEVICE for it. */
 int rf_dedup_digests_device(rf_ctx *ctx, const void *d_digests32, uint32_t n, void *d_canon,
                             void *d_n_unique, void *stream);
 

@@ -85,13 +85,6 @@ extern "C" int rf_init(int device, rf_ctx** out) {
     e = probe_kernels();
     if (e != hipSuccess)
         return fail(RF_EDEVICE, "gfx950 code object not loadable: %s", hipGetErrorString(e));
-    // device-form calls take per-call scratch from the default pool in stream
-    // order; keep freed blocks pooled for the next call instead of unmapping
-    hipMemPool_t pool = nullptr;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
-        uint64_t keep = ~0ull;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
     rf_ctx* ctx = new rf_ctx();
     ctx->device = device;
     ctx->n_cu = prop.multiProcessorCount;
@@ -116,6 +109,8 @@ extern "C" void rf_destroy(rf_ctx* ctx) {
     ctx->d_tab3.release();
     ctx->d_place.release();
     ctx->h_stage.release();
+    ctx->sc_dedup.destroy();
+    ctx->sc_collect.destroy();
     rf_sha_plan_destroy(ctx->tplan);
     delete ctx->pool;
     if (ctx->t0) (void)hipEventDestroy(ctx->t0);
@@ -2046,16 +2041,17 @@ extern "C" int rf_bloom_collect_device(rf_bloom* bl, const void* d_digests32, co
     hipStream_t s = pick(bl->ctx, stream);
     HIPC(hipMemsetAsync(d_counts2, 0, 16, s));
     if (!n) return RF_OK;
-    // per-call scratch in stream order (see dedup_on_stream)
-    void *dead = nullptr, *tiles = nullptr;
-    HIPC(hipMallocAsync(&dead, n, s));
-    hipError_t e = hipMallocAsync(&tiles, 4 * bloom_collect_tiles(n), s);
-    if (e == hipSuccess)
-        e = launch_bloom_collect(bl->b, static_cast<const uint8_t*>(d_digests32), static_cast<const int64_t*>(d_sizes),
-                                 n, static_cast<uint8_t*>(dead), static_cast<uint32_t*>(tiles),
-                                 static_cast<uint64_t*>(d_dead_idx), static_cast<uint64_t*>(d_counts2), s);
-    if (tiles) (void)hipFreeAsync(tiles, s);
-    (void)hipFreeAsync(dead, s);
+    // scratch handed between streams in stream order (StreamScratch, ctx.h)
+    StreamScratch& sc = bl->ctx->sc_collect;
+    std::lock_guard<std::mutex> lk(sc.mu);
+    const size_t dead_bytes = (n + 255) / 256 * 256;
+    HIPC(sc.acquire(dead_bytes + 4 * bloom_collect_tiles(n), s));
+    uint8_t* dead = sc.buf.as<uint8_t>();
+    hipError_t e = launch_bloom_collect(bl->b, static_cast<const uint8_t*>(d_digests32),
+                                        static_cast<const int64_t*>(d_sizes), n, dead,
+                                        reinterpret_cast<uint32_t*>(dead + dead_bytes),
+                                        static_cast<uint64_t*>(d_dead_idx), static_cast<uint64_t*>(d_counts2), s);
+    HIPC(sc.release(s));
     if (e != hipSuccess) return fail(RF_EDEVICE, "collect: %s", hipGetErrorString(e));
     return RF_OK;
 }
@@ -2088,20 +2084,18 @@ extern "C" int rf_bloom_collect(rf_bloom* bl, const uint8_t* digests32, const in
 
 // ---------------------------------------------------------------------------
 // K5: Canonicalize's flowMap (flow.go:814-843, flowMap.Get/Put :881-907)
-// Scratch of a device-form call lives in stream order on the caller's
-// stream (hipMallocAsync / hipFreeAsync): calls on different streams or
-// threads never share it (the context's scratch buffers are only for the
-// host forms, which run under ctx->mu on ctx->stream).
-static int dedup_on_stream(const void* d_digests32, uint32_t n, void* d_canon, void* d_n_unique, hipStream_t s) {
-    void *tab = nullptr, *slot_of = nullptr;
-    HIPC(hipMallocAsync(&tab, 4ull * dedup_table_slots(n), s));
-    hipError_t e = hipMallocAsync(&slot_of, 4ull * std::max<uint32_t>(n, 1), s);
-    if (e == hipSuccess)
-        e = launch_dedup(static_cast<const uint8_t*>(d_digests32), n, static_cast<uint32_t*>(tab),
-                         static_cast<uint32_t*>(slot_of), static_cast<uint32_t*>(d_canon),
-                         static_cast<uint32_t*>(d_n_unique), s);
-    if (slot_of) (void)hipFreeAsync(slot_of, s);
-    (void)hipFreeAsync(tab, s);
+// Scratch of a device-form call: the context's StreamScratch, handed
+// between the callers' streams in stream order (ctx.h).
+static int dedup_on_stream(rf_ctx* ctx, const void* d_digests32, uint32_t n, void* d_canon, void* d_n_unique,
+                           hipStream_t s) {
+    StreamScratch& sc = ctx->sc_dedup;
+    std::lock_guard<std::mutex> lk(sc.mu);
+    const size_t tab_bytes = 4ull * dedup_table_slots(n);
+    HIPC(sc.acquire(tab_bytes + 4ull * std::max<uint32_t>(n, 1), s));
+    uint32_t* tab = sc.buf.as<uint32_t>();
+    hipError_t e = launch_dedup(static_cast<const uint8_t*>(d_digests32), n, tab, tab + tab_bytes / 4,
+                                static_cast<uint32_t*>(d_canon), static_cast<uint32_t*>(d_n_unique), s);
+    HIPC(sc.release(s));
     if (e != hipSuccess) return fail(RF_EDEVICE, "dedup: %s", hipGetErrorString(e));
     return RF_OK;
 }
@@ -2111,7 +2105,7 @@ extern "C" int rf_dedup_digests_device(rf_ctx* ctx, const void* d_digests32, uin
     ARG(ctx && d_n_unique && (n == 0 || (d_digests32 && d_canon)), "null argument");
     ARG(n <= (1u << 30), "dedup batch too large (n <= 2^30)");
     DevGuard dg(ctx->device);
-    return dedup_on_stream(d_digests32, n, d_canon, d_n_unique, pick(ctx, stream));
+    return dedup_on_stream(ctx, d_digests32, n, d_canon, d_n_unique, pick(ctx, stream));
 }
 
 extern "C" int rf_dedup_digests(rf_ctx* ctx, const uint8_t* digests32, uint32_t n, uint32_t* canon,
@@ -2131,6 +2125,7 @@ extern "C" int rf_dedup_digests(rf_ctx* ctx, const uint8_t* digests32, uint32_t 
     if (n) HIPC(hipMemcpyAsync(canon, d_canon, 4ull * n, hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipMemcpyAsync(n_unique, d_nu, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
+    if (*n_unique & 0x80000000u) return fail(RF_EDEVICE, "dedup: probe bound exceeded (table not usable)");
     return RF_OK;
 }
 

@@ -78,6 +78,39 @@ struct HostBuf {  // pinned staging
     uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
 };
 
+// Scratch of the device-form calls (rf_dedup_digests_device,
+// rf_bloom_collect_device), which run on the caller's stream, not under the
+// context mutex's stream: one buffer per kind of call, handed between
+// streams in stream order -- a call waits on its stream for the previous
+// user's event and records its own after its last kernel.  (Per-call
+// hipMallocAsync/hipFreeAsync blocks from the default pool were tried: on
+// ROCm 7.2 a second call's table came back holding the first call's other
+// array, tools/dedup_probe.py)
+struct StreamScratch {
+    std::mutex mu;
+    DevBuf buf;
+    hipEvent_t last = nullptr;  // never recorded = complete
+    // with mu held: a buffer of >= bytes that stream s may use
+    hipError_t acquire(size_t bytes, hipStream_t s) {
+        hipError_t e = hipSuccess;
+        if (!last && (e = hipEventCreateWithFlags(&last, hipEventDisableTiming)) != hipSuccess) return e;
+        if (bytes > buf.cap) {
+            if ((e = hipEventSynchronize(last)) != hipSuccess) return e;
+            return buf.ensure(bytes);
+        }
+        return hipStreamWaitEvent(s, last, 0);
+    }
+    hipError_t release(hipStream_t s) { return hipEventRecord(last, s); }
+    void destroy() {
+        if (last) {
+            (void)hipEventSynchronize(last);
+            (void)hipEventDestroy(last);
+        }
+        last = nullptr;
+        buf.release();
+    }
+};
+
 struct rf_ctx {
     int device = 0;
     int n_cu = 256;
@@ -89,6 +122,7 @@ struct rf_ctx {
     rf_sha_plan* tplan = nullptr;  // one-shot batches (transient_plan)
     int host_threads = -1;         // K1 host leg: -1 default width, 0 none
     HostPool* pool = nullptr;      // created on first use
+    StreamScratch sc_dedup, sc_collect;
 };
 
 // Host-leg width of a context (0 when the CPU has no SHA extensions).

@@ -30,6 +30,7 @@
 
 #include "engine.h"
 #include "sha256_dev.h"
+#include "lag_chain.h"
 
 namespace rf {
 
@@ -292,7 +293,7 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
     for (uint32_t b = 0; b < cur.nb; ++b) {
         uint32_t w[16];
         cur.block(a, b, ring, w);
-        if (a.dbg_twice) {
+        if (a.dbg_twice == 1) {  // (2 = RF_K2_STAMPS=2, not a hashing mode)
             ShaState s2 = st;
             uint32_t w2[16];
 #pragma unroll
@@ -554,6 +555,394 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
     }
 }
 
+// k2_level_pl: k2_level_pc with two chain waves running the two-lane lagged
+// chain (lag_chain.h RF_L2_*: 9 instructions per round instead of
+// compress_kw's 14; ~1.2 instead of ~1.9 us per block).  A workgroup still
+// takes 64 jobs: chain wave c holds jobs 32c..32c+31 (job j's e-lane and its
+// row_half_mirror a-lane), the producer (kW = 2) or assembler + expander (kW
+// = 3) waves hold one job per lane as before.  The chain runs every block
+// step for all its lanes (a lane past its job's last block hashes stale rows
+// and is ignored): a job's digest is its chaining value after group 0 of
+// block nb (the k1_sha256_octo rule), combined into the e-lane with one
+// mirror move per word.  Block counts differ between the waves' job sets,
+// so the iteration count comes from LDS: s_nb[j] = the fused target's block
+// count, published with s_next at the hand-over.
+// stamps (RF_K2_STAMPS): workgroup 0's chain wave 0 (row 0) and producer (row 1)
+#define RF_STAMP_PL(k)                                                                                \
+    do {                                                                                              \
+        if (a.stamps && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == kProd) && (k) < 64)    \
+            a.stamps[128 * a.lvl + 64 * (wave != 0) + (k)] = __builtin_amdgcn_s_memrealtime();        \
+    } while (0)
+
+// Streamed hand-over (kStream, kW = 2): no per-block barrier.  The producer
+// publishes K+W rows in 16-word chunks -- s_prod counts chunks written over
+// the workgroup's life (block gb's chunk c: 4 gb + c + 1) -- and the chain
+// waits for exactly the chunk its next LDS read needs, so a fused job's
+// block 0 starts right after its assembly instead of after its whole
+// expansion; s_cons[c] counts blocks chain wave c has finished, and the
+// producer reuses a row buffer only once both chain waves are past it.
+// Flags are written after s_waitcnt lgkmcnt(0) (the rows are in LDS) and
+// polled with s_sleep; no global-memory wait is involved.
+__device__ __forceinline__ uint32_t lds_poll(volatile uint32_t* flag, uint32_t need, uint32_t known) {
+    while ((int32_t)(known - need) < 0) {
+        known = __builtin_amdgcn_readfirstlane(*flag);
+        if ((int32_t)(known - need) < 0) __builtin_amdgcn_s_sleep(1);
+    }
+    __asm__ volatile("" ::: "memory");
+    return known;
+}
+__device__ __forceinline__ void lds_publish(volatile uint32_t* flag, uint32_t v, uint32_t lane) {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) *flag = v;
+}
+// As lds_publish for the chunk before the last one: its four row writes are
+// complete once at most the four younger ones (the chunk just written) are
+// outstanding -- the drain of a chunk's writes overlaps the next expansion.
+__device__ __forceinline__ void lds_publish_prev(volatile uint32_t* flag, uint32_t v, uint32_t lane) {
+    __asm__ volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    if (lane == 0) *flag = v;
+}
+
+// K+W[16c .. 16c+15] of a block into its row (kw_expand_store in chunks; w
+// is the rolling 16-word schedule window, as there)
+__device__ __forceinline__ void kw_expand_chunk(uint32_t (&w)[16], uint4* row, int c) {
+    constexpr uint32_t K[64] = RF_SHA_K;
+#pragma unroll
+    for (int t4 = 4 * c; t4 < 4 * c + 4; ++t4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = 4 * t4 + u;
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+                w[t & 15] = wt;
+            }
+            v[u] = K[t] + wt;
+        }
+        row[t4] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+template <uint32_t kW, bool kStream>
+__global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
+    static_assert(kW == 2 || kW == 3, "producer (+ expander)");
+    static_assert(!kStream || kW == 2, "streamed hand-over: producer + chain only");
+    constexpr uint32_t lag = kW - 1;
+    constexpr uint32_t kProd = 2, kExp = 3;  // wave roles: 0, 1 chain
+    __shared__ __attribute__((aligned(16))) uint32_t kw[(2 * 64 + 1) * kPcRow];  // + the a-lanes' k row
+    __shared__ __attribute__((aligned(16))) uint32_t wbuf[kW == 3 ? 2 * 64 * kWRow : 4];
+    __shared__ uint32_t ring_all[64 * kRing];
+    __shared__ uint4 s_dig[64][2];
+    __shared__ uint32_t s_next[64];
+    __shared__ uint32_t s_nb[64];
+    __shared__ uint32_t s_prod, s_cons[2];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t* ring = &ring_all[lane * kRing];
+    // chain lanes: half-row position hp; e-lanes hp & 4 == 0, partner 7 - hp
+    const uint32_t hp = lane & 15;
+    const bool elane = (hp & 4) == 0;
+    const uint32_t ep = elane ? hp : ((hp & 8) | (7 - (hp & 7)));
+    const uint32_t jl = wave < 2 ? 32 * wave + 8 * (lane >> 4) + ((ep & 3) | ((ep >> 3) << 2)) : lane;
+    const bool chain = wave < 2;
+    uint32_t* const ones = &kw[128 * kPcRow];
+    if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        ones[lane] = lane ? 1u : 0u;
+        if (lane < kPcRow - 64) ones[64 + lane] = 1u;
+    }
+    if (wave == 1) __builtin_amdgcn_s_setprio(3);
+    if (threadIdx.x == 0) {
+        s_prod = 0;
+        s_cons[0] = s_cons[1] = 0;
+    }
+    lds_barrier();
+    uint32_t gb = 0, known = 0, known_c0 = 0, known_c1 = 0;  // streamed: global block, flags seen
+    // Σ amounts of the lane's half (Σ1: 6 11 25 on e-lanes, Σ0: 2 13 22 on a-lanes)
+    const uint32_t sh1 = elane ? 6u : 2u, sh2 = elane ? 11u : 13u, sh3 = elane ? 25u : 22u;
+    const uint32_t M = elane ? 0u : ~0u;
+    const uint32_t one = 1u, zero = 0u;
+    constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    const uint32_t n = a.counts[a.lvl];
+    const uint32_t* lst = a.list + a.s;
+    for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+        const uint32_t i = base + jl;
+        bool has = i < n;
+        uint32_t p = has ? lst[i] : 0u;
+        uint32_t fslot = ~0u;
+        uint32_t maxnb;
+        {
+            const uint32_t il = base + lane;
+            uint32_t x = il < n ? a.meta[2ull * lst[il]].y : 0u;
+            for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+            maxnb = __builtin_amdgcn_readfirstlane(x);
+        }
+        uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
+        uint4 nt[8];
+        uint2 nr = make_uint2(0, 0);
+        uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+        uint32_t sk = 0;
+        while (maxnb) {
+            RF_STAMP_PL(sk); ++sk;
+            const bool fused = fslot != ~0u;
+            uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+            if (has) {
+                if (fused) {
+                    m0 = nm0;
+                    m1 = nm1;
+                    nm0 = nnm0;
+                    nm1 = nnm1;
+                } else {
+                    m0 = a.meta[2 * p];
+                    m1 = a.meta[2 * p + 1];
+                }
+            }
+            const bool nfu = has && m1.w != ~0u;
+            if (nfu && !fused) {
+                nm0 = a.meta[2ull * m1.w];
+                nm1 = a.meta[2ull * m1.w + 1];
+            }
+            MatCursor cur;
+            uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
+            uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+            if (!kStream && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+            if (wave == kProd && has) {
+                cur.fslot = fslot;
+                if (fused) {
+                    cur.flo = s_dig[lane][0];
+                    cur.fhi = s_dig[lane][1];
+                    cur.begin_pre(m0, reinterpret_cast<const uint4*>(a.tmpl), nt, nr, ring);
+                } else {
+                    cur.begin(a, m0, ring);
+                }
+            }
+            if (chain && has) {
+                if (fused) {
+                    olo = nolo;
+                    ohi = nohi;
+                    pre[0] = npre[0];
+                    pre[1] = npre[1];
+                } else {
+                    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+                    olo = od[0];
+                    ohi = od[1];
+                    if (m1.y < m1.z) pre[0] = a.cons[m1.y];
+                    if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+                }
+                if (nfu) {
+                    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
+                    nolo = od[0];
+                    nohi = od[1];
+                    if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
+                    if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
+                    if (nm1.w != ~0u) {
+                        nnm0 = a.meta[2ull * nm1.w];
+                        nnm1 = a.meta[2ull * nm1.w + 1];
+                    }
+                }
+            }
+            if (kW == 3 && wave == kExp && nfu && nm1.w != ~0u) {
+                nnm0 = a.meta[2ull * nm1.w];
+                nnm1 = a.meta[2ull * nm1.w + 1];
+            }
+            // the chain's lagged state: as after a block whose raw state is zero
+            // with chaining value IV (lag_chain.h / k1_sha256_duo)
+            uint32_t Hr0 = elane ? IV[4] : IV[0], Hr1 = elane ? IV[5] : IV[1];
+            uint32_t Hr2 = elane ? IV[6] : IV[2], Hr3 = elane ? IV[7] : IV[3];
+            uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
+            uint32_t Z = elane ? IV[7] + IV[3] : 0u, Y = 0;
+            uint32_t c63 = 0, c64 = elane ? IV[2] : 0u - IV[4], c65 = elane ? IV[1] : 0u - IV[3];
+            uint32_t t0, t1, t2, t3;
+            uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+            const uint32_t nbl = m0.y;  // this lane's job's blocks (0: no job)
+            // one block step of the chain over block b's rows (group 0 first
+            // finishes block b-1: feed-forward, the a-half's last two rounds)
+            // b: the job's block (capture rule), bufb: its row buffer (kStream:
+            // the global block gb, whose chunks it waits for)
+            auto chain_block = [&](uint32_t b, uint32_t bufb, bool full) {
+                if (kStream && full) known = lds_poll(&s_prod, 4 * bufb + 1, known);
+                if (kStream && full && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                const uint32_t row_off = (((bufb & 1) * 64 + jl) * kPcRow) * 4, ones_off = 128 * kPcRow * 4;
+                const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
+                                                                 ((M & ones_off) | (~M & row_off)));
+                uint4 v = r4[0], vn = r4[1];
+                {
+                    const uint32_t k1 = v.y + c64, k2 = v.z + c65;
+                    asm volatile(RF_L2_GROUP0
+                                 : RF_LAG_STATE, RF_L2_TMP, RF_LAG_H,
+                                   [c63] "=&v"(c63), [c64] "+v"(c64), [c65] "+v"(c65)
+                                 : RF_L2_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one),
+                                   [zero] "v"(zero));
+                }
+                if (b == nbl) {  // the job's final chaining value
+                    D0 = Hr0; D1 = Hr1; D2 = Hr2; D3 = Hr3;
+                }
+                if (!full) return;
+                v = vn;
+                vn = r4[2];
+#pragma unroll
+                for (int g = 1; g < 16; ++g) {
+                    uint4 vnn = vn;
+                    if (kStream && (g == 2 || g == 6 || g == 10)) {  // r4[g + 2] opens chunk (g + 2) / 4
+                        known = lds_poll(&s_prod, 4 * bufb + (g + 2) / 4 + 1, known);
+                        if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                    }
+                    if (g < 14) vnn = r4[g + 2];
+                    const uint32_t k4 = g == 15 ? c63 : vn.x;
+                    asm volatile(RF_L2_GROUP : RF_LAG_STATE, RF_L2_TMP : RF_L2_IN(v.y, v.z, v.w, k4));
+                    v = vn;
+                    vn = vnn;
+                }
+            };
+            if constexpr (kStream) {
+                if (wave == kProd) {
+                    for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
+                        if (gb >= 2) {  // row buffer gb & 1: both chain waves past block gb - 2
+                            known_c0 = lds_poll(&s_cons[0], gb - 1, known_c0);
+                            known_c1 = lds_poll(&s_cons[1], gb - 1, known_c1);
+                        }
+                        const bool mine = b < m0.y;
+                        if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                        uint32_t w[16];
+                        if (mine) cur.block(a, b, ring, w);
+                        uint4* row = reinterpret_cast<uint4*>(&kw[((gb & 1) * 64 + lane) * kPcRow]);
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            if (mine) kw_expand_chunk(w, row, c);
+                            if (c == 0)  // the chain starts on it: publish at once
+                                lds_publish(&s_prod, 4 * gb + 1, lane);
+                            else if (c >= 2)  // chunk c - 1, its writes drained behind chunk c's
+                                lds_publish_prev(&s_prod, 4 * gb + c, lane);
+                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                        }
+                        lds_publish(&s_prod, 4 * gb + 4, lane);
+                        if (b == 0 && nfu) {
+                            const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
+                            nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
+                            if (nm0.y > 1) {
+                                nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
+                            }
+                            nr = a.holes[nm0.z];
+                            if (nm1.w != ~0u) {
+                                nnm0 = a.meta[2ull * nm1.w];
+                                nnm1 = a.meta[2ull * nm1.w + 1];
+                            }
+                        }
+                        RF_STAMP_PL(sk); ++sk;
+                    }
+                } else {
+                    for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
+                        chain_block(b, gb, true);
+                        lds_publish(&s_cons[wave], gb + 1, lane);
+                        RF_STAMP_PL(sk); ++sk;
+                    }
+                }
+            } else {
+            for (uint32_t it = 0; it < maxnb + lag; ++it) {
+                if (wave == kProd) {
+                    if (it < m0.y) {
+                        uint32_t w[16];
+                        cur.block(a, it, ring, w);
+                        if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
+                        if (kW == 2) {
+                            kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
+                        } else {
+                            uint4* row = reinterpret_cast<uint4*>(&wbuf[((it & 1) * 64 + lane) * kWRow]);
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                row[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+                        }
+                    }
+                    if (it == 0 && nfu) {
+                        const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
+                        nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
+                        if (nm0.y > 1) {
+                            nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
+                        }
+                        nr = a.holes[nm0.z];
+                        if (nm1.w != ~0u) {
+                            nnm0 = a.meta[2ull * nm1.w];
+                            nnm1 = a.meta[2ull * nm1.w + 1];
+                        }
+                    }
+                } else if (kW == 3 && wave == kExp) {
+                    if (it >= 1 && it - 1 < m0.y) {
+                        const uint32_t bb = (it - 1) & 1;
+                        const uint4* row = reinterpret_cast<const uint4*>(&wbuf[(bb * 64 + lane) * kWRow]);
+                        uint32_t w[16];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint4 v = row[q];
+                            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+                        }
+                        kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(bb * 64 + lane) * kPcRow]));
+                    }
+                } else if (chain && it >= lag) {
+                    chain_block(it - lag, it - lag, true);
+                }
+                lds_barrier();
+                RF_STAMP_PL(sk); ++sk;
+            }
+            }
+            bool changed = false;
+            const bool own = chain && has && elane;
+            if (chain) {
+                chain_block(maxnb, kStream ? gb : maxnb, false);  // group 0 of block maxnb: the longest jobs' final value
+                // the a-lane's half (H0..H3) into its e-lane (H4..H7 there)
+                ShaState st;
+                st.h[0] = __builtin_amdgcn_mov_dpp((int)D0, 0x141, 0xf, 0xf, true);
+                st.h[1] = __builtin_amdgcn_mov_dpp((int)D1, 0x141, 0xf, 0xf, true);
+                st.h[2] = __builtin_amdgcn_mov_dpp((int)D2, 0x141, 0xf, 0xf, true);
+                st.h[3] = __builtin_amdgcn_mov_dpp((int)D3, 0x141, 0xf, 0xf, true);
+                st.h[4] = D0; st.h[5] = D1; st.h[6] = D2; st.h[7] = D3;
+                uint32_t next = ~0u, nbn = 0;
+                if (own) {
+                    changed = finish_job_pre(a, m1, st, olo, ohi);
+                    if (changed && m1.w != ~0u) {
+                        next = m1.w;
+                        nbn = nm0.y;
+                        s_dig[jl][0] = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
+                                                  bswap32(st.h[3]));
+                        s_dig[jl][1] = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]),
+                                                  bswap32(st.h[7]));
+                    }
+                }
+                if (elane) {
+                    s_next[jl] = next;
+                    s_nb[jl] = nbn;
+                }
+            }
+            RF_STAMP_PL(sk); ++sk;
+            lds_barrier();
+            RF_STAMP_PL(sk); ++sk;
+            const uint32_t nx = s_next[jl];
+            {
+                uint32_t x = s_nb[lane];
+                for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+                maxnb = __builtin_amdgcn_readfirstlane(x);
+            }
+            if (chain) {
+                uint32_t cb = 0, ce = 0;
+                if (own) {
+                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                    cb = m1.y;
+                    ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
+                }
+                propagate_pre(a, cb, ce, pre);
+                const uint64_t fb = __ballot(own && nx != ~0u);
+                if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
+            }
+            fslot = has ? m1.x : ~0u;
+            has = nx != ~0u;
+            p = has ? nx : 0u;
+        }
+    }
+}
+
 // set_slots: write input digests; a changed slot queues its consumers.
 __global__ __launch_bounds__(256) void k3_mark_slots(const uint32_t* __restrict__ sl,
                                                      const uint8_t* __restrict__ dig, uint32_t n,
@@ -713,7 +1102,8 @@ hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, con
 hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s) {
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
-    static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u : 0u;
+    // RF_DBG_HASH2: hash twice (k2_level); RF_K2_STAMPS=2: per-chunk stamps (k2_level_pl)
+    static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u : 0u;
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps};
     // incremental: the dirty count is only known on device; 1024 blocks (4
@@ -726,10 +1116,29 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         if (!g.inc_level[lvl]) return hipSuccess;  // every job of the level is a fusion target
         uint64_t wg = (e - b + 63) / 64;
         if (wg > 2048) wg = 2048;
-        if (g.inc_level[lvl] == 2)
+        // RF_K2_CHAIN=14: the one-lane chain (k2_level_pc), for A/B runs
+        static const bool one_lane = [] {
+            const char* v = getenv("RF_K2_CHAIN");
+            return v && atoi(v) == 14;
+        }();
+        const bool wide = g.inc_level[lvl] == 2;
+        // RF_K2_STREAM=1: the streamed hand-over (measured no faster on
+        // configs[2]: the producer serializes a fused job's blocks 0 and 1,
+        // DESIGN.md §5); default per-block barriers
+        static const bool no_stream = [] {
+            const char* v = getenv("RF_K2_STREAM");
+            return !(v && atoi(v) == 1);
+        }();
+        if (one_lane && wide)
             hipLaunchKernelGGL(k2_level_pc<3>, dim3((uint32_t)wg), dim3(192), 0, s, a);
-        else
+        else if (one_lane)
             hipLaunchKernelGGL(k2_level_pc<2>, dim3((uint32_t)wg), dim3(128), 0, s, a);
+        else if (wide)
+            hipLaunchKernelGGL((k2_level_pl<3, false>), dim3((uint32_t)wg), dim3(256), 0, s, a);
+        else if (no_stream)
+            hipLaunchKernelGGL((k2_level_pl<2, false>), dim3((uint32_t)wg), dim3(192), 0, s, a);
+        else
+            hipLaunchKernelGGL((k2_level_pl<2, true>), dim3((uint32_t)wg), dim3(192), 0, s, a);
         return hipGetLastError();
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);

@@ -21,6 +21,7 @@
 namespace rf {
 
 constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr uint32_t kMaxProbe = 1u << 16;
 
 __device__ __forceinline__ bool dig_eq(const uint4& alo, const uint4& ahi, const uint8_t* b) {
     const uint4* q = reinterpret_cast<const uint4*>(b);
@@ -39,12 +40,27 @@ __global__ __launch_bounds__(256) void k5_dedup_insert(const uint8_t* __restrict
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint4* d = reinterpret_cast<const uint4*>(dig + 32ull * i);
         const uint4 lo = d[0], hi = d[1];
-        uint32_t slot = lo.x & mask;
-        for (;;) {
+        // slot from four words of the digest: inputs that share a prefix
+        // (not SHA-256 output, or adversarial) still spread over the table
+        uint32_t slot = ((lo.x ^ __builtin_rotateleft32(lo.z, 13) ^ hi.y ^ __builtin_rotateleft32(hi.w, 7)) *
+                         0x9E3779B1u) & mask;
+        // bounded probing: the table is >= 2n slots (load <= 1/2), where
+        // linear probing's runs are a few slots long; the bound guarantees
+        // that every wave exits, and a batch that hits it is flagged
+        uint32_t probes = 0;
+        for (;; ++probes) {
+            if (probes >= kMaxProbe) {
+                slot = kEmpty;
+                break;
+            }
             uint32_t cur = __hip_atomic_load(&table[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (cur == kEmpty) {
                 cur = atomicCAS(&table[slot], kEmpty, i);
                 if (cur == kEmpty) break;  // claimed: this node opens its class
+            }
+            if (cur >= n) {  // not an index of this batch: the table was not cleared
+                slot = kEmpty;
+                break;
             }
             if (dig_eq(lo, hi, dig + 32ull * cur)) {
                 if (i < cur) atomicMin(&table[slot], i);
@@ -65,7 +81,13 @@ __global__ __launch_bounds__(256) void k5_dedup_resolve(uint32_t n, const uint32
     __shared__ uint32_t s_w[4];
     uint32_t uniq = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t c = table[slot_of[i]];
+        const uint32_t so = slot_of[i];
+        if (so == kEmpty) {  // insert gave up (see k5_dedup_insert): flag the batch
+            canon[i] = kEmpty;
+            atomicOr(n_unique, 0x80000000u);
+            continue;
+        }
+        const uint32_t c = table[so];
         canon[i] = c;
         uniq += c == i;
     }

@@ -98,6 +98,35 @@ def test_dedup_probe_collisions_and_hot_class(ctx):
     assert (canon == 0).all() and nu == 1
 
 
+@pytest.mark.gpu
+def test_dedup_device_repeated_calls(ctx):
+    """The device form, called back to back on the context's stream and then
+    on another stream (the context's scratch is handed between streams in
+    stream order): every call gives first-occurrence classes."""
+    from reflow_amd import capi
+    rng = np.random.default_rng(11)
+    n = 2_000_000
+    d = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    d[n // 2:n // 2 + 20000] = d[:20000]
+    d[-5000:] = d[100:5100]
+    want = _first_occurrence(d)
+    dd = ctx.upload(d)
+    canon, nu = ctx.alloc(4 * n), ctx.alloc(64)
+    for k in range(4):
+        ctx.dedup_digests_device(dd.ptr, n, canon.ptr, nu.ptr)
+        ctx.sync()
+        got_nu = int(nu.to_numpy()[:4].view(np.uint32)[0])
+        assert got_nu == len(np.unique(want)), (k, hex(got_nu))
+        assert (canon.to_numpy().view(np.uint32) == want).all(), k
+    c2 = capi.Context(0, host_threads=0)
+    ctx.dedup_digests_device(dd.ptr, n, canon.ptr, nu.ptr, stream=c2.stream)
+    c2.sync()
+    assert (canon.to_numpy().view(np.uint32) == want).all()
+    c2.close()
+    for x in (dd, canon, nu):
+        x.free()
+
+
 def _gpu_canonical(ctx, top, v1):
     from reflow_amd import capi
     post = _postorder(top)

@@ -16,9 +16,12 @@ def main():
     ap.add_argument("--dag-pairs", type=int, default=32)
     ap.add_argument("--dag-steps", type=int, default=20)
     a = ap.parse_args()
+    import faulthandler
+    faulthandler.dump_traceback_later(80, exit=True)  # a stuck run names its line
     dist = bench.Dist(1)
-    ctx = capi.Context(0)
-    r, _ = bench.bench_dag(a, dist, ctx, None)
+    ctx = capi.Context(0, host_threads=0)
+    r = bench.bench_dag(a, dist, ctx, None, bench.Budget(600))
+    r.pop("_cpu", None)
     print(json.dumps(r), flush=True)
     ctx.close()
 
