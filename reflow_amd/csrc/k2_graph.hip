@@ -565,8 +565,10 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
 // and is ignored): a job's digest is its chaining value after group 0 of
 // block nb (the k1_sha256_octo rule), combined into the e-lane with one
 // mirror move per word.  Block counts differ between the waves' job sets,
-// so the iteration count comes from LDS: s_nb[j] = the fused target's block
-// count, published with s_next at the hand-over.
+// so the iteration count comes from LDS: s_nbx[j] = the fused target's block
+// count, published with s_next at the hand-over and max-reduced by every
+// wave (six shuffles; an LDS atomicMax into one word measured 10 us per step
+// slower: 32 lanes per wave serialise on it).
 // stamps (RF_K2_STAMPS): workgroup 0's chain wave 0 (row 0) and producer (row 1)
 #define RF_STAMP_PL(k)                                                                                \
     do {                                                                                              \
@@ -574,13 +576,18 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
             a.stamps[128 * a.lvl + 64 * (wave != 0) + (k)] = __builtin_amdgcn_s_memrealtime();        \
     } while (0)
 
-// Streamed hand-over (kStream, kW = 2): no per-block barrier.  The producer
-// publishes K+W rows in 16-word chunks -- s_prod counts chunks written over
-// the workgroup's life (block gb's chunk c: 4 gb + c + 1) -- and the chain
-// waits for exactly the chunk its next LDS read needs, so a fused job's
-// block 0 starts right after its assembly instead of after its whole
-// expansion; s_cons[c] counts blocks chain wave c has finished, and the
-// producer reuses a row buffer only once both chain waves are past it.
+// Streamed hand-over (kStream, kW = 2): no per-block barrier.  Blocks get
+// workgroup-wide ids (consecutive over the launch; both waves count them the
+// same way) and live in a ring of three LDS row buffers, id % 3.  The
+// producer publishes a block's K+W rows in 16-word chunks -- s_flag[buffer]
+// = 4 id + chunks written -- and the chain waits for exactly the chunk its
+// next LDS read needs, so a fused job's block 0 starts right after its
+// assembly, not after its whole expansion.  s_cons[c] = 1 + the last id
+// chain wave c finished; the producer writes id only once both are >= id - 2.
+// While the chain hashes a job's last block the producer is idle: it then
+// builds the fusion target's block 1 (id + 1 of the next job) when that block
+// is template-only (the fused hole ends in block 0: every 1000align link), so
+// the next link's chain runs its blocks 0 and 1 back to back.
 // Flags are written after s_waitcnt lgkmcnt(0) (the rows are in LDS) and
 // polled with s_sleep; no global-memory wait is involved.
 __device__ __forceinline__ uint32_t lds_poll(volatile uint32_t* flag, uint32_t need, uint32_t known) {
@@ -626,19 +633,33 @@ __device__ __forceinline__ void kw_expand_chunk(uint32_t (&w)[16], uint4* row, i
     }
 }
 
+// Workgroup-uniform max of a lane value that is usually small (block counts):
+// count up with ballots -- a compare and a scalar branch per step -- instead
+// of six dependent ds_bpermute shuffles; shuffles above 64.
+__device__ __forceinline__ uint32_t wave_max_small(uint32_t x) {
+    uint32_t m = 0;
+    while (m < 64 && __any(x > m)) ++m;
+    if (m == 64) {
+        for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+        m = x;
+    }
+    return __builtin_amdgcn_readfirstlane(m);
+}
+
 template <uint32_t kW, bool kStream>
 __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     static_assert(kW == 2 || kW == 3, "producer (+ expander)");
     static_assert(!kStream || kW == 2, "streamed hand-over: producer + chain only");
     constexpr uint32_t lag = kW - 1;
     constexpr uint32_t kProd = 2, kExp = 3;  // wave roles: 0, 1 chain
-    __shared__ __attribute__((aligned(16))) uint32_t kw[(2 * 64 + 1) * kPcRow];  // + the a-lanes' k row
+    constexpr uint32_t kBufs = kStream ? 3 : 2;  // row buffers of 64 rows
+    __shared__ __attribute__((aligned(16))) uint32_t kw[(kBufs * 64 + 1) * kPcRow];  // + the a-lanes' k row
     __shared__ __attribute__((aligned(16))) uint32_t wbuf[kW == 3 ? 2 * 64 * kWRow : 4];
     __shared__ uint32_t ring_all[64 * kRing];
     __shared__ uint4 s_dig[64][2];
     __shared__ uint32_t s_next[64];
-    __shared__ uint32_t s_nb[64];
-    __shared__ uint32_t s_prod, s_cons[2];
+    __shared__ uint32_t s_flag[3], s_cons[2];
+    __shared__ uint32_t s_nbx[64];  // fused targets' block counts (the next iteration's max)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* ring = &ring_all[lane * kRing];
@@ -648,7 +669,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     const uint32_t ep = elane ? hp : ((hp & 8) | (7 - (hp & 7)));
     const uint32_t jl = wave < 2 ? 32 * wave + 8 * (lane >> 4) + ((ep & 3) | ((ep >> 3) << 2)) : lane;
     const bool chain = wave < 2;
-    uint32_t* const ones = &kw[128 * kPcRow];
+    uint32_t* const ones = &kw[kBufs * 64 * kPcRow];
     if (wave == 0) {
         __builtin_amdgcn_s_setprio(3);
         ones[lane] = lane ? 1u : 0u;
@@ -656,11 +677,19 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     }
     if (wave == 1) __builtin_amdgcn_s_setprio(3);
     if (threadIdx.x == 0) {
-        s_prod = 0;
+        s_flag[0] = s_flag[1] = s_flag[2] = 0;
         s_cons[0] = s_cons[1] = 0;
     }
     lds_barrier();
-    uint32_t gb = 0, known = 0, known_c0 = 0, known_c1 = 0;  // streamed: global block, flags seen
+    // streamed: next block id, flags seen, a pre-built block 1 of the next job
+    uint32_t gb = 0, known = 0, known_c0 = 0, known_c1 = 0, pre_id = ~0u;
+    // (producer) a pre-built block the next job did not use -- it had one
+    // block, or there was none -- must not stay published: its id is the next
+    // job's block 0 (or later), whose rows are not written yet
+    auto drop_pre = [&]() {
+        if (pre_id != ~0u && pre_id >= gb) lds_publish(&s_flag[pre_id % 3], 4 * pre_id, lane);
+        pre_id = ~0u;
+    };
     // Σ amounts of the lane's half (Σ1: 6 11 25 on e-lanes, Σ0: 2 13 22 on a-lanes)
     const uint32_t sh1 = elane ? 6u : 2u, sh2 = elane ? 11u : 13u, sh3 = elane ? 25u : 22u;
     const uint32_t M = elane ? 0u : ~0u;
@@ -677,9 +706,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         uint32_t maxnb;
         {
             const uint32_t il = base + lane;
-            uint32_t x = il < n ? a.meta[2ull * lst[il]].y : 0u;
-            for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
-            maxnb = __builtin_amdgcn_readfirstlane(x);
+            maxnb = wave_max_small(il < n ? a.meta[2ull * lst[il]].y : 0u);
         }
         uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
         uint4 nt[8];
@@ -764,9 +791,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             // b: the job's block (capture rule), bufb: its row buffer (kStream:
             // the global block gb, whose chunks it waits for)
             auto chain_block = [&](uint32_t b, uint32_t bufb, bool full) {
-                if (kStream && full) known = lds_poll(&s_prod, 4 * bufb + 1, known);
+                const uint32_t bi = kStream ? bufb % 3 : (bufb & 1);
+                if (kStream && full) known = lds_poll(&s_flag[bi], 4 * bufb + 1, 4 * bufb);
                 if (kStream && full && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
-                const uint32_t row_off = (((bufb & 1) * 64 + jl) * kPcRow) * 4, ones_off = 128 * kPcRow * 4;
+                const uint32_t row_off = ((bi * 64 + jl) * kPcRow) * 4, ones_off = kBufs * 64 * kPcRow * 4;
                 const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
                                                                  ((M & ones_off) | (~M & row_off)));
                 uint4 v = r4[0], vn = r4[1];
@@ -788,7 +816,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 for (int g = 1; g < 16; ++g) {
                     uint4 vnn = vn;
                     if (kStream && (g == 2 || g == 6 || g == 10)) {  // r4[g + 2] opens chunk (g + 2) / 4
-                        known = lds_poll(&s_prod, 4 * bufb + (g + 2) / 4 + 1, known);
+                        known = lds_poll(&s_flag[bi], 4 * bufb + (g + 2) / 4 + 1, known);
                         if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                     }
                     if (g < 14) vnn = r4[g + 2];
@@ -801,25 +829,27 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             if constexpr (kStream) {
                 if (wave == kProd) {
                     for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
-                        if (gb >= 2) {  // row buffer gb & 1: both chain waves past block gb - 2
-                            known_c0 = lds_poll(&s_cons[0], gb - 1, known_c0);
-                            known_c1 = lds_poll(&s_cons[1], gb - 1, known_c1);
+                        if (gb == pre_id) continue;  // built during the previous job, flag published
+                        if (gb >= 3) {  // buffer gb % 3: both chain waves past block gb - 3
+                            known_c0 = lds_poll(&s_cons[0], gb - 2, known_c0);
+                            known_c1 = lds_poll(&s_cons[1], gb - 2, known_c1);
                         }
-                        const bool mine = b < m0.y;
                         if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                        const bool mine = b < m0.y;
                         uint32_t w[16];
                         if (mine) cur.block(a, b, ring, w);
-                        uint4* row = reinterpret_cast<uint4*>(&kw[((gb & 1) * 64 + lane) * kPcRow]);
+                        volatile uint32_t* fl = &s_flag[gb % 3];
+                        uint4* row = reinterpret_cast<uint4*>(&kw[((gb % 3) * 64 + lane) * kPcRow]);
 #pragma unroll
                         for (int c = 0; c < 4; ++c) {
                             if (mine) kw_expand_chunk(w, row, c);
                             if (c == 0)  // the chain starts on it: publish at once
-                                lds_publish(&s_prod, 4 * gb + 1, lane);
+                                lds_publish(fl, 4 * gb + 1, lane);
                             else if (c >= 2)  // chunk c - 1, its writes drained behind chunk c's
-                                lds_publish_prev(&s_prod, 4 * gb + c, lane);
+                                lds_publish_prev(fl, 4 * gb + c, lane);
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                         }
-                        lds_publish(&s_prod, 4 * gb + 4, lane);
+                        lds_publish(fl, 4 * gb + 4, lane);
                         if (b == 0 && nfu) {
                             const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
                             nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
@@ -833,6 +863,29 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             }
                         }
                         RF_STAMP_PL(sk); ++sk;
+                    }
+                    // idle until the hand-over: build the fusion targets' block 1
+                    // (the next job's second id) if every lane whose target has
+                    // a block 1 can -- it holds no hole (the fused digest ends
+                    // in block 0) and the target has exactly two blocks
+                    const bool need = nfu && nm0.y >= 2;
+                    const bool can = nm0.y == 2 && nr.x + 32 <= 64;
+                    drop_pre();
+                    if (__any(need) && __all(!need || can)) {
+                        const uint32_t id1 = gb + 1;
+                        known_c0 = lds_poll(&s_cons[0], id1 - 2, known_c0);
+                        known_c1 = lds_poll(&s_cons[1], id1 - 2, known_c1);
+                        uint4* row = reinterpret_cast<uint4*>(&kw[((id1 % 3) * 64 + lane) * kPcRow]);
+                        if (need) {
+                            uint32_t w[16] = {nt[4].x, nt[4].y, nt[4].z, nt[4].w, nt[5].x, nt[5].y, nt[5].z, nt[5].w,
+                                              nt[6].x, nt[6].y, nt[6].z, nt[6].w, nt[7].x, nt[7].y, nt[7].z, nt[7].w};
+#pragma unroll
+                            for (int q = 0; q < 16; ++q) w[q] = bswap32(w[q]);
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) kw_expand_chunk(w, row, c);
+                        }
+                        lds_publish(&s_flag[id1 % 3], 4 * id1 + 4, lane);
+                        pre_id = id1;
                     }
                 } else {
                     for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
@@ -913,18 +966,14 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 }
                 if (elane) {
                     s_next[jl] = next;
-                    s_nb[jl] = nbn;
+                    s_nbx[jl] = nbn;
                 }
             }
             RF_STAMP_PL(sk); ++sk;
             lds_barrier();
             RF_STAMP_PL(sk); ++sk;
             const uint32_t nx = s_next[jl];
-            {
-                uint32_t x = s_nb[lane];
-                for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
-                maxnb = __builtin_amdgcn_readfirstlane(x);
-            }
+            maxnb = wave_max_small(s_nbx[lane]);
             if (chain) {
                 uint32_t cb = 0, ce = 0;
                 if (own) {
@@ -940,6 +989,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             has = nx != ~0u;
             p = has ? nx : 0u;
         }
+        if (kStream && wave == kProd) drop_pre();
     }
 }
 
@@ -1129,16 +1179,23 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_STREAM");
             return !(v && atoi(v) == 1);
         }();
+        // RF_K2_PAD_KB: dynamic LDS per workgroup on top of the static arrays
+        // (A/B: enough to keep a second workgroup off the CU, so no wave
+        // shares a SIMD with another workgroup's prioritised chain wave)
+        static const uint32_t pad = [] {
+            const char* v = getenv("RF_K2_PAD_KB");
+            return v ? (uint32_t)atoi(v) * 1024u : 0u;
+        }();
         if (one_lane && wide)
-            hipLaunchKernelGGL(k2_level_pc<3>, dim3((uint32_t)wg), dim3(192), 0, s, a);
+            hipLaunchKernelGGL(k2_level_pc<3>, dim3((uint32_t)wg), dim3(192), pad, s, a);
         else if (one_lane)
-            hipLaunchKernelGGL(k2_level_pc<2>, dim3((uint32_t)wg), dim3(128), 0, s, a);
+            hipLaunchKernelGGL(k2_level_pc<2>, dim3((uint32_t)wg), dim3(128), pad, s, a);
         else if (wide)
-            hipLaunchKernelGGL((k2_level_pl<3, false>), dim3((uint32_t)wg), dim3(256), 0, s, a);
+            hipLaunchKernelGGL((k2_level_pl<3, false>), dim3((uint32_t)wg), dim3(256), pad, s, a);
         else if (no_stream)
-            hipLaunchKernelGGL((k2_level_pl<2, false>), dim3((uint32_t)wg), dim3(192), 0, s, a);
+            hipLaunchKernelGGL((k2_level_pl<2, false>), dim3((uint32_t)wg), dim3(192), pad, s, a);
         else
-            hipLaunchKernelGGL((k2_level_pl<2, true>), dim3((uint32_t)wg), dim3(192), 0, s, a);
+            hipLaunchKernelGGL((k2_level_pl<2, true>), dim3((uint32_t)wg), dim3(192), pad, s, a);
         return hipGetLastError();
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
