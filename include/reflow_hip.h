@@ -368,6 +368,20 @@ int rf_bloom_load(rf_ctx *ctx, uint64_t m, uint64_t k, const uint64_t *words, ui
                   uint64_t length, rf_bloom **out);
 /* Go JSON wire form {"m":M,"k":K,"b":"<base64url(BE64 len ‖ BE64 words)>"} (bloom.go:264-286). */
 int rf_bloom_load_json(rf_ctx *ctx, const char *json, size_t len, rf_bloom **out);
+/* The liveset's wire forms on the host alone (no device; what the loaders
+ * above and the marshalers below use): parse into m, k, the bitset length
+ * and its wordsNeeded(length) words (*n_words; RF_EINVAL with *n_words set
+ * when cap_words is short), and format from host words (*out_len = bytes
+ * needed, RF_EINVAL when cap is short).  Malformed or truncated input is
+ * RF_EINVAL, never a read past len. */
+int rf_bloom_parse_binary(const uint8_t *buf, size_t len, uint64_t *m, uint64_t *k, uint64_t *length,
+                          uint64_t *words, uint64_t cap_words, uint64_t *n_words);
+int rf_bloom_parse_json(const char *json, size_t len, uint64_t *m, uint64_t *k, uint64_t *length,
+                        uint64_t *words, uint64_t cap_words, uint64_t *n_words);
+int rf_bloom_format_binary(uint64_t m, uint64_t k, uint64_t length, const uint64_t *words, uint64_t n_words,
+                           uint8_t *out, uint64_t cap, uint64_t *out_len);
+int rf_bloom_format_json(uint64_t m, uint64_t k, uint64_t length, const uint64_t *words, uint64_t n_words,
+                         uint8_t *out, uint64_t cap, uint64_t *out_len);
 /* Go binary wire form BE64 m ‖ BE64 k ‖ BE64 len ‖ BE64 words (bloom.go:290-325). */
 int rf_bloom_load_binary(rf_ctx *ctx, const uint8_t *buf, size_t len, rf_bloom **out);
 /* New empty filter with m bits and k hashes (bloom.New, bloom.go:81-83). */

@@ -39,7 +39,8 @@ EXPORTS = [
     "rf_timer_start", "rf_timer_stop", "rf_comm_unique_id", "rf_comm_init", "rf_comm_destroy",
     "rf_comm_allgather", "rf_comm_allreduce_or", "rf_memcpy_d2d", "rf_graph_gather_device",
     "rf_fileset_marshal_json", "rf_fileset_value_digest_batch",
-    "rf_bloom_marshal_json", "rf_bloom_marshal_binary", "rf_bloom_collect", "rf_bloom_collect_device",
+    "rf_bloom_marshal_json", "rf_bloom_marshal_binary", "rf_bloom_parse_binary", "rf_bloom_parse_json",
+    "rf_bloom_format_binary", "rf_bloom_format_json", "rf_bloom_collect", "rf_bloom_collect_device",
     "rf_dedup_digests", "rf_dedup_digests_device", "rf_assoc_lookup",
     "rf_assoc_new", "rf_assoc_destroy", "rf_assoc_put", "rf_assoc_get", "rf_assoc_get_device",
     "rf_assoc_get_abbrev", "rf_assoc_stats", "rf_assoc_put_device",

@@ -36,25 +36,9 @@
 #include "graph_internal.h"
 #include "host_sha.h"
 #include "reflow_hip.h"
+#include "wire.h"
 
 using namespace rf;
-
-// ---------------------------------------------------------------------------
-// errors (declared in ctx.h)
-static thread_local std::string g_err;
-
-int rf::fail(int code, const char* fmt, ...) {
-    char buf[1024];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    return code;
-}
-
-extern "C" const char* rf_last_error(void) { return g_err.c_str(); }
-extern "C" const char* rf_version(void) { return "reflow-hip 0.2 gfx950"; }
 
 extern "C" int rf_device_count(int* n) {
     ARG(n, "null out");
@@ -1201,159 +1185,18 @@ extern "C" int rf_install_entries(const rf_install* in, char* paths, uint64_t* p
 extern "C" void rf_install_destroy(rf_install* in) { delete in; }
 
 // ---------------------------------------------------------------------------
-// Fileset JSON: json.Marshal(Fileset) -> Repository.Put (eval.go:1961-1967),
-// the assoc value CacheWrite stores under every cache key (eval.go:1141).
-// Byte rules of Go 1.9/1.10 encoding/json (.travis.yml:3-5): struct fields
-// in declaration order with their tags (executor.go:25-38: "List" and
-// "Fileset", both omitempty, i.e. omitted when len == 0), map keys sorted
-// bytewise, strings escaped by encodeState.string with escapeHTML.
-static const char kHex[] = "0123456789abcdef";
-
-// Length of the valid UTF-8 sequence at s[i] (s[i] >= 0x80), 0 if invalid:
-// the acceptance ranges of unicode/utf8.DecodeRuneInString.
-static size_t utf8_seq(const uint8_t* s, size_t n, size_t i) {
-    const uint8_t b0 = s[i];
-    auto in = [&](size_t j, uint8_t lo, uint8_t hi) { return j < n && s[j] >= lo && s[j] <= hi; };
-    if (b0 >= 0xC2 && b0 <= 0xDF) return in(i + 1, 0x80, 0xBF) ? 2 : 0;
-    if (b0 >= 0xE0 && b0 <= 0xEF) {
-        const uint8_t lo = b0 == 0xE0 ? 0xA0 : 0x80, hi = b0 == 0xED ? 0x9F : 0xBF;
-        return in(i + 1, lo, hi) && in(i + 2, 0x80, 0xBF) ? 3 : 0;
-    }
-    if (b0 >= 0xF0 && b0 <= 0xF4) {
-        const uint8_t lo = b0 == 0xF0 ? 0x90 : 0x80, hi = b0 == 0xF4 ? 0x8F : 0xBF;
-        return in(i + 1, lo, hi) && in(i + 2, 0x80, 0xBF) && in(i + 3, 0x80, 0xBF) ? 4 : 0;
-    }
-    return 0;
-}
-
-static void json_string(std::string& o, const uint8_t* s, size_t n) {
-    o.push_back('"');
-    size_t i = 0;
-    while (i < n) {
-        const uint8_t b = s[i];
-        if (b < 0x80) {
-            switch (b) {
-                case '"': case '\\': o.push_back('\\'); o.push_back((char)b); break;
-                case '\n': o += "\\n"; break;
-                case '\r': o += "\\r"; break;
-                case '\t': o += "\\t"; break;
-                default:
-                    if (b < 0x20 || b == '<' || b == '>' || b == '&') {
-                        o += "\\u00";
-                        o.push_back(kHex[b >> 4]);
-                        o.push_back(kHex[b & 15]);
-                    } else {
-                        o.push_back((char)b);
-                    }
-            }
-            ++i;
-            continue;
-        }
-        const size_t len = utf8_seq(s, n, i);
-        if (len == 0) {  // utf8.RuneError of size 1: one replacement per bad byte
-            o += "\\ufffd";
-            ++i;
-        } else if (len == 3 && b == 0xE2 && s[i + 1] == 0x80 && (s[i + 2] == 0xA8 || s[i + 2] == 0xA9)) {
-            o += "\\u202";  // U+2028 / U+2029
-            o.push_back(kHex[s[i + 2] - 0xA0]);
-            i += 3;
-        } else {
-            o.append(reinterpret_cast<const char*>(s + i), len);
-            i += len;
-        }
-    }
-    o.push_back('"');
-}
-
-static int marshal_fileset(const rf_fileset_tree* t, uint32_t node, int depth, std::string& o,
-                           std::vector<uint64_t>& idx) {
-    if (node >= t->n_nodes) return fail(RF_EINVAL, "fileset node %u >= n_nodes %llu", node,
-                                        (unsigned long long)t->n_nodes);
-    if (depth > 4096) return fail(RF_EINVAL, "fileset tree deeper than 4096 (cycle?)");
-    const uint64_t lb = t->list_ptr[node], le = t->list_ptr[node + 1];
-    const uint64_t eb = t->entry_ptr[node], ee = t->entry_ptr[node + 1];
-    if (lb > le || eb > ee) return fail(RF_EINVAL, "fileset node %u: CSR not monotone", node);
-    o.push_back('{');
-    if (le > lb) {
-        o += "\"List\":[";
-        for (uint64_t c = lb; c < le; ++c) {
-            if (c > lb) o.push_back(',');
-            int rc = marshal_fileset(t, t->list_child[c], depth + 1, o, idx);
-            if (rc) return rc;
-        }
-        o.push_back(']');
-    }
-    if (ee > eb) {
-        if (le > lb) o.push_back(',');
-        o += "\"Fileset\":{";
-        const size_t base = idx.size();
-        for (uint64_t e = eb; e < ee; ++e) idx.push_back(e);
-        auto less = [&](uint64_t a, uint64_t b) {
-            const size_t la = t->path_lens[a], lb2 = t->path_lens[b];
-            const int c = memcmp(t->paths[a], t->paths[b], std::min(la, lb2));
-            return c < 0 || (c == 0 && la < lb2);
-        };
-        std::sort(idx.begin() + base, idx.end(), less);
-        for (size_t q = base; q < idx.size(); ++q) {
-            const uint64_t e = idx[q];
-            if (q > base && !less(idx[q - 1], e))
-                return fail(RF_EINVAL, "fileset node %u: duplicate map key", node);
-            const uint8_t* id = t->ids32 + 32 * e;
-            bool zero = true;
-            for (int k = 0; k < 32; ++k) zero &= id[k] == 0;
-            if (zero)  // digest.Digest's zero text form is grailbio/base's (unvendored)
-                return fail(RF_EINVAL, "fileset node %u: zero file ID has no pinned JSON form", node);
-            if (q > base) o.push_back(',');
-            json_string(o, reinterpret_cast<const uint8_t*>(t->paths[e]), t->path_lens[e]);
-            o += ":{\"ID\":\"sha256:";
-            for (int k = 0; k < 32; ++k) {
-                o.push_back(kHex[id[k] >> 4]);
-                o.push_back(kHex[id[k] & 15]);
-            }
-            o += "\",\"Size\":";
-            o += std::to_string((long long)t->sizes[e]);
-            o.push_back('}');
-        }
-        idx.resize(base);
-        o.push_back('}');
-    }
-    o.push_back('}');
-    return RF_OK;
-}
-
-static int check_tree(const rf_fileset_tree* t) {
-    ARG(t && t->list_ptr && t->entry_ptr, "null fileset tree");
-    const uint64_t nl = t->list_ptr[t->n_nodes], ne = t->entry_ptr[t->n_nodes];
-    ARG(nl == 0 || t->list_child, "null list_child");
-    ARG(ne == 0 || (t->paths && t->path_lens && t->ids32 && t->sizes), "null entry arrays");
-    return RF_OK;
-}
-
-extern "C" int rf_fileset_marshal_json(const rf_fileset_tree* t, uint32_t root, uint8_t* out,
-                                       uint64_t cap, uint64_t* out_len) {
-    int rc = check_tree(t);
-    if (rc) return rc;
-    ARG(out_len, "null out_len");
-    std::string o;
-    std::vector<uint64_t> idx;
-    if ((rc = marshal_fileset(t, root, 0, o, idx))) return rc;
-    *out_len = o.size();
-    if (o.size() > cap) return fail(RF_EINVAL, "output buffer too small: need %zu bytes", o.size());
-    if (!o.empty() && out) memcpy(out, o.data(), o.size());
-    return RF_OK;
-}
-
+// Fileset JSON marshal: wire.cpp (host-only)
 extern "C" int rf_fileset_value_digest_batch(rf_ctx* ctx, const rf_fileset_tree* t, const uint32_t* roots,
                                              uint64_t n, uint8_t* out32) {
     ARG(ctx && (n == 0 || (roots && out32)), "null argument");
     if (n == 0) return RF_OK;
-    int rc = check_tree(t);
+    int rc = fileset_check_tree(t);
     if (rc) return rc;
     std::string arena;
-    std::vector<uint64_t> offs(n), lens(n), idx;
+    std::vector<uint64_t> offs(n), lens(n);
     for (uint64_t i = 0; i < n; ++i) {
         offs[i] = arena.size();
-        if ((rc = marshal_fileset(t, roots[i], 0, arena, idx))) return rc;
+        if ((rc = fileset_marshal_append(t, roots[i], arena))) return rc;
         lens[i] = arena.size() - offs[i];
     }
     return rf_sha256_arena(ctx, reinterpret_cast<const uint8_t*>(arena.data()), offs.data(), lens.data(),
@@ -1773,8 +1616,8 @@ static int bloom_make(rf_ctx* ctx, uint64_t m, uint64_t k, const uint64_t* words
     ARG(ctx && out, "null argument");
     ARG(m >= 1, "bloom m must be >= 1 (location() divides by m)");
     ARG(k < (1ull << 31), "bloom k too large");
-    // bitset words needed for `length` bits (bitset.go:89-94)
-    const uint64_t need = (length + 63) / 64;
+    // bitset words needed for `length` bits (bitset.go:89-94), without wrapping
+    const uint64_t need = length / 64 + (length % 64 != 0);
     ARG(!words || nwords >= need, "fewer words than the bitset length needs");
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
@@ -1812,79 +1655,18 @@ extern "C" int rf_bloom_new(rf_ctx* ctx, uint64_t m, uint64_t k, rf_bloom** out)
     return bloom_make(ctx, std::max<uint64_t>(1, m), std::max<uint64_t>(1, k), nullptr, 0, m, out);
 }
 
-static uint64_t be64(const uint8_t* p) {
-    uint64_t v = 0;
-    for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
-    return v;
-}
-
-static int bloom_from_bitset_bytes(rf_ctx* ctx, uint64_t m, uint64_t k, const uint8_t* p, size_t n,
-                                   rf_bloom** out) {
-    ARG(n >= 8, "truncated bitset");
-    const uint64_t length = be64(p);
-    const uint64_t nw = (length + 63) / 64;
-    ARG((n - 8) / 8 >= nw, "truncated bitset words");
-    std::vector<uint64_t> w(nw);
-    for (uint64_t i = 0; i < nw; ++i) w[i] = be64(p + 8 + 8 * i);
-    return bloom_make(ctx, m, k, w.data(), nw, length, out);
-}
-
 extern "C" int rf_bloom_load_binary(rf_ctx* ctx, const uint8_t* buf, size_t len, rf_bloom** out) {
-    ARG(buf && len >= 16, "truncated bloom binary");
-    return bloom_from_bitset_bytes(ctx, be64(buf), be64(buf + 8), buf + 16, len - 16, out);
-}
-
-static int b64url_val(char c) {
-    if (c >= 'A' && c <= 'Z') return c - 'A';
-    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
-    if (c >= '0' && c <= '9') return c - '0' + 52;
-    if (c == '-') return 62;
-    if (c == '_') return 63;
-    return -1;
-}
-
-static bool json_uint(const std::string& s, const char* key, uint64_t* v) {
-    const std::string k = std::string("\"") + key + "\"";
-    size_t p = s.find(k);
-    if (p == std::string::npos) return false;
-    p = s.find(':', p + k.size());
-    if (p == std::string::npos) return false;
-    ++p;
-    while (p < s.size() && isspace((unsigned char)s[p])) ++p;
-    if (p >= s.size() || !isdigit((unsigned char)s[p])) return false;
-    uint64_t x = 0;
-    while (p < s.size() && isdigit((unsigned char)s[p])) x = x * 10 + (uint64_t)(s[p++] - '0');
-    *v = x;
-    return true;
+    uint64_t m = 0, k = 0, length = 0;
+    std::vector<uint64_t> w;
+    int rc = bloom_parse_binary(buf, len, &m, &k, &length, w);
+    return rc ? rc : bloom_make(ctx, m, k, w.data(), w.size(), length, out);
 }
 
 extern "C" int rf_bloom_load_json(rf_ctx* ctx, const char* json, size_t len, rf_bloom** out) {
-    ARG(json, "null json");
-    const std::string s(json, len);
-    uint64_t m = 0, k = 0;
-    ARG(json_uint(s, "m", &m) && json_uint(s, "k", &k), "bloom json: missing m or k");
-    size_t p = s.find("\"b\"");
-    ARG(p != std::string::npos, "bloom json: missing b");
-    p = s.find('"', s.find(':', p) + 1);
-    ARG(p != std::string::npos, "bloom json: b is not a string");
-    const size_t q = s.find('"', p + 1);
-    ARG(q != std::string::npos, "bloom json: unterminated b");
-    std::vector<uint8_t> bytes;
-    uint32_t acc = 0;
-    int nbits = 0;
-    for (size_t i = p + 1; i < q; ++i) {
-        const char c = s[i];
-        if (c == '=') break;
-        const int v = b64url_val(c);
-        ARG(v >= 0, "bloom json: bad base64url character");
-        acc = (acc << 6) | (uint32_t)v;
-        nbits += 6;
-        if (nbits >= 8) {
-            nbits -= 8;
-            bytes.push_back((uint8_t)(acc >> nbits));
-        }
-    }
-    return bloom_from_bitset_bytes(ctx, m, k, bytes.data(), bytes.size(), out);
+    uint64_t m = 0, k = 0, length = 0;
+    std::vector<uint64_t> w;
+    int rc = bloom_parse_json(json, len, &m, &k, &length, w);
+    return rc ? rc : bloom_make(ctx, m, k, w.data(), w.size(), length, out);
 }
 
 extern "C" void rf_bloom_destroy(rf_bloom* bl) {
@@ -1962,74 +1744,33 @@ extern "C" int rf_bloom_words(rf_bloom* bl, uint64_t* words, uint64_t nwords) {
 }
 
 // ---- Liveset wire formats out (bloom.go:264-301, bitset.go:623-702) ----------
-// The bitset's words in its binary form: BE64 length ‖ BE64 words, with
-// wordsNeeded(length) words (bitset.go:628-640).
-static int bloom_bitset_bytes(rf_bloom* bl, std::vector<uint8_t>& o) {
-    uint64_t length = 0;
-    HIPC(sync_copy(bl->ctx, &length, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
-    const uint64_t nw = (length + 63) / 64;
+// The bitset as the device holds it: its length and wordsNeeded(length)
+// words (bitset.go:628-640); the byte layout is wire.cpp's.
+static int bloom_host_words(rf_bloom* bl, uint64_t* length, std::vector<uint64_t>& w) {
+    HIPC(sync_copy(bl->ctx, length, bl->b.len_dev, 8, hipMemcpyDeviceToHost));
+    const uint64_t nw = (*length + 63) / 64;
     if (nw > bl->b.nwords) return fail(RF_EINVAL, "bitset length exceeds filter capacity");
-    std::vector<uint64_t> w(nw);
+    w.resize(nw);
     if (nw) HIPC(sync_copy(bl->ctx, w.data(), bl->b.words, 8 * nw, hipMemcpyDeviceToHost));
-    auto put = [&](uint64_t v) {
-        for (int i = 7; i >= 0; --i) o.push_back((uint8_t)(v >> (8 * i)));
-    };
-    put(length);
-    for (uint64_t x : w) put(x);
-    return RF_OK;
-}
-
-static int copy_out(const std::vector<uint8_t>& o, uint8_t* out, uint64_t cap, uint64_t* out_len) {
-    ARG(out_len, "null out_len");
-    *out_len = o.size();
-    if (o.size() > cap) return fail(RF_EINVAL, "output buffer too small: need %zu bytes", o.size());
-    if (!o.empty() && out) memcpy(out, o.data(), o.size());
     return RF_OK;
 }
 
 extern "C" int rf_bloom_marshal_binary(rf_bloom* bl, uint8_t* out, uint64_t cap, uint64_t* out_len) {
     ARG(bl, "null bloom");
     DevGuard dg(bl->ctx->device);
-    std::vector<uint8_t> o;
-    for (uint64_t v : {bl->b.m, bl->b.k})  // WriteTo: BE64 m ‖ BE64 k ‖ bitset
-        for (int i = 7; i >= 0; --i) o.push_back((uint8_t)(v >> (8 * i)));
-    int rc = bloom_bitset_bytes(bl, o);
-    return rc ? rc : copy_out(o, out, cap, out_len);
+    uint64_t length = 0;
+    std::vector<uint64_t> w;
+    int rc = bloom_host_words(bl, &length, w);
+    return rc ? rc : rf_bloom_format_binary(bl->b.m, bl->b.k, length, w.data(), w.size(), out, cap, out_len);
 }
 
 extern "C" int rf_bloom_marshal_json(rf_bloom* bl, uint8_t* out, uint64_t cap, uint64_t* out_len) {
     ARG(bl, "null bloom");
     DevGuard dg(bl->ctx->device);
-    std::vector<uint8_t> bits;
-    int rc = bloom_bitset_bytes(bl, bits);
-    if (rc) return rc;
-    // json.Marshal(bloomFilterJSON{m, k, b}) with b's MarshalJSON =
-    // json.Marshal(base64.URLEncoding.EncodeToString(bits)) (padded; the
-    // alphabet needs no JSON escaping)
-    static const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
-    std::string s = "{\"m\":" + std::to_string(bl->b.m) + ",\"k\":" + std::to_string(bl->b.k) + ",\"b\":\"";
-    size_t i = 0;
-    for (; i + 3 <= bits.size(); i += 3) {
-        const uint32_t v = (uint32_t)bits[i] << 16 | (uint32_t)bits[i + 1] << 8 | bits[i + 2];
-        s += A[v >> 18];
-        s += A[(v >> 12) & 63];
-        s += A[(v >> 6) & 63];
-        s += A[v & 63];
-    }
-    if (bits.size() - i == 1) {
-        const uint32_t v = (uint32_t)bits[i] << 16;
-        s += A[v >> 18];
-        s += A[(v >> 12) & 63];
-        s += "==";
-    } else if (bits.size() - i == 2) {
-        const uint32_t v = (uint32_t)bits[i] << 16 | (uint32_t)bits[i + 1] << 8;
-        s += A[v >> 18];
-        s += A[(v >> 12) & 63];
-        s += A[(v >> 6) & 63];
-        s += '=';
-    }
-    s += "\"}";
-    return copy_out(std::vector<uint8_t>(s.begin(), s.end()), out, cap, out_len);
+    uint64_t length = 0;
+    std::vector<uint64_t> w;
+    int rc = bloom_host_words(bl, &length, w);
+    return rc ? rc : rf_bloom_format_json(bl->b.m, bl->b.k, length, w.data(), w.size(), out, cap, out_len);
 }
 
 // ---- Repository.Collect over a batch of objects (repository/file/repository.go:304-327)

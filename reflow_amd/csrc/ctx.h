@@ -13,10 +13,7 @@
 #include "host_sha.h"
 #include "reflow_hip.h"
 
-namespace rf {
-// Sets the thread-local rf_last_error() message; returns code.
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-}  // namespace rf
+#include "errors.h"
 
 #define HIPC(x)                                                                                  \
     do {                                                                                         \
@@ -24,10 +21,6 @@ int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
         if (e_ != hipSuccess) return rf::fail(RF_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
     } while (0)
 
-#define ARG(cond, msg)                                       \
-    do {                                                     \
-        if (!(cond)) return rf::fail(RF_EINVAL, "%s", msg); \
-    } while (0)
 
 // ---------------------------------------------------------------------------
 // device buffers

@@ -1,6 +1,9 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
 
-    python tools/pmc_summary.py FETCH_DIR/x_counter_collection.csv WRITE_DIR/x_counter_collection.csv OUT.json
+    python tools/pmc_summary.py FETCH_DIR/x_counter_collection.csv WRITE_DIR/x_counter_collection.csv OUT.json [BENCH.json]
+
+BENCH.json (the profiled bench's stdout line) supplies the "workload" key
+bench.py matches before it uses these figures as its roofline `traffic`.
 
 FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB.  Per
 MI355X_MICROARCH.md (HBM / rocprofv3): on gfx950 FETCH_SIZE reads exactly
@@ -37,6 +40,10 @@ def main():
     f, w, out = sys.argv[1:4]
     F, W = load(f), load(w)
     res = {}
+    if len(sys.argv) > 4:
+        for line in open(sys.argv[4]):
+            if line.startswith("{"):
+                res["workload"] = json.loads(line)["config"]["workload"]
     for k in sorted(set(F) | set(W)):
         nf, vf, mf = F.get(k, [0, 0.0, 0.0])
         nw, vw, mw = W.get(k, [0, 0.0, 0.0])
@@ -52,6 +59,9 @@ def main():
                   "traffic_bytes_largest_launch": (mf * corr + mw) * 1024}
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
+        if k == "workload":
+            print("workload:", v)
+            continue
         print("%-36s traffic/launch %.4e B, largest launch %.4e B (fetch raw %.4e x%.0f, write %.4e)"
               % (k, v["traffic_bytes_per_launch"], v["traffic_bytes_largest_launch"], v["fetch_bytes_raw"],
                  v["fetch_correction"], v["write_bytes"]))
