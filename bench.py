@@ -80,11 +80,14 @@ class Budget:
         return True
 
 
-def pmc_traffic(kernel, workload):
+def pmc_traffic(kernel, workload, algo_bytes=None):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 --pmc
     FETCH_SIZE/WRITE_SIZE pass (tools/pmc_summary.py, corrected as
     MI355X_MICROARCH.md prescribes) -- only when that pass ran this same
-    workload (its "workload" key); None otherwise.  PMC counters cannot be read
+    workload (its "workload" key); None otherwise.  A kernel launched more
+    than once there (the hybrid step's duo launch on three files, the GPU-only
+    run's on 35) is matched to this launch by its algorithmic bytes: the
+    launch whose traffic is nearest in ratio.  PMC counters cannot be read
     inside this process."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
@@ -93,6 +96,10 @@ def pmc_traffic(kernel, workload):
             continue
         v = d.get("rf::" + kernel)
         if v:
+            launches = v.get("launch_traffic_bytes") or []
+            if algo_bytes and launches:
+                t = min(launches, key=lambda x: abs(np.log(max(x, 1.0) / algo_bytes)))
+                return t, os.path.relpath(path, ROOT)
             return v.get("traffic_bytes_largest_launch", v["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
     return None, None
 
@@ -266,8 +273,12 @@ def bench_sha(args, dist, ctx, budget):
     workload = ("configs[1]: %.1f GiB Fileset per GPU, %d files 4 KiB-2 GiB (98%% log-uniform 4 KiB-1 MiB, "
                 "2%% 64 MiB-2 GiB), SHA-256 of every file" % (lens.sum() / GiB, len(lens)))
     if roof:
-        traffic, tsrc = pmc_traffic(roof["kernel"], workload)
+        traffic, tsrc = pmc_traffic(roof["kernel"], workload, roof["bytes_per_launch"])
         roof["traffic"] = traffic
+        if traffic and traffic > 2 * roof["bytes_per_launch"]:
+            roof["traffic_note"] = ("FETCH_SIZE/WRITE_SIZE are device-wide over the launch window: in the hybrid step "
+                                    "they include the host leg's D2H stream of the largest files and the pair "
+                                    "kernel; the GPU-only launch (roofline_gpu_only) measures the duo kernel alone")
         roof["traffic_source"] = tsrc or "not measured in this process (rocprofv3 --pmc needs its own pass)"
         roof["legs"] = {name: {"ms": round(ms, 3), "messages": int(len(ids)), "bytes": float(lens[ids].sum())}
                         for name, ids, ms in legs}
@@ -301,7 +312,7 @@ def bench_sha(args, dist, ctx, budget):
         duo_ids = o2[:int(s2.n_solo)]
         r2 = kernel_roofline("k1_sha256_duo", lens, duo_ids, s2.last_ms_solo) if s2.n_solo else None
         if r2:
-            tr2, ts2 = pmc_traffic("k1_sha256_duo", workload)
+            tr2, ts2 = pmc_traffic("k1_sha256_duo", workload, r2["bytes_per_launch"])
             r2["traffic"], r2["traffic_source"] = tr2, ts2 or "not measured in this process"
         same = bool((out2.to_numpy() == out.to_numpy()).all())
         res["roofline_gpu_only"] = r2

@@ -17,22 +17,25 @@ import csv
 import json
 import sys
 
-WIDE_STREAM = {"rf::k1_sha256_duo", "rf::k1_sha256_octo", "rf::k1_sha256_solo", "rf::k1_sha256_lanes", "rf::k_gen_fill"}
+WIDE_STREAM = {"rf::k1_sha256_duo", "rf::k1_sha256_octo", "rf::k1_sha256_solo", "rf::k1_sha256_lanes",
+               "rf::k1_sha256_pair", "rf::k_gen_fill"}
 
 
 def load(path):
-    """kernel -> [dispatches, total KiB, largest dispatch's KiB]"""
-    per = collections.defaultdict(float)
+    """kernel -> [dispatches, total KiB, largest dispatch's KiB, [KiB per dispatch in order]]"""
+    per = collections.OrderedDict()
     for i, r in enumerate(csv.DictReader(open(path))):
         k = r["Kernel_Name"].split("(")[0]
         k = k[5:] if k.startswith("void ") else k
         k = k.split("<")[0]  # one entry per kernel template
-        per[(k, r.get("Dispatch_Id", i))] += float(r["Counter_Value"])
-    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
-    for (k, _), v in per.items():
+        key = (k, int(r.get("Dispatch_Id", i)))
+        per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0, []])
+    for (k, _), v in sorted(per.items(), key=lambda kv: kv[0][1]):
         agg[k][0] += 1
         agg[k][1] += v
         agg[k][2] = max(agg[k][2], v)
+        agg[k][3].append(v)
     return agg
 
 
@@ -45,8 +48,8 @@ def main():
             if line.startswith("{"):
                 res["workload"] = json.loads(line)["config"]["workload"]
     for k in sorted(set(F) | set(W)):
-        nf, vf, mf = F.get(k, [0, 0.0, 0.0])
-        nw, vw, mw = W.get(k, [0, 0.0, 0.0])
+        nf, vf, mf, lf = F.get(k, [0, 0.0, 0.0, []])
+        nw, vw, mw, lw = W.get(k, [0, 0.0, 0.0, []])
         fb = vf / max(nf, 1) * 1024
         wb = vw / max(nw, 1) * 1024
         corr = 2.0 if k in WIDE_STREAM else 1.0
@@ -56,7 +59,10 @@ def main():
         res[k] = {"calls": nf, "fetch_bytes_raw": fb, "fetch_bytes_corrected": fb * corr,
                   "fetch_correction": corr, "write_bytes": wb,
                   "traffic_bytes_per_launch": fb * corr + wb,
-                  "traffic_bytes_largest_launch": (mf * corr + mw) * 1024}
+                  "traffic_bytes_largest_launch": (mf * corr + mw) * 1024,
+                  # every launch in dispatch order (the fetch and write passes
+                  # run the same command, so their launches pair up in order)
+                  "launch_traffic_bytes": [(a * corr + b) * 1024 for a, b in zip(lf, lw)] if len(lf) == len(lw) else []}
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         if k == "workload":
