@@ -259,6 +259,39 @@ int rf_fileset_marshal_json(const rf_fileset_tree *t, uint32_t root, uint8_t *ou
 int rf_fileset_value_digest_batch(rf_ctx *ctx, const rf_fileset_tree *t, const uint32_t *roots,
                                   uint64_t n, uint8_t *out32);
 
+/* ---- Coalescing concurrent callers (SURVEY §8(b) "Threading") -----------
+ * The reference digests files in <=60 goroutines (local/executor.go:41,
+ * 522-538) and looks cache keys up in a goroutine per node (eval.go:402-411);
+ * called one request at a time, each would be its own tiny device batch.  A
+ * coalescer is a queue any number of threads call into: the first caller
+ * that finds no flush running becomes the flusher, waits up to max_wait_us
+ * (or until max_batch requests are queued), and runs ONE batched call --
+ * rf_sha256_batch, rf_bloom_probe or rf_assoc_get -- for everything queued;
+ * requests arriving meanwhile form the next batch.  Blocking calls (a cgo
+ * call per goroutine) and async tickets (submit, then poll or wait) share
+ * it.  A failed batch returns its status to every request in it. */
+enum { RF_COALESCE_SHA256 = 1, RF_COALESCE_PROBE = 2, RF_COALESCE_ASSOC_GET = 3 };
+typedef struct rf_coalescer rf_coalescer;
+typedef struct rf_coalesce_ticket rf_coalesce_ticket;
+/* target: the rf_bloom (PROBE) or rf_assoc (ASSOC_GET, with assoc_kind);
+ * NULL for SHA256. */
+int rf_coalescer_open(rf_ctx *ctx, int kind, void *target, int assoc_kind, uint64_t max_batch,
+                      uint64_t max_wait_us, rf_coalescer **out);
+void rf_coalescer_close(rf_coalescer *c); /* completes what is queued */
+int rf_coalesce_sha256(rf_coalescer *c, const uint8_t *msg, uint64_t len, uint8_t *out32);
+int rf_coalesce_probe(rf_coalescer *c, const uint8_t *digest32, uint8_t *contains);
+int rf_coalesce_assoc_get(rf_coalescer *c, const uint8_t *key32, uint8_t *val32, uint8_t *found);
+/* Async: msg and out32 must stay valid until the ticket is done. */
+int rf_coalesce_sha256_async(rf_coalescer *c, const uint8_t *msg, uint64_t len, uint8_t *out32,
+                             rf_coalesce_ticket **out);
+/* *done = 1 once out32 is written (returns its status); a poll that finds the
+ * queue idle flushes it. */
+int rf_coalesce_poll(rf_coalescer *c, rf_coalesce_ticket *t, int *done);
+int rf_coalesce_wait(rf_coalescer *c, rf_coalesce_ticket *t);
+void rf_coalesce_ticket_free(rf_coalescer *c, rf_coalesce_ticket *t); /* completes it first */
+/* Batches flushed, requests served, largest batch. */
+int rf_coalescer_stats(rf_coalescer *c, uint64_t *batches, uint64_t *requests, uint64_t *largest);
+
 /* ---- K2/K3: incremental digest DAG (Flow.Digest / CacheKeys) ------------
  * The host lowers a Flow graph (flow.go:653-802) into hash JOBS over digest
  * SLOTS.  Job j hashes a byte template (its digest material, flow.go:675-750

@@ -47,6 +47,9 @@ EXPORTS = [
     "rf_set_host_threads", "rf_host_info", "rf_assoc_repair",
     "rf_sha_streams_open", "rf_sha_streams_close", "rf_sha_streams_write", "rf_sha_streams_digest",
     "rf_sha_streams_len", "rf_sha_streams_verify", "rf_sha256_verify", "rf_flow_dirty",
+    "rf_coalescer_open", "rf_coalescer_close", "rf_coalesce_sha256", "rf_coalesce_probe", "rf_coalesce_assoc_get",
+    "rf_coalesce_sha256_async", "rf_coalesce_poll", "rf_coalesce_wait", "rf_coalesce_ticket_free",
+    "rf_coalescer_stats",
     "rf_graph_set_part", "rf_graph_recompute_part", "rf_graph_part_gathered", "rf_graph_split",
     "rf_graph_piece_free", "rf_graph_piece_desc", "rf_graph_piece_part", "rf_graph_piece_slots",
 ]
@@ -342,6 +345,16 @@ def lib():
             "rf_graph_piece_desc": ([vp, vp], i32), "rf_graph_piece_part": ([vp, vp], i32),
             "rf_graph_piece_slots": ([vp, vp, vp], i32),
             "rf_host_info": ([vp, vp, vp, vp], i32),
+            "rf_bloom_parse_binary": ([vp, u64, vp, vp, vp, vp, u64, vp], i32),
+            "rf_bloom_parse_json": ([vp, u64, vp, vp, vp, vp, u64, vp], i32),
+            "rf_bloom_format_binary": ([u64, u64, u64, vp, u64, vp, u64, vp], i32),
+            "rf_bloom_format_json": ([u64, u64, u64, vp, u64, vp, u64, vp], i32),
+            "rf_coalescer_open": ([vp, i32, vp, i32, u64, u64, vp], i32), "rf_coalescer_close": ([vp], None),
+            "rf_coalesce_sha256": ([vp, vp, u64, vp], i32), "rf_coalesce_probe": ([vp, vp, vp], i32),
+            "rf_coalesce_assoc_get": ([vp, vp, vp, vp], i32),
+            "rf_coalesce_sha256_async": ([vp, vp, u64, vp, vp], i32),
+            "rf_coalesce_poll": ([vp, vp, vp], i32), "rf_coalesce_wait": ([vp, vp], i32),
+            "rf_coalesce_ticket_free": ([vp, vp], None), "rf_coalescer_stats": ([vp, vp, vp, vp], i32),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -917,6 +930,66 @@ class Bloom:
             self.close()
         except Exception:
             pass
+
+
+RF_COALESCE_SHA256, RF_COALESCE_PROBE, RF_COALESCE_ASSOC_GET = 1, 2, 3
+
+
+class Coalescer:
+    """rf_coalescer: concurrent callers (threads) coalesced into device
+    batches.  target: a Bloom (PROBE) or an Assoc (ASSOC_GET)."""
+
+    def __init__(self, ctx, kind, target=None, assoc_kind=0, max_batch=4096, max_wait_us=200):
+        self.ctx, self.kind, self.target = ctx, kind, target
+        self._h = ctypes.c_void_p()
+        _check(lib().rf_coalescer_open(ctx.handle, kind, target._h if target is not None else None, assoc_kind,
+                                       max_batch, max_wait_us, ctypes.byref(self._h)))
+
+    def sha256(self, msg: bytes) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        _check(lib().rf_coalesce_sha256(self._h, msg, len(msg), out))
+        return out.raw
+
+    def probe(self, digest32: bytes) -> bool:
+        out = ctypes.c_uint8(0)
+        _check(lib().rf_coalesce_probe(self._h, digest32, ctypes.byref(out)))
+        return bool(out.value)
+
+    def assoc_get(self, key32: bytes):
+        val, found = ctypes.create_string_buffer(32), ctypes.c_uint8(0)
+        _check(lib().rf_coalesce_assoc_get(self._h, key32, val, ctypes.byref(found)))
+        return bool(found.value), val.raw
+
+    def sha256_async(self, msg: bytes):
+        """-> ticket (msg and the result buffer are kept alive by it)."""
+        buf = ctypes.create_string_buffer(msg, len(msg)) if msg else ctypes.create_string_buffer(1)
+        out = ctypes.create_string_buffer(32)
+        t = ctypes.c_void_p()
+        _check(lib().rf_coalesce_sha256_async(self._h, buf, len(msg), out, ctypes.byref(t)))
+        return {"t": t, "buf": buf, "out": out}
+
+    def poll(self, ticket) -> bool:
+        done = ctypes.c_int(0)
+        _check(lib().rf_coalesce_poll(self._h, ticket["t"], ctypes.byref(done)))
+        return bool(done.value)
+
+    def wait(self, ticket) -> bytes:
+        _check(lib().rf_coalesce_wait(self._h, ticket["t"]))
+        return ticket["out"].raw
+
+    def free(self, ticket):
+        lib().rf_coalesce_ticket_free(self._h, ticket["t"])
+        ticket["t"] = None
+
+    def stats(self):
+        b, r, m = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().rf_coalescer_stats(self._h, ctypes.byref(b), ctypes.byref(r), ctypes.byref(m)))
+        return b.value, r.value, m.value
+
+    def close(self):
+        if self._h:
+            lib().rf_coalescer_close(self._h)
+            self._h = ctypes.c_void_p()
 
 
 class Assoc:
