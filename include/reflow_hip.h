@@ -230,6 +230,16 @@ int rf_install_info(const rf_install *in, uint64_t *n_entries, uint64_t *path_by
 int rf_install_entries(const rf_install *in, char *paths, uint64_t *path_offs, uint8_t *ids32,
                        int64_t *sizes);
 void rf_install_destroy(rf_install *in);
+/* The walk alone, host-only (no device): internal/walker's Scan as install
+ * uses it -- relpaths ("." for a file root) and Stat sizes of every
+ * non-directory entry, bytewise-sorted depth-first pre-order, links
+ * followed, vanished entries skipped.  rf_walk_entries: paths concatenated,
+ * path_offs[n_entries + 1]. */
+typedef struct rf_walk rf_walk;
+int rf_walk_dir(const char *root, rf_walk **out);
+int rf_walk_info(const rf_walk *w, uint64_t *n_entries, uint64_t *path_bytes);
+int rf_walk_entries(const rf_walk *w, char *paths, uint64_t *path_offs, int64_t *sizes);
+void rf_walk_free(rf_walk *w);
 
 /* ---- Fileset values as JSON (the assoc value, eval.go:1141 -> marshal
  * eval.go:1961-1967 = json.Marshal + Repository.Put, repository.go:108-114) --

@@ -49,7 +49,7 @@ EXPORTS = [
     "rf_sha_streams_len", "rf_sha_streams_verify", "rf_sha256_verify", "rf_flow_dirty",
     "rf_coalescer_open", "rf_coalescer_close", "rf_coalesce_sha256", "rf_coalesce_probe", "rf_coalesce_assoc_get",
     "rf_coalesce_sha256_async", "rf_coalesce_poll", "rf_coalesce_wait", "rf_coalesce_ticket_free",
-    "rf_coalescer_stats",
+    "rf_coalescer_stats", "rf_walk_dir", "rf_walk_info", "rf_walk_entries", "rf_walk_free",
     "rf_graph_set_part", "rf_graph_recompute_part", "rf_graph_part_gathered", "rf_graph_split",
     "rf_graph_piece_free", "rf_graph_piece_desc", "rf_graph_piece_part", "rf_graph_piece_slots",
 ]
@@ -355,6 +355,8 @@ def lib():
             "rf_coalesce_sha256_async": ([vp, vp, u64, vp, vp], i32),
             "rf_coalesce_poll": ([vp, vp, vp], i32), "rf_coalesce_wait": ([vp, vp], i32),
             "rf_coalesce_ticket_free": ([vp, vp], None), "rf_coalescer_stats": ([vp, vp, vp, vp], i32),
+            "rf_walk_dir": ([ctypes.c_char_p, vp], i32), "rf_walk_info": ([vp, vp, vp], i32),
+            "rf_walk_entries": ([vp, vp, vp, vp], i32), "rf_walk_free": ([vp], None),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -930,6 +932,24 @@ class Bloom:
             self.close()
         except Exception:
             pass
+
+
+def walk_dir(root):
+    """rf_walk_dir (host-only, no device): internal/walker's Scan as install
+    uses it -> [(relpath bytes, Stat size)] in walk order."""
+    w = ctypes.c_void_p()
+    _check(lib().rf_walk_dir(os.fsencode(root), ctypes.byref(w)))
+    try:
+        n, pb = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().rf_walk_info(w, ctypes.byref(n), ctypes.byref(pb)))
+        paths = ctypes.create_string_buffer(max(pb.value, 1))
+        offs = np.zeros(n.value + 1, np.uint64)
+        sizes = np.zeros(n.value + 1, np.int64)
+        _check(lib().rf_walk_entries(w, paths, _ptr(offs), _ptr(sizes)))
+        raw = paths.raw
+        return [(raw[int(offs[i]):int(offs[i + 1])], int(sizes[i])) for i in range(n.value)]
+    finally:
+        lib().rf_walk_free(w)
 
 
 RF_COALESCE_SHA256, RF_COALESCE_PROBE, RF_COALESCE_ASSOC_GET = 1, 2, 3

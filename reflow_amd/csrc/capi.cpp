@@ -36,6 +36,7 @@
 #include "graph_internal.h"
 #include "host_sha.h"
 #include "reflow_hip.h"
+#include "walk.h"
 #include "wire.h"
 
 using namespace rf;
@@ -913,51 +914,6 @@ struct rf_install {
 static constexpr uint64_t kInstallChunk = 8ull << 30;
 static constexpr uint64_t kInstallSeg = 32ull << 20;
 
-// Entry `path` (stat follows links, as os.Stat).  A directory is read,
-// sorted and closed before its children are visited, so the walk holds one
-// directory open at a time whatever the depth (walker.Scan closes each
-// directory after Readdirnames too).
-static int install_walk(const std::string& path, const std::string& rel, rf_install* in, int depth = 0) {
-    struct stat st;
-    if (::stat(path.c_str(), &st) != 0) {
-        if (errno == ENOENT) return RF_OK;
-        return fail(RF_EIO, "stat %s: %s", path.c_str(), strerror(errno));
-    }
-    if (!S_ISDIR(st.st_mode)) {
-        in->full.push_back(path);
-        in->rel.push_back(rel);
-        in->sizes.push_back((int64_t)st.st_size);
-        return RF_OK;
-    }
-    if (depth > 4096) return fail(RF_EIO, "walk %s: directory nesting deeper than 4096 (link cycle?)", path.c_str());
-    DIR* d = ::opendir(path.c_str());
-    if (!d) return fail(RF_EIO, "open %s: %s", path.c_str(), strerror(errno));
-    std::vector<std::pair<std::string, unsigned char>> names;
-    errno = 0;
-    while (struct dirent* de = ::readdir(d)) {
-        if (strcmp(de->d_name, ".") && strcmp(de->d_name, "..")) names.emplace_back(de->d_name, de->d_type);
-        errno = 0;
-    }
-    const int rerr = errno;
-    ::closedir(d);
-    if (rerr) return fail(RF_EIO, "readdir %s: %s", path.c_str(), strerror(rerr));
-    // char_traits<char>: bytewise (unsigned) order
-    std::sort(names.begin(), names.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-    for (const auto& [nm, type] : names) {
-        std::string cpath = path + "/" + nm, crel = rel == "." ? nm : rel + "/" + nm;
-        if (type == DT_REG) {
-            // a regular file (not a link): its Stat size is taken by the
-            // parallel pass in rf_install_dir (-1 = pending)
-            in->full.push_back(std::move(cpath));
-            in->rel.push_back(std::move(crel));
-            in->sizes.push_back(-1);
-        } else if (int rc = install_walk(cpath, crel, in, depth + 1)) {  // dirs, links, unknown: stat
-            return rc;
-        }
-    }
-    return RF_OK;
-}
-
 // Read file f (expected `want` bytes) into dst; the content must not have
 // changed size since the walk's stat.
 static bool install_read(const std::string& f, uint8_t* dst, uint64_t want, std::string& err) {
@@ -998,52 +954,8 @@ extern "C" int rf_install_dir(rf_ctx* ctx, const char* root, rf_install** out) {
     const bool timing = getenv("RF_INSTALL_TIMING") != nullptr;
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_begin = now();
-    int rc = install_walk(root, ".", in.get());
+    int rc = walk_tree(root, in->rel, in->full, in->sizes);
     if (rc) return rc;
-    {
-        // Stat sizes of the regular files the walk did not stat, in parallel;
-        // one removed since the readdir is skipped, as the walker's Stat would
-        std::vector<uint64_t> pend;
-        for (uint64_t i = 0; i < in->sizes.size(); ++i)
-            if (in->sizes[i] < 0) pend.push_back(i);
-        std::vector<int> err(pend.size(), 0);
-        std::atomic<uint64_t> nx{0};
-        auto st_worker = [&]() {
-            for (uint64_t k; (k = nx.fetch_add(1)) < pend.size();) {
-                struct stat st;
-                if (::stat(in->full[pend[k]].c_str(), &st) == 0)
-                    in->sizes[pend[k]] = (int64_t)st.st_size;
-                else
-                    err[k] = errno;
-            }
-        };
-        const uint64_t hw = std::max(1u, std::thread::hardware_concurrency());
-        const uint64_t nt = std::min<uint64_t>({60, hw, pend.size() / 64 + 1});
-        std::vector<std::thread> pool;
-        for (uint64_t t = 1; t < nt; ++t) pool.emplace_back(st_worker);
-        st_worker();
-        for (auto& t : pool) t.join();
-        bool drop = false;
-        for (uint64_t k = 0; k < pend.size(); ++k) {
-            if (err[k] == ENOENT) {
-                drop = true;
-            } else if (err[k]) {
-                return fail(RF_EIO, "stat %s: %s", in->full[pend[k]].c_str(), strerror(err[k]));
-            }
-        }
-        if (drop) {  // rare: compact out the vanished entries (sizes still -1)
-            uint64_t w = 0;
-            for (uint64_t i = 0; i < in->sizes.size(); ++i) {
-                if (in->sizes[i] < 0) continue;
-                in->full[w] = std::move(in->full[i]);
-                in->rel[w] = std::move(in->rel[i]);
-                in->sizes[w++] = in->sizes[i];
-            }
-            in->full.resize(w);
-            in->rel.resize(w);
-            in->sizes.resize(w);
-        }
-    }
     const double t_walk = now();
     const uint64_t n = in->rel.size();
     in->ids.assign(32 * n, 0);

@@ -7,12 +7,16 @@
 //     would wrap;
 //   * rf_graph_split (partition_split.cpp): random DAGs and owners, every
 //     piece's arrays walked, malformed descs rejected;
+//   * the install walk (walk.cpp: rf_walk_dir) over a real tree with links,
+//     a dangling link, empty dirs, a file root and a link cycle;
 //   * host SHA-256 (host_sha.cpp) against FIPS 180 vectors;
 //   * reflow_host.cpp's host-only helpers (Digest text forms, MarshalJSON).
 // Prints PASS; any sanitizer report aborts the process.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <random>
 #include <string>
@@ -271,6 +275,69 @@ static void test_graph_split() {
     EXPECT(rf_graph_split(&d, 2, 2, ow, &pc) == RF_EINVAL);  // rank out of range
 }
 
+// ---- install walk ------------------------------------------------------------------
+static void put_file(const std::string& p, const std::string& body) {
+    FILE* f = fopen(p.c_str(), "wb");
+    if (!f) {
+        ++fails;
+        return;
+    }
+    fwrite(body.data(), 1, body.size(), f);
+    fclose(f);
+}
+
+static std::vector<std::pair<std::string, int64_t>> walk(const std::string& root, int* rc_out) {
+    rf_walk* w = nullptr;
+    std::vector<std::pair<std::string, int64_t>> out;
+    *rc_out = rf_walk_dir(root.c_str(), &w);
+    if (*rc_out != RF_OK) return out;
+    uint64_t n = 0, pb = 0;
+    EXPECT(rf_walk_info(w, &n, &pb) == RF_OK);
+    std::vector<char> paths(pb + 1);
+    std::vector<uint64_t> offs(n + 1);
+    std::vector<int64_t> sizes(n + 1);
+    EXPECT(rf_walk_entries(w, paths.data(), offs.data(), sizes.data()) == RF_OK);
+    for (uint64_t i = 0; i < n; ++i) out.push_back({std::string(&paths[offs[i]], offs[i + 1] - offs[i]), sizes[i]});
+    rf_walk_free(w);
+    return out;
+}
+
+static void test_walk() {
+    char tmpl[] = "/tmp/rf_asan_walkXXXXXX";
+    const char* d = mkdtemp(tmpl);
+    if (!d) {
+        ++fails;
+        return;
+    }
+    const std::string r(d);
+    mkdir((r + "/a").c_str(), 0755);
+    mkdir((r + "/empty").c_str(), 0755);
+    put_file(r + "/a/x", "hello");
+    put_file(r + "/a/y", "");
+    put_file(r + "/b.txt", "abc");
+    put_file(r + "/Z", "z");
+    put_file(r + "/\xc3\xa9", "accent");
+    EXPECT(symlink("a", (r + "/link_dir").c_str()) == 0);
+    EXPECT(symlink("b.txt", (r + "/link_file").c_str()) == 0);
+    EXPECT(symlink("nowhere", (r + "/dangling").c_str()) == 0);
+    int rc = 0;
+    auto got = walk(r, &rc);
+    const std::vector<std::pair<std::string, int64_t>> want = {
+        {"Z", 1}, {"a/x", 5}, {"a/y", 0}, {"b.txt", 3}, {"link_dir/x", 5}, {"link_dir/y", 0}, {"link_file", 3},
+        {"\xc3\xa9", 6}};
+    EXPECT(rc == RF_OK && got == want);
+    auto one = walk(r + "/b.txt", &rc);  // a file root: relpath "."
+    EXPECT(rc == RF_OK && one.size() == 1 && one[0].first == "." && one[0].second == 3);
+    auto none = walk(r + "/does-not-exist", &rc);  // ENOENT: skipped, as walker.go:40-43
+    EXPECT(rc == RF_OK && none.empty());
+    mkdir((r + "/cyc").c_str(), 0755);
+    EXPECT(symlink(".", (r + "/cyc/loop").c_str()) == 0);  // cyc/loop/loop/... : ELOOP or too deep
+    (void)walk(r + "/cyc", &rc);
+    EXPECT(rc == RF_EIO);
+    std::string cmd = "rm -rf '" + r + "'";
+    EXPECT(system(cmd.c_str()) == 0);
+}
+
 // ---- host SHA-256 ----------------------------------------------------------------
 static void test_host_sha() {
     if (!rf::host_sha_available()) return;
@@ -311,6 +378,7 @@ int main() {
     test_fileset_json();
     test_bloom_wire();
     test_graph_split();
+    test_walk();
     test_host_sha();
     test_host_mirror();
     if (fails) {

@@ -135,3 +135,22 @@ def test_gpu_install_deep_tree(ctx, tmp_path):
     ents, fs = ctx.install_dir(d)
     w_ents, w_fs = O.install_dir(d)
     assert ents == w_ents and fs == w_fs and len(ents) == 300
+
+
+@pytest.mark.parametrize("tree", ["rich", "symlinks", "file_root", "missing"])
+def test_host_walk_matches_oracle(tmp_path, tree):
+    """rf_walk_dir -- the walk rf_install_dir digests, host-only (no GPU) --
+    lists exactly the oracle walker's (relpath, size) in its order."""
+    from reflow_amd import capi
+    root = str(tmp_path)
+    if tree == "rich":
+        _rich_tree(root)
+    elif tree == "symlinks":
+        _symlink_tree(root)
+    elif tree == "file_root":
+        root = os.path.join(root, "out")
+        _write(root, b"foobar\n")
+    else:
+        root = os.path.join(root, "missing")
+    ents, _ = O.install_dir(root)
+    assert capi.walk_dir(root) == [(r, s) for r, _, s in ents]
