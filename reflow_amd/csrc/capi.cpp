@@ -1219,17 +1219,29 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // padded templates (64-B blocks, FIPS padding pre-applied)
     std::vector<uint32_t> meta(8ull * J, 0), holes(2ull * H);
     std::vector<uint64_t> job_off(J);
+    // Constant leading blocks: a job whose first hole starts in block L > 0
+    // begins every hash with the same L blocks -- hashed once at load into a
+    // midstate (k2_midstates); the record's template offset and block count
+    // skip them and its hole positions move back by 64 L (jobs without holes
+    // are hashed only by a full recompute and keep their blocks).
+    std::vector<uint32_t> lead(J, 0), lead_start(J, 0);
+    uint64_t n_lead = 0;
     uint64_t tb = 0, hcur = 0;
     for (uint32_t i = 0; i < J; ++i) {
         const uint32_t j = perm[i];
         const uint32_t s = d->out_slot[j];
         job_off[i] = tb;
+        const uint32_t ld = d->hole_ptr[j + 1] > d->hole_ptr[j]
+                                ? std::min<uint32_t>(d->hole_pos[d->hole_ptr[j]] / 64, nblk[j] - 1) : 0;
+        lead[i] = ld;
+        lead_start[i] = (uint32_t)(tb / 64);
+        n_lead += ld != 0;
         uint32_t* m = &meta[8ull * i];
-        m[0] = (uint32_t)(tb / 64);
-        m[1] = nblk[j];
+        m[0] = (uint32_t)(tb / 64) + ld;
+        m[1] = nblk[j] - ld;
         m[2] = (uint32_t)hcur;
         for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h, ++hcur) {
-            holes[2 * hcur] = d->hole_pos[h];
+            holes[2 * hcur] = d->hole_pos[h] - 64 * ld;
             holes[2 * hcur + 1] = d->hole_slot[h];
         }
         m[3] = (uint32_t)hcur;
@@ -1238,7 +1250,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         m[6] = (uint32_t)cptr[s + 1];
         m[7] = fuse[j] >= 0 ? gr->ext2int[(uint32_t)fuse[j]] : 0xffffffffu;
         tb += 64ull * nblk[j];
-        gr->total_blocks += nblk[j];
+        gr->total_blocks += nblk[j] - ld;
     }
     if (tb / 64 >= 0xffffffffull) return fail(RF_EINVAL, "templates exceed 256 GiB");
     std::vector<uint8_t> tmpl(std::max<uint64_t>(tb, 64), 0);
@@ -1320,6 +1332,29 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     G.counts = gr->b_counts.as<uint32_t>();
     G.counts_last = gr->b_counts_last.as<uint32_t>();
     G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
+    if (n_lead && !getenv("RF_K2_NO_MIDSTATE")) {  // (RF_K2_NO_MIDSTATE: A/B)
+        struct Tmp {
+            DevBuf b;
+            ~Tmp() { b.release(); }
+        } d_start, d_lead;
+        if ((e = up(d_start.b, lead_start.data(), 4ull * J)) != hipSuccess ||
+            (e = up(d_lead.b, lead.data(), 4ull * J)) != hipSuccess || (e = gr->b_mid.ensure(32ull * J)) != hipSuccess)
+            return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph midstates: %s", hipGetErrorString(e));
+        HIPC(launch_graph_midstates(G.tmpl, d_start.b.as<uint32_t>(), d_lead.b.as<uint32_t>(), J,
+                                    gr->b_mid.as<uint4>(), ctx->stream));
+        HIPC(hipStreamSynchronize(ctx->stream));
+        G.mid = gr->b_mid.as<uint4>();
+    } else if (n_lead) {  // A/B: keep every block, the records as if no job had a constant prefix
+        for (uint32_t i = 0; i < J; ++i) {
+            if (!lead[i]) continue;
+            meta[8ull * i] -= lead[i];
+            meta[8ull * i + 1] += lead[i];
+            gr->total_blocks += lead[i];
+            for (uint32_t h = meta[8ull * i + 2]; h < meta[8ull * i + 3]; ++h) holes[2ull * h] += 64 * lead[i];
+        }
+        HIPC(sync_copy(ctx, gr->b_meta.p, meta.data(), 32ull * J, hipMemcpyHostToDevice));
+        HIPC(sync_copy(ctx, gr->b_holes.p, holes.data(), 8ull * H, hipMemcpyHostToDevice));
+    }
     if (getenv("RF_K2_STAMPS")) {  // diagnostic: per-phase times of workgroup 0 of each level
         HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
@@ -1338,8 +1373,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
                           &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_counts, &gr->b_counts_last,
-                          &gr->b_lvl_start, &gr->b_tmp_idx,
-                          &gr->b_tmp_dig})
+                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);

@@ -85,7 +85,16 @@ struct GraphDev {
     std::vector<uint32_t> lvl_start; // host copy [L+1]
     std::vector<uint8_t> inc_level;  // [L] level has jobs that can be queued (not all fusion targets)
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
+    // [2J] each job's initial chaining value (IV, or the midstate after the
+    // constant blocks its template starts with -- the record's template
+    // offset and block count already skip them); null when no job has any
+    uint4* mid = nullptr;
 };
+// Midstates of the jobs' leading constant blocks, hashed once at load: job i
+// (internal order) hashes lead[i] blocks of its template from block
+// start[i] (64-B units) into mid[2i..2i+1] (state words); IV when lead[i] = 0.
+hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, const uint32_t* lead, uint32_t n,
+                                  uint4* mid, hipStream_t s);
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);
 hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s);

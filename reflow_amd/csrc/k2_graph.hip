@@ -52,7 +52,19 @@ struct LevelArgs {
     uint32_t* list;
     uint32_t* counts;
     unsigned long long* stamps;  // diagnostic (RF_K2_STAMPS): phase times of workgroup 0, else null
+    const uint4* __restrict__ mid;  // [2J] initial chaining values, or null (= IV for every job)
 };
+
+// A job's initial chaining value (GraphDev::mid).
+__device__ __forceinline__ void init_state(const LevelArgs& a, uint32_t p, ShaState& st) {
+    if (a.mid) {
+        const uint4 lo = a.mid[2ull * p], hi = a.mid[2ull * p + 1];
+        st.h[0] = lo.x; st.h[1] = lo.y; st.h[2] = lo.z; st.h[3] = lo.w;
+        st.h[4] = hi.x; st.h[5] = hi.y; st.h[6] = hi.z; st.h[7] = hi.w;
+    } else {
+        st.init();
+    }
+}
 
 // Append the lanes' jobs j (need) at level lv to their levels' lists; one
 // atomicAdd per distinct level in the wave.  Called by every lane of the wave.
@@ -289,7 +301,7 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
     MatCursor cur;
     cur.begin(a, m0, ring);
     ShaState st;
-    st.init();
+    init_state(a, p, st);
     for (uint32_t b = 0; b < cur.nb; ++b) {
         uint32_t w[16];
         cur.block(a, b, ring, w);
@@ -425,7 +437,7 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
             maxnb = __builtin_amdgcn_readfirstlane(maxnb);
             MatCursor cur;
             ShaState st;
-            st.init();
+            init_state(a, has ? p : 0u, st);
             uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
             uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
             if (wave == 1 && has) {
@@ -712,6 +724,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         uint4 nt[8];
         uint2 nr = make_uint2(0, 0);
         uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+        uint4 nmlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nmhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
         uint32_t sk = 0;
         while (maxnb) {
             RF_STAMP_PL(sk); ++sk;
@@ -747,18 +760,27 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     cur.begin(a, m0, ring);
                 }
             }
+            // the job's initial chaining value H (IV, or the midstate after its
+            // constant leading blocks): the fused target's was fetched a job ahead
+            uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
             if (chain && has) {
                 if (fused) {
                     olo = nolo;
                     ohi = nohi;
                     pre[0] = npre[0];
                     pre[1] = npre[1];
+                    hlo = nmlo;
+                    hhi = nmhi;
                 } else {
                     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
                     olo = od[0];
                     ohi = od[1];
                     if (m1.y < m1.z) pre[0] = a.cons[m1.y];
                     if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+                    if (a.mid) {
+                        hlo = a.mid[2ull * p];
+                        hhi = a.mid[2ull * p + 1];
+                    }
                 }
                 if (nfu) {
                     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
@@ -770,6 +792,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         nnm0 = a.meta[2ull * nm1.w];
                         nnm1 = a.meta[2ull * nm1.w + 1];
                     }
+                    if (a.mid) {
+                        nmlo = a.mid[2ull * m1.w];
+                        nmhi = a.mid[2ull * m1.w + 1];
+                    }
                 }
             }
             if (kW == 3 && wave == kExp && nfu && nm1.w != ~0u) {
@@ -777,12 +803,12 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 nnm1 = a.meta[2ull * nm1.w + 1];
             }
             // the chain's lagged state: as after a block whose raw state is zero
-            // with chaining value IV (lag_chain.h / k1_sha256_duo)
-            uint32_t Hr0 = elane ? IV[4] : IV[0], Hr1 = elane ? IV[5] : IV[1];
-            uint32_t Hr2 = elane ? IV[6] : IV[2], Hr3 = elane ? IV[7] : IV[3];
+            // with chaining value H (lag_chain.h / k1_sha256_duo, there H = IV)
+            uint32_t Hr0 = elane ? hhi.x : hlo.x, Hr1 = elane ? hhi.y : hlo.y;
+            uint32_t Hr2 = elane ? hhi.z : hlo.z, Hr3 = elane ? hhi.w : hlo.w;
             uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
-            uint32_t Z = elane ? IV[7] + IV[3] : 0u, Y = 0;
-            uint32_t c63 = 0, c64 = elane ? IV[2] : 0u - IV[4], c65 = elane ? IV[1] : 0u - IV[3];
+            uint32_t Z = elane ? hhi.w + hlo.w : 0u, Y = 0;
+            uint32_t c63 = 0, c64 = elane ? hlo.z : 0u - hhi.x, c65 = elane ? hlo.y : 0u - hlo.w;
             uint32_t t0, t1, t2, t3;
             uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
             const uint32_t nbl = m0.y;  // this lane's job's blocks (0: no job)
@@ -993,6 +1019,30 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     }
 }
 
+// Load time: the chaining value after each job's constant leading blocks.
+__global__ __launch_bounds__(256) void k2_midstates(const uint8_t* __restrict__ tmpl,
+                                                    const uint32_t* __restrict__ start,
+                                                    const uint32_t* __restrict__ lead, uint32_t n,
+                                                    uint4* __restrict__ mid) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        ShaState st;
+        st.init();
+        const uint4* T = reinterpret_cast<const uint4*>(tmpl) + 4ull * start[i];
+        for (uint32_t b = 0; b < lead[i]; ++b) {
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = T[4 * b + q];
+                w[4 * q] = bswap32(v.x); w[4 * q + 1] = bswap32(v.y);
+                w[4 * q + 2] = bswap32(v.z); w[4 * q + 3] = bswap32(v.w);
+            }
+            sha256_compress(st, w);
+        }
+        mid[2ull * i] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+        mid[2ull * i + 1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+    }
+}
+
 // set_slots: write input digests; a changed slot queues its consumers.
 __global__ __launch_bounds__(256) void k3_mark_slots(const uint32_t* __restrict__ sl,
                                                      const uint8_t* __restrict__ dig, uint32_t n,
@@ -1155,7 +1205,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     // RF_DBG_HASH2: hash twice (k2_level); RF_K2_STAMPS=2: per-chunk stamps (k2_level_pl)
     static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u : 0u;
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
@@ -1200,6 +1250,13 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
     hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, const uint32_t* lead, uint32_t n,
+                                  uint4* mid, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k2_midstates, dim3(grid_for(n, 16384)), dim3(256), 0, s, tmpl, start, lead, n, mid);
     return hipGetLastError();
 }
 
