@@ -1201,6 +1201,25 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
             }
         }
     }
+    // Sinks (jobs nothing reads: physical cache keys, roots) may run at any
+    // level after their inputs: move them to the last level that launches
+    // anyway (one holding queueable non-sink jobs), where they fill their own
+    // workgroups beside that level's longer chains instead of lengthening an
+    // earlier level's (configs[2]: the pE1 keys, 4 blocks, left level 0's
+    // 1+2-block Val -> Coerce chains waiting).  RF_K2_SINK_ALAP=0: off (A/B).
+    {
+        static const bool alap = [] {
+            const char* v = getenv("RF_K2_SINK_ALAP");
+            return !(v && atoi(v) == 0);
+        }();
+        auto sink = [&](uint32_t j) { return cptr[d->out_slot[j]] == cptr[d->out_slot[j] + 1]; };
+        int64_t lq = -1;
+        for (uint32_t j = 0; j < J; ++j)
+            if (!fused_target[j] && !sink(j)) lq = std::max<int64_t>(lq, level[j]);
+        if (alap && lq > 0)
+            for (uint32_t j = 0; j < J; ++j)
+                if (!fused_target[j] && sink(j) && level[j] < (uint32_t)lq) level[j] = (uint32_t)lq;
+    }
     // internal order: level ascending, blocks descending (similar lanes per wave)
     std::vector<uint32_t> perm(J);
     std::iota(perm.begin(), perm.end(), 0u);
