@@ -1301,14 +1301,18 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
             const char* v = getenv("RF_K2_WIDE");
             return v ? (uint64_t)strtoull(v, nullptr, 10) : 8ull;
         }();
-        std::vector<uint64_t> qj(L, 0), qb(L, 0);
+        // the average over the level's non-sink queueable jobs: sinks moved
+        // here run in their own short workgroups, the chains set the shape
+        std::vector<uint64_t> qj(L, 0), qb(L, 0), qall(L, 0);
         for (uint32_t j = 0; j < J; ++j)
             if (!fused_target[j]) {
+                qall[level[j]] += 1;
+                if (cptr[d->out_slot[j]] == cptr[d->out_slot[j] + 1]) continue;  // a sink
                 qj[level[j]] += 1;
                 qb[level[j]] += nblk[j];
             }
         for (uint32_t l = 0; l < L; ++l)
-            if (qj[l]) gr->g.inc_level[l] = (wide && qb[l] >= wide * qj[l]) ? 2 : 1;
+            if (qall[l]) gr->g.inc_level[l] = (wide && qj[l] && qb[l] >= wide * qj[l]) ? 2 : 1;
     }
     gr->tmpl_bytes = tb;
     // upload
