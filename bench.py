@@ -490,9 +490,17 @@ def bench_dag(args, dist, ctx, comm, budget):
     n_dirty_nodes = n_dirty_jobs - len(pairs)  # minus the pE1 physical keys
     state = {"v": 0}
 
+    # RF_BENCH_DAG_ONE_LAUNCH=1: mark node + levels as one graph launch
+    # (update_recompute_async); measured ~2 us/step slower than the separate
+    # mark launch on configs[2] (profiles/r02/k2_ab.txt), so off by default
+    one_launch = part is None and os.environ.get("RF_BENCH_DAG_ONE_LAUNCH", "0") == "1"
+
     def step():
         ver = d_new if state["v"] == 0 else d_old
         state["v"] ^= 1
+        if one_launch:
+            g.update_recompute_async(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
+            return
         g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
         if part is not None:
             recompute(False)

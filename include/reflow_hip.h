@@ -337,6 +337,13 @@ int rf_graph_set_slots_device(rf_graph *g, const void *d_slots, const void *d_di
 int rf_graph_recompute(rf_graph *g, int full, uint64_t *out_recomputed);
 /* Asynchronous form (no count readback). */
 int rf_graph_recompute_async(rf_graph *g, int full, void *stream);
+/* rf_graph_set_slots_device + rf_graph_recompute_async(g, 0, stream) as ONE
+ * graph launch (the changed inputs' mark kernel is the graph's first node,
+ * its parameters updated per call on the host): an incremental step with no
+ * launch boundary before its first level.  The first call on a fresh graph
+ * runs a full recompute. */
+int rf_graph_update_recompute_async(rf_graph *g, const void *d_slots, const void *d_digests32, uint32_t n,
+                                    void *stream);
 int rf_graph_get_slots(rf_graph *g, const uint32_t *slots, uint32_t n, uint8_t *out32);
 /* Device-resident gather: d_out32[i] = slot d_slots[i] (e.g. boundary digests
  * for rf_comm_allgather).  Asynchronous on `stream`. */

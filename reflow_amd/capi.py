@@ -49,7 +49,7 @@ EXPORTS = [
     "rf_sha_streams_len", "rf_sha_streams_verify", "rf_sha256_verify", "rf_flow_dirty",
     "rf_coalescer_open", "rf_coalescer_close", "rf_coalesce_sha256", "rf_coalesce_probe", "rf_coalesce_assoc_get",
     "rf_coalesce_sha256_async", "rf_coalesce_poll", "rf_coalesce_wait", "rf_coalesce_ticket_free",
-    "rf_coalescer_stats", "rf_walk_dir", "rf_walk_info", "rf_walk_entries", "rf_walk_free",
+    "rf_coalescer_stats", "rf_graph_update_recompute_async", "rf_walk_dir", "rf_walk_info", "rf_walk_entries", "rf_walk_free",
     "rf_graph_set_part", "rf_graph_recompute_part", "rf_graph_part_gathered", "rf_graph_split",
     "rf_graph_piece_free", "rf_graph_piece_desc", "rf_graph_piece_part", "rf_graph_piece_slots",
 ]
@@ -355,6 +355,7 @@ def lib():
             "rf_coalesce_sha256_async": ([vp, vp, u64, vp, vp], i32),
             "rf_coalesce_poll": ([vp, vp, vp], i32), "rf_coalesce_wait": ([vp, vp], i32),
             "rf_coalesce_ticket_free": ([vp, vp], None), "rf_coalescer_stats": ([vp, vp, vp, vp], i32),
+            "rf_graph_update_recompute_async": ([vp, vp, vp, u32, vp], i32),
             "rf_walk_dir": ([ctypes.c_char_p, vp], i32), "rf_walk_info": ([vp, vp, vp], i32),
             "rf_walk_entries": ([vp, vp, vp, vp], i32), "rf_walk_free": ([vp], None),
         }
@@ -770,6 +771,10 @@ class Graph:
 
     def recompute_async(self, full=False, stream=None):
         _check(lib().rf_graph_recompute_async(self._h, 1 if full else 0, stream))
+
+    def update_recompute_async(self, d_slots, d_digests32, n, stream=None):
+        """set_slots_device + recompute_async(full=False) as one graph launch."""
+        _check(lib().rf_graph_update_recompute_async(self._h, d_slots, d_digests32, n, stream))
 
     def gather_device(self, d_slots, n, d_out, stream=None):
         _check(lib().rf_graph_gather_device(self._h, d_slots, n, d_out, stream))

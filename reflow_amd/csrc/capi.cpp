@@ -1401,6 +1401,8 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);
         if (gr->exec_inc) (void)hipGraphExecDestroy(gr->exec_inc);
+        if (gr->exec_upd) (void)hipGraphExecDestroy(gr->exec_upd);
+        if (gr->graph_upd) (void)hipGraphDestroy(gr->graph_upd);
         if (gr->exec_full) (void)hipGraphExecDestroy(gr->exec_full);
         graph_part_release(gr);
     }
@@ -1486,6 +1488,76 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
     HIPC(hipEventRecord(gr->e1, s));
     gr->timed = true;
     gr->initialized = true;
+    return RF_OK;
+}
+
+// Mark + incremental levels as ONE graph launch: the mark kernel is the
+// graph's first node and only its parameters change between calls
+// (hipGraphExecKernelNodeSetParams, host side), so a step is one launch --
+// no separate mark launch and no gap before the first level.
+static int graph_capture_upd(rf_graph* gr, const MarkArgs& ma, const hipKernelNodeParams& mp) {
+    hipStream_t cs = nullptr;
+    HIPC(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t graph = nullptr;
+    int rc = RF_OK;
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+        e = hipLaunchKernel(mp.func, mp.gridDim, mp.blockDim, mp.kernelParams, 0, cs);
+        if (e == hipSuccess) rc = graph_enqueue(gr, 0, cs);
+        const hipError_t e2 = hipStreamEndCapture(cs, &graph);
+        if (e == hipSuccess) e = e2;
+    }
+    (void)ma;
+    if (e == hipSuccess && rc == RF_OK) {  // the mark node: the kernel node running k3_mark_slots
+        size_t nn = 0;
+        e = hipGraphGetNodes(graph, nullptr, &nn);
+        std::vector<hipGraphNode_t> nodes(nn);
+        if (e == hipSuccess && nn) e = hipGraphGetNodes(graph, nodes.data(), &nn);
+        for (size_t i = 0; e == hipSuccess && i < nn && !gr->upd_mark; ++i) {
+            hipGraphNodeType t;
+            if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+            hipKernelNodeParams kp{};
+            if (hipGraphKernelNodeGetParams(nodes[i], &kp) == hipSuccess && kp.func == graph_mark_kernel())
+                gr->upd_mark = nodes[i];
+        }
+        if (e == hipSuccess && !gr->upd_mark) e = hipErrorNotFound;
+        if (e == hipSuccess) e = hipGraphInstantiate(&gr->exec_upd, graph, nullptr, nullptr, 0);
+    }
+    (void)hipStreamDestroy(cs);
+    if (rc != RF_OK || e != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        gr->upd_mark = nullptr;
+        gr->exec_upd = nullptr;
+        return rc != RF_OK ? rc : fail(RF_EDEVICE, "update graph capture: %s", hipGetErrorString(e));
+    }
+    gr->graph_upd = graph;
+    return RF_OK;
+}
+
+extern "C" int rf_graph_update_recompute_async(rf_graph* gr, const void* d_slots, const void* d_digests32,
+                                               uint32_t n, void* stream) {
+    ARG(gr && (n == 0 || (d_slots && d_digests32)), "null argument");
+    std::lock_guard<std::mutex> lk(gr->ctx->mu);
+    DevGuard dg(gr->ctx->device);
+    hipStream_t s = pick(gr->ctx, stream);
+    if (!gr->initialized) {  // the first recompute is a full one: mark, then the full sequence
+        HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
+                                     static_cast<const uint8_t*>(d_digests32), n, s));
+        return graph_recompute_locked(gr, 1, s);
+    }
+    MarkArgs ma;
+    hipKernelNodeParams mp{};
+    graph_mark_params(gr->g, static_cast<const uint32_t*>(d_slots), static_cast<const uint8_t*>(d_digests32), n,
+                      &ma, &mp);
+    if (!gr->exec_upd) {
+        if (int rc = graph_capture_upd(gr, ma, mp)) return rc;
+    } else {
+        HIPC(hipGraphExecKernelNodeSetParams(gr->exec_upd, gr->upd_mark, &mp));
+    }
+    HIPC(hipEventRecord(gr->e0, s));
+    HIPC(hipGraphLaunch(gr->exec_upd, s));
+    HIPC(hipEventRecord(gr->e1, s));
+    gr->timed = true;
     return RF_OK;
 }
 

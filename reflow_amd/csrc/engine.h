@@ -97,6 +97,23 @@ hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, co
                                   uint4* mid, hipStream_t s);
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);
+// k3_mark_slots as a graph kernel node: argument values + node parameters
+struct MarkArgs {
+    const uint32_t* sl;
+    const uint8_t* dig;
+    uint32_t n;
+    uint8_t* slots;
+    const uint32_t* cons_ptr;
+    const uint2* cons;
+    uint32_t* dirty;
+    uint32_t* list;
+    uint32_t* counts;
+    const uint32_t* ls;
+    void* ptrs[10];
+};
+void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,
+                       MarkArgs* args, hipKernelNodeParams* p);
+const void* graph_mark_kernel();
 hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s);
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,

@@ -36,6 +36,11 @@ struct rf_graph {
     uint32_t max_level_jobs = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipGraphExec_t exec_inc = nullptr, exec_full = nullptr;
+    // mark + incremental levels as one graph (rf_graph_update_recompute_async);
+    // the template graph is kept: its mark node's parameters change per call
+    hipGraph_t graph_upd = nullptr;
+    hipGraphExec_t exec_upd = nullptr;
+    hipGraphNode_t upd_mark = nullptr;
     bool timed = false;
     GraphPart* part = nullptr;  // multi-GPU partition (rf_graph_set_part), else null
 };

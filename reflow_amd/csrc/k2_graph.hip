@@ -1199,6 +1199,33 @@ hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, con
     return hipGetLastError();
 }
 
+// The mark kernel as a graph kernel node (rf_graph_update_recompute_async):
+// its launch parameters for this batch, argument values in `args`.
+void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,
+                       MarkArgs* args, hipKernelNodeParams* p) {
+    args->sl = slots;
+    args->dig = digests;
+    args->n = n;
+    args->slots = g.slots;
+    args->cons_ptr = g.cons_ptr;
+    args->cons = g.cons;
+    args->dirty = g.dirty;
+    args->list = g.list;
+    args->counts = g.counts;
+    args->ls = g.lvl_start_dev;
+    void* v[10] = {&args->sl, &args->dig, &args->n, &args->slots, &args->cons_ptr, &args->cons,
+                   &args->dirty, &args->list, &args->counts, &args->ls};
+    for (int i = 0; i < 10; ++i) args->ptrs[i] = v[i];
+    p->func = reinterpret_cast<void*>(k3_mark_slots);
+    p->gridDim = dim3(n ? grid_for(n, 4096) : 1);  // an empty batch still runs (and marks nothing)
+    p->blockDim = dim3(256);
+    p->sharedMemBytes = 0;
+    p->kernelParams = args->ptrs;
+    p->extra = nullptr;
+}
+
+const void* graph_mark_kernel() { return reinterpret_cast<const void*>(k3_mark_slots); }
+
 hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s) {
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
