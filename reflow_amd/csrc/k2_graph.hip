@@ -206,8 +206,13 @@ struct MatCursor {
         ring_put(ring, 0, t);
         t[0] = nt[4]; t[1] = nt[5]; t[2] = nt[6]; t[3] = nt[7];
     }
-    // the 16 big-endian words of block b (blocks taken in order)
-    __device__ __forceinline__ void block(const LevelArgs& a, uint32_t b, uint32_t* ring, uint32_t (&w)[16]) {
+    // the 16 big-endian words of block b (blocks taken in order).  one: every
+    // active lane of the wave holds a fused job (begin_pre: its single hole is
+    // q0) -- wave-uniform, so that path has no queue rotation: no record or
+    // digest loads and no register moves of loads in flight (each such move
+    // compiled to an s_waitcnt vmcnt(0), an HBM round trip inside the block)
+    __device__ __forceinline__ void block(const LevelArgs& a, uint32_t b, uint32_t* ring, uint32_t (&w)[16],
+                                          bool one = false) {
         const uint32_t half = (b & 1) * 16;
         if (b + 1 < nb) {
             ring_put(ring, half ^ 16, t);
@@ -218,7 +223,12 @@ struct MatCursor {
         }
         // holes that start in block b (they may run into block b+1)
         const uint32_t lim = 64 * (b + 1);
-        if (q0.r.x < lim) {
+        if (one) {
+            if (q0.r.x < lim) {
+                apply(ring, q0);
+                q0.r = make_uint2(~0u, 0u);
+            }
+        } else if (q0.r.x < lim) {
             apply(ring, q0);
             if (q1.r.x < lim) {
                 apply(ring, q1);
@@ -729,6 +739,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         while (maxnb) {
             RF_STAMP_PL(sk); ++sk;
             const bool fused = fslot != ~0u;
+            // a job is fused in every lane that has one after the first pass
+            const bool wfused = __any(fused);
             uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
             if (has) {
                 if (fused) {
@@ -782,21 +794,6 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         hhi = a.mid[2ull * p + 1];
                     }
                 }
-                if (nfu) {
-                    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
-                    nolo = od[0];
-                    nohi = od[1];
-                    if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
-                    if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
-                    if (nm1.w != ~0u) {
-                        nnm0 = a.meta[2ull * nm1.w];
-                        nnm1 = a.meta[2ull * nm1.w + 1];
-                    }
-                    if (a.mid) {
-                        nmlo = a.mid[2ull * m1.w];
-                        nmhi = a.mid[2ull * m1.w + 1];
-                    }
-                }
             }
             if (kW == 3 && wave == kExp && nfu && nm1.w != ~0u) {
                 nnm0 = a.meta[2ull * nm1.w];
@@ -809,6 +806,27 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
             uint32_t Z = elane ? hhi.w + hlo.w : 0u, Y = 0;
             uint32_t c63 = 0, c64 = elane ? hlo.z : 0u - hhi.x, c65 = elane ? hlo.y : 0u - hlo.w;
+            // the fusion target's records, issued only after the state above
+            // is built from this job's: a wait for this job's loads must not
+            // also wait for these (they are used one job later).  The empty
+            // asm pins the order (the compiler otherwise sinks the state's
+            // selects below the loads and waits for everything, vmcnt(0)).
+            __asm__ volatile("" ::"v"(Hr0), "v"(Hr1), "v"(Hr2), "v"(Hr3), "v"(Z), "v"(c64), "v"(c65) : "memory");
+            if (chain && has && nfu) {
+                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
+                nolo = od[0];
+                nohi = od[1];
+                if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
+                if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
+                if (nm1.w != ~0u) {
+                    nnm0 = a.meta[2ull * nm1.w];
+                    nnm1 = a.meta[2ull * nm1.w + 1];
+                }
+                if (a.mid) {
+                    nmlo = a.mid[2ull * m1.w];
+                    nmhi = a.mid[2ull * m1.w + 1];
+                }
+            }
             uint32_t t0, t1, t2, t3;
             uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
             const uint32_t nbl = m0.y;  // this lane's job's blocks (0: no job)
@@ -863,7 +881,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                         const bool mine = b < m0.y;
                         uint32_t w[16];
-                        if (mine) cur.block(a, b, ring, w);
+                        if (mine) cur.block(a, b, ring, w, wfused);
                         volatile uint32_t* fl = &s_flag[gb % 3];
                         uint4* row = reinterpret_cast<uint4*>(&kw[((gb % 3) * 64 + lane) * kPcRow]);
 #pragma unroll
@@ -923,9 +941,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             } else {
             for (uint32_t it = 0; it < maxnb + lag; ++it) {
                 if (wave == kProd) {
-                    if (it < m0.y) {
+                    if (it < m0.y && !((a.dbg_twice == 3 && it >= 1) || a.dbg_twice == 4)) {
                         uint32_t w[16];
-                        cur.block(a, it, ring, w);
+                        cur.block(a, it, ring, w, wfused);
                         if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
                         if (kW == 2) {
                             kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
@@ -949,7 +967,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         }
                     }
                 } else if (kW == 3 && wave == kExp) {
-                    if (it >= 1 && it - 1 < m0.y) {
+                    if (it >= 1 && it - 1 < m0.y && !((a.dbg_twice == 3 && it >= 2) || a.dbg_twice == 4)) {
                         const uint32_t bb = (it - 1) & 1;
                         const uint4* row = reinterpret_cast<const uint4*>(&wbuf[(bb * 64 + lane) * kWRow]);
                         uint32_t w[16];
@@ -970,6 +988,18 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             bool changed = false;
             const bool own = chain && has && elane;
             if (chain) {
+                // The fusion target's prefetched records (issued at this job's
+                // start, blocks ago: arrived) are made to count as arrived here,
+                // before the digest store and frontier atomics: vmcnt also counts
+                // those, so a wait for the records at the next job's start would
+                // otherwise be a vmcnt(0) that waits for the store's HBM ack.
+                __asm__ volatile("" ::"v"(nolo.x), "v"(nolo.y), "v"(nolo.z), "v"(nolo.w), "v"(nohi.x), "v"(nohi.y),
+                                 "v"(nohi.z), "v"(nohi.w), "v"(npre[0].x), "v"(npre[0].y), "v"(npre[1].x),
+                                 "v"(npre[1].y), "v"(nmlo.x), "v"(nmlo.y), "v"(nmlo.z), "v"(nmlo.w));
+                __asm__ volatile("" ::"v"(nmhi.x), "v"(nmhi.y), "v"(nmhi.z), "v"(nmhi.w), "v"(nnm0.x), "v"(nnm0.y),
+                                 "v"(nnm0.z), "v"(nnm0.w), "v"(nnm1.x), "v"(nnm1.y), "v"(nnm1.z), "v"(nnm1.w),
+                                 "v"(nm0.x), "v"(nm0.y), "v"(nm0.z), "v"(nm0.w));
+                __asm__ volatile("" ::"v"(nm1.x), "v"(nm1.y), "v"(nm1.z), "v"(nm1.w));
                 chain_block(maxnb, kStream ? gb : maxnb, false);  // group 0 of block maxnb: the longest jobs' final value
                 // the a-lane's half (H0..H3) into its e-lane (H4..H7 there)
                 ShaState st;
@@ -1230,7 +1260,12 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
     // RF_DBG_HASH2: hash twice (k2_level); RF_K2_STAMPS=2: per-chunk stamps (k2_level_pl)
-    static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u : 0u;
+    // RF_K2_DBG_NOEXP=3|4 (timing diagnostic, WRONG digests): the producer
+    // skips assembling + expanding blocks >= 1 (3) or every block (4)
+    static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u
+                                 : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u
+                                 : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
+                                                              : 0u;
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid};
     // incremental: the dirty count is only known on device; 1024 blocks (4
