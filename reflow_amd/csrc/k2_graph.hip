@@ -592,10 +592,13 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
 // wave (six shuffles; an LDS atomicMax into one word measured 10 us per step
 // slower: 32 lanes per wave serialise on it).
 // stamps (RF_K2_STAMPS): workgroup 0's chain wave 0 (row 0) and producer (row 1)
+// Stamps go to LDS and are copied out at the kernel's end: a global store per
+// stamp counts in vmcnt and turned the next vmcnt wait of the wave into a wait
+// for the store's acknowledgement (phases looked ~0.5-1 us longer than they are).
 #define RF_STAMP_PL(k)                                                                                \
     do {                                                                                              \
         if (a.stamps && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == kProd) && (k) < 64)    \
-            a.stamps[128 * a.lvl + 64 * (wave != 0) + (k)] = __builtin_amdgcn_s_memrealtime();        \
+            s_stamp[wave != 0][(k)] = __builtin_amdgcn_s_memrealtime();                              \
     } while (0)
 
 // Streamed hand-over (kStream, kW = 2): no per-block barrier.  Blocks get
@@ -612,9 +615,25 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
 // the next link's chain runs its blocks 0 and 1 back to back.
 // Flags are written after s_waitcnt lgkmcnt(0) (the rows are in LDS) and
 // polled with s_sleep; no global-memory wait is involved.
+// Flag accesses are explicit ds_read/ds_write: a volatile access through the
+// (generic) flag pointer compiles to a FLAT load/store, which counts in vmcnt
+// as well, and every poll then waited for all the wave's HBM loads in flight
+// (s_waitcnt vmcnt(0) lgkmcnt(0)).  The low 32 bits of a generic pointer into
+// LDS are its LDS offset.
+__device__ __forceinline__ uint32_t lds_ld(const volatile uint32_t* p) {
+    uint32_t v;
+    __asm__ volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v)
+                     : "v"((uint32_t)reinterpret_cast<uintptr_t>(p))
+                     : "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_st(volatile uint32_t* p, uint32_t v) {
+    __asm__ volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)reinterpret_cast<uintptr_t>(p)), "v"(v) : "memory");
+}
 __device__ __forceinline__ uint32_t lds_poll(volatile uint32_t* flag, uint32_t need, uint32_t known) {
     while ((int32_t)(known - need) < 0) {
-        known = __builtin_amdgcn_readfirstlane(*flag);
+        known = __builtin_amdgcn_readfirstlane(lds_ld(flag));
         if ((int32_t)(known - need) < 0) __builtin_amdgcn_s_sleep(1);
     }
     __asm__ volatile("" ::: "memory");
@@ -622,14 +641,14 @@ __device__ __forceinline__ uint32_t lds_poll(volatile uint32_t* flag, uint32_t n
 }
 __device__ __forceinline__ void lds_publish(volatile uint32_t* flag, uint32_t v, uint32_t lane) {
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) *flag = v;
+    if (lane == 0) lds_st(flag, v);
 }
 // As lds_publish for the chunk before the last one: its four row writes are
 // complete once at most the four younger ones (the chunk just written) are
 // outstanding -- the drain of a chunk's writes overlaps the next expansion.
 __device__ __forceinline__ void lds_publish_prev(volatile uint32_t* flag, uint32_t v, uint32_t lane) {
     __asm__ volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-    if (lane == 0) *flag = v;
+    if (lane == 0) lds_st(flag, v);
 }
 
 // K+W[16c .. 16c+15] of a block into its row (kw_expand_store in chunks; w
@@ -682,6 +701,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint32_t s_next[64];
     __shared__ uint32_t s_flag[3], s_cons[2];
     __shared__ uint32_t s_nbx[64];  // fused targets' block counts (the next iteration's max)
+    __shared__ unsigned long long s_stamp[2][64];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* ring = &ring_all[lane * kRing];
@@ -702,6 +722,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         s_flag[0] = s_flag[1] = s_flag[2] = 0;
         s_cons[0] = s_cons[1] = 0;
     }
+    if (a.stamps && threadIdx.x < 128) s_stamp[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     lds_barrier();
     // streamed: next block id, flags seen, a pre-built block 1 of the next job
     uint32_t gb = 0, known = 0, known_c0 = 0, known_c1 = 0, pre_id = ~0u;
@@ -1047,6 +1068,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         }
         if (kStream && wave == kProd) drop_pre();
     }
+    if (a.stamps && blockIdx.x == 0 && (wave == 0 || wave == kProd))
+        a.stamps[128 * a.lvl + 64 * (wave != 0) + lane] = s_stamp[wave != 0][lane];
 }
 
 // Load time: the chaining value after each job's constant leading blocks.
