@@ -710,7 +710,6 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     const bool elane = (hp & 4) == 0;
     const uint32_t ep = elane ? hp : ((hp & 8) | (7 - (hp & 7)));
     const uint32_t jl = wave < 2 ? 32 * wave + 8 * (lane >> 4) + ((ep & 3) | ((ep >> 3) << 2)) : lane;
-    const bool chain = wave < 2;
     uint32_t* const ones = &kw[kBufs * 64 * kPcRow];
     if (wave == 0) {
         __builtin_amdgcn_s_setprio(3);
@@ -741,181 +740,249 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     const uint32_t n = a.counts[a.lvl];
     const uint32_t* lst = a.list + a.s;
-    for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
-        const uint32_t i = base + jl;
-        bool has = i < n;
-        uint32_t p = has ? lst[i] : 0u;
-        uint32_t fslot = ~0u;
-        uint32_t maxnb;
-        {
-            const uint32_t il = base + lane;
-            maxnb = wave_max_small(il < n ? a.meta[2ull * lst[il]].y : 0u);
-        }
-        uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
-        uint4 nt[8];
-        uint2 nr = make_uint2(0, 0);
-        uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
-        uint4 nmlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nmhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
-        uint32_t sk = 0;
-        while (maxnb) {
-            RF_STAMP_PL(sk); ++sk;
-            const bool fused = fslot != ~0u;
-            // a job is fused in every lane that has one after the first pass
-            const bool wfused = __any(fused);
-            uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-            if (has) {
-                if (fused) {
-                    m0 = nm0;
-                    m1 = nm1;
-                    nm0 = nnm0;
-                    nm1 = nnm1;
-                } else {
-                    m0 = a.meta[2 * p];
-                    m1 = a.meta[2 * p + 1];
-                }
+    // One copy of the loop per wave role (chain / producer / expander), each
+    // with only its own state: the register allocator then sizes the kernel
+    // for the largest role instead of the sum of all roles' live values, and
+    // a role's waits no longer cover the other roles' loads in flight.  Every
+    // role runs the same barrier sequence (its control comes from LDS).
+    auto body = [&](auto rc) {
+        constexpr uint32_t R = decltype(rc)::value;
+        constexpr bool kChain = R < 2, kIsProd = R == kProd, kIsExp = R == kExp;
+        for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+            const uint32_t i = base + jl;
+            bool has = i < n;
+            uint32_t p = has ? lst[i] : 0u;
+            uint32_t fslot = ~0u;
+            uint32_t maxnb;
+            {
+                const uint32_t il = base + lane;
+                maxnb = wave_max_small(il < n ? a.meta[2ull * lst[il]].y : 0u);
             }
-            const bool nfu = has && m1.w != ~0u;
-            if (nfu && !fused) {
-                nm0 = a.meta[2ull * m1.w];
-                nm1 = a.meta[2ull * m1.w + 1];
-            }
-            MatCursor cur;
-            uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
-            uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
-            if (!kStream && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
-            if (wave == kProd && has) {
-                cur.fslot = fslot;
-                if (fused) {
-                    cur.flo = s_dig[lane][0];
-                    cur.fhi = s_dig[lane][1];
-                    cur.begin_pre(m0, reinterpret_cast<const uint4*>(a.tmpl), nt, nr, ring);
-                } else {
-                    cur.begin(a, m0, ring);
-                }
-            }
-            // the job's initial chaining value H (IV, or the midstate after its
-            // constant leading blocks): the fused target's was fetched a job ahead
-            uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
-            if (chain && has) {
-                if (fused) {
-                    olo = nolo;
-                    ohi = nohi;
-                    pre[0] = npre[0];
-                    pre[1] = npre[1];
-                    hlo = nmlo;
-                    hhi = nmhi;
-                } else {
-                    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
-                    olo = od[0];
-                    ohi = od[1];
-                    if (m1.y < m1.z) pre[0] = a.cons[m1.y];
-                    if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
-                    if (a.mid) {
-                        hlo = a.mid[2ull * p];
-                        hhi = a.mid[2ull * p + 1];
+            uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
+            uint4 nt[8];
+            uint2 nr = make_uint2(0, 0);
+            uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+            uint4 nmlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nmhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
+            uint32_t sk = 0;
+            while (maxnb) {
+                RF_STAMP_PL(sk); ++sk;
+                const bool fused = fslot != ~0u;
+                // a job is fused in every lane that has one after the first pass
+                const bool wfused = __any(fused);
+                uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+                if (has) {
+                    if (fused) {
+                        m0 = nm0;
+                        m1 = nm1;
+                        nm0 = nnm0;
+                        nm1 = nnm1;
+                    } else {
+                        m0 = a.meta[2 * p];
+                        m1 = a.meta[2 * p + 1];
                     }
                 }
-            }
-            if (kW == 3 && wave == kExp && nfu && nm1.w != ~0u) {
-                nnm0 = a.meta[2ull * nm1.w];
-                nnm1 = a.meta[2ull * nm1.w + 1];
-            }
-            // the chain's lagged state: as after a block whose raw state is zero
-            // with chaining value H (lag_chain.h / k1_sha256_duo, there H = IV)
-            uint32_t Hr0 = elane ? hhi.x : hlo.x, Hr1 = elane ? hhi.y : hlo.y;
-            uint32_t Hr2 = elane ? hhi.z : hlo.z, Hr3 = elane ? hhi.w : hlo.w;
-            uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
-            uint32_t Z = elane ? hhi.w + hlo.w : 0u, Y = 0;
-            uint32_t c63 = 0, c64 = elane ? hlo.z : 0u - hhi.x, c65 = elane ? hlo.y : 0u - hlo.w;
-            // the fusion target's records, issued only after the state above
-            // is built from this job's: a wait for this job's loads must not
-            // also wait for these (they are used one job later).  The empty
-            // asm pins the order (the compiler otherwise sinks the state's
-            // selects below the loads and waits for everything, vmcnt(0)).
-            __asm__ volatile("" ::"v"(Hr0), "v"(Hr1), "v"(Hr2), "v"(Hr3), "v"(Z), "v"(c64), "v"(c65) : "memory");
-            if (chain && has && nfu) {
-                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
-                nolo = od[0];
-                nohi = od[1];
-                if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
-                if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
-                if (nm1.w != ~0u) {
+                const bool nfu = has && m1.w != ~0u;
+                if (nfu && !fused) {
+                    nm0 = a.meta[2ull * m1.w];
+                    nm1 = a.meta[2ull * m1.w + 1];
+                }
+                MatCursor cur;
+                uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
+                uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+                if (!kStream && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                if (kIsProd && has) {
+                    cur.fslot = fslot;
+                    if (fused) {
+                        cur.flo = s_dig[lane][0];
+                        cur.fhi = s_dig[lane][1];
+                        cur.begin_pre(m0, reinterpret_cast<const uint4*>(a.tmpl), nt, nr, ring);
+                    } else {
+                        cur.begin(a, m0, ring);
+                    }
+                }
+                // the job's initial chaining value H (IV, or the midstate after its
+                // constant leading blocks): the fused target's was fetched a job ahead
+                uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
+                if (kChain && has) {
+                    if (fused) {
+                        olo = nolo;
+                        ohi = nohi;
+                        pre[0] = npre[0];
+                        pre[1] = npre[1];
+                        hlo = nmlo;
+                        hhi = nmhi;
+                    } else {
+                        const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+                        olo = od[0];
+                        ohi = od[1];
+                        if (m1.y < m1.z) pre[0] = a.cons[m1.y];
+                        if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+                        if (a.mid) {
+                            hlo = a.mid[2ull * p];
+                            hhi = a.mid[2ull * p + 1];
+                        }
+                    }
+                }
+                if (kIsExp && nfu && nm1.w != ~0u) {
                     nnm0 = a.meta[2ull * nm1.w];
                     nnm1 = a.meta[2ull * nm1.w + 1];
                 }
-                if (a.mid) {
-                    nmlo = a.mid[2ull * m1.w];
-                    nmhi = a.mid[2ull * m1.w + 1];
-                }
-            }
-            uint32_t t0, t1, t2, t3;
-            uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
-            const uint32_t nbl = m0.y;  // this lane's job's blocks (0: no job)
-            // one block step of the chain over block b's rows (group 0 first
-            // finishes block b-1: feed-forward, the a-half's last two rounds)
-            // b: the job's block (capture rule), bufb: its row buffer (kStream:
-            // the global block gb, whose chunks it waits for)
-            auto chain_block = [&](uint32_t b, uint32_t bufb, bool full) {
-                const uint32_t bi = kStream ? bufb % 3 : (bufb & 1);
-                if (kStream && full) known = lds_poll(&s_flag[bi], 4 * bufb + 1, 4 * bufb);
-                if (kStream && full && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
-                const uint32_t row_off = ((bi * 64 + jl) * kPcRow) * 4, ones_off = kBufs * 64 * kPcRow * 4;
-                const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
-                                                                 ((M & ones_off) | (~M & row_off)));
-                uint4 v = r4[0], vn = r4[1];
-                {
-                    const uint32_t k1 = v.y + c64, k2 = v.z + c65;
-                    asm volatile(RF_L2_GROUP0
-                                 : RF_LAG_STATE, RF_L2_TMP, RF_LAG_H,
-                                   [c63] "=&v"(c63), [c64] "+v"(c64), [c65] "+v"(c65)
-                                 : RF_L2_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one),
-                                   [zero] "v"(zero));
-                }
-                if (b == nbl) {  // the job's final chaining value
-                    D0 = Hr0; D1 = Hr1; D2 = Hr2; D3 = Hr3;
-                }
-                if (!full) return;
-                v = vn;
-                vn = r4[2];
-#pragma unroll
-                for (int g = 1; g < 16; ++g) {
-                    uint4 vnn = vn;
-                    if (kStream && (g == 2 || g == 6 || g == 10)) {  // r4[g + 2] opens chunk (g + 2) / 4
-                        known = lds_poll(&s_flag[bi], 4 * bufb + (g + 2) / 4 + 1, known);
-                        if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                // the chain's lagged state: as after a block whose raw state is zero
+                // with chaining value H (lag_chain.h / k1_sha256_duo, there H = IV)
+                uint32_t Hr0 = elane ? hhi.x : hlo.x, Hr1 = elane ? hhi.y : hlo.y;
+                uint32_t Hr2 = elane ? hhi.z : hlo.z, Hr3 = elane ? hhi.w : hlo.w;
+                uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
+                uint32_t Z = elane ? hhi.w + hlo.w : 0u, Y = 0;
+                uint32_t c63 = 0, c64 = elane ? hlo.z : 0u - hhi.x, c65 = elane ? hlo.y : 0u - hlo.w;
+                // the fusion target's records, issued only after the state above
+                // is built from this job's: a wait for this job's loads must not
+                // also wait for these (they are used one job later).  The empty
+                // asm pins the order (the compiler otherwise sinks the state's
+                // selects below the loads and waits for everything, vmcnt(0)).
+                __asm__ volatile("" ::"v"(Hr0), "v"(Hr1), "v"(Hr2), "v"(Hr3), "v"(Z), "v"(c64), "v"(c65) : "memory");
+                if (kChain && has && nfu) {
+                    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
+                    nolo = od[0];
+                    nohi = od[1];
+                    if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
+                    if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
+                    if (nm1.w != ~0u) {
+                        nnm0 = a.meta[2ull * nm1.w];
+                        nnm1 = a.meta[2ull * nm1.w + 1];
                     }
-                    if (g < 14) vnn = r4[g + 2];
-                    const uint32_t k4 = g == 15 ? c63 : vn.x;
-                    asm volatile(RF_L2_GROUP : RF_LAG_STATE, RF_L2_TMP : RF_L2_IN(v.y, v.z, v.w, k4));
-                    v = vn;
-                    vn = vnn;
+                    if (a.mid) {
+                        nmlo = a.mid[2ull * m1.w];
+                        nmhi = a.mid[2ull * m1.w + 1];
+                    }
                 }
-            };
-            if constexpr (kStream) {
-                if (wave == kProd) {
-                    for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
-                        if (gb == pre_id) continue;  // built during the previous job, flag published
-                        if (gb >= 3) {  // buffer gb % 3: both chain waves past block gb - 3
-                            known_c0 = lds_poll(&s_cons[0], gb - 2, known_c0);
-                            known_c1 = lds_poll(&s_cons[1], gb - 2, known_c1);
-                        }
-                        if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
-                        const bool mine = b < m0.y;
-                        uint32_t w[16];
-                        if (mine) cur.block(a, b, ring, w, wfused);
-                        volatile uint32_t* fl = &s_flag[gb % 3];
-                        uint4* row = reinterpret_cast<uint4*>(&kw[((gb % 3) * 64 + lane) * kPcRow]);
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            if (mine) kw_expand_chunk(w, row, c);
-                            if (c == 0)  // the chain starts on it: publish at once
-                                lds_publish(fl, 4 * gb + 1, lane);
-                            else if (c >= 2)  // chunk c - 1, its writes drained behind chunk c's
-                                lds_publish_prev(fl, 4 * gb + c, lane);
+                uint32_t t0, t1, t2, t3;
+                uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+                const uint32_t nbl = m0.y;  // this lane's job's blocks (0: no job)
+                // one block step of the chain over block b's rows (group 0 first
+                // finishes block b-1: feed-forward, the a-half's last two rounds)
+                // b: the job's block (capture rule), bufb: its row buffer (kStream:
+                // the global block gb, whose chunks it waits for)
+                auto chain_block = [&](uint32_t b, uint32_t bufb, bool full) {
+                    const uint32_t bi = kStream ? bufb % 3 : (bufb & 1);
+                    if (kStream && full) known = lds_poll(&s_flag[bi], 4 * bufb + 1, 4 * bufb);
+                    if (kStream && full && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                    const uint32_t row_off = ((bi * 64 + jl) * kPcRow) * 4, ones_off = kBufs * 64 * kPcRow * 4;
+                    const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
+                                                                     ((M & ones_off) | (~M & row_off)));
+                    uint4 v = r4[0], vn = r4[1];
+                    {
+                        const uint32_t k1 = v.y + c64, k2 = v.z + c65;
+                        asm volatile(RF_L2_GROUP0
+                                     : RF_LAG_STATE, RF_L2_TMP, RF_LAG_H,
+                                       [c63] "=&v"(c63), [c64] "+v"(c64), [c65] "+v"(c65)
+                                     : RF_L2_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one),
+                                       [zero] "v"(zero));
+                    }
+                    if (b == nbl) {  // the job's final chaining value
+                        D0 = Hr0; D1 = Hr1; D2 = Hr2; D3 = Hr3;
+                    }
+                    if (!full) return;
+                    v = vn;
+                    vn = r4[2];
+    #pragma unroll
+                    for (int g = 1; g < 16; ++g) {
+                        uint4 vnn = vn;
+                        if (kStream && (g == 2 || g == 6 || g == 10)) {  // r4[g + 2] opens chunk (g + 2) / 4
+                            known = lds_poll(&s_flag[bi], 4 * bufb + (g + 2) / 4 + 1, known);
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                         }
-                        lds_publish(fl, 4 * gb + 4, lane);
-                        if (b == 0 && nfu) {
+                        if (g < 14) vnn = r4[g + 2];
+                        const uint32_t k4 = g == 15 ? c63 : vn.x;
+                        asm volatile(RF_L2_GROUP : RF_LAG_STATE, RF_L2_TMP : RF_L2_IN(v.y, v.z, v.w, k4));
+                        v = vn;
+                        vn = vnn;
+                    }
+                };
+                if constexpr (kStream) {
+                    if (kIsProd) {
+                        for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
+                            if (gb == pre_id) continue;  // built during the previous job, flag published
+                            if (gb >= 3) {  // buffer gb % 3: both chain waves past block gb - 3
+                                known_c0 = lds_poll(&s_cons[0], gb - 2, known_c0);
+                                known_c1 = lds_poll(&s_cons[1], gb - 2, known_c1);
+                            }
+                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            const bool mine = b < m0.y;
+                            uint32_t w[16];
+                            if (mine) cur.block(a, b, ring, w, wfused);
+                            volatile uint32_t* fl = &s_flag[gb % 3];
+                            uint4* row = reinterpret_cast<uint4*>(&kw[((gb % 3) * 64 + lane) * kPcRow]);
+    #pragma unroll
+                            for (int c = 0; c < 4; ++c) {
+                                if (mine) kw_expand_chunk(w, row, c);
+                                if (c == 0)  // the chain starts on it: publish at once
+                                    lds_publish(fl, 4 * gb + 1, lane);
+                                else if (c >= 2)  // chunk c - 1, its writes drained behind chunk c's
+                                    lds_publish_prev(fl, 4 * gb + c, lane);
+                                if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            }
+                            lds_publish(fl, 4 * gb + 4, lane);
+                            if (b == 0 && nfu) {
+                                const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
+                                nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
+                                if (nm0.y > 1) {
+                                    nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
+                                }
+                                nr = a.holes[nm0.z];
+                                if (nm1.w != ~0u) {
+                                    nnm0 = a.meta[2ull * nm1.w];
+                                    nnm1 = a.meta[2ull * nm1.w + 1];
+                                }
+                            }
+                            RF_STAMP_PL(sk); ++sk;
+                        }
+                        // idle until the hand-over: build the fusion targets' block 1
+                        // (the next job's second id) if every lane whose target has
+                        // a block 1 can -- it holds no hole (the fused digest ends
+                        // in block 0) and the target has exactly two blocks
+                        const bool need = nfu && nm0.y >= 2;
+                        const bool can = nm0.y == 2 && nr.x + 32 <= 64;
+                        drop_pre();
+                        if (__any(need) && __all(!need || can)) {
+                            const uint32_t id1 = gb + 1;
+                            known_c0 = lds_poll(&s_cons[0], id1 - 2, known_c0);
+                            known_c1 = lds_poll(&s_cons[1], id1 - 2, known_c1);
+                            uint4* row = reinterpret_cast<uint4*>(&kw[((id1 % 3) * 64 + lane) * kPcRow]);
+                            if (need) {
+                                uint32_t w[16] = {nt[4].x, nt[4].y, nt[4].z, nt[4].w, nt[5].x, nt[5].y, nt[5].z, nt[5].w,
+                                                  nt[6].x, nt[6].y, nt[6].z, nt[6].w, nt[7].x, nt[7].y, nt[7].z, nt[7].w};
+    #pragma unroll
+                                for (int q = 0; q < 16; ++q) w[q] = bswap32(w[q]);
+    #pragma unroll
+                                for (int c = 0; c < 4; ++c) kw_expand_chunk(w, row, c);
+                            }
+                            lds_publish(&s_flag[id1 % 3], 4 * id1 + 4, lane);
+                            pre_id = id1;
+                        }
+                    } else {
+                        for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
+                            chain_block(b, gb, true);
+                            lds_publish(&s_cons[wave], gb + 1, lane);
+                            RF_STAMP_PL(sk); ++sk;
+                        }
+                    }
+                } else {
+                for (uint32_t it = 0; it < maxnb + lag; ++it) {
+                    if (kIsProd) {
+                        if (it < m0.y && !((a.dbg_twice == 3 && it >= 1) || a.dbg_twice == 4)) {
+                            uint32_t w[16];
+                            cur.block(a, it, ring, w, wfused);
+                            if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
+                            if (kW == 2) {
+                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
+                            } else {
+                                uint4* row = reinterpret_cast<uint4*>(&wbuf[((it & 1) * 64 + lane) * kWRow]);
+    #pragma unroll
+                                for (int q = 0; q < 4; ++q)
+                                    row[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+                            }
+                        }
+                        if (it == 0 && nfu) {
                             const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
                             nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
                             if (nm0.y > 1) {
@@ -927,146 +994,94 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 nnm1 = a.meta[2ull * nm1.w + 1];
                             }
                         }
-                        RF_STAMP_PL(sk); ++sk;
-                    }
-                    // idle until the hand-over: build the fusion targets' block 1
-                    // (the next job's second id) if every lane whose target has
-                    // a block 1 can -- it holds no hole (the fused digest ends
-                    // in block 0) and the target has exactly two blocks
-                    const bool need = nfu && nm0.y >= 2;
-                    const bool can = nm0.y == 2 && nr.x + 32 <= 64;
-                    drop_pre();
-                    if (__any(need) && __all(!need || can)) {
-                        const uint32_t id1 = gb + 1;
-                        known_c0 = lds_poll(&s_cons[0], id1 - 2, known_c0);
-                        known_c1 = lds_poll(&s_cons[1], id1 - 2, known_c1);
-                        uint4* row = reinterpret_cast<uint4*>(&kw[((id1 % 3) * 64 + lane) * kPcRow]);
-                        if (need) {
-                            uint32_t w[16] = {nt[4].x, nt[4].y, nt[4].z, nt[4].w, nt[5].x, nt[5].y, nt[5].z, nt[5].w,
-                                              nt[6].x, nt[6].y, nt[6].z, nt[6].w, nt[7].x, nt[7].y, nt[7].z, nt[7].w};
-#pragma unroll
-                            for (int q = 0; q < 16; ++q) w[q] = bswap32(w[q]);
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) kw_expand_chunk(w, row, c);
+                    } else if (kIsExp) {
+                        if (it >= 1 && it - 1 < m0.y && !((a.dbg_twice == 3 && it >= 2) || a.dbg_twice == 4)) {
+                            const uint32_t bb = (it - 1) & 1;
+                            const uint4* row = reinterpret_cast<const uint4*>(&wbuf[(bb * 64 + lane) * kWRow]);
+                            uint32_t w[16];
+    #pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const uint4 v = row[q];
+                                w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+                            }
+                            kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(bb * 64 + lane) * kPcRow]));
                         }
-                        lds_publish(&s_flag[id1 % 3], 4 * id1 + 4, lane);
-                        pre_id = id1;
+                    } else if (kChain && it >= lag) {
+                        chain_block(it - lag, it - lag, true);
                     }
-                } else {
-                    for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
-                        chain_block(b, gb, true);
-                        lds_publish(&s_cons[wave], gb + 1, lane);
-                        RF_STAMP_PL(sk); ++sk;
+                    lds_barrier();
+                    RF_STAMP_PL(sk); ++sk;
+                }
+                }
+                bool changed = false;
+                const bool own = kChain && has && elane;
+                if (kChain) {
+                    // The fusion target's prefetched records (issued at this job's
+                    // start, blocks ago: arrived) are made to count as arrived here,
+                    // before the digest store and frontier atomics: vmcnt also counts
+                    // those, so a wait for the records at the next job's start would
+                    // otherwise be a vmcnt(0) that waits for the store's HBM ack.
+                    __asm__ volatile("" ::"v"(nolo.x), "v"(nolo.y), "v"(nolo.z), "v"(nolo.w), "v"(nohi.x), "v"(nohi.y),
+                                     "v"(nohi.z), "v"(nohi.w), "v"(npre[0].x), "v"(npre[0].y), "v"(npre[1].x),
+                                     "v"(npre[1].y), "v"(nmlo.x), "v"(nmlo.y), "v"(nmlo.z), "v"(nmlo.w));
+                    __asm__ volatile("" ::"v"(nmhi.x), "v"(nmhi.y), "v"(nmhi.z), "v"(nmhi.w), "v"(nnm0.x), "v"(nnm0.y),
+                                     "v"(nnm0.z), "v"(nnm0.w), "v"(nnm1.x), "v"(nnm1.y), "v"(nnm1.z), "v"(nnm1.w),
+                                     "v"(nm0.x), "v"(nm0.y), "v"(nm0.z), "v"(nm0.w));
+                    __asm__ volatile("" ::"v"(nm1.x), "v"(nm1.y), "v"(nm1.z), "v"(nm1.w));
+                    chain_block(maxnb, kStream ? gb : maxnb, false);  // group 0 of block maxnb: the longest jobs' final value
+                    // the a-lane's half (H0..H3) into its e-lane (H4..H7 there)
+                    ShaState st;
+                    st.h[0] = __builtin_amdgcn_mov_dpp((int)D0, 0x141, 0xf, 0xf, true);
+                    st.h[1] = __builtin_amdgcn_mov_dpp((int)D1, 0x141, 0xf, 0xf, true);
+                    st.h[2] = __builtin_amdgcn_mov_dpp((int)D2, 0x141, 0xf, 0xf, true);
+                    st.h[3] = __builtin_amdgcn_mov_dpp((int)D3, 0x141, 0xf, 0xf, true);
+                    st.h[4] = D0; st.h[5] = D1; st.h[6] = D2; st.h[7] = D3;
+                    uint32_t next = ~0u, nbn = 0;
+                    if (own) {
+                        changed = finish_job_pre(a, m1, st, olo, ohi);
+                        if (changed && m1.w != ~0u) {
+                            next = m1.w;
+                            nbn = nm0.y;
+                            s_dig[jl][0] = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
+                                                      bswap32(st.h[3]));
+                            s_dig[jl][1] = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]),
+                                                      bswap32(st.h[7]));
+                        }
+                    }
+                    if (elane) {
+                        s_next[jl] = next;
+                        s_nbx[jl] = nbn;
                     }
                 }
-            } else {
-            for (uint32_t it = 0; it < maxnb + lag; ++it) {
-                if (wave == kProd) {
-                    if (it < m0.y && !((a.dbg_twice == 3 && it >= 1) || a.dbg_twice == 4)) {
-                        uint32_t w[16];
-                        cur.block(a, it, ring, w, wfused);
-                        if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
-                        if (kW == 2) {
-                            kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
-                        } else {
-                            uint4* row = reinterpret_cast<uint4*>(&wbuf[((it & 1) * 64 + lane) * kWRow]);
-#pragma unroll
-                            for (int q = 0; q < 4; ++q)
-                                row[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-                        }
-                    }
-                    if (it == 0 && nfu) {
-                        const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
-                        nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
-                        if (nm0.y > 1) {
-                            nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
-                        }
-                        nr = a.holes[nm0.z];
-                        if (nm1.w != ~0u) {
-                            nnm0 = a.meta[2ull * nm1.w];
-                            nnm1 = a.meta[2ull * nm1.w + 1];
-                        }
-                    }
-                } else if (kW == 3 && wave == kExp) {
-                    if (it >= 1 && it - 1 < m0.y && !((a.dbg_twice == 3 && it >= 2) || a.dbg_twice == 4)) {
-                        const uint32_t bb = (it - 1) & 1;
-                        const uint4* row = reinterpret_cast<const uint4*>(&wbuf[(bb * 64 + lane) * kWRow]);
-                        uint32_t w[16];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const uint4 v = row[q];
-                            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-                        }
-                        kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(bb * 64 + lane) * kPcRow]));
-                    }
-                } else if (chain && it >= lag) {
-                    chain_block(it - lag, it - lag, true);
-                }
+                RF_STAMP_PL(sk); ++sk;
                 lds_barrier();
                 RF_STAMP_PL(sk); ++sk;
-            }
-            }
-            bool changed = false;
-            const bool own = chain && has && elane;
-            if (chain) {
-                // The fusion target's prefetched records (issued at this job's
-                // start, blocks ago: arrived) are made to count as arrived here,
-                // before the digest store and frontier atomics: vmcnt also counts
-                // those, so a wait for the records at the next job's start would
-                // otherwise be a vmcnt(0) that waits for the store's HBM ack.
-                __asm__ volatile("" ::"v"(nolo.x), "v"(nolo.y), "v"(nolo.z), "v"(nolo.w), "v"(nohi.x), "v"(nohi.y),
-                                 "v"(nohi.z), "v"(nohi.w), "v"(npre[0].x), "v"(npre[0].y), "v"(npre[1].x),
-                                 "v"(npre[1].y), "v"(nmlo.x), "v"(nmlo.y), "v"(nmlo.z), "v"(nmlo.w));
-                __asm__ volatile("" ::"v"(nmhi.x), "v"(nmhi.y), "v"(nmhi.z), "v"(nmhi.w), "v"(nnm0.x), "v"(nnm0.y),
-                                 "v"(nnm0.z), "v"(nnm0.w), "v"(nnm1.x), "v"(nnm1.y), "v"(nnm1.z), "v"(nnm1.w),
-                                 "v"(nm0.x), "v"(nm0.y), "v"(nm0.z), "v"(nm0.w));
-                __asm__ volatile("" ::"v"(nm1.x), "v"(nm1.y), "v"(nm1.z), "v"(nm1.w));
-                chain_block(maxnb, kStream ? gb : maxnb, false);  // group 0 of block maxnb: the longest jobs' final value
-                // the a-lane's half (H0..H3) into its e-lane (H4..H7 there)
-                ShaState st;
-                st.h[0] = __builtin_amdgcn_mov_dpp((int)D0, 0x141, 0xf, 0xf, true);
-                st.h[1] = __builtin_amdgcn_mov_dpp((int)D1, 0x141, 0xf, 0xf, true);
-                st.h[2] = __builtin_amdgcn_mov_dpp((int)D2, 0x141, 0xf, 0xf, true);
-                st.h[3] = __builtin_amdgcn_mov_dpp((int)D3, 0x141, 0xf, 0xf, true);
-                st.h[4] = D0; st.h[5] = D1; st.h[6] = D2; st.h[7] = D3;
-                uint32_t next = ~0u, nbn = 0;
-                if (own) {
-                    changed = finish_job_pre(a, m1, st, olo, ohi);
-                    if (changed && m1.w != ~0u) {
-                        next = m1.w;
-                        nbn = nm0.y;
-                        s_dig[jl][0] = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
-                                                  bswap32(st.h[3]));
-                        s_dig[jl][1] = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]),
-                                                  bswap32(st.h[7]));
+                const uint32_t nx = s_next[jl];
+                maxnb = wave_max_small(s_nbx[lane]);
+                if (kChain) {
+                    uint32_t cb = 0, ce = 0;
+                    if (own) {
+                        atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                        cb = m1.y;
+                        ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
                     }
+                    propagate_pre(a, cb, ce, pre);
+                    const uint64_t fb = __ballot(own && nx != ~0u);
+                    if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
                 }
-                if (elane) {
-                    s_next[jl] = next;
-                    s_nbx[jl] = nbn;
-                }
+                fslot = has ? m1.x : ~0u;
+                has = nx != ~0u;
+                p = has ? nx : 0u;
             }
-            RF_STAMP_PL(sk); ++sk;
-            lds_barrier();
-            RF_STAMP_PL(sk); ++sk;
-            const uint32_t nx = s_next[jl];
-            maxnb = wave_max_small(s_nbx[lane]);
-            if (chain) {
-                uint32_t cb = 0, ce = 0;
-                if (own) {
-                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
-                    cb = m1.y;
-                    ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
-                }
-                propagate_pre(a, cb, ce, pre);
-                const uint64_t fb = __ballot(own && nx != ~0u);
-                if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
-            }
-            fslot = has ? m1.x : ~0u;
-            has = nx != ~0u;
-            p = has ? nx : 0u;
+            if (kStream && kIsProd) drop_pre();
         }
-        if (kStream && wave == kProd) drop_pre();
+    };
+    if (wave < 2) {
+        body(std::integral_constant<uint32_t, 0>{});
+    } else if (wave == kProd) {
+        body(std::integral_constant<uint32_t, kProd>{});
+    } else {
+        if constexpr (kW == 3) body(std::integral_constant<uint32_t, kExp>{});
     }
     if (a.stamps && blockIdx.x == 0 && (wave == 0 || wave == kProd))
         a.stamps[128 * a.lvl + 64 * (wave != 0) + lane] = s_stamp[wave != 0][lane];
