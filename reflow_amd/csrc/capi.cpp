@@ -1201,6 +1201,34 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
             }
         }
     }
+    // Slot fusion: an input slot's consumer whose only hole is that slot
+    // depends on nothing else, so the lane that writes the slot (k3_mark_slots,
+    // k_part_apply) hashes it -- and its fusion chain -- at once instead of
+    // queueing it.  At most one per slot, moved to the front of the slot's
+    // range and flagged there (kSlotFused).  Jobs without holes can never be
+    // queued either.  RF_K2_SLOT_FUSE=0: off (A/B).
+    std::vector<uint8_t> slot_fused(J, 0);
+    {
+        static const bool on = [] {
+            const char* v = getenv("RF_K2_SLOT_FUSE");
+            return !(v && atoi(v) == 0);
+        }();
+        if (on)
+            for (uint32_t s = 0; s < S; ++s) {
+                if (gr->producer[s] >= 0) continue;
+                for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
+                    const uint32_t k = cjob[c];
+                    if (d->hole_ptr[k + 1] - d->hole_ptr[k] == 1 && !slot_fused[k]) {
+                        slot_fused[k] = 1;
+                        std::swap(cjob[c], cjob[cptr[s]]);
+                        break;
+                    }
+                }
+            }
+    }
+    auto queueable = [&](uint32_t j) {
+        return !fused_target[j] && !slot_fused[j] && d->hole_ptr[j + 1] > d->hole_ptr[j];
+    };
     // Sinks (jobs nothing reads: physical cache keys, roots) may run at any
     // level after their inputs: move them to the last level that launches
     // anyway (one holding queueable non-sink jobs), where they fill their own
@@ -1215,10 +1243,10 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         auto sink = [&](uint32_t j) { return cptr[d->out_slot[j]] == cptr[d->out_slot[j] + 1]; };
         int64_t lq = -1;
         for (uint32_t j = 0; j < J; ++j)
-            if (!fused_target[j] && !sink(j)) lq = std::max<int64_t>(lq, level[j]);
+            if (queueable(j) && !sink(j)) lq = std::max<int64_t>(lq, level[j]);
         if (alap && lq > 0)
             for (uint32_t j = 0; j < J; ++j)
-                if (!fused_target[j] && sink(j) && level[j] < (uint32_t)lq) level[j] = (uint32_t)lq;
+                if (queueable(j) && sink(j) && level[j] < (uint32_t)lq) level[j] = (uint32_t)lq;
     }
     // internal order: level ascending, blocks descending (similar lanes per wave)
     std::vector<uint32_t> perm(J);
@@ -1289,7 +1317,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     for (uint32_t s = 0; s <= S; ++s) cons_ptr[s] = (uint32_t)cptr[s];
     for (uint64_t c = 0; c < H; ++c) {
         cons_job[2 * c] = gr->ext2int[cjob[c]];
-        cons_job[2 * c + 1] = level[cjob[c]];
+        cons_job[2 * c + 1] = level[cjob[c]] | (slot_fused[cjob[c]] ? 0x80000000u : 0u);  // kSlotFused
     }
     gr->hole_count = H;
     // 1: the level has queueable jobs (k2_level_pc<2>); 2: they average at
@@ -1305,7 +1333,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         // here run in their own short workgroups, the chains set the shape
         std::vector<uint64_t> qj(L, 0), qb(L, 0), qall(L, 0);
         for (uint32_t j = 0; j < J; ++j)
-            if (!fused_target[j]) {
+            if (queueable(j)) {
                 qall[level[j]] += 1;
                 if (cptr[d->out_slot[j]] == cptr[d->out_slot[j] + 1]) continue;  // a sink
                 qj[level[j]] += 1;
@@ -2021,9 +2049,7 @@ static int assoc_put_locked(rf_assoc* a, int kind, const uint8_t* d_exp, const u
     HIPC(launch_dedup(d_keys, (uint32_t)n, ctx->d_tab.as<uint32_t>(), ctx->d_tab2.as<uint32_t>(), canon, d_nu, s));
     HIPC(launch_assoc_insert(a->view(), (uint32_t)kind, d_keys, canon, (uint32_t)n, a->b_aslot.as<uint32_t>(), s));
     // ops in batch order per key: round r applies each key's r-th op
-    std::vector<uint32_t> iota(n);
-    std::iota(iota.begin(), iota.end(), 0u);
-    HIPC(hipMemcpyAsync(a->b_rem.p, iota.data(), 4 * n, hipMemcpyHostToDevice, s));
+    HIPC(launch_iota(a->b_rem.as<uint32_t>(), (uint32_t)n, s));
     HIPC(hipMemsetAsync(a->b_cls.p, 0, 8 * n, s));
     uint32_t* cnt = a->b_cnt.as<uint32_t>();  // cnt[0] = remaining, cnt[1] = next
     uint32_t n_rem = (uint32_t)n;

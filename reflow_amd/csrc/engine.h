@@ -102,14 +102,8 @@ struct MarkArgs {
     const uint32_t* sl;
     const uint8_t* dig;
     uint32_t n;
-    uint8_t* slots;
-    const uint32_t* cons_ptr;
-    const uint2* cons;
-    uint32_t* dirty;
-    uint32_t* list;
-    uint32_t* counts;
-    const uint32_t* ls;
-    void* ptrs[10];
+    alignas(16) unsigned char a[160];  // the kernel's LevelArgs (k2_graph.hip), by value
+    void* ptrs[4];
 };
 void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,
                        MarkArgs* args, hipKernelNodeParams* p);
@@ -180,6 +174,7 @@ hipError_t launch_assoc_select(const uint8_t* found, const uint8_t* vals, const 
 hipError_t launch_assoc_abbrev(const AssocView& t, uint32_t kind, uint32_t cap, const uint8_t* qkeys,
                                const uint8_t* nhex, uint32_t q, uint32_t* matches, uint32_t* hit_slot,
                                hipStream_t s);
+hipError_t launch_iota(uint32_t* out, uint32_t n, hipStream_t s);
 hipError_t launch_assoc_rehash(const AssocView& from, uint32_t cap_from, const AssocView& to, hipStream_t s);
 
 }  // namespace rf

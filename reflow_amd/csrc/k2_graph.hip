@@ -27,6 +27,7 @@
 // propagates.  A level's jobs all depend only on lower levels, so a level's
 // list is complete when its kernel starts.
 #include <cstdlib>
+#include <cstring>
 
 #include "engine.h"
 #include "sha256_dev.h"
@@ -53,7 +54,14 @@ struct LevelArgs {
     uint32_t* counts;
     unsigned long long* stamps;  // diagnostic (RF_K2_STAMPS): phase times of workgroup 0, else null
     const uint4* __restrict__ mid;  // [2J] initial chaining values, or null (= IV for every job)
+    const uint32_t* __restrict__ cons_ptr;  // [S+1] slot -> reverse-edge range (mark / apply kernels)
 };
+
+// Reverse edges of an INPUT slot: bit 31 of the level field flags its
+// slot-fused consumer (at most one, first in the slot's range): a job whose
+// only hole is that slot, hashed by the lane that writes the slot
+// (mark_input_slot) instead of being queued (rf_graph_load).
+constexpr uint32_t kSlotFused = 0x80000000u;
 
 // A job's initial chaining value (GraphDev::mid).
 __device__ __forceinline__ void init_state(const LevelArgs& a, uint32_t p, ShaState& st) {
@@ -1111,32 +1119,149 @@ __global__ __launch_bounds__(256) void k2_midstates(const uint8_t* __restrict__ 
     }
 }
 
-// set_slots: write input digests; a changed slot queues its consumers.
-__global__ __launch_bounds__(256) void k3_mark_slots(const uint32_t* __restrict__ sl,
-                                                     const uint8_t* __restrict__ dig, uint32_t n,
-                                                     uint8_t* slots, const uint32_t* __restrict__ cons_ptr,
-                                                     const uint2* __restrict__ cons, uint32_t* dirty,
-                                                     uint32_t* list, uint32_t* counts,
-                                                     const uint32_t* __restrict__ ls) {
+// A changed input slot s (digest nlo/nhi, already stored; cp0/cp1 its
+// reverse-edge range): its consumers join their levels' lists, except the
+// slot-fused one, which this lane hashes at once (one-lane SHA-256, the new
+// digest handed over in registers) and follows through its fusion chain like
+// the level kernels do -- never queued, so a level whose queueable jobs are
+// all slot-fused is not launched (configs[2]: every leaf OpVal and its
+// Coerce; before, a mark kernel, a launch gap and a level kernel whose list ->
+// record -> hole -> digest loads started cold).  Each job of the chain starts
+// with its record, first two template blocks, hole record, old digest and
+// start state in registers: they and the next job's record are fetched while
+// the job before it is hashed.  Called by every lane of the wave.
+__device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ring, bool changed, uint32_t s,
+                                                const uint4& nlo, const uint4& nhi, uint32_t cp0, uint32_t cp1) {
+    constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    const uint4* T4 = reinterpret_cast<const uint4*>(a.tmpl);
+    uint32_t c = changed ? cp0 : 0u, ce = changed ? cp1 : 0u, p = ~0u;
+    const uint2 f = a.cons[c < ce ? c : 0u];
+    if (c < ce && (f.y & kSlotFused)) {
+        p = f.x;
+        ++c;
+    }
+    // the job's operands (fetched a job ahead after the first)
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, nm0 = m0, nm1 = m0, olo = m0, ohi = m0;
+    uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
+    uint4 t[8];
+    uint2 r = make_uint2(~0u, 0u);
+    auto fetch = [&](uint32_t q, const uint4& q0, const uint4& q1, uint4 (&tt)[8], uint2& rr, uint4& ol, uint4& oh,
+                     uint4& hl, uint4& hh) {
+        const uint4* T = T4 + 4ull * q0.x;
+        tt[0] = T[0]; tt[1] = T[1]; tt[2] = T[2]; tt[3] = T[3];
+        if (q0.y > 1) {
+            tt[4] = T[4]; tt[5] = T[5]; tt[6] = T[6]; tt[7] = T[7];
+        }
+        rr = a.holes[q0.z];
+        const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * q1.x);
+        ol = od[0];
+        oh = od[1];
+        if (a.mid) {
+            hl = a.mid[2ull * q];
+            hh = a.mid[2ull * q + 1];
+        }
+    };
+    if (p != ~0u) {
+        m0 = a.meta[2ull * p];
+        m1 = a.meta[2ull * p + 1];
+        fetch(p, m0, m1, t, r, olo, ohi, hlo, hhi);
+        if (m1.w != ~0u) {
+            nm0 = a.meta[2ull * m1.w];
+            nm1 = a.meta[2ull * m1.w + 1];
+        }
+    }
+    uint32_t fslot = s, hashed = 0;
+    uint4 flo = nlo, fhi = nhi;
+    while (__any(p != ~0u)) {
+        uint32_t cb = 0, cz = 0, nx = ~0u;
+        if (p != ~0u) {
+            const bool nf = m1.w != ~0u;
+            uint4 nt[8], nolo = olo, nohi = ohi;
+            uint4 nhlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nhhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
+            uint2 nr = r;
+            uint4 nnm0 = nm0, nnm1 = nm1;
+            if (nf) {
+                fetch(m1.w, nm0, nm1, nt, nr, nolo, nohi, nhlo, nhhi);
+                if (nm1.w != ~0u) {
+                    nnm0 = a.meta[2ull * nm1.w];
+                    nnm1 = a.meta[2ull * nm1.w + 1];
+                }
+            }
+            MatCursor cur;
+            cur.fslot = fslot;
+            cur.flo = flo;
+            cur.fhi = fhi;
+            cur.begin_pre(m0, T4, t, r, ring);
+            ShaState st;
+            st.h[0] = hlo.x; st.h[1] = hlo.y; st.h[2] = hlo.z; st.h[3] = hlo.w;
+            st.h[4] = hhi.x; st.h[5] = hhi.y; st.h[6] = hhi.z; st.h[7] = hhi.w;
+            for (uint32_t b = 0; b < cur.nb; ++b) {
+                uint32_t w[16];
+                cur.block(a, b, ring, w, true);
+                sha256_compress(st, w);
+            }
+            const bool ch = finish_job_pre(a, m1, st, olo, ohi);
+            ++hashed;
+            cb = m1.y;
+            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
+            if (ch && nf) {
+                nx = m1.w;
+                fslot = m1.x;
+                flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+                m0 = nm0;
+                m1 = nm1;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) t[q] = nt[q];
+                r = nr;
+                olo = nolo;
+                ohi = nohi;
+                hlo = nhlo;
+                hhi = nhhi;
+                nm0 = nnm0;
+                nm1 = nnm1;
+            }
+        }
+        propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, cb, cz);
+        p = nx;
+    }
+    // the slot's other consumers
+    propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, c, ce);
+    // counts[L]: jobs hashed outside the level lists (k3_step_end)
+    for (int o = 32; o > 0; o >>= 1) hashed += __shfl_xor(hashed, o, 64);
+    if (__lane_id() == 0 && hashed) atomicAdd(&a.counts[a.n_levels], hashed);
+}
+
+constexpr uint32_t kMarkBlock = 256;
+
+// set_slots: write input digests; a changed slot queues (or hashes) its consumers.
+__global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __restrict__ sl,
+                                                            const uint8_t* __restrict__ dig, uint32_t n, LevelArgs a) {
+    __shared__ uint32_t ring_all[kMarkBlock * kRing];
+    uint32_t* ring = &ring_all[threadIdx.x * kRing];
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
-        uint32_t c = 0, ce = 0;
+        bool changed = false;
+        uint32_t s = 0, cp0 = 0, cp1 = 0;
+        uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
         if (i < n) {
-            const uint32_t s = sl[i];
+            s = sl[i];
             const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
-            uint4* dst = reinterpret_cast<uint4*>(slots + 32ull * s);
-            const uint4 nlo = src[0], nhi = src[1], olo = dst[0], ohi = dst[1];
-            const bool changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) |
-                                 (olo.w != nlo.w) | (ohi.x != nhi.x) | (ohi.y != nhi.y) |
-                                 (ohi.z != nhi.z) | (ohi.w != nhi.w);
+            uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
+            nlo = src[0];
+            nhi = src[1];
+            cp0 = a.cons_ptr[s];  // with the digests, not after the compare
+            cp1 = a.cons_ptr[s + 1];
+            const uint4 olo = dst[0], ohi = dst[1];
+            changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                      (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
             if (changed) {
                 dst[0] = nlo;
                 dst[1] = nhi;
-                c = cons_ptr[s];
-                ce = cons_ptr[s + 1];
             }
         }
-        propagate(cons, dirty, list, counts, ls, c, ce);
+        mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
     }
 }
 
@@ -1189,34 +1314,37 @@ __global__ __launch_bounds__(256) void k_part_any(const uint64_t* __restrict__ b
 
 // Imports whose boundary bit is set: the gathered digest into the slot; a
 // changed slot queues its local consumers (as k3_mark_slots).
-__global__ __launch_bounds__(256) void k_part_apply(const uint32_t* __restrict__ import_slot,
-                                                    const uint32_t* __restrict__ import_bid, uint32_t n,
-                                                    const uint32_t* __restrict__ bits,
-                                                    const uint8_t* __restrict__ gather, uint8_t* slots,
-                                                    const uint32_t* __restrict__ cons_ptr,
-                                                    const uint2* __restrict__ cons, uint32_t* dirty, uint32_t* list,
-                                                    uint32_t* counts, const uint32_t* __restrict__ ls) {
+__global__ __launch_bounds__(kMarkBlock) void k_part_apply(const uint32_t* __restrict__ import_slot,
+                                                           const uint32_t* __restrict__ import_bid, uint32_t n,
+                                                           const uint32_t* __restrict__ bits,
+                                                           const uint8_t* __restrict__ gather, LevelArgs a) {
+    __shared__ uint32_t ring_all[kMarkBlock * kRing];
+    uint32_t* ring = &ring_all[threadIdx.x * kRing];
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
-        uint32_t c = 0, ce = 0;
+        bool changed = false;
+        uint32_t s = 0, cp0 = 0, cp1 = 0;
+        uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
         if (i < n) {
             const uint32_t b = import_bid[i];
             if ((bits[b >> 5] >> (b & 31)) & 1u) {
-                const uint32_t s = import_slot[i];
+                s = import_slot[i];
                 const uint4* src = reinterpret_cast<const uint4*>(gather + 32ull * b);
-                uint4* dst = reinterpret_cast<uint4*>(slots + 32ull * s);
-                const uint4 nlo = src[0], nhi = src[1], olo = dst[0], ohi = dst[1];
-                const bool changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
-                                     (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
+                uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
+                nlo = src[0];
+                nhi = src[1];
+                cp0 = a.cons_ptr[s];
+                cp1 = a.cons_ptr[s + 1];
+                const uint4 olo = dst[0], ohi = dst[1];
+                changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                          (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
                 if (changed) {
                     dst[0] = nlo;
                     dst[1] = nhi;
-                    c = cons_ptr[s];
-                    ce = cons_ptr[s + 1];
                 }
             }
         }
-        propagate(cons, dirty, list, counts, ls, c, ce);
+        mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
     }
 }
 
@@ -1259,11 +1387,18 @@ static uint32_t grid_for(uint64_t items, uint32_t cap) {
     return (uint32_t)g;
 }
 
+// The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
+static LevelArgs mark_level_args(const GraphDev& g) {
+    LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr};
+    return a;
+}
+
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k3_mark_slots, dim3(grid_for(n, 4096)), dim3(256), 0, s, slots, digests, n,
-                       g.slots, g.cons_ptr, g.cons, g.dirty, g.list, g.counts, g.lvl_start_dev);
+    hipLaunchKernelGGL(k3_mark_slots, dim3(grid_for(n, 4096)), dim3(kMarkBlock), 0, s, slots, digests, n,
+                       mark_level_args(g));
     return hipGetLastError();
 }
 
@@ -1271,22 +1406,17 @@ hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, con
 // its launch parameters for this batch, argument values in `args`.
 void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,
                        MarkArgs* args, hipKernelNodeParams* p) {
+    static_assert(sizeof(MarkArgs::a) >= sizeof(LevelArgs), "MarkArgs::a holds the mark kernel's LevelArgs");
     args->sl = slots;
     args->dig = digests;
     args->n = n;
-    args->slots = g.slots;
-    args->cons_ptr = g.cons_ptr;
-    args->cons = g.cons;
-    args->dirty = g.dirty;
-    args->list = g.list;
-    args->counts = g.counts;
-    args->ls = g.lvl_start_dev;
-    void* v[10] = {&args->sl, &args->dig, &args->n, &args->slots, &args->cons_ptr, &args->cons,
-                   &args->dirty, &args->list, &args->counts, &args->ls};
-    for (int i = 0; i < 10; ++i) args->ptrs[i] = v[i];
+    const LevelArgs a = mark_level_args(g);
+    memcpy(args->a, &a, sizeof(a));
+    void* v[4] = {&args->sl, &args->dig, &args->n, args->a};
+    for (int i = 0; i < 4; ++i) args->ptrs[i] = v[i];
     p->func = reinterpret_cast<void*>(k3_mark_slots);
     p->gridDim = dim3(n ? grid_for(n, 4096) : 1);  // an empty batch still runs (and marks nothing)
-    p->blockDim = dim3(256);
+    p->blockDim = dim3(kMarkBlock);
     p->sharedMemBytes = 0;
     p->kernelParams = args->ptrs;
     p->extra = nullptr;
@@ -1305,7 +1435,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                                  : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
                                                               : 0u;
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
@@ -1377,8 +1507,8 @@ hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, const uint32_t
 hipError_t launch_part_apply(const GraphDev& g, const uint32_t* import_slot, const uint32_t* import_bid, uint32_t n,
                              const uint32_t* bits, const uint8_t* gather, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_part_apply, dim3(grid_for(n, 4096)), dim3(256), 0, s, import_slot, import_bid, n, bits,
-                       gather, g.slots, g.cons_ptr, g.cons, g.dirty, g.list, g.counts, g.lvl_start_dev);
+    hipLaunchKernelGGL(k_part_apply, dim3(grid_for(n, 4096)), dim3(kMarkBlock), 0, s, import_slot, import_bid, n,
+                       bits, gather, mark_level_args(g));
     return hipGetLastError();
 }
 

@@ -131,25 +131,39 @@ constexpr uint32_t kTagEmpty = 0, kTagBusy = 1, kTagReady = 2;
 
 
 
+// Add a per-thread count to a global counter: one atomic per wave.  Called by
+// every lane of the wave after its grid-stride loop (converged).
+__device__ __forceinline__ void wave_count_add(uint32_t* counter, uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
+}
+
 __device__ __forceinline__ bool key_eq(const uint4* k, const uint4& lo, const uint4& hi) {
     const uint4 a = k[0], b = k[1];
     return ((a.x ^ lo.x) | (a.y ^ lo.y) | (a.z ^ lo.z) | (a.w ^ lo.w) | (b.x ^ hi.x) | (b.y ^ hi.y) |
             (b.z ^ hi.z) | (b.w ^ hi.w)) == 0;
 }
 
-// Insert (or find) the batch's DISTINCT keys (canon[i] == i): a busy slot is
-// some other key being written in this launch, so it is skipped, never waited on.
+// Insert (or find) the batch's DISTINCT keys (canon[i] == i).  A slot is
+// claimed empty -> busy with one CAS and its key written with plain stores --
+// no per-slot fences (an acquire load + release store per insert, a cache
+// invalidate and a store drain each, made a 1e8-key Put 234 ms).  A busy slot
+// is a key of this launch, never this lane's (the batch's keys are distinct),
+// so it is skipped without reading its key, which another XCD's L2 may not
+// show yet; k5_assoc_publish turns this launch's claims into ready tags after
+// the kernel boundary.  slot_of[i] carries bit 31 for a claim.
 __global__ __launch_bounds__(256) void k5_assoc_insert(AssocView t, uint32_t kind, const uint8_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ canon, uint32_t n,
                                                        uint32_t* __restrict__ slot_of) {
     const uint32_t ready = kTagReady + kind;
+    uint32_t added = 0;  // one atomicAdd per wave: a single counter word serialises ~88 atomics/us
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         if (canon[i] != i) continue;
         const uint4* k = reinterpret_cast<const uint4*>(keys + 32ull * i);
         const uint4 lo = k[0], hi = k[1];
-        uint32_t slot = lo.x & t.mask;
+        uint32_t slot = lo.x & t.mask, mark = 0;
         for (;;) {
-            uint32_t tg = __hip_atomic_load(&t.tag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t tg = __hip_atomic_load(&t.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (tg == kTagEmpty) {
                 tg = atomicCAS(&t.tag[slot], kTagEmpty, kTagBusy);
                 if (tg == kTagEmpty) {
@@ -157,15 +171,30 @@ __global__ __launch_bounds__(256) void k5_assoc_insert(AssocView t, uint32_t kin
                     t.keys[2 * slot + 1] = hi;
                     t.vals[2 * slot] = make_uint4(0, 0, 0, 0);
                     t.vals[2 * slot + 1] = make_uint4(0, 0, 0, 0);
-                    __hip_atomic_store(&t.tag[slot], ready, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    atomicAdd(t.count, 1u);
+                    ++added;
+                    mark = 0x80000000u;
                     break;
                 }
             }
+            // ready tags were set by earlier launches: their keys are visible
             if (tg == ready && key_eq(&t.keys[2 * slot], lo, hi)) break;
             slot = (slot + 1) & t.mask;
         }
-        slot_of[i] = slot;
+        slot_of[i] = slot | mark;
+    }
+    wave_count_add(t.count, added);
+}
+
+// The insert launch's claims become ready (and slot_of plain slot indices).
+__global__ __launch_bounds__(256) void k5_assoc_publish(AssocView t, uint32_t kind, const uint32_t* __restrict__ canon,
+                                                        uint32_t n, uint32_t* __restrict__ slot_of) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (canon[i] != i) continue;
+        const uint32_t so = slot_of[i];
+        if (so & 0x80000000u) {
+            t.tag[so & 0x7fffffffu] = kTagReady + kind;
+            slot_of[i] = so & 0x7fffffffu;
+        }
     }
 }
 
@@ -300,19 +329,27 @@ __global__ __launch_bounds__(256) void k5_assoc_abbrev(AssocView t, uint32_t kin
 
 // Rehash every occupied slot into a larger (empty) table; keys are distinct.
 __global__ __launch_bounds__(256) void k5_assoc_rehash(AssocView from, uint32_t cap_from, AssocView to) {
+    uint32_t added = 0;
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < cap_from; s += gridDim.x * blockDim.x) {
         const uint32_t tg = from.tag[s];
         if (tg < kTagReady) continue;
         const uint4 lo = from.keys[2 * s], hi = from.keys[2 * s + 1];
+        // keys are distinct and nothing compares them in this launch: claim
+        // the slot with its final tag, no fences (the kernel boundary publishes)
         uint32_t slot = lo.x & to.mask;
-        while (atomicCAS(&to.tag[slot], kTagEmpty, kTagBusy) != kTagEmpty) slot = (slot + 1) & to.mask;
+        while (atomicCAS(&to.tag[slot], kTagEmpty, tg) != kTagEmpty) slot = (slot + 1) & to.mask;
         to.keys[2 * slot] = lo;
         to.keys[2 * slot + 1] = hi;
         to.vals[2 * slot] = from.vals[2 * s];
         to.vals[2 * slot + 1] = from.vals[2 * s + 1];
-        __hip_atomic_store(&to.tag[slot], tg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        atomicAdd(to.count, 1u);
+        ++added;
     }
+    wave_count_add(to.count, added);
+}
+
+// rem[q] = q: a Put batch's first round holds every op, in index order
+__global__ __launch_bounds__(256) void k5_iota(uint32_t* __restrict__ out, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = i;
 }
 
 static uint32_t grid256(uint64_t n) {
@@ -324,6 +361,7 @@ hipError_t launch_assoc_insert(const AssocView& t, uint32_t kind, const uint8_t*
                                uint32_t n, uint32_t* slot_of, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k5_assoc_insert, dim3(grid256(n)), dim3(256), 0, s, t, kind, keys, canon, n, slot_of);
+    hipLaunchKernelGGL(k5_assoc_publish, dim3(grid256(n)), dim3(256), 0, s, t, kind, canon, n, slot_of);
     return hipGetLastError();
 }
 
@@ -357,6 +395,12 @@ hipError_t launch_assoc_abbrev(const AssocView& t, uint32_t kind, uint32_t cap, 
                                hipStream_t s) {
     hipLaunchKernelGGL(k5_assoc_abbrev, dim3(grid256(cap)), dim3(256), 0, s, t, kind, cap, qkeys, nhex, q,
                        matches, hit_slot);
+    return hipGetLastError();
+}
+
+hipError_t launch_iota(uint32_t* out, uint32_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k5_iota, dim3(grid256(n)), dim3(256), 0, s, out, n);
     return hipGetLastError();
 }
 
