@@ -54,6 +54,13 @@ SHA_VALU_PEAK_GBS = VALU_LANE_OPS / SHA_OPS_PER_BLOCK * 64 / 1e9
 # "Dependent-chain latency"; tools/micro.py lat: 4-5).  So no GPU
 # implementation can finish a message of B blocks in less than B*64*3*4 cycles.
 CHAIN_CYCLES_PER_BLOCK = 64 * 3 * 4
+# The same chain at the wave64 ISSUE floor (reported beside frac, never as
+# peak): a wave64 VALU instruction occupies its 16-lane SIMD for 4 cycles, so
+# one wave cannot issue faster than one per 4 cycles, dependent or not
+# (measured 4.5-5.5, profiles/r01/valu_issue_cost.log); k1_sha256_duo's
+# two-lane lagged round is 8 instructions.
+DUO_INSTR_PER_ROUND = 8
+ISSUE_CYCLES_PER_INSTR = 4
 HBM_PEAK_GBS = 8000.0
 T_START = time.perf_counter()
 
@@ -218,8 +225,15 @@ def kernel_roofline(name, lens, ids, ms):
     t_floor = max(t_chain, t_valu)
     ach = b / (ms * 1e-3) / 1e9
     peak = b / t_floor / 1e9
+    extra = {}
+    if name == "k1_sha256_duo":  # the chain at the measured single-wave issue rate (not the peak)
+        t_issue = float(nblk[ids].max()) * 64 * DUO_INSTR_PER_ROUND * ISSUE_CYCLES_PER_INSTR / CLOCK_HZ
+        extra = {"issue_floor_s": round(t_issue, 4), "frac_of_issue_floor": round(t_issue / (ms * 1e-3), 4),
+                 "us_per_chain_block": round(ms * 1e3 / float(nblk[ids].max()), 4),
+                 "issue_floor_kind": "longest message's blocks x 64 rounds x 8 instructions (the duo round) "
+                                     "x 4 cycles (a wave64 VALU op occupies a 16-lane SIMD 4 cycles) @2.4GHz"}
     return {"bound": "valu", "kernel": name, "achieved": round(ach, 3), "peak": round(peak, 3), "unit": "GB/s",
-            "frac": round(ach / peak, 4),
+            "frac": round(ach / peak, 4), **extra,
             "peak_kind": "skew-aware floor: max(longest message's blocks x 64 rounds x 3 dependent VALU x 4 cyc "
                          "@2.4GHz, sum blocks x 1464 ops / INT32 VALU peak)",
             "floor_s": round(t_floor, 4), "chain_floor_s": round(t_chain, 4),

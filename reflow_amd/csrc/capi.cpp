@@ -1362,6 +1362,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
         (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
         (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
+        (e = gr->b_lmeta.ensure(32ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_counts.ensure(4ull * (L + 1))) != hipSuccess ||
         (e = gr->b_counts_last.ensure(4ull * (L + 1))) != hipSuccess ||
         (e = up(gr->b_lvl_start, G.lvl_start.data(), 4ull * (L + 1))) != hipSuccess)
@@ -1380,6 +1381,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     G.slots = gr->b_slots.as<uint8_t>();
     G.dirty = gr->b_dirty.as<uint32_t>();
     G.list = gr->b_list.as<uint32_t>();
+    G.lmeta = gr->b_lmeta.as<uint4>();
     G.counts = gr->b_counts.as<uint32_t>();
     G.counts_last = gr->b_counts_last.as<uint32_t>();
     G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
@@ -1423,7 +1425,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
     if (gr->ctx) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
-                          &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_counts, &gr->b_counts_last,
+                          &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_lmeta, &gr->b_counts, &gr->b_counts_last,
                           &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);

@@ -79,6 +79,7 @@ struct GraphDev {
     uint8_t* slots = nullptr;        // [S][32] digest table
     uint32_t* dirty = nullptr;       // [(J+31)/32] queued-this-step bitset over internal ids
     uint32_t* list = nullptr;        // [J] per-level work lists (level l at lvl_start[l])
+    uint4* lmeta = nullptr;          // [2J] each listed job's record, at its list position
     uint32_t* counts = nullptr;      // [L+1] list lengths (append cursors); [L] = fused jobs hashed
     uint32_t* counts_last = nullptr; // [L+1] jobs hashed per level by the last recompute; [L] fused
     uint32_t* lvl_start_dev = nullptr; // [L+1]

@@ -55,6 +55,7 @@ struct LevelArgs {
     unsigned long long* stamps;  // diagnostic (RF_K2_STAMPS): phase times of workgroup 0, else null
     const uint4* __restrict__ mid;  // [2J] initial chaining values, or null (= IV for every job)
     const uint32_t* __restrict__ cons_ptr;  // [S+1] slot -> reverse-edge range (mark / apply kernels)
+    uint4* lmeta;                           // [2J] the listed jobs' records, beside list
 };
 
 // Reverse edges of an INPUT slot: bit 31 of the level field flags its
@@ -74,10 +75,13 @@ __device__ __forceinline__ void init_state(const LevelArgs& a, uint32_t p, ShaSt
     }
 }
 
-// Append the lanes' jobs j (need) at level lv to their levels' lists; one
-// atomicAdd per distinct level in the wave.  Called by every lane of the wave.
-__device__ __forceinline__ void append_jobs(uint32_t* list, uint32_t* counts, const uint32_t* ls,
-                                            bool need, uint32_t j, uint32_t lv) {
+// Append the lanes' jobs j (need) at level lv to their levels' lists, each
+// with its 32-B record (q0, q1) beside it in lmeta, so a level kernel's first
+// job starts one HBM round trip earlier (list -> record -> template was three
+// dependent loads); one atomicAdd per distinct level in the wave.  Called by
+// every lane of the wave.
+__device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint32_t j, uint32_t lv, const uint4& q0,
+                                            const uint4& q1) {
     const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t mask = __ballot(need);
@@ -87,10 +91,13 @@ __device__ __forceinline__ void append_jobs(uint32_t* list, uint32_t* counts, co
         const bool mine = need && lv == lvl;
         const uint64_t same = __ballot(mine);
         uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&counts[lvl], (uint32_t)__popcll(same));
-        base = ls[lvl] + __shfl(base, leader, 64);
+        if (lane == leader) base = atomicAdd(&a.counts[lvl], (uint32_t)__popcll(same));
+        base = a.lvl_start[lvl] + __shfl(base, leader, 64);
         if (mine) {
-            list[base + (uint32_t)__popcll(same & lt)] = j;
+            const uint32_t at = base + (uint32_t)__popcll(same & lt);
+            a.list[at] = j;
+            a.lmeta[2ull * at] = q0;
+            a.lmeta[2ull * at + 1] = q1;
             need = false;
         }
         mask = __ballot(need);
@@ -98,18 +105,21 @@ __device__ __forceinline__ void append_jobs(uint32_t* list, uint32_t* counts, co
 }
 
 // Mark consumers [c, ce) of the lanes whose slot changed (c == ce otherwise)
-// dirty, queueing the newly dirty ones.  Wave-uniform loop.
-__device__ __forceinline__ void propagate(const uint2* __restrict__ cons, uint32_t* dirty, uint32_t* list,
-                                          uint32_t* counts, const uint32_t* ls, uint32_t c, uint32_t ce) {
+// dirty, queueing the newly dirty ones (their records are fetched beside the
+// dirty-bit atomic).  Wave-uniform loop.
+__device__ __forceinline__ void propagate(const LevelArgs& a, uint32_t c, uint32_t ce) {
     while (__any(c < ce)) {
         bool need = false;
         uint2 jl = make_uint2(0, 0);
+        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
         if (c < ce) {
-            jl = cons[c++];
+            jl = a.cons[c++];
+            q0 = a.meta[2ull * jl.x];
+            q1 = a.meta[2ull * jl.x + 1];
             const uint32_t bit = 1u << (jl.x & 31);
-            need = !(atomicOr(&dirty[jl.x >> 5], bit) & bit);
+            need = !(atomicOr(&a.dirty[jl.x >> 5], bit) & bit);
         }
-        append_jobs(list, counts, ls, need, jl.x, jl.y);
+        append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
 }
 
@@ -302,14 +312,17 @@ __device__ __forceinline__ void propagate_pre(const LevelArgs& a, uint32_t c, ui
     for (int k = 0; k < 2; ++k) {
         bool need = false;
         const uint2 jl = pre[k];
+        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
         if (c < ce) {
             ++c;
+            q0 = a.meta[2ull * jl.x];
+            q1 = a.meta[2ull * jl.x + 1];
             const uint32_t bit = 1u << (jl.x & 31);
             need = !(atomicOr(&a.dirty[jl.x >> 5], bit) & bit);
         }
-        append_jobs(a.list, a.counts, a.lvl_start, need, jl.x, jl.y);
+        append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
-    propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, c, ce);
+    propagate(a, c, ce);
 }
 
 // Hash job p in one lane; returns whether its slot changed.
@@ -357,7 +370,7 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
                 if (!changed) ce = cb;
             }
         }
-        if (!a.full) propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, cb, ce);
+        if (!a.full) propagate(a, cb, ce);
     }
 }
 
@@ -748,6 +761,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     const uint32_t n = a.counts[a.lvl];
     const uint32_t* lst = a.list + a.s;
+    const uint4* lmt = a.lmeta + 2ull * a.s;
     // One copy of the loop per wave role (chain / producer / expander), each
     // with only its own state: the register allocator then sizes the kernel
     // for the largest role instead of the sum of all roles' live values, and
@@ -760,11 +774,17 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             const uint32_t i = base + jl;
             bool has = i < n;
             uint32_t p = has ? lst[i] : 0u;
+            // the listed job's record (append_jobs wrote it beside the list)
+            uint4 lm0 = make_uint4(0, 0, 0, 0), lm1 = lm0;
+            if (has) {
+                lm0 = lmt[2ull * i];
+                lm1 = lmt[2ull * i + 1];
+            }
             uint32_t fslot = ~0u;
             uint32_t maxnb;
             {
                 const uint32_t il = base + lane;
-                maxnb = wave_max_small(il < n ? a.meta[2ull * lst[il]].y : 0u);
+                maxnb = wave_max_small(il < n ? lmt[2ull * il].y : 0u);
             }
             uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
             uint4 nt[8];
@@ -785,8 +805,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         nm0 = nnm0;
                         nm1 = nnm1;
                     } else {
-                        m0 = a.meta[2 * p];
-                        m1 = a.meta[2 * p + 1];
+                        m0 = lm0;
+                        m1 = lm1;
                     }
                 }
                 const bool nfu = has && m1.w != ~0u;
@@ -1223,11 +1243,11 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
                 nm1 = nnm1;
             }
         }
-        propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, cb, cz);
+        propagate(a, cb, cz);
         p = nx;
     }
     // the slot's other consumers
-    propagate(a.cons, a.dirty, a.list, a.counts, a.lvl_start, c, ce);
+    propagate(a, c, ce);
     // counts[L]: jobs hashed outside the level lists (k3_step_end)
     for (int o = 32; o > 0; o >>= 1) hashed += __shfl_xor(hashed, o, 64);
     if (__lane_id() == 0 && hashed) atomicAdd(&a.counts[a.n_levels], hashed);
@@ -1390,7 +1410,7 @@ static uint32_t grid_for(uint64_t items, uint32_t cap) {
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta};
     return a;
 }
 
@@ -1435,7 +1455,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                                  : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
                                                               : 0u;
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
