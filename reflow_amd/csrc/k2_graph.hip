@@ -1253,7 +1253,7 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
     if (__lane_id() == 0 && hashed) atomicAdd(&a.counts[a.n_levels], hashed);
 }
 
-constexpr uint32_t kMarkBlock = 256;
+constexpr uint32_t kMarkBlock = 64;
 
 // set_slots: write input digests; a changed slot queues (or hashes) its consumers.
 __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __restrict__ sl,
@@ -1407,6 +1407,11 @@ static uint32_t grid_for(uint64_t items, uint32_t cap) {
     return (uint32_t)g;
 }
 
+static uint32_t grid_mark(uint64_t items) {
+    uint64_t g = (items + kMarkBlock - 1) / kMarkBlock;
+    return (uint32_t)(g < 1 ? 1 : g > 16384 ? 16384 : g);
+}
+
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
@@ -1417,7 +1422,7 @@ static LevelArgs mark_level_args(const GraphDev& g) {
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k3_mark_slots, dim3(grid_for(n, 4096)), dim3(kMarkBlock), 0, s, slots, digests, n,
+    hipLaunchKernelGGL(k3_mark_slots, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, slots, digests, n,
                        mark_level_args(g));
     return hipGetLastError();
 }
@@ -1435,7 +1440,7 @@ void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* 
     void* v[4] = {&args->sl, &args->dig, &args->n, args->a};
     for (int i = 0; i < 4; ++i) args->ptrs[i] = v[i];
     p->func = reinterpret_cast<void*>(k3_mark_slots);
-    p->gridDim = dim3(n ? grid_for(n, 4096) : 1);  // an empty batch still runs (and marks nothing)
+    p->gridDim = dim3(n ? grid_mark(n) : 1);  // an empty batch still runs (and marks nothing)
     p->blockDim = dim3(kMarkBlock);
     p->sharedMemBytes = 0;
     p->kernelParams = args->ptrs;
@@ -1527,7 +1532,7 @@ hipError_t launch_part_any(const uint64_t* bits, uint64_t nwords, const uint32_t
 hipError_t launch_part_apply(const GraphDev& g, const uint32_t* import_slot, const uint32_t* import_bid, uint32_t n,
                              const uint32_t* bits, const uint8_t* gather, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_part_apply, dim3(grid_for(n, 4096)), dim3(kMarkBlock), 0, s, import_slot, import_bid, n,
+    hipLaunchKernelGGL(k_part_apply, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, import_slot, import_bid, n,
                        bits, gather, mark_level_args(g));
     return hipGetLastError();
 }
