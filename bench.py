@@ -461,8 +461,9 @@ def bench_dag(args, dist, ctx, comm, budget):
     """configs[2] at N = 1 (one 10M-node DAG); configs[3] at N > 1: ONE global
     DAG of N x 12.5M nodes (100M at N = 8), partitioned by sample subtree
     (workloads.PartitionedDag1000) and recomputed with
-    rf_graph_recompute_part's supersteps (boundary bitset OR + boundary
-    digest all-gather over RCCL)."""
+    rf_graph_recompute_part: the layout's one fixed exchange round (every
+    rank root all-gathered over RCCL, rank 0 recomputes the global root) --
+    a step queues kernels and RCCL calls with no host round trip)."""
     t0 = time.perf_counter()
     part = None
     if dist.world > 1:
@@ -483,8 +484,10 @@ def bench_dag(args, dist, ctx, comm, budget):
         if comm is None:  # RF_BENCH_SHARE_GPU rehearsal: gloo host transport
             ag = lambda b: [x.tobytes() for x in np.split(dist.all_gather_bytes(np.frombuffer(b, np.uint8)), dist.world)]  # noqa: E731,E501
 
-        def recompute(full):
-            return g.recompute_part(comm=comm, allgather=ag, nranks=dist.world, full=full)
+        def recompute(full, count=True):
+            # the timed steps read nothing back: with RCCL and the layout's fixed
+            # exchange round (rounds = 1) a step never waits on the host
+            return g.recompute_part(comm=comm, allgather=ag, nranks=dist.world, full=full, count=count)
     else:
         recompute = lambda full: g.recompute(full=full)  # noqa: E731
     recompute(True)  # first call also captures the hipGraphs (host work): untimed
@@ -517,7 +520,7 @@ def bench_dag(args, dist, ctx, comm, budget):
             return
         g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
         if part is not None:
-            recompute(False)
+            recompute(False, count=False)
         else:
             g.recompute_async(False, ctx.stream)
 
@@ -531,7 +534,7 @@ def bench_dag(args, dist, ctx, comm, budget):
     if part is not None:
         wl = ("configs[3]: one 1000align DAG of %d samples x P=%d (%d nodes), partitioned by sample subtree "
               "over %d ranks (%d samples each; shared reference chain replicated; per-rank Merge tree; global root "
-              "on rank 0), 1%% leaf File IDs toggled per step on every rank; supersteps %d"
+              "on rank 0), 1%% leaf File IDs toggled per step on every rank; local passes per step %d"
               % (S * dist.world, args.dag_pairs, dist.sum(n_nodes), dist.world, S,
                  g.part_gathered()[2]))
     else:

@@ -380,6 +380,15 @@ typedef struct {
     const uint32_t *import_slot;
     const uint32_t *import_bid;
     int any_import; /* some rank imports something (the same on every rank) */
+    /* Exchange rounds per recompute, the same on every rank: the most
+     * rank-boundary crossings on any path of the global graph (rf_graph_split;
+     * 1 for configs[3]: sample roots -> the global root).  > 0 selects the
+     * fixed-round protocol -- recompute, then `rounds` times: all-gather every
+     * export digest, write the imports that differ (queueing their consumers)
+     * and recompute -- with no OR-reduce and no host round trip, so with an
+     * rf_comm and out_recomputed == NULL the whole call is asynchronous on the
+     * context's stream.  0: the superstep protocol above (until no change). */
+    uint32_t rounds;
 } rf_graph_part;
 typedef int (*rf_host_allgather_fn)(void *user, const void *send, void *recv, uint64_t bytes);
 int rf_graph_set_part(rf_graph *g, const rf_graph_part *p);

@@ -150,7 +150,7 @@ class GraphPart(ctypes.Structure):
     _fields_ = [("nranks", ctypes.c_int), ("rank", ctypes.c_int), ("max_export", ctypes.c_uint32),
                 ("n_export", ctypes.c_uint32), ("export_slot", ctypes.c_void_p),
                 ("n_import", ctypes.c_uint32), ("import_slot", ctypes.c_void_p),
-                ("import_bid", ctypes.c_void_p), ("any_import", ctypes.c_int)]
+                ("import_bid", ctypes.c_void_p), ("any_import", ctypes.c_int), ("rounds", ctypes.c_uint32)]
 
 
 # int (*)(void *user, const void *send, void *recv, uint64_t bytes)
@@ -215,7 +215,8 @@ class GraphPiece:
             self.part = dict(nranks=pt.nranks, rank=pt.rank, max_export=pt.max_export,
                              export_slot=_arr(pt.export_slot, pt.n_export, np.uint32),
                              import_slot=_arr(pt.import_slot, pt.n_import, np.uint32),
-                             import_bid=_arr(pt.import_bid, pt.n_import, np.uint32), any_import=bool(pt.any_import))
+                             import_bid=_arr(pt.import_bid, pt.n_import, np.uint32), any_import=bool(pt.any_import),
+                             rounds=int(pt.rounds))
             gp, gn = ctypes.c_void_p(), ctypes.c_uint32()
             _check(lib().rf_graph_piece_slots(h, ctypes.byref(gp), ctypes.byref(gn)))
             self.global_of_local = _arr(gp, gn.value, np.uint32)
@@ -797,24 +798,26 @@ class Graph:
 
     def set_part(self, part):
         """part: dict(nranks, rank, max_export, export_slot, import_slot,
-        import_bid, any_import) (GraphPiece.part)."""
+        import_bid, any_import[, rounds]) (GraphPiece.part); rounds > 0 selects
+        the fixed-round exchange (0: supersteps until nothing changes)."""
         ex = np.ascontiguousarray(part["export_slot"], dtype=np.uint32)
         im = np.ascontiguousarray(part["import_slot"], dtype=np.uint32)
         ib = np.ascontiguousarray(part["import_bid"], dtype=np.uint32)
         p = GraphPart(part["nranks"], part["rank"], part["max_export"], len(ex), _ptr(ex) if len(ex) else None,
                       len(im), _ptr(im) if len(im) else None, _ptr(ib) if len(ib) else None,
-                      1 if part.get("any_import", True) else 0)
+                      1 if part.get("any_import", True) else 0, int(part.get("rounds", 0)))
         _check(lib().rf_graph_set_part(self._h, ctypes.byref(p)))
 
-    def recompute_part(self, comm=None, allgather=None, nranks=1, full=False) -> int:
-        """Superstep recompute across ranks: comm (Comm, RCCL) or allgather
-        (bytes -> [bytes per rank], a host transport)."""
+    def recompute_part(self, comm=None, allgather=None, nranks=1, full=False, count=True) -> int:
+        """Recompute across ranks: comm (Comm, RCCL) or allgather (bytes ->
+        [bytes per rank], a host transport).  count=False: no readback of the
+        jobs hashed (with comm and fixed rounds the call is then asynchronous)."""
         fn = host_allgather_fn(allgather, nranks) if allgather is not None else None
         self._fn = fn  # alive during the call
         n = ctypes.c_uint64(0)
         _check(lib().rf_graph_recompute_part(self._h, comm._h if comm is not None else None,
                                              ctypes.cast(fn, ctypes.c_void_p) if fn is not None else None, None,
-                                             1 if full else 0, ctypes.byref(n)))
+                                             1 if full else 0, ctypes.byref(n) if count else None))
         return n.value
 
     def part_gathered(self):

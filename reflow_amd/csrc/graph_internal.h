@@ -12,6 +12,7 @@ struct GraphPart {
     int nranks = 1, rank = 0;
     uint32_t max_export = 0, n_export = 0, n_import = 0;
     bool any_import = true;   // some rank imports (else one exchange ends a step)
+    uint32_t rounds = 0;      // > 0: fixed-round protocol (rf_graph_part::rounds)
     uint64_t nwords = 0;      // u64 words of the boundary bitset (nranks * max_export bits)
     DevBuf d_export_slot, d_import_slot, d_import_bid;
     DevBuf d_snap;            // [n_export][32] export digests as last sent

@@ -1347,7 +1347,7 @@ __global__ __launch_bounds__(kMarkBlock) void k_part_apply(const uint32_t* __res
         uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
         if (i < n) {
             const uint32_t b = import_bid[i];
-            if ((bits[b >> 5] >> (b & 31)) & 1u) {
+            if (!bits || ((bits[b >> 5] >> (b & 31)) & 1u)) {  // null bits: every import (fixed rounds)
                 s = import_slot[i];
                 const uint4* src = reinterpret_cast<const uint4*>(gather + 32ull * b);
                 uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
@@ -1469,8 +1469,14 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }();
     if (!full) {
         if (!g.inc_level[lvl]) return hipSuccess;  // every job of the level is a fusion target
+        // grid cap (RF_K2_GRID): workgroups past the dirty count exit at once,
+        // but each still costs a dispatch before the kernel can end
+        static const uint64_t wg_cap = [] {
+            const char* v = getenv("RF_K2_GRID");
+            return v ? (uint64_t)strtoull(v, nullptr, 10) : 2048ull;
+        }();
         uint64_t wg = (e - b + 63) / 64;
-        if (wg > 2048) wg = 2048;
+        if (wg > wg_cap) wg = wg_cap;
         // RF_K2_CHAIN=14: the one-lane chain (k2_level_pc), for A/B runs
         static const bool one_lane = [] {
             const char* v = getenv("RF_K2_CHAIN");

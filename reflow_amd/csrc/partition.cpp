@@ -77,6 +77,7 @@ extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
     P->n_export = p->n_export;
     P->n_import = p->n_import;
     P->any_import = p->any_import != 0;
+    P->rounds = p->rounds;
     P->nwords = ((uint64_t)p->nranks * p->max_export + 63) / 64;
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
         hipError_t e = b.ensure(std::max<size_t>(bytes, 64));
@@ -145,6 +146,38 @@ static int part_counts(rf_graph* gr, hipStream_t s, uint64_t* tot) {
     return RF_OK;
 }
 
+// Fixed-round protocol (rf_graph_part::rounds > 0): the splitter knows the
+// most boundary crossings R on any path, so a change settles after R
+// exchanges.  Each round gathers EVERY export digest (no changed-since-sent
+// bitset, no OR-reduce, no "anything left?" readback), and k_part_apply
+// writes the imports whose digest differs from the slot's and queues (or
+// hashes, slot fusion) their consumers.  A rank without imports has nothing
+// to recompute after its first pass.  With an rf_comm and no count readback
+// nothing here waits on the host: kernels and RCCL calls queue on the stream.
+static int recompute_rounds(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn, void* user, int full,
+                            uint64_t* out_recomputed, hipStream_t s) {
+    GraphPart* P = gr->part;
+    uint64_t tot = 0;
+    if (int rc = graph_recompute_locked(gr, full, s)) return rc;
+    if (out_recomputed)
+        if (int rc = part_counts(gr, s, &tot)) return rc;
+    for (uint32_t r = 0; r < P->rounds; ++r) {
+        if (P->n_export)
+            HIPC(launch_gather_slots(gr->g.slots, P->d_export_slot.as<uint32_t>(), P->n_export,
+                                     P->d_send.as<uint8_t>(), s));
+        if (int rc = part_gather(gr, comm, fn, user, s)) return rc;
+        if (!P->n_import) continue;
+        HIPC(launch_part_apply(gr->g, P->d_import_slot.as<uint32_t>(), P->d_import_bid.as<uint32_t>(), P->n_import,
+                               nullptr, P->d_gather.as<uint8_t>(), s));
+        if (int rc = graph_recompute_locked(gr, 0, s)) return rc;
+        if (out_recomputed)
+            if (int rc = part_counts(gr, s, &tot)) return rc;
+    }
+    P->last_supersteps = 1 + P->rounds;
+    if (out_recomputed) *out_recomputed = tot;
+    return RF_OK;
+}
+
 extern "C" int rf_graph_recompute_part(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn, void* user, int full,
                                        uint64_t* out_recomputed) {
     ARG(gr && gr->part, "graph has no partition (rf_graph_set_part)");
@@ -154,6 +187,7 @@ extern "C" int rf_graph_recompute_part(rf_graph* gr, rf_comm* comm, rf_host_allg
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
     hipStream_t s = ctx->stream;
+    if (P->rounds && P->nranks > 1) return recompute_rounds(gr, comm, fn, user, full, out_recomputed, s);
     uint64_t tot = 0, steps = 0;
     bool run = true;  // this rank has new inputs for the superstep
     for (;;) {

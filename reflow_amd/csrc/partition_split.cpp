@@ -26,7 +26,48 @@ struct rf_graph_piece {
     uint32_t max_export = 0;
     int nranks = 1, rank = 0;
     bool any_import = false;
+    uint32_t rounds = 0;  // the most rank-boundary crossings on any path
 };
+
+// The most rank-boundary crossings on any path of the global job graph: an
+// edge producer p -> consumer k crosses when p is owned (not replicated) and
+// k is hashed elsewhere (another rank, or every rank).  Kahn order over the
+// jobs; RF_EINVAL on a cycle.
+static int max_crossings(const rf_graph_desc* d, const int32_t* owner, const std::vector<int64_t>& producer,
+                         uint32_t* out) {
+    const uint32_t J = d->n_jobs, S = d->n_slots;
+    const uint64_t H = J ? d->hole_ptr[J] : 0;
+    std::vector<uint64_t> cptr(S + 1, 0);
+    for (uint64_t h = 0; h < H; ++h) cptr[d->hole_slot[h] + 1]++;
+    for (uint32_t s = 0; s < S; ++s) cptr[s + 1] += cptr[s];
+    std::vector<uint32_t> cjob(H), indeg(J, 0), cross(J, 0);
+    {
+        std::vector<uint64_t> fill(cptr.begin(), cptr.end() - 1);
+        for (uint32_t k = 0; k < J; ++k)
+            for (uint64_t h = d->hole_ptr[k]; h < d->hole_ptr[k + 1]; ++h) {
+                cjob[fill[d->hole_slot[h]]++] = k;
+                if (producer[d->hole_slot[h]] >= 0) indeg[k]++;
+            }
+    }
+    std::vector<uint32_t> q;
+    q.reserve(J);
+    for (uint32_t j = 0; j < J; ++j)
+        if (!indeg[j]) q.push_back(j);
+    uint32_t best = 0;
+    for (size_t i = 0; i < q.size(); ++i) {
+        const uint32_t p = q[i], s = d->out_slot[p];
+        best = std::max(best, cross[p]);
+        for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
+            const uint32_t k = cjob[c];
+            const uint32_t x = cross[p] + ((owner[p] >= 0 && owner[k] != owner[p]) ? 1u : 0u);
+            cross[k] = std::max(cross[k], x);
+            if (--indeg[k] == 0) q.push_back(k);
+        }
+    }
+    if (q.size() != J) return fail(RF_EINVAL, "job graph has a cycle");
+    *out = best;
+    return RF_OK;
+}
 
 extern "C" int rf_graph_split(const rf_graph_desc* d, int nranks, int rank, const int32_t* owner,
                               rf_graph_piece** out) {
@@ -106,6 +147,7 @@ extern "C" int rf_graph_split(const rf_graph_desc* d, int nranks, int rank, cons
                 break;
             }
         }
+    if (int rc = max_crossings(d, owner, producer, &pc->rounds)) return rc;
     // imports: slots this piece reads that another rank's job produces
     for (uint32_t ls = 0; ls < pc->global_of_local.size(); ++ls) {
         const uint32_t s = pc->global_of_local[ls];
@@ -147,6 +189,7 @@ extern "C" int rf_graph_piece_part(const rf_graph_piece* pc, rf_graph_part* o) {
     o->import_slot = pc->import_slot.data();
     o->import_bid = pc->import_bid.data();
     o->any_import = pc->any_import ? 1 : 0;
+    o->rounds = pc->rounds;
     return RF_OK;
 }
 

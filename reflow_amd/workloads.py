@@ -504,4 +504,4 @@ class PartitionedDag1000:
         self.part = dict(nranks=nranks, rank=rank, max_export=1 if nranks > 1 else 0, export_slot=ex,
                          import_slot=self.import_slot,
                          import_bid=np.arange(1, nranks, dtype=np.uint32) if rank == 0 else np.zeros(0, np.uint32),
-                         any_import=nranks > 1)
+                         any_import=nranks > 1, rounds=1 if nranks > 1 else 0)

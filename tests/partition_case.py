@@ -170,7 +170,9 @@ def superstep_oracle(desc, part, allgather, inputs=None, changed=None, state=Non
     """Rank's side of rf_graph_recompute_part with the oracle as local engine.
     allgather(bytes) -> [bytes per rank].  First call (state None): inputs =
     (local slots, IDs) loaded, full recompute; later calls: `changed` = (local
-    slots, new IDs).  Returns (state, supersteps)."""
+    slots, new IDs).  part["rounds"] > 0: the fixed-round protocol (every
+    export digest gathered each round, imports that differ written), else
+    supersteps until nothing changed.  Returns (state, supersteps)."""
     nr, me, mx = part["nranks"], part["rank"], part["max_export"]
     if state is None:
         og = O.OGraph(desc)
@@ -182,6 +184,20 @@ def superstep_oracle(desc, part, allgather, inputs=None, changed=None, state=Non
         og = state["og"]
         if changed is not None and len(changed[0]):
             og.update(changed[0], changed[1])
+    rounds = part.get("rounds", 0)
+    if rounds and nr > 1:
+        for _ in range(rounds):
+            cur = og.slots[part["export_slot"]] if len(part["export_slot"]) else np.zeros((0, 32), np.uint8)
+            send = np.zeros((mx, 32), np.uint8)
+            send[:len(cur)] = cur
+            gathered = np.concatenate([np.frombuffer(b, np.uint8).reshape(mx, 32) for b in allgather(send.tobytes())])
+            if len(part["import_slot"]):
+                imp = np.asarray(part["import_slot"])
+                new = gathered[np.asarray(part["import_bid"])]
+                diff = (og.slots[imp] != new).any(axis=1)
+                if diff.any():
+                    og.update(imp[diff], new[diff])
+        return state, 1 + rounds
     steps = 0
     nbits = nr * mx
     while True:

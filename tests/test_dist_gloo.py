@@ -69,7 +69,7 @@ def test_gloo_world2_bench_dist():
     assert ids0 != ids1  # per-rank DAG seeds differ
 
 
-def _part_worker(rank, world, port, q):
+def _part_worker(rank, world, port, q, protocol="rounds"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -89,6 +89,8 @@ def _part_worker(rank, world, port, q):
 
     dag, arrays, owner, root_slot, tail_slot = PC.global_case(S=6, P=4, nranks=world)
     piece = capi.GraphPiece(arrays, world, rank, owner)
+    if protocol == "supersteps":
+        piece.part = dict(piece.part, rounds=0)
     ids = dag.leaf_ids.copy()
     state, steps1 = PC.superstep_oracle(piece.desc, piece.part, allgather, inputs=PC.piece_inputs(piece, dag, ids))
     first = state["og"].slots[:len(piece.global_of_local)].copy()
@@ -105,10 +107,12 @@ def _part_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_partitioned_dag():
+@pytest.mark.parametrize("protocol", ["supersteps", "rounds"])
+def test_gloo_world2_partitioned_dag(protocol):
     """One DAG over 2 ranks: every rank's local slots equal the single-rank
     recompute, before and after an incremental change, and the change crosses
-    ranks twice (global root on rank 0, its consumer on rank 1)."""
+    ranks twice (global root on rank 0, its consumer on rank 1) -- with the
+    superstep exchange and with the splitter's fixed rounds."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import partition_case as PC
@@ -116,7 +120,7 @@ def test_gloo_world2_partitioned_dag():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_part_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_part_worker, args=(r, 2, port, q, protocol)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)

@@ -3,7 +3,9 @@ rf_graph_recompute_part): each rank holds its piece in its own
 rf_ctx and runs the superstep exchange through a host all-gather; every
 rank's slots equal the oracle's single-rank recompute of the whole graph,
 slot for slot, after a full recompute and after incremental changes that
-cross ranks.  Pieces come from the library's splitter (rf_graph_split of
+cross ranks -- with both exchange protocols: the supersteps until nothing
+changes (rf_graph_part.rounds = 0) and the fixed rounds the splitter counts
+(the most rank-boundary crossings on any path; no host round trip).  Pieces come from the library's splitter (rf_graph_split of
 partition_case.global_case: a change crosses ranks twice) and from bench.py's
 per-rank layout of configs[3] (workloads.PartitionedDag1000).  Ranks are
 threads of one process sharing the GPU (RCCL needs one GPU per rank; bench.py
@@ -60,16 +62,22 @@ def _run(ctx_rank_setup, nranks, changes):
     return PC.run_threads(nranks, body)
 
 
+def _part(part, protocol):
+    return part if protocol == "rounds" else dict(part, rounds=0)
+
+
+@pytest.mark.parametrize("protocol", ["supersteps", "rounds"])
 @pytest.mark.parametrize("nranks,S,P", [(2, 6, 4), (3, 40, 8), (4, 64, 16)])
-def test_split_pieces_match_single_rank(nranks, S, P):
+def test_split_pieces_match_single_rank(nranks, S, P, protocol):
     dag, arrays, owner, root_slot, tail_slot = PC.global_case(S=S, P=P, nranks=nranks)
     changes = _changes(len(dag.file_slots), np.random.default_rng(nranks), (0.01, 0.3))
     pieces = [capi.GraphPiece(arrays, nranks, r, owner) for r in range(nranks)]
+    assert all(pc.part["rounds"] == 2 for pc in pieces)  # sample roots -> global root -> tail
 
     def setup(r, ctx):
         pc = pieces[r]
         g = capi.Graph.from_arrays(ctx, pc.desc)
-        g.set_part(pc.part)
+        g.set_part(_part(pc.part, protocol))
         return (g, len(pc.global_of_local), PC.piece_inputs(pc, dag, dag.leaf_ids),
                 lambda pick, new: PC.piece_inputs(pc, dag, _scatter(dag, pick, new), pick))
 
@@ -81,8 +89,12 @@ def test_split_pieces_match_single_rank(nranks, S, P):
         covered |= set(gl.tolist())
         for step, ((n, slots, supersteps), want) in enumerate(zip(out, wants)):
             assert (slots == want[gl]).all(), (r, step)
-        assert out[2][2] >= 3  # 30% change: sample roots -> global root -> tail
-        assert out[3][0] == 0 and out[3][2] == 1  # nothing changed: one quiet superstep
+        if protocol == "rounds":
+            assert all(st == 3 for _, _, st in out)  # a local pass + two exchange rounds, always
+            assert out[3][0] == 0  # nothing changed: nothing hashed
+        else:
+            assert out[2][2] >= 3  # 30% change: sample roots -> global root -> tail
+            assert out[3][0] == 0 and out[3][2] == 1  # nothing changed: one quiet superstep
     assert covered == set(range(arrays["n_slots"]))
 
 
@@ -92,8 +104,9 @@ def _scatter(dag, pick, new):
     return x
 
 
+@pytest.mark.parametrize("protocol", ["supersteps", "rounds"])
 @pytest.mark.parametrize("nranks,S,P,fanin", [(2, 30, 8, 32), (4, 100, 4, 8)])
-def test_bench_layout_pieces_match_global_dag(nranks, S, P, fanin):
+def test_bench_layout_pieces_match_global_dag(nranks, S, P, fanin, protocol):
     G, ga, owner, roots, trees, groot = PC.global_c4(S, P, nranks, fanin=fanin)
     changes = _changes(len(G.file_slots), np.random.default_rng(7), (0.01, 0.25))
     pcs = [PartitionedDag1000(S, P, nranks, r, fanin=fanin) for r in range(nranks)]
@@ -102,7 +115,7 @@ def test_bench_layout_pieces_match_global_dag(nranks, S, P, fanin):
         pc = pcs[r]
         f0, nf = 2 * pc.dag.Q * r, 2 * pc.dag.Q
         g = capi.Graph.from_arrays(ctx, pc.desc)
-        g.set_part(pc.part)
+        g.set_part(_part(pc.part, protocol))
 
         def to_local(pick, new):
             sel = (pick >= f0) & (pick < f0 + nf)
@@ -115,6 +128,6 @@ def test_bench_layout_pieces_match_global_dag(nranks, S, P, fanin):
         m = PC.c4_local_to_global(pcs[r], G, roots, trees, groot)
         for step, ((n, slots, supersteps), want) in enumerate(zip(out, wants)):
             assert (slots == want[m]).all(), (r, step)
-            assert supersteps == (1 if step == 3 else 2)
+            assert supersteps == (2 if protocol == "rounds" or step != 3 else 1)
         # ranks > 0 have no imports: their second superstep launches nothing
         assert r == 0 or out[1][0] > 0

@@ -29,8 +29,9 @@ def test_sample0_slices_the_global_dag():
                     bytes(ga["blob"][ga["tmpl_off"][gj]:ga["tmpl_off"][gj] + ga["tmpl_len"][gj]])
 
 
+@pytest.mark.parametrize("protocol", ["supersteps", "rounds"])
 @pytest.mark.parametrize("nranks,S,P,fanin", [(2, 5, 3, 32), (3, 40, 4, 8), (4, 9, 2, 4)])
-def test_c4_pieces_equal_global_dag(nranks, S, P, fanin):
+def test_c4_pieces_equal_global_dag(nranks, S, P, fanin, protocol):
     G, ga, owner, roots, trees, groot = PC.global_c4(S, P, nranks, fanin=fanin)
     rng = np.random.default_rng(nranks)
     nf = len(G.file_slots)
@@ -47,6 +48,8 @@ def test_c4_pieces_equal_global_dag(nranks, S, P, fanin):
 
     def body(r, ag):
         pc = PartitionedDag1000(S, P, nranks, r, fanin=fanin)
+        if protocol == "supersteps":
+            pc.part = dict(pc.part, rounds=0)
         m = PC.c4_local_to_global(pc, G, roots, trees, groot)
         f0 = 2 * pc.dag.Q * r
         out = []
@@ -79,3 +82,17 @@ def test_split_finds_the_same_boundary():
         assert sorted(gl[piece.part["import_slot"]].tolist()) == (sorted(roots[1:]) if r == 0 else [])
         assert len(piece.desc["out_slot"]) == len(pc.desc["out_slot"])
         assert piece.part["any_import"]
+        assert piece.part["rounds"] == pc.part["rounds"] == 1  # rank roots -> global root
+
+
+def test_split_counts_boundary_crossings():
+    """rf_graph_split's rounds: the most rank-boundary crossings on any path."""
+    dag, arrays, owner, root_slot, tail_slot = PC.global_case(S=6, P=2, nranks=3)
+    assert capi.GraphPiece(arrays, 3, 1, owner).part["rounds"] == 2  # sample roots -> root (0) -> tail (2)
+    one = np.zeros_like(owner)  # everything on rank 0 (replicated kinds stay replicated)
+    one[owner < 0] = -1
+    p = capi.GraphPiece(arrays, 2, 0, one).part
+    assert p["rounds"] == 0 and not p["any_import"]
+    rep = owner.copy()  # the tail replicated: still read across ranks once more
+    rep[-1] = -1
+    assert capi.GraphPiece(arrays, 3, 0, rep).part["rounds"] == 2
