@@ -1296,6 +1296,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         m[5] = (uint32_t)cptr[s];
         m[6] = (uint32_t)cptr[s + 1];
         m[7] = fuse[j] >= 0 ? gr->ext2int[(uint32_t)fuse[j]] : 0xffffffffu;
+        if (fused_target[j] && holes[2 * m[2]] != 2) gr->g.fuse_pos2 = false;  // (cb0 = 2 needs every one at 2)
         tb += 64ull * nblk[j];
         gr->total_blocks += nblk[j] - ld;
     }
@@ -1398,6 +1399,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         HIPC(hipStreamSynchronize(ctx->stream));
         G.mid = gr->b_mid.as<uint4>();
     } else if (n_lead) {  // A/B: keep every block, the records as if no job had a constant prefix
+        G.hole_in_b0 = false;
         for (uint32_t i = 0; i < J; ++i) {
             if (!lead[i]) continue;
             meta[8ull * i] -= lead[i];

@@ -85,6 +85,13 @@ struct GraphDev {
     uint32_t* lvl_start_dev = nullptr; // [L+1]
     std::vector<uint32_t> lvl_start; // host copy [L+1]
     std::vector<uint8_t> inc_level;  // [L] level has jobs that can be queued (not all fusion targets)
+    // every job's first hole starts in block 0 of its (midstate-trimmed)
+    // template, so a fusion target's block 0 can be built by the chain wave
+    // (k2_level_pl cb0); false only for the RF_K2_NO_MIDSTATE A/B load
+    bool hole_in_b0 = true;
+    // every fusion target's hole is at material byte 2 (right after its WD
+    // prefix: no Universe), so the chain assembles its block 0 in registers
+    bool fuse_pos2 = true;
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the
     // constant blocks its template starts with -- the record's template

@@ -56,6 +56,7 @@ struct LevelArgs {
     const uint4* __restrict__ mid;  // [2J] initial chaining values, or null (= IV for every job)
     const uint32_t* __restrict__ cons_ptr;  // [S+1] slot -> reverse-edge range (mark / apply kernels)
     uint4* lmeta;                           // [2J] the listed jobs' records, beside list
+    uint32_t cb0;  // k2_level_pl<2,false>: chain-built block 0 of fused jobs (1: via the ring, 2: in registers)
 };
 
 // Reverse edges of an INPUT slot: bit 31 of the level field flags its
@@ -223,6 +224,20 @@ struct MatCursor {
         t[0] = nt[0]; t[1] = nt[1]; t[2] = nt[2]; t[3] = nt[3];
         ring_put(ring, 0, t);
         t[0] = nt[4]; t[1] = nt[5]; t[2] = nt[6]; t[3] = nt[7];
+    }
+    // begin() for a fused job whose block 0 the chain wave builds (k2_level_pl,
+    // cb0): the ring already holds its template blocks 0 and 1 with the
+    // producer's digest OR-ed into the one hole, so the cursor starts at block
+    // 1 with no hole left; t is block 2's template
+    __device__ __forceinline__ void begin_chain(const uint4& m0, const uint4* __restrict__ tmpl) {
+        T = tmpl + 4ull * m0.x;
+        nb = m0.y;
+        he = m0.w;
+        hn = m0.z;
+        q0.r = q1.r = q2.r = q3.r = r4 = r5 = make_uint2(~0u, 0u);
+        if (nb > 2) {
+            t[0] = T[8]; t[1] = T[9]; t[2] = T[10]; t[3] = T[11];
+        }
     }
     // the 16 big-endian words of block b (blocks taken in order).  one: every
     // active lane of the wave holds a fused job (begin_pre: its single hole is
@@ -695,6 +710,39 @@ __device__ __forceinline__ void kw_expand_chunk(uint32_t (&w)[16], uint4* row, i
     }
 }
 
+// Block 0 of a fused job on the CHAIN wave (k2_level_pl, cb0): both lanes of
+// the job (e-lane, a-lane: row_half_mirror partners) hold W[0..15] and
+// expand W[16..63] together -- the e-lane sigma1(W[t-2]) + W[t-7], the a-lane
+// sigma0(W[t-15]) + W[t-16], summed across the pair by one DPP add -- and the
+// pair stores K+W into the job's row.  ~9 instructions per word instead of the
+// producer's ~12, and no hand-over: the chain starts the rounds right after.
+__device__ __forceinline__ void chain_expand_b0(uint32_t (&w)[16], bool elane, uint4* row) {
+    constexpr uint32_t K[64] = RF_SHA_K;
+    const uint32_t r1 = elane ? 17u : 7u, r2 = elane ? 19u : 18u, r3 = elane ? 10u : 3u;
+    const uint32_t E = elane ? ~0u : 0u;  // selects by mask (one bitop3), never by address
+#pragma unroll
+    for (int t4 = 0; t4 < 16; ++t4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = 4 * t4 + u;
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                const uint32_t x = __builtin_amdgcn_bitop3_b32(E, w[(t - 2) & 15], w[(t - 15) & 15], 0xCA);
+                const uint32_t y = __builtin_amdgcn_bitop3_b32(E, w[(t - 7) & 15], w[t & 15], 0xCA);
+                const uint32_t h = xor3(__builtin_amdgcn_alignbit(x, x, r1), __builtin_amdgcn_alignbit(x, x, r2),
+                                        x >> r3) + y;
+                wt = h + (uint32_t)__builtin_amdgcn_mov_dpp((int)h, 0x141, 0xf, 0xf, true);  // + partner's half
+                w[t & 15] = wt;
+            }
+            v[u] = K[t] + wt;
+        }
+        row[t4] = make_uint4(v[0], v[1], v[2], v[3]);  // both lanes: identical values, no EXEC change
+    }
+}
+
 // Workgroup-uniform max of a lane value that is usually small (block counts):
 // count up with ballots -- a compare and a scalar branch per step -- instead
 // of six dependent ds_bpermute shuffles; shuffles above 64.
@@ -722,6 +770,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint32_t s_next[64];
     __shared__ uint32_t s_flag[3], s_cons[2];
     __shared__ uint32_t s_nbx[64];  // fused targets' block counts (the next iteration's max)
+    __shared__ uint4 s_pp[64][2];   // cb0: a finished job's {id, consumer range, valid}, first two edges
     __shared__ unsigned long long s_stamp[2][64];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -792,8 +841,30 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
             uint4 nmlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nmhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
             uint32_t sk = 0;
+            // cb0 (kW == 2, barrier hand-over): from the second pass on every job
+            // is a fusion target whose block 0 the chain wave builds itself --
+            // W[0..15] (wb0) read back from the producer's ring at the previous
+            // job's finish, after the chain OR-ed the new digest into its hole
+            // (nrc: the target's hole record, fetched a job ahead)
+            constexpr bool kCB = kW == 2 && !kStream;
+            uint32_t pass = 0;
+            bool pend = false;  // (producer) s_pp holds the last finished jobs, not yet propagated
+            // cb0: the frontier atomics of a finished job run on the producer
+            // (idle in a pass's last iteration), not on the chain's critical path
+            auto producer_propagate = [&]() {
+                const uint4 q = s_pp[lane][0], e = s_pp[lane][1];
+                const bool v = q.w != 0;
+                if (v) atomicAnd(&a.dirty[q.x >> 5], ~(1u << (q.x & 31)));
+                const uint2 pe[2] = {make_uint2(e.x, e.y), make_uint2(e.z, e.w)};
+                propagate_pre(a, v ? q.y : 0u, v ? q.z : 0u, pe);
+                pend = false;
+            };
+            uint32_t wb0[16];
+            uint2 nrc = make_uint2(0, 0);
+            uint4 ntc[4];  // cb0 = 2: the fusion target's template block 0, fetched a job ahead
             while (maxnb) {
                 RF_STAMP_PL(sk); ++sk;
+                const bool cb0 = kCB && a.cb0 && pass > 0;  // workgroup-uniform
                 const bool fused = fslot != ~0u;
                 // a job is fused in every lane that has one after the first pass
                 const bool wfused = __any(fused);
@@ -820,7 +891,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 if (!kStream && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                 if (kIsProd && has) {
                     cur.fslot = fslot;
-                    if (fused) {
+                    if (cb0) {
+                        cur.begin_chain(m0, reinterpret_cast<const uint4*>(a.tmpl));
+                    } else if (fused) {
                         cur.flo = s_dig[lane][0];
                         cur.fhi = s_dig[lane][1];
                         cur.begin_pre(m0, reinterpret_cast<const uint4*>(a.tmpl), nt, nr, ring);
@@ -872,6 +945,13 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
                     nolo = od[0];
                     nohi = od[1];
+                    if (kCB) {
+                        nrc = a.holes[nm0.z];
+                        if (a.cb0 == 2) {
+                            const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
+                            ntc[0] = nT[0]; ntc[1] = nT[1]; ntc[2] = nT[2]; ntc[3] = nT[3];
+                        }
+                    }
                     if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
                     if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
                     if (nm1.w != ~0u) {
@@ -995,14 +1075,16 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         }
                     }
                 } else {
-                for (uint32_t it = 0; it < maxnb + lag; ++it) {
+                const uint32_t iters = cb0 ? maxnb : maxnb + lag;
+                for (uint32_t it = 0; it < iters; ++it) {
                     if (kIsProd) {
-                        if (it < m0.y && !((a.dbg_twice == 3 && it >= 1) || a.dbg_twice == 4)) {
+                        const uint32_t pb = cb0 ? it + 1 : it;  // the block this iteration builds
+                        if (pb < m0.y && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
                             uint32_t w[16];
-                            cur.block(a, it, ring, w, wfused);
+                            cur.block(a, pb, ring, w, wfused);
                             if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
                             if (kW == 2) {
-                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((it & 1) * 64 + lane) * kPcRow]));
+                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((pb & 1) * 64 + lane) * kPcRow]));
                             } else {
                                 uint4* row = reinterpret_cast<uint4*>(&wbuf[((it & 1) * 64 + lane) * kWRow]);
     #pragma unroll
@@ -1022,6 +1104,15 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 nnm1 = a.meta[2ull * nm1.w + 1];
                             }
                         }
+                        // idle in the last iteration (every block of the pass built):
+                        // the fusion target's template blocks 0 and 1 into the ring,
+                        // for the chain to OR the digest into at the hand-over
+                        if (kCB && a.cb0 && it + 1 == iters && pend) producer_propagate();
+                        if (kCB && a.cb0 && it + 1 == iters && nfu) {
+                            const uint4 b0[4] = {nt[0], nt[1], nt[2], nt[3]}, b1[4] = {nt[4], nt[5], nt[6], nt[7]};
+                            ring_put(ring, 0, b0);
+                            if (nm0.y > 1) ring_put(ring, 16, b1);
+                        }
                     } else if (kIsExp) {
                         if (it >= 1 && it - 1 < m0.y && !((a.dbg_twice == 3 && it >= 2) || a.dbg_twice == 4)) {
                             const uint32_t bb = (it - 1) & 1;
@@ -1034,8 +1125,14 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             }
                             kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(bb * 64 + lane) * kPcRow]));
                         }
-                    } else if (kChain && it >= lag) {
-                        chain_block(it - lag, it - lag, true);
+                    } else if (kChain) {
+                        if (cb0) {
+                            if (it == 0)
+                                chain_expand_b0(wb0, elane, reinterpret_cast<uint4*>(&kw[jl * kPcRow]));
+                            chain_block(it, it, true);
+                        } else if (it >= lag) {
+                            chain_block(it - lag, it - lag, true);
+                        }
                     }
                     lds_barrier();
                     RF_STAMP_PL(sk); ++sk;
@@ -1070,15 +1167,54 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         if (changed && m1.w != ~0u) {
                             next = m1.w;
                             nbn = nm0.y;
-                            s_dig[jl][0] = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
-                                                      bswap32(st.h[3]));
-                            s_dig[jl][1] = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]),
-                                                      bswap32(st.h[7]));
+                            const uint32_t D[8] = {bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]),
+                                                   bswap32(st.h[3]), bswap32(st.h[4]), bswap32(st.h[5]),
+                                                   bswap32(st.h[6]), bswap32(st.h[7])};
+                            if (kCB && a.cb0 == 1) {  // into the target's block 0 (and 1), in the producer's ring
+                                or_digest(&ring_all[jl * kRing], nrc.x, D);
+                            } else if (!(kCB && a.cb0 == 2)) {
+                                s_dig[jl][0] = make_uint4(D[0], D[1], D[2], D[3]);
+                                s_dig[jl][1] = make_uint4(D[4], D[5], D[6], D[7]);
+                            }
                         }
+                    }
+                    if (kCB && a.cb0 == 1) {  // both lanes of the job: the target's W[0..15]
+    #pragma unroll
+                        for (int q = 0; q < 16; ++q) wb0[q] = bswap32(ring_all[jl * kRing + q]);
+                    } else if (kCB && a.cb0 == 2) {
+                        // the digest's big-endian words H0..H7 in both lanes (the
+                        // e-lane holds H4..7, its a-lane H0..3, each the other's
+                        // half by the mirror moves above), then block 0 = the
+                        // template with H at byte 2: W0 = T0 | H0 >> 16, Wk =
+                        // H(k-1):Hk >> 16, W8 = H7 << 16 | T8
+                        const uint32_t E = elane ? ~0u : 0u;
+                        uint32_t H[8];
+                        H[0] = __builtin_amdgcn_bitop3_b32(E, st.h[0], D0, 0xCA);
+                        H[1] = __builtin_amdgcn_bitop3_b32(E, st.h[1], D1, 0xCA);
+                        H[2] = __builtin_amdgcn_bitop3_b32(E, st.h[2], D2, 0xCA);
+                        H[3] = __builtin_amdgcn_bitop3_b32(E, st.h[3], D3, 0xCA);
+                        H[4] = __builtin_amdgcn_bitop3_b32(E, D0, st.h[0], 0xCA);
+                        H[5] = __builtin_amdgcn_bitop3_b32(E, D1, st.h[1], 0xCA);
+                        H[6] = __builtin_amdgcn_bitop3_b32(E, D2, st.h[2], 0xCA);
+                        H[7] = __builtin_amdgcn_bitop3_b32(E, D3, st.h[3], 0xCA);
+                        const uint32_t T[16] = {ntc[0].x, ntc[0].y, ntc[0].z, ntc[0].w, ntc[1].x, ntc[1].y,
+                                                ntc[1].z, ntc[1].w, ntc[2].x, ntc[2].y, ntc[2].z, ntc[2].w,
+                                                ntc[3].x, ntc[3].y, ntc[3].z, ntc[3].w};
+    #pragma unroll
+                        for (int q = 0; q < 16; ++q) wb0[q] = bswap32(T[q]);
+                        wb0[0] |= H[0] >> 16;
+    #pragma unroll
+                        for (int q = 1; q < 8; ++q) wb0[q] = __builtin_amdgcn_alignbit(H[q - 1], H[q], 16);
+                        wb0[8] |= H[7] << 16;
                     }
                     if (elane) {
                         s_next[jl] = next;
                         s_nbx[jl] = nbn;
+                        if (kCB && a.cb0) {
+                            s_pp[jl][0] = make_uint4(p, m1.y, !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z),
+                                                     own ? 1u : 0u);
+                            s_pp[jl][1] = make_uint4(pre[0].x, pre[0].y, pre[1].x, pre[1].y);
+                        }
                     }
                 }
                 RF_STAMP_PL(sk); ++sk;
@@ -1087,21 +1223,26 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 const uint32_t nx = s_next[jl];
                 maxnb = wave_max_small(s_nbx[lane]);
                 if (kChain) {
-                    uint32_t cb = 0, ce = 0;
-                    if (own) {
-                        atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
-                        cb = m1.y;
-                        ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
+                    if (!(kCB && a.cb0)) {
+                        uint32_t cb = 0, ce = 0;
+                        if (own) {
+                            atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                            cb = m1.y;
+                            ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
+                        }
+                        propagate_pre(a, cb, ce, pre);
                     }
-                    propagate_pre(a, cb, ce, pre);
                     const uint64_t fb = __ballot(own && nx != ~0u);
                     if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
                 }
+                if (kIsProd && kCB && a.cb0) pend = true;
                 fslot = has ? m1.x : ~0u;
                 has = nx != ~0u;
                 p = has ? nx : 0u;
+                ++pass;
             }
             if (kStream && kIsProd) drop_pre();
+            if (kIsProd && kCB && pend) producer_propagate();  // the last pass's jobs
         }
     };
     if (wave < 2) {
@@ -1415,7 +1556,7 @@ static uint32_t grid_mark(uint64_t items) {
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0};
     return a;
 }
 
@@ -1459,8 +1600,14 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                                  : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u
                                  : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
                                                               : 0u;
+    // RF_K2_CB0=0: fused jobs' block 0 built by the producer (A/B), else by the chain
+    static const uint32_t cb0 = [] {
+        const char* v = getenv("RF_K2_CB0");
+        return (v && atoi(v) == 0) ? 0u : 1u;
+    }();
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
+                g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
