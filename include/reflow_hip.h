@@ -337,11 +337,12 @@ int rf_graph_set_slots_device(rf_graph *g, const void *d_slots, const void *d_di
 int rf_graph_recompute(rf_graph *g, int full, uint64_t *out_recomputed);
 /* Asynchronous form (no count readback). */
 int rf_graph_recompute_async(rf_graph *g, int full, void *stream);
-/* rf_graph_set_slots_device + rf_graph_recompute_async(g, 0, stream) as ONE
- * graph launch (the changed inputs' mark kernel is the graph's first node,
- * its parameters updated per call on the host): an incremental step with no
- * launch boundary before its first level.  The first call on a fresh graph
- * runs a full recompute. */
+/* rf_graph_set_slots_device + rf_graph_recompute_async(g, 0, stream) in one
+ * call.  By default that is the mark kernel and the step's plain level
+ * launches (measured faster than a graph replay); with RF_K2_GRAPH=1 it is ONE
+ * graph launch (the mark kernel the graph's first node, its parameters updated
+ * per call on the host).  The first call on a fresh graph runs a full
+ * recompute. */
 int rf_graph_update_recompute_async(rf_graph *g, const void *d_slots, const void *d_digests32, uint32_t n,
                                     void *stream);
 int rf_graph_get_slots(rf_graph *g, const uint32_t *slots, uint32_t n, uint8_t *out32);

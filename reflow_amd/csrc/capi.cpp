@@ -1364,7 +1364,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
         (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_lmeta.ensure(32ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_counts.ensure(4ull * (L + 1))) != hipSuccess ||
+        (e = gr->b_counts.ensure(8ull * (L + 1))) != hipSuccess ||  // two halves (plain-step parity)
         (e = gr->b_counts_last.ensure(4ull * (L + 1))) != hipSuccess ||
         (e = up(gr->b_lvl_start, G.lvl_start.data(), 4ull * (L + 1))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
@@ -1372,7 +1372,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     HIPC(gr->b_holes.ensure(8));  // k2's record loads read element 0 unconditionally
     HIPC(sync_memset(ctx, gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
     HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
-    HIPC(sync_memset(ctx, gr->b_counts.p, 0, 4ull * (L + 1)));
+    HIPC(sync_memset(ctx, gr->b_counts.p, 0, 8ull * (L + 1)));
     HIPC(sync_memset(ctx, gr->b_counts_last.p, 0, 4ull * (L + 1)));
     G.meta = gr->b_meta.as<uint4>();
     G.holes = gr->b_holes.as<uint2>();
@@ -1384,7 +1384,9 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     G.list = gr->b_list.as<uint32_t>();
     G.lmeta = gr->b_lmeta.as<uint4>();
     G.counts = gr->b_counts.as<uint32_t>();
+    G.counts_other = G.counts + (L + 1);
     G.counts_last = gr->b_counts_last.as<uint32_t>();
+    gr->last_counts = G.counts_last;
     G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
     if (n_lead && !getenv("RF_K2_NO_MIDSTATE")) {  // (RF_K2_NO_MIDSTATE: A/B)
         struct Tmp {
@@ -1484,11 +1486,30 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
 // host launch each; MI355X_MICROARCH "boundary" / "graph-replay-floor").  An
 // incremental step leaves the dirty set empty (each hashed job clears its
 // bit); a full one discards whatever set_slots queued.
-static int graph_enqueue(rf_graph* gr, int full, hipStream_t s) {
+static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = false) {
     GraphDev& G = gr->g;
+    bool any = false;
+    for (uint32_t l = 0; l < G.n_levels; ++l) any |= G.inc_level[l] != 0;
+    if (plain && !full && any) {
+        // the first launched level zeroes the previous step's half; the next
+        // step (and set_slots / imports before it) uses that half
+        bool first = true;
+        for (uint32_t l = 0; l < G.n_levels; ++l) {
+            if (!G.inc_level[l]) continue;
+            HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr));
+            first = false;
+        }
+        gr->last_counts = G.counts;
+        std::swap(G.counts, G.counts_other);
+        return RF_OK;
+    }
     for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
     HIPC(launch_graph_step_end(G, full, s));
-    if (full) HIPC(hipMemsetAsync(G.dirty, 0, 4ull * ((G.n_jobs + 31) / 32 + 1), s));
+    gr->last_counts = G.counts_last;
+    if (full) {
+        HIPC(hipMemsetAsync(G.dirty, 0, 4ull * ((G.n_jobs + 31) / 32 + 1), s));
+        HIPC(hipMemsetAsync(G.counts_other, 0, 4ull * (G.n_levels + 1), s));  // both halves clear
+    }
     return RF_OK;
 }
 
@@ -1510,22 +1531,33 @@ static int graph_capture(rf_graph* gr, int full, hipGraphExec_t* out) {
     return RF_OK;
 }
 
-int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
-    if (!gr->initialized) full = 1;
-    // An incremental step launches only its few queueable levels (configs[2]:
-    // two level kernels and k3_step_end): queued back to back as plain
-    // launches they start sooner than as a replayed hipGraph (same-box A/B:
-    // 0.1827 -> 0.1752 ms per step).  The full recompute (every level) keeps
-    // its graph.  RF_K2_GRAPH=1: the incremental graph (A/B).
-    static const bool no_graph = [] {
+// An incremental step launches only its few queueable levels (configs[2]:
+// two level kernels): queued back to back as plain launches they start
+// sooner than as a replayed hipGraph (same-box A/B: 0.1827 -> 0.1752 ms per
+// step), and with the cursor halves alternating (GraphDev::counts_other) no
+// step-end kernel is needed.  The full recompute (every level) keeps its
+// graph.  RF_K2_GRAPH=1: the incremental graph (A/B).
+static bool inc_plain() {
+    static const bool on = [] {
         const char* v = getenv("RF_K2_GRAPH");
         return !(v && atoi(v) == 1);
     }();
-    if (no_graph && !full) {
+    return on;
+}
+
+int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
+    if (!gr->initialized) full = 1;
+    const bool no_graph = inc_plain();
+    static const bool full_plain = [] {  // RF_K2_FULL_GRAPH=0 (A/B): the full recompute as plain launches too
+        const char* v = getenv("RF_K2_FULL_GRAPH");
+        return v && atoi(v) == 0;
+    }();
+    if ((no_graph && !full) || (full_plain && full)) {
         HIPC(hipEventRecord(gr->e0, s));
-        if (int rc = graph_enqueue(gr, 0, s)) return rc;
+        if (int rc = graph_enqueue(gr, full, s, true)) return rc;
         HIPC(hipEventRecord(gr->e1, s));
         gr->timed = true;
+        gr->initialized = true;
         return RF_OK;
     }
     hipGraphExec_t& ex = full ? gr->exec_full : gr->exec_inc;
@@ -1533,6 +1565,7 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
         if (int rc = graph_capture(gr, full, &ex)) return rc;
     HIPC(hipEventRecord(gr->e0, s));
     if (ex) HIPC(hipGraphLaunch(ex, s));
+    gr->last_counts = gr->g.counts_last;
     HIPC(hipEventRecord(gr->e1, s));
     gr->timed = true;
     gr->initialized = true;
@@ -1588,10 +1621,10 @@ extern "C" int rf_graph_update_recompute_async(rf_graph* gr, const void* d_slots
     std::lock_guard<std::mutex> lk(gr->ctx->mu);
     DevGuard dg(gr->ctx->device);
     hipStream_t s = pick(gr->ctx, stream);
-    if (!gr->initialized) {  // the first recompute is a full one: mark, then the full sequence
+    if (!gr->initialized || inc_plain()) {  // mark, then the level launches (first call: the full sequence)
         HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
                                      static_cast<const uint8_t*>(d_digests32), n, s));
-        return graph_recompute_locked(gr, 1, s);
+        return graph_recompute_locked(gr, gr->initialized ? 0 : 1, s);
     }
     MarkArgs ma;
     hipKernelNodeParams mp{};
@@ -1624,7 +1657,7 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
     if (int rc = graph_recompute_locked(gr, full, ctx->stream)) return rc;
     std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
     if (gr->g.n_levels)  // [L]: jobs hashed inside fused chains
-        HIPC(hipMemcpyAsync(counts.data(), gr->g.counts_last, 4ull * (gr->g.n_levels + 1),
+        HIPC(hipMemcpyAsync(counts.data(), gr->last_counts, 4ull * (gr->g.n_levels + 1),
                             hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
     uint64_t tot = 0;

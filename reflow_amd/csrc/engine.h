@@ -82,6 +82,11 @@ struct GraphDev {
     uint4* lmeta = nullptr;          // [2J] each listed job's record, at its list position
     uint32_t* counts = nullptr;      // [L+1] list lengths (append cursors); [L] = fused jobs hashed
     uint32_t* counts_last = nullptr; // [L+1] jobs hashed per level by the last recompute; [L] fused
+    // Plain-launch incremental steps alternate between two halves of the
+    // cursor array (counts = the half the next step appends to and reads,
+    // counts_other = the previous step's, zeroed by this step's first level
+    // kernel), so no step-end kernel is needed.
+    uint32_t* counts_other = nullptr;
     uint32_t* lvl_start_dev = nullptr; // [L+1]
     std::vector<uint32_t> lvl_start; // host copy [L+1]
     std::vector<uint8_t> inc_level;  // [L] level has jobs that can be queued (not all fusion targets)
@@ -116,7 +121,8 @@ struct MarkArgs {
 void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,
                        MarkArgs* args, hipKernelNodeParams* p);
 const void* graph_mark_kernel();
-hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s);
+hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s,
+                              uint32_t* zero_counts = nullptr);
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);

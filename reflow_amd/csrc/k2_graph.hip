@@ -57,7 +57,15 @@ struct LevelArgs {
     const uint32_t* __restrict__ cons_ptr;  // [S+1] slot -> reverse-edge range (mark / apply kernels)
     uint4* lmeta;                           // [2J] the listed jobs' records, beside list
     uint32_t cb0;  // k2_level_pl<2,false>: chain-built block 0 of fused jobs (1: via the ring, 2: in registers)
+    uint32_t* zero_counts;  // [L+1] the previous plain step's cursor half, zeroed by workgroup 0 (or null)
 };
+
+// (first level kernel of a plain incremental step) the previous step's
+// cursor half back to zero -- nobody reads or appends to it during this step
+__device__ __forceinline__ void zero_other_counts(const LevelArgs& a) {
+    if (a.zero_counts && blockIdx.x == 0)
+        for (uint32_t l = threadIdx.x; l <= a.n_levels; l += blockDim.x) a.zero_counts[l] = 0;
+}
 
 // Reverse edges of an INPUT slot: bit 31 of the level field flags its
 // slot-fused consumer (at most one, first in the slot's range): a job whose
@@ -440,6 +448,7 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 chain, 1 producer, 2 expander
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* ring = &ring_all[lane * kRing];
+    zero_other_counts(a);
     const uint32_t n = a.counts[a.lvl];
     const uint32_t* lst = a.list + a.s;
     for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
@@ -808,6 +817,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     const uint32_t one = 1u, zero = 0u;
     constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    zero_other_counts(a);
     const uint32_t n = a.counts[a.lvl];
     const uint32_t* lst = a.list + a.s;
     const uint4* lmt = a.lmeta + 2ull * a.s;
@@ -1556,7 +1566,7 @@ static uint32_t grid_mark(uint64_t items) {
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, nullptr};
     return a;
 }
 
@@ -1590,7 +1600,7 @@ void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* 
 
 const void* graph_mark_kernel() { return reinterpret_cast<const void*>(k3_mark_slots); }
 
-hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s) {
+hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s, uint32_t* zero_counts) {
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
     // RF_DBG_HASH2: hash twice (k2_level); RF_K2_STAMPS=2: per-chunk stamps (k2_level_pl)
@@ -1607,7 +1617,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }();
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
-                g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u};
+                g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, zero_counts};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
