@@ -353,7 +353,8 @@ typedef struct {
     uint32_t n_jobs, n_slots, n_levels, max_level_jobs;
     uint64_t total_blocks, hole_count, template_bytes;
     uint64_t last_recomputed;
-    float last_ms;
+    float last_ms; /* device time of the last synchronous rf_graph_recompute (asynchronous
+                    * incremental steps record no events: RF_K2_EVENTS=1 does) */
 } rf_graph_stats;
 int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
 

@@ -1537,6 +1537,12 @@ static int graph_capture(rf_graph* gr, int full, hipGraphExec_t* out) {
 // step), and with the cursor halves alternating (GraphDev::counts_other) no
 // step-end kernel is needed.  The full recompute (every level) keeps its
 // graph.  RF_K2_GRAPH=1: the incremental graph (A/B).
+// RF_K2_EVENTS=1: record the timing events on asynchronous recomputes too
+static bool events_always() {
+    static const bool on = getenv("RF_K2_EVENTS") && atoi(getenv("RF_K2_EVENTS")) == 1;
+    return on;
+}
+
 static bool inc_plain() {
     static const bool on = [] {
         const char* v = getenv("RF_K2_GRAPH");
@@ -1553,10 +1559,14 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
         return v && atoi(v) == 0;
     }();
     if ((no_graph && !full) || (full_plain && full)) {
-        HIPC(hipEventRecord(gr->e0, s));
+        // the timing events (rf_graph_stats.last_ms) only where a caller waits
+        // anyway: each event record put a ~6 us bubble on either side of the
+        // step's level launches (rocprofv3 trace)
+        const bool ev = gr->time_next || events_always();
+        if (ev) HIPC(hipEventRecord(gr->e0, s));
         if (int rc = graph_enqueue(gr, full, s, true)) return rc;
-        HIPC(hipEventRecord(gr->e1, s));
-        gr->timed = true;
+        if (ev) HIPC(hipEventRecord(gr->e1, s));
+        gr->timed = ev;
         gr->initialized = true;
         return RF_OK;
     }
@@ -1654,7 +1664,10 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
     rf_ctx* ctx = gr->ctx;
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
-    if (int rc = graph_recompute_locked(gr, full, ctx->stream)) return rc;
+    gr->time_next = true;
+    const int rc0 = graph_recompute_locked(gr, full, ctx->stream);
+    gr->time_next = false;
+    if (rc0) return rc0;
     std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
     if (gr->g.n_levels)  // [L]: jobs hashed inside fused chains
         HIPC(hipMemcpyAsync(counts.data(), gr->last_counts, 4ull * (gr->g.n_levels + 1),

@@ -43,6 +43,7 @@ struct rf_graph {
     hipGraphExec_t exec_upd = nullptr;
     hipGraphNode_t upd_mark = nullptr;
     bool timed = false;
+    bool time_next = false;  // record e0/e1 around the next plain recompute (synchronous callers)
     uint32_t* last_counts = nullptr;  // device cursors of the last recompute (counts_last, or a plain step's half)
     GraphPart* part = nullptr;  // multi-GPU partition (rf_graph_set_part), else null
 };
