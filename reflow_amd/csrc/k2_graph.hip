@@ -780,6 +780,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint32_t s_flag[3], s_cons[2];
     __shared__ uint32_t s_nbx[64];  // fused targets' block counts (the next iteration's max)
     __shared__ uint4 s_pp[64][2];   // cb0: a finished job's {id, consumer range, valid}, first two edges
+    __shared__ uint32_t s_w0[kStream ? 64 * 17 : 1];  // stream cb0: W[0..15] per job, staged by the chain
+    __shared__ uint32_t s_cw[2];                      // ... block id + 1 staged, per chain wave
     __shared__ unsigned long long s_stamp[2][64];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -799,6 +801,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     if (threadIdx.x == 0) {
         s_flag[0] = s_flag[1] = s_flag[2] = 0;
         s_cons[0] = s_cons[1] = 0;
+        s_cw[0] = s_cw[1] = 0;
     }
     if (a.stamps && threadIdx.x < 128) s_stamp[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     lds_barrier();
@@ -875,6 +878,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             while (maxnb) {
                 RF_STAMP_PL(sk); ++sk;
                 const bool cb0 = kCB && a.cb0 && pass > 0;  // workgroup-uniform
+                // streamed hand-over with a register-built block 0: the chain
+                // writes chunk 0 (K+W[0..15]) itself and stages W[0..15] for the
+                // producer, which expands chunks 1-3 while the chain runs rounds 0-15
+                const bool sc = kStream && a.cb0 == 2 && pass > 0;
                 const bool fused = fslot != ~0u;
                 // a job is fused in every lane that has one after the first pass
                 const bool wfused = __any(fused);
@@ -901,7 +908,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 if (!kStream && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                 if (kIsProd && has) {
                     cur.fslot = fslot;
-                    if (cb0) {
+                    if (cb0 || sc) {
                         cur.begin_chain(m0, reinterpret_cast<const uint4*>(a.tmpl));
                     } else if (fused) {
                         cur.flo = s_dig[lane][0];
@@ -955,7 +962,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
                     nolo = od[0];
                     nohi = od[1];
-                    if (kCB) {
+                    if (kW == 2) {
                         nrc = a.holes[nm0.z];
                         if (a.cb0 == 2) {
                             const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
@@ -980,9 +987,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 // finishes block b-1: feed-forward, the a-half's last two rounds)
                 // b: the job's block (capture rule), bufb: its row buffer (kStream:
                 // the global block gb, whose chunks it waits for)
-                auto chain_block = [&](uint32_t b, uint32_t bufb, bool full) {
+                auto chain_block = [&](uint32_t b, uint32_t bufb, bool full, bool own0 = false) {
                     const uint32_t bi = kStream ? bufb % 3 : (bufb & 1);
-                    if (kStream && full) known = lds_poll(&s_flag[bi], 4 * bufb + 1, 4 * bufb);
+                    if (kStream && full && !own0) known = lds_poll(&s_flag[bi], 4 * bufb + 1, 4 * bufb);
                     if (kStream && full && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                     const uint32_t row_off = ((bi * 64 + jl) * kPcRow) * 4, ones_off = kBufs * 64 * kPcRow * 4;
                     const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
@@ -1027,19 +1034,32 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                             const bool mine = b < m0.y;
                             uint32_t w[16];
-                            if (mine) cur.block(a, b, ring, w, wfused);
                             volatile uint32_t* fl = &s_flag[gb % 3];
                             uint4* row = reinterpret_cast<uint4*>(&kw[((gb % 3) * 64 + lane) * kPcRow]);
+                            if (sc && b == 0) {
+                                // the chain wrote chunk 0 and staged W[0..15]: expand 1-3
+                                (void)lds_poll(&s_cw[0], gb + 1, 0u);
+                                (void)lds_poll(&s_cw[1], gb + 1, 0u);
     #pragma unroll
-                            for (int c = 0; c < 4; ++c) {
-                                if (mine) kw_expand_chunk(w, row, c);
-                                if (c == 0)  // the chain starts on it: publish at once
-                                    lds_publish(fl, 4 * gb + 1, lane);
-                                else if (c >= 2)  // chunk c - 1, its writes drained behind chunk c's
-                                    lds_publish_prev(fl, 4 * gb + c, lane);
-                                if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                                for (int q = 0; q < 16; ++q) w[q] = s_w0[lane * 17 + q];
+    #pragma unroll
+                                for (int c = 1; c < 4; ++c) {
+                                    if (mine) kw_expand_chunk(w, row, c);
+                                    lds_publish(fl, 4 * gb + c + 1, lane);
+                                }
+                            } else {
+                                if (mine) cur.block(a, b, ring, w, wfused);
+    #pragma unroll
+                                for (int c = 0; c < 4; ++c) {
+                                    if (mine) kw_expand_chunk(w, row, c);
+                                    if (c == 0)  // the chain starts on it: publish at once
+                                        lds_publish(fl, 4 * gb + 1, lane);
+                                    else if (c >= 2)  // chunk c - 1, its writes drained behind chunk c's
+                                        lds_publish_prev(fl, 4 * gb + c, lane);
+                                    if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                                }
+                                lds_publish(fl, 4 * gb + 4, lane);
                             }
-                            lds_publish(fl, 4 * gb + 4, lane);
                             if (b == 0 && nfu) {
                                 const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
                                 nt[0] = nT[0]; nt[1] = nT[1]; nt[2] = nT[2]; nt[3] = nT[3];
@@ -1060,6 +1080,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         // in block 0) and the target has exactly two blocks
                         const bool need = nfu && nm0.y >= 2;
                         const bool can = nm0.y == 2 && nr.x + 32 <= 64;
+                        if (a.cb0 == 2 && nfu && nm0.y > 1) {
+                            const uint4 b1[4] = {nt[4], nt[5], nt[6], nt[7]};
+                            ring_put(ring, 16, b1);
+                        }
                         drop_pre();
                         if (__any(need) && __all(!need || can)) {
                             const uint32_t id1 = gb + 1;
@@ -1079,7 +1103,22 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         }
                     } else {
                         for (uint32_t b = 0; b < maxnb; ++b, ++gb) {
-                            chain_block(b, gb, true);
+                            const bool own0 = sc && b == 0;
+                            if (own0) {  // chunk 0 into the row, W[0..15] staged for the producer
+                                constexpr uint32_t K[16] = {0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u,
+                                                            0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+                                                            0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u,
+                                                            0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u};
+                                uint4* row = reinterpret_cast<uint4*>(&kw[((gb % 3) * 64 + jl) * kPcRow]);
+    #pragma unroll
+                                for (int q = 0; q < 4; ++q)
+                                    row[q] = make_uint4(K[4 * q] + wb0[4 * q], K[4 * q + 1] + wb0[4 * q + 1],
+                                                        K[4 * q + 2] + wb0[4 * q + 2], K[4 * q + 3] + wb0[4 * q + 3]);
+    #pragma unroll
+                                for (int q = 0; q < 16; ++q) s_w0[jl * 17 + q] = wb0[q];
+                                lds_publish(&s_cw[wave], gb + 1, lane);
+                            }
+                            chain_block(b, gb, true, own0);
                             lds_publish(&s_cons[wave], gb + 1, lane);
                             RF_STAMP_PL(sk); ++sk;
                         }
@@ -1182,7 +1221,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                                    bswap32(st.h[6]), bswap32(st.h[7])};
                             if (kCB && a.cb0 == 1) {  // into the target's block 0 (and 1), in the producer's ring
                                 or_digest(&ring_all[jl * kRing], nrc.x, D);
-                            } else if (!(kCB && a.cb0 == 2)) {
+                            } else if (!(kW == 2 && a.cb0 == 2)) {
                                 s_dig[jl][0] = make_uint4(D[0], D[1], D[2], D[3]);
                                 s_dig[jl][1] = make_uint4(D[4], D[5], D[6], D[7]);
                             }
@@ -1191,7 +1230,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     if (kCB && a.cb0 == 1) {  // both lanes of the job: the target's W[0..15]
     #pragma unroll
                         for (int q = 0; q < 16; ++q) wb0[q] = bswap32(ring_all[jl * kRing + q]);
-                    } else if (kCB && a.cb0 == 2) {
+                    } else if (kW == 2 && a.cb0 == 2) {
                         // the digest's big-endian words H0..H7 in both lanes (the
                         // e-lane holds H4..7, its a-lane H0..3, each the other's
                         // half by the mirror moves above), then block 0 = the
