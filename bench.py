@@ -119,17 +119,10 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            # gloo prints "[Gloo] Rank r is connected ..." on the C-level
-            # stdout: keep stdout for the one JSON line (send it to stderr)
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-                dist.barrier()
-            finally:
-                os.dup2(saved, 1)
-                os.close(saved)
+            # (gloo's "[Gloo] Rank r is connected ..." goes to stderr: main()
+            # points the C-level stdout there for the whole run)
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            dist.barrier()
             self.dist = dist
         if n_gpus != self.world and self.world > 1:
             log("warning: --gpus %d but WORLD_SIZE %d" % (n_gpus, self.world))
@@ -481,7 +474,7 @@ def bench_dag(args, dist, ctx, comm, budget):
     if part is not None:
         g.set_part(part.part)
         ag = None
-        if comm is None:  # RF_BENCH_SHARE_GPU rehearsal: gloo host transport
+        if comm is None:  # RF_BENCH_SHARE_GPU rehearsal (or no RCCL communicator): gloo host transport
             ag = lambda b: [x.tobytes() for x in np.split(dist.all_gather_bytes(np.frombuffer(b, np.uint8)), dist.world)]  # noqa: E731,E501
 
         def recompute(full, count=True):
@@ -954,6 +947,13 @@ def cpu_baseline(args, sha, dag_res, budget):
 
 
 def main():
+    # stdout carries exactly ONE line, the JSON result: everything else any
+    # library prints on the C-level stdout (gloo's "[Gloo] Rank r is
+    # connected", RCCL's "RCCL version : ..." banner and NCCL WARN lines at
+    # communicator init) goes to stderr; the result is written to the saved fd
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -984,12 +984,26 @@ def main():
     ctx = capi.Context(device)
     comm, exchange = None, "none (1 rank)"
     if dist.world > 1:
-        if share:
+        # RF_BENCH_TRY_RCCL=1 with RF_BENCH_SHARE_GPU: attempt the communicator anyway (RCCL refuses two
+        # ranks on one GPU), which rehearses the fallback below
+        if share and os.environ.get("RF_BENCH_TRY_RCCL") != "1":
             exchange = "gloo host all-gather (RF_BENCH_SHARE_GPU: RCCL needs one GPU per rank)"
         else:
             uid = dist.bcast_bytes(capi.Comm.unique_id() if dist.rank == 0 else None)
-            comm = capi.Comm(ctx, dist.world, dist.rank, uid)
-            exchange = "RCCL all-gather over xGMI"
+            err = None
+            try:
+                comm = capi.Comm(ctx, dist.world, dist.rank, uid)
+            except Exception as e:  # noqa: BLE001 - keep the run: the DAG exchange then goes over gloo
+                err, comm = str(e), None
+            # every rank must take the same transport
+            if dist.max(1.0 if comm is None else 0.0) > 0:
+                if comm is not None:
+                    comm.close()
+                    comm = None
+                exchange = "gloo host all-gather (RCCL communicator failed: %s)" % (err or "on another rank")
+                log("warning: " + exchange)
+            else:
+                exchange = "RCCL all-gather over xGMI"
 
     sha = bench_sha(args, dist, ctx, budget)
     c1 = bench_c1(args, dist, ctx, budget) if "c1" not in args.skip and budget.allow("c1", 15) else None
@@ -1043,7 +1057,8 @@ def main():
             "budget": {"seconds": args.budget_s, "skipped": budget.skipped,
                        "elapsed_s": round(time.perf_counter() - T_START, 1)},
         }
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(result_fd, (json.dumps(line) + "\n").encode())
     if comm is not None:
         comm.close()
     ctx.close()
