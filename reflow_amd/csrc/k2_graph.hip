@@ -415,6 +415,9 @@ __device__ __forceinline__ void lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+#ifndef RF_K2_JOIN_WAIT
+#define RF_K2_JOIN_WAIT 0  // (A/B build: 1 = the compiler's wait at the join)
+#endif
 constexpr uint32_t kPcRow = 68;  // words per K+W row: 16-B reads of 64 rows hit distinct banks
 
 // Fused chains: a job whose only input is one job's digest, and which that
@@ -873,6 +876,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 pend = false;
             };
             uint32_t wb0[16];
+    #pragma unroll
+            for (int q = 0; q < 16; ++q) wb0[q] = lane + q;  // (pass 0's warm-up expands these)
             uint2 nrc = make_uint2(0, 0);
             uint4 ntc[4];  // cb0 = 2: the fusion target's template block 0, fetched a job ahead
             while (maxnb) {
@@ -901,6 +906,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 if (nfu && !fused) {
                     nm0 = a.meta[2ull * m1.w];
                     nm1 = a.meta[2ull * m1.w + 1];
+                    // (chain: as below -- the wait in the branch, not at the join;
+                    // the chain idles in a pass-0 job's first iteration anyway)
+                    if (kChain && !RF_K2_JOIN_WAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
                 }
                 MatCursor cur;
                 uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
@@ -939,6 +947,12 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             hlo = a.mid[2ull * p];
                             hhi = a.mid[2ull * p + 1];
                         }
+                        // Wait for these loads here, inside the branch: at the join
+                        // below the compiler placed a vmcnt(0) that every pass ran,
+                        // and on a fused pass it waited for the previous job's digest
+                        // store and atomics (vmcnt counts stores on gfx9): ~1-4 us
+                        // on each link's block 0 (stamps, pass 1 5.4 us vs 1.7).
+                        if (!RF_K2_JOIN_WAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
                     }
                 }
                 if (kIsExp && nfu && nm1.w != ~0u) {
@@ -1175,13 +1189,25 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(bb * 64 + lane) * kPcRow]));
                         }
                     } else if (kChain) {
-                        if (cb0) {
-                            if (it == 0)
-                                chain_expand_b0(wb0, elane, reinterpret_cast<uint4*>(&kw[jl * kPcRow]));
-                            chain_block(it, it, true);
-                        } else if (it >= lag) {
-                            chain_block(it - lag, it - lag, true);
+                        // One call site each for the expansion and the block step, so
+                        // pass 0 (producer-built rows) and the cb0 passes run the same
+                        // code.  Every launch starts with a cold instruction cache:
+                        // the first cb0 pass used to fetch ~9 KB of new code (its own
+                        // inlined block step and the expansion) and took ~4.5 us
+                        // longer than the later links.  In pass 0's first iteration
+                        // the chain only waits for the producer's first row, so it
+                        // runs the expansion there once on dummy words into the
+                        // other row buffer (the producer writes it only after the
+                        // barrier): the code is then cached when the links start.
+                        const bool exb = it == 0 && (cb0 || (kCB && a.cb0 && pass == 0 && a.dbg_twice != 5));
+                        if (exb)
+                            chain_expand_b0(wb0, elane, reinterpret_cast<uint4*>(&kw[((cb0 ? 0u : 64u) + jl) * kPcRow]));
+                        if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
+                        if (cb0 || it >= lag) {
+                            const uint32_t cbk = cb0 ? it : it - lag;
+                            chain_block(cbk, cbk, true);
                         }
+                        if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
                     }
                     lds_barrier();
                     RF_STAMP_PL(sk); ++sk;
@@ -1644,7 +1670,8 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     if (e <= b) return hipSuccess;
     // RF_DBG_HASH2: hash twice (k2_level); RF_K2_STAMPS=2: per-chunk stamps (k2_level_pl)
     // RF_K2_DBG_NOEXP=3|4 (timing diagnostic, WRONG digests): the producer
-    // skips assembling + expanding blocks >= 1 (3) or every block (4)
+    // skips assembling + expanding blocks >= 1 (3) or every block (4); =5
+    // (A/B, digests right): no instruction-cache warm-up in k2_level_pl's pass 0
     static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u
                                  : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u
                                  : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
