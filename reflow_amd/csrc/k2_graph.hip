@@ -1437,6 +1437,24 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
                 cur.block(a, b, ring, w, true);
                 sha256_compress(st, w);
             }
+            // The next job's operands (issued at this job's start: arrived) are
+            // made to count as arrived here, before the digest store and the
+            // frontier atomics: vmcnt also counts stores, and the compiler's wait
+            // for them after the store was a vmcnt(0) -- a store acknowledgement
+            // on every job of the chain (as in k2_level_pl).
+            if (!RF_K2_JOIN_WAIT) {
+                __asm__ volatile("" ::"v"(nt[0].x), "v"(nt[0].y), "v"(nt[0].z), "v"(nt[0].w), "v"(nt[1].x), "v"(nt[1].y),
+                                 "v"(nt[1].z), "v"(nt[1].w), "v"(nt[2].x), "v"(nt[2].y), "v"(nt[2].z), "v"(nt[2].w),
+                                 "v"(nt[3].x), "v"(nt[3].y), "v"(nt[3].z), "v"(nt[3].w));
+                __asm__ volatile("" ::"v"(nt[4].x), "v"(nt[4].y), "v"(nt[4].z), "v"(nt[4].w), "v"(nt[5].x), "v"(nt[5].y),
+                                 "v"(nt[5].z), "v"(nt[5].w), "v"(nt[6].x), "v"(nt[6].y), "v"(nt[6].z), "v"(nt[6].w),
+                                 "v"(nt[7].x), "v"(nt[7].y), "v"(nt[7].z), "v"(nt[7].w));
+                __asm__ volatile("" ::"v"(nolo.x), "v"(nolo.y), "v"(nolo.z), "v"(nolo.w), "v"(nohi.x), "v"(nohi.y),
+                                 "v"(nohi.z), "v"(nohi.w), "v"(nhlo.x), "v"(nhlo.y), "v"(nhlo.z), "v"(nhlo.w),
+                                 "v"(nhhi.x), "v"(nhhi.y), "v"(nhhi.z), "v"(nhhi.w));
+                __asm__ volatile("" ::"v"(nnm0.x), "v"(nnm0.y), "v"(nnm0.z), "v"(nnm0.w), "v"(nnm1.x), "v"(nnm1.y),
+                                 "v"(nnm1.z), "v"(nnm1.w), "v"(nr.x), "v"(nr.y));
+            }
             const bool ch = finish_job_pre(a, m1, st, olo, ohi);
             ++hashed;
             cb = m1.y;
