@@ -875,6 +875,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 propagate_pre(a, v ? q.y : 0u, v ? q.z : 0u, pe);
                 pend = false;
             };
+            // kW = 3: as with cb0, a finished job's frontier atomics run on the
+            // producer in its idle last iteration of the next pass, not on the
+            // chain's critical path (RF_K2_DBG_NOEXP=6: on the chain, A/B)
+            const bool pp3 = kW == 3 && !kStream && a.dbg_twice != 6;
             uint32_t wb0[16];
     #pragma unroll
             for (int q = 0; q < 16; ++q) wb0[q] = lane + q;  // (pass 0's warm-up expands these)
@@ -1170,7 +1174,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         // idle in the last iteration (every block of the pass built):
                         // the fusion target's template blocks 0 and 1 into the ring,
                         // for the chain to OR the digest into at the hand-over
-                        if (kCB && a.cb0 && it + 1 == iters && pend) producer_propagate();
+                        if (((kCB && a.cb0) || pp3) && it + 1 == iters && pend) producer_propagate();
                         if (kCB && a.cb0 && it + 1 == iters && nfu) {
                             const uint4 b0[4] = {nt[0], nt[1], nt[2], nt[3]}, b1[4] = {nt[4], nt[5], nt[6], nt[7]};
                             ring_put(ring, 0, b0);
@@ -1285,7 +1289,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     if (elane) {
                         s_next[jl] = next;
                         s_nbx[jl] = nbn;
-                        if (kCB && a.cb0) {
+                        if ((kCB && a.cb0) || pp3) {
                             s_pp[jl][0] = make_uint4(p, m1.y, !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z),
                                                      own ? 1u : 0u);
                             s_pp[jl][1] = make_uint4(pre[0].x, pre[0].y, pre[1].x, pre[1].y);
@@ -1298,7 +1302,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 const uint32_t nx = s_next[jl];
                 maxnb = wave_max_small(s_nbx[lane]);
                 if (kChain) {
-                    if (!(kCB && a.cb0)) {
+                    if (!(kCB && a.cb0) && !pp3) {
                         uint32_t cb = 0, ce = 0;
                         if (own) {
                             atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
@@ -1310,14 +1314,14 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     const uint64_t fb = __ballot(own && nx != ~0u);
                     if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
                 }
-                if (kIsProd && kCB && a.cb0) pend = true;
+                if (kIsProd && ((kCB && a.cb0) || pp3)) pend = true;
                 fslot = has ? m1.x : ~0u;
                 has = nx != ~0u;
                 p = has ? nx : 0u;
                 ++pass;
             }
             if (kStream && kIsProd) drop_pre();
-            if (kIsProd && kCB && pend) producer_propagate();  // the last pass's jobs
+            if (kIsProd && (kCB || kW == 3) && pend) producer_propagate();  // the last pass's jobs
         }
     };
     if (wave < 2) {
@@ -1689,7 +1693,8 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     // RF_DBG_HASH2: hash twice (k2_level); RF_K2_STAMPS=2: per-chunk stamps (k2_level_pl)
     // RF_K2_DBG_NOEXP=3|4 (timing diagnostic, WRONG digests): the producer
     // skips assembling + expanding blocks >= 1 (3) or every block (4); =5
-    // (A/B, digests right): no instruction-cache warm-up in k2_level_pl's pass 0
+    // (A/B, digests right): no instruction-cache warm-up in k2_level_pl's pass 0;
+    // =6 (A/B): k2_level_pl<3>'s frontier atomics on the chain, not the producer
     static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u
                                  : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u
                                  : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
