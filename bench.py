@@ -275,34 +275,56 @@ def bench_sha(args, dist, ctx, budget):
         lk = "k1_sha256_octo" if len(lane_ids) <= 4 * n_simd else "k1_sha256_pair" if len(lane_ids) <= 16 * n_simd \
             else "k1_sha256_lanes"
         legs.append((lk, lane_ids, float(np.mean(rec["lanes"]))))
-    dom = max(legs, key=lambda x: x[2]) if legs else None
-    roof = kernel_roofline(dom[0], lens, dom[1], dom[2]) if dom else None
+    gpu_roofs = [kernel_roofline(name, lens, ids, ms) for name, ids, ms in legs]
+    for r, (name, ids, ms) in zip(gpu_roofs, legs):
+        r["traffic"] = None
+        r["traffic_note"] = ("not measured in the hybrid step: device-wide FETCH/WRITE counters there also see the "
+                             "host leg's D2H stream; the GPU-only pass (roofline_gpu_only) measures the duo alone")
     workload = ("configs[1]: %.1f GiB Fileset per GPU, %d files 4 KiB-2 GiB (98%% log-uniform 4 KiB-1 MiB, "
                 "2%% 64 MiB-2 GiB), SHA-256 of every file" % (lens.sum() / GiB, len(lens)))
-    if roof:
-        traffic, tsrc = pmc_traffic(roof["kernel"], workload, roof["bytes_per_launch"])
-        roof["traffic"] = traffic
-        if traffic and traffic > 2 * roof["bytes_per_launch"]:
-            roof["traffic_note"] = ("FETCH_SIZE/WRITE_SIZE are device-wide over the launch window: in the hybrid step "
-                                    "they include the host leg's D2H stream of the largest files and the pair "
-                                    "kernel; the GPU-only launch (roofline_gpu_only) measures the duo kernel alone")
-        roof["traffic_source"] = tsrc or "not measured in this process (rocprofv3 --pmc needs its own pass)"
-        roof["legs"] = {name: {"ms": round(ms, 3), "messages": int(len(ids)), "bytes": float(lens[ids].sum())}
-                        for name, ids, ms in legs}
     hb = float(lens[host_ids].sum()) if h else 0.0
     host_ms = float(np.mean(rec["host"])) if h else 0.0
     thr, core_rate, sha_ext = ctx.host_info()
+    ways, thread_rate = ctx.host_rate()
     host_leg = None
+    step_ms = t / args.steps * 1e3
     if h:
         per_thread = hb / (host_ms * 1e-3) / st.host_threads / 1e9
         host_leg = {"threads": int(st.host_threads), "files": h, "bytes": hb, "ms": round(host_ms, 2),
                     "gbps": round(hb / (host_ms * 1e-3) / 1e9, 3), "per_thread_gbps": round(per_thread, 3),
                     "core_sha_ni_gbps": round(core_rate / 1e9, 3),
+                    "thread_rate_gbps": round(thread_rate / 1e9, 3), "chains_per_thread": ways,
                     "frac_of_core_rate": round(per_thread / (core_rate / 1e9), 3) if core_rate else None,
                     "largest_file_gib": round(float(lens[host_ids].max()) / GiB, 3),
                     "feed": "D2H in 8 MiB chunks per thread, double-buffered (PCIe), from the HBM-resident set",
                     "why": "one file is one serial chain: a SHA-NI core runs it ~40x faster than a GPU wave"}
-    res = dict(value=bytes_all / t / 1e9, ms_per_step=t / args.steps * 1e3, roofline=roof, host_leg=host_leg,
+    # the step's roofline is the leg that sets it: on configs[1] the host leg
+    # (the chain-bound largest files on SHA-NI threads), priced against its
+    # own peak -- threads x one thread's measured rate at the configured
+    # chain interleave on this box; the GPU kernels' rooflines sit beside it
+    if h and thread_rate and host_ms >= max([ms for _, _, ms in legs] or [0.0]):
+        ach = hb / (host_ms * 1e-3) / 1e9
+        peak = st.host_threads * thread_rate / 1e9
+        roof = {"bound": "host SHA-NI issue", "leg": "host_leg", "achieved": round(ach, 3), "peak": round(peak, 3),
+                "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None,
+                "traffic_note": "a CPU leg: its input is the files' bytes streamed D2H once (PCIe), no HBM "
+                                "re-reads to count; device PMC counters do not describe it",
+                "peak_kind": "host-leg threads x one thread's measured SHA-NI rate with %d interleaved chains "
+                             "(rf_host_rate, this box)" % ways,
+                "leg_ms": round(host_ms, 2), "step_ms": round(step_ms, 2), "bytes": hb,
+                "threads": int(st.host_threads)}
+    else:
+        dom = max(zip(gpu_roofs, legs), key=lambda x: x[1][2])[0] if legs else None
+        roof = dom
+    gpu_bytes = float(lens[np.concatenate([solo_ids, lane_ids])].sum()) if len(lane_ids) + k else 0.0
+    composition = {"host_leg_bytes": hb, "gpu_bytes": gpu_bytes,
+                   "host_leg_bytes_frac": round(hb / max(hb + gpu_bytes, 1.0), 4),
+                   "gpu_legs_gbps": round(gpu_bytes / (max([ms for _, _, ms in legs] or [1e-9]) * 1e-3) / 1e9, 3)
+                   if legs else None,
+                   "note": "value is the whole hybrid step (CPU SHA-NI host leg + GPU kernels, split by the K1 "
+                           "planner's makespan model); the GPU-only rate of the same set is gpu_only.gbps"}
+    res = dict(value=bytes_all / t / 1e9, ms_per_step=step_ms, roofline=roof, roofline_gpu_legs=gpu_roofs,
+               host_leg=host_leg, composition=composition,
                files=int(len(lens)), bytes_per_gpu=int(lens.sum()), workload=workload, glob=glob_info,
                split={"host": h, "duo": k, "lanes": int(len(lane_ids))},
                step_ms={kk: round(float(np.mean(v)), 3) for kk, v in rec.items()})
@@ -450,69 +472,136 @@ def bench_c1_install(ctx, arena, offs, want_fsd, cpu_leg=False):
 
 
 # ------------------------------------------------------- C3: incremental --
-def bench_dag(args, dist, ctx, comm, budget):
-    """configs[2] at N = 1 (one 10M-node DAG); configs[3] at N > 1: ONE global
-    DAG of N x 12.5M nodes (100M at N = 8), partitioned by sample subtree
-    (workloads.PartitionedDag1000) and recomputed with
-    rf_graph_recompute_part: the layout's one fixed exchange round (every
-    rank root all-gathered over RCCL, rank 0 recomputes the global root) --
-    a step queues kernels and RCCL calls with no host round trip)."""
+def bench_dag(args, dist, ctx, budget):
+    """configs[2] (N = 1): one 10M-node 1000align DAG, 1% of leaf File IDs
+    toggled per step (K3 frontier + K2 levels), plus Canonicalize's flowMap
+    over its node digests and the CPU legs' inputs."""
     t0 = time.perf_counter()
-    part = None
-    if dist.world > 1:
-        S = args.c4_samples
-        part = PartitionedDag1000(S, args.dag_pairs, dist.world, dist.rank)
-        dag, a = part.dag, part.desc
-    else:
-        S = args.dag_samples
-        dag = Dag1000(S, args.dag_pairs)
-        a = dag.arrays()
-    n_nodes = part.n_nodes if part is not None else dag.n_nodes
+    S = args.dag_samples
+    dag = Dag1000(S, args.dag_pairs)
+    a = dag.arrays()
+    t_build = time.perf_counter() - t0
     g = capi.Graph.from_arrays(ctx, a)
     g.set_slots(dag.file_slots, dag.leaf_ids)
-    log("C3: %d nodes, %d jobs built+loaded in %.1f s" % (n_nodes, len(a["out_slot"]), time.perf_counter() - t0))
-    if part is not None:
-        g.set_part(part.part)
-        ag = None
-        if comm is None:  # RF_BENCH_SHARE_GPU rehearsal (or no RCCL communicator): gloo host transport
-            ag = lambda b: [x.tobytes() for x in np.split(dist.all_gather_bytes(np.frombuffer(b, np.uint8)), dist.world)]  # noqa: E731,E501
-
-        def recompute(full, count=True):
-            # the timed steps read nothing back: with RCCL and the layout's fixed
-            # exchange round (rounds = 1) a step never waits on the host
-            return g.recompute_part(comm=comm, allgather=ag, nranks=dist.world, full=full, count=count)
-    else:
-        recompute = lambda full: g.recompute(full=full)  # noqa: E731
-    recompute(True)  # first call also captures the hipGraphs (host work): untimed
-    dist.barrier()
+    t_load = time.perf_counter() - t0 - t_build
+    log("C3: %d nodes, %d jobs built in %.1f s, loaded in %.1f s" % (dag.n_nodes, len(a["out_slot"]), t_build, t_load))
+    g.recompute(True)  # first call also captures the hipGraph (host work): untimed
     ctx.timer_start()
-    recompute(True)
+    g.recompute(True)
     full_ms = ctx.timer_stop()
     slots, old, new = dag.change_set(0.01)
     d_slots = ctx.upload(slots)
     d_old, d_new = ctx.upload(old), ctx.upload(new)
     # one counted step to learn the dirty-set size
     g.set_slots(slots, new)
-    n_dirty_jobs = recompute(False)
+    n_dirty_jobs = g.recompute(False)
     g.set_slots(slots, old)
-    recompute(False)
+    g.recompute(False)
     pairs = np.unique(slots // 2)
     n_dirty_nodes = n_dirty_jobs - len(pairs)  # minus the pE1 physical keys
     state = {"v": 0}
 
-    # RF_BENCH_DAG_ONE_LAUNCH=1: mark node + levels as one graph launch
-    # (update_recompute_async); measured ~2 us/step slower than the separate
-    # mark launch on configs[2] (profiles/r02/k2_ab.txt), so off by default
-    one_launch = part is None and os.environ.get("RF_BENCH_DAG_ONE_LAUNCH", "0") == "1"
+    def step():
+        ver = d_new if state["v"] == 0 else d_old
+        state["v"] ^= 1
+        g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
+        g.recompute_async(False, ctx.stream)
+
+    steps = args.dag_steps
+    t = timed_steps(dist, ctx, step, steps, 2)
+    ctx.timer_start()
+    for _ in range(steps):
+        step()
+    dev_ms = ctx.timer_stop() / steps
+    res = {"workload": "configs[2]: 1000align DAG S=%d P=%d, 1%% leaf File IDs toggled per step" % (S, args.dag_pairs),
+           "nodes": dag.n_nodes, "jobs": len(a["out_slot"]),
+           "dirty_nodes_per_step": int(n_dirty_nodes), "dirty_jobs_per_step": int(n_dirty_jobs),
+           "ms_per_step": t / steps * 1e3, "device_ms_per_step": dev_ms,
+           "mnodes_per_s": n_dirty_nodes * steps / t / 1e6,
+           "effective_mnodes_per_s": dag.n_nodes * steps / t / 1e6,
+           "full_recompute_ms": full_ms,
+           "full_recompute_mnodes_per_s": dag.n_nodes / (full_ms * 1e-3) / 1e6,
+           "levels": g.stats().n_levels, "build_s": round(t_build, 2), "load_s": round(t_load, 2)}
+    st = g.stats()
+    ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
+    res["roofline_full"] = {"bound": "valu", "achieved": round(ach, 2), "peak": round(SHA_VALU_PEAK_GBS, 1),
+                            "unit": "GB/s", "frac": round(ach / SHA_VALU_PEAK_GBS, 4)}
+    res["canonicalize"] = bench_canon(ctx, g, dag)
+    # the configs[2] CPU legs need the host arrays (rank 0, N = 1)
+    res["_cpu"] = {"a": a, "dag": dag, "slots": slots, "old": old, "new": new,
+                   "gpu_dirty_jobs": int(n_dirty_jobs)}
+    for b in (d_slots, d_old, d_new):
+        b.free()
+    g.close()
+    return res
+
+
+def bench_dag100m(args, dist, ctx, comm, budget):
+    """configs[3]'s DAG, strong scaling: ONE global 1000align DAG of
+    c4_parts x c4_samples samples (8 x 27,594 x P=32: 100M nodes, 121.6M
+    jobs) cut into parts by sample subtree (workloads.PartitionedDag1000,
+    SURVEY §8(e)); N ranks hold 8/N parts each -- N = 1 all of it, no
+    exchange.  1% of the GLOBAL leaf File IDs toggle per step (every rank
+    its own share of the same change set); with N > 1 a step is the local
+    recompute, one fixed exchange round of the part roots (RCCL all-gather
+    over xGMI) and rank 0's global root -- queued on the stream, no host
+    round trip.  Dirty-node and block counts come from the layout
+    (PartitionedDag1000.dirty_work, pinned against the oracle in
+    tests/test_partition.py) and are checked against the device's count."""
+    nparts, S, P = args.c4_parts, args.c4_samples, args.dag_pairs
+    if nparts % dist.world:
+        raise SystemExit("--c4-parts %d is not a multiple of the %d ranks" % (nparts, dist.world))
+    t0 = time.perf_counter()
+    pc = PartitionedDag1000(S, P, dist.world, dist.rank, nparts=nparts)
+    a = pc.desc
+    t_build = time.perf_counter() - t0
+    g = capi.Graph.from_arrays(ctx, a)
+    g.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
+    t_load = time.perf_counter() - t0 - t_build
+    nodes_global = dist.sum(pc.n_nodes - (3 * (dist.world - 1) if dist.rank else 0))  # the ref chain once
+    log("C4 DAG: rank %d of %d holds %d of %d parts: %d nodes, %d jobs (%.1f GB of templates) built in %.1f s, "
+        "loaded in %.1f s" % (dist.rank, dist.world, pc.k, nparts, pc.n_nodes, len(a["out_slot"]),
+                              g.stats().template_bytes / 1e9, t_build, t_load))
+    multi = dist.world > 1
+    if multi:
+        g.set_part(pc.part)
+        ag = None
+        if comm is None:  # RF_BENCH_SHARE_GPU rehearsal (or no RCCL communicator): gloo host transport
+            ag = lambda b: [x.tobytes() for x in np.split(dist.all_gather_bytes(np.frombuffer(b, np.uint8)), dist.world)]  # noqa: E731,E501
+
+        def recompute(full, count=True):
+            return g.recompute_part(comm=comm, allgather=ag, nranks=dist.world, full=full, count=count)
+    else:
+        def recompute(full, count=True):
+            return g.recompute(full=full)
+    recompute(True)  # first call also captures the hipGraphs (host work): untimed
+    dist.barrier()
+    ctx.sync()
+    t1 = time.perf_counter()
+    recompute(True)
+    ctx.sync()
+    dist.barrier()
+    full_ms = dist.max(time.perf_counter() - t1) * 1e3
+    n_files_global = 2 * P * S * nparts
+    slots, old, new = pc.dag.change_set(0.01, n_global=n_files_global)
+    d_slots = ctx.upload(slots if len(slots) else np.zeros(1, np.uint32))
+    d_old = ctx.upload(old if len(slots) else np.zeros((1, 32), np.uint8))
+    d_new = ctx.upload(new if len(slots) else np.zeros((1, 32), np.uint8))
+    jobs_l, nodes_l, blocks_l = pc.dirty_work(slots)
+    # one counted step: the device's dirty-job count against the layout's
+    g.set_slots(slots, new)
+    got_jobs = recompute(False)
+    g.set_slots(slots, old)
+    recompute(False)
+    jobs_ok = dist.max(0.0 if got_jobs == jobs_l else 1.0) == 0.0
+    state = {"v": 0}
 
     def step():
         ver = d_new if state["v"] == 0 else d_old
         state["v"] ^= 1
-        if one_launch:
-            g.update_recompute_async(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
-            return
-        g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
-        if part is not None:
+        if len(slots):
+            g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
+        if multi:
             recompute(False, count=False)
         else:
             g.recompute_async(False, ctx.stream)
@@ -523,32 +612,35 @@ def bench_dag(args, dist, ctx, comm, budget):
     for _ in range(steps):
         step()
     dev_ms = ctx.timer_stop() / steps
-    total_dirty_nodes = dist.sum(n_dirty_nodes) * steps
-    if part is not None:
-        wl = ("configs[3]: one 1000align DAG of %d samples x P=%d (%d nodes), partitioned by sample subtree "
-              "over %d ranks (%d samples each; shared reference chain replicated; per-rank Merge tree; global root "
-              "on rank 0), 1%% leaf File IDs toggled per step on every rank; local passes per step %d"
-              % (S * dist.world, args.dag_pairs, dist.sum(n_nodes), dist.world, S,
-                 g.part_gathered()[2]))
-    else:
-        wl = "configs[2]: 1000align DAG S=%d P=%d, 1%% leaf File IDs toggled per step" % (S, args.dag_pairs)
-    res = {"workload": wl,
-           "nodes_per_gpu": n_nodes, "jobs_per_gpu": len(a["out_slot"]),
-           "dirty_nodes_per_step": int(n_dirty_nodes), "dirty_jobs_per_step": int(n_dirty_jobs),
-           "ms_per_step": t / steps * 1e3, "device_ms_per_step": dev_ms,
-           "mnodes_per_s": total_dirty_nodes / t / 1e6,
-           "effective_mnodes_per_s": dist.sum(n_nodes) * steps / t / 1e6,
+    nodes_all, blocks_all = dist.sum(nodes_l), dist.sum(blocks_l)
+    per_rank = [dict(rank=i, **{k: int(v) for k, v in zip(("jobs", "dirty_nodes", "dirty_blocks"), row)})
+                for i, row in enumerate(np.frombuffer(dist.all_gather_bytes(
+                    np.array([len(a["out_slot"]), nodes_l, blocks_l], np.int64)), np.int64).reshape(-1, 3))] \
+        if multi else None
+    ops = blocks_all * SHA_OPS_PER_BLOCK
+    res = {"workload": "configs[3] DAG, strong scaling: one 1000align DAG of %d parts x %d samples x P=%d (%d nodes), "
+                       "%d parts per rank over %d ranks; per part a fan-in-32 Merge tree, the global root on rank 0; "
+                       "1%% of the global leaf File IDs toggled per step" % (nparts, S, P, nodes_global, pc.k,
+                                                                              dist.world),
+           "nodes_global": int(nodes_global), "nodes_rank0": int(pc.n_nodes), "jobs_rank0": len(a["out_slot"]),
+           "dirty_nodes_per_step": int(nodes_all), "dirty_blocks_per_step": int(blocks_all),
+           "dirty_jobs_match_device": bool(jobs_ok),
+           "ms_per_step": t / steps * 1e3, "device_ms_per_step_rank0": dev_ms,
+           "mnodes_per_s": nodes_all * steps / t / 1e6,
+           "effective_mnodes_per_s": nodes_global * steps / t / 1e6,
            "full_recompute_ms": full_ms,
-           "full_recompute_mnodes_per_s": n_nodes / (full_ms * 1e-3) / 1e6,
-           "levels": g.stats().n_levels}
-    st = g.stats()
-    ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
-    res["roofline_full"] = {"bound": "valu", "achieved": round(ach, 2), "peak": round(SHA_VALU_PEAK_GBS, 1),
-                            "unit": "GB/s", "frac": round(ach / SHA_VALU_PEAK_GBS, 4)}
-    res["canonicalize"] = bench_canon(ctx, g, dag)
-    # the configs[2] CPU legs need the host arrays (rank 0, N = 1)
-    res["_cpu"] = {"a": a, "dag": dag, "slots": slots, "old": old, "new": new,
-                   "gpu_dirty_jobs": int(n_dirty_jobs)} if dist.world == 1 else None
+           "build_s_rank0": round(t_build, 2), "load_s_rank0": round(t_load, 2),
+           "exchange": ("none (1 rank)" if not multi else "RCCL all-gather of %d part roots" % nparts if comm
+                        else "gloo host all-gather of %d part roots" % nparts),
+           "per_rank": per_rank,
+           "roofline_incremental": {
+               "bound": "valu", "achieved_tops": round(ops / (t / steps) / 1e12, 3),
+               "peak_tops": round(dist.world * VALU_LANE_OPS / 1e12, 1),
+               "frac": round(ops / (t / steps) / (dist.world * VALU_LANE_OPS), 4),
+               "note": "dirty material blocks x 1464 ops per step / wall time per step, against the INT32 "
+                       "VALU peak of the ranks' GPUs"}}
+    for b in (d_slots, d_old, d_new):
+        b.free()
     g.close()
     return res
 
@@ -962,7 +1054,9 @@ def main():
     ap.add_argument("--dag-samples", type=int, default=22075)  # ~10M nodes at P=32
     ap.add_argument("--dag-pairs", type=int, default=32)
     ap.add_argument("--c4-samples", type=int, default=27594,
-                    help="samples per rank at N > 1 (12.5M nodes: the global DAG is 100M nodes at N = 8)")
+                    help="samples per part of configs[3]'s DAG (12.5M nodes per part)")
+    ap.add_argument("--c4-parts", type=int, default=8,
+                    help="parts of configs[3]'s DAG (8 x 12.5M = 100M nodes, fixed for every N: strong scaling)")
     ap.add_argument("--dag-steps", type=int, default=20)
     ap.add_argument("--probe-keys", type=int, default=100_000_000)
     ap.add_argument("--probe-big-keys", type=int, default=1_200_000_000)
@@ -971,7 +1065,7 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
     ap.add_argument("--gpu-only-run", type=int, default=1, help="one GPU-only run (duo roofline)")
     ap.add_argument("--budget-s", type=float, default=420.0)
-    ap.add_argument("--skip", default="", help="comma list of: c1,install,dag,probe,cpu")
+    ap.add_argument("--skip", default="", help="comma list of: c1,install,dag,dag100m,probe,cpu")
     args = ap.parse_args()
     args.skip = set(filter(None, args.skip.split(",")))
     budget = Budget(args.budget_s)
@@ -982,7 +1076,7 @@ def main():
     if share:  # rehearsal of the N-rank path on a box with fewer GPUs (never the driver's run)
         device = dist.local % max(capi.device_count(), 1)
     ctx = capi.Context(device)
-    comm, exchange = None, "none (1 rank)"
+    comm, exchange, rccl = None, "none (1 rank)", None
     if dist.world > 1:
         # RF_BENCH_TRY_RCCL=1 with RF_BENCH_SHARE_GPU: attempt the communicator anyway (RCCL refuses two
         # ranks on one GPU), which rehearses the fallback below
@@ -1002,14 +1096,31 @@ def main():
                     comm = None
                 exchange = "gloo host all-gather (RCCL communicator failed: %s)" % (err or "on another rank")
                 log("warning: " + exchange)
+                rccl = False
+                # a real multi-GPU run must not report a host exchange as the
+                # xGMI result: RF_BENCH_REQUIRE_RCCL=1 makes this fatal, and
+                # the line always carries "rccl": false for the driver
+                if os.environ.get("RF_BENCH_REQUIRE_RCCL") == "1":
+                    raise SystemExit("RCCL communicator could not be created (RF_BENCH_REQUIRE_RCCL=1): %s" % err)
             else:
                 exchange = "RCCL all-gather over xGMI"
+                rccl = True
 
     sha = bench_sha(args, dist, ctx, budget)
+    sha_ranks = None
+    if dist.world > 1:  # per rank: host-leg threads and bytes, GPU-leg bytes, step ms (is the curve host-bound?)
+        hl, comp = sha["host_leg"] or {}, sha["composition"]
+        row = np.array([hl.get("threads", 0), comp["host_leg_bytes"], comp["gpu_bytes"], sha["ms_per_step"]],
+                       np.float64)
+        sha_ranks = [dict(rank=i, host_threads=int(r[0]), host_leg_bytes=float(r[1]), gpu_bytes=float(r[2]),
+                          ms_per_step=round(float(r[3]), 2))
+                     for i, r in enumerate(np.frombuffer(dist.all_gather_bytes(row), np.float64).reshape(-1, 4))]
     c1 = bench_c1(args, dist, ctx, budget) if "c1" not in args.skip and budget.allow("c1", 15) else None
-    dag_res = None
-    if "dag" not in args.skip and budget.allow("dag", 40):
-        dag_res = bench_dag(args, dist, ctx, comm, budget)
+    dag_res = dag100 = None
+    if dist.world == 1 and "dag" not in args.skip and budget.allow("dag", 30):
+        dag_res = bench_dag(args, dist, ctx, budget)
+    if "dag100m" not in args.skip and budget.allow("dag100m", 150):
+        dag100 = bench_dag100m(args, dist, ctx, comm, budget)
     probe = bench_probe(args, dist, ctx, budget) if "probe" not in args.skip and budget.allow("probe", 30) else None
     cpu = None
     if dist.rank == 0 and dist.world == 1 and "cpu" not in args.skip and budget.allow("cpu", 60):
@@ -1046,13 +1157,18 @@ def main():
                                       "GPU kernels split by the K1 planner; DAG partitioned by sample subtree, "
                                       "RCCL only for its boundary exchange",
                        "exchange": exchange, "split_rank0": sha["split"], "step_ms_rank0": sha["step_ms"]},
+            "rccl": rccl,
             "roofline": sha["roofline"],
+            "roofline_gpu_legs": sha["roofline_gpu_legs"],
+            "composition": sha["composition"],
             "host_leg": sha["host_leg"],
+            "sha_per_rank": sha_ranks,
             "roofline_gpu_only": sha.get("roofline_gpu_only"),
             "gpu_only": sha.get("gpu_only"),
             "cpu_baseline": cpu,
             "c1": c1,
             "incremental": dag_res,
+            "incremental_100m": dag100,
             "probe": probe,
             "budget": {"seconds": args.budget_s, "skipped": budget.skipped,
                        "elapsed_s": round(time.perf_counter() - T_START, 1)},

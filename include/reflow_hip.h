@@ -79,6 +79,11 @@ int rf_set_host_threads(rf_ctx *ctx, int n);
 /* Host leg threads in effect, one core's measured SHA-NI rate (bytes/s; 0 if
  * unavailable) and whether the CPU has the SHA extensions. */
 int rf_host_info(rf_ctx *ctx, int *threads, double *core_bytes_per_s, int *sha_ext);
+/* The host leg's chains per thread (RF_HOST_WAYS, default 2: SHA-NI rounds
+ * are latency-bound, two interleaved messages fill the issue slots) and one
+ * thread's measured rate at that interleave (bytes/s) -- the per-thread peak
+ * bench.py prices the host leg against. */
+int rf_host_rate(rf_ctx *ctx, int *ways, double *thread_bytes_per_s);
 
 /* ---- device memory and timing -------------------------------------------
  * The engine owns its HIP runtime; callers (the cgo shim, bench.py, tests)

@@ -121,6 +121,14 @@ extern "C" int rf_set_host_threads(rf_ctx* ctx, int n) {
     return RF_OK;
 }
 
+extern "C" int rf_host_rate(rf_ctx* ctx, int* ways, double* thread_bytes_per_s) {
+    ARG(ctx, "null ctx");
+    const int w = host_ways();
+    if (ways) *ways = w;
+    if (thread_bytes_per_s) *thread_bytes_per_s = host_sha_rate(w);
+    return RF_OK;
+}
+
 extern "C" int rf_host_info(rf_ctx* ctx, int* threads, double* core_bytes_per_s, int* sha_ext) {
     ARG(ctx, "null ctx");
     if (threads) *threads = (int)ctx_host_threads(ctx);
@@ -1326,7 +1334,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // assembly + expansion outlasts the chain's rounds (k2_level_pc<3>)
     gr->g.inc_level.assign(L, 0);
     {
-        static const uint64_t wide = [] {
+        const uint64_t wide = [] {  // read per load: tests force a mode
             const char* v = getenv("RF_K2_WIDE");
             return v ? (uint64_t)strtoull(v, nullptr, 10) : 8ull;
         }();
@@ -1388,6 +1396,10 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     G.counts_last = gr->b_counts_last.as<uint32_t>();
     gr->last_counts = G.counts_last;
     G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
+    {
+        const char* v = getenv("RF_K2_STREAM");  // (opt-in variant, read per load)
+        G.stream_handover = v && atoi(v) == 1;
+    }
     if (n_lead && !getenv("RF_K2_NO_MIDSTATE")) {  // (RF_K2_NO_MIDSTATE: A/B)
         struct Tmp {
             DevBuf b;
@@ -2113,6 +2125,12 @@ static int assoc_put_locked(rf_assoc* a, int kind, const uint8_t* d_exp, const u
     HIPC(ctx->d_tab.ensure(4ull * dedup_table_slots((uint32_t)n)));
     HIPC(ctx->d_tab2.ensure(4ull * n));
     HIPC(launch_dedup(d_keys, (uint32_t)n, ctx->d_tab.as<uint32_t>(), ctx->d_tab2.as<uint32_t>(), canon, d_nu, s));
+    // a batch that hit the dedup probe bound has canon[i] = ~0 for some ops:
+    // the insert / claim / apply kernels index by canon, so stop here
+    uint32_t nu = 0;
+    HIPC(hipMemcpyAsync(&nu, d_nu, 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (nu & 0x80000000u) return fail(RF_EDEVICE, "assoc put: dedup probe bound exceeded (batch not applied)");
     HIPC(launch_assoc_insert(a->view(), (uint32_t)kind, d_keys, canon, (uint32_t)n, a->b_aslot.as<uint32_t>(), s));
     // ops in batch order per key: round r applies each key's r-th op
     HIPC(launch_iota(a->b_rem.as<uint32_t>(), (uint32_t)n, s));

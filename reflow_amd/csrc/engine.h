@@ -97,6 +97,9 @@ struct GraphDev {
     // every fusion target's hole is at material byte 2 (right after its WD
     // prefix: no Universe), so the chain assembles its block 0 in registers
     bool fuse_pos2 = true;
+    // RF_K2_STREAM=1 at load: the streamed hand-over variant of k2_level_pl
+    // (opt-in, measured slower; kept correct by a forced-mode GPU test)
+    bool stream_handover = false;
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the
     // constant blocks its template starts with -- the record's template

@@ -691,11 +691,13 @@ __device__ __forceinline__ void lds_publish(volatile uint32_t* flag, uint32_t v,
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) lds_st(flag, v);
 }
-// As lds_publish for the chunk before the last one: its four row writes are
-// complete once at most the four younger ones (the chunk just written) are
-// outstanding -- the drain of a chunk's writes overlaps the next expansion.
+// As lds_publish for the chunk before the last one.  A partial count
+// (lgkmcnt(4): "the four younger row writes may still be out") would let the
+// drain overlap the next expansion, but it silently relies on the compiler
+// emitting exactly four LDS writes per chunk and no SMEM load in between
+// (SMEM also counts in lgkmcnt and returns out of order), so the wait is full.
 __device__ __forceinline__ void lds_publish_prev(volatile uint32_t* flag, uint32_t v, uint32_t lane) {
-    __asm__ volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) lds_st(flag, v);
 }
 
@@ -1729,13 +1731,10 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             return v && atoi(v) == 14;
         }();
         const bool wide = g.inc_level[lvl] == 2;
-        // RF_K2_STREAM=1: the streamed hand-over (measured no faster on
-        // configs[2]: the producer serializes a fused job's blocks 0 and 1,
-        // DESIGN.md §5); default per-block barriers
-        static const bool no_stream = [] {
-            const char* v = getenv("RF_K2_STREAM");
-            return !(v && atoi(v) == 1);
-        }();
+        // g.stream_handover (RF_K2_STREAM=1 at load): the streamed hand-over
+        // (measured no faster on configs[2]: the producer serializes a fused
+        // job's blocks 0 and 1); default per-block barriers
+        const bool no_stream = !g.stream_handover;
         // RF_K2_PAD_KB: dynamic LDS per workgroup on top of the static arrays
         // (A/B: enough to keep a second workgroup off the CU, so no wave
         // shares a SIMD with another workgroup's prioritised chain wave)

@@ -10,8 +10,8 @@
 // subtrees never hold that minimum).
 //
 // Layout: open addressing, linear probing, a power-of-two table of u32 node
-// indices (empty = ~0), at most half full.  The probe start is the digest's
-// first 8 bytes (SHA-256 output: uniform), and a slot whose index points at an
+// indices (empty = ~0), at most half full.  The probe start is key_hash of
+// all eight digest words, and a slot whose index points at an
 // equal 32-B digest is a hit -- slots store indices, the digests stay in their
 // input array, so an insert is: one slot read, one CAS (or an atomicMin on a
 // hit), one 32-B compare read.  All of it is random access: the bound is the
@@ -22,6 +22,23 @@ namespace rf {
 
 constexpr uint32_t kEmpty = 0xffffffffu;
 constexpr uint32_t kMaxProbe = 1u << 16;
+
+// 32-bit slot hash over all eight words of a 32-B key.  Each word enters
+// through an xor with a rotated partner and an odd multiply (bijections), so
+// two keys that differ in any single word never share a pre-finaliser value,
+// and the finaliser (also a bijection) spreads them over the low bits.  Keys
+// are usually SHA-256 output (any word would do), but callers may hand in
+// digests that share all but a few bytes.
+__device__ __forceinline__ uint32_t key_hash(const uint4& lo, const uint4& hi) {
+    uint32_t h = ((lo.x ^ __builtin_rotateleft32(lo.y, 5)) * 0x9E3779B1u) ^
+                 ((lo.z ^ __builtin_rotateleft32(lo.w, 11)) * 0x85EBCA77u) ^
+                 ((hi.x ^ __builtin_rotateleft32(hi.y, 17)) * 0xC2B2AE3Du) ^
+                 ((hi.z ^ __builtin_rotateleft32(hi.w, 23)) * 0x27D4EB2Fu);
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    return h;
+}
 
 __device__ __forceinline__ bool dig_eq(const uint4& alo, const uint4& ahi, const uint8_t* b) {
     const uint4* q = reinterpret_cast<const uint4*>(b);
@@ -40,10 +57,7 @@ __global__ __launch_bounds__(256) void k5_dedup_insert(const uint8_t* __restrict
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint4* d = reinterpret_cast<const uint4*>(dig + 32ull * i);
         const uint4 lo = d[0], hi = d[1];
-        // slot from four words of the digest: inputs that share a prefix
-        // (not SHA-256 output, or adversarial) still spread over the table
-        uint32_t slot = ((lo.x ^ __builtin_rotateleft32(lo.z, 13) ^ hi.y ^ __builtin_rotateleft32(hi.w, 7)) *
-                         0x9E3779B1u) & mask;
+        uint32_t slot = key_hash(lo, hi) & mask;
         // bounded probing: the table is >= 2n slots (load <= 1/2), where
         // linear probing's runs are a few slots long; the bound guarantees
         // that every wave exits, and a batch that hits it is flagged
@@ -124,7 +138,7 @@ hipError_t launch_dedup(const uint8_t* dig, uint32_t n, uint32_t* table, uint32_
 // HBM-resident assoc (assoc.Assoc, assoc/assoc.go:26-38) with the in-memory
 // implementation's semantics (test/testutil/assoc.go:34-56): (kind, key) ->
 // value; Put with a nonzero `expect` is a compare-and-set, a zero value
-// deletes.  Table: open addressing on the key's first 4 bytes, a tag word per
+// deletes.  Table: open addressing on key_hash(key), a tag word per
 // slot (0 empty, 1 being written, 2 + kind ready), keys and values 32 B each.
 // Deleted entries keep their slot with a zero value (Get: NotExist).
 constexpr uint32_t kTagEmpty = 0, kTagBusy = 1, kTagReady = 2;
@@ -161,7 +175,7 @@ __global__ __launch_bounds__(256) void k5_assoc_insert(AssocView t, uint32_t kin
         if (canon[i] != i) continue;
         const uint4* k = reinterpret_cast<const uint4*>(keys + 32ull * i);
         const uint4 lo = k[0], hi = k[1];
-        uint32_t slot = lo.x & t.mask, mark = 0;
+        uint32_t slot = key_hash(lo, hi) & t.mask, mark = 0;
         for (;;) {
             uint32_t tg = __hip_atomic_load(&t.tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (tg == kTagEmpty) {
@@ -200,7 +214,7 @@ __global__ __launch_bounds__(256) void k5_assoc_publish(AssocView t, uint32_t ki
 
 __device__ __forceinline__ uint32_t assoc_find(const AssocView& t, uint32_t kind, const uint4& lo, const uint4& hi) {
     const uint32_t ready = kTagReady + kind;
-    uint32_t slot = lo.x & t.mask;
+    uint32_t slot = key_hash(lo, hi) & t.mask;
     for (;;) {
         const uint32_t tg = t.tag[slot];
         if (tg == kTagEmpty) return kEmpty;
@@ -218,7 +232,8 @@ __global__ __launch_bounds__(256) void k5_assoc_claim(const uint32_t* __restrict
     const uint32_t n = *n_rem;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
         const uint32_t i = rem[q];
-        atomicMax(&cls[canon[i]], ((unsigned long long)round << 32) | (unsigned long long)(~i));
+        if (canon[i] == kEmpty) continue;  // never reached: the host stops a flagged batch
+        atomicMax(&cls[canon[i]],((unsigned long long)round << 32) | (unsigned long long)(~i));
     }
 }
 
@@ -234,7 +249,8 @@ __global__ __launch_bounds__(256) void k5_assoc_apply(AssocView t, const uint32_
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
         const uint32_t i = rem[q];
         const uint32_t c = canon[i];
-        if (cls[c] != (((unsigned long long)round << 32) | (unsigned long long)(~i))) {
+        if (c == kEmpty) continue;
+        if (cls[c] !=(((unsigned long long)round << 32) | (unsigned long long)(~i))) {
             next[atomicAdd(n_next, 1u)] = i;  // a later op of the same key: next round
             continue;
         }
@@ -336,7 +352,7 @@ __global__ __launch_bounds__(256) void k5_assoc_rehash(AssocView from, uint32_t 
         const uint4 lo = from.keys[2 * s], hi = from.keys[2 * s + 1];
         // keys are distinct and nothing compares them in this launch: claim
         // the slot with its final tag, no fences (the kernel boundary publishes)
-        uint32_t slot = lo.x & to.mask;
+        uint32_t slot = key_hash(lo, hi) & to.mask;
         while (atomicCAS(&to.tag[slot], kTagEmpty, tg) != kTagEmpty) slot = (slot + 1) & to.mask;
         to.keys[2 * slot] = lo;
         to.keys[2 * slot + 1] = hi;

@@ -55,6 +55,10 @@ struct rf_sha_streams {
     std::vector<uint8_t> carry;   // [n][64] partial block
     std::vector<uint32_t> clen;   // [n]
     std::vector<uint64_t> total;  // [n] bytes written since the last digest
+    // a feed that failed part-way (a HIP error after the host leg absorbed
+    // its segments) leaves midstates, carries and lengths out of step: every
+    // later call on the set fails
+    bool failed = false;
     DevBuf d_arena, d_mid, d_offs, d_nb;
     HostBuf h_stage, h_mid;
 };
@@ -233,29 +237,41 @@ extern "C" int rf_sha_streams_write(rf_sha_streams* S, const uint64_t* ids, cons
                                         (unsigned long long)S->n);
         ARG(chunks[i] || lens[i] == 0, "null chunk with nonzero length");
     }
+    // every read and update of the per-stream state happens under the
+    // context lock (a concurrent rf_sha_streams_digest resets clen / total)
+    std::lock_guard<std::mutex> lk(S->ctx->mu);
+    if (S->failed) return fail(RF_EDEVICE, "stream set failed in an earlier call");
     // group the chunks by stream, batch order within a stream (Write order)
     std::vector<uint64_t> idx(n);
     std::iota(idx.begin(), idx.end(), 0ull);
     std::stable_sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return ids[a] < ids[b]; });
     std::vector<Piece> pieces;
     std::vector<Seg> segs;
+    std::vector<uint64_t> added;  // per segment: the bytes this batch writes
     pieces.reserve(n);
     for (uint64_t q = 0; q < n;) {
         const uint64_t s = ids[idx[q]];
         Seg g{s, S->clen[s], 0, (uint32_t)pieces.size(), 0, false};
+        uint64_t add = 0;
         for (; q < n && ids[idx[q]] == s; ++q) {
             if (!lens[idx[q]]) continue;
             pieces.push_back(Piece{chunks[idx[q]], lens[idx[q]]});
             g.bytes += lens[idx[q]];
-            S->total[s] += lens[idx[q]];
+            add += lens[idx[q]];
         }
         g.p1 = (uint32_t)pieces.size();
         g.nb = g.bytes / 64;
         segs.push_back(g);
+        added.push_back(add);
     }
-    std::lock_guard<std::mutex> lk(S->ctx->mu);
     DevGuard dg(S->ctx->device);
-    return streams_feed(S, segs, pieces);
+    if (int rc = streams_feed(S, segs, pieces)) {
+        S->failed = true;
+        return rc;
+    }
+    // lengths are committed only with the midstates they describe
+    for (size_t k = 0; k < segs.size(); ++k) S->total[segs[k].stream] += added[k];
+    return RF_OK;
 }
 
 // Pads each stream's carried block (FIPS 180-4: 0x80, zeros, the bit length
@@ -309,13 +325,19 @@ extern "C" int rf_sha_streams_digest(rf_sha_streams* S, const uint64_t* ids, uin
     if (!n) return RF_OK;
     if (int rc = check_distinct(S, ids, n)) return rc;
     std::lock_guard<std::mutex> lk(S->ctx->mu);
+    if (S->failed) return fail(RF_EDEVICE, "stream set failed in an earlier call");
     DevGuard dg(S->ctx->device);
-    return streams_final(S, ids, n, out32);
+    if (int rc = streams_final(S, ids, n, out32)) {
+        S->failed = true;
+        return rc;
+    }
+    return RF_OK;
 }
 
 extern "C" int rf_sha_streams_len(rf_sha_streams* S, uint64_t id, uint64_t* len) {
     ARG(S && len, "null argument");
     ARG(id < S->n, "stream id out of range");
+    std::lock_guard<std::mutex> lk(S->ctx->mu);
     *len = S->total[id];
     return RF_OK;
 }

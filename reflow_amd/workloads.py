@@ -94,6 +94,29 @@ def _digits(a: np.ndarray, width: int) -> np.ndarray:
     return out
 
 
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(z):
+    """splitmix64's finaliser over a uint64 array (wrapping arithmetic)."""
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _ids_vec(domain: bytes, seed: int, idx) -> np.ndarray:
+    """[n, 32] uint8: four splitmix64 outputs per global index, keyed by
+    SHA256(domain || seed)."""
+    key = np.uint64(int.from_bytes(_h(domain + b":%d" % seed)[:8], "little"))
+    idx = np.asarray(idx, dtype=np.int64).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        base = key + idx * np.uint64(4) * _GOLD
+        out = np.empty((len(idx), 4), dtype=np.uint64)
+        for k in range(4):
+            out[:, k] = _mix64(base + np.uint64(k + 1) * _GOLD)
+    return out.view(np.uint8).reshape(len(idx), 32)
+
+
 class _Kind:
     """One node kind: a template of fixed length, per-instance digit fields,
     per-instance literal byte fields and holes."""
@@ -139,15 +162,19 @@ class Dag1000:
         self.n_nodes = 3 + self.Q * 14 + S * 5
         self._build()
 
-    # deterministic "previous run" values
+    # deterministic "previous run" values: 32 bytes per (domain, seed, global
+    # index) from a keyed splitmix64 stream, vectorised (hashlib per node took
+    # ~35 s of Python at 100M nodes); any fixed values serve, what matters is
+    # that a rank's piece and the global DAG agree (global indices)
     def file_id(self, i):  # File ID of leaf file i (2 per pair)
-        return _h(b"file:%d:%d" % (self.seed, i + 2 * self.P * self.sample0))
+        return _ids_vec(b"file", self.seed, np.array([i + 2 * self.P * self.sample0]))[0].tobytes()
 
     def out_id(self, tag, i):  # output File ID of exec instance i (per pair; "es" per sample)
-        return _h(b"out:%s:%d:%d" % (tag, self.seed, i + (self.sample0 if tag == b"es" else self.P * self.sample0)))
+        return self._out_ids(tag, np.array([i]))[0].tobytes()
 
-    def _ids(self, fn, n):
-        return np.frombuffer(b"".join(fn(i) for i in range(n)), dtype=np.uint8).reshape(n, 32)
+    def _out_ids(self, tag, idx):
+        off = self.sample0 if tag == b"es" else self.P * self.sample0
+        return _ids_vec(b"out:" + tag, self.seed, np.asarray(idx, dtype=np.int64) + off)
 
     def _build(self):
         S, P, Q = self.S, self.P, self.Q
@@ -287,7 +314,7 @@ class Dag1000:
         for name, src, tag in [("pE2", "E2", b"e1"), ("pE3", "E3", b"e2")]:
             suffix = kinds[src].tmpl[34 + len(b"OpExec"):]
             kk = _Kind(name, b"." + b"\x00\x05" + b"\0" * 32 + suffix, Q)
-            kk.bytes_at(3, self._ids(lambda i, t=tag: self.out_id(t, i), Q))
+            kk.bytes_at(3, self._out_ids(tag, np.arange(Q)))
             for pos, width, vals in kinds[src].digit_fields:
                 kk.digits(pos - 34 - len(b"OpExec") + 35, width, vals)
             kk.out_slot = alloc(Q)
@@ -295,7 +322,7 @@ class Dag1000:
         # ES: dep CS1's value = list of P sorted bams (paths "." each)
         suffix = kinds["ES"].tmpl[34 + len(b"OpExec"):]
         kk = _Kind("pES", (b"." + b"\x00\x05" + b"\0" * 32) * P + suffix, S)
-        bam_ids = self._ids(lambda i: self.out_id(b"e3", i), Q).reshape(S, P, 32)
+        bam_ids = self._out_ids(b"e3", np.arange(Q)).reshape(S, P, 32)
         for j in range(P):
             kk.bytes_at(35 * j + 3, bam_ids[:, j, :])
         for pos, width, vals in kinds["ES"].digit_fields:
@@ -304,7 +331,7 @@ class Dag1000:
         kinds["pES"] = kk
         # XS extern: dep CS2 value = {".": merged} + URL
         kk = _Kind("pXS", b"." + b"\x00\x05" + b"\0" * 32 + url, S)
-        kk.bytes_at(3, self._ids(lambda i: self.out_id(b"es", i), S))
+        kk.bytes_at(3, self._out_ids(b"es", np.arange(S)))
         kk.digits(35 + url.index(b"S0000000") + 1, 7, sidx)
         kk.out_slot = alloc(S)
         kinds["pXS"] = kk
@@ -313,47 +340,62 @@ class Dag1000:
         self.n_slots = next_slot[0]
         self.n_jobs = sum(kk.count for kk in kinds.values())
         self.file_slots = np.arange(2 * Q, dtype=np.uint32)
-        self.leaf_ids = self._ids(self.file_id, 2 * Q)
+        self.leaf_ids = _ids_vec(b"file", self.seed, np.arange(2 * Q, dtype=np.int64) + 2 * P * self.sample0)
 
     # -------------------------------------------------------------- lowering
     def arrays(self):
         """rf_graph_desc arrays (out_slot, tmpl_off, tmpl_len, hole_ptr,
-        hole_pos, hole_slot, blob)."""
-        out_slot, off, ln, nh, hpos, hslot, blobs = [], [], [], [], [], [], []
-        base = 0
-        for kk in self.kinds.values():
+        hole_pos, hole_slot, blob).  The blob is allocated once and each
+        kind's rows are written into their view on a thread of their own
+        (numpy releases the GIL for the copies): ~15 GB at 100M nodes."""
+        from concurrent.futures import ThreadPoolExecutor
+        kinds = list(self.kinds.values())
+        L16 = [(len(kk.tmpl) + 15) // 16 * 16 for kk in kinds]
+        sizes = [kk.count * l16 for kk, l16 in zip(kinds, L16)]
+        bases = np.concatenate([[0], np.cumsum(sizes, dtype=np.int64)]).astype(np.int64)
+        blob = np.empty(int(bases[-1]), dtype=np.uint8)
+
+        def fill(x):
+            kk, l16, b = kinds[x], L16[x], int(bases[x])
             L = len(kk.tmpl)
-            L16 = (L + 15) // 16 * 16
-            arr = np.zeros((kk.count, L16), dtype=np.uint8)
+            arr = blob[b:b + kk.count * l16].reshape(kk.count, l16)
             arr[:, :L] = np.frombuffer(kk.tmpl, dtype=np.uint8)
+            arr[:, L:] = 0
             for pos, width, vals in kk.digit_fields:
                 arr[:, pos:pos + width] = _digits(vals, width)
             for pos, vals in kk.byte_fields:
                 arr[:, pos:pos + vals.shape[1]] = vals
-            blobs.append(arr.reshape(-1))
-            out_slot.append(kk.out_slot)
-            off.append(base + np.arange(kk.count, dtype=np.uint64) * np.uint64(L16))
-            ln.append(np.full(kk.count, L, dtype=np.uint32))
-            nh.append(np.full(kk.count, len(kk.holes), dtype=np.uint64))
-            if kk.holes:
-                hpos.append(np.tile(np.array([p for p, _ in kk.holes], dtype=np.uint32), kk.count))
-                hslot.append(np.stack([sl for _, sl in kk.holes], axis=1).reshape(-1))
-            base += kk.count * L16
-        hole_ptr = np.zeros(self.n_jobs + 1, dtype=np.uint64)
-        hole_ptr[1:] = np.cumsum(np.concatenate(nh))
-        return dict(n_slots=self.n_slots, out_slot=np.concatenate(out_slot),
-                    tmpl_off=np.concatenate(off), tmpl_len=np.concatenate(ln), hole_ptr=hole_ptr,
-                    hole_pos=np.concatenate(hpos), hole_slot=np.concatenate(hslot).astype(np.uint32),
-                    blob=np.concatenate(blobs))
 
-    def change_set(self, frac=0.01, seed=0x5EED0003):
+        with ThreadPoolExecutor(min(8, len(kinds))) as ex:
+            list(ex.map(fill, range(len(kinds))))
+        out_slot = np.concatenate([kk.out_slot for kk in kinds]).astype(np.uint32)
+        off = np.concatenate([bases[x] + np.arange(kk.count, dtype=np.int64) * L16[x]
+                              for x, kk in enumerate(kinds)]).astype(np.uint64)
+        ln = np.concatenate([np.full(kk.count, len(kk.tmpl), dtype=np.uint32) for kk in kinds])
+        nh = np.concatenate([np.full(kk.count, len(kk.holes), dtype=np.uint64) for kk in kinds])
+        hpos = [np.tile(np.array([p for p, _ in kk.holes], dtype=np.uint32), kk.count) for kk in kinds if kk.holes]
+        hslot = [np.stack([sl for _, sl in kk.holes], axis=1).reshape(-1).astype(np.uint32)
+                 for kk in kinds if kk.holes]
+        hole_ptr = np.zeros(self.n_jobs + 1, dtype=np.uint64)
+        hole_ptr[1:] = np.cumsum(nh)
+        return dict(n_slots=self.n_slots, out_slot=out_slot, tmpl_off=off, tmpl_len=ln, hole_ptr=hole_ptr,
+                    hole_pos=np.concatenate(hpos), hole_slot=np.concatenate(hslot), blob=blob)
+
+    def change_set(self, frac=0.01, seed=0x5EED0003, n_global=None):
         """File slots to change (1% of leaf files) and their two versions:
-        v_old = current IDs, v_new = SHA256(old || "v2")."""
+        v_old = current IDs, v_new = SHA256(old || "v2").  n_global: this DAG
+        is the slice (sample0) of a global DAG with n_global leaf files -- the
+        change set is the global one's, restricted to this slice (so every
+        partition of one global DAG changes the same files)."""
+        nf = len(self.file_slots)
+        f0 = 2 * self.P * self.sample0 if n_global is not None else 0
+        n_all = nf if n_global is None else n_global
         rng = np.random.default_rng(seed)
-        n = max(1, int(round(frac * len(self.file_slots))))
-        pick = np.sort(rng.choice(len(self.file_slots), size=n, replace=False)).astype(np.uint32)
+        n = max(1, int(round(frac * n_all)))
+        pick = np.sort(rng.choice(n_all, size=n, replace=False)).astype(np.int64)
+        pick = (pick[(pick >= f0) & (pick < f0 + nf)] - f0).astype(np.uint32)
         old = self.leaf_ids[pick]
-        new = np.frombuffer(b"".join(_h(o.tobytes() + b"v2") for o in old), dtype=np.uint8).reshape(n, 32)
+        new = np.frombuffer(b"".join(_h(o.tobytes() + b"v2") for o in old), dtype=np.uint8).reshape(len(pick), 32)
         return self.file_slots[pick], old, new
 
     # ------------------------------------------------ oracle twin (small S)
@@ -431,23 +473,28 @@ def merge_tmpl(k):
 def append_jobs(a, jobs):
     """Append jobs to rf_graph_desc arrays: jobs = [(tmpl bytes, [(pos,
     slot)...])], each given the next fresh output slot.  Returns (arrays,
-    out slots)."""
-    blob = bytearray(np.asarray(a["blob"], dtype=np.uint8).tobytes())
-    while len(blob) % 16:
-        blob.append(0)
+    out slots).  One concatenation of the blob (it is ~15 GB at 100M nodes):
+    callers that append in stages collect the jobs first (merge_tree_jobs)."""
+    old = np.asarray(a["blob"], dtype=np.uint8)
+    pad = (-len(old)) % 16
+    base = len(old) + pad
     n = int(a["n_slots"])
-    offs, lens, hp, pos, sl, outs = [], [], [], [], [], []
+    parts, offs, lens, hp, pos, sl, outs = [], [], [], [], [], [], []
     h = int(a["hole_ptr"][-1])
+    cur = base
     for tmpl, holes in jobs:
-        offs.append(len(blob))
+        offs.append(cur)
         lens.append(len(tmpl))
-        blob += tmpl + bytes((-len(tmpl)) % 16)
+        t = tmpl + bytes((-len(tmpl)) % 16)
+        parts.append(t)
+        cur += len(t)
         h += len(holes)
         hp.append(h)
         pos += [p for p, _ in holes]
         sl += [x for _, x in holes]
         outs.append(n)
         n += 1
+    blob = np.concatenate([old, np.zeros(pad, np.uint8), np.frombuffer(b"".join(parts), dtype=np.uint8)])
     out = dict(n_slots=n,
                out_slot=np.concatenate([a["out_slot"], np.array(outs, np.uint32)]).astype(np.uint32),
                tmpl_off=np.concatenate([a["tmpl_off"], np.array(offs, np.uint64)]).astype(np.uint64),
@@ -455,53 +502,126 @@ def append_jobs(a, jobs):
                hole_ptr=np.concatenate([a["hole_ptr"], np.array(hp, np.uint64)]).astype(np.uint64),
                hole_pos=np.concatenate([a["hole_pos"], np.array(pos, np.uint32)]).astype(np.uint32),
                hole_slot=np.concatenate([a["hole_slot"], np.array(sl, np.uint32)]).astype(np.uint32),
-               blob=np.frombuffer(bytes(blob), dtype=np.uint8))
+               blob=blob)
     return out, np.array(outs, dtype=np.uint32)
+
+
+def merge_tree_jobs(next_slot, leaves, fanin=32):
+    """The jobs of a fan-in-`fanin` Merge tree over `leaves` slots whose
+    outputs will be numbered from next_slot on (as append_jobs numbers them).
+    Returns (jobs, root slot, [tree slots in job order])."""
+    cur, made, jobs = np.asarray(leaves, dtype=np.uint32), [], []
+    while len(cur) > 1:
+        lvl = [(merge_tmpl(len(g)), [(34 * j + 2, int(x)) for j, x in enumerate(g)])
+               for g in (cur[i:i + fanin] for i in range(0, len(cur), fanin))]
+        cur = np.arange(next_slot, next_slot + len(lvl), dtype=np.uint32)
+        next_slot += len(lvl)
+        jobs += lvl
+        made.append(cur)
+    return jobs, int(cur[0]), (np.concatenate(made) if made else np.zeros(0, np.uint32))
 
 
 def merge_tree(a, leaves, fanin=32):
     """Fan-in-`fanin` Merge tree over `leaves` slots, appended to arrays a.
     Returns (arrays, root slot, [tree slots in job order])."""
-    cur, made = np.asarray(leaves, dtype=np.uint32), []
-    while len(cur) > 1:
-        jobs = [(merge_tmpl(len(g)), [(34 * j + 2, int(x)) for j, x in enumerate(g)])
-                for g in (cur[i:i + fanin] for i in range(0, len(cur), fanin))]
-        a, cur = append_jobs(a, jobs)
-        made.append(cur)
-    return a, int(cur[0]), (np.concatenate(made) if made else np.zeros(0, np.uint32))
+    jobs, root, made = merge_tree_jobs(int(a["n_slots"]), leaves, fanin)
+    if jobs:
+        a, _ = append_jobs(a, jobs)
+    return a, root, made
 
 
 class PartitionedDag1000:
-    """configs[3]'s DAG, one rank's piece: the global 1000align DAG has
-    nranks*S samples and rank r owns samples [r*S, (r+1)*S) -- SURVEY §8(e):
-    partition by sample subtree, the shared reference-index chain replicated
-    on every rank, the global root on rank 0.  Each rank merges its sample
-    roots (XS) with a fan-in-32 Merge tree into a rank root; rank 0's global
-    root merges the rank roots (its own locally, the others imported: one
-    boundary digest per rank, so the exchange per step is nranks bits + 32*
-    nranks bytes).  desc: this piece's rf_graph_desc arrays; part: its
-    rf_graph_part (exports = the rank root on ranks > 0, boundary id = rank).
-    Slot layout: the rank's Dag1000 slots, then its tree slots, then (rank 0)
-    the import slots of ranks 1.. and the global root."""
+    """configs[3]'s DAG, one rank's piece.  The global DAG is a 1000align DAG
+    of nparts*S samples cut into nparts parts of S samples; each part's
+    sample roots (XS) are merged by a fan-in-32 Merge tree into a part root,
+    and the global root merges the nparts part roots (none when nparts = 1).
+    Rank r of nranks owns k = nparts/nranks consecutive parts (samples [r*k*S,
+    (r+1)*k*S)) -- SURVEY §8(e): partition by sample subtree, the shared
+    reference-index chain replicated on every rank, the global root on rank
+    0, which imports the other ranks' part roots (one 32-B boundary digest per
+    part, so the exchange per step is nparts bits + 32*nparts bytes).  The
+    global DAG is the same for every nranks dividing nparts (strong scaling:
+    nranks = 1 holds all of it, no exchange), node for node.
+    desc: this piece's rf_graph_desc arrays; part: its rf_graph_part (exports
+    = the rank's part roots on ranks > 0; boundary id of part q = q).  Slot
+    layout: the rank's Dag1000 slots, its tree slots (part by part), then
+    (rank 0) the global root and the import slots of the other ranks' parts."""
 
-    def __init__(self, S, P, nranks, rank, seed=0x5EED0003, fanin=32):
-        self.nranks, self.rank = nranks, rank
-        self.dag = Dag1000(S, P, seed, sample0=rank * S)
+    def __init__(self, S, P, nranks, rank, seed=0x5EED0003, fanin=32, nparts=None):
+        nparts = nranks if nparts is None else nparts
+        if nparts % nranks:
+            raise ValueError("nparts (%d) must be a multiple of nranks (%d)" % (nparts, nranks))
+        k = nparts // nranks
+        self.nranks, self.rank, self.nparts, self.k = nranks, rank, nparts, k
+        self.dag = Dag1000(k * S, P, seed, sample0=rank * k * S)
         a = self.dag.arrays()
-        a, self.rank_root, self.tree_slots = merge_tree(a, self.dag.kinds["XS"].out_slot, fanin)
+        xs = self.dag.kinds["XS"].out_slot
+        nxt = int(a["n_slots"])
+        jobs, roots, trees = [], [], []
+        for p in range(k):
+            jb, root, tree = merge_tree_jobs(nxt, xs[p * S:(p + 1) * S], fanin)
+            nxt += len(jb)
+            jobs += jb
+            roots.append(root)
+            trees.append(tree)
+        self.part_roots = np.array(roots, dtype=np.uint32)
+        self.tree_slots = np.concatenate(trees) if trees else np.zeros(0, np.uint32)
+        self.rank_root = roots[0] if k == 1 else None
         self.import_slot = np.zeros(0, np.uint32)
         self.global_root = None
-        if rank == 0 and nranks > 1:
-            base = int(a["n_slots"])
-            self.import_slot = np.arange(base, base + nranks - 1, dtype=np.uint32)
-            a["n_slots"] = base + nranks - 1
-            holes = [self.rank_root] + self.import_slot.tolist()
-            a, outs = append_jobs(a, [(merge_tmpl(nranks), [(34 * j + 2, x) for j, x in enumerate(holes)])])
-            self.global_root = int(outs[0])
+        if rank == 0 and nparts > 1:
+            # the global root takes the next slot, the imports the ones after
+            # it, so every appended job goes in one append (one blob copy)
+            self.global_root = nxt
+            self.import_slot = np.arange(nxt + 1, nxt + 1 + nparts - k, dtype=np.uint32)
+            holes = roots + self.import_slot.tolist()
+            jobs.append((merge_tmpl(nparts), [(34 * j + 2, int(x)) for j, x in enumerate(holes)]))
+        if jobs:
+            a, outs = append_jobs(a, jobs)
+        if self.global_root is not None:
+            assert int(outs[-1]) == self.global_root
+            a["n_slots"] = int(a["n_slots"]) + nparts - k
         self.desc = a
         self.n_nodes = self.dag.n_nodes + len(self.tree_slots) + (1 if self.global_root is not None else 0)
-        ex = np.array([self.rank_root] if rank > 0 else [], dtype=np.uint32)
-        self.part = dict(nranks=nranks, rank=rank, max_export=1 if nranks > 1 else 0, export_slot=ex,
+        multi = nranks > 1
+        self.part = dict(nranks=nranks, rank=rank, max_export=k if multi else 0,
+                         export_slot=self.part_roots if rank > 0 else np.zeros(0, np.uint32),
                          import_slot=self.import_slot,
-                         import_bid=np.arange(1, nranks, dtype=np.uint32) if rank == 0 else np.zeros(0, np.uint32),
-                         any_import=nranks > 1, rounds=1 if nranks > 1 else 0)
+                         import_bid=np.arange(k, nparts, dtype=np.uint32) if rank == 0 and multi
+                         else np.zeros(0, np.uint32),
+                         any_import=multi, rounds=1 if multi else 0)
+
+    def dirty_work(self, file_slots, global_changed=True):
+        """(jobs, nodes, material blocks) a change of the local leaf-file slots
+        `file_slots` makes this piece hash -- the dirty closure, counted on the
+        host from the layout: per changed file its Val + Coerce, per changed
+        pair its ten-node chain + the pE1 physical key, per changed sample its
+        five-node tail, the Merge-tree ancestors, and (rank 0, when anything
+        anywhere changed) the global root.  Blocks are the full materials'
+        (ceil((len + 9) / 64)), as the reference hashes them."""
+        d, a = self.dag, self.desc
+        blk = {k: (len(kk.tmpl) + 9 + 63) // 64 for k, kk in d.kinds.items()}
+        f = np.asarray(file_slots, dtype=np.int64)
+        odd = int((f % 2).sum())
+        even = len(f) - odd
+        jobs = 2 * len(f)
+        blocks = even * (blk["V1"] + blk["C1"]) + odd * (blk["V2"] + blk["C2"])
+        pairs = np.unique(f // 2)
+        chain = ("E1", "C3", "K1", "C4", "E2", "C5", "K2", "C6", "E3", "C7", "pE1")
+        jobs += len(pairs) * len(chain)
+        blocks += len(pairs) * sum(blk[k] for k in chain)
+        samples = np.unique(pairs // d.P)
+        tail = ("KS", "CS1", "ES", "CS2", "XS")
+        jobs += len(samples) * len(tail)
+        blocks += len(samples) * sum(blk[k] for k in tail)
+        # the Merge trees (and the global root): the jobs appended after the DAG's
+        dirty = set(d.kinds["XS"].out_slot[samples].tolist())
+        hp, hs, osl, tl = a["hole_ptr"], a["hole_slot"], a["out_slot"], a["tmpl_len"]
+        imports = set(self.import_slot.tolist())
+        for j in range(d.n_jobs, len(osl)):
+            deps = hs[int(hp[j]):int(hp[j + 1])].tolist()
+            if any(x in dirty for x in deps) or (global_changed and any(x in imports for x in deps)):
+                dirty.add(int(osl[j]))
+                jobs += 1
+                blocks += (int(tl[j]) + 9 + 63) // 64
+        return jobs, jobs - len(pairs), blocks

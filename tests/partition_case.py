@@ -17,7 +17,7 @@ import threading
 import numpy as np
 
 import reflow_oracle as O
-from reflow_amd.workloads import Dag1000, append_jobs, merge_tmpl, merge_tree
+from reflow_amd.workloads import Dag1000, PartitionedDag1000, merge_tree_jobs
 
 WD0 = b"\x00\x05" + bytes(32)
 
@@ -85,7 +85,7 @@ class ThreadGather:
     """All-gather between threads of one process (ranks as threads)."""
 
     def __init__(self, n):
-        self.n, self.bar, self.buf = n, threading.Barrier(n, timeout=120), [None] * n
+        self.n, self.bar, self.buf = n, threading.Barrier(n, timeout=600), [None] * n
 
     def fn(self, rank):
         def allgather(b):
@@ -122,19 +122,13 @@ def run_threads(nranks, body):
 
 def global_c4(S, P, nranks, seed=0x5EED0003, fanin=32):
     """The whole configs[3] DAG that PartitionedDag1000(S, P, nranks, r)
-    pieces: Dag1000(nranks*S) + per-rank Merge trees + the global root.
-    Returns (G, arrays, owner, rank roots, rank tree slots, global root)."""
-    G = Dag1000(S * nranks, P, seed)
-    a = G.arrays()
-    roots, trees = [], []
-    for r in range(nranks):
-        a, root, tree = merge_tree(a, G.kinds["XS"].out_slot[r * S:(r + 1) * S], fanin)
-        roots.append(root)
-        trees.append(tree)
-    groot = None
-    if nranks > 1:
-        a, outs = append_jobs(a, [(merge_tmpl(nranks), [(34 * j + 2, x) for j, x in enumerate(roots)])])
-        groot = int(outs[0])
+    pieces -- itself the one-rank piece of nranks parts -- with an owner per
+    job (part r -> rank r).  Returns (G, arrays, owner, part roots, part tree
+    slots, global root)."""
+    whole = PartitionedDag1000(S, P, 1, 0, seed=seed, fanin=fanin, nparts=nranks)
+    G, a = whole.dag, whole.desc
+    sizes = [len(merge_tree_jobs(0, np.zeros(S, np.uint32), fanin)[0])] * nranks
+    trees = np.split(whole.tree_slots, np.cumsum(sizes)[:-1])
     owner = []
     for name, kk in G.kinds.items():
         if name in SHARED:
@@ -145,22 +139,22 @@ def global_c4(S, P, nranks, seed=0x5EED0003, fanin=32):
             owner.append(np.arange(kk.count) // S)
     for r in range(nranks):
         owner.append(np.full(len(trees[r]), r))
-    if groot is not None:
+    if whole.global_root is not None:
         owner.append([0])
-    return G, a, np.concatenate(owner).astype(np.int32), roots, trees, groot
+    return G, a, np.concatenate(owner).astype(np.int32), whole.part_roots.tolist(), trees, whole.global_root
 
 
 def c4_local_to_global(piece, G, roots, trees, groot):
     """Global slot of every slot of a PartitionedDag1000 piece."""
-    d, r = piece.dag, piece.rank
+    d, r, k = piece.dag, piece.rank, piece.k
     m = np.full(int(piece.desc["n_slots"]), -1, dtype=np.int64)
     m[d.file_slots] = G.file_slots[2 * d.Q * r:2 * d.Q * (r + 1)]
     for name, kk in d.kinds.items():
         off = 0 if name in SHARED else r * kk.count
         m[kk.out_slot] = G.kinds[name].out_slot[off:off + kk.count]
-    m[piece.tree_slots] = trees[r]
+    m[piece.tree_slots] = np.concatenate(trees[r * k:(r + 1) * k])
     if piece.global_root is not None:
-        m[piece.import_slot] = roots[1:]
+        m[piece.import_slot] = roots[k:]
         m[piece.global_root] = groot
     assert (m >= 0).all()
     return m

@@ -83,6 +83,33 @@ def test_assoc_large_and_growth(ctx):
     a.close()
 
 
+@pytest.mark.parametrize("word", [1, 3, 4, 6])
+def test_assoc_keys_differing_in_one_word(ctx, word):
+    """A Put batch of 100k keys equal everywhere but one 4-byte word (the
+    ADVICE r02 case: the batch dedup's probe run used to exceed its bound and
+    the apply kernels then indexed by ~0), with repeats: every op applies in
+    index order, a later Get sees the last value per key."""
+    rng = np.random.default_rng(100 + word)
+    n = 100_000
+    keys = np.tile(rng.integers(0, 256, size=(1, 32), dtype=np.uint8), (n, 1))
+    keys[:, 4 * word:4 * word + 4] = np.arange(n, dtype=np.uint32).view(np.uint8).reshape(n, 4)
+    rep = rng.integers(0, n, size=n // 4)
+    batch = np.concatenate([keys, keys[rep]])
+    vals = rng.integers(1, 256, size=(len(batch), 32), dtype=np.uint8)
+    from reflow_amd import capi
+    a = capi.Assoc(ctx, capacity=1024)
+    st = a.put(0, batch.reshape(-1), vals.reshape(-1))
+    assert (st == 0).all()
+    src = np.arange(n)
+    for j, r in enumerate(rep.tolist()):  # ops in index order: the last Put per key wins
+        src[r] = n + j
+    last = vals[src]
+    got, found = a.get(0, keys.reshape(-1))
+    assert found.all() and (got == last).all()
+    assert a.stats()[0] == n
+    a.close()
+
+
 def test_assoc_abbrev_expansion(ctx):
     from reflow_amd import capi
     rng = random.Random(9)

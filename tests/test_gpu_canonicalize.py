@@ -99,6 +99,23 @@ def test_dedup_probe_collisions_and_hot_class(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("word", [1, 3, 4, 6])
+def test_dedup_keys_differing_in_one_word(ctx, word):
+    """100k distinct digests equal everywhere but one 4-byte word (bytes 4-7,
+    12-15, 16-19, 24-27: the words the round-2 slot hash left out), each
+    twice: every class is found (no probe-bound overflow) and canon is the
+    first occurrence."""
+    rng = np.random.default_rng(word)
+    n = 100_000
+    d = np.tile(rng.integers(0, 256, size=(1, 32), dtype=np.uint8), (n, 1))
+    d[:, 4 * word:4 * word + 4] = np.arange(n, dtype=np.uint32).view(np.uint8).reshape(n, 4)
+    d = np.concatenate([d, d[rng.permutation(n)]])
+    canon, nu = ctx.dedup_digests(d)
+    assert nu == n
+    assert canon.tolist() == _first_occurrence(d).tolist()
+
+
+@pytest.mark.gpu
 def test_dedup_device_repeated_calls(ctx):
     """The device form, called back to back on the context's stream and then
     on another stream (the context's scratch is handed between streams in

@@ -1,0 +1,82 @@
+"""The opt-in and forced K2 level variants stay correct: the streamed
+hand-over (RF_K2_STREAM=1: k2_level_pl<2, true>, whose chunk flags are
+published after an LDS wait -- ADVICE r02) and every queueable level run as a
+three-wave "wide" workgroup (RF_K2_WIDE=1: k2_level_pl<3>).  Both are read
+when a graph is loaded, so one process covers them.  Checked against the
+oracle on the random fused-chain graphs and the 1000align DAG, and on a
+larger 1000align DAG against the default mode's incremental recompute."""
+import numpy as np
+import pytest
+
+from reflow_amd.workloads import Dag1000
+from test_gpu_dag import check_against_oracle
+from test_gpu_dag import load as load_dag
+from test_gpu_dag_fusion import evaluate, random_jobs
+from test_gpu_dag_fusion import load as load_jobs
+
+pytestmark = pytest.mark.gpu
+
+MODES = [("RF_K2_STREAM", "1"), ("RF_K2_WIDE", "1")]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from reflow_amd import capi
+    c = capi.Context(0, host_threads=0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("var,val", MODES)
+def test_forced_mode_random_jobs(ctx, monkeypatch, var, val):
+    monkeypatch.setenv(var, val)
+    rng = np.random.default_rng(5)
+    n_in = 64
+    jobs = random_jobs(31, n_in=n_in)
+    inputs = [rng.integers(0, 256, size=32, dtype=np.uint8).tobytes() for _ in range(n_in)]
+    g = load_jobs(ctx, n_in, jobs)
+    g.set_slots(np.arange(n_in, dtype=np.uint32), np.frombuffer(b"".join(inputs), np.uint8).reshape(-1, 32))
+    g.recompute(full=True)
+    for step in range(3):
+        k = [1, 5, 20][step]
+        pick = rng.choice(n_in, size=k, replace=False)
+        for i in pick:
+            inputs[i] = rng.integers(0, 256, size=32, dtype=np.uint8).tobytes()
+        g.set_slots(pick.astype(np.uint32), np.frombuffer(b"".join(inputs[i] for i in pick), np.uint8).reshape(-1, 32))
+        g.recompute(full=False)
+        want = evaluate(n_in, jobs, inputs)
+        outs = np.array([o for o, _, _ in jobs], np.uint32)
+        got = g.get_slots(outs)
+        for i, o in enumerate(outs.tolist()):
+            assert got[i].tobytes() == want[o], (var, step, o)
+    g.close()
+
+
+@pytest.mark.parametrize("var,val", MODES)
+def test_forced_mode_dag1000(ctx, monkeypatch, var, val):
+    monkeypatch.setenv(var, val)
+    dag = Dag1000(4, 8)
+    g = load_dag(ctx, dag)
+    g.recompute(full=True)
+    ids = dag.leaf_ids.copy()
+    slots, old, new = dag.change_set(0.1)
+    for version in (new, old):
+        g.set_slots(slots, version)
+        g.recompute(full=False)
+        ids[slots] = version
+        check_against_oracle(g, dag, ids)
+    g.close()
+    # 0.45M nodes: the forced mode's incremental slots == the default mode's
+    big = Dag1000(1000, 32)
+    gf = load_dag(ctx, big)
+    monkeypatch.delenv(var)
+    gd = load_dag(ctx, big)
+    sl, _, nw = big.change_set(0.01)
+    every = np.arange(big.n_slots, dtype=np.uint32)
+    for gg in (gf, gd):
+        gg.recompute(full=True)
+        gg.set_slots(sl, nw)
+        gg.recompute(full=False)
+    assert (gf.get_slots(every) == gd.get_slots(every)).all()
+    gf.close()
+    gd.close()

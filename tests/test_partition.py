@@ -71,6 +71,45 @@ def test_c4_pieces_equal_global_dag(nranks, S, P, fanin, protocol):
     assert (wants[2][groot] != wants[1][groot]).any()  # rank 0 saw only imported changes
 
 
+@pytest.mark.parametrize("nranks", [1, 2, 4])
+def test_strong_layout_fixed_global_dag(nranks):
+    """bench.py's strong-scaling layout: ONE global DAG of nparts = 4 parts,
+    nranks | nparts, rank r holding parts [r*k, (r+1)*k) -- every rank count
+    computes the same digests (nranks = 1: the whole DAG, no exchange)."""
+    S, P, nparts, fanin = 6, 3, 4, 4
+    G, ga, owner, roots, trees, groot = PC.global_c4(S, P, nparts, fanin=fanin)
+    rng = np.random.default_rng(3)
+    nf = len(G.file_slots)
+    pick = np.sort(rng.choice(nf, size=7, replace=False))
+    new = G.leaf_ids.copy()
+    new[pick] = rng.integers(0, 256, size=(len(pick), 32), dtype=np.uint8)
+    wants = [PC.global_digests(G, ga, x) for x in (G.leaf_ids, new)]
+
+    def body(r, ag):
+        pc = PartitionedDag1000(S, P, nranks, r, fanin=fanin, nparts=nparts)
+        assert pc.k == nparts // nranks
+        m = PC.c4_local_to_global(pc, G, roots, trees, groot)
+        f0, nfl = 2 * pc.dag.Q * r, 2 * pc.dag.Q
+        st, _ = PC.superstep_oracle(pc.desc, pc.part, ag, inputs=(pc.dag.file_slots, G.leaf_ids[f0:f0 + nfl]))
+        out = [st["og"].slots[:len(m)].copy()]
+        mine = pick[(pick >= f0) & (pick < f0 + nfl)]
+        st, _ = PC.superstep_oracle(pc.desc, pc.part, ag, changed=(pc.dag.file_slots[mine - f0], new[mine]), state=st)
+        out.append(st["og"].slots[:len(m)].copy())
+        st["og"].close()
+        return m, out, pc.part
+
+    res = PC.run_threads(nranks, body)
+    for r, (m, out, part) in enumerate(res):
+        for step, (slots, want) in enumerate(zip(out, wants)):
+            assert (slots == want[m]).all(), (r, step)
+        if nranks > 1:
+            assert part["max_export"] == nparts // nranks and part["rounds"] == 1
+            assert len(part["import_slot"]) == (nparts - nparts // nranks if r == 0 else 0)
+    assert (wants[1][groot] != wants[0][groot]).any()
+    with pytest.raises(ValueError):
+        PartitionedDag1000(S, P, 3, 0, nparts=nparts)
+
+
 def test_split_finds_the_same_boundary():
     nranks, S, P = 3, 10, 2
     G, ga, owner, roots, trees, groot = PC.global_c4(S, P, nranks, fanin=4)
@@ -96,3 +135,21 @@ def test_split_counts_boundary_crossings():
     rep = owner.copy()  # the tail replicated: still read across ranks once more
     rep[-1] = -1
     assert capi.GraphPiece(arrays, 3, 0, rep).part["rounds"] == 2
+
+
+@pytest.mark.parametrize("nparts,fanin", [(1, 32), (4, 4)])
+def test_dirty_work_matches_oracle(nparts, fanin):
+    """PartitionedDag1000.dirty_work (bench.py's dirty-node and block counts
+    for the 100M leg, where the oracle is too slow) equals the oracle's
+    incremental update: jobs hashed and material blocks."""
+    import reflow_oracle as O
+    pc = PartitionedDag1000(10, 3, 1, 0, fanin=fanin, nparts=nparts)
+    slots, old, new = pc.dag.change_set(0.1)
+    og = O.OGraph(pc.desc)
+    og.set_inputs(pc.dag.file_slots, pc.dag.leaf_ids)
+    og.full()
+    jobs = og.update(slots, new)
+    blocks = og.last_blocks()
+    og.close()
+    assert pc.dirty_work(slots)[0] == jobs
+    assert pc.dirty_work(slots)[2] == blocks
