@@ -527,6 +527,8 @@ def bench_dag(args, dist, ctx, budget):
     res["roofline_full"] = {"bound": "valu", "achieved": round(ach, 2), "peak": round(SHA_VALU_PEAK_GBS, 1),
                             "unit": "GB/s", "frac": round(ach / SHA_VALU_PEAK_GBS, 4)}
     res["canonicalize"] = bench_canon(ctx, g, dag)
+    if "checkpoint" not in args.skip and budget.allow("checkpoint", 25):
+        res["checkpoint"] = bench_checkpoint(ctx, g, a, t_build + t_load + full_ms * 1e-3)
     # the configs[2] CPU legs need the host arrays (rank 0, N = 1)
     res["_cpu"] = {"a": a, "dag": dag, "slots": slots, "old": old, "new": new,
                    "gpu_dirty_jobs": int(n_dirty_jobs)}
@@ -643,6 +645,36 @@ def bench_dag100m(args, dist, ctx, comm, budget):
         b.free()
     g.close()
     return res
+
+
+def bench_checkpoint(ctx, g, a, cold_s):
+    """Checkpoint / resume of the loaded configs[2] graph (rf_graph_save /
+    rf_graph_restore): the file holds the lowered device form and
+    every slot digest, so a restarted process resumes incremental steps
+    without lowering, level analysis or a full recompute.  cold_s: what the
+    same process paid to get there (build + load + full recompute)."""
+    import shutil
+    import tempfile
+    d = tempfile.mkdtemp(prefix="rf_ckpt_")
+    try:
+        path = os.path.join(d, "c3.ckpt")
+        t0 = time.perf_counter()
+        g.save(path)
+        save_s = time.perf_counter() - t0
+        size = os.path.getsize(path)
+        t0 = time.perf_counter()
+        r = capi.Graph.restore(ctx, path)
+        restore_s = time.perf_counter() - t0
+        every = np.arange(a["n_slots"], dtype=np.uint32)
+        same = bool((r.get_slots(every) == g.get_slots(every)).all())
+        r.close()
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    log("  checkpoint: %.2f GB saved in %.1f s, restored in %.1f s (cold start %.1f s), slots equal: %s"
+        % (size / 1e9, save_s, restore_s, cold_s, same))
+    return {"file_bytes": size, "save_s": round(save_s, 2), "restore_s": round(restore_s, 2),
+            "cold_start_s": round(cold_s, 2), "slots_equal": same,
+            "what": "rf_graph_save after the timed steps, rf_graph_restore into a new graph, every slot compared"}
 
 
 def bench_canon(ctx, g, dag):
@@ -1065,7 +1097,7 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
     ap.add_argument("--gpu-only-run", type=int, default=1, help="one GPU-only run (duo roofline)")
     ap.add_argument("--budget-s", type=float, default=420.0)
-    ap.add_argument("--skip", default="", help="comma list of: c1,install,dag,dag100m,probe,cpu")
+    ap.add_argument("--skip", default="", help="comma list of: c1,install,dag,dag100m,checkpoint,probe,cpu")
     args = ap.parse_args()
     args.skip = set(filter(None, args.skip.split(",")))
     budget = Budget(args.budget_s)

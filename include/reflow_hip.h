@@ -363,6 +363,24 @@ typedef struct {
 } rf_graph_stats;
 int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
 
+/* ---- Checkpoint / resume of a loaded DAG ------------------------
+ * Reference: a run's State is marshalled after every runner step
+ * (runner/runner.go:51-85) and the local executor restores its execs from
+ * manifests (local/executor.go:122-200); memoization is the resume mechanism.
+ * rf_graph_save writes the graph's lowered device form (job records, holes,
+ * reverse edges, padded templates, midstates, level layout) AND its current
+ * slot digests to `path` (written to path.tmp, fsync'ed, renamed), with a
+ * SHA-256 per 64 MiB chunk and one over them.  Steps queued on any stream
+ * complete first (device synchronise).  rf_graph_restore loads such a file on
+ * ctx's device: the graph is ready for incremental steps (set_slots +
+ * recompute) at once -- no lowering, no level analysis, no full recompute.
+ * A partition (rf_graph_set_part) is not part of the file: re-attach it.
+ * Errors: RF_EIO (cannot create / open / write), RF_EINVAL (not a graph
+ * checkpoint, or another version), RF_EINTEGRITY (truncated, or the bytes do
+ * not match their checksums: errors.Integrity). */
+int rf_graph_save(rf_graph *g, const char *path);
+int rf_graph_restore(rf_ctx *ctx, const char *path, rf_graph **out);
+
 /* ---- One DAG over many GPUs ---------------------------------
  * Each rank loads its PIECE of the global job graph (rf_graph_load on a local
  * desc: its own jobs plus replicated ones, slots renumbered locally) and

@@ -31,6 +31,7 @@ EXPORTS = [
     "rf_fileset_digest_device", "rf_install_dir", "rf_install_info", "rf_install_entries",
     "rf_install_destroy",
     "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
+    "rf_graph_save", "rf_graph_restore",
     "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
     "rf_bloom_destroy", "rf_bloom_probe", "rf_bloom_probe_device", "rf_bloom_add",
@@ -289,6 +290,7 @@ def lib():
             "rf_install_entries": ([vp, vp, vp, vp, vp], i32),
             "rf_install_destroy": ([vp], None),
             "rf_graph_load": ([vp, vp, vp], i32), "rf_graph_destroy": ([vp], None),
+            "rf_graph_save": ([vp, ctypes.c_char_p], i32), "rf_graph_restore": ([vp, ctypes.c_char_p, vp], i32),
             "rf_graph_set_slots": ([vp, vp, vp, u32], i32),
             "rf_graph_set_slots_device": ([vp, vp, vp, u32, vp], i32),
             "rf_graph_recompute": ([vp, i32, vp], i32),
@@ -796,6 +798,19 @@ class Graph:
         s = GraphStats()
         _check(lib().rf_graph_stats_get(self._h, ctypes.byref(s)))
         return s
+
+    def save(self, path):
+        """rf_graph_save: the lowered graph and its slot digests to `path`."""
+        _check(lib().rf_graph_save(self._h, os.fsencode(path)))
+
+    @classmethod
+    def restore(cls, ctx, path):
+        """rf_graph_restore: a graph saved by save(), ready for incremental steps."""
+        g = cls.__new__(cls)
+        g.ctx, g._keep = ctx, None
+        g._h = ctypes.c_void_p()
+        _check(lib().rf_graph_restore(ctx.handle, os.fsencode(path), ctypes.byref(g._h)))
+        return g
 
     @classmethod
     def from_arrays(cls, ctx, a):

@@ -1125,6 +1125,53 @@ extern "C" int rf_fileset_value_digest_batch(rf_ctx* ctx, const rf_fileset_tree*
 
 // ---------------------------------------------------------------------------
 // Digest DAG
+// Device buffers of a graph of J jobs, S slots, L levels, H holes and
+// tmpl_bytes of padded templates (contents not uploaded: rf_graph_load and
+// rf_graph_restore fill them), the per-step state zeroed and gr->g pointed at
+// them.  Caller holds ctx->mu.
+int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes) {
+    rf_ctx* ctx = gr->ctx;
+    GraphDev& G = gr->g;
+    G.n_jobs = J;
+    G.n_slots = S;
+    G.n_levels = L;
+    hipError_t e;
+    if ((e = gr->b_meta.ensure(std::max<size_t>(32ull * J, 64))) != hipSuccess ||
+        (e = gr->b_holes.ensure(std::max<size_t>(8ull * H, 64))) != hipSuccess ||  // k2 reads element 0 always
+        (e = gr->b_cons_ptr.ensure(std::max<size_t>(4ull * (S + 1), 64))) != hipSuccess ||
+        (e = gr->b_cons_job.ensure(std::max<size_t>(8ull * H, 64))) != hipSuccess ||
+        (e = gr->b_tmpl.ensure(std::max<size_t>(tmpl_bytes, 64))) != hipSuccess ||
+        (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
+        (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
+        (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
+        (e = gr->b_lmeta.ensure(32ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
+        (e = gr->b_counts.ensure(8ull * (L + 1))) != hipSuccess ||  // two halves (plain-step parity)
+        (e = gr->b_counts_last.ensure(4ull * (L + 1))) != hipSuccess ||
+        (e = gr->b_lvl_start.ensure(std::max<size_t>(4ull * (L + 1), 64))) != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph alloc: %s", hipGetErrorString(e));
+    HIPC(sync_memset(ctx, gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
+    HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
+    HIPC(sync_memset(ctx, gr->b_counts.p, 0, 8ull * (L + 1)));
+    HIPC(sync_memset(ctx, gr->b_counts_last.p, 0, 4ull * (L + 1)));
+    G.meta = gr->b_meta.as<uint4>();
+    G.holes = gr->b_holes.as<uint2>();
+    G.cons_ptr = gr->b_cons_ptr.as<uint32_t>();
+    G.cons = gr->b_cons_job.as<uint2>();
+    G.tmpl = gr->b_tmpl.as<uint8_t>();
+    G.slots = gr->b_slots.as<uint8_t>();
+    G.dirty = gr->b_dirty.as<uint32_t>();
+    G.list = gr->b_list.as<uint32_t>();
+    G.lmeta = gr->b_lmeta.as<uint4>();
+    G.counts = gr->b_counts.as<uint32_t>();
+    G.counts_other = G.counts + (L + 1);
+    G.counts_last = gr->b_counts_last.as<uint32_t>();
+    gr->last_counts = G.counts_last;
+    G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
+    if (!gr->e0) HIPC(hipEventCreate(&gr->e0));
+    if (!gr->e1) HIPC(hipEventCreate(&gr->e1));
+    return RF_OK;
+}
+
 extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out) {
     ARG(ctx && d && out, "null argument");
     *out = nullptr;
@@ -1354,48 +1401,20 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     gr->tmpl_bytes = tb;
     // upload
     GraphDev& G = gr->g;
-    G.n_jobs = J;
-    G.n_slots = S;
-    G.n_levels = L;
+    if (int rc = graph_device_alloc(gr, J, S, L, H, tmpl.size())) return rc;
+    hipError_t e;
+    if ((e = sync_copy(ctx, gr->b_meta.p, meta.data(), 32ull * J, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = sync_copy(ctx, gr->b_holes.p, holes.data(), 8ull * H, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = sync_copy(ctx, gr->b_cons_ptr.p, cons_ptr.data(), 4ull * (S + 1), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = sync_copy(ctx, gr->b_cons_job.p, cons_job.data(), 8ull * H, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = sync_copy(ctx, gr->b_tmpl.p, tmpl.data(), tmpl.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = sync_copy(ctx, gr->b_lvl_start.p, G.lvl_start.data(), 4ull * (L + 1), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(RF_EDEVICE, "graph upload: %s", hipGetErrorString(e));
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
         hipError_t e = b.ensure(std::max<size_t>(bytes, 64));
         if (e != hipSuccess) return e;
         return bytes ? sync_copy(ctx, b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
     };
-    hipError_t e;
-    if ((e = up(gr->b_meta, meta.data(), 32ull * J)) != hipSuccess ||
-        (e = up(gr->b_holes, holes.data(), 8ull * H)) != hipSuccess ||
-        (e = up(gr->b_cons_ptr, cons_ptr.data(), 4ull * (S + 1))) != hipSuccess ||
-        (e = up(gr->b_cons_job, cons_job.data(), 8ull * H)) != hipSuccess ||
-        (e = up(gr->b_tmpl, tmpl.data(), tmpl.size())) != hipSuccess ||
-        (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
-        (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
-        (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_lmeta.ensure(32ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_counts.ensure(8ull * (L + 1))) != hipSuccess ||  // two halves (plain-step parity)
-        (e = gr->b_counts_last.ensure(4ull * (L + 1))) != hipSuccess ||
-        (e = up(gr->b_lvl_start, G.lvl_start.data(), 4ull * (L + 1))) != hipSuccess)
-        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph upload: %s",
-                    hipGetErrorString(e));
-    HIPC(gr->b_holes.ensure(8));  // k2's record loads read element 0 unconditionally
-    HIPC(sync_memset(ctx, gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
-    HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
-    HIPC(sync_memset(ctx, gr->b_counts.p, 0, 8ull * (L + 1)));
-    HIPC(sync_memset(ctx, gr->b_counts_last.p, 0, 4ull * (L + 1)));
-    G.meta = gr->b_meta.as<uint4>();
-    G.holes = gr->b_holes.as<uint2>();
-    G.cons_ptr = gr->b_cons_ptr.as<uint32_t>();
-    G.cons = gr->b_cons_job.as<uint2>();
-    G.tmpl = gr->b_tmpl.as<uint8_t>();
-    G.slots = gr->b_slots.as<uint8_t>();
-    G.dirty = gr->b_dirty.as<uint32_t>();
-    G.list = gr->b_list.as<uint32_t>();
-    G.lmeta = gr->b_lmeta.as<uint4>();
-    G.counts = gr->b_counts.as<uint32_t>();
-    G.counts_other = G.counts + (L + 1);
-    G.counts_last = gr->b_counts_last.as<uint32_t>();
-    gr->last_counts = G.counts_last;
-    G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
     {
         const char* v = getenv("RF_K2_STREAM");  // (opt-in variant, read per load)
         G.stream_handover = v && atoi(v) == 1;
@@ -1429,8 +1448,6 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
         G.stamps = static_cast<unsigned long long*>(gr->b_stamps.p);
     }
-    HIPC(hipEventCreate(&gr->e0));
-    HIPC(hipEventCreate(&gr->e1));
     guard.release();
     *out = gr;
     return RF_OK;
@@ -1974,8 +1991,44 @@ extern "C" int rf_bloom_collect(rf_bloom* bl, const uint8_t* digests32, const in
 // K5: Canonicalize's flowMap (flow.go:814-843, flowMap.Get/Put :881-907)
 // Scratch of a device-form call: the context's StreamScratch, handed
 // between the callers' streams in stream order (ctx.h).
+// RF_DEDUP_SCRATCH (diagnostic, tools/pool_diag.py): the round-2 per-call
+// stream-ordered pool scratch that came back corrupted, and variants that
+// bisect it -- "pool" as it was (release threshold max, hipMemsetAsync),
+// "pool_sync" + a stream sync after the allocations, "pool_fill" a fill kernel
+// instead of hipMemsetAsync, "pool_nothresh" the pool's default threshold.
+static int dedup_pool_diag(const char* mode, rf_ctx* ctx, const void* d_digests32, uint32_t n, void* d_canon,
+                           void* d_n_unique, hipStream_t s) {
+    static std::once_flag once;
+    if (strcmp(mode, "pool_nothresh") != 0)
+        std::call_once(once, [&] {
+            hipMemPool_t pool = nullptr;
+            if (hipDeviceGetDefaultMemPool(&pool, ctx->device) == hipSuccess && pool) {
+                uint64_t keep = ~0ull;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            }
+        });
+    void *tab = nullptr, *slot_of = nullptr;
+    const size_t tab_bytes = 4ull * dedup_table_slots(n);
+    HIPC(hipMallocAsync(&tab, tab_bytes, s));
+    HIPC(hipMallocAsync(&slot_of, 4ull * std::max<uint32_t>(n, 1), s));
+    if (strcmp(mode, "pool_sync") == 0) HIPC(hipStreamSynchronize(s));
+    if (strcmp(mode, "pool_fill") == 0) HIPC(launch_fill_u32(static_cast<uint32_t*>(tab), 0xffffffffu, tab_bytes / 4, s));
+    hipError_t e = launch_dedup(static_cast<const uint8_t*>(d_digests32), n, static_cast<uint32_t*>(tab),
+                                static_cast<uint32_t*>(slot_of), static_cast<uint32_t*>(d_canon),
+                                static_cast<uint32_t*>(d_n_unique), s, strcmp(mode, "pool_fill") != 0);
+    (void)hipFreeAsync(slot_of, s);
+    (void)hipFreeAsync(tab, s);
+    if (e != hipSuccess) return fail(RF_EDEVICE, "dedup: %s", hipGetErrorString(e));
+    if (getenv("RF_DEDUP_PTRS"))
+        fprintf(stderr, "[dedup %s] tab %p slot_of %p canon %p n_unique %p stream %p\n", mode, tab, slot_of, d_canon,
+                d_n_unique, (void*)s);
+    return RF_OK;
+}
+
 static int dedup_on_stream(rf_ctx* ctx, const void* d_digests32, uint32_t n, void* d_canon, void* d_n_unique,
                            hipStream_t s) {
+    if (const char* mode = getenv("RF_DEDUP_SCRATCH"))
+        if (strncmp(mode, "pool", 4) == 0) return dedup_pool_diag(mode, ctx, d_digests32, n, d_canon, d_n_unique, s);
     StreamScratch& sc = ctx->sc_dedup;
     std::lock_guard<std::mutex> lk(sc.mu);
     const size_t tab_bytes = 4ull * dedup_table_slots(n);

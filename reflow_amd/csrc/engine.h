@@ -167,8 +167,10 @@ hipError_t launch_bloom_collect(const BloomDev& b, const uint8_t* d32, const int
 uint32_t dedup_table_slots(uint32_t n);
 // canon[i] = min{j : dig[j] == dig[i]}; table [dedup_table_slots(n)] and
 // slot_of [n] are scratch; *n_unique = |{i : canon[i] == i}|.
+// clear_table = false: the caller has already filled the table with ~0
 hipError_t launch_dedup(const uint8_t* dig, uint32_t n, uint32_t* table, uint32_t* slot_of, uint32_t* canon,
-                        uint32_t* n_unique, hipStream_t s);
+                        uint32_t* n_unique, hipStream_t s, bool clear_table = true);
+hipError_t launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s);
 
 // HBM assoc (assoc.Assoc with test/testutil/assoc.go semantics)
 struct AssocView {

@@ -50,4 +50,5 @@ struct rf_graph {
 
 
 int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s);
+int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes);
 void graph_part_release(rf_graph* gr);

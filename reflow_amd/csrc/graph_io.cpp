@@ -1,0 +1,306 @@
+// graph_io.cpp -- checkpoint / resume of a loaded digest DAG: rf_graph_save
+// writes the lowered device form (job records, holes, reverse edges, padded
+// templates, midstates, level layout) together with the current slot digests;
+// rf_graph_restore brings it back onto a device ready for incremental steps,
+// without the lowering, the level / fusion analysis, the midstate hashing or a
+// full recompute.
+//
+// Reference: memoization is Reflow's resume mechanism: a run's
+// State is marshalled after every runner step (runner/runner.go:51-85) and
+// the local executor restores its execs from manifests
+// (local/executor.go:122-200); the digests themselves are recomputed per Eval
+// (flow.go:653-664).  Here the digests ARE the state a resumed run needs, so
+// they are persisted with the graph they belong to, and a later process
+// applies only what changed since.
+//
+// File: a 128-B header, the sections in a fixed order (each a u64 length and
+// its bytes), then one SHA-256 per 64 MiB chunk of each section, the SHA-256
+// of header || chunk digests, and an end marker.  The chunk digests are
+// computed on the host leg's threads (SHA-NI); a mismatch on restore is
+// RF_EINTEGRITY (errors.Integrity, repository/file/repository.go:160-162).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "graph_internal.h"
+
+using namespace rf;
+
+namespace {
+
+constexpr char kMagic[8] = {'R', 'F', 'G', 'R', 'A', 'P', 'H', '1'};
+constexpr char kEnd[8] = {'R', 'F', 'G', 'R', 'E', 'N', 'D', '1'};
+constexpr uint32_t kVersion = 1;
+constexpr uint64_t kChunk = 64ull << 20;   // checksum granule
+constexpr uint64_t kStage = 256ull << 20;  // D2H / H2D staging (4 chunks)
+
+enum : uint32_t { kHoleInB0 = 1, kFusePos2 = 2, kHasMid = 4, kInitialized = 8 };
+
+struct Header {
+    char magic[8];
+    uint32_t version, flags;
+    uint32_t n_jobs, n_slots, n_levels, max_level_jobs;
+    uint64_t n_holes, tmpl_bytes, total_blocks, chunk;
+    uint64_t n_sections;
+    uint8_t reserved[128 - 8 - 6 * 4 - 5 * 8];
+};
+static_assert(sizeof(Header) == 128, "header layout");
+
+// One section of the file: host bytes, or a device buffer moved through the
+// pinned stage.
+struct Section {
+    const char* name;
+    uint64_t bytes;
+    void* host = nullptr;  // host memory (save: source; restore: destination)
+    void* dev = nullptr;   // device memory
+};
+
+std::vector<Section> sections(rf_graph* gr, std::vector<uint32_t>& lvl, std::vector<uint8_t>& inc,
+                              std::vector<uint32_t>& ext2int, bool has_mid) {
+    const GraphDev& G = gr->g;
+    const uint64_t J = G.n_jobs, S = G.n_slots, L = G.n_levels, H = gr->hole_count;
+    std::vector<Section> v = {
+        {"lvl_start", 4 * (L + 1), lvl.data()},
+        {"inc_level", L, inc.data()},
+        {"ext2int", 4 * J, ext2int.data()},
+        {"meta", 32 * J, nullptr, gr->b_meta.p},
+        {"holes", 8 * H, nullptr, gr->b_holes.p},
+        {"cons_ptr", 4 * (S + 1), nullptr, gr->b_cons_ptr.p},
+        {"cons_job", 8 * H, nullptr, gr->b_cons_job.p},
+        {"tmpl", gr->tmpl_bytes, nullptr, gr->b_tmpl.p},
+        {"slots", 32 * S, nullptr, gr->b_slots.p},
+    };
+    if (has_mid) v.push_back({"mid", 32 * J, nullptr, gr->b_mid.p});
+    return v;
+}
+
+// SHA-256 of each kChunk granule of buf[0, n) into out (in order), on the
+// host pool when there is one.
+void hash_chunks(rf_ctx* ctx, const uint8_t* buf, uint64_t n, uint8_t* out) {
+    const uint64_t nc = (n + kChunk - 1) / kChunk;
+    HostPool* pool = ctx_pool(ctx);
+    if (!pool || nc < 2) {
+        for (uint64_t c = 0; c < nc; ++c) host_sha256(buf + c * kChunk, std::min(kChunk, n - c * kChunk), out + 32 * c);
+        return;
+    }
+    std::atomic<uint64_t> next{0};
+    pool->run([&](unsigned) {
+        for (uint64_t c; (c = next.fetch_add(1)) < nc;)
+            host_sha256(buf + c * kChunk, std::min(kChunk, n - c * kChunk), out + 32 * c);
+    });
+}
+
+// Range checks of a piece [o, o + n) of a device section: every index a
+// kernel follows stays inside its array.  kStage keeps records whole.
+int check_piece(const char* name, const uint8_t* p, uint64_t n, uint64_t o, const Header& h) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+    const uint64_t J = h.n_jobs, S = h.n_slots, H = h.n_holes, TB = h.tmpl_bytes / 64;
+    if (!strcmp(name, "meta")) {
+        for (uint64_t r = 0; r < n / 32; ++r) {
+            const uint32_t* m = w + 8 * r;
+            if ((uint64_t)m[0] + m[1] > TB || m[2] > m[3] || m[3] > H || m[4] >= S || m[5] > m[6] || m[6] > H ||
+                (m[7] != 0xffffffffu && m[7] >= J))
+                return fail(RF_EINTEGRITY, "graph restore: job record %llu out of range",
+                            (unsigned long long)(o / 32 + r));
+        }
+    } else if (!strcmp(name, "holes")) {
+        for (uint64_t r = 0; r < n / 8; ++r)
+            if (w[2 * r + 1] >= S || w[2 * r] >= (1u << 24))
+                return fail(RF_EINTEGRITY, "graph restore: hole %llu out of range", (unsigned long long)(o / 8 + r));
+    } else if (!strcmp(name, "cons_ptr")) {
+        for (uint64_t r = 0; r < n / 4; ++r)
+            if (w[r] > H || (o + 4 * r > 0 && r > 0 && w[r] < w[r - 1]))
+                return fail(RF_EINTEGRITY, "graph restore: reverse-edge index out of range");
+    } else if (!strcmp(name, "cons_job")) {
+        for (uint64_t r = 0; r < n / 8; ++r)
+            if (w[2 * r] >= J || (w[2 * r + 1] & 0x7fffffffu) >= h.n_levels)
+                return fail(RF_EINTEGRITY, "graph restore: reverse edge %llu out of range",
+                            (unsigned long long)(o / 8 + r));
+    }
+    return RF_OK;
+}
+
+struct Stage {  // pinned staging, released on every path
+    HostBuf b;
+    ~Stage() { b.release(); }
+};
+
+struct File {
+    FILE* f = nullptr;
+    ~File() {
+        if (f) fclose(f);
+    }
+};
+
+}  // namespace
+
+extern "C" int rf_graph_save(rf_graph* gr, const char* path) {
+    ARG(gr && path && *path, "null argument");
+    rf_ctx* ctx = gr->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    // steps queued on callers' streams must be complete before the state is read
+    HIPC(hipDeviceSynchronize());
+    GraphDev& G = gr->g;
+    std::vector<uint32_t> lvl(G.lvl_start.begin(), G.lvl_start.end());
+    std::vector<uint8_t> inc(G.inc_level.begin(), G.inc_level.end());
+    std::vector<uint32_t> ext2int(gr->ext2int.begin(), gr->ext2int.end());
+    const bool has_mid = G.mid != nullptr;
+    std::vector<Section> secs = sections(gr, lvl, inc, ext2int, has_mid);
+    Header h{};
+    memcpy(h.magic, kMagic, 8);
+    h.version = kVersion;
+    h.flags = (G.hole_in_b0 ? kHoleInB0 : 0) | (G.fuse_pos2 ? kFusePos2 : 0) | (has_mid ? kHasMid : 0) |
+              (gr->initialized ? kInitialized : 0);
+    h.n_jobs = G.n_jobs;
+    h.n_slots = G.n_slots;
+    h.n_levels = G.n_levels;
+    h.max_level_jobs = gr->max_level_jobs;
+    h.n_holes = gr->hole_count;
+    h.tmpl_bytes = gr->tmpl_bytes;
+    h.total_blocks = gr->total_blocks;
+    h.chunk = kChunk;
+    h.n_sections = secs.size();
+    const std::string tmp = std::string(path) + ".tmp";
+    File out;
+    if (!(out.f = fopen(tmp.c_str(), "wb"))) return fail(RF_EIO, "graph save: cannot create %s", tmp.c_str());
+    auto put = [&](const void* p, uint64_t n) { return fwrite(p, 1, n, out.f) == n; };
+    if (!put(&h, sizeof h)) return fail(RF_EIO, "graph save: write failed");
+    Stage st;
+    HostBuf& stage = st.b;
+    HIPC(stage.ensure(kStage));
+    std::vector<uint8_t> digests;
+    for (const Section& sc : secs) {
+        if (!put(&sc.bytes, 8)) return fail(RF_EIO, "graph save: write failed");
+        for (uint64_t o = 0; o < sc.bytes; o += kStage) {
+            const uint64_t n = std::min(kStage, sc.bytes - o);
+            const uint8_t* src;
+            if (sc.dev) {
+                HIPC(sync_copy(ctx, stage.p, static_cast<const uint8_t*>(sc.dev) + o, n, hipMemcpyDeviceToHost));
+                src = stage.bytes();
+            } else {
+                src = static_cast<const uint8_t*>(sc.host) + o;
+            }
+            const size_t d0 = digests.size();
+            digests.resize(d0 + 32 * ((n + kChunk - 1) / kChunk));
+            hash_chunks(ctx, src, n, digests.data() + d0);
+            if (!put(src, n)) return fail(RF_EIO, "graph save: write failed (%s)", sc.name);
+        }
+    }
+    std::vector<uint8_t> all(sizeof h + digests.size());
+    memcpy(all.data(), &h, sizeof h);
+    if (!digests.empty()) memcpy(all.data() + sizeof h, digests.data(), digests.size());
+    uint8_t root[32];
+    host_sha256(all.data(), all.size(), root);
+    const uint64_t nd = digests.size() / 32;
+    if (!put(&nd, 8) || !put(digests.data(), digests.size()) || !put(root, 32) || !put(kEnd, 8))
+        return fail(RF_EIO, "graph save: write failed");
+    if (fflush(out.f) != 0 || fsync(fileno(out.f)) != 0) return fail(RF_EIO, "graph save: flush failed");
+    fclose(out.f);
+    out.f = nullptr;
+    if (rename(tmp.c_str(), path) != 0) return fail(RF_EIO, "graph save: cannot rename to %s", path);
+    return RF_OK;
+}
+
+extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
+    ARG(ctx && path && out, "null argument");
+    *out = nullptr;
+    File in;
+    if (!(in.f = fopen(path, "rb"))) return fail(RF_EIO, "graph restore: cannot open %s", path);
+    auto get = [&](void* p, uint64_t n) { return fread(p, 1, n, in.f) == n; };
+    Header h;
+    if (!get(&h, sizeof h) || memcmp(h.magic, kMagic, 8) != 0)
+        return fail(RF_EINVAL, "graph restore: %s is not a graph checkpoint", path);
+    if (h.version != kVersion || h.chunk != kChunk)
+        return fail(RF_EINVAL, "graph restore: checkpoint version %u not supported", h.version);
+    if (h.n_sections != ((h.flags & kHasMid) ? 10u : 9u) || h.n_jobs > (1u << 31) || h.n_levels > h.n_jobs + 1)
+        return fail(RF_EINTEGRITY, "graph restore: corrupt header");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    auto* gr = new rf_graph();
+    std::unique_ptr<rf_graph, void (*)(rf_graph*)> guard(gr, [](rf_graph* x) { rf_graph_destroy(x); });
+    gr->ctx = ctx;
+    gr->hole_count = h.n_holes;
+    gr->tmpl_bytes = h.tmpl_bytes;
+    gr->total_blocks = h.total_blocks;
+    gr->max_level_jobs = h.max_level_jobs;
+    GraphDev& G = gr->g;
+    G.hole_in_b0 = (h.flags & kHoleInB0) != 0;
+    G.fuse_pos2 = (h.flags & kFusePos2) != 0;
+    {
+        const char* v = getenv("RF_K2_STREAM");
+        G.stream_handover = v && atoi(v) == 1;
+    }
+    if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes)) return rc;
+    const bool has_mid = (h.flags & kHasMid) != 0;
+    if (has_mid) {
+        HIPC(gr->b_mid.ensure(std::max<size_t>(32ull * h.n_jobs, 64)));
+        G.mid = gr->b_mid.as<uint4>();
+    }
+    std::vector<uint32_t> lvl(h.n_levels + 1);
+    std::vector<uint8_t> inc(h.n_levels);
+    std::vector<uint32_t> ext2int(h.n_jobs);
+    std::vector<Section> secs = sections(gr, lvl, inc, ext2int, has_mid);
+    std::vector<uint32_t> out_slot(h.n_jobs);  // internal job -> out slot (from the records)
+    Stage st;
+    HostBuf& stage = st.b;
+    HIPC(stage.ensure(kStage));
+    std::vector<uint8_t> digests;
+    for (const Section& sc : secs) {
+        uint64_t n_sec = 0;
+        if (!get(&n_sec, 8) || n_sec != sc.bytes)
+            return fail(RF_EINTEGRITY, "graph restore: section %s truncated or resized", sc.name);
+        for (uint64_t o = 0; o < sc.bytes; o += kStage) {
+            const uint64_t n = std::min(kStage, sc.bytes - o);
+            uint8_t* dst = sc.dev ? stage.bytes() : static_cast<uint8_t*>(sc.host) + o;
+            if (!get(dst, n)) return fail(RF_EINTEGRITY, "graph restore: section %s truncated", sc.name);
+            const size_t d0 = digests.size();
+            digests.resize(d0 + 32 * ((n + kChunk - 1) / kChunk));
+            hash_chunks(ctx, dst, n, digests.data() + d0);
+            // the indices the kernels follow are range-checked as on load (a
+            // file with valid checksums may still come from anywhere)
+            if (int rc = check_piece(sc.name, dst, n, o, h)) return rc;
+            if (!strcmp(sc.name, "meta"))  // kStage is a multiple of the 32-B record
+                for (uint64_t r = 0; r < n / 32; ++r) memcpy(&out_slot[o / 32 + r], dst + 32 * r + 16, 4);
+            if (sc.dev) HIPC(sync_copy(ctx, static_cast<uint8_t*>(sc.dev) + o, dst, n, hipMemcpyHostToDevice));
+        }
+    }
+    uint64_t nd = 0;
+    uint8_t root[32], want[32], end[8];
+    if (!get(&nd, 8) || nd != digests.size() / 32) return fail(RF_EINTEGRITY, "graph restore: checksum list damaged");
+    std::vector<uint8_t> stored(32 * nd);
+    if (!get(stored.data(), stored.size()) || !get(want, 32) || !get(end, 8) || memcmp(end, kEnd, 8) != 0)
+        return fail(RF_EINTEGRITY, "graph restore: trailer truncated");
+    std::vector<uint8_t> all(sizeof h + stored.size());
+    memcpy(all.data(), &h, sizeof h);
+    if (!stored.empty()) memcpy(all.data() + sizeof h, stored.data(), stored.size());
+    host_sha256(all.data(), all.size(), root);
+    if (memcmp(root, want, 32) != 0 || stored != digests)
+        return fail(RF_EINTEGRITY, "graph restore: %s does not match its checksums", path);
+    // host-side state: level layout (and its device copy, which every level
+    // kernel reads), and slot -> producing (external) job
+    for (uint32_t l = 0; l < h.n_levels; ++l)
+        if (lvl[l] > lvl[l + 1] || lvl[l + 1] > h.n_jobs) return fail(RF_EINTEGRITY, "graph restore: bad level layout");
+    if (lvl[0] != 0 || lvl[h.n_levels] != h.n_jobs) return fail(RF_EINTEGRITY, "graph restore: bad level layout");
+    HIPC(sync_copy(ctx, gr->b_lvl_start.p, lvl.data(), 4ull * (h.n_levels + 1), hipMemcpyHostToDevice));
+    G.lvl_start.assign(lvl.begin(), lvl.end());
+    G.inc_level.assign(inc.begin(), inc.end());
+    gr->ext2int = std::move(ext2int);
+    gr->producer.assign(h.n_slots, -1);
+    for (uint32_t j = 0; j < h.n_jobs; ++j) {
+        const uint32_t i = gr->ext2int[j];
+        if (i >= h.n_jobs || out_slot[i] >= h.n_slots) return fail(RF_EINTEGRITY, "graph restore: bad job record");
+        gr->producer[out_slot[i]] = j;
+    }
+    gr->initialized = (h.flags & kInitialized) != 0;
+    guard.release();
+    *out = gr;
+    return RF_OK;
+}

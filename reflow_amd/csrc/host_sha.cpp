@@ -170,12 +170,57 @@ bool host_sha_available() {
 
 void host_sha_init(uint32_t st[8]) { memcpy(st, kIV, sizeof kIV); }
 
+// Portable compression for hosts without the SHA extensions (the host leg is
+// then off -- host_sha_available() -- but checkpoint checksums still need it).
+static inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+static void scalar_blocks(uint32_t st[8], const uint8_t* p, uint64_t nblocks) {
+    for (; nblocks--; p += 64) {
+        uint32_t w[64];
+        for (int t = 0; t < 16; ++t)
+            w[t] = (uint32_t)p[4 * t] << 24 | (uint32_t)p[4 * t + 1] << 16 | (uint32_t)p[4 * t + 2] << 8 | p[4 * t + 3];
+        for (int t = 16; t < 64; ++t) {
+            const uint32_t s0 = rotr(w[t - 15], 7) ^ rotr(w[t - 15], 18) ^ (w[t - 15] >> 3);
+            const uint32_t s1 = rotr(w[t - 2], 17) ^ rotr(w[t - 2], 19) ^ (w[t - 2] >> 10);
+            w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+        }
+        uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+        for (int t = 0; t < 64; ++t) {
+            const uint32_t t1 = h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + kK[t] + w[t];
+            const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            h = g;
+            g = f;
+            f = e;
+            e = d + t1;
+            d = c;
+            c = b;
+            b = a;
+            a = t1 + t2;
+        }
+        st[0] += a;
+        st[1] += b;
+        st[2] += c;
+        st[3] += d;
+        st[4] += e;
+        st[5] += f;
+        st[6] += g;
+        st[7] += h;
+    }
+}
+
 void host_sha_blocks(uint32_t st[8], const uint8_t* p, uint64_t nblocks) {
-    if (nblocks) ni_blocks(st, p, nblocks);
+    if (!nblocks) return;
+    if (host_sha_available())
+        ni_blocks(st, p, nblocks);
+    else
+        scalar_blocks(st, p, nblocks);
 }
 
 void host_sha_blocks_multi(int n, uint32_t* const* st, const uint8_t* const* p, uint64_t nblocks) {
     if (!nblocks) return;
+    if (!host_sha_available()) {
+        for (int i = 0; i < n; ++i) scalar_blocks(st[i], p[i], nblocks);
+        return;
+    }
     switch (n) {
         case 1: ni_blocks(st[0], p[0], nblocks); break;
         case 2: ni_multi<2>(st, p, nblocks); break;

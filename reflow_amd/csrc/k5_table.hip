@@ -120,10 +120,22 @@ uint32_t dedup_table_slots(uint32_t n) {
     return cap;
 }
 
+__global__ __launch_bounds__(256) void k5_fill_u32(uint32_t* __restrict__ p, uint32_t v, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
+hipError_t launch_fill_u32(uint32_t* p, uint32_t v, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    uint64_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(k5_fill_u32, dim3((uint32_t)(g > 16384 ? 16384 : g)), dim3(256), 0, s, p, v, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_dedup(const uint8_t* dig, uint32_t n, uint32_t* table, uint32_t* slot_of, uint32_t* canon,
-                        uint32_t* n_unique, hipStream_t s) {
+                        uint32_t* n_unique, hipStream_t s, bool clear_table) {
     const uint32_t cap = dedup_table_slots(n);
-    hipError_t e = hipMemsetAsync(table, 0xff, 4ull * cap, s);
+    hipError_t e = clear_table ? hipMemsetAsync(table, 0xff, 4ull * cap, s) : hipSuccess;
     if (e == hipSuccess) e = hipMemsetAsync(n_unique, 0, 4, s);
     if (e != hipSuccess || n == 0) return e;
     uint32_t grid = (n + 255) / 256;

@@ -1,0 +1,162 @@
+"""Checkpoint / resume of a loaded digest DAG (rf_graph_save,
+rf_graph_restore): a graph saved after a full recompute and an incremental
+step, destroyed, and restored in place of a fresh load gives -- after a
+further 1% change -- exactly the oracle's digests (the reference's resume is
+memoization: runner/runner.go:51-85 persists State per step,
+local/executor.go:122-200 restores execs from manifests).  Damaged files are
+refused: flipped bytes and truncation with RF_EINTEGRITY (errors.Integrity),
+a file that is not a checkpoint with RF_EINVAL, a missing one with RF_EIO."""
+import os
+
+import numpy as np
+import pytest
+
+import partition_case as PC
+import reflow_oracle as O
+from reflow_amd import capi
+from reflow_amd.workloads import Dag1000, PartitionedDag1000
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = capi.Context(0, host_threads=0)
+    yield c
+    c.close()
+
+
+def _load(ctx, dag):
+    g = capi.Graph.from_arrays(ctx, dag.arrays())
+    g.set_slots(dag.file_slots, dag.leaf_ids)
+    return g
+
+
+def test_save_restore_then_incremental_matches_oracle(ctx, tmp_path):
+    dag = Dag1000(12, 6)
+    a = dag.arrays()
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+    g = _load(ctx, dag)
+    g.recompute(full=True)
+    sa, _, na = dag.change_set(0.1, seed=1)
+    g.set_slots(sa, na)
+    g.recompute(full=False)
+    before = g.get_slots(every)
+    path = str(tmp_path / "g.ckpt")
+    g.save(path)
+    g.close()
+    r = capi.Graph.restore(ctx, path)
+    assert (r.get_slots(every) == before).all()
+    st = r.stats()
+    assert st.n_jobs == len(a["out_slot"]) and st.n_slots == a["n_slots"]
+    # a second change on the restored graph, against the oracle from scratch
+    sb, _, nb = dag.change_set(0.1, seed=2)
+    nb = np.frombuffer(bytes(np.asarray(nb).tobytes()[::-1]), np.uint8).reshape(-1, 32)  # not SHA(old||v2)
+    r.set_slots(sb, nb)
+    n = r.recompute(full=False)
+    assert 0 < n < len(a["out_slot"])
+    og = O.OGraph(a)
+    og.set_inputs(dag.file_slots, dag.leaf_ids)
+    og.full()
+    og.update(sa, na)
+    og.update(sb, nb)
+    assert (r.get_slots(every) == og.slots[:a["n_slots"]]).all()
+    og.close()
+    # input slots stay inputs, job outputs stay refused
+    with pytest.raises(capi.RfError):
+        r.set_slots(np.array([a["out_slot"][0]], np.uint32), np.zeros((1, 32), np.uint8))
+    r.close()
+
+
+def test_restore_equals_fresh_load_large(ctx, tmp_path):
+    """~0.9M nodes: restored + 1% change == fresh load + full recompute of the
+    same inputs, slot for slot."""
+    dag = Dag1000(2000, 32)
+    every = np.arange(dag.n_slots, dtype=np.uint32)
+    g = _load(ctx, dag)
+    g.recompute(full=True)
+    path = str(tmp_path / "big.ckpt")
+    g.save(path)
+    g.close()
+    r = capi.Graph.restore(ctx, path)
+    sl, _, nw = dag.change_set(0.01)
+    r.set_slots(sl, nw)
+    r.recompute(full=False)
+    f = _load(ctx, dag)
+    f.set_slots(sl, nw)
+    f.recompute(full=True)
+    assert (r.get_slots(every) == f.get_slots(every)).all()
+    r.close()
+    f.close()
+
+
+def test_damaged_checkpoints_refused(ctx, tmp_path):
+    dag = Dag1000(3, 4)
+    g = _load(ctx, dag)
+    g.recompute(full=True)
+    path = str(tmp_path / "d.ckpt")
+    g.save(path)
+    g.close()
+    raw = open(path, "rb").read()
+    assert not os.path.exists(path + ".tmp")
+
+    def refused(data, code):
+        p = str(tmp_path / "x.ckpt")
+        open(p, "wb").write(data)
+        with pytest.raises(capi.RfError) as e:
+            capi.Graph.restore(ctx, p)
+        assert e.value.code == code, e.value
+
+    for pos in (200, len(raw) // 2, len(raw) - 50):  # a section byte, the middle, the checksum list
+        bad = bytearray(raw)
+        bad[pos] ^= 0x40
+        refused(bytes(bad), capi.RF_EINTEGRITY)
+    refused(raw[:len(raw) // 3], capi.RF_EINTEGRITY)
+    refused(raw[:-1], capi.RF_EINTEGRITY)
+    refused(b"not a checkpoint" * 20, capi.RF_EINVAL)
+    with pytest.raises(capi.RfError) as e:
+        capi.Graph.restore(ctx, str(tmp_path / "missing.ckpt"))
+    assert e.value.code == capi.RF_EIO
+    # the intact file still restores
+    open(str(tmp_path / "ok.ckpt"), "wb").write(raw)
+    capi.Graph.restore(ctx, str(tmp_path / "ok.ckpt")).close()
+
+
+def test_restored_pieces_resume_partitioned(tmp_path):
+    """Two ranks (threads, one GPU) save their pieces of configs[3]'s layout,
+    restore them, re-attach the partition and take an incremental step
+    across ranks: the slots equal the oracle's single-rank evaluation."""
+    S, P, nr = 8, 4, 2
+    G, ga, owner, roots, trees, groot = PC.global_c4(S, P, nr, fanin=4)
+    rng = np.random.default_rng(4)
+    pick = np.sort(rng.choice(len(G.file_slots), size=9, replace=False))
+    new = G.leaf_ids.copy()
+    new[pick] = rng.integers(0, 256, size=(len(pick), 32), dtype=np.uint8)
+    want = PC.global_digests(G, ga, new)
+
+    def body(r, ag):
+        pc = PartitionedDag1000(S, P, nr, r, fanin=4)
+        m = PC.c4_local_to_global(pc, G, roots, trees, groot)
+        c = capi.Context(0, host_threads=0)
+        try:
+            g = capi.Graph.from_arrays(c, pc.desc)
+            g.set_part(pc.part)
+            g.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
+            g.recompute_part(allgather=ag, nranks=nr, full=True)
+            path = str(tmp_path / ("piece%d.ckpt" % r))
+            g.save(path)
+            g.close()
+            g = capi.Graph.restore(c, path)
+            g.set_part(pc.part)
+            f0 = 2 * pc.dag.Q * r
+            mine = pick[(pick >= f0) & (pick < f0 + 2 * pc.dag.Q)]
+            if len(mine):
+                g.set_slots(pc.dag.file_slots[mine - f0], new[mine])
+            g.recompute_part(allgather=ag, nranks=nr)
+            ok = bool((g.get_slots(np.arange(len(m), dtype=np.uint32)) == want[m]).all())
+            g.close()
+            return ok
+        finally:
+            c.close()
+
+    assert all(PC.run_threads(nr, body))
