@@ -471,6 +471,36 @@ def bench_c1_install(ctx, arena, offs, want_fsd, cpu_leg=False):
     return res
 
 
+# ---------------------------------------------------------- lowering leg --
+def bench_lowering(args):
+    """The per-Eval host cost a Go shim pays before the device sees a job:
+    tools/lower_bench (the product's C++ host mirror, include/reflow_host.hpp)
+    builds a configs[2]-sized 1000align Flow graph, Canonicalizes it, lowers
+    it to rf_graph jobs, loads it, and takes one 1%-of-files incremental step
+    (checked against a full recompute)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "lower_bench")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/lower_bench not built"}
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run([exe, str(args.dag_samples), str(args.dag_pairs)], capture_output=True, text=True,
+                           timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 300 s"}
+    wall = time.perf_counter() - t0
+    if r.returncode != 0 or not r.stdout.strip():
+        return {"error": "rc %d: %s" % (r.returncode, (r.stderr or "")[-300:])}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res["wall_s"] = round(wall, 2)
+    res["what"] = ("tools/lower_bench: reflow::Canonicalize + Eval lowering (reflow_host.cpp) of a 1000align "
+                   "Flow graph of the configs[2] shape; load = blob + rf_graph_load + full recompute")
+    log("lowering: %d nodes: build %.1f s, canonicalize %.1f s, lower %.1f s, load %.1f s, incremental %.1f ms"
+        % (res["nodes"], res["build_s"], res["canonicalize_s"], res["lower_s"], res["load_s"],
+           res["incremental_s"] * 1e3))
+    return res
+
+
 # ------------------------------------------------------- C3: incremental --
 def bench_dag(args, dist, ctx, budget):
     """configs[2] (N = 1): one 10M-node 1000align DAG, 1% of leaf File IDs
@@ -1097,12 +1127,17 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
     ap.add_argument("--gpu-only-run", type=int, default=1, help="one GPU-only run (duo roofline)")
     ap.add_argument("--budget-s", type=float, default=420.0)
-    ap.add_argument("--skip", default="", help="comma list of: c1,install,dag,dag100m,checkpoint,probe,cpu")
+    ap.add_argument("--skip", default="", help="comma list of: lower,c1,install,dag,dag100m,checkpoint,probe,cpu")
     args = ap.parse_args()
     args.skip = set(filter(None, args.skip.split(",")))
     budget = Budget(args.budget_s)
 
     dist = Dist(args.gpus)
+    # the product lowering leg runs first, in a child process of its own,
+    # before this process touches the GPU (N = 1 only)
+    lowering = None
+    if dist.world == 1 and "lower" not in args.skip:
+        lowering = bench_lowering(args)
     device = dist.local
     share = os.environ.get("RF_BENCH_SHARE_GPU") == "1"
     if share:  # rehearsal of the N-rank path on a box with fewer GPUs (never the driver's run)
@@ -1201,6 +1236,7 @@ def main():
             "c1": c1,
             "incremental": dag_res,
             "incremental_100m": dag100,
+            "lowering": lowering,
             "probe": probe,
             "budget": {"seconds": args.budget_s, "skipped": budget.skipped,
                        "elapsed_s": round(time.perf_counter() - T_START, 1)},

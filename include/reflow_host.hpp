@@ -55,13 +55,102 @@ struct Digest {
 };
 struct DigestHash {
     size_t operator()(const Digest& d) const {
-        size_t h;
-        memcpy(&h, d.b.data(), sizeof h);
-        return h;
+        uint64_t w[4];
+        memcpy(w, d.b.data(), sizeof w);
+        uint64_t h = (w[0] ^ (w[1] << 17 | w[1] >> 47) ^ (w[2] << 31 | w[2] >> 33) ^ (w[3] << 47 | w[3] >> 17));
+        h ^= h >> 32;
+        h *= 0x9E3779B97F4A7C15ull;
+        return (size_t)(h ^ (h >> 29));
     }
 };
 // digest.WriteDigest: big-endian uint16(crypto.SHA256 = 5) then the 32 bytes.
 void WriteDigest(std::string& w, const Digest& d);
+
+namespace detail {
+// Open-addressing hash map (linear probing, backward-shift erase) for the
+// lowering's hot lookups -- Flow pointers and File IDs, tens of millions of
+// them per Eval: one probe run per lookup instead of a node-based map's
+// allocation and pointer chase.
+template <class K, class V, class Hash, class Eq = std::equal_to<K>>
+class FlatMap {
+   public:
+    size_t size() const { return n_; }
+    void reserve(size_t n) {
+        size_t cap = 16;
+        while (cap < 2 * n) cap <<= 1;
+        if (cap > slots_.size()) rehash(cap);
+    }
+    V* find(const K& k) {
+        if (slots_.empty()) return nullptr;
+        for (size_t i = Hash{}(k) & mask_;; i = (i + 1) & mask_) {
+            Slot& s = slots_[i];
+            if (!s.used) return nullptr;
+            if (Eq{}(s.k, k)) return &s.v;
+        }
+    }
+    const V* find(const K& k) const { return const_cast<FlatMap*>(this)->find(k); }
+    // k must be absent
+    V& insert(const K& k, V v) {
+        if (2 * (n_ + 1) > slots_.size()) rehash(slots_.empty() ? 16 : 2 * slots_.size());
+        size_t i = Hash{}(k) & mask_;
+        while (slots_[i].used) i = (i + 1) & mask_;
+        slots_[i] = Slot{k, std::move(v), true};
+        ++n_;
+        return slots_[i].v;
+    }
+    bool erase(const K& k) {
+        if (slots_.empty()) return false;
+        size_t i = Hash{}(k) & mask_;
+        for (;; i = (i + 1) & mask_) {
+            if (!slots_[i].used) return false;
+            if (Eq{}(slots_[i].k, k)) break;
+        }
+        // backward shift: move later members of the run into the hole
+        for (size_t j = (i + 1) & mask_;; j = (j + 1) & mask_) {
+            if (!slots_[j].used) break;
+            const size_t h = Hash{}(slots_[j].k) & mask_;
+            if (((j - h) & mask_) >= ((j - i) & mask_)) {
+                slots_[i] = std::move(slots_[j]);
+                i = j;
+            }
+        }
+        slots_[i].used = false;
+        --n_;
+        return true;
+    }
+    template <class F>
+    void for_each(F f) const {
+        for (const Slot& s : slots_)
+            if (s.used) f(s.k, s.v);
+    }
+
+   private:
+    struct Slot {
+        K k{};
+        V v{};
+        bool used = false;
+    };
+    void rehash(size_t cap) {
+        std::vector<Slot> old(cap);
+        old.swap(slots_);
+        mask_ = cap - 1;
+        n_ = 0;
+        for (Slot& s : old)
+            if (s.used) insert(s.k, std::move(s.v));
+    }
+    std::vector<Slot> slots_;
+    size_t mask_ = 0, n_ = 0;
+};
+struct PtrHash {
+    size_t operator()(const void* p) const {
+        uint64_t x = (uint64_t)(uintptr_t)p;
+        x ^= x >> 33;
+        x *= 0xff51afd7ed558ccdull;
+        x ^= x >> 33;
+        return (size_t)x;
+    }
+};
+}  // namespace detail
 
 // ---- engine (one rf_ctx per GPU) -------------------------------------------
 class Engine {
@@ -211,28 +300,36 @@ class Eval {
     // Change one File ID wherever Fileset values reference it (needs file_slots).
     void SetFileID(const Digest& old_id, const Digest& new_id);
     uint64_t Recompute(bool full = false);
-    size_t Jobs() const { return jobs_.size(); }
+    size_t Jobs() const { return out_slot_.size(); }
 
    private:
-    struct Job {
-        std::string tmpl;
-        std::vector<std::pair<uint32_t, uint32_t>> holes;  // (byte pos, slot)
-        uint32_t out;
+    using Holes = std::vector<std::pair<uint32_t, uint32_t>>;  // (byte pos, slot)
+    // a job's material is built in the scratch of its recursion depth (a
+    // dep's job is lowered while its consumer's material is being written),
+    // then appended to the graph's arrays: no allocation per job
+    struct Scratch {
+        std::string t;
+        Holes h;
     };
-    void material(const Flow* f, std::string& out, std::vector<std::pair<uint32_t, uint32_t>>& holes);
-    void fileset_material(const Fileset& v, std::string& out,
-                          std::vector<std::pair<uint32_t, uint32_t>>& holes);
+    void material(const Flow* f, std::string& out, Holes& holes);
+    void fileset_material(const Fileset& v, std::string& out, Holes& holes);
     uint32_t lower(const Flow* f);
     void lower_physical(const Flow* f);
+    void commit(const Scratch& sc, uint32_t out);
     uint32_t new_slot() { return n_slots_++; }
 
     Engine& e_;
     std::string U_;
     bool file_slots_;
     uint32_t n_slots_ = 0;
-    std::vector<Job> jobs_;
-    std::unordered_map<const Flow*, uint32_t> logical_, physical_, job_of_;
-    std::unordered_map<Digest, uint32_t, DigestHash> file_slot_;
+    // the jobs, as the rf_graph_desc arrays
+    std::vector<uint32_t> out_slot_, tmpl_len_, hole_pos_, hole_slot_;
+    std::vector<uint64_t> tmpl_off_, hole_ptr_{0};
+    std::string blob_;
+    std::deque<Scratch> scratch_;  // deque: growing it keeps the outer depths' references valid
+    uint32_t depth_ = 0;
+    detail::FlatMap<const Flow*, uint32_t, detail::PtrHash> logical_, physical_;
+    detail::FlatMap<Digest, uint32_t, DigestHash> file_slot_;
     rf_graph* g_ = nullptr;
     mutable std::vector<uint8_t> cache_;  // all slots after the last recompute
     mutable bool cache_ok_ = false;

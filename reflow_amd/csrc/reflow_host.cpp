@@ -305,8 +305,7 @@ Eval::~Eval() {
     if (g_) rf_graph_destroy(g_);
 }
 
-void Eval::fileset_material(const Fileset& v, std::string& out,
-                            std::vector<std::pair<uint32_t, uint32_t>>& holes) {
+void Eval::fileset_material(const Fileset& v, std::string& out, Holes& holes) {
     if (v.List) {
         for (const Fileset& c : *v.List) fileset_material(c, out, holes);
         return;
@@ -314,13 +313,12 @@ void Eval::fileset_material(const Fileset& v, std::string& out,
     for (const auto& [path, file] : v.Map) {
         out += path;
         if (file_slots_) {
-            auto it = file_slot_.find(file.ID);
             uint32_t s;
-            if (it == file_slot_.end()) {
-                s = new_slot();
-                file_slot_.emplace(file.ID, s);
+            if (const uint32_t* p = file_slot_.find(file.ID)) {
+                s = *p;
             } else {
-                s = it->second;
+                s = new_slot();
+                file_slot_.insert(file.ID, s);
             }
             out.push_back('\0');
             out.push_back('\5');
@@ -337,7 +335,7 @@ void Eval::fileset_material(const Fileset& v, std::string& out,
 // 692-697); an inlined dep follows its own config in turn, and so does a
 // Parent (Canonicalize merges the config into the copies it makes, never
 // into f.Parent: flow.go:818-843).
-void Eval::material(const Flow* f, std::string& out, std::vector<std::pair<uint32_t, uint32_t>>& holes) {
+void Eval::material(const Flow* f, std::string& out, Holes& holes) {
     out += U_;
     if (f->op == OpRequirements) {
         material(f->Deps.at(0), out, holes);
@@ -385,44 +383,70 @@ void Eval::material(const Flow* f, std::string& out, std::vector<std::pair<uint3
     }
 }
 
+void Eval::commit(const Scratch& sc, uint32_t out) {
+    out_slot_.push_back(out);
+    tmpl_off_.push_back(blob_.size());
+    tmpl_len_.push_back((uint32_t)sc.t.size());
+    blob_ += sc.t;
+    for (const auto& [pos, slot] : sc.h) {
+        hole_pos_.push_back(pos);
+        hole_slot_.push_back(slot);
+    }
+    hole_ptr_.push_back(hole_pos_.size());
+}
+
 uint32_t Eval::lower(const Flow* f) {
-    auto it = logical_.find(f);
-    if (it != logical_.end()) return it->second;
-    Job j;
-    material(f, j.tmpl, j.holes);
-    j.out = new_slot();
-    logical_[f] = j.out;
-    jobs_.push_back(std::move(j));
-    return logical_[f];
+    if (const uint32_t* s = logical_.find(f)) return *s;
+    if (scratch_.size() <= depth_) scratch_.resize(depth_ + 1);
+    Scratch& sc = scratch_[depth_];
+    sc.t.clear();
+    sc.h.clear();
+    ++depth_;
+    try {
+        material(f, sc.t, sc.h);
+    } catch (...) {
+        --depth_;
+        throw;
+    }
+    --depth_;
+    // (a dep lowered inside material() may have grown scratch_: re-index)
+    const uint32_t out = new_slot();
+    logical_.insert(f, out);
+    commit(scratch_[depth_], out);
+    return out;
 }
 
 // Flow.PhysicalDigest (flow.go:764-792): no Universe, no op name, no WD.
 void Eval::lower_physical(const Flow* f) {
     if (f->op != OpExec && f->op != OpExtern) return;
-    if (physical_.count(f)) return;
+    if (physical_.find(f)) return;
     for (const Flow* d : f->Deps)
         if (!d->Done) return;
-    Job j;
+    if (scratch_.size() <= depth_) scratch_.resize(depth_ + 1);
+    Scratch& sc = scratch_[depth_];
+    sc.t.clear();
+    sc.h.clear();
     for (const Flow* d : f->Deps) {
         if (!d->Value) throw Error(RF_EINVAL, "done dependency without a Fileset value");
-        fileset_material(*d->Value, j.tmpl, j.holes);
+        fileset_material(*d->Value, sc.t, sc.h);
     }
     if (f->op == OpExtern)
-        j.tmpl += f->URL;
+        sc.t += f->URL;
     else
-        exec_suffix(f, j.tmpl);
-    j.out = new_slot();
-    physical_[f] = j.out;
-    jobs_.push_back(std::move(j));
+        exec_suffix(f, sc.t);
+    const uint32_t out = new_slot();
+    physical_.insert(f, out);
+    commit(sc, out);
 }
 
 void Eval::Add(Flow* root) {
     std::vector<const Flow*> stack{root};
-    std::unordered_set<const Flow*> seen;
+    detail::FlatMap<const Flow*, char, detail::PtrHash> seen;
     while (!stack.empty()) {
         const Flow* f = stack.back();
         stack.pop_back();
-        if (!f || !seen.insert(f).second) continue;
+        if (!f || seen.find(f)) continue;
+        seen.insert(f, 1);
         lower(f);
         lower_physical(f);
         for (const Flow* d : f->Deps) stack.push_back(d);
@@ -432,42 +456,29 @@ void Eval::Add(Flow* root) {
 }
 
 void Eval::Build() {
-    const uint32_t J = (uint32_t)jobs_.size();
-    std::vector<uint32_t> out_slot(J), tmpl_len(J), hole_pos, hole_slot;
-    std::vector<uint64_t> tmpl_off(J), hole_ptr(J + 1, 0);
-    std::string blob;
-    for (uint32_t i = 0; i < J; ++i) {
-        const Job& j = jobs_[i];
-        out_slot[i] = j.out;
-        tmpl_off[i] = blob.size();
-        tmpl_len[i] = (uint32_t)j.tmpl.size();
-        blob += j.tmpl;
-        for (auto [pos, slot] : j.holes) {
-            hole_pos.push_back(pos);
-            hole_slot.push_back(slot);
-        }
-        hole_ptr[i + 1] = hole_pos.size();
-    }
+    const uint32_t J = (uint32_t)out_slot_.size();
     rf_graph_desc d{J,
                     n_slots_,
-                    out_slot.data(),
-                    tmpl_off.data(),
-                    tmpl_len.data(),
-                    hole_ptr.data(),
-                    hole_pos.data(),
-                    hole_slot.data(),
-                    reinterpret_cast<const uint8_t*>(blob.data()),
-                    blob.size()};
+                    out_slot_.data(),
+                    tmpl_off_.data(),
+                    tmpl_len_.data(),
+                    hole_ptr_.data(),
+                    hole_pos_.empty() ? nullptr : hole_pos_.data(),
+                    hole_slot_.empty() ? nullptr : hole_slot_.data(),
+                    reinterpret_cast<const uint8_t*>(blob_.data()),
+                    blob_.size()};
     if (g_) rf_graph_destroy(g_);
     g_ = nullptr;
     Check(rf_graph_load(e_.ctx(), &d, &g_));
-    if (!file_slot_.empty()) {
+    if (file_slot_.size()) {
         std::vector<uint32_t> s;
         std::vector<uint8_t> ids;
-        for (const auto& [id, slot] : file_slot_) {
+        s.reserve(file_slot_.size());
+        ids.reserve(32 * file_slot_.size());
+        file_slot_.for_each([&](const Digest& id, uint32_t slot) {
             s.push_back(slot);
             ids.insert(ids.end(), id.b.begin(), id.b.end());
-        }
+        });
         Check(rf_graph_set_slots(g_, s.data(), ids.data(), (uint32_t)s.size()));
     }
     Recompute(true);
@@ -491,17 +502,19 @@ void Eval::fetch() const {
 
 Digest Eval::FlowDigest(const Flow* f) const {
     fetch();
+    const uint32_t* s = logical_.find(f);
+    if (!s) throw Error(RF_ENOTFOUND, "flow not in this Eval");
     Digest d;
-    memcpy(d.b.data(), cache_.data() + 32ull * logical_.at(f), 32);
+    memcpy(d.b.data(), cache_.data() + 32ull * *s, 32);
     return d;
 }
 
 std::optional<Digest> Eval::PhysicalDigest(const Flow* f) const {
-    auto it = physical_.find(f);
-    if (it == physical_.end()) return std::nullopt;
+    const uint32_t* s = physical_.find(f);
+    if (!s) return std::nullopt;
     fetch();
     Digest d;
-    memcpy(d.b.data(), cache_.data() + 32ull * it->second, 32);
+    memcpy(d.b.data(), cache_.data() + 32ull * *s, 32);
     return d;
 }
 
@@ -514,11 +527,14 @@ std::vector<Digest> Eval::CacheKeys(const Flow* f) const {
 }
 
 void Eval::SetFileID(const Digest& old_id, const Digest& new_id) {
-    auto it = file_slot_.find(old_id);
-    if (it == file_slot_.end()) throw Error(RF_ENOTFOUND, "file id not referenced: " + old_id.String());
-    const uint32_t s = it->second;
-    file_slot_.erase(it);
-    file_slot_[new_id] = s;
+    const uint32_t* p = file_slot_.find(old_id);
+    if (!p) throw Error(RF_ENOTFOUND, "file id not referenced: " + old_id.String());
+    const uint32_t s = *p;
+    file_slot_.erase(old_id);
+    if (uint32_t* q = file_slot_.find(new_id))
+        *q = s;  // (an ID already in use elsewhere: the map keeps the last slot, as before)
+    else
+        file_slot_.insert(new_id, s);
     Check(rf_graph_set_slots(g_, &s, new_id.b.data(), 1));
 }
 
@@ -526,21 +542,35 @@ void Eval::SetFileID(const Digest& old_id, const Digest& new_id) {
 Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const std::string& U) {
     // 1. one copy per original node, config merged, deps (and MapFlow) pointing
     //    at copies -- the f.Copy()/Config.Merge/recursion of flow.go:820-839.
-    std::unordered_map<const Flow*, Flow*> copy;
+    //    Iterative post-order (a node is copied when its deps are).
+    detail::FlatMap<const Flow*, Flow*, detail::PtrHash> copy;
     std::vector<Flow*> post;  // copies in post-order (the order of m.Put)
-    std::function<Flow*(Flow*)> rec = [&](Flow* f) -> Flow* {
-        auto it = copy.find(f);
-        if (it != copy.end()) return it->second;
+    struct Frame {
+        Flow* f;
+        size_t next;  // next dep (then MapFlow) to visit
+    };
+    std::vector<Frame> st{{root, 0}};
+    while (!st.empty()) {
+        Frame& fr = st.back();
+        Flow* f = fr.f;
+        const size_t nd = f->Deps.size() + (f->MapFlow ? 1 : 0);
+        if (fr.next < nd) {
+            Flow* d = fr.next < f->Deps.size() ? f->Deps[fr.next] : f->MapFlow;
+            ++fr.next;
+            if (!copy.find(d)) st.push_back(Frame{d, 0});
+            continue;
+        }
+        st.pop_back();
+        if (copy.find(f)) continue;  // reached twice before its first copy completed
         Flow c = *f;
         c.config.Merge(config);
         Flow* cp = arena.New(std::move(c));
-        copy[f] = cp;
-        for (Flow*& d : cp->Deps) d = rec(d);
-        if (cp->MapFlow) cp->MapFlow = rec(cp->MapFlow);
+        for (Flow*& d : cp->Deps) d = *copy.find(d);
+        if (cp->MapFlow) cp->MapFlow = *copy.find(cp->MapFlow);
+        copy.insert(f, cp);
         post.push_back(cp);
-        return cp;
-    };
-    Flow* croot = rec(root);
+    }
+    Flow* croot = *copy.find(root);
     // 2. digests of every copy on the device
     Eval ev(e, U);
     ev.Add(croot);
@@ -557,13 +587,15 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
     uint32_t n_unique = 0;
     if (!post.empty())
         Check(rf_dedup_digests(e.ctx(), digs.data(), (uint32_t)post.size(), first.data(), &n_unique));
-    std::unordered_map<Flow*, Flow*> canon;
-    for (size_t i = 0; i < post.size(); ++i) canon[post[i]] = post[first[i]];
+    detail::FlatMap<const Flow*, uint32_t, detail::PtrHash> index;
+    index.reserve(post.size());
+    for (size_t i = 0; i < post.size(); ++i) index.insert(post[i], (uint32_t)i);
+    auto canon = [&](Flow* c) { return post[first[*index.find(c)]]; };
     for (Flow* c : post) {
-        for (Flow*& d : c->Deps) d = canon[d];
-        if (c->MapFlow) c->MapFlow = canon[c->MapFlow];
+        for (Flow*& d : c->Deps) d = canon(d);
+        if (c->MapFlow) c->MapFlow = canon(c->MapFlow);
     }
-    return canon[croot];
+    return canon(croot);
 }
 
 // ---- Liveset ---------------------------------------------------------------------

@@ -20,6 +20,7 @@
 
 #include <random>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "reflow_hip.h"
@@ -374,7 +375,41 @@ static void test_host_mirror() {
     EXPECT(!w.empty() && top.N() == 1);
 }
 
+// the lowering's open-addressing map against std::unordered_map: random
+// inserts / finds / erases (backward-shift deletion keeps every probe run
+// intact), keys crowded into a few home slots as well as spread
+static void test_flat_map() {
+    struct Crowd {  // 8 home slots for every key: long runs, wrap-around
+        size_t operator()(uint64_t k) const { return (size_t)(k & 7) * 0x1000001ull; }
+    };
+    for (int crowd = 0; crowd < 2; ++crowd) {
+        reflow::detail::FlatMap<uint64_t, uint32_t, std::hash<uint64_t>> a;
+        reflow::detail::FlatMap<uint64_t, uint32_t, Crowd> b;
+        std::unordered_map<uint64_t, uint32_t> ref;
+        uint64_t x = 12345;
+        for (int op = 0; op < 200000; ++op) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            const uint64_t k = (x >> 33) % (crowd ? 300 : 5000);
+            const int what = (int)((x >> 20) % 3);
+            auto it = ref.find(k);
+            if (what == 0 && it == ref.end()) {
+                ref[k] = (uint32_t)op;
+                if (crowd) b.insert(k, (uint32_t)op); else a.insert(k, (uint32_t)op);
+            } else if (what == 1 && it != ref.end()) {
+                ref.erase(it);
+                EXPECT(crowd ? b.erase(k) : a.erase(k));
+            } else {
+                const uint32_t* v = crowd ? b.find(k) : a.find(k);
+                EXPECT((v != nullptr) == (it != ref.end()));
+                if (v && it != ref.end()) EXPECT(*v == it->second);
+            }
+        }
+        EXPECT((crowd ? b.size() : a.size()) == ref.size());
+    }
+}
+
 int main() {
+    test_flat_map();
     test_fileset_json();
     test_bloom_wire();
     test_graph_split();
