@@ -302,7 +302,10 @@ def bench_sha(args, dist, ctx, budget):
     # (the chain-bound largest files on SHA-NI threads), priced against its
     # own peak -- threads x one thread's measured rate at the configured
     # chain interleave on this box; the GPU kernels' rooflines sit beside it
-    if h and thread_rate and host_ms >= max([ms for _, _, ms in legs] or [0.0]):
+    gpu_b = float(lens[np.concatenate([solo_ids, lane_ids])].sum()) if len(lane_ids) + k else 0.0
+    # the planner balances the legs' times (the duo leg ends within ~2 % of
+    # the host leg), so "dominant" is by bytes: the host leg's 98 %
+    if h and thread_rate and hb >= gpu_b:
         ach = hb / (host_ms * 1e-3) / 1e9
         peak = st.host_threads * thread_rate / 1e9
         roof = {"bound": "host SHA-NI issue", "leg": "host_leg", "achieved": round(ach, 3), "peak": round(peak, 3),
@@ -312,11 +315,12 @@ def bench_sha(args, dist, ctx, budget):
                 "peak_kind": "host-leg threads x one thread's measured SHA-NI rate with %d interleaved chains "
                              "(rf_host_rate, this box)" % ways,
                 "leg_ms": round(host_ms, 2), "step_ms": round(step_ms, 2), "bytes": hb,
-                "threads": int(st.host_threads)}
+                "bytes_frac": round(hb / max(hb + gpu_b, 1.0), 4), "threads": int(st.host_threads),
+                "gpu_legs_ms": {name: round(ms, 2) for name, _, ms in legs}}
     else:
         dom = max(zip(gpu_roofs, legs), key=lambda x: x[1][2])[0] if legs else None
         roof = dom
-    gpu_bytes = float(lens[np.concatenate([solo_ids, lane_ids])].sum()) if len(lane_ids) + k else 0.0
+    gpu_bytes = gpu_b
     composition = {"host_leg_bytes": hb, "gpu_bytes": gpu_bytes,
                    "host_leg_bytes_frac": round(hb / max(hb + gpu_bytes, 1.0), 4),
                    "gpu_legs_gbps": round(gpu_bytes / (max([ms for _, _, ms in legs] or [1e-9]) * 1e-3) / 1e9, 3)
@@ -625,7 +629,7 @@ def bench_dag100m(args, dist, ctx, comm, budget):
     got_jobs = recompute(False)
     g.set_slots(slots, old)
     recompute(False)
-    jobs_ok = dist.max(0.0 if got_jobs == jobs_l else 1.0) == 0.0
+    jobs_ok = dist.max(0.0 if got_jobs == jobs_l + pc.last_twice else 1.0) == 0.0
     state = {"v": 0}
 
     def step():
@@ -995,11 +999,12 @@ def cpu_threads():
 
 
 def cpu_baseline(args, sha, dag_res, budget):
-    """The headline's CPU leg: OpenSSL SHA-256 (hashlib; SHA-NI, what Go >= 1.21
-    crypto/sha256 uses) over the WHOLE configs[1] set on min(60, CPU share)
-    threads, LPT order; the oracle's scalar C port (~Go 1.9/1.10 speed class)
-    on a bounded sample; configs[0]; configs[2] on its own DAG and change set
-    (1 thread: Canonicalize is serial)."""
+    """The headline's CPU leg: the oracle's scalar C port (~Go 1.9/1.10 speed
+    class, kind "port") on a bounded sample of configs[1] -- the value; beside
+    it OpenSSL SHA-256 (hashlib; SHA-NI, what Go >= 1.21 crypto/sha256 uses)
+    over the WHOLE set on min(60, CPU share) threads, LPT order; configs[0];
+    configs[2] on its own DAG and change set (1 thread: Canonicalize is
+    serial)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import reflow_oracle as O  # the oracle: cpu_baseline leg only
     from concurrent.futures import ThreadPoolExecutor
@@ -1023,10 +1028,10 @@ def cpu_baseline(args, sha, dag_res, budget):
         dig = list(ex.map(one, order.tolist()))
     dt = time.perf_counter() - t0
     ok = all(d == sha["_digests"][int(i)].tobytes() for d, i in zip(dig, order))
-    res.update({"value": float(lens.sum()) / dt / 1e9, "unit": "GB/s", "kind": "library",
-                "what": "SHA-256 of every configs[1] file, hashlib/OpenSSL (SHA-NI), LPT order",
-                "sample": "the whole configs[1] set (%d files, %.1f GiB)" % (len(lens), lens.sum() / GiB),
-                "seconds": dt, "gpu_digests_match": ok})
+    res["openssl"] = {"value": float(lens.sum()) / dt / 1e9, "unit": "GB/s", "kind": "library", "cores": threads,
+                      "what": "SHA-256 of every configs[1] file, hashlib/OpenSSL (SHA-NI), LPT order",
+                      "sample": "the whole configs[1] set (%d files, %.1f GiB)" % (len(lens), lens.sum() / GiB),
+                      "seconds": dt, "gpu_digests_match": ok}
     # scalar port on a bounded sample (files in generation order up to the budget)
     budget_b = int(args.cpu_sample_gib * GiB)
     n = min(int(np.searchsorted(np.cumsum(lens.astype(np.int64)), budget_b)) + 1, len(lens))
@@ -1040,10 +1045,14 @@ def cpu_baseline(args, sha, dag_res, budget):
     dt = time.perf_counter() - t0
     back = np.empty_like(out)
     back[s_order.astype(np.int64)] = out
-    res["port"] = {"value": float(s_lens.sum()) / dt / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
-                   "sample": "first %d files (%.2f GiB, largest %.2f GiB) of configs[1], oracle/oracle.c scalar "
-                             "SHA-256, largest-first" % (n, s_lens.sum() / GiB, s_lens.max() / GiB),
-                   "seconds": dt, "gpu_digests_match": bool((back == sha["_digests"][:n]).all())}
+    # the cpu_baseline proper: the oracle's port (the reference is Go and
+    # cannot be built here) on a bounded sample of the same workload
+    res.update({"value": float(s_lens.sum()) / dt / 1e9, "unit": "GB/s", "kind": "port",
+                "what": "oracle/oracle.c scalar SHA-256 (the Go 1.9/1.10 speed class: no SHA-NI) on %d threads "
+                        "(min(60, CPU share): DigestLimiter), largest-first" % threads,
+                "sample": "first %d files (%.2f GiB, largest %.2f GiB) of configs[1]"
+                          % (n, s_lens.sum() / GiB, s_lens.max() / GiB),
+                "seconds": dt, "gpu_digests_match": bool((back == sha["_digests"][:n]).all())})
     del mv, host
     # configs[0]: port and OpenSSL
     c1l = np.full(C1_N, C1_LEN, dtype=np.uint64)

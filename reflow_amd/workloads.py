@@ -598,7 +598,9 @@ class PartitionedDag1000:
         pair its ten-node chain + the pE1 physical key, per changed sample its
         five-node tail, the Merge-tree ancestors, and (rank 0, when anything
         anywhere changed) the global root.  Blocks are the full materials'
-        (ceil((len + 9) / 64)), as the reference hashes them."""
+        (ceil((len + 9) / 64)), as the reference hashes them.  self.last_twice:
+        the jobs the partitioned recompute hashes twice (local pass, then
+        after the exchange) -- the device's count is jobs + last_twice."""
         d, a = self.dag, self.desc
         blk = {k: (len(kk.tmpl) + 9 + 63) // 64 for k, kk in d.kinds.items()}
         f = np.asarray(file_slots, dtype=np.int64)
@@ -618,10 +620,17 @@ class PartitionedDag1000:
         dirty = set(d.kinds["XS"].out_slot[samples].tolist())
         hp, hs, osl, tl = a["hole_ptr"], a["hole_slot"], a["out_slot"], a["tmpl_len"]
         imports = set(self.import_slot.tolist())
+        self.last_twice = 0
         for j in range(d.n_jobs, len(osl)):
             deps = hs[int(hp[j]):int(hp[j + 1])].tolist()
-            if any(x in dirty for x in deps) or (global_changed and any(x in imports for x in deps)):
+            local = any(x in dirty for x in deps)
+            imported = global_changed and any(x in imports for x in deps)
+            if local or imported:
                 dirty.add(int(osl[j]))
                 jobs += 1
                 blocks += (int(tl[j]) + 9 + 63) // 64
+                # rf_graph_recompute_part hashes a job that reads imports in the
+                # local pass (its local deps changed) and again after the
+                # exchange (its imports changed): jobs hashed = jobs + this
+                self.last_twice += int(local and imported)
         return jobs, jobs - len(pairs), blocks

@@ -131,3 +131,38 @@ def test_bench_layout_pieces_match_global_dag(nranks, S, P, fanin, protocol):
             assert supersteps == (2 if protocol == "rounds" or step != 3 else 1)
         # ranks > 0 have no imports: their second superstep launches nothing
         assert r == 0 or out[1][0] > 0
+
+
+@pytest.mark.parametrize("nranks,nparts", [(2, 4), (4, 4), (2, 2)])
+def test_strong_layout_counts_match_dirty_work(nranks, nparts):
+    """bench.py's strong layout (nparts fixed, nranks | nparts): each rank's
+    jobs hashed by an incremental step equal the layout's dirty closure
+    (PartitionedDag1000.dirty_work) plus the jobs hashed twice (rank 0's
+    global root: local pass, then after the exchange)."""
+    S, P = 12, 4
+    nf = 2 * P * S * nparts
+
+    def setup(r, ctx):
+        pc = PartitionedDag1000(S, P, nranks, r, fanin=4, nparts=nparts)
+        g = capi.Graph.from_arrays(ctx, pc.desc)
+        g.set_part(pc.part)
+        return g, pc
+
+    def body(r, ag):
+        ctx = capi.Context(0, host_threads=0)
+        try:
+            g, pc = setup(r, ctx)
+            g.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
+            g.recompute_part(allgather=ag, nranks=nranks, full=True)
+            sl, _, nw = pc.dag.change_set(0.05, n_global=nf)
+            if len(sl):
+                g.set_slots(sl, nw)
+            got = g.recompute_part(allgather=ag, nranks=nranks)
+            jobs, _, _ = pc.dirty_work(sl)
+            g.close()
+            return got, jobs + pc.last_twice
+        finally:
+            ctx.close()
+
+    for got, want in PC.run_threads(nranks, body):
+        assert got == want
