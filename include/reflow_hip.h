@@ -130,8 +130,11 @@ int rf_sha256_arena(rf_ctx *ctx, const uint8_t *arena, const uint64_t *offs, con
  * bytes streamed D2H in 8 MiB chunks), wave-per-message duo chains, and the
  * lane-per-message kernels; rf_sha_plan_run then digests messages already in
  * HBM.  The GPU legs are queued asynchronously on `stream`; with a host leg
- * the call returns once the host threads are done (their digests' upload and
- * scatter into out queued on `stream`).
+ * the call is SYNCHRONOUS: it returns once the host threads are done (their
+ * digests' upload and scatter into out queued on `stream`) -- ~1.3 s on
+ * configs[1].  The context's mutex is released while the host threads hash,
+ * so other calls on the context proceed meanwhile (calls that need the host
+ * leg themselves wait for it); one run of a given plan at a time.
  * Requirements: offs[i] % 16 == 0.  out is n*32 bytes of device memory. */
 int rf_sha_plan_create(rf_ctx *ctx, const uint64_t *offs, const uint64_t *lens, uint64_t n,
                        uint32_t flags, rf_sha_plan **out);

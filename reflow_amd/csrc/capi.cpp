@@ -97,7 +97,7 @@ extern "C" void rf_destroy(rf_ctx* ctx) {
     ctx->sc_dedup.destroy();
     ctx->sc_collect.destroy();
     rf_sha_plan_destroy(ctx->tplan);
-    delete ctx->pool;
+    ctx->pool.reset();
     if (ctx->t0) (void)hipEventDestroy(ctx->t0);
     if (ctx->t1) (void)hipEventDestroy(ctx->t1);
     (void)hipStreamDestroy(ctx->stream);
@@ -116,8 +116,7 @@ extern "C" int rf_set_host_threads(rf_ctx* ctx, int n) {
     ARG(n >= -1 && n <= 1024, "host threads must be -1 (default), 0 (none) or 1..1024");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->host_threads = n;
-    delete ctx->pool;
-    ctx->pool = nullptr;
+    ctx->pool.reset();  // a host leg running unlocked keeps its own reference
     return RF_OK;
 }
 
@@ -282,6 +281,7 @@ extern "C" int rf_comm_allreduce_or(rf_comm* c, void* d_words, uint64_t nwords, 
 // K1 planner
 struct rf_sha_plan {
     rf_ctx* ctx = nullptr;
+    std::mutex mu;  // one run of a plan at a time (its host leg runs without ctx->mu)
     uint64_t n = 0;
     uint32_t n_lanes = 0, n_solo = 0, n_host = 0, grid = 0, n_shards = 1;
     bool duo = true;  // wave-per-message kernel: two-lane chain (default) or one-lane
@@ -576,8 +576,11 @@ extern "C" int rf_sha_plan_create(rf_ctx* ctx, const uint64_t* offs, const uint6
 // host leg runs on the context's pool meanwhile and this call returns when
 // it is done, with the upload + scatter of its digests queued on s.  The
 // host leg reads h_arena (host memory) when given, else d_arena via D2H.
+// ctx_lock (rf_sha_plan_run): the context mutex, released while the host leg
+// hashes -- ~1.3 s on configs[1], during which other calls on the context
+// (graph steps, probes, assoc) proceed; the plan's own mutex is held.
 static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hipStream_t s,
-                           const uint8_t* h_arena = nullptr) {
+                           const uint8_t* h_arena = nullptr, std::unique_lock<std::mutex>* ctx_lock = nullptr) {
     HIPC(hipEventRecord(p->e0, s));
     const uint32_t* order = p->d_order.as<uint32_t>();
     if (p->n_lanes) HIPC(hipMemsetAsync(p->d_heads.p, 0, 4 * 64, s));
@@ -606,7 +609,7 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
     HIPC(hipEventRecord(p->e_lanes, s));
     p->last_ms_host = 0.f;
     if (p->n_host) {
-        HostPool* pool = ctx_pool(p->ctx);
+        std::shared_ptr<HostPool> pool = ctx_pool_ref(p->ctx);
         if (!pool) return fail(RF_EINVAL, "plan has a host leg but the context's host leg is off");
         if (p->hcopy_pending) {
             HIPC(hipEventSynchronize(p->e_hcopy));
@@ -617,9 +620,12 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
         if (!h_arena) HIPC(hipEventSynchronize(p->e0));
         const auto t0 = std::chrono::steady_clock::now();
         std::string err;
-        if (!host_leg_run(*pool, p->host.data(), p->n_host, h_arena ? nullptr : static_cast<const uint8_t*>(d_arena),
-                          h_arena, p->h_host_dig.bytes(), &err))
-            return fail(RF_EDEVICE, "%s", err.c_str());
+        if (ctx_lock) ctx_lock->unlock();
+        const bool ok = host_leg_run(*pool, p->host.data(), p->n_host,
+                                     h_arena ? nullptr : static_cast<const uint8_t*>(d_arena), h_arena,
+                                     p->h_host_dig.bytes(), &err);
+        if (ctx_lock) ctx_lock->lock();
+        if (!ok) return fail(RF_EDEVICE, "%s", err.c_str());
         p->last_ms_host = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         HIPC(hipMemcpyAsync(p->d_host_dig.p, p->h_host_dig.p, 32ull * p->n_host, hipMemcpyHostToDevice, s));
         HIPC(hipEventRecord(p->e_hcopy, s));
@@ -636,9 +642,10 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
 extern "C" int rf_sha_plan_run(rf_sha_plan* p, const void* d_arena, void* d_out32, void* stream) {
     ARG(p, "null plan");
     ARG(p->n == 0 || (d_arena && d_out32), "null device buffer");
-    std::lock_guard<std::mutex> lk(p->ctx->mu);
+    std::lock_guard<std::mutex> plk(p->mu);
+    std::unique_lock<std::mutex> lk(p->ctx->mu);
     DevGuard g(p->ctx->device);
-    return plan_run_locked(p, d_arena, d_out32, pick(p->ctx, stream));
+    return plan_run_locked(p, d_arena, d_out32, pick(p->ctx, stream), nullptr, &lk);
 }
 
 extern "C" int rf_sha_plan_stats(rf_sha_plan* p, rf_sha_stats* out) {

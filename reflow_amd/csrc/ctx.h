@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <string>
 
@@ -114,7 +115,9 @@ struct rf_ctx {
     hipEvent_t t0 = nullptr, t1 = nullptr;
     rf_sha_plan* tplan = nullptr;  // one-shot batches (transient_plan)
     int host_threads = -1;         // K1 host leg: -1 default width, 0 none
-    HostPool* pool = nullptr;      // created on first use
+    // created on first use; shared so a plan's host leg that runs with the
+    // context mutex released keeps its pool alive across rf_set_host_threads
+    std::shared_ptr<HostPool> pool;
     StreamScratch sc_dedup, sc_collect;
 };
 
@@ -124,16 +127,15 @@ inline unsigned ctx_host_threads(rf_ctx* ctx) {
     return ctx->host_threads < 0 ? host_default_threads() : (unsigned)ctx->host_threads;
 }
 
-inline HostPool* ctx_pool(rf_ctx* ctx) {
+// (caller holds ctx->mu)
+inline std::shared_ptr<HostPool> ctx_pool_ref(rf_ctx* ctx) {
     const unsigned n = ctx_host_threads(ctx);
     if (!n) return nullptr;
-    if (ctx->pool && ctx->pool->size() != n) {
-        delete ctx->pool;
-        ctx->pool = nullptr;
-    }
-    if (!ctx->pool) ctx->pool = new HostPool(ctx->device, n);
+    if (ctx->pool && ctx->pool->size() != n) ctx->pool.reset();
+    if (!ctx->pool) ctx->pool = std::make_shared<HostPool>(ctx->device, n);
     return ctx->pool;
 }
+inline HostPool* ctx_pool(rf_ctx* ctx) { return ctx_pool_ref(ctx).get(); }
 
 
 // Blocking copy / memset on the context's own (non-blocking) stream, never

@@ -182,3 +182,40 @@ def test_c2_largest_file_on_duo_vs_fixture(ctx, c2_set):
     assert out.to_numpy().tobytes() == ids[i].tobytes()
     plan.close()
     out.free()
+
+
+def test_plan_host_leg_does_not_hold_the_context(ctx, oracle):
+    """rf_sha_plan_run releases the context mutex while its host leg hashes
+    (ADVICE r02): a dedup batch on the same context, issued from another
+    thread while a 2 GiB message runs on the host leg, returns before the
+    plan does; both results are right."""
+    import threading
+    import time
+    lens = np.array([2 * GiB - 100] + [4096] * 64, dtype=np.uint64)
+    ds = DeviceSet(ctx, lens, 77)
+    plan = ctx.sha_plan(ds.offs, ds.lens, capi.RF_SHA_ALL_HOST)
+    assert plan.stats().n_host == len(lens)
+    rng = np.random.default_rng(3)
+    dig = rng.integers(0, 256, size=(200_000, 32), dtype=np.uint8)
+    dig[100_000:] = dig[:100_000]
+    done = {}
+
+    def run_plan():
+        plan.run(ds.arena.ptr, ds.out.ptr)
+        plan.stats()  # synchronises
+        done["plan"] = time.perf_counter()
+
+    th = threading.Thread(target=run_plan)
+    th.start()
+    time.sleep(0.2)  # the host leg is hashing by now (~0.6 s for 2 GiB on one thread)
+    canon, nu = ctx.dedup_digests(dig)
+    done["dedup"] = time.perf_counter()
+    th.join()
+    plan.close()
+    assert nu == 100_000 and (canon[100_000:] == np.arange(100_000)).all()
+    assert done["dedup"] < done["plan"], done
+    got = ds.out.to_numpy().reshape(-1, 32)
+    host = ds.arena.to_numpy()
+    for i in range(len(lens)):  # hashlib over the device's own bytes (the big one would take the oracle ~7 s)
+        o = int(ds.offs[i])
+        assert got[i].tobytes() == hashlib.sha256(host[o:o + int(lens[i])].tobytes()).digest(), i
