@@ -57,6 +57,11 @@ struct LevelArgs {
     const uint32_t* __restrict__ cons_ptr;  // [S+1] slot -> reverse-edge range (mark / apply kernels)
     uint4* lmeta;                           // [2J] the listed jobs' records, beside list
     uint32_t cb0;  // k2_level_pl<2,false>: chain-built block 0 of fused jobs (1: via the ring, 2: in registers)
+    // k2_level_pl: workgroups take the level's list from its END -- the jobs
+    // appended last (the chains that reached this level) before the sinks the
+    // mark kernel queued early (ALAP-moved physical keys): at 100M nodes the
+    // sinks alone fill the first ~2k workgroups of the OpK level
+    uint32_t rev;
     uint32_t* zero_counts;  // [L+1] the previous plain step's cursor half, zeroed by workgroup 0 (or null)
 };
 
@@ -840,18 +845,19 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
             const uint32_t i = base + jl;
             bool has = i < n;
-            uint32_t p = has ? lst[i] : 0u;
+            const uint32_t ii = a.rev ? n - 1 - i : i;  // (list position, when has)
+            uint32_t p = has ? lst[ii] : 0u;
             // the listed job's record (append_jobs wrote it beside the list)
             uint4 lm0 = make_uint4(0, 0, 0, 0), lm1 = lm0;
             if (has) {
-                lm0 = lmt[2ull * i];
-                lm1 = lmt[2ull * i + 1];
+                lm0 = lmt[2ull * ii];
+                lm1 = lmt[2ull * ii + 1];
             }
             uint32_t fslot = ~0u;
             uint32_t maxnb;
             {
                 const uint32_t il = base + lane;
-                maxnb = wave_max_small(il < n ? lmt[2ull * il].y : 0u);
+                maxnb = wave_max_small(il < n ? lmt[2ull * (a.rev ? n - 1 - il : il)].y : 0u);
             }
             uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
             uint4 nt[8];
@@ -1655,7 +1661,7 @@ static uint32_t grid_mark(uint64_t items) {
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, nullptr};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr};
     return a;
 }
 
@@ -1706,9 +1712,14 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         const char* v = getenv("RF_K2_CB0");
         return (v && atoi(v) == 0) ? 0u : 1u;
     }();
+    // RF_K2_REV=0: the list in append order (A/B)
+    static const uint32_t rev = [] {
+        const char* v = getenv("RF_K2_REV");
+        return (v && atoi(v) == 0) ? 0u : 1u;
+    }();
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
-                g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, zero_counts};
+                g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
