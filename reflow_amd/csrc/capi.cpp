@@ -1504,6 +1504,7 @@ extern "C" int rf_graph_set_slots(rf_graph* gr, const uint32_t* slots, const uin
     HIPC(launch_graph_mark_slots(gr->g, gr->b_tmp_idx.as<uint32_t>(), gr->b_tmp_dig.as<uint8_t>(), n,
                                  ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
+    gr->marked += n;
     return RF_OK;
 }
 
@@ -1513,8 +1514,13 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
     DevGuard dg(gr->ctx->device);
     HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
                                  static_cast<const uint8_t*>(d_digests32), n, pick(gr->ctx, stream)));
+    gr->marked += n;
     return RF_OK;
 }
+
+// Change sets (input slots marked since the last step) from this size on run
+// their incremental levels in the lane-per-job throughput form (k2_level_lf).
+static constexpr uint64_t kThruSlots = 65536;
 
 // The launch sequence (one kernel per level + a step-end kernel) only reads
 // device-side list lengths, so it is fixed for a loaded graph: capture it once
@@ -1524,9 +1530,20 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
 // bit); a full one discards whatever set_slots queued.
 static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = false) {
     GraphDev& G = gr->g;
+    struct MarkedReset {  // every recompute consumes the change set marked before it
+        rf_graph* gr;
+        ~MarkedReset() { gr->marked = 0; }
+    } marked_reset{gr};
     bool any = false;
     for (uint32_t l = 0; l < G.n_levels; ++l) any |= G.inc_level[l] != 0;
     if (plain && !full && any) {
+        // the level-kernel form for this step: a change set of at least
+        // RF_K2_THRU input slots (default kThruSlots) fills the chip with
+        // chains, and the lane-per-job form (k2_level_lf) outruns the
+        // two-lane latency form (k2_level_pl) -- DESIGN.md §5
+        const char* tv = getenv("RF_K2_THRU");  // (read per step: tests force either form)
+        const uint64_t thr = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
+        G.thru = gr->marked >= thr;
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
@@ -1539,6 +1556,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         std::swap(G.counts, G.counts_other);
         return RF_OK;
     }
+    G.thru = false;  // (captured sequences: the latency form)
     for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
     HIPC(launch_graph_step_end(G, full, s));
     gr->last_counts = G.counts_last;
@@ -1609,6 +1627,7 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
     hipGraphExec_t& ex = full ? gr->exec_full : gr->exec_inc;
     if (!ex && gr->g.n_levels)
         if (int rc = graph_capture(gr, full, &ex)) return rc;
+    gr->marked = 0;
     HIPC(hipEventRecord(gr->e0, s));
     if (ex) HIPC(hipGraphLaunch(ex, s));
     gr->last_counts = gr->g.counts_last;
@@ -1670,6 +1689,7 @@ extern "C" int rf_graph_update_recompute_async(rf_graph* gr, const void* d_slots
     if (!gr->initialized || inc_plain()) {  // mark, then the level launches (first call: the full sequence)
         HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
                                      static_cast<const uint8_t*>(d_digests32), n, s));
+        gr->marked += n;
         return graph_recompute_locked(gr, gr->initialized ? 0 : 1, s);
     }
     MarkArgs ma;

@@ -100,6 +100,10 @@ struct GraphDev {
     // RF_K2_STREAM=1 at load: the streamed hand-over variant of k2_level_pl
     // (opt-in, measured slower; kept correct by a forced-mode GPU test)
     bool stream_handover = false;
+    // the next plain incremental step's levels run k2_level_lf (one lane per
+    // listed job, the throughput form) instead of k2_level_pl: set per step by
+    // graph_enqueue from the size of the change set (rf_graph::marked)
+    bool thru = false;
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the
     // constant blocks its template starts with -- the record's template

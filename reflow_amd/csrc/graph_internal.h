@@ -44,6 +44,9 @@ struct rf_graph {
     hipGraphNode_t upd_mark = nullptr;
     bool timed = false;
     bool time_next = false;  // record e0/e1 around the next plain recompute (synchronous callers)
+    // input slots written (set_slots / update / imports) since the last
+    // incremental step: picks that step's level-kernel form (graph_enqueue)
+    uint64_t marked = 0;
     uint32_t* last_counts = nullptr;  // device cursors of the last recompute (counts_last, or a plain step's half)
     GraphPart* part = nullptr;  // multi-GPU partition (rf_graph_set_part), else null
 };

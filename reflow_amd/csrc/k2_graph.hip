@@ -1367,60 +1367,42 @@ __global__ __launch_bounds__(256) void k2_midstates(const uint8_t* __restrict__ 
     }
 }
 
-// A changed input slot s (digest nlo/nhi, already stored; cp0/cp1 its
-// reverse-edge range): its consumers join their levels' lists, except the
-// slot-fused one, which this lane hashes at once (one-lane SHA-256, the new
-// digest handed over in registers) and follows through its fusion chain like
-// the level kernels do -- never queued, so a level whose queueable jobs are
-// all slot-fused is not launched (configs[2]: every leaf OpVal and its
-// Coerce; before, a mark kernel, a launch gap and a level kernel whose list ->
-// record -> hole -> digest loads started cold).  Each job of the chain starts
-// with its record, first two template blocks, hole record, old digest and
-// start state in registers: they and the next job's record are fetched while
-// the job before it is hashed.  Called by every lane of the wave.
-__device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ring, bool changed, uint32_t s,
-                                                const uint4& nlo, const uint4& nhi, uint32_t cp0, uint32_t cp1) {
+// A fused job's operands, fetched a job ahead: its first two template blocks
+// (tt), its one hole record (rr), its old digest (ol, oh) and its start state
+// (hl, hh: the midstate, or untouched = IV).
+__device__ __forceinline__ void fetch_fused_ops(const LevelArgs& a, uint32_t q, const uint4& q0, const uint4& q1,
+                                                uint4 (&tt)[8], uint2& rr, uint4& ol, uint4& oh, uint4& hl,
+                                                uint4& hh) {
+    const uint4* T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * q0.x;
+    tt[0] = T[0]; tt[1] = T[1]; tt[2] = T[2]; tt[3] = T[3];
+    if (q0.y > 1) {
+        tt[4] = T[4]; tt[5] = T[5]; tt[6] = T[6]; tt[7] = T[7];
+    }
+    rr = a.holes[q0.z];
+    const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * q1.x);
+    ol = od[0];
+    oh = od[1];
+    if (a.mid) {
+        hl = a.mid[2ull * q];
+        hh = a.mid[2ull * q + 1];
+    }
+}
+
+// Hashes, one lane per chain, the fused chain that starts at job p (~0u: the
+// lane has none): p's records m0/m1, its operands (fetch_fused_ops: t, r,
+// olo/ohi, hlo/hhi) and its fusion target's records nm0/nm1 are in
+// registers, and its one hole reads slot fslot, whose new digest flo/fhi is
+// handed over in registers.  Each job whose digest changed hands it to its
+// fusion target; a job's other consumers are queued (propagate).  Returns the
+// jobs this lane hashed.  Called by every lane of the wave.
+__device__ __forceinline__ uint32_t hash_fused_chain(const LevelArgs& a, uint32_t* ring, uint32_t p, uint4 m0,
+                                                     uint4 m1, uint4 nm0, uint4 nm1, uint4 (&t)[8], uint2 r,
+                                                     uint4 olo, uint4 ohi, uint4 hlo, uint4 hhi, uint32_t fslot,
+                                                     uint4 flo, uint4 fhi) {
     constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     const uint4* T4 = reinterpret_cast<const uint4*>(a.tmpl);
-    uint32_t c = changed ? cp0 : 0u, ce = changed ? cp1 : 0u, p = ~0u;
-    const uint2 f = a.cons[c < ce ? c : 0u];
-    if (c < ce && (f.y & kSlotFused)) {
-        p = f.x;
-        ++c;
-    }
-    // the job's operands (fetched a job ahead after the first)
-    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, nm0 = m0, nm1 = m0, olo = m0, ohi = m0;
-    uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
-    uint4 t[8];
-    uint2 r = make_uint2(~0u, 0u);
-    auto fetch = [&](uint32_t q, const uint4& q0, const uint4& q1, uint4 (&tt)[8], uint2& rr, uint4& ol, uint4& oh,
-                     uint4& hl, uint4& hh) {
-        const uint4* T = T4 + 4ull * q0.x;
-        tt[0] = T[0]; tt[1] = T[1]; tt[2] = T[2]; tt[3] = T[3];
-        if (q0.y > 1) {
-            tt[4] = T[4]; tt[5] = T[5]; tt[6] = T[6]; tt[7] = T[7];
-        }
-        rr = a.holes[q0.z];
-        const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * q1.x);
-        ol = od[0];
-        oh = od[1];
-        if (a.mid) {
-            hl = a.mid[2ull * q];
-            hh = a.mid[2ull * q + 1];
-        }
-    };
-    if (p != ~0u) {
-        m0 = a.meta[2ull * p];
-        m1 = a.meta[2ull * p + 1];
-        fetch(p, m0, m1, t, r, olo, ohi, hlo, hhi);
-        if (m1.w != ~0u) {
-            nm0 = a.meta[2ull * m1.w];
-            nm1 = a.meta[2ull * m1.w + 1];
-        }
-    }
-    uint32_t fslot = s, hashed = 0;
-    uint4 flo = nlo, fhi = nhi;
+    uint32_t hashed = 0;
     while (__any(p != ~0u)) {
         uint32_t cb = 0, cz = 0, nx = ~0u;
         if (p != ~0u) {
@@ -1430,7 +1412,7 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
             uint2 nr = r;
             uint4 nnm0 = nm0, nnm1 = nm1;
             if (nf) {
-                fetch(m1.w, nm0, nm1, nt, nr, nolo, nohi, nhlo, nhhi);
+                fetch_fused_ops(a, m1.w, nm0, nm1, nt, nr, nolo, nohi, nhlo, nhhi);
                 if (nm1.w != ~0u) {
                     nnm0 = a.meta[2ull * nm1.w];
                     nnm1 = a.meta[2ull * nm1.w + 1];
@@ -1492,11 +1474,132 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
         propagate(a, cb, cz);
         p = nx;
     }
-    // the slot's other consumers
-    propagate(a, c, ce);
-    // counts[L]: jobs hashed outside the level lists (k3_step_end)
+    return hashed;
+}
+
+// Adds the wave's fused-chain job counts to counts[L] (jobs hashed outside
+// the level lists, k3_step_end / rf_graph_recompute's total).
+__device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed) {
     for (int o = 32; o > 0; o >>= 1) hashed += __shfl_xor(hashed, o, 64);
     if (__lane_id() == 0 && hashed) atomicAdd(&a.counts[a.n_levels], hashed);
+}
+
+// A changed input slot s (digest nlo/nhi, already stored; cp0/cp1 its
+// reverse-edge range): its consumers join their levels' lists, except the
+// slot-fused one, which this lane hashes at once (one-lane SHA-256, the new
+// digest handed over in registers) and follows through its fusion chain like
+// the level kernels do -- never queued, so a level whose queueable jobs are
+// all slot-fused is not launched (configs[2]: every leaf OpVal and its
+// Coerce; before, a mark kernel, a launch gap and a level kernel whose list ->
+// record -> hole -> digest loads started cold).  Each job of the chain starts
+// with its record, first two template blocks, hole record, old digest and
+// start state in registers: they and the next job's record are fetched while
+// the job before it is hashed.  Called by every lane of the wave.
+__device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ring, bool changed, uint32_t s,
+                                                const uint4& nlo, const uint4& nhi, uint32_t cp0, uint32_t cp1) {
+    constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    uint32_t c = changed ? cp0 : 0u, ce = changed ? cp1 : 0u, p = ~0u;
+    const uint2 f = a.cons[c < ce ? c : 0u];
+    if (c < ce && (f.y & kSlotFused)) {
+        p = f.x;
+        ++c;
+    }
+    // the job's operands (fetched a job ahead after the first)
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, nm0 = m0, nm1 = m0, olo = m0, ohi = m0;
+    uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
+    uint4 t[8];
+    uint2 r = make_uint2(~0u, 0u);
+    if (p != ~0u) {
+        m0 = a.meta[2ull * p];
+        m1 = a.meta[2ull * p + 1];
+        fetch_fused_ops(a, p, m0, m1, t, r, olo, ohi, hlo, hhi);
+        if (m1.w != ~0u) {
+            nm0 = a.meta[2ull * m1.w];
+            nm1 = a.meta[2ull * m1.w + 1];
+        }
+    }
+    const uint32_t hashed = hash_fused_chain(a, ring, p, m0, m1, nm0, nm1, t, r, olo, ohi, hlo, hhi, s, nlo, nhi);
+    // the slot's other consumers
+    propagate(a, c, ce);
+    count_fused(a, hashed);
+}
+
+// Throughput form of an incremental level (GraphDev::thru: a step whose
+// change set fills the chip): one lane per listed job, 256-thread
+// workgroups, no producer / chain split -- every lane of every wave hashes
+// (one-lane rounds, the schedule in registers), so four workgroups share a
+// CU and their waves' issue slots interleave.  A listed job's fused chain is
+// followed in its lane (hash_fused_chain), as the mark kernel does for the
+// slot-fused chains.  k2_level_pl's two-lane chains shorten a link's latency
+// but keep only 64 jobs per 192-thread workgroup resident (two per CU), so
+// once a level's list is several times the resident set the step is bound by
+// rounds of resident workgroups x link latency (configs[3]'s 100M-node DAG
+// on one GPU), and this form is faster.
+__global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
+    __shared__ uint32_t ring_all[kLevelBlock * kRing];
+    uint32_t* ring = &ring_all[threadIdx.x * kRing];
+    zero_other_counts(a);
+    const uint32_t n = a.counts[a.lvl];
+    const uint32_t* lst = a.list + a.s;
+    const uint4* lmt = a.lmeta + 2ull * a.s;
+    uint32_t hashed = 0;
+    for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
+        const uint32_t i = base + threadIdx.x;
+        uint32_t p = ~0u;
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        if (i < n) {
+            const uint32_t ii = a.rev ? n - 1 - i : i;
+            p = lst[ii];
+            m0 = lmt[2ull * ii];  // the record append_jobs wrote beside the list
+            m1 = lmt[2ull * ii + 1];
+        }
+        // the lane's chain: the listed job, then while its digest changed its
+        // fusion target (never queued), whose one hole is the slot just
+        // written -- handed over in registers (fslot / flo / fhi)
+        bool listed = true;
+        uint32_t fslot = ~0u;
+        uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo;
+        while (__any(p != ~0u)) {
+            uint32_t cb = 0, cz = 0, nx = ~0u;
+            if (p != ~0u) {
+                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+                const uint4 olo = od[0], ohi = od[1];
+                MatCursor cur;
+                cur.fslot = fslot;
+                cur.flo = flo;
+                cur.fhi = fhi;
+                cur.begin(a, m0, ring);
+                ShaState st;
+                init_state(a, p, st);
+                for (uint32_t b = 0; b < cur.nb; ++b) {
+                    uint32_t w[16];
+                    cur.block(a, b, ring, w);
+                    sha256_compress(st, w);
+                }
+                const bool ch = finish_job_pre(a, m1, st, olo, ohi);
+                if (listed)
+                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                else
+                    ++hashed;
+                const bool nf = m1.w != ~0u;
+                cb = m1.y;
+                cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
+                if (ch && nf) {
+                    nx = m1.w;
+                    fslot = m1.x;
+                    flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                    fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+                    m0 = a.meta[2ull * nx];
+                    m1 = a.meta[2ull * nx + 1];
+                }
+            }
+            propagate(a, cb, cz);
+            p = nx;
+            listed = false;
+        }
+    }
+    count_fused(a, hashed);
 }
 
 constexpr uint32_t kMarkBlock = 64;
@@ -1753,7 +1856,17 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_PAD_KB");
             return v ? (uint32_t)atoi(v) * 1024u : 0u;
         }();
-        if (one_lane && wide)
+        if (g.thru) {
+            // the throughput form: 256 lanes per workgroup, four resident per
+            // CU, grid-stride over the device-side count
+            static const uint64_t lf_cap = [] {
+                const char* v = getenv("RF_K2_LF_GRID");
+                return v ? (uint64_t)strtoull(v, nullptr, 10) : 1024ull;
+            }();
+            uint64_t lg = (e - b + kLevelBlock - 1) / kLevelBlock;
+            if (lg > lf_cap) lg = lf_cap;
+            hipLaunchKernelGGL(k2_level_lf, dim3((uint32_t)lg), dim3(kLevelBlock), 0, s, a);
+        } else if (one_lane && wide)
             hipLaunchKernelGGL(k2_level_pc<3>, dim3((uint32_t)wg), dim3(192), pad, s, a);
         else if (one_lane)
             hipLaunchKernelGGL(k2_level_pc<2>, dim3((uint32_t)wg), dim3(128), pad, s, a);

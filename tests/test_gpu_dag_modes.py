@@ -1,8 +1,10 @@
 """The opt-in and forced K2 level variants stay correct: the streamed
 hand-over (RF_K2_STREAM=1: k2_level_pl<2, true>, whose chunk flags are
-published after an LDS wait -- ADVICE r02) and every queueable level run as a
-three-wave "wide" workgroup (RF_K2_WIDE=1: k2_level_pl<3>).  Both are read
-when a graph is loaded, so one process covers them.  Checked against the
+published after an LDS wait -- ADVICE r02), every queueable level run as a
+three-wave "wide" workgroup (RF_K2_WIDE=1: k2_level_pl<3>), and every
+incremental step in the lane-per-job throughput form (RF_K2_THRU=0:
+k2_level_lf).  The first two are read when a graph is loaded, the third per
+step, so one process covers them.  Checked against the
 oracle on the random fused-chain graphs and the 1000align DAG, and on a
 larger 1000align DAG against the default mode's incremental recompute."""
 import numpy as np
@@ -16,7 +18,9 @@ from test_gpu_dag_fusion import load as load_jobs
 
 pytestmark = pytest.mark.gpu
 
-MODES = [("RF_K2_STREAM", "1"), ("RF_K2_WIDE", "1")]
+# RF_K2_THRU=0: every incremental step in the lane-per-job throughput form
+# (k2_level_lf), which the library picks for change sets of >= 64k slots
+MODES = [("RF_K2_STREAM", "1"), ("RF_K2_WIDE", "1"), ("RF_K2_THRU", "0")]
 
 
 @pytest.fixture(scope="module")
@@ -68,15 +72,19 @@ def test_forced_mode_dag1000(ctx, monkeypatch, var, val):
     g.close()
     # 0.45M nodes: the forced mode's incremental slots == the default mode's
     big = Dag1000(1000, 32)
-    gf = load_dag(ctx, big)
-    monkeypatch.delenv(var)
-    gd = load_dag(ctx, big)
     sl, _, nw = big.change_set(0.01)
     every = np.arange(big.n_slots, dtype=np.uint32)
-    for gg in (gf, gd):
+
+    def run(gg):
         gg.recompute(full=True)
         gg.set_slots(sl, nw)
         gg.recompute(full=False)
+
+    gf = load_dag(ctx, big)
+    run(gf)  # with the mode set (load-time and per-step variables alike)
+    monkeypatch.delenv(var)
+    gd = load_dag(ctx, big)
+    run(gd)
     assert (gf.get_slots(every) == gd.get_slots(every)).all()
     gf.close()
     gd.close()

@@ -1,0 +1,103 @@
+"""A/B of the two incremental level-kernel forms on the bench's DAGs, one
+process, one graph load each: k2_level_pl (two-lane latency form) vs
+k2_level_lf (lane-per-job throughput form), picked per step by RF_K2_THRU
+(read per step).  For each graph: ms/step of both forms over the same toggled
+1 % change set, and every slot of both forms compared after an odd step.
+
+  python tools/dag_forms.py [--c2] [--c4-ranks 1,2,4,8] [--steps 20]
+
+--c4-ranks r: rank 0's piece of the strong-scaling 100M-node layout at r
+ranks (the local step only, no exchange): what one GPU of an r-GPU run hashes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from reflow_amd import capi  # noqa: E402
+from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
+
+FORMS = {"pl": str(1 << 62), "lf": "0"}
+
+
+def run(ctx, name, g, slots, old, new, steps):
+    d_slots = ctx.upload(slots)
+    d_old, d_new = ctx.upload(old), ctx.upload(new)
+    every = np.arange(g.stats().n_slots, dtype=np.uint32)
+    res = {"graph": name, "changed_slots": int(len(slots))}
+    snaps = {}
+    for rep in range(2):
+        for form, thr in FORMS.items():
+            os.environ["RF_K2_THRU"] = thr
+            state = {"v": 0}
+
+            def step():
+                ver = d_new if state["v"] == 0 else d_old
+                state["v"] ^= 1
+                g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
+                g.recompute_async(False, ctx.stream)
+
+            for _ in range(2):
+                step()
+            ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            ctx.sync()
+            ms = (time.perf_counter() - t0) / steps * 1e3
+            res.setdefault(form, []).append(round(ms, 4))
+            if rep == 0:  # an odd step: the changed version everywhere
+                step()
+                ctx.sync()
+                snaps[form] = g.get_slots(every)
+                step()
+                ctx.sync()
+            print(name, form, "%.4f ms/step" % ms, file=sys.stderr, flush=True)
+    res["slots_equal"] = bool((snaps["pl"] == snaps["lf"]).all())
+    os.environ.pop("RF_K2_THRU", None)
+    for b in (d_slots, d_old, d_new):
+        b.free()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c2", action="store_true")
+    ap.add_argument("--c4-ranks", default="")
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    import faulthandler
+    faulthandler.dump_traceback_later(500, exit=True)
+    ctx = capi.Context(0, host_threads=0)
+    out = []
+    if a.c2:
+        dag = Dag1000(22075, 32)
+        g = capi.Graph.from_arrays(ctx, dag.arrays())
+        g.set_slots(dag.file_slots, dag.leaf_ids)
+        g.recompute(True)
+        slots, old, new = dag.change_set(0.01)
+        out.append(run(ctx, "configs[2]", g, slots, old, new, a.steps))
+        g.close()
+        del dag
+    for r in [int(x) for x in a.c4_ranks.split(",") if x]:
+        t0 = time.perf_counter()
+        pc = PartitionedDag1000(27594, 32, r, 0, nparts=8)
+        g = capi.Graph.from_arrays(ctx, pc.desc)
+        g.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
+        g.recompute(True)
+        slots, old, new = pc.dag.change_set(0.01, n_global=2 * 32 * 27594 * 8)
+        print("c4 r=%d loaded in %.1f s" % (r, time.perf_counter() - t0), file=sys.stderr, flush=True)
+        res = run(ctx, "configs[3] rank 0 of %d (%d nodes)" % (r, pc.n_nodes), g, slots, old, new, a.steps)
+        out.append(res)
+        g.close()
+        del pc, g
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
