@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -1149,7 +1150,7 @@ int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_
         (e = gr->b_cons_job.ensure(std::max<size_t>(8ull * H, 64))) != hipSuccess ||
         (e = gr->b_tmpl.ensure(std::max<size_t>(tmpl_bytes, 64))) != hipSuccess ||
         (e = gr->b_slots.ensure(32ull * std::max<uint32_t>(S, 1))) != hipSuccess ||
-        (e = gr->b_dirty.ensure(4ull * ((J + 31) / 32 + 1))) != hipSuccess ||
+        (e = gr->b_dirty.ensure(4ull * (J + 1))) != hipSuccess ||
         (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_lmeta.ensure(32ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_counts.ensure(8ull * (L + 1))) != hipSuccess ||  // two halves (plain-step parity)
@@ -1157,7 +1158,7 @@ int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_
         (e = gr->b_lvl_start.ensure(std::max<size_t>(4ull * (L + 1), 64))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph alloc: %s", hipGetErrorString(e));
     HIPC(sync_memset(ctx, gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
-    HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * ((J + 31) / 32 + 1)));
+    HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * (J + 1)));
     HIPC(sync_memset(ctx, gr->b_counts.p, 0, 8ull * (L + 1)));
     HIPC(sync_memset(ctx, gr->b_counts_last.p, 0, 4ull * (L + 1)));
     G.meta = gr->b_meta.as<uint4>();
@@ -1455,6 +1456,12 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
         G.stamps = static_cast<unsigned long long*>(gr->b_stamps.p);
     }
+    if (getenv("RF_K2_WGSTAMPS")) {  // diagnostic: every incremental level kernel's workgroups
+        const uint64_t bytes = 8ull * 4 * 2048 * std::max<uint32_t>(L, 1);
+        HIPC(gr->b_wgst.ensure(bytes));
+        HIPC(sync_memset(ctx, gr->b_wgst.p, 0, bytes));
+        G.wgst = static_cast<unsigned long long*>(gr->b_wgst.p);
+    }
     guard.release();
     *out = gr;
     return RF_OK;
@@ -1466,7 +1473,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
                           &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_lmeta, &gr->b_counts, &gr->b_counts_last,
-                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid})
+                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);
@@ -1537,13 +1544,14 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
     bool any = false;
     for (uint32_t l = 0; l < G.n_levels; ++l) any |= G.inc_level[l] != 0;
     if (plain && !full && any) {
-        // the level-kernel form for this step: a change set of at least
-        // RF_K2_THRU input slots (default kThruSlots) fills the chip with
-        // chains, and the lane-per-job form (k2_level_lf) outruns the
-        // two-lane latency form (k2_level_pl) -- DESIGN.md §5
+        // the level-kernel forms for this step: a level that can receive at
+        // least RF_K2_THRU chains (default kThruSlots) fills the chip, and the
+        // lane-per-job form (k2_level_lf) outruns the two-lane latency form
+        // (k2_level_pl) there -- DESIGN.md §5
         const char* tv = getenv("RF_K2_THRU");  // (read per step: tests force either form)
         const uint64_t thr = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
-        G.thru = gr->marked >= thr;
+        G.step_marked = gr->marked;
+        G.thru_slots = thr;
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
@@ -1556,12 +1564,12 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         std::swap(G.counts, G.counts_other);
         return RF_OK;
     }
-    G.thru = false;  // (captured sequences: the latency form)
+    G.thru_slots = ~0ull;  // (captured sequences: the latency form)
     for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
     HIPC(launch_graph_step_end(G, full, s));
     gr->last_counts = G.counts_last;
     if (full) {
-        HIPC(hipMemsetAsync(G.dirty, 0, 4ull * ((G.n_jobs + 31) / 32 + 1), s));
+        HIPC(hipMemsetAsync(G.dirty, 0, 4ull * (G.n_jobs + 1), s));
         HIPC(hipMemsetAsync(G.counts_other, 0, 4ull * (G.n_levels + 1), s));  // both halves clear
     }
     return RF_OK;
@@ -1715,6 +1723,68 @@ extern "C" int rf_graph_recompute_async(rf_graph* gr, int full, void* stream) {
     return graph_recompute_locked(gr, full, pick(gr->ctx, stream));
 }
 
+// RF_K2_WGSTAMPS=1 diagnostic: per launched level, the workgroups that took
+// jobs -- how many, their durations (min / median / max), how late the last
+// one started, and how many shared a CU with another working workgroup (and
+// their mean duration against the ones alone) -- then the records are cleared.
+static void wgst_report(rf_graph* gr) {
+    const GraphDev& G = gr->g;
+    std::vector<unsigned long long> w(4ull * 2048 * G.n_levels);
+    if (sync_copy(gr->ctx, w.data(), G.wgst, 8 * w.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+    unsigned long long step0 = ~0ull;  // the step's first workgroup start, any level
+    for (size_t i = 0; i < w.size(); i += 4)
+        if (w[i + 1]) step0 = std::min(step0, w[i]);
+    for (uint32_t l = 0; l < G.n_levels; ++l) {
+        const unsigned long long* r = &w[4ull * 2048 * l];
+        // every workgroup of the launch (working or not): its first start and
+        // last end on the step's clock
+        unsigned long long a0 = ~0ull, a1 = 0;
+        uint32_t nall = 0;
+        for (uint32_t i = 0; i < 2048; ++i)
+            if (r[4 * i + 1]) {
+                a0 = std::min(a0, r[4 * i]);
+                a1 = std::max(a1, r[4 * i + 1]);
+                ++nall;
+            }
+        std::vector<uint32_t> act;
+        unsigned long long t0 = ~0ull;
+        for (uint32_t i = 0; i < 2048; ++i)
+            if (r[4 * i + 1] && r[4 * i + 3]) {
+                act.push_back(i);
+                t0 = std::min(t0, r[4 * i]);
+            }
+        if (act.empty()) continue;
+        std::map<unsigned long long, std::vector<uint32_t>> cu;  // xcc | se/sh/cu -> workgroups
+        std::vector<double> dur;
+        double late = 0;
+        for (uint32_t i : act) {
+            const unsigned long long hw = r[4 * i + 2];
+            cu[((hw >> 32) << 8) | ((hw >> 8) & 0xff)].push_back(i);
+            dur.push_back((r[4 * i + 1] - r[4 * i]) * 0.01);
+            late = std::max(late, (r[4 * i] - t0) * 0.01);
+        }
+        std::vector<double> ds = dur;
+        std::sort(ds.begin(), ds.end());
+        double sh = 0, al = 0;
+        uint32_t nsh = 0, nal = 0, cus_shared = 0;
+        for (auto& kv : cu) {
+            if (kv.second.size() > 1) ++cus_shared;
+            for (uint32_t i : kv.second) {
+                const double d = (r[4 * i + 1] - r[4 * i]) * 0.01;
+                if (kv.second.size() > 1) sh += d, ++nsh;
+                else al += d, ++nal;
+            }
+        }
+        fprintf(stderr,
+                "[wgstamps] level %u: launch %u workgroups, first start %.1f, last end %.1f us into the step; "
+                "%zu working on %zu CUs (%u CUs shared); us min %.1f median %.1f max %.1f; last start +%.1f; "
+                "mean alone %.1f (%u), shared %.1f (%u)\n",
+                l, nall, (a0 - step0) * 0.01, (a1 - step0) * 0.01, act.size(), cu.size(), cus_shared, ds.front(),
+                ds[ds.size() / 2], ds.back(), late, nal ? al / nal : 0.0, nal, nsh ? sh / nsh : 0.0, nsh);
+    }
+    (void)sync_memset(gr->ctx, G.wgst, 0, 8 * w.size());
+}
+
 extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomputed) {
     ARG(gr, "null graph");
     rf_ctx* ctx = gr->ctx;
@@ -1731,9 +1801,13 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
     HIPC(hipStreamSynchronize(ctx->stream));
     uint64_t tot = 0;
     for (uint32_t l = 0; l <= gr->g.n_levels; ++l) tot += counts[l];
+    if (gr->g.wgst && !full) wgst_report(gr);
     if (gr->g.stamps && !full) {  // diagnostic print: per level, chain wave then producer wave
         std::vector<unsigned long long> st(128ull * gr->g.n_levels);
         HIPC(sync_copy(ctx, st.data(), gr->g.stamps, 8 * st.size(), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[counts] jobs per level:");
+        for (uint32_t l = 0; l <= gr->g.n_levels; ++l) fprintf(stderr, " %u", counts[l]);
+        fprintf(stderr, " (last: fused)\n");
         for (uint32_t l = 0; l < gr->g.n_levels; ++l)
             for (int w = 0; w < 2; ++w) {
                 const unsigned long long* x = &st[128ull * l + 64 * w];

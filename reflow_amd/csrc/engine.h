@@ -77,7 +77,7 @@ struct GraphDev {
     uint2* cons = nullptr;           // [C] {consumer job, its level}
     uint8_t* tmpl = nullptr;         // padded templates, zero at the holes (read-only)
     uint8_t* slots = nullptr;        // [S][32] digest table
-    uint32_t* dirty = nullptr;       // [(J+31)/32] queued-this-step bitset over internal ids
+    uint32_t* dirty = nullptr;       // [J] queued-this-step flag per internal id (a word each)
     uint32_t* list = nullptr;        // [J] per-level work lists (level l at lvl_start[l])
     uint4* lmeta = nullptr;          // [2J] each listed job's record, at its list position
     uint32_t* counts = nullptr;      // [L+1] list lengths (append cursors); [L] = fused jobs hashed
@@ -100,11 +100,15 @@ struct GraphDev {
     // RF_K2_STREAM=1 at load: the streamed hand-over variant of k2_level_pl
     // (opt-in, measured slower; kept correct by a forced-mode GPU test)
     bool stream_handover = false;
-    // the next plain incremental step's levels run k2_level_lf (one lane per
-    // listed job, the throughput form) instead of k2_level_pl: set per step by
-    // graph_enqueue from the size of the change set (rf_graph::marked)
-    bool thru = false;
+    // The next plain incremental step's level-kernel forms, set per step by
+    // graph_enqueue: a level runs k2_level_lf (one lane per listed job, the
+    // throughput form) instead of k2_level_pl when min(its jobs, step_marked)
+    // >= thru_slots -- step_marked = the input slots marked for the step (an
+    // upper bound of the chains that can reach the level), the level's size
+    // the other bound (merge-tree levels stay in the latency form)
+    uint64_t step_marked = 0, thru_slots = ~0ull;
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
+    unsigned long long* wgst = nullptr;    // diagnostic per-workgroup records [L][2048][4] (RF_K2_WGSTAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the
     // constant blocks its template starts with -- the record's template
     // offset and block count already skip them); null when no job has any

@@ -30,7 +30,7 @@ struct rf_graph {
     std::vector<int64_t> producer;   // slot -> external job or -1
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
-    DevBuf b_stamps, b_mid;
+    DevBuf b_stamps, b_mid, b_wgst;
     DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_lmeta, b_counts,
         b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;

@@ -14,7 +14,10 @@
 //             consumer range): two 16-B loads per job.
 //   holes     {byte position, slot} pairs, sorted by position per job.
 //   slots     [S][32] digest table (node digests, physical keys, File IDs).
-//   dirty     bitset over jobs in level order: "already queued this step".
+//   dirty     one word per job in level order: "already queued this step"
+//             (a word each, not a bit: a bitset packed 32 consumers into one
+//             word, and a merge node's producers -- 32 of them for each of
+//             the word's 32 jobs -- serialised their atomics on it).
 //   list      [J] per-level work lists; level l's list lives at lvl_start[l]
 //             (a level can never hold more dirty jobs than it has jobs).
 //   cons      slot -> consumer jobs (reverse edges for the frontier).
@@ -26,6 +29,7 @@
 // ring (template block + digests OR-ed into the zero holes), hashes it and
 // propagates.  A level's jobs all depend only on lower levels, so a level's
 // list is complete when its kernel starts.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -63,6 +67,30 @@ struct LevelArgs {
     // sinks alone fill the first ~2k workgroups of the OpK level
     uint32_t rev;
     uint32_t* zero_counts;  // [L+1] the previous plain step's cursor half, zeroed by workgroup 0 (or null)
+    unsigned long long* wgst;  // diagnostic (RF_K2_WGSTAMPS=1): per-workgroup records [L][kWgStamps][4], else null
+};
+
+// Diagnostic per-workgroup record of an incremental level kernel: start and
+// end (s_memrealtime, 100 MHz), the hardware ids of the CU it ran on
+// (HW_REG_HW_ID | HW_REG_XCC_ID << 32) and the jobs it took from the list.
+constexpr uint32_t kWgStamps = 2048;
+struct WgStamp {
+    unsigned long long t0 = 0;
+    uint32_t jobs = 0;
+    __device__ __forceinline__ void begin(const LevelArgs& a) {
+        if (a.wgst && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ void end(const LevelArgs& a) {
+        if (!a.wgst || threadIdx.x != 0 || blockIdx.x >= kWgStamps) return;
+        uint32_t hw, xcc;
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                         : "=s"(hw), "=s"(xcc));
+        unsigned long long* r = a.wgst + 4ull * (a.lvl * kWgStamps + blockIdx.x);
+        r[0] = t0;
+        r[1] = __builtin_amdgcn_s_memrealtime();
+        r[2] = hw | ((unsigned long long)xcc << 32);
+        r[3] = jobs;
+    }
 };
 
 // (first level kernel of a plain incremental step) the previous step's
@@ -120,7 +148,7 @@ __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint3
 
 // Mark consumers [c, ce) of the lanes whose slot changed (c == ce otherwise)
 // dirty, queueing the newly dirty ones (their records are fetched beside the
-// dirty-bit atomic).  Wave-uniform loop.
+// dirty-flag atomic).  Wave-uniform loop.
 __device__ __forceinline__ void propagate(const LevelArgs& a, uint32_t c, uint32_t ce) {
     while (__any(c < ce)) {
         bool need = false;
@@ -130,8 +158,7 @@ __device__ __forceinline__ void propagate(const LevelArgs& a, uint32_t c, uint32
             jl = a.cons[c++];
             q0 = a.meta[2ull * jl.x];
             q1 = a.meta[2ull * jl.x + 1];
-            const uint32_t bit = 1u << (jl.x & 31);
-            need = !(atomicOr(&a.dirty[jl.x >> 5], bit) & bit);
+            need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
         }
         append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
@@ -345,8 +372,7 @@ __device__ __forceinline__ void propagate_pre(const LevelArgs& a, uint32_t c, ui
             ++c;
             q0 = a.meta[2ull * jl.x];
             q1 = a.meta[2ull * jl.x + 1];
-            const uint32_t bit = 1u << (jl.x & 31);
-            need = !(atomicOr(&a.dirty[jl.x >> 5], bit) & bit);
+            need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
         }
         append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
@@ -394,7 +420,7 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
             const uint32_t p = a.full ? a.s + i : lst[i];
             const bool changed = hash_job(a, p, ring, cb, ce);
             if (!a.full) {
-                atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                a.dirty[p] = 0u;
                 if (!changed) ce = cb;
             }
         }
@@ -614,7 +640,7 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
             if (wave == 0) {
                 uint32_t cb = 0, ce = 0;
                 if (has) {
-                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                    a.dirty[p] = 0u;
                     cb = m1.y;
                     // the fusion target's edge is the last of the range
                     ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
@@ -831,6 +857,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     zero_other_counts(a);
+    WgStamp ws;
+    ws.begin(a);
     const uint32_t n = a.counts[a.lvl];
     const uint32_t* lst = a.list + a.s;
     const uint4* lmt = a.lmeta + 2ull * a.s;
@@ -843,6 +871,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         constexpr uint32_t R = decltype(rc)::value;
         constexpr bool kChain = R < 2, kIsProd = R == kProd, kIsExp = R == kExp;
         for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+            if (threadIdx.x == 0) ws.jobs += min(64u, n - base);
             const uint32_t i = base + jl;
             bool has = i < n;
             const uint32_t ii = a.rev ? n - 1 - i : i;  // (list position, when has)
@@ -878,7 +907,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             auto producer_propagate = [&]() {
                 const uint4 q = s_pp[lane][0], e = s_pp[lane][1];
                 const bool v = q.w != 0;
-                if (v) atomicAnd(&a.dirty[q.x >> 5], ~(1u << (q.x & 31)));
+                if (v) a.dirty[q.x] = 0u;
                 const uint2 pe[2] = {make_uint2(e.x, e.y), make_uint2(e.z, e.w)};
                 propagate_pre(a, v ? q.y : 0u, v ? q.z : 0u, pe);
                 pend = false;
@@ -1313,7 +1342,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     if (!(kCB && a.cb0) && !pp3) {
                         uint32_t cb = 0, ce = 0;
                         if (own) {
-                            atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                            a.dirty[p] = 0u;
                             cb = m1.y;
                             ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
                         }
@@ -1341,6 +1370,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     }
     if (a.stamps && blockIdx.x == 0 && (wave == 0 || wave == kProd))
         a.stamps[128 * a.lvl + 64 * (wave != 0) + lane] = s_stamp[wave != 0][lane];
+    ws.end(a);
 }
 
 // Load time: the chaining value after each job's constant leading blocks.
@@ -1540,11 +1570,14 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
     zero_other_counts(a);
+    WgStamp ws;
+    ws.begin(a);
     const uint32_t n = a.counts[a.lvl];
     const uint32_t* lst = a.list + a.s;
     const uint4* lmt = a.lmeta + 2ull * a.s;
     uint32_t hashed = 0;
     for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
+        if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
         const uint32_t i = base + threadIdx.x;
         uint32_t p = ~0u;
         uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
@@ -1579,7 +1612,7 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
                 }
                 const bool ch = finish_job_pre(a, m1, st, olo, ohi);
                 if (listed)
-                    atomicAnd(&a.dirty[p >> 5], ~(1u << (p & 31)));
+                    a.dirty[p] = 0u;
                 else
                     ++hashed;
                 const bool nf = m1.w != ~0u;
@@ -1600,6 +1633,7 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
         }
     }
     count_fused(a, hashed);
+    ws.end(a);
 }
 
 constexpr uint32_t kMarkBlock = 64;
@@ -1764,7 +1798,7 @@ static uint32_t grid_mark(uint64_t items) {
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
-                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr};
+                g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
     return a;
 }
 
@@ -1822,7 +1856,8 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }();
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
-                g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts};
+                g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
+                full ? nullptr : g.wgst};
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
@@ -1856,7 +1891,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_PAD_KB");
             return v ? (uint32_t)atoi(v) * 1024u : 0u;
         }();
-        if (g.thru) {
+        if (std::min<uint64_t>(e - b, g.step_marked) >= g.thru_slots) {
             // the throughput form: 256 lanes per workgroup, four resident per
             // CU, grid-stride over the device-side count
             static const uint64_t lf_cap = [] {

@@ -1,8 +1,9 @@
-"""A/B of the two incremental level-kernel forms on the bench's DAGs, one
-process, one graph load each: k2_level_pl (two-lane latency form) vs
-k2_level_lf (lane-per-job throughput form), picked per step by RF_K2_THRU
-(read per step).  For each graph: ms/step of both forms over the same toggled
-1 % change set, and every slot of both forms compared after an odd step.
+"""A/B of the incremental level-kernel forms on the bench's DAGs, one process,
+one graph load each: every level in k2_level_pl (two-lane latency form), every
+level in k2_level_lf (lane-per-job throughput form), and the library's
+per-level choice -- set per step by RF_K2_THRU (read per step).  For each
+graph: ms/step of each form over the same toggled 1 % change set, and every
+slot of each form compared after an odd step.
 
   python tools/dag_forms.py [--c2] [--c4-ranks 1,2,4,8] [--steps 20]
 
@@ -21,7 +22,9 @@ import numpy as np  # noqa: E402
 from reflow_amd import capi  # noqa: E402
 from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
-FORMS = {"pl": str(1 << 62), "lf": "0"}
+# pl: every level in the latency form; lf: every level in the throughput
+# form; auto: the library's per-level choice (RF_K2_THRU unset)
+FORMS = {"pl": str(1 << 62), "lf": "0", "auto": None}
 
 
 def run(ctx, name, g, slots, old, new, steps):
@@ -32,7 +35,10 @@ def run(ctx, name, g, slots, old, new, steps):
     snaps = {}
     for rep in range(2):
         for form, thr in FORMS.items():
-            os.environ["RF_K2_THRU"] = thr
+            if thr is None:
+                os.environ.pop("RF_K2_THRU", None)
+            else:
+                os.environ["RF_K2_THRU"] = thr
             state = {"v": 0}
 
             def step():
@@ -57,7 +63,7 @@ def run(ctx, name, g, slots, old, new, steps):
                 step()
                 ctx.sync()
             print(name, form, "%.4f ms/step" % ms, file=sys.stderr, flush=True)
-    res["slots_equal"] = bool((snaps["pl"] == snaps["lf"]).all())
+    res["slots_equal"] = bool(all((snaps["pl"] == snaps[f]).all() for f in snaps))
     os.environ.pop("RF_K2_THRU", None)
     for b in (d_slots, d_old, d_new):
         b.free()

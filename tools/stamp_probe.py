@@ -1,20 +1,29 @@
-"""One configs[2] incremental step with RF_K2_STAMPS=1: prints workgroup 0's
-per-phase times for every launched level (chain wave, producer wave)."""
+"""One incremental step with RF_K2_STAMPS=1: prints workgroup 0's per-phase
+times for every launched level (chain wave, producer wave) and the jobs
+hashed per level.
+
+  python tools/stamp_probe.py [S]        configs[2] (S samples, default 22075)
+  python tools/stamp_probe.py c4 R       rank 0's piece of the 100M layout at R ranks
+"""
 import os
 import sys
 
 os.environ.setdefault("RF_K2_STAMPS", "1")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from reflow_amd import capi  # noqa: E402
-from reflow_amd.workloads import Dag1000  # noqa: E402
+from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
-S = int(sys.argv[1]) if len(sys.argv) > 1 else 22075
 ctx = capi.Context(0, host_threads=0)
-dag = Dag1000(S, 32)
-g = capi.Graph.from_arrays(ctx, dag.arrays())
+if len(sys.argv) > 2 and sys.argv[1] == "c4":
+    pc = PartitionedDag1000(27594, 32, int(sys.argv[2]), 0, nparts=8)
+    dag, desc, n_global = pc.dag, pc.desc, 2 * 32 * 27594 * 8
+else:
+    dag = Dag1000(int(sys.argv[1]) if len(sys.argv) > 1 else 22075, 32)
+    desc, n_global = dag.arrays(), None
+g = capi.Graph.from_arrays(ctx, desc)
 g.set_slots(dag.file_slots, dag.leaf_ids)
 g.recompute(full=True)
-slots, old, new = dag.change_set(0.01)
+slots, old, new = dag.change_set(0.01, n_global=n_global) if n_global else dag.change_set(0.01)
 for v in (new, old, new):
     g.set_slots(slots, v)
     print("recomputed", g.recompute(full=False), flush=True)
