@@ -1567,6 +1567,8 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
 // rounds of resident workgroups x link latency (configs[3]'s 100M-node DAG
 // on one GPU), and this form is faster.
 __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
+    constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
     zero_other_counts(a);
@@ -1580,57 +1582,64 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
         if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
         const uint32_t i = base + threadIdx.x;
         uint32_t p = ~0u;
-        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, nm0 = m0, nm1 = m0, olo = m0, ohi = m0;
+        uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
         if (i < n) {
             const uint32_t ii = a.rev ? n - 1 - i : i;
             p = lst[ii];
             m0 = lmt[2ull * ii];  // the record append_jobs wrote beside the list
             m1 = lmt[2ull * ii + 1];
+            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+            olo = od[0];
+            ohi = od[1];
+            if (a.mid) {
+                hlo = a.mid[2ull * p];
+                hhi = a.mid[2ull * p + 1];
+            }
+            if (m1.w != ~0u) {
+                nm0 = a.meta[2ull * m1.w];
+                nm1 = a.meta[2ull * m1.w + 1];
+            }
         }
-        // the lane's chain: the listed job, then while its digest changed its
-        // fusion target (never queued), whose one hole is the slot just
-        // written -- handed over in registers (fslot / flo / fhi)
-        bool listed = true;
-        uint32_t fslot = ~0u;
+        // the fusion target's operands and records, fetched while p is hashed
+        // (hash_fused_chain then fetches each next target's a job ahead)
+        uint4 nt[8], nolo = olo, nohi = ohi, nnm0 = nm0, nnm1 = nm1;
+        uint4 nhlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nhhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
+        uint2 nr = make_uint2(~0u, 0u);
+        uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
         uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo;
-        while (__any(p != ~0u)) {
-            uint32_t cb = 0, cz = 0, nx = ~0u;
-            if (p != ~0u) {
-                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
-                const uint4 olo = od[0], ohi = od[1];
-                MatCursor cur;
-                cur.fslot = fslot;
-                cur.flo = flo;
-                cur.fhi = fhi;
-                cur.begin(a, m0, ring);
-                ShaState st;
-                init_state(a, p, st);
-                for (uint32_t b = 0; b < cur.nb; ++b) {
-                    uint32_t w[16];
-                    cur.block(a, b, ring, w);
-                    sha256_compress(st, w);
-                }
-                const bool ch = finish_job_pre(a, m1, st, olo, ohi);
-                if (listed)
-                    a.dirty[p] = 0u;
-                else
-                    ++hashed;
-                const bool nf = m1.w != ~0u;
-                cb = m1.y;
-                cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
-                if (ch && nf) {
-                    nx = m1.w;
-                    fslot = m1.x;
-                    flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
-                    fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
-                    m0 = a.meta[2ull * nx];
-                    m1 = a.meta[2ull * nx + 1];
+        if (p != ~0u) {
+            MatCursor cur;
+            cur.begin(a, m0, ring);
+            const bool nf = m1.w != ~0u;
+            if (nf) {
+                fetch_fused_ops(a, m1.w, nm0, nm1, nt, nr, nolo, nohi, nhlo, nhhi);
+                if (nm1.w != ~0u) {
+                    nnm0 = a.meta[2ull * nm1.w];
+                    nnm1 = a.meta[2ull * nm1.w + 1];
                 }
             }
-            propagate(a, cb, cz);
-            p = nx;
-            listed = false;
+            ShaState st;
+            st.h[0] = hlo.x; st.h[1] = hlo.y; st.h[2] = hlo.z; st.h[3] = hlo.w;
+            st.h[4] = hhi.x; st.h[5] = hhi.y; st.h[6] = hhi.z; st.h[7] = hhi.w;
+            for (uint32_t b = 0; b < cur.nb; ++b) {
+                uint32_t w[16];
+                cur.block(a, b, ring, w);
+                sha256_compress(st, w);
+            }
+            const bool ch = finish_job_pre(a, m1, st, olo, ohi);
+            a.dirty[p] = 0u;
+            cb = m1.y;
+            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
+            if (ch && nf) {
+                nx = m1.w;
+                fslot = m1.x;
+                flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+            }
         }
+        propagate(a, cb, cz);
+        hashed += hash_fused_chain(a, ring, nx, nm0, nm1, nnm0, nnm1, nt, nr, nolo, nohi, nhlo, nhhi, fslot, flo, fhi);
     }
     count_fused(a, hashed);
     ws.end(a);
