@@ -1525,9 +1525,13 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
     return RF_OK;
 }
 
-// Change sets (input slots marked since the last step) from this size on run
-// their incremental levels in the lane-per-job throughput form (k2_level_lf).
-static constexpr uint64_t kThruSlots = 65536;
+// A level that can receive this many chains (min(level jobs, input slots
+// marked since the last step)) runs in the lane-per-job throughput form
+// (k2_level_lf): from 24k for levels of short jobs (the latency form holds
+// 16k chains at full speed, one 64-job workgroup per CU), from 64k for levels
+// of long jobs (inc_level 2: a lane alone hashes an 18-block job at ~5 us a
+// block, memory-latency-bound, against the three-wave latency form's ~1.5).
+static constexpr uint64_t kThruSlots = 24576, kThruSlotsWide = 65536;
 
 // The launch sequence (one kernel per level + a step-end kernel) only reads
 // device-side list lengths, so it is fixed for a loaded graph: capture it once
@@ -1545,13 +1549,15 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
     for (uint32_t l = 0; l < G.n_levels; ++l) any |= G.inc_level[l] != 0;
     if (plain && !full && any) {
         // the level-kernel forms for this step: a level that can receive at
-        // least RF_K2_THRU chains (default kThruSlots) fills the chip, and the
-        // lane-per-job form (k2_level_lf) outruns the two-lane latency form
-        // (k2_level_pl) there -- DESIGN.md §5
+        // least RF_K2_THRU chains (default kThruSlots; RF_K2_THRU_WIDE,
+        // default kThruSlotsWide, for levels of long jobs) fills the chip, and
+        // the lane-per-job form (k2_level_lf) outruns the two-lane latency
+        // form (k2_level_pl) there -- DESIGN.md §5
         const char* tv = getenv("RF_K2_THRU");  // (read per step: tests force either form)
-        const uint64_t thr = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
+        const char* tw = getenv("RF_K2_THRU_WIDE");
         G.step_marked = gr->marked;
-        G.thru_slots = thr;
+        G.thru_slots = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
+        G.thru_slots_wide = tw ? (uint64_t)strtoull(tw, nullptr, 10) : tv ? G.thru_slots : kThruSlotsWide;
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
@@ -1564,7 +1570,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         std::swap(G.counts, G.counts_other);
         return RF_OK;
     }
-    G.thru_slots = ~0ull;  // (captured sequences: the latency form)
+    G.thru_slots = G.thru_slots_wide = ~0ull;  // (captured sequences: the latency form)
     for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
     HIPC(launch_graph_step_end(G, full, s));
     gr->last_counts = G.counts_last;

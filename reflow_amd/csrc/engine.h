@@ -106,7 +106,7 @@ struct GraphDev {
     // >= thru_slots -- step_marked = the input slots marked for the step (an
     // upper bound of the chains that can reach the level), the level's size
     // the other bound (merge-tree levels stay in the latency form)
-    uint64_t step_marked = 0, thru_slots = ~0ull;
+    uint64_t step_marked = 0, thru_slots = ~0ull, thru_slots_wide = ~0ull;  // (wide: inc_level 2)
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     unsigned long long* wgst = nullptr;    // diagnostic per-workgroup records [L][2048][4] (RF_K2_WGSTAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the

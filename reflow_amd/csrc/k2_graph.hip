@@ -1900,7 +1900,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_PAD_KB");
             return v ? (uint32_t)atoi(v) * 1024u : 0u;
         }();
-        if (std::min<uint64_t>(e - b, g.step_marked) >= g.thru_slots) {
+        if (std::min<uint64_t>(e - b, g.step_marked) >= (g.inc_level[lvl] == 2 ? g.thru_slots_wide : g.thru_slots)) {
             // the throughput form: 256 lanes per workgroup, four resident per
             // CU, grid-stride over the device-side count
             static const uint64_t lf_cap = [] {
