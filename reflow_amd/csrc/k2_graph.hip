@@ -265,6 +265,22 @@ struct MatCursor {
         ring_put(ring, 0, t);
         t[0] = nt[4]; t[1] = nt[5]; t[2] = nt[6]; t[3] = nt[7];
     }
+    // begin() for a job with one hole, whose digest is handed over in
+    // registers (fslot / flo / fhi): only its hole record and template blocks
+    // are loaded (hash_fused_chain_lean; then block(..., one = true))
+    __device__ __forceinline__ void begin_fused(const LevelArgs& a, const uint4& m0, uint32_t* ring) {
+        T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
+        nb = m0.y;
+        he = m0.w;
+        hn = m0.z;
+        q0.r = a.holes[m0.z];
+        q1.r = q2.r = q3.r = r4 = r5 = make_uint2(~0u, 0u);
+        t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
+        ring_put(ring, 0, t);
+        if (nb > 1) {
+            t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
+        }
+    }
     // begin() for a fused job whose block 0 the chain wave builds (k2_level_pl,
     // cb0): the ring already holds its template blocks 0 and 1 with the
     // producer's digest OR-ed into the one hole, so the cursor starts at block
@@ -1555,80 +1571,34 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
     count_fused(a, hashed);
 }
 
-// Throughput form of an incremental level (GraphDev::thru: a step whose
-// change set fills the chip): one lane per listed job, 256-thread
-// workgroups, no producer / chain split -- every lane of every wave hashes
-// (one-lane rounds, the schedule in registers), so four workgroups share a
-// CU and their waves' issue slots interleave.  A listed job's fused chain is
-// followed in its lane (hash_fused_chain), as the mark kernel does for the
-// slot-fused chains.  k2_level_pl's two-lane chains shorten a link's latency
-// but keep only 64 jobs per 192-thread workgroup resident (two per CU), so
-// once a level's list is several times the resident set the step is bound by
-// rounds of resident workgroups x link latency (configs[3]'s 100M-node DAG
-// on one GPU), and this form is faster.
-__global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
-    constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                                0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    __shared__ uint32_t ring_all[kLevelBlock * kRing];
-    uint32_t* ring = &ring_all[threadIdx.x * kRing];
-    zero_other_counts(a);
-    WgStamp ws;
-    ws.begin(a);
-    const uint32_t n = a.counts[a.lvl];
-    const uint32_t* lst = a.list + a.s;
-    const uint4* lmt = a.lmeta + 2ull * a.s;
+// Hashes, one lane per chain, the fused chain that starts at job p (~0u:
+// none) with records m0/m1 and its one hole reading slot fslot, whose new
+// digest flo/fhi is handed over in registers -- as hash_fused_chain, without
+// fetching each next job's operands a job ahead (the throughput forms: other
+// waves of the SIMD cover the round trips, and the registers the look-ahead
+// needs would cost a wave per SIMD).  Returns the jobs this lane hashed.
+// Called by every lane of the wave.
+__device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, uint32_t* ring, uint32_t p, uint4 m0,
+                                                          uint4 m1, uint32_t fslot, uint4 flo, uint4 fhi) {
     uint32_t hashed = 0;
-    for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
-        if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
-        const uint32_t i = base + threadIdx.x;
-        uint32_t p = ~0u;
-        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, nm0 = m0, nm1 = m0, olo = m0, ohi = m0;
-        uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
-        if (i < n) {
-            const uint32_t ii = a.rev ? n - 1 - i : i;
-            p = lst[ii];
-            m0 = lmt[2ull * ii];  // the record append_jobs wrote beside the list
-            m1 = lmt[2ull * ii + 1];
-            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
-            olo = od[0];
-            ohi = od[1];
-            if (a.mid) {
-                hlo = a.mid[2ull * p];
-                hhi = a.mid[2ull * p + 1];
-            }
-            if (m1.w != ~0u) {
-                nm0 = a.meta[2ull * m1.w];
-                nm1 = a.meta[2ull * m1.w + 1];
-            }
-        }
-        // the fusion target's operands and records, fetched while p is hashed
-        // (hash_fused_chain then fetches each next target's a job ahead)
-        uint4 nt[8], nolo = olo, nohi = ohi, nnm0 = nm0, nnm1 = nm1;
-        uint4 nhlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nhhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
-        uint2 nr = make_uint2(~0u, 0u);
-        uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
-        uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo;
+    while (__any(p != ~0u)) {
+        uint32_t cb = 0, cz = 0, nx = ~0u;
         if (p != ~0u) {
             MatCursor cur;
-            cur.begin(a, m0, ring);
-            const bool nf = m1.w != ~0u;
-            if (nf) {
-                fetch_fused_ops(a, m1.w, nm0, nm1, nt, nr, nolo, nohi, nhlo, nhhi);
-                if (nm1.w != ~0u) {
-                    nnm0 = a.meta[2ull * nm1.w];
-                    nnm1 = a.meta[2ull * nm1.w + 1];
-                }
-            }
+            cur.fslot = fslot;
+            cur.flo = flo;
+            cur.fhi = fhi;
+            cur.begin_fused(a, m0, ring);
             ShaState st;
-            st.h[0] = hlo.x; st.h[1] = hlo.y; st.h[2] = hlo.z; st.h[3] = hlo.w;
-            st.h[4] = hhi.x; st.h[5] = hhi.y; st.h[6] = hhi.z; st.h[7] = hhi.w;
+            init_state(a, p, st);
             for (uint32_t b = 0; b < cur.nb; ++b) {
                 uint32_t w[16];
-                cur.block(a, b, ring, w);
+                cur.block(a, b, ring, w, true);
                 sha256_compress(st, w);
             }
-            const bool ch = finish_job_pre(a, m1, st, olo, ohi);
-            a.dirty[p] = 0u;
+            const bool ch = finish_job(a, m1, st);
+            ++hashed;
+            const bool nf = m1.w != ~0u;
             cb = m1.y;
             cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
             if (ch && nf) {
@@ -1636,16 +1606,20 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
                 fslot = m1.x;
                 flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
                 fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+                m0 = a.meta[2ull * nx];
+                m1 = a.meta[2ull * nx + 1];
             }
         }
         propagate(a, cb, cz);
-        hashed += hash_fused_chain(a, ring, nx, nm0, nm1, nnm0, nnm1, nt, nr, nolo, nohi, nhlo, nhhi, fslot, flo, fhi);
+        p = nx;
     }
-    count_fused(a, hashed);
-    ws.end(a);
+    return hashed;
 }
 
 constexpr uint32_t kMarkBlock = 64;
+// change sets from this size mark in k3_mark_slots_lf (the resident waves of
+// k3_mark_slots, two per SIMD at 240 VGPRs, hold 131k lanes)
+constexpr uint64_t kThruMark = 98304;
 
 // set_slots: write input digests; a changed slot queues (or hashes) its consumers.
 __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __restrict__ sl,
@@ -1675,6 +1649,120 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __re
         }
         mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
     }
+}
+
+// Throughput form of an incremental level (chosen per level and step when
+// the change set fills the chip, launch_graph_level): one lane per listed
+// job, 256-thread workgroups, no producer / chain split -- every lane of
+// every wave hashes (one-lane rounds, the schedule in registers).  A listed
+// job's fused chain is followed in its lane by hash_fused_chain_lean (one
+// hole, its digest handed over in registers, no look-ahead: 168 VGPRs, three
+// waves per SIMD; the look-ahead form needed 251 and two, and measured 2 %
+// slower on the 100M step).  k2_level_pl's two-lane chains shorten a link's
+// latency but keep only 64 jobs per 192-thread workgroup resident (two per
+// CU), so once a level's list is several times the resident set the step is
+// bound by rounds of resident workgroups x link latency (configs[3]'s
+// 100M-node DAG on one GPU), and this form is faster.
+__global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
+    __shared__ uint32_t ring_all[kLevelBlock * kRing];
+    uint32_t* ring = &ring_all[threadIdx.x * kRing];
+    zero_other_counts(a);
+    WgStamp ws;
+    ws.begin(a);
+    const uint32_t n = a.counts[a.lvl];
+    const uint32_t* lst = a.list + a.s;
+    const uint4* lmt = a.lmeta + 2ull * a.s;
+    uint32_t hashed = 0;
+    for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
+        if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
+        const uint32_t i = base + threadIdx.x;
+        uint32_t p = ~0u;
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        if (i < n) {
+            const uint32_t ii = a.rev ? n - 1 - i : i;
+            p = lst[ii];
+            m0 = lmt[2ull * ii];
+            m1 = lmt[2ull * ii + 1];
+        }
+        uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
+        uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
+        if (p != ~0u) {
+            MatCursor cur;
+            cur.begin(a, m0, ring);
+            ShaState st;
+            init_state(a, p, st);
+            for (uint32_t b = 0; b < cur.nb; ++b) {
+                uint32_t w[16];
+                cur.block(a, b, ring, w);
+                sha256_compress(st, w);
+            }
+            const bool ch = finish_job(a, m1, st);
+            a.dirty[p] = 0u;
+            const bool nf = m1.w != ~0u;
+            cb = m1.y;
+            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);
+            if (ch && nf) {
+                nx = m1.w;
+                fslot = m1.x;
+                flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+                nm0 = a.meta[2ull * nx];
+                nm1 = a.meta[2ull * nx + 1];
+            }
+        }
+        propagate(a, cb, cz);
+        hashed += hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi);
+    }
+    count_fused(a, hashed);
+    ws.end(a);
+}
+
+// k3_mark_slots for change sets that fill the chip (GraphDev::thru form
+// choice, at least kThruMark slots): the slot-fused chains without the
+// look-ahead (hash_fused_chain_lean), so three waves fit a SIMD instead of
+// two and a 100M-node DAG's 141k changed slots run in one round of resident
+// waves.
+__global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* __restrict__ sl,
+                                                               const uint8_t* __restrict__ dig, uint32_t n,
+                                                               LevelArgs a) {
+    __shared__ uint32_t ring_all[kMarkBlock * kRing];
+    uint32_t* ring = &ring_all[threadIdx.x * kRing];
+    uint32_t hashed = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        bool changed = false;
+        uint32_t s = 0, c = 0, ce = 0;
+        uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
+        if (i < n) {
+            s = sl[i];
+            const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
+            uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
+            nlo = src[0];
+            nhi = src[1];
+            c = a.cons_ptr[s];
+            ce = a.cons_ptr[s + 1];
+            const uint4 olo = dst[0], ohi = dst[1];
+            changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                      (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
+            if (changed) {
+                dst[0] = nlo;
+                dst[1] = nhi;
+            }
+        }
+        if (!changed) c = ce = 0;
+        uint32_t p = ~0u;
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        const uint2 f = a.cons[c < ce ? c : 0u];
+        if (c < ce && (f.y & kSlotFused)) {
+            p = f.x;
+            ++c;
+            m0 = a.meta[2ull * p];
+            m1 = a.meta[2ull * p + 1];
+        }
+        hashed += hash_fused_chain_lean(a, ring, p, m0, m1, s, nlo, nhi);
+        propagate(a, c, ce);  // the slot's other consumers
+    }
+    count_fused(a, hashed);
 }
 
 // ---- partitioned DAG exchange (partition.cpp) --------------------------------
@@ -1814,8 +1902,16 @@ static LevelArgs mark_level_args(const GraphDev& g) {
 hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k3_mark_slots, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, slots, digests, n,
-                       mark_level_args(g));
+    // RF_K2_THRU (as for the level kernels; read per call): the lean form from
+    // kThruMark slots
+    const char* tv = getenv("RF_K2_THRU");
+    const uint64_t thr = tv ? strtoull(tv, nullptr, 10) : kThruMark;
+    if (n >= thr)
+        hipLaunchKernelGGL(k3_mark_slots_lf, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, slots, digests, n,
+                           mark_level_args(g));
+    else
+        hipLaunchKernelGGL(k3_mark_slots, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, slots, digests, n,
+                           mark_level_args(g));
     return hipGetLastError();
 }
 
