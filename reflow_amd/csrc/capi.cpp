@@ -1539,12 +1539,20 @@ static constexpr uint64_t kThruSlots = 24576, kThruSlotsWide = 65536;
 // host launch each; MI355X_MICROARCH "boundary" / "graph-replay-floor").  An
 // incremental step leaves the dirty set empty (each hashed job clears its
 // bit); a full one discards whatever set_slots queued.
-static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = false) {
+// lvl_lo / lvl_hi / swap (plain incremental steps only): launch the levels in
+// [lvl_lo, lvl_hi), and whether this call ends the step (swaps the cursor
+// halves) -- a partitioned step may split its levels around the boundary
+// exchange (recompute_rounds, GraphPart::defer_lvl)
+static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = false, uint32_t lvl_lo = 0,
+                         uint32_t lvl_hi = ~0u, bool swap = true) {
     GraphDev& G = gr->g;
-    struct MarkedReset {  // every recompute consumes the change set marked before it
+    struct MarkedReset {  // every step consumes the change set marked before it
         rf_graph* gr;
-        ~MarkedReset() { gr->marked = 0; }
-    } marked_reset{gr};
+        bool on;
+        ~MarkedReset() {
+            if (on) gr->marked = 0;
+        }
+    } marked_reset{gr, swap || full || !plain};
     bool any = false;
     for (uint32_t l = 0; l < G.n_levels; ++l) any |= G.inc_level[l] != 0;
     if (plain && !full && any) {
@@ -1561,13 +1569,13 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
-        for (uint32_t l = 0; l < G.n_levels; ++l) {
+        for (uint32_t l = lvl_lo; l < std::min(lvl_hi, G.n_levels); ++l) {
             if (!G.inc_level[l]) continue;
             HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr));
             first = false;
         }
         gr->last_counts = G.counts;
-        std::swap(G.counts, G.counts_other);
+        if (swap) std::swap(G.counts, G.counts_other);
         return RF_OK;
     }
     G.thru_slots = G.thru_slots_wide = ~0ull;  // (captured sequences: the latency form)
@@ -1619,7 +1627,9 @@ static bool inc_plain() {
     return on;
 }
 
-int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
+bool graph_plain_steps() { return inc_plain(); }
+
+int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s, uint32_t lvl_lo, uint32_t lvl_hi, bool swap) {
     if (!gr->initialized) full = 1;
     const bool no_graph = inc_plain();
     static const bool full_plain = [] {  // RF_K2_FULL_GRAPH=0 (A/B): the full recompute as plain launches too
@@ -1632,7 +1642,7 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s) {
         // step's level launches (rocprofv3 trace)
         const bool ev = gr->time_next || events_always();
         if (ev) HIPC(hipEventRecord(gr->e0, s));
-        if (int rc = graph_enqueue(gr, full, s, true)) return rc;
+        if (int rc = graph_enqueue(gr, full, s, true, lvl_lo, lvl_hi, swap)) return rc;
         if (ev) HIPC(hipEventRecord(gr->e1, s));
         gr->timed = ev;
         gr->initialized = true;

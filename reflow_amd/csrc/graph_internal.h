@@ -22,6 +22,11 @@ struct GraphPart {
     DevBuf d_flag;
     HostBuf h_buf;            // host transport staging
     uint64_t last_supersteps = 0;
+    // Fixed-round protocol on a rank with imports and every export produced
+    // below the lowest level that reads an import: that level and the ones
+    // above wait for the exchange (one hash of the import readers per step
+    // instead of one before and one after it); ~0u: no deferral
+    uint32_t defer_lvl = ~0u;
 };
 
 struct rf_graph {
@@ -52,6 +57,9 @@ struct rf_graph {
 };
 
 
-int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s);
+// lvl_lo / lvl_hi / swap: plain incremental steps only (graph_enqueue)
+int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s, uint32_t lvl_lo = 0, uint32_t lvl_hi = ~0u,
+                           bool swap = true);
+bool graph_plain_steps();  // incremental steps are plain launches (not RF_K2_GRAPH=1)
 int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes);
 void graph_part_release(rf_graph* gr);

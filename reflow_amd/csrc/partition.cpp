@@ -96,6 +96,34 @@ extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "partition alloc: %s", hipGetErrorString(e));
     // nothing sent yet: every export counts as changed at the first exchange
     HIPC(sync_memset(ctx, P->d_snap.p, 0, 32ull * std::max<uint32_t>(p->n_export, 1)));
+    // Deferral (fixed rounds, plain steps): the lowest level reading an import
+    // and the highest level producing an export.  If every export is final
+    // before any import is read, the levels from the lowest import reader up
+    // wait for the exchange -- a step then hashes each import reader once
+    // (configs[3]'s global root on rank 0: 1+1 hashes of 5 blocks and five
+    // empty level launches fewer).  RF_PART_DEFER=0: off (A/B).
+    const char* dv = getenv("RF_PART_DEFER");
+    if (P->rounds && P->nranks > 1 && P->n_import && !(dv && atoi(dv) == 0)) {
+        const GraphDev& G = gr->g;
+        uint32_t lmin = ~0u;
+        for (uint32_t i = 0; i < p->n_import; ++i) {
+            uint32_t cp[2];
+            HIPC(sync_copy(ctx, cp, gr->b_cons_ptr.as<uint32_t>() + p->import_slot[i], 8, hipMemcpyDeviceToHost));
+            if (cp[1] <= cp[0]) continue;
+            std::vector<uint32_t> ce(2ull * (cp[1] - cp[0]));
+            HIPC(sync_copy(ctx, ce.data(), gr->b_cons_job.as<uint32_t>() + 2ull * cp[0], 4 * ce.size(),
+                           hipMemcpyDeviceToHost));
+            for (size_t k = 1; k < ce.size(); k += 2) lmin = std::min(lmin, ce[k] & 0x7fffffffu);  // (kSlotFused)
+        }
+        uint32_t emax = 0;
+        for (uint32_t i = 0; i < p->n_export; ++i) {
+            const uint32_t j = gr->ext2int[(size_t)gr->producer[p->export_slot[i]]];
+            const uint32_t l = (uint32_t)(std::upper_bound(G.lvl_start.begin(), G.lvl_start.end(), j) -
+                                          G.lvl_start.begin()) - 1;
+            emax = std::max(emax, l + 1);
+        }
+        if (lmin != ~0u && emax <= lmin) P->defer_lvl = lmin;
+    }
     return RF_OK;
 }
 
@@ -158,8 +186,13 @@ static int recompute_rounds(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn
                             uint64_t* out_recomputed, hipStream_t s) {
     GraphPart* P = gr->part;
     uint64_t tot = 0;
-    if (int rc = graph_recompute_locked(gr, full, s)) return rc;
-    if (out_recomputed)
+    // deferred levels (GraphPart::defer_lvl): the local pass stops below them
+    // and leaves the step open (no cursor swap: their queued jobs stay listed),
+    // the post-exchange passes start at them
+    const bool defer = P->defer_lvl != ~0u && !full && gr->initialized && graph_plain_steps();
+    const uint32_t lo = defer ? P->defer_lvl : 0u;
+    if (int rc = graph_recompute_locked(gr, full, s, 0, defer ? lo : ~0u, !defer)) return rc;
+    if (out_recomputed && !defer)  // (deferred: the post pass counts the whole step, same cursor half)
         if (int rc = part_counts(gr, s, &tot)) return rc;
     for (uint32_t r = 0; r < P->rounds; ++r) {
         if (P->n_export)
@@ -169,7 +202,7 @@ static int recompute_rounds(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn
         if (!P->n_import) continue;
         HIPC(launch_part_apply(gr->g, P->d_import_slot.as<uint32_t>(), P->d_import_bid.as<uint32_t>(), P->n_import,
                                nullptr, P->d_gather.as<uint8_t>(), s));
-        if (int rc = graph_recompute_locked(gr, 0, s)) return rc;
+        if (int rc = graph_recompute_locked(gr, 0, s, lo)) return rc;
         if (out_recomputed)
             if (int rc = part_counts(gr, s, &tot)) return rc;
     }

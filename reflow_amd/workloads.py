@@ -599,8 +599,11 @@ class PartitionedDag1000:
         five-node tail, the Merge-tree ancestors, and (rank 0, when anything
         anywhere changed) the global root.  Blocks are the full materials'
         (ceil((len + 9) / 64)), as the reference hashes them.  self.last_twice:
-        the jobs the partitioned recompute hashes twice (local pass, then
-        after the exchange) -- the device's count is jobs + last_twice."""
+        the jobs the partitioned recompute hashes twice -- none: rank 0 holds
+        the imports and no exports, so the library defers the levels from its
+        import readers up until after the exchange (GraphPart::defer_lvl) and
+        hashes the global root once; the device's count is jobs +
+        last_twice."""
         d, a = self.dag, self.desc
         blk = {k: (len(kk.tmpl) + 9 + 63) // 64 for k, kk in d.kinds.items()}
         f = np.asarray(file_slots, dtype=np.int64)
@@ -629,8 +632,4 @@ class PartitionedDag1000:
                 dirty.add(int(osl[j]))
                 jobs += 1
                 blocks += (int(tl[j]) + 9 + 63) // 64
-                # rf_graph_recompute_part hashes a job that reads imports in the
-                # local pass (its local deps changed) and again after the
-                # exchange (its imports changed): jobs hashed = jobs + this
-                self.last_twice += int(local and imported)
         return jobs, jobs - len(pairs), blocks
