@@ -61,6 +61,8 @@ CHAIN_CYCLES_PER_BLOCK = 64 * 3 * 4
 # two-lane lagged round is 8 instructions.
 DUO_INSTR_PER_ROUND = 8
 ISSUE_CYCLES_PER_INSTR = 4
+# k2_level_pl's two-lane round (lag_chain.h RF_L2_STEP): 9 instructions
+K2_INSTR_PER_ROUND = 9
 HBM_PEAK_GBS = 8000.0
 T_START = time.perf_counter()
 
@@ -205,6 +207,24 @@ def rank_sizes(args, dist):
                  "rank_bytes_max_over_min": float(np.bincount(owner, weights=allsz.astype(np.float64)).max()
                                                   / max(np.bincount(owner, weights=allsz.astype(np.float64)).min(), 1))}
     return mine, 0x5EED0004 + 0x100 * dist.rank, glob_info
+
+
+def latency_roofline(crit_blocks, ms):
+    """The incremental DAG step's latency roofline: its critical path is the
+    longest chain of dependent compressions the change set starts
+    (workloads critical_path: blocks, constant leading blocks excluded), and
+    no implementation hashes a chain faster than 64 rounds x 3 dependent VALU
+    x 4 cycles a block (the K1 skew-aware floor); the issue floor is the same
+    chain at k2_level_pl's 9-instruction two-lane round."""
+    t_chain = crit_blocks * CHAIN_CYCLES_PER_BLOCK / CLOCK_HZ
+    t_issue = crit_blocks * 64 * K2_INSTR_PER_ROUND * ISSUE_CYCLES_PER_INSTR / CLOCK_HZ
+    return {"bound": "critical path (latency)", "critical_path_blocks": int(crit_blocks),
+            "chain_floor_us": round(t_chain * 1e6, 2), "issue_floor_us": round(t_issue * 1e6, 2),
+            "achieved_us": round(ms * 1e3, 2), "frac": round(t_chain / (ms * 1e-3), 4),
+            "frac_of_issue_floor": round(t_issue / (ms * 1e-3), 4),
+            "peak_kind": "critical-path floor: the longest dependent-compression chain of the step x 64 rounds "
+                         "x 3 dependent VALU x 4 cycles @2.4GHz (frac = floor / step time); issue floor: the same "
+                         "chain x 9 instructions a round (two-lane chain) x 4 cycles"}
 
 
 def kernel_roofline(name, lens, ids, ms):
@@ -556,6 +576,7 @@ def bench_dag(args, dist, ctx, budget):
            "full_recompute_ms": full_ms,
            "full_recompute_mnodes_per_s": dag.n_nodes / (full_ms * 1e-3) / 1e6,
            "levels": g.stats().n_levels, "build_s": round(t_build, 2), "load_s": round(t_load, 2)}
+    res["roofline_latency"] = latency_roofline(dag.critical_path(slots), res["device_ms_per_step"])
     st = g.stats()
     ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
     res["roofline_full"] = {"bound": "valu", "achieved": round(ach, 2), "peak": round(SHA_VALU_PEAK_GBS, 1),
@@ -669,6 +690,9 @@ def bench_dag100m(args, dist, ctx, comm, budget):
            "exchange": ("none (1 rank)" if not multi else "RCCL all-gather of %d part roots" % nparts if comm
                         else "gloo host all-gather of %d part roots" % nparts),
            "per_rank": per_rank,
+           # (N > 1: rank 0's path also runs through the global root, and
+           # every part's chain is the same shape)
+           "roofline_latency": latency_roofline(dist.max(float(pc.critical_path(slots))), t / steps * 1e3),
            "roofline_incremental": {
                "bound": "valu", "achieved_tops": round(ops / (t / steps) / 1e12, 3),
                "peak_tops": round(dist.world * VALU_LANE_OPS / 1e12, 1),

@@ -138,6 +138,14 @@ class _Kind:
         self.holes.append((pos, np.asarray(slots, dtype=np.uint32)))
 
 
+def _kind_blocks(kk):
+    """Blocks an incremental recompute of one job of kind kk must hash: its
+    padded material's, less the constant leading blocks before its first hole
+    (hashed once at load, the midstate)."""
+    nb = (len(kk.tmpl) + 9 + 63) // 64
+    return nb - (min(p for p, _ in kk.holes) // 64 if kk.holes else 0)
+
+
 class Dag1000:
     """1000align-shaped DAG: S samples x P read pairs (~S*(14P+5) nodes).
 
@@ -380,6 +388,20 @@ class Dag1000:
         hole_ptr[1:] = np.cumsum(nh)
         return dict(n_slots=self.n_slots, out_slot=out_slot, tmpl_off=off, tmpl_len=ln, hole_ptr=hole_ptr,
                     hole_pos=np.concatenate(hpos), hole_slot=np.concatenate(hslot), blob=blob)
+
+    def critical_path(self, file_slots):
+        """The longest chain of dependent compressions a change of leaf-file
+        slots `file_slots` starts: Val -> Coerce -> the pair's ten-job chain
+        (E1 .. C7) -> the sample's tail (KS .. XS), in blocks (0 if nothing
+        changed).  Every dirty pair's chain has this shape, so the maximum is
+        over the two leaf parities present."""
+        f = np.asarray(file_slots, dtype=np.int64)
+        if not len(f):
+            return 0
+        b = {k: _kind_blocks(kk) for k, kk in self.kinds.items()}
+        lead = max([b["V1"] + b["C1"]] * bool((f % 2 == 0).any()) + [b["V2"] + b["C2"]] * bool((f % 2).any()))
+        chain = ("E1", "C3", "K1", "C4", "E2", "C5", "K2", "C6", "E3", "C7")
+        return lead + sum(b[k] for k in chain) + sum(b[k] for k in self.SAMPLE_KINDS)
 
     def change_set(self, frac=0.01, seed=0x5EED0003, n_global=None):
         """File slots to change (1% of leaf files) and their two versions:
@@ -633,3 +655,26 @@ class PartitionedDag1000:
                 jobs += 1
                 blocks += (int(tl[j]) + 9 + 63) // 64
         return jobs, jobs - len(pairs), blocks
+
+    def critical_path(self, file_slots):
+        """The longest chain of dependent compressions in this piece for a
+        change of its leaf-file slots: the Dag1000 chain to a dirty sample
+        root, then the Merge tree above it and (rank 0) the global root --
+        blocks, each job's constant leading blocks excluded."""
+        d, a = self.dag, self.desc
+        f = np.asarray(file_slots, dtype=np.int64)
+        base = d.critical_path(f)
+        if not base:
+            return 0
+        dirty_xs = set(d.kinds["XS"].out_slot[np.unique(f // 2 // d.P)].tolist())
+        hp, hs, hpos = a["hole_ptr"], a["hole_slot"], a["hole_pos"]
+        osl, tl = a["out_slot"], a["tmpl_len"]
+        path = {s: base for s in dirty_xs}
+        best = base
+        for j in range(d.n_jobs, len(osl)):  # the appended jobs, in dependency order
+            deps = [path[x] for x in hs[int(hp[j]):int(hp[j + 1])].tolist() if x in path]
+            if deps:
+                lead = int(hpos[int(hp[j])]) // 64 if hp[j + 1] > hp[j] else 0
+                path[int(osl[j])] = max(deps) + (int(tl[j]) + 9 + 63) // 64 - lead
+                best = max(best, path[int(osl[j])])
+        return best

@@ -76,3 +76,34 @@ def test_c2_sizes_distribution():
     assert lens[big].sum() / lens.sum() > 0.9  # most bytes in the big files
     offs, total = arena_layout(lens)
     assert (offs % 256 == 0).all() and total >= int(lens.sum())
+
+
+def _critical_path_dp(desc, changed):
+    """Generic longest path, in blocks, over the jobs a change of `changed`
+    slots dirties (creation order is a dependency order): each job counts its
+    blocks after the constant leading ones (before its first hole)."""
+    osl, tl, hp, hs, hpos = (desc[k] for k in ("out_slot", "tmpl_len", "hole_ptr", "hole_slot", "hole_pos"))
+    path = {int(s): 0 for s in changed}
+    best = 0
+    for j in range(len(osl)):
+        deps = [path[x] for x in hs[int(hp[j]):int(hp[j + 1])].tolist() if x in path]
+        if deps:
+            lead = int(hpos[int(hp[j])]) // 64
+            path[int(osl[j])] = max(deps) + (int(tl[j]) + 9 + 63) // 64 - lead
+            best = max(best, path[int(osl[j])])
+    return best
+
+
+def test_critical_path_matches_generic_dp():
+    """bench.py's latency floor for the DAG legs (critical_path) == a generic
+    longest-path DP over the dirtied jobs, for configs[2]'s shape and a piece
+    of the strong-scaling layout (its Merge tree and global root)."""
+    from reflow_amd.workloads import Dag1000, PartitionedDag1000
+    d = Dag1000(40, 8)
+    for frac in (0.01, 0.2):
+        s, _, _ = d.change_set(frac)
+        assert d.critical_path(s) == _critical_path_dp(d.arrays(), s)
+    for nranks, rank in ((1, 0), (2, 0), (2, 1)):
+        p = PartitionedDag1000(300, 8, nranks, rank, nparts=2)
+        s, _, _ = p.dag.change_set(0.02, n_global=2 * 8 * 300 * 2)
+        assert p.critical_path(s) == _critical_path_dp(p.desc, s) > d.critical_path(s)
