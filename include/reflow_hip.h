@@ -341,7 +341,14 @@ int rf_graph_set_slots_device(rf_graph *g, const void *d_slots, const void *d_di
 /* Recompute dirty jobs level by level (K3 frontier + K2 node digests).
  * full != 0 recomputes every job.  Early cut-off: a job whose digest did not
  * change does not dirty its consumers.  *out_recomputed (may be NULL) receives
- * the number of jobs hashed (synchronises). */
+ * the number of jobs hashed (synchronises).
+ * Each incremental level runs in one of two kernel forms, chosen per level
+ * and step from the input slots marked since the last step (set_slots /
+ * update): the two-lane latency form, or -- when min(level jobs, marked
+ * slots) reaches 24,576 (65,536 for levels of long jobs) -- the lane-per-job
+ * throughput form; change sets of >= 98,304 slots also mark in the
+ * throughput form.  Results are identical; RF_K2_THRU / RF_K2_THRU_WIDE
+ * (read per step) override the thresholds (0: always the throughput form). */
 int rf_graph_recompute(rf_graph *g, int full, uint64_t *out_recomputed);
 /* Asynchronous form (no count readback). */
 int rf_graph_recompute_async(rf_graph *g, int full, void *stream);

@@ -1584,6 +1584,16 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
     while (__any(p != ~0u)) {
         uint32_t cb = 0, cz = 0, nx = ~0u;
         if (p != ~0u) {
+            // issued at the job's start, used at its end: its old digest and
+            // its fusion target's record (two round trips off each link)
+            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+            const uint4 olo = od[0], ohi = od[1];
+            const bool nf = m1.w != ~0u;
+            uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0;
+            if (nf) {
+                nm0 = a.meta[2ull * m1.w];
+                nm1 = a.meta[2ull * m1.w + 1];
+            }
             MatCursor cur;
             cur.fslot = fslot;
             cur.flo = flo;
@@ -1596,9 +1606,8 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
                 cur.block(a, b, ring, w, true);
                 sha256_compress(st, w);
             }
-            const bool ch = finish_job(a, m1, st);
+            const bool ch = finish_job_pre(a, m1, st, olo, ohi);
             ++hashed;
-            const bool nf = m1.w != ~0u;
             cb = m1.y;
             cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
             if (ch && nf) {
@@ -1606,8 +1615,8 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
                 fslot = m1.x;
                 flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
                 fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
-                m0 = a.meta[2ull * nx];
-                m1 = a.meta[2ull * nx + 1];
+                m0 = nm0;
+                m1 = nm1;
             }
         }
         propagate(a, cb, cz);
