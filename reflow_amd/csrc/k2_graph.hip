@@ -343,6 +343,146 @@ struct MatCursor {
     }
 };
 
+// The producer wave's material cursor in k2_level_pl: MatCursor's template
+// stream, with the holes in chunks of four per job.  While chunk c is applied
+// from the lane's LDS buffer, chunk c+1's digests and chunk c+2's records are
+// in flight in fixed registers; at the first hole of chunk c+1 (a transition)
+// chunk c+1's records and digests go to LDS buffer (c+1) & 1, chunk c+2's
+// records move in, and chunk c+2's digests and chunk c+3's records are
+// issued.  Every register move or store reads loads issued a chunk (about two
+// blocks) earlier: MatCursor's queue moved digests issued one block earlier
+// and waited for them (an 18-block Merge job's producer took 1.1-1.9 us a
+// block against the chain's 1.36, RF_K2_STAMPS=3).
+constexpr uint32_t kHq = 73;  // words per lane: [2 chunks][4 holes][pos + 8 digest words] + 1 (odd stride)
+struct ChunkCursor {
+    const uint4* __restrict__ T;
+    uint32_t nb, he, h0, hn, staged;  // holes [h0, he), hn the next to apply, staged: chunks in LDS
+    uint4 t[4];
+    uint32_t fslot = ~0u;  // a slot whose new digest is handed over in registers (fused chains)
+    uint4 flo, fhi;
+    uint2 single;          // one-hole fused jobs (begin_pre): the hole's record
+    uint2 rn[4], rnn[4];   // records of chunks c+1 and c+2
+    uint4 dlo[4], dhi[4];  // digests of chunk c+1
+    uint32_t* hq;          // the lane's LDS buffers
+
+    __device__ __forceinline__ uint2 record(const LevelArgs& a, uint32_t h) const {
+        const uint2 v = a.holes[h < he ? h : 0u];
+        return h < he ? v : make_uint2(~0u, 0u);
+    }
+    __device__ __forceinline__ void load_records(const LevelArgs& a, uint32_t c, uint2 (&r)[4]) const {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = record(a, h0 + 4 * c + q);
+    }
+    __device__ __forceinline__ void load_digests(const LevelArgs& a, const uint2 (&r)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * (r[q].x == ~0u ? 0u : r[q].y));
+            dlo[q] = src[0];
+            dhi[q] = src[1];
+        }
+    }
+    // chunk c's records r and digests dlo/dhi into LDS buffer c & 1
+    __device__ __forceinline__ void stash(uint32_t c, const uint2 (&r)[4]) const {
+        uint32_t* q = hq + (c & 1) * 36;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool f = r[k].y == fslot && r[k].x != ~0u;
+            const uint4 lo = f ? flo : dlo[k], hi = f ? fhi : dhi[k];
+            q[9 * k] = r[k].x;
+            q[9 * k + 1] = lo.x; q[9 * k + 2] = lo.y; q[9 * k + 3] = lo.z; q[9 * k + 4] = lo.w;
+            q[9 * k + 5] = hi.x; q[9 * k + 6] = hi.y; q[9 * k + 7] = hi.z; q[9 * k + 8] = hi.w;
+        }
+    }
+    __device__ __forceinline__ void begin(const LevelArgs& a, const uint4& m0, uint32_t* ring) {
+        T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
+        nb = m0.y;
+        he = m0.w;
+        h0 = hn = m0.z;
+        single = make_uint2(~0u, 0u);
+        uint2 r0[4];
+        load_records(a, 0, r0);
+        load_records(a, 1, rn);
+        load_records(a, 2, rnn);
+        t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
+        load_digests(a, r0);
+        stash(0, r0);
+        load_digests(a, rn);  // chunk 1's, in flight until its transition
+        staged = 1;
+        ring_put(ring, 0, t);
+        if (nb > 1) {
+            t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
+        }
+    }
+    // (as MatCursor's) a fused job: one hole, its digest handed over in registers
+    __device__ __forceinline__ void begin_pre(const uint4& m0, const uint4* __restrict__ tmpl, const uint4 (&nt)[8],
+                                              const uint2& nr, uint32_t* ring) {
+        T = tmpl + 4ull * m0.x;
+        nb = m0.y;
+        he = m0.w;
+        h0 = hn = m0.z;
+        single = nr;
+        t[0] = nt[0]; t[1] = nt[1]; t[2] = nt[2]; t[3] = nt[3];
+        ring_put(ring, 0, t);
+        t[0] = nt[4]; t[1] = nt[5]; t[2] = nt[6]; t[3] = nt[7];
+    }
+    __device__ __forceinline__ void begin_chain(const uint4& m0, const uint4* __restrict__ tmpl) {
+        T = tmpl + 4ull * m0.x;
+        nb = m0.y;
+        he = m0.w;
+        h0 = hn = m0.z;
+        single = make_uint2(~0u, 0u);
+        if (nb > 2) {
+            t[0] = T[8]; t[1] = T[9]; t[2] = T[10]; t[3] = T[11];
+        }
+    }
+    // the next hole hn: its chunk staged first (a transition), then applied
+    // if it starts below lim
+    __device__ __forceinline__ void next_hole(const LevelArgs& a, uint32_t* ring, uint32_t lim) {
+        if (hn >= he) return;
+        const uint32_t c = (hn - h0) >> 2;
+        if (c >= staged) {  // chunk c (= staged) enters: stash it, move the pipeline on
+            stash(c, rn);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rn[q] = rnn[q];
+            load_digests(a, rn);
+            load_records(a, c + 2, rnn);
+            staged = c + 1;
+        }
+        const uint32_t* q = hq + (c & 1) * 36 + 9 * ((hn - h0) & 3);
+        const uint32_t pos = q[0];
+        if (pos < lim) {
+            const uint32_t D[8] = {q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8]};
+            or_digest(ring, pos, D);
+            ++hn;
+        }
+    }
+    __device__ __forceinline__ void block(const LevelArgs& a, uint32_t b, uint32_t* ring, uint32_t (&w)[16],
+                                          bool one = false) {
+        const uint32_t half = (b & 1) * 16;
+        if (b + 1 < nb) {
+            ring_put(ring, half ^ 16, t);
+            if (b + 2 < nb) {
+                const uint4* s = T + 4 * (b + 2);
+                t[0] = s[0]; t[1] = s[1]; t[2] = s[2]; t[3] = s[3];
+            }
+        }
+        const uint32_t lim = 64 * (b + 1);
+        if (one) {
+            if (single.x < lim) {  // (the hole reads the handed-over slot: begin_pre)
+                const uint32_t D[8] = {flo.x, flo.y, flo.z, flo.w, fhi.x, fhi.y, fhi.z, fhi.w};
+                or_digest(ring, single.x, D);
+                single = make_uint2(~0u, 0u);
+            }
+        } else {
+            // holes that start in block b: at most two (they are >= 32 B apart)
+            next_hole(a, ring, lim);
+            next_hole(a, ring, lim);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
+    }
+};
+
 // Store the digest into its slot if it changed (always in full mode).
 __device__ __forceinline__ bool finish_job(const LevelArgs& a, const uint4& m1, const ShaState& st) {
     uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * m1.x);
@@ -834,6 +974,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint4 s_pp[64][2];   // cb0: a finished job's {id, consumer range, valid}, first two edges
     __shared__ uint32_t s_w0[kStream ? 64 * 17 : 1];  // stream cb0: W[0..15] per job, staged by the chain
     __shared__ uint32_t s_cw[2];                      // ... block id + 1 staged, per chain wave
+    __shared__ uint32_t s_hq[64 * kHq];               // the producer's hole chunks (ChunkCursor)
     __shared__ unsigned long long s_stamp[2][64];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -967,7 +1108,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     // the chain idles in a pass-0 job's first iteration anyway)
                     if (kChain && !RF_K2_JOIN_WAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
                 }
-                MatCursor cur;
+                ChunkCursor cur;
+                cur.hq = &s_hq[lane * kHq];
                 uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
                 uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
                 if (!kStream && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
@@ -1202,7 +1344,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         if (pb < m0.y && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
                             uint32_t w[16];
                             cur.block(a, pb, ring, w, wfused);
-                            if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
+                            // (RF_K2_STAMPS=3: every block's assembly end on the producer)
+                            if ((a.dbg_twice == 2 && it == 0) || a.dbg_twice == 8) { RF_STAMP_PL(sk); ++sk; }
                             if (kW == 2) {
                                 kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((pb & 1) * 64 + lane) * kPcRow]));
                             } else {
@@ -1956,6 +2099,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     // =6 (A/B): k2_level_pl<3>'s frontier atomics on the chain, not the producer
     static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u
                                  : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u
+                                 : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 3) ? 8u
                                  : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
                                                               : 0u;
     // RF_K2_CB0=0: fused jobs' block 0 built by the producer (A/B), else by the chain
