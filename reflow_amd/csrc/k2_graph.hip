@@ -459,13 +459,11 @@ struct ChunkCursor {
     __device__ __forceinline__ void block(const LevelArgs& a, uint32_t b, uint32_t* ring, uint32_t (&w)[16],
                                           bool one = false) {
         const uint32_t half = (b & 1) * 16;
-        if (b + 1 < nb) {
-            ring_put(ring, half ^ 16, t);
-            if (b + 2 < nb) {
-                const uint4* s = T + 4 * (b + 2);
-                t[0] = s[0]; t[1] = s[1]; t[2] = s[2]; t[3] = s[3];
-            }
-        }
+        // the next block's template into the ring first (a hole may run into
+        // it); block b+2's template is issued only after the holes: the
+        // compiler's waits in a transition are vmcnt(0), and a load issued
+        // just before them would be waited for in full
+        if (b + 1 < nb) ring_put(ring, half ^ 16, t);
         const uint32_t lim = 64 * (b + 1);
         if (one) {
             if (single.x < lim) {  // (the hole reads the handed-over slot: begin_pre)
@@ -477,6 +475,10 @@ struct ChunkCursor {
             // holes that start in block b: at most two (they are >= 32 B apart)
             next_hole(a, ring, lim);
             next_hole(a, ring, lim);
+        }
+        if (b + 2 < nb) {
+            const uint4* s = T + 4 * (b + 2);
+            t[0] = s[0]; t[1] = s[1]; t[2] = s[2]; t[3] = s[3];
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
