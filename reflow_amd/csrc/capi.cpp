@@ -1297,16 +1297,38 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // anyway (one holding queueable non-sink jobs), where they fill their own
     // workgroups beside that level's longer chains instead of lengthening an
     // earlier level's (configs[2]: the pE1 keys, 4 blocks, left level 0's
-    // 1+2-block Val -> Coerce chains waiting).  RF_K2_SINK_ALAP=0: off (A/B).
+    // 1+2-block Val -> Coerce chains waiting).
+    // Default (RF_K2_SINK_ALAP=2): the last such level whose non-sink
+    // queueable jobs number at least 1/64 of the sinks -- a level wide enough
+    // that the sinks do not wait behind a few long merge jobs (the 100M
+    // layout's part roots, 15 blocks each, held its 140k pE1 keys in the
+    // throughput form's lanes: 0.820 -> 0.781 ms/step; configs[2] and the
+    // 8-rank piece unchanged, profiles/r03/s3/sink_fill_ab.log).
+    // RF_K2_SINK_ALAP=1: the last level (A/B); 0: off.
     {
-        static const bool alap = [] {
+        static const int alap = [] {
             const char* v = getenv("RF_K2_SINK_ALAP");
-            return !(v && atoi(v) == 0);
+            return v ? atoi(v) : 2;
         }();
         auto sink = [&](uint32_t j) { return cptr[d->out_slot[j]] == cptr[d->out_slot[j] + 1]; };
         int64_t lq = -1;
+        std::vector<uint64_t> nsq(L, 0);
+        uint64_t n_sink = 0;
         for (uint32_t j = 0; j < J; ++j)
-            if (queueable(j) && !sink(j)) lq = std::max<int64_t>(lq, level[j]);
+            if (queueable(j)) {
+                if (!sink(j)) {
+                    lq = std::max<int64_t>(lq, level[j]);
+                    nsq[level[j]]++;
+                } else {
+                    n_sink++;
+                }
+            }
+        if (alap == 2)
+            for (int64_t l = lq; l > 0; --l)
+                if (nsq[l] * 64 >= n_sink) {
+                    lq = l;
+                    break;
+                }
         if (alap && lq > 0)
             for (uint32_t j = 0; j < J; ++j)
                 if (queueable(j) && sink(j) && level[j] < (uint32_t)lq) level[j] = (uint32_t)lq;
