@@ -1298,13 +1298,17 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // workgroups beside that level's longer chains instead of lengthening an
     // earlier level's (configs[2]: the pE1 keys, 4 blocks, left level 0's
     // 1+2-block Val -> Coerce chains waiting).
-    // Default (RF_K2_SINK_ALAP=2): the last such level whose non-sink
-    // queueable jobs number at least 1/64 of the sinks -- a level wide enough
-    // that the sinks do not wait behind a few long merge jobs (the 100M
+    // RF_K2_SINK_ALAP=3: the last such level whose non-sink queueable jobs
+    // number at least 1/64 of the sinks (the fill level) -- a level wide
+    // enough that the sinks do not wait behind a few long merge jobs (the 100M
     // layout's part roots, 15 blocks each, held its 140k pE1 keys in the
     // throughput form's lanes: 0.820 -> 0.781 ms/step; configs[2] and the
-    // 8-rank piece unchanged, profiles/r03/s3/sink_fill_ab.log).
-    // RF_K2_SINK_ALAP=1: the last level (A/B); 0: off.
+    // 8-rank piece unchanged, profiles/r03/s3/sink_fill_ab.log).  Default (2):
+    // those sinks in a level of their own whose list a plain step attaches to
+    // the first throughput-form launch from their inputs' level up to the
+    // fill level, else to the fill level's launch.  1: the last level (A/B);
+    // 0: off.
+    uint32_t sink_fill = ~0u, sink_min = 0;
     {
         static const int alap = [] {
             const char* v = getenv("RF_K2_SINK_ALAP");
@@ -1323,15 +1327,32 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
                     n_sink++;
                 }
             }
-        if (alap == 2)
+        if (alap >= 2)
             for (int64_t l = lq; l > 0; --l)
                 if (nsq[l] * 64 >= n_sink) {
                     lq = l;
                     break;
                 }
-        if (alap && lq > 0)
+        if (alap == 2 && lq > 0) {
+            // the sinks whose inputs are final by the fill level get a level of
+            // their own, the last; its list runs attached to a level launch
+            // (GraphDev kLvlSink, graph_enqueue)
+            uint32_t smin = 0, nm = 0;
+            for (uint32_t j = 0; j < J; ++j)
+                if (queueable(j) && sink(j) && level[j] <= (uint32_t)lq) {
+                    smin = std::max(smin, level[j]);
+                    level[j] = L;
+                    ++nm;
+                }
+            if (nm) {
+                sink_fill = (uint32_t)lq;
+                sink_min = smin;
+                ++L;
+            }
+        } else if (alap && lq > 0) {
             for (uint32_t j = 0; j < J; ++j)
                 if (queueable(j) && sink(j) && level[j] < (uint32_t)lq) level[j] = (uint32_t)lq;
+        }
     }
     // internal order: level ascending, blocks descending (similar lanes per wave)
     std::vector<uint32_t> perm(J);
@@ -1427,7 +1448,13 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
             }
         for (uint32_t l = 0; l < L; ++l)
             if (qall[l]) gr->g.inc_level[l] = (wide && qj[l] && qb[l] >= wide * qj[l]) ? 2 : 1;
+        if (sink_fill != ~0u) {
+            gr->g.inc_level[L - 1] |= kLvlSink;
+            gr->g.inc_level[sink_fill] |= kLvlFill;
+            gr->g.inc_level[sink_min] |= kLvlSinkMin;
+        }
     }
+    gr->g.sink_attach_ok = true;
     gr->tmpl_bytes = tb;
     // upload
     GraphDev& G = gr->g;
@@ -1576,7 +1603,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         }
     } marked_reset{gr, swap || full || !plain};
     bool any = false;
-    for (uint32_t l = 0; l < G.n_levels; ++l) any |= G.inc_level[l] != 0;
+    for (uint32_t l = 0; l < G.n_levels; ++l) any |= (G.inc_level[l] & kLvlForm) != 0;
     if (plain && !full && any) {
         // the level-kernel forms for this step: a level that can receive at
         // least RF_K2_THRU chains (default kThruSlots; RF_K2_THRU_WIDE,
@@ -1588,12 +1615,31 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         G.step_marked = gr->marked;
         G.thru_slots = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
         G.thru_slots_wide = tw ? (uint64_t)strtoull(tw, nullptr, 10) : tv ? G.thru_slots : kThruSlotsWide;
+        // the sink level's list rides on the launch of the last level from
+        // kLvlSinkMin to kLvlFill that runs in the throughput form (the short
+        // sink jobs fill SIMDs its waves leave idle; the latency form is a
+        // poor fit for them), else on the fill level's (GraphDev kLvlSink).  The choice depends only on the
+        // step's forms, so the calls of a deferred partitioned step agree.
+        uint32_t sink = ~0u, attach = ~0u;
+        {
+            uint32_t fill = ~0u, smin = 0;
+            for (uint32_t l = 0; l < G.n_levels; ++l) {
+                if (G.inc_level[l] & kLvlSink) sink = l;
+                if (G.inc_level[l] & kLvlFill) fill = l;
+                if (G.inc_level[l] & kLvlSinkMin) smin = l;
+            }
+            if (sink != ~0u && fill != ~0u && G.sink_attach_ok) {
+                for (uint32_t l = fill + 1; l-- > smin && attach == ~0u;)
+                    if ((G.inc_level[l] & kLvlForm) && graph_level_lf(G, l)) attach = l;
+                if (attach == ~0u) attach = fill;
+            }
+        }
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
         for (uint32_t l = lvl_lo; l < std::min(lvl_hi, G.n_levels); ++l) {
-            if (!G.inc_level[l]) continue;
-            HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr));
+            if (!(G.inc_level[l] & kLvlForm) || (l == sink && attach != ~0u)) continue;
+            HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr, l == attach ? sink : ~0u));
             first = false;
         }
         gr->last_counts = G.counts;

@@ -64,6 +64,14 @@ hipError_t launch_gen_fill(uint8_t* arena, const uint64_t* offs, const uint64_t*
                            uint64_t seed, uint64_t arena_bytes, hipStream_t s);
 
 // ---- K2/K3: digest DAG -----------------------------------------------------
+// GraphDev::inc_level flags.  The sink level (kLvlSink, the last level) holds
+// the queueable jobs nothing reads (physical cache keys) whose inputs are
+// final by the fill level (kLvlFill); its list is attached to the launch of
+// the last level from kLvlSinkMin (the highest level a sink's inputs need
+// below it) to the fill level that runs in the throughput form -- the sinks
+// fill the SIMDs a wide level's waves leave idle -- else to the fill level's
+// launch.
+constexpr uint8_t kLvlForm = 3, kLvlSinkMin = 0x20, kLvlFill = 0x40, kLvlSink = 0x80;
 struct GraphDev {
     uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;
     // jobs in internal (level) order
@@ -89,7 +97,14 @@ struct GraphDev {
     uint32_t* counts_other = nullptr;
     uint32_t* lvl_start_dev = nullptr; // [L+1]
     std::vector<uint32_t> lvl_start; // host copy [L+1]
-    std::vector<uint8_t> inc_level;  // [L] level has jobs that can be queued (not all fusion targets)
+    // [L] per level: bits kLvlForm = 1 (has jobs that can be queued, i.e. not
+    // all fusion targets) or 2 (those average >= RF_K2_WIDE blocks), 0 = never
+    // launched by an incremental step; plus the sink-list flags below
+    std::vector<uint8_t> inc_level;
+    // plain incremental steps: the sink level's list runs attached to another
+    // level's launch (graph_enqueue), not as a level of its own -- unless a
+    // partition import feeds one of its jobs (rf_graph_set_part)
+    bool sink_attach_ok = true;
     // every job's first hole starts in block 0 of its (midstate-trimmed)
     // template, so a fusion target's block 0 can be built by the chain wave
     // (k2_level_pl cb0); false only for the RF_K2_NO_MIDSTATE A/B load
@@ -126,14 +141,15 @@ struct MarkArgs {
     const uint32_t* sl;
     const uint8_t* dig;
     uint32_t n;
-    alignas(16) unsigned char a[160];  // the kernel's LevelArgs (k2_graph.hip), by value
+    alignas(16) unsigned char a[176];  // the kernel's LevelArgs (k2_graph.hip), by value
     void* ptrs[4];
 };
 void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,
                        MarkArgs* args, hipKernelNodeParams* p);
 const void* graph_mark_kernel();
 hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s,
-                              uint32_t* zero_counts = nullptr);
+                              uint32_t* zero_counts = nullptr, uint32_t sink_lvl = ~0u);
+bool graph_level_lf(const GraphDev& g, uint32_t lvl);
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);

@@ -68,6 +68,21 @@ struct LevelArgs {
     uint32_t rev;
     uint32_t* zero_counts;  // [L+1] the previous plain step's cursor half, zeroed by workgroup 0 (or null)
     unsigned long long* wgst;  // diagnostic (RF_K2_WGSTAMPS=1): per-workgroup records [L][kWgStamps][4], else null
+    // an attached sink list (k2_level_pl / k2_level_lf): the sink level lvl2's
+    // list (at s2) is taken after this level's own, in the same launch
+    // (graph_enqueue, GraphDev kLvlSink); lvl2 = ~0u: none
+    uint32_t s2 = 0, lvl2 = ~0u;
+};
+
+// Entries of a level launch: the level's own list (from its end when rev),
+// then the attached sink list.  Offsets into a.list / a.lmeta.
+struct LaunchList {
+    uint32_t n1, n;
+    __device__ __forceinline__ explicit LaunchList(const LevelArgs& a)
+        : n1(a.counts[a.lvl]), n(n1 + (a.lvl2 != ~0u ? a.counts[a.lvl2] : 0u)) {}
+    __device__ __forceinline__ uint32_t at(const LevelArgs& a, uint32_t i) const {
+        return i < n1 ? a.s + (a.rev ? n1 - 1 - i : i) : a.s2 + (i - n1);
+    }
 };
 
 // Diagnostic per-workgroup record of an incremental level kernel: start and
@@ -344,7 +359,7 @@ struct MatCursor {
 };
 
 // The producer wave's material cursor in k2_level_pl: MatCursor's template
-// stream, with the holes in chunks of four per job.  While chunk c is applied
+// stream, with the holes in chunks of kHC per job.  While chunk c is applied
 // from the lane's LDS buffer, chunk c+1's digests and chunk c+2's records are
 // in flight in fixed registers; at the first hole of chunk c+1 (a transition)
 // chunk c+1's records and digests go to LDS buffer (c+1) & 1, chunk c+2's
@@ -353,7 +368,16 @@ struct MatCursor {
 // blocks) earlier: MatCursor's queue moved digests issued one block earlier
 // and waited for them (an 18-block Merge job's producer took 1.1-1.9 us a
 // block against the chain's 1.36, RF_K2_STAMPS=3).
-constexpr uint32_t kHq = 73;  // words per lane: [2 chunks][4 holes][pos + 8 digest words] + 1 (odd stride)
+// Chunks of two holes (round 3, session 3): a transition every block or so,
+// each staging half as much, instead of a heavy one every other block (the
+// per-block barrier makes the slowest block set the pace): 8-rank piece
+// 0.330 -> 0.325 ms/step, configs[2] unchanged; 3 measured the same as 2
+// (profiles/r03/s3/hole_chunk_ab.log).  -DRF_HOLE_CHUNK=4: the previous form.
+#ifndef RF_HOLE_CHUNK
+#define RF_HOLE_CHUNK 2
+#endif
+constexpr uint32_t kHC = RF_HOLE_CHUNK;  // holes per chunk
+constexpr uint32_t kHq = 2 * kHC * 9 + 1;  // words per lane: [2 chunks][kHC holes][pos + 8 digest words] + 1 (odd stride)
 struct ChunkCursor {
     const uint4* __restrict__ T;
     uint32_t nb, he, h0, hn, staged;  // holes [h0, he), hn the next to apply, staged: chunks in LDS
@@ -361,31 +385,31 @@ struct ChunkCursor {
     uint32_t fslot = ~0u;  // a slot whose new digest is handed over in registers (fused chains)
     uint4 flo, fhi;
     uint2 single;          // one-hole fused jobs (begin_pre): the hole's record
-    uint2 rn[4], rnn[4];   // records of chunks c+1 and c+2
-    uint4 dlo[4], dhi[4];  // digests of chunk c+1
+    uint2 rn[kHC], rnn[kHC];   // records of chunks c+1 and c+2
+    uint4 dlo[kHC], dhi[kHC];  // digests of chunk c+1
     uint32_t* hq;          // the lane's LDS buffers
 
     __device__ __forceinline__ uint2 record(const LevelArgs& a, uint32_t h) const {
         const uint2 v = a.holes[h < he ? h : 0u];
         return h < he ? v : make_uint2(~0u, 0u);
     }
-    __device__ __forceinline__ void load_records(const LevelArgs& a, uint32_t c, uint2 (&r)[4]) const {
+    __device__ __forceinline__ void load_records(const LevelArgs& a, uint32_t c, uint2 (&r)[kHC]) const {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) r[q] = record(a, h0 + 4 * c + q);
+        for (uint32_t q = 0; q < kHC; ++q) r[q] = record(a, h0 + kHC * c + q);
     }
-    __device__ __forceinline__ void load_digests(const LevelArgs& a, const uint2 (&r)[4]) {
+    __device__ __forceinline__ void load_digests(const LevelArgs& a, const uint2 (&r)[kHC]) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (uint32_t q = 0; q < kHC; ++q) {
             const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * (r[q].x == ~0u ? 0u : r[q].y));
             dlo[q] = src[0];
             dhi[q] = src[1];
         }
     }
     // chunk c's records r and digests dlo/dhi into LDS buffer c & 1
-    __device__ __forceinline__ void stash(uint32_t c, const uint2 (&r)[4]) const {
-        uint32_t* q = hq + (c & 1) * 36;
+    __device__ __forceinline__ void stash(uint32_t c, const uint2 (&r)[kHC]) const {
+        uint32_t* q = hq + (c & 1) * 9 * kHC;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (uint32_t k = 0; k < kHC; ++k) {
             const bool f = r[k].y == fslot && r[k].x != ~0u;
             const uint4 lo = f ? flo : dlo[k], hi = f ? fhi : dhi[k];
             q[9 * k] = r[k].x;
@@ -399,7 +423,7 @@ struct ChunkCursor {
         he = m0.w;
         h0 = hn = m0.z;
         single = make_uint2(~0u, 0u);
-        uint2 r0[4];
+        uint2 r0[kHC];
         load_records(a, 0, r0);
         load_records(a, 1, rn);
         load_records(a, 2, rnn);
@@ -439,16 +463,16 @@ struct ChunkCursor {
     // if it starts below lim
     __device__ __forceinline__ void next_hole(const LevelArgs& a, uint32_t* ring, uint32_t lim) {
         if (hn >= he) return;
-        const uint32_t c = (hn - h0) >> 2;
+        const uint32_t c = (hn - h0) / kHC;
         if (c >= staged) {  // chunk c (= staged) enters: stash it, move the pipeline on
             stash(c, rn);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) rn[q] = rnn[q];
+            for (uint32_t q = 0; q < kHC; ++q) rn[q] = rnn[q];
             load_digests(a, rn);
             load_records(a, c + 2, rnn);
             staged = c + 1;
         }
-        const uint32_t* q = hq + (c & 1) * 36 + 9 * ((hn - h0) & 3);
+        const uint32_t* q = hq + (c & 1) * 9 * kHC + 9 * ((hn - h0) % kHC);
         const uint32_t pos = q[0];
         if (pos < lim) {
             const uint32_t D[8] = {q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8]};
@@ -1018,9 +1042,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     zero_other_counts(a);
     WgStamp ws;
     ws.begin(a);
-    const uint32_t n = a.counts[a.lvl];
-    const uint32_t* lst = a.list + a.s;
-    const uint4* lmt = a.lmeta + 2ull * a.s;
+    const LaunchList ll(a);
+    const uint32_t n = ll.n;
     // One copy of the loop per wave role (chain / producer / expander), each
     // with only its own state: the register allocator then sizes the kernel
     // for the largest role instead of the sum of all roles' live values, and
@@ -1033,19 +1056,19 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             if (threadIdx.x == 0) ws.jobs += min(64u, n - base);
             const uint32_t i = base + jl;
             bool has = i < n;
-            const uint32_t ii = a.rev ? n - 1 - i : i;  // (list position, when has)
-            uint32_t p = has ? lst[ii] : 0u;
+            const uint32_t ii = has ? ll.at(a, i) : 0u;  // (list position, when has)
+            uint32_t p = has ? a.list[ii] : 0u;
             // the listed job's record (append_jobs wrote it beside the list)
             uint4 lm0 = make_uint4(0, 0, 0, 0), lm1 = lm0;
             if (has) {
-                lm0 = lmt[2ull * ii];
-                lm1 = lmt[2ull * ii + 1];
+                lm0 = a.lmeta[2ull * ii];
+                lm1 = a.lmeta[2ull * ii + 1];
             }
             uint32_t fslot = ~0u;
             uint32_t maxnb;
             {
                 const uint32_t il = base + lane;
-                maxnb = wave_max_small(il < n ? lmt[2ull * (a.rev ? n - 1 - il : il)].y : 0u);
+                maxnb = wave_max_small(il < n ? a.lmeta[2ull * ll.at(a, il)].y : 0u);
             }
             uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
             uint4 nt[8];
@@ -1823,9 +1846,8 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
     zero_other_counts(a);
     WgStamp ws;
     ws.begin(a);
-    const uint32_t n = a.counts[a.lvl];
-    const uint32_t* lst = a.list + a.s;
-    const uint4* lmt = a.lmeta + 2ull * a.s;
+    const LaunchList ll(a);
+    const uint32_t n = ll.n;
     uint32_t hashed = 0;
     for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
         if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
@@ -1833,10 +1855,10 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
         uint32_t p = ~0u;
         uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
         if (i < n) {
-            const uint32_t ii = a.rev ? n - 1 - i : i;
-            p = lst[ii];
-            m0 = lmt[2ull * ii];
-            m1 = lmt[2ull * ii + 1];
+            const uint32_t ii = ll.at(a, i);
+            p = a.list[ii];
+            m0 = a.lmeta[2ull * ii];
+            m1 = a.lmeta[2ull * ii + 1];
         }
         uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
         uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
@@ -2091,7 +2113,17 @@ void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* 
 
 const void* graph_mark_kernel() { return reinterpret_cast<const void*>(k3_mark_slots); }
 
-hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s, uint32_t* zero_counts) {
+// Whether an incremental plain step runs level lvl in the throughput form
+// (k2_level_lf): min(its jobs, the step's marked input slots) reaches the
+// threshold of its kind (GraphDev::thru_slots / thru_slots_wide).
+bool graph_level_lf(const GraphDev& g, uint32_t lvl) {
+    const uint64_t n = g.lvl_start[lvl + 1] - g.lvl_start[lvl];
+    return std::min<uint64_t>(n, g.step_marked) >=
+           ((g.inc_level[lvl] & kLvlForm) == 2 ? g.thru_slots_wide : g.thru_slots);
+}
+
+hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s, uint32_t* zero_counts,
+                              uint32_t sink_lvl) {
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
     if (e <= b) return hipSuccess;
     // RF_DBG_HASH2: hash twice (k2_level); RF_K2_STAMPS=2: per-chunk stamps (k2_level_pl)
@@ -2125,21 +2157,28 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         return v ? (uint32_t)atoi(v) : 1024u;
     }();
     if (!full) {
-        if (!g.inc_level[lvl]) return hipSuccess;  // every job of the level is a fusion target
+        if (!(g.inc_level[lvl] & kLvlForm)) return hipSuccess;  // every job of the level is a fusion target
+        // an attached sink list: its jobs after the level's own, same launch
+        // (the grid sized for both)
+        const uint32_t n2 = sink_lvl != ~0u ? g.lvl_start[sink_lvl + 1] - g.lvl_start[sink_lvl] : 0u;
+        if (sink_lvl != ~0u) {
+            a.s2 = g.lvl_start[sink_lvl];
+            a.lvl2 = sink_lvl;
+        }
         // grid cap (RF_K2_GRID): workgroups past the dirty count exit at once,
         // but each still costs a dispatch before the kernel can end
         static const uint64_t wg_cap = [] {
             const char* v = getenv("RF_K2_GRID");
             return v ? (uint64_t)strtoull(v, nullptr, 10) : 2048ull;
         }();
-        uint64_t wg = (e - b + 63) / 64;
+        uint64_t wg = (e - b + n2 + 63) / 64;
         if (wg > wg_cap) wg = wg_cap;
         // RF_K2_CHAIN=14: the one-lane chain (k2_level_pc), for A/B runs
         static const bool one_lane = [] {
             const char* v = getenv("RF_K2_CHAIN");
             return v && atoi(v) == 14;
         }();
-        const bool wide = g.inc_level[lvl] == 2;
+        const bool wide = (g.inc_level[lvl] & kLvlForm) == 2;
         // g.stream_handover (RF_K2_STREAM=1 at load): the streamed hand-over
         // (measured no faster on configs[2]: the producer serializes a fused
         // job's blocks 0 and 1); default per-block barriers
@@ -2151,14 +2190,18 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_PAD_KB");
             return v ? (uint32_t)atoi(v) * 1024u : 0u;
         }();
-        if (std::min<uint64_t>(e - b, g.step_marked) >= (g.inc_level[lvl] == 2 ? g.thru_slots_wide : g.thru_slots)) {
+        if (one_lane && sink_lvl != ~0u) {  // (k2_level_pc takes no attached list: the sink level after it)
+            if (hipError_t err = launch_graph_level(g, lvl, 0, s, zero_counts)) return err;
+            return launch_graph_level(g, sink_lvl, 0, s);
+        }
+        if (graph_level_lf(g, lvl)) {
             // the throughput form: 256 lanes per workgroup, four resident per
             // CU, grid-stride over the device-side count
             static const uint64_t lf_cap = [] {
                 const char* v = getenv("RF_K2_LF_GRID");
                 return v ? (uint64_t)strtoull(v, nullptr, 10) : 1024ull;
             }();
-            uint64_t lg = (e - b + kLevelBlock - 1) / kLevelBlock;
+            uint64_t lg = (e - b + n2 + kLevelBlock - 1) / kLevelBlock;
             if (lg > lf_cap) lg = lf_cap;
             hipLaunchKernelGGL(k2_level_lf, dim3((uint32_t)lg), dim3(kLevelBlock), 0, s, a);
         } else if (one_lane && wide)

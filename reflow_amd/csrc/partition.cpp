@@ -96,6 +96,26 @@ extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "partition alloc: %s", hipGetErrorString(e));
     // nothing sent yet: every export counts as changed at the first exchange
     HIPC(sync_memset(ctx, P->d_snap.p, 0, 32ull * std::max<uint32_t>(p->n_export, 1)));
+    // An import read by a job of the sink level (GraphDev kLvlSink): that
+    // level then runs as a level of its own, after the exchange passes'
+    // levels, not attached to an earlier launch
+    {
+        GraphDev& G = gr->g;
+        uint32_t sink = ~0u;
+        for (uint32_t l = 0; l < G.n_levels; ++l)
+            if (G.inc_level[l] & kLvlSink) sink = l;
+        G.sink_attach_ok = true;
+        for (uint32_t i = 0; sink != ~0u && i < p->n_import && G.sink_attach_ok; ++i) {
+            uint32_t cp[2];
+            HIPC(sync_copy(ctx, cp, gr->b_cons_ptr.as<uint32_t>() + p->import_slot[i], 8, hipMemcpyDeviceToHost));
+            if (cp[1] <= cp[0]) continue;
+            std::vector<uint32_t> ce(2ull * (cp[1] - cp[0]));
+            HIPC(sync_copy(ctx, ce.data(), gr->b_cons_job.as<uint32_t>() + 2ull * cp[0], 4 * ce.size(),
+                           hipMemcpyDeviceToHost));
+            for (size_t k = 1; k < ce.size(); k += 2)
+                if ((ce[k] & 0x7fffffffu) == sink) G.sink_attach_ok = false;
+        }
+    }
     // Deferral (fixed rounds, plain steps): the lowest level reading an import
     // and the highest level producing an export.  If every export is final
     // before any import is read, the levels from the lowest import reader up
