@@ -1305,9 +1305,9 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // throughput form's lanes: 0.820 -> 0.781 ms/step; configs[2] and the
     // 8-rank piece unchanged, profiles/r03/s3/sink_fill_ab.log).  Default (2):
     // those sinks in a level of their own whose list a plain step attaches to
-    // the first throughput-form launch from their inputs' level up to the
-    // fill level, else to the fill level's launch.  1: the last level (A/B);
-    // 0: off.
+    // the last throughput-form launch from their inputs' level up to the fill
+    // level, else to the fill level's launch (4-rank piece 0.408 -> 0.380
+    // ms/step, sink_attach_ab.log).  1: the last level (A/B); 0: off.
     uint32_t sink_fill = ~0u, sink_min = 0;
     {
         static const int alap = [] {

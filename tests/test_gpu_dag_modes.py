@@ -88,3 +88,34 @@ def test_forced_mode_dag1000(ctx, monkeypatch, var, val):
     assert (gf.get_slots(every) == gd.get_slots(every)).all()
     gf.close()
     gd.close()
+
+
+def test_sink_list_attached_below_fill_level(ctx, monkeypatch):
+    """The sink level's list (physical keys) rides on the last throughput-form
+    launch at or below the fill level: short-job levels forced into the
+    throughput form (RF_K2_THRU=1) and the wide OpK level kept in the latency
+    form (RF_K2_THRU_WIDE huge) attach it to the Exec level's launch, below the
+    fill level -- the strong layout's 4-rank piece.  Checked against the oracle
+    and against the default forms' slots."""
+    dag = Dag1000(8, 32)  # OpK: 32 holes, 18 blocks (a wide level)
+    every = np.arange(dag.n_slots, dtype=np.uint32)
+    gd = load_dag(ctx, dag)
+    gd.recompute(full=True)
+    monkeypatch.setenv("RF_K2_THRU", "1")
+    monkeypatch.setenv("RF_K2_THRU_WIDE", str(1 << 62))
+    g = load_dag(ctx, dag)
+    g.recompute(full=True)
+    ids = dag.leaf_ids.copy()
+    slots, old, new = dag.change_set(0.1)
+    for version in (new, old, new):
+        g.set_slots(slots, version)
+        g.recompute(full=False)
+        ids[slots] = version
+        check_against_oracle(g, dag, ids)
+    monkeypatch.delenv("RF_K2_THRU")
+    monkeypatch.delenv("RF_K2_THRU_WIDE")
+    gd.set_slots(slots, new)
+    gd.recompute(full=False)
+    assert (g.get_slots(every) == gd.get_slots(every)).all()
+    g.close()
+    gd.close()
