@@ -89,17 +89,22 @@ class Budget:
         return True
 
 
+PMC_ROUND = "r04"  # traffic is read only from this round's pass over the current library
+
+
 def pmc_traffic(kernel, workload, algo_bytes=None):
-    """HBM bytes per launch of `kernel` from a committed rocprofv3 --pmc
-    FETCH_SIZE/WRITE_SIZE pass (tools/pmc_summary.py, corrected as
-    MI355X_MICROARCH.md prescribes) -- only when that pass ran this same
-    workload (its "workload" key); None otherwise.  A kernel launched more
-    than once there (the hybrid step's duo launch on three files, the GPU-only
-    run's on 35) is matched to this launch by its algorithmic bytes: the
-    launch whose traffic is nearest in ratio.  PMC counters cannot be read
-    inside this process."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+    """HBM bytes per launch of `kernel` from this round's committed rocprofv3
+    --pmc FETCH_SIZE/WRITE_SIZE pass (profiles/<PMC_ROUND>/pmc_traffic.json,
+    tools/pmc_summary.py, corrected as MI355X_MICROARCH.md prescribes) --
+    only when that pass ran this same workload (its "workload" key); None
+    otherwise (never an earlier round's file: the library changes between
+    rounds).  A kernel launched more than once there (the hybrid step's duo
+    launch on three files, the GPU-only run's on 35) is matched to this
+    launch by its algorithmic bytes: the launch whose traffic is nearest in
+    ratio.  PMC counters cannot be read inside this process."""
+    for path in [os.path.join(ROOT, "profiles", PMC_ROUND, "pmc_traffic.json")]:
+        if not os.path.exists(path):
+            continue
         d = json.load(open(path))
         if d.get("workload") != workload:
             continue
@@ -366,7 +371,8 @@ def bench_sha(args, dist, ctx, budget):
         r2 = kernel_roofline("k1_sha256_duo", lens, duo_ids, s2.last_ms_solo) if s2.n_solo else None
         if r2:
             tr2, ts2 = pmc_traffic("k1_sha256_duo", workload, r2["bytes_per_launch"])
-            r2["traffic"], r2["traffic_source"] = tr2, ts2 or "not measured in this process"
+            r2["traffic"], r2["traffic_source"] = tr2, ts2 or ("no %s PMC pass of this workload on the current "
+                                                               "library (profiles/%s/pmc_traffic.json)" % (PMC_ROUND, PMC_ROUND))
         same = bool((out2.to_numpy() == out.to_numpy()).all())
         res["roofline_gpu_only"] = r2
         res["gpu_only"] = {"gbps": float(lens.sum()) / wall / 1e9, "ms": wall * 1e3, "duo_files": int(s2.n_solo),
@@ -543,6 +549,8 @@ def bench_dag(args, dist, ctx, budget):
     ctx.timer_start()
     g.recompute(True)
     full_ms = ctx.timer_stop()
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+    snap_full = g.get_slots(every)  # the full recompute's table (the original File IDs)
     slots, old, new = dag.change_set(0.01)
     d_slots = ctx.upload(slots)
     d_old, d_new = ctx.upload(old), ctx.upload(new)
@@ -567,6 +575,18 @@ def bench_dag(args, dist, ctx, budget):
     for _ in range(steps):
         step()
     dev_ms = ctx.timer_stop() / steps
+    # parity snapshots after the timed steps (untimed): the table one more
+    # incremental step leaves with the changed IDs (checked against the
+    # oracle in the cpu leg), and the table after stepping back, which must
+    # equal the full recompute's slot for slot
+    if state["v"] == 1:
+        step()
+    step()
+    ctx.sync()
+    snap_new = g.get_slots(every)
+    step()
+    ctx.sync()
+    back_equal_full = bool((g.get_slots(every) == snap_full).all())
     res = {"workload": "configs[2]: 1000align DAG S=%d P=%d, 1%% leaf File IDs toggled per step" % (S, args.dag_pairs),
            "nodes": dag.n_nodes, "jobs": len(a["out_slot"]),
            "dirty_nodes_per_step": int(n_dirty_nodes), "dirty_jobs_per_step": int(n_dirty_jobs),
@@ -575,7 +595,10 @@ def bench_dag(args, dist, ctx, budget):
            "effective_mnodes_per_s": dag.n_nodes * steps / t / 1e6,
            "full_recompute_ms": full_ms,
            "full_recompute_mnodes_per_s": dag.n_nodes / (full_ms * 1e-3) / 1e6,
-           "levels": g.stats().n_levels, "build_s": round(t_build, 2), "load_s": round(t_load, 2)}
+           "levels": g.stats().n_levels, "build_s": round(t_build, 2), "load_s": round(t_load, 2),
+           "incremental_equals_full": back_equal_full,
+           # filled in by the cpu leg's oracle checks (null if it did not run)
+           "digests_equal_oracle": None, "full_digests_equal_oracle": None}
     res["roofline_latency"] = latency_roofline(dag.critical_path(slots), res["device_ms_per_step"])
     st = g.stats()
     ach = st.total_blocks * 64 / (full_ms * 1e-3) / 1e9
@@ -586,7 +609,7 @@ def bench_dag(args, dist, ctx, budget):
         res["checkpoint"] = bench_checkpoint(ctx, g, a, t_build + t_load + full_ms * 1e-3)
     # the configs[2] CPU legs need the host arrays (rank 0, N = 1)
     res["_cpu"] = {"a": a, "dag": dag, "slots": slots, "old": old, "new": new,
-                   "gpu_dirty_jobs": int(n_dirty_jobs)}
+                   "gpu_dirty_jobs": int(n_dirty_jobs), "snap_full": snap_full, "snap_new": snap_new}
     for b in (d_slots, d_old, d_new):
         b.free()
     g.close()
@@ -639,6 +662,8 @@ def bench_dag100m(args, dist, ctx, comm, budget):
     ctx.sync()
     dist.barrier()
     full_ms = dist.max(time.perf_counter() - t1) * 1e3
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+    snap_full = g.get_slots(every)  # the full recompute's table (the original File IDs)
     n_files_global = 2 * P * S * nparts
     slots, old, new = pc.dag.change_set(0.01, n_global=n_files_global)
     d_slots = ctx.upload(slots if len(slots) else np.zeros(1, np.uint32))
@@ -669,6 +694,31 @@ def bench_dag100m(args, dist, ctx, comm, budget):
     for _ in range(steps):
         step()
     dev_ms = ctx.timer_stop() / steps
+    # parity after the timed steps (untimed): one more incremental step to the
+    # changed IDs -- its table re-derived job by job by the oracle (N = 1) --
+    # and one back, which must equal the full recompute's table slot for slot
+    if state["v"] == 1:
+        step()
+    step()
+    ctx.sync()
+    dist.barrier()
+    snap_new = g.get_slots(every)
+    step()
+    ctx.sync()
+    dist.barrier()
+    back_equal = bool((g.get_slots(every) == snap_full).all())
+    del snap_full
+    inc_equal_full = dist.max(0.0 if back_equal else 1.0) == 0.0
+    want_in = pc.dag.leaf_ids.copy()
+    if len(slots):
+        pos = np.searchsorted(pc.dag.file_slots, slots)
+        assert (pc.dag.file_slots[pos] == slots).all()
+        want_in[pos] = new
+    inputs_ok = dist.max(0.0 if (snap_new[pc.dag.file_slots] == want_in).all() else 1.0) == 0.0
+    oracle = None
+    if not multi and "cpu" not in args.skip and budget.allow("dag100m_oracle", 25):
+        oracle = oracle_check_table(a, snap_new)
+    del snap_new
     nodes_all, blocks_all = dist.sum(nodes_l), dist.sum(blocks_l)
     per_rank = [dict(rank=i, **{k: int(v) for k, v in zip(("jobs", "dirty_nodes", "dirty_blocks"), row)})
                 for i, row in enumerate(np.frombuffer(dist.all_gather_bytes(
@@ -682,6 +732,9 @@ def bench_dag100m(args, dist, ctx, comm, budget):
            "nodes_global": int(nodes_global), "nodes_rank0": int(pc.n_nodes), "jobs_rank0": len(a["out_slot"]),
            "dirty_nodes_per_step": int(nodes_all), "dirty_blocks_per_step": int(blocks_all),
            "dirty_jobs_match_device": bool(jobs_ok),
+           "incremental_equals_full": bool(inc_equal_full), "input_slots_ok": bool(inputs_ok),
+           "digests_equal_oracle": None if oracle is None else oracle["jobs_mismatching"] == 0 and bool(inputs_ok),
+           "oracle_parity": oracle,
            "ms_per_step": t / steps * 1e3, "device_ms_per_step_rank0": dev_ms,
            "mnodes_per_s": nodes_all * steps / t / 1e6,
            "effective_mnodes_per_s": nodes_global * steps / t / 1e6,
@@ -703,6 +756,72 @@ def bench_dag100m(args, dist, ctx, comm, budget):
         b.free()
     g.close()
     return res
+
+
+def bench_piece(args, ctx, ranks, n1_ms):
+    """N = 1 only: rank 0's piece of the strong-scaling layout at `ranks`
+    ranks (8/ranks parts of configs[3]'s DAG, the global root included),
+    stepped on this GPU like bench_dag100m's rank 0 but with no exchange --
+    what one GPU of a `ranks`-GPU run hashes per step, so the 1 -> N curve's
+    DAG ceiling is visible before the driver's SCALE run."""
+    S, P, nparts = args.c4_samples, args.dag_pairs, args.c4_parts
+    pc = PartitionedDag1000(S, P, ranks, 0, nparts=nparts)
+    g = capi.Graph.from_arrays(ctx, pc.desc)
+    g.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
+    g.recompute(True)
+    slots, old, new = pc.dag.change_set(0.01, n_global=2 * P * S * nparts)
+    d_slots, d_old, d_new = ctx.upload(slots), ctx.upload(old), ctx.upload(new)
+    every = np.arange(pc.desc["n_slots"], dtype=np.uint32)
+    full = g.get_slots(every)
+    state = {"v": 0}
+
+    def step():
+        ver = d_new if state["v"] == 0 else d_old
+        state["v"] ^= 1
+        g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
+        g.recompute_async(False, ctx.stream)
+
+    for _ in range(2):
+        step()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.dag_steps):
+        step()
+    ctx.sync()
+    ms = (time.perf_counter() - t0) / args.dag_steps * 1e3
+    if state["v"] == 1:
+        step()
+    ctx.sync()
+    same = bool((g.get_slots(every) == full).all())
+    for b in (d_slots, d_old, d_new):
+        b.free()
+    g.close()
+    log("  rank 0's piece at %d ranks: %d nodes, %.4f ms/step (N = 1: %.4f ms, ratio %.2f)"
+        % (ranks, pc.n_nodes, ms, n1_ms, n1_ms / ms))
+    return {"ranks": ranks, "nodes": int(pc.n_nodes), "changed_slots": int(len(slots)), "ms_per_step": round(ms, 4),
+            "projected_speedup": round(n1_ms / ms, 3), "incremental_equals_full": same,
+            "what": "rank 0's piece of the strong layout at %d ranks, local step only (no exchange), on this GPU; "
+                    "projected_speedup = incremental_100m.ms_per_step (N = 1) / this" % ranks}
+
+
+def oracle_check_table(a, table):
+    """Checker leg (untimed, rank 0 at N = 1): the oracle re-derives every
+    job of a GPU slot table from that table's own hole digests
+    (orc_graph_check, flow.go:675-750 per node on cpu_threads() threads);
+    with the input slots at their assigned values (checked by the caller)
+    this is the table's parity with the full evaluation."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import reflow_oracle as O  # the oracle: as the checker only
+    th = cpu_threads()
+    t0 = time.perf_counter()
+    bad, first = O.check_slots(a, table, th)
+    dt = time.perf_counter() - t0
+    log("  oracle check: %d jobs re-derived on %d threads in %.1f s: %d mismatching"
+        % (len(a["out_slot"]), th, dt, bad))
+    return {"what": "every job of the GPU's table after an incremental step re-hashed by the oracle from the "
+                    "table's own hole digests (orc_graph_check); inputs checked against the change set",
+            "jobs_checked": int(len(a["out_slot"])), "jobs_mismatching": bad, "first_bad_job": first,
+            "seconds": round(dt, 2), "threads": th}
 
 
 def bench_checkpoint(ctx, g, a, cold_s):
@@ -735,6 +854,34 @@ def bench_checkpoint(ctx, g, a, cold_s):
             "what": "rf_graph_save after the timed steps, rf_graph_restore into a new graph, every slot compared"}
 
 
+def first_index_of_equal(dig):
+    """For rows of 32-B digests: the first row index holding an equal digest
+    (flowMap.Put keeps the first flow of each digest, flow.go:897-907) --
+    a stable sort by the first 64-bit word, then each run's minimum; if two
+    different digests share that word (~n^2/2^65) the full lexicographic
+    sort decides."""
+    n = len(dig)
+    w = np.ascontiguousarray(dig).view(np.uint64).reshape(n, 4)
+    order = np.argsort(w[:, 0], kind="stable")
+    sw = w[order, 0]
+    start = np.ones(n, dtype=bool)
+    start[1:] = sw[1:] != sw[:-1]
+    run = np.cumsum(start) - 1
+    out = np.empty(n, dtype=np.int64)
+    out[order] = order[start][run]
+    if (w[out] == w).all():
+        return out
+    order = np.lexsort((np.arange(n), w[:, 3], w[:, 2], w[:, 1], w[:, 0]))
+    sw = w[order]
+    start = np.ones(n, dtype=bool)
+    start[1:] = (sw[1:] != sw[:-1]).any(axis=1)
+    run = np.cumsum(start) - 1
+    first_of_run = order[start]  # the lowest index of each run (the sort is stable by index)
+    out = np.empty(n, dtype=np.int64)
+    out[order] = first_of_run[run]
+    return out
+
+
 def bench_canon(ctx, g, dag):
     """K5: Canonicalize's flowMap over every node digest of the C3 DAG, as a
     program that builds the shared reference-index chain (Intern -> Exec(bwa
@@ -760,8 +907,15 @@ def bench_canon(ctx, g, dag):
     ms = float(np.median(times))
     ok = nu == dag.n_nodes and n == dag.n_nodes + 3 * (dag.S - 1) and bool(
         (canon[:3 * dag.S].reshape(dag.S, 3) == np.arange(3)).all())
+    # every canon[i] against flowMap's answer computed on the host: the first
+    # index in Put order holding an equal digest (flow.go:897-907)
+    dig = d_dig.to_numpy().reshape(n, 32)
+    want = first_index_of_equal(dig)
+    canon_equal = bool((canon.astype(np.int64) == want).all())
     res = {"workload": "dedup of %d node digests (C3 DAG + %d duplicated ref-index nodes)" % (n, 3 * (dag.S - 1)),
            "ms": ms, "mnodes_per_s": n / (ms * 1e-3) / 1e6, "unique": nu, "parity_ok": ok,
+           "canon_equal_host": canon_equal,
+           "canon_check": "every canon[i] == the first index with an equal 32-B digest (host, numpy sort)",
            "random_accesses_per_node": 3,
            "achieved_g_accesses_per_s": round(3 * n / (ms * 1e-3) / 1e9, 2)}
     for b in (d_idx, d_dig, d_canon, d_nu):
@@ -875,7 +1029,7 @@ def bench_probe(args, dist, ctx, budget):
     if dist.world == 1 and "cpu" not in args.skip:
         ns = min(n_probe, 20_000_000)
         res["_cpu"] = {"words": b.words(), "length": b.params()[2], "m": h["m"], "k": h["k"],
-                       "keys": keys.to_numpy(count=32 * ns), "n": ns}
+                       "keys": keys.to_numpy(count=32 * ns), "n": ns, "gpu_bits": out.to_numpy(count=ns)}
     for x in (keys, out) + h["extra"]:
         x.free()
     b.close()
@@ -915,6 +1069,23 @@ def bench_assoc(ctx, keys, n_ins, n_probe, hits):
     get_ms = ctx.timer_stop()
     found = int(d_f.to_numpy().astype(np.int64).sum())
     occ, cap = a.stats()
+    # sampled parity with the Go map the reference's test assoc is
+    # (test/testutil/assoc.go:34-56): a dict of the first 2M Puts, asked for
+    # the first 1M probes (inserted keys) and the last 1M (fresh keys)
+    ns = min(1_000_000, n_ins, n_probe // 2)
+    d = dict(zip(map(bytes, keys.to_numpy(count=32 * 2 * ns).reshape(-1, 32)),
+                 map(bytes, vals.to_numpy(count=32 * 2 * ns).reshape(-1, 32))))
+    assoc_ok = True
+    for lo in ((0, n_probe - ns) if n_ins <= n_probe // 2 else (0,)):  # (rows past n_ins: fresh keys)
+        pk = keys.to_numpy(count=32 * ns, offset=32 * lo).reshape(ns, 32)
+        gv = d_v.to_numpy(count=32 * ns, offset=32 * lo).reshape(ns, 32)
+        gf = d_f.to_numpy(count=ns, offset=lo)
+        for i in range(ns):
+            w = d.get(bytes(pk[i]))
+            if (w is None) != (gf[i] == 0) or (w is not None and w != bytes(gv[i])):
+                assoc_ok = False
+                break
+    del d
     for b in (vals, st, d_v, d_f):
         b.free()
     n_nodes = min(2_000_000, n_ins)
@@ -938,6 +1109,8 @@ def bench_assoc(ctx, keys, n_ins, n_probe, hits):
             "put_ms": put_s * 1e3, "put_mkeys_per_s": n_ins / put_s / 1e6, "put_ok": ok_put,
             "get_ms": get_ms, "get_g_keys_per_s": n_probe / (get_ms * 1e-3) / 1e9,
             "found_exact": found == (n_probe // 2) // n_ins * n_ins,
+            "get_equal_dict": assoc_ok,
+            "get_check": "%d inserted + %d fresh probe keys: found flag and value vs a dict of the Puts" % (ns, ns),
             "bloom_false_positives_resolved": hits - found,
             "table_slots": cap, "occupied": occ, "lookup": lookup}
 
@@ -990,6 +1163,8 @@ def cpu_probe_and_tables(probe, canon_n=2_000_000):
         dt = time.perf_counter() - t0
         r["probe_%dt" % th] = {"value": n / dt / 1e9, "unit": "G probes/s", "cores": th, "kind": "port",
                                "sample": "%d probes of the configs[4] set against its filter" % n}
+    # the last run covered every sampled key: the GPU's answers bit for bit
+    r["probe_bits_equal_gpu"] = bool(((out != 0) == (c["gpu_bits"] != 0)).all())
     ks = [keys[32 * i:32 * i + 32].tobytes() for i in range(canon_n)]
     t0 = time.perf_counter()
     first = {}
@@ -1076,7 +1251,12 @@ def cpu_baseline(args, sha, dag_res, budget):
                         "(min(60, CPU share): DigestLimiter), largest-first" % threads,
                 "sample": "first %d files (%.2f GiB, largest %.2f GiB) of configs[1]"
                           % (n, s_lens.sum() / GiB, s_lens.max() / GiB),
-                "seconds": dt, "gpu_digests_match": bool((back == sha["_digests"][:n]).all())})
+                "seconds": dt, "gpu_digests_match": bool((back == sha["_digests"][:n]).all()),
+                # the same cores with SHA-NI (what Go >= 1.21 crypto/sha256 runs): the
+                # CPU figure the GPU step should be read against
+                "value_openssl": res["openssl"]["value"],
+                "note": "value = the scalar port (Go 1.9/1.10 speed class); value_openssl = OpenSSL SHA-NI on the "
+                        "same %d threads over the whole set" % threads})
     del mv, host
     # configs[0]: port and OpenSSL
     c1l = np.full(C1_N, C1_LEN, dtype=np.uint64)
@@ -1104,10 +1284,24 @@ def cpu_baseline(args, sha, dag_res, budget):
         t0 = time.perf_counter()
         og.full()
         full_s = time.perf_counter() - t0
+        full_eq = int((og.slots != c["snap_full"]).any(axis=1).sum())  # slots differing (0 = parity)
         t0 = time.perf_counter()
         hashed = og.update(c["slots"], c["new"])
         inc_s = time.perf_counter() - t0
         blocks = og.last_blocks()
+        inc_eq = int((og.slots != c["snap_new"]).any(axis=1).sum())
+        # and every job of the GPU's post-step table re-derived from its own
+        # holes (orc_graph_check: job-local, threaded)
+        bad, first = O.check_slots(c["a"], c["snap_new"], threads)
+        if dag_res is not None:
+            dag_res["digests_equal_oracle"] = inc_eq == 0 and bad == 0
+            dag_res["full_digests_equal_oracle"] = full_eq == 0
+            dag_res["oracle_parity"] = {
+                "what": "every slot of the GPU's tables vs the oracle's serial evaluation (orc_graph_full; "
+                        "orc_graph_update on the bench's change set), plus every job of the post-step table "
+                        "re-hashed from its own holes (orc_graph_check)",
+                "slots": int(len(og.slots)), "full_slots_differing": full_eq, "incremental_slots_differing": inc_eq,
+                "jobs_checked": int(len(c["a"]["out_slot"])), "jobs_mismatching": bad, "first_bad_job": first}
         n_nodes = c["dag"].n_nodes
         res["dag_full"] = {"value": n_nodes / full_s / 1e6, "unit": "M graph nodes/s", "cores": 1, "kind": "port",
                            "what": "every digest recomputed, the reference's behaviour per Eval (flow.go:653-664 "
@@ -1131,6 +1325,39 @@ def cpu_baseline(args, sha, dag_res, budget):
                         "chains of dependent jobs), not throughput-bound"}
         og.close()
     return res
+
+
+def parity_summary(sha, c1, dag, dag100, probe, cpu):
+    """Every digest / answer check this run made, one boolean each (None =
+    not run here: a section skipped, or a check that needs the N = 1 cpu
+    leg).  `all` is true iff every check that ran passed."""
+    def get(d, *path):
+        for p in path:
+            if not isinstance(d, dict) or d.get(p) is None:
+                return None
+            d = d[p]
+        return bool(d)
+    checks = {
+        "configs1_ids_vs_openssl": get(cpu, "openssl", "gpu_digests_match"),
+        "configs1_ids_vs_oracle_sample": get(cpu, "gpu_digests_match"),
+        "configs1_gpu_only_equals_hybrid": get(sha, "gpu_only", "digests_equal_hybrid"),
+        "configs0_fileset_vs_fixture": get(c1, "fixture_match"),
+        "configs0_install_vs_fixture": get(c1, "install", "fileset_digest_match"),
+        "configs2_incremental_vs_oracle": get(dag, "digests_equal_oracle"),
+        "configs2_full_vs_oracle": get(dag, "full_digests_equal_oracle"),
+        "configs2_incremental_equals_full": get(dag, "incremental_equals_full"),
+        "configs2_dedup_vs_host": get(dag, "canonicalize", "canon_equal_host"),
+        "configs2_checkpoint_slots": get(dag, "checkpoint", "slots_equal"),
+        "configs3_incremental_vs_oracle": get(dag100, "digests_equal_oracle"),
+        "configs3_incremental_equals_full": get(dag100, "incremental_equals_full"),
+        "configs3_dirty_jobs_vs_layout": get(dag100, "dirty_jobs_match_device"),
+        "configs4_probe_vs_oracle": get(cpu, "probe_bits_equal_gpu"),
+        "configs4_no_false_negatives": get(probe, "no_false_negatives"),
+        "configs4_collect_vs_probe": get(probe, "collect", "dead_matches_probe"),
+        "assoc_get_vs_dict": get(probe, "assoc", "get_equal_dict"),
+    }
+    ran = [v for v in checks.values() if v is not None]
+    return {"all": bool(ran) and all(ran), "checks_run": len(ran), **checks}
 
 
 def main():
@@ -1160,7 +1387,7 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
     ap.add_argument("--gpu-only-run", type=int, default=1, help="one GPU-only run (duo roofline)")
     ap.add_argument("--budget-s", type=float, default=420.0)
-    ap.add_argument("--skip", default="", help="comma list of: lower,c1,install,dag,dag100m,checkpoint,probe,cpu")
+    ap.add_argument("--skip", default="", help="comma list of: lower,c1,install,dag,dag100m,piece,checkpoint,probe,cpu")
     args = ap.parse_args()
     args.skip = set(filter(None, args.skip.split(",")))
     budget = Budget(args.budget_s)
@@ -1210,17 +1437,27 @@ def main():
     sha_ranks = None
     if dist.world > 1:  # per rank: host-leg threads and bytes, GPU-leg bytes, step ms (is the curve host-bound?)
         hl, comp = sha["host_leg"] or {}, sha["composition"]
-        row = np.array([hl.get("threads", 0), comp["host_leg_bytes"], comp["gpu_bytes"], sha["ms_per_step"]],
-                       np.float64)
+        gpu_ms = max([v for k, v in sha["step_ms"].items() if k in ("solo", "lanes")] or [0.0])
+        row = np.array([hl.get("threads", 0), comp["host_leg_bytes"], comp["gpu_bytes"], sha["ms_per_step"],
+                        hl.get("ms", 0.0), gpu_ms], np.float64)
+        # per rank: the host leg's and the GPU legs' own rates, so a 1 -> N SHA
+        # curve shows which leg it measures (the host legs share the node's CPUs)
         sha_ranks = [dict(rank=i, host_threads=int(r[0]), host_leg_bytes=float(r[1]), gpu_bytes=float(r[2]),
-                          ms_per_step=round(float(r[3]), 2))
-                     for i, r in enumerate(np.frombuffer(dist.all_gather_bytes(row), np.float64).reshape(-1, 4))]
+                          ms_per_step=round(float(r[3]), 2),
+                          host_leg_gbps=round(r[1] / (r[4] * 1e-3) / 1e9, 3) if r[4] else None,
+                          gpu_legs_ms=round(float(r[5]), 2),
+                          gpu_legs_gbps=round(r[2] / (r[5] * 1e-3) / 1e9, 3) if r[5] else None)
+                     for i, r in enumerate(np.frombuffer(dist.all_gather_bytes(row), np.float64).reshape(-1, 6))]
     c1 = bench_c1(args, dist, ctx, budget) if "c1" not in args.skip and budget.allow("c1", 15) else None
     dag_res = dag100 = None
     if dist.world == 1 and "dag" not in args.skip and budget.allow("dag", 30):
         dag_res = bench_dag(args, dist, ctx, budget)
     if "dag100m" not in args.skip and budget.allow("dag100m", 150):
         dag100 = bench_dag100m(args, dist, ctx, comm, budget)
+        if dist.world == 1 and "piece" not in args.skip and budget.allow("piece_8", 20):
+            pc8 = bench_piece(args, ctx, 8, dag100["ms_per_step"])
+            dag100["piece_8"] = pc8
+            dag100["piece_ms_8"], dag100["projected_speedup_8"] = pc8["ms_per_step"], pc8["projected_speedup"]
     probe = bench_probe(args, dist, ctx, budget) if "probe" not in args.skip and budget.allow("probe", 30) else None
     cpu = None
     if dist.rank == 0 and dist.world == 1 and "cpu" not in args.skip and budget.allow("cpu", 60):
@@ -1238,6 +1475,7 @@ def main():
     if dag_res is not None:
         dag_res.pop("_cpu", None)
     sha["_arena"].free()
+    parity = parity_summary(sha, c1, dag_res, dag100, probe, cpu)
 
     if dist.rank == 0:
         workload = sha["workload"]
@@ -1258,6 +1496,7 @@ def main():
                                       "RCCL only for its boundary exchange",
                        "exchange": exchange, "split_rank0": sha["split"], "step_ms_rank0": sha["step_ms"]},
             "rccl": rccl,
+            "parity": parity,
             "roofline": sha["roofline"],
             "roofline_gpu_legs": sha["roofline_gpu_legs"],
             "composition": sha["composition"],

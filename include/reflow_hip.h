@@ -347,9 +347,19 @@ int rf_graph_set_slots_device(rf_graph *g, const void *d_slots, const void *d_di
  * update): the two-lane latency form, or -- when min(level jobs, marked
  * slots) reaches 24,576 (65,536 for levels of long jobs) -- the lane-per-job
  * throughput form; change sets of >= 98,304 slots also mark in the
- * throughput form.  Results are identical; RF_K2_THRU / RF_K2_THRU_WIDE
- * (read per step) override the thresholds (0: always the throughput form). */
+ * throughput form.  Results are identical.  The thresholds are fixed per
+ * graph: the defaults below, RF_K2_THRU / RF_K2_THRU_WIDE (read once when the
+ * graph is loaded or restored; RF_K2_THRU also sets the mark threshold), or
+ * rf_graph_set_forms. */
 int rf_graph_recompute(rf_graph *g, int full, uint64_t *out_recomputed);
+#define RF_K2_THRU_DEFAULT 24576ull      /* levels of short jobs */
+#define RF_K2_THRU_WIDE_DEFAULT 65536ull /* levels of long jobs (the per-sample OpK) */
+#define RF_K2_THRU_MARK_DEFAULT 98304ull /* the mark kernel's lean form */
+/* Kernel-form thresholds for this graph's next incremental steps (tuning and
+ * A/B; results never depend on them): 0 = always the throughput form,
+ * UINT64_MAX = never.  Not thread-safe against a step in flight on the
+ * graph: call it between steps (the caller owns the graph, as for set_slots). */
+int rf_graph_set_forms(rf_graph *g, uint64_t thru, uint64_t thru_wide, uint64_t thru_mark);
 /* Asynchronous form (no count readback). */
 int rf_graph_recompute_async(rf_graph *g, int full, void *stream);
 /* rf_graph_set_slots_device + rf_graph_recompute_async(g, 0, stream) in one
@@ -370,6 +380,8 @@ typedef struct {
     uint64_t last_recomputed;
     float last_ms; /* device time of the last synchronous rf_graph_recompute (asynchronous
                     * incremental steps record no events: RF_K2_EVENTS=1 does) */
+    uint32_t last_levels_lf;  /* levels the last plain incremental step ran in the throughput form */
+    uint32_t last_mark_lf;    /* the last set_slots batch marked in the throughput form (0/1) */
 } rf_graph_stats;
 int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
 
@@ -386,8 +398,11 @@ int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
  * recompute) at once -- no lowering, no level analysis, no full recompute.
  * A partition (rf_graph_set_part) is not part of the file: re-attach it.
  * Errors: RF_EIO (cannot create / open / write), RF_EINVAL (not a graph
- * checkpoint, or another version), RF_EINTEGRITY (truncated, or the bytes do
- * not match their checksums: errors.Integrity). */
+ * checkpoint, or another version), RF_EINTEGRITY (truncated, the bytes do
+ * not match their checksums, or the structure is inconsistent:
+ * errors.Integrity), RF_EPRECONDITION from save when input slots were set
+ * since the last recompute (the file holds digests, not a pending change
+ * set: recompute first). */
 int rf_graph_save(rf_graph *g, const char *path);
 int rf_graph_restore(rf_ctx *ctx, const char *path, rf_graph **out);
 

@@ -414,6 +414,72 @@ void orc_graph_full(orc_graph *g, uint8_t *slots32) {
 }
 
 /* ------------------------------------------------------------------ */
+/* Job-local check of a whole slot table (the parity checker at sizes   */
+/* the serial evaluators above cannot reach in seconds): every job's    */
+/* output slot must equal SHA-256 of its material with the table's own  */
+/* digests in its holes -- flow.go:675-750's WriteDigest of one node    */
+/* from its deps' memoised digests (:653-658).  With every input slot   */
+/* at its assigned value this is parity of the whole table with the     */
+/* full evaluation, by induction over a topological order, whatever     */
+/* path (incremental or full) produced it.  Jobs are split over         */
+/* nthreads pthreads in chunks of 4096; returns the number of           */
+/* mismatching jobs and *first = the lowest one (~0 if none).           */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint64_t n_jobs; const uint32_t *out_slot, *tmpl_len, *hole_pos, *hole_slot;
+    const uint64_t *tmpl_off, *hole_ptr; const uint8_t *blob, *slots32;
+    int tid, nth; uint64_t bad, first;
+} check_job;
+
+static void *check_worker(void *p) {
+    check_job *c = (check_job *)p;
+    enum { CHUNK = 4096 };
+    uint8_t *buf = NULL, d[32];
+    uint64_t cap = 0;
+    c->bad = 0; c->first = ~0ull;
+    for (uint64_t lo = (uint64_t)c->tid * CHUNK; lo < c->n_jobs; lo += (uint64_t)c->nth * CHUNK) {
+        const uint64_t hi = lo + CHUNK < c->n_jobs ? lo + CHUNK : c->n_jobs;
+        for (uint64_t j = lo; j < hi; ++j) {
+            const uint32_t len = c->tmpl_len[j];
+            if (len > cap) { cap = 2 * (uint64_t)len + 64; buf = (uint8_t *)realloc(buf, cap); }
+            memcpy(buf, c->blob + c->tmpl_off[j], len);
+            for (uint64_t h = c->hole_ptr[j]; h < c->hole_ptr[j + 1]; ++h)
+                memcpy(buf + c->hole_pos[h], c->slots32 + 32ull * c->hole_slot[h], 32);
+            orc_sha256(buf, len, d);
+            if (memcmp(d, c->slots32 + 32ull * c->out_slot[j], 32)) {
+                if (!c->bad || j < c->first) c->first = j;
+                ++c->bad;
+            }
+        }
+    }
+    free(buf);
+    return NULL;
+}
+
+uint64_t orc_graph_check(uint64_t n_jobs, const uint32_t *out_slot, const uint64_t *tmpl_off,
+                         const uint32_t *tmpl_len, const uint64_t *hole_ptr, const uint32_t *hole_pos,
+                         const uint32_t *hole_slot, const uint8_t *blob, const uint8_t *slots32, int nthreads,
+                         uint64_t *first) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    check_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (check_job){n_jobs, out_slot, tmpl_len, hole_pos, hole_slot, tmpl_off, hole_ptr, blob, slots32,
+                              t, nthreads, 0, ~0ull};
+        pthread_create(&th[t], NULL, check_worker, &jobs[t]);
+    }
+    uint64_t bad = 0, f = ~0ull;
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        bad += jobs[t].bad;
+        if (jobs[t].bad && jobs[t].first < f) f = jobs[t].first;
+    }
+    if (first) *first = f;
+    return bad;
+}
+
+/* ------------------------------------------------------------------ */
 /* MurmurHash3 x64_128, seed 0 (murmur128.go:56-171)                   */
 /* ------------------------------------------------------------------ */
 static const uint64_t C1 = 0x87c37b91114253d5ULL, C2 = 0x4cf5ad432745937fULL;

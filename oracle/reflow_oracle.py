@@ -75,6 +75,8 @@ def lib():
         L.orc_graph_last_blocks.argtypes = [ctypes.c_void_p]
         L.orc_graph_last_blocks.restype = ctypes.c_uint64
         L.orc_graph_eval.argtypes = [ctypes.c_uint64, u8p, u8p, u8p, u8p, u8p, u8p, u8p, u8p, u8p]
+        L.orc_graph_check.argtypes = [ctypes.c_uint64, u8p, u8p, u8p, u8p, u8p, u8p, u8p, u8p, ctypes.c_int, u8p]
+        L.orc_graph_check.restype = ctypes.c_uint64
         _LIB = L
     return _LIB
 
@@ -119,6 +121,28 @@ class OGraph:
 
     def __del__(self):
         self.close()
+
+
+def check_slots(a, slots32, nthreads=1):
+    """orc_graph_check: every job of the rf_graph_desc-shaped arrays `a`
+    against a whole slot table ([n_slots][32] uint8, e.g. every slot a GPU
+    graph holds): (mismatching jobs, lowest such job or None).  Together with
+    the input slots' values this is parity with the full evaluation."""
+    s = np.ascontiguousarray(slots32, dtype=np.uint8).reshape(-1, 32)
+    assert len(s) >= int(a["n_slots"])
+    blob = np.frombuffer(a["blob"], dtype=np.uint8) if isinstance(a["blob"], (bytes, bytearray)) \
+        else np.ascontiguousarray(a["blob"], dtype=np.uint8)
+    arr = {k: np.ascontiguousarray(a[k], dtype=t) for k, t in (
+        ("out_slot", np.uint32), ("tmpl_off", np.uint64), ("tmpl_len", np.uint32), ("hole_ptr", np.uint64),
+        ("hole_pos", np.uint32), ("hole_slot", np.uint32))}
+    first = np.zeros(1, dtype=np.uint64)
+    n_jobs = len(arr["out_slot"])
+    bad = lib().orc_graph_check(n_jobs, arr["out_slot"].ctypes.data, arr["tmpl_off"].ctypes.data,
+                                arr["tmpl_len"].ctypes.data, arr["hole_ptr"].ctypes.data,
+                                arr["hole_pos"].ctypes.data if len(arr["hole_pos"]) else None,
+                                arr["hole_slot"].ctypes.data if len(arr["hole_slot"]) else None,
+                                blob.ctypes.data, s.ctypes.data, int(nthreads), first.ctypes.data)
+    return int(bad), (int(first[0]) if bad else None)
 
 
 def _buf(b: bytes):

@@ -31,7 +31,7 @@ EXPORTS = [
     "rf_fileset_digest_device", "rf_install_dir", "rf_install_info", "rf_install_entries",
     "rf_install_destroy",
     "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
-    "rf_graph_save", "rf_graph_restore",
+    "rf_graph_save", "rf_graph_restore", "rf_graph_set_forms",
     "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
     "rf_bloom_destroy", "rf_bloom_probe", "rf_bloom_probe_device", "rf_bloom_add",
@@ -230,7 +230,8 @@ class GraphStats(ctypes.Structure):
                 ("n_levels", ctypes.c_uint32), ("max_level_jobs", ctypes.c_uint32),
                 ("total_blocks", ctypes.c_uint64), ("hole_count", ctypes.c_uint64),
                 ("template_bytes", ctypes.c_uint64), ("last_recomputed", ctypes.c_uint64),
-                ("last_ms", ctypes.c_float)]
+                ("last_ms", ctypes.c_float), ("last_levels_lf", ctypes.c_uint32),
+                ("last_mark_lf", ctypes.c_uint32)]
 
 
 _lib = None
@@ -291,6 +292,7 @@ def lib():
             "rf_install_destroy": ([vp], None),
             "rf_graph_load": ([vp, vp, vp], i32), "rf_graph_destroy": ([vp], None),
             "rf_graph_save": ([vp, ctypes.c_char_p], i32), "rf_graph_restore": ([vp, ctypes.c_char_p, vp], i32),
+            "rf_graph_set_forms": ([vp, u64, u64, u64], i32),
             "rf_graph_set_slots": ([vp, vp, vp, u32], i32),
             "rf_graph_set_slots_device": ([vp, vp, vp, u32, vp], i32),
             "rf_graph_recompute": ([vp, i32, vp], i32),
@@ -662,11 +664,14 @@ class DeviceBuffer:
         assert arr.nbytes <= self.nbytes
         _check(lib().rf_memcpy_h2d(self.ctx.handle, self._p, arr.ctypes.data, arr.nbytes))
 
-    def to_numpy(self, dtype=np.uint8, count=None) -> np.ndarray:
+    def to_numpy(self, dtype=np.uint8, count=None, offset=0) -> np.ndarray:
+        """count elements of dtype from byte `offset` (default: the rest)."""
         dt = np.dtype(dtype)
-        n = self.nbytes // dt.itemsize if count is None else count
+        n = (self.nbytes - offset) // dt.itemsize if count is None else count
+        assert 0 <= offset and offset + n * dt.itemsize <= self.nbytes
         out = np.empty(n, dtype=dt)
-        _check(lib().rf_memcpy_d2h(self.ctx.handle, out.ctypes.data, self._p, out.nbytes))
+        _check(lib().rf_memcpy_d2h(self.ctx.handle, out.ctypes.data, ctypes.c_void_p(self.ptr + offset),
+                                   out.nbytes))
         return out
 
     def zero(self):
@@ -798,6 +803,16 @@ class Graph:
         s = GraphStats()
         _check(lib().rf_graph_stats_get(self._h, ctypes.byref(s)))
         return s
+
+    # kernel-form thresholds (include/reflow_hip.h RF_K2_THRU*_DEFAULT)
+    THRU_DEFAULT, THRU_WIDE_DEFAULT, THRU_MARK_DEFAULT = 24576, 65536, 98304
+    NEVER = (1 << 64) - 1
+
+    def set_forms(self, thru, thru_wide=None, thru_mark=None):
+        """rf_graph_set_forms: 0 = always the throughput form, Graph.NEVER =
+        never; thru_wide / thru_mark default to thru."""
+        _check(lib().rf_graph_set_forms(self._h, int(thru), int(thru if thru_wide is None else thru_wide),
+                                        int(thru if thru_mark is None else thru_mark)))
 
     def save(self, path):
         """rf_graph_save: the lowered graph and its slot digests to `path`."""

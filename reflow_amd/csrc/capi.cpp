@@ -1476,6 +1476,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         const char* v = getenv("RF_K2_STREAM");  // (opt-in variant, read per load)
         G.stream_handover = v && atoi(v) == 1;
     }
+    graph_forms_from_env(G);
     if (n_lead && !getenv("RF_K2_NO_MIDSTATE")) {  // (RF_K2_NO_MIDSTATE: A/B)
         struct Tmp {
             DevBuf b;
@@ -1580,7 +1581,28 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
 // 16k chains at full speed, one 64-job workgroup per CU), from 64k for levels
 // of long jobs (inc_level 2: a lane alone hashes an 18-block job at ~5 us a
 // block, memory-latency-bound, against the three-wave latency form's ~1.5).
-static constexpr uint64_t kThruSlots = 24576, kThruSlotsWide = 65536;
+static constexpr uint64_t kThruSlots = RF_K2_THRU_DEFAULT, kThruSlotsWide = RF_K2_THRU_WIDE_DEFAULT;
+
+// The form thresholds of a graph being loaded or restored: the defaults, or
+// RF_K2_THRU / RF_K2_THRU_WIDE (tests and A/B runs force either form); read
+// here once, never per step (a libc call per step, and racy against setenv
+// in threaded callers).  rf_graph_set_forms changes them later.
+void graph_forms_from_env(GraphDev& G) {
+    const char* tv = getenv("RF_K2_THRU");
+    const char* tw = getenv("RF_K2_THRU_WIDE");
+    G.cfg_thru = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
+    G.cfg_thru_wide = tw ? (uint64_t)strtoull(tw, nullptr, 10) : tv ? G.cfg_thru : kThruSlotsWide;
+    G.cfg_thru_mark = tv ? G.cfg_thru : RF_K2_THRU_MARK_DEFAULT;
+}
+
+extern "C" int rf_graph_set_forms(rf_graph* gr, uint64_t thru, uint64_t thru_wide, uint64_t thru_mark) {
+    ARG(gr, "null argument");
+    std::lock_guard<std::mutex> lk(gr->ctx->mu);
+    gr->g.cfg_thru = thru;
+    gr->g.cfg_thru_wide = thru_wide;
+    gr->g.cfg_thru_mark = thru_mark;
+    return RF_OK;
+}
 
 // The launch sequence (one kernel per level + a step-end kernel) only reads
 // device-side list lengths, so it is fixed for a loaded graph: capture it once
@@ -1606,15 +1628,13 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
     for (uint32_t l = 0; l < G.n_levels; ++l) any |= (G.inc_level[l] & kLvlForm) != 0;
     if (plain && !full && any) {
         // the level-kernel forms for this step: a level that can receive at
-        // least RF_K2_THRU chains (default kThruSlots; RF_K2_THRU_WIDE,
-        // default kThruSlotsWide, for levels of long jobs) fills the chip, and
-        // the lane-per-job form (k2_level_lf) outruns the two-lane latency
-        // form (k2_level_pl) there -- DESIGN.md §5
-        const char* tv = getenv("RF_K2_THRU");  // (read per step: tests force either form)
-        const char* tw = getenv("RF_K2_THRU_WIDE");
+        // least cfg_thru chains (default kThruSlots; cfg_thru_wide, default
+        // kThruSlotsWide, for levels of long jobs) fills the chip, and the
+        // lane-per-job form (k2_level_lf) outruns the two-lane latency form
+        // (k2_level_pl) there -- DESIGN.md §5
         G.step_marked = gr->marked;
-        G.thru_slots = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
-        G.thru_slots_wide = tw ? (uint64_t)strtoull(tw, nullptr, 10) : tv ? G.thru_slots : kThruSlotsWide;
+        G.thru_slots = G.cfg_thru;
+        G.thru_slots_wide = G.cfg_thru_wide;
         // the sink level's list rides on the launch of the last level from
         // kLvlSinkMin to kLvlFill that runs in the throughput form (the short
         // sink jobs fill SIMDs its waves leave idle; the latency form is a
@@ -1637,9 +1657,11 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
+        if (lvl_lo == 0) G.last_levels_lf = 0;
         for (uint32_t l = lvl_lo; l < std::min(lvl_hi, G.n_levels); ++l) {
             if (!(G.inc_level[l] & kLvlForm) || (l == sink && attach != ~0u)) continue;
             HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr, l == attach ? sink : ~0u));
+            G.last_levels_lf += graph_level_lf(G, l) ? 1u : 0u;
             first = false;
         }
         gr->last_counts = G.counts;
@@ -1945,6 +1967,8 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
     out->hole_count = gr->hole_count;
     out->template_bytes = gr->tmpl_bytes;
     out->last_recomputed = gr->last_recomputed;
+    out->last_levels_lf = gr->g.last_levels_lf;
+    out->last_mark_lf = gr->g.last_mark_lf;
     if (gr->timed) {
         HIPC(hipEventSynchronize(gr->e1));
         HIPC(hipEventElapsedTime(&out->last_ms, gr->e0, gr->e1));
@@ -2176,44 +2200,8 @@ extern "C" int rf_bloom_collect(rf_bloom* bl, const uint8_t* digests32, const in
 // K5: Canonicalize's flowMap (flow.go:814-843, flowMap.Get/Put :881-907)
 // Scratch of a device-form call: the context's StreamScratch, handed
 // between the callers' streams in stream order (ctx.h).
-// RF_DEDUP_SCRATCH (diagnostic, tools/pool_diag.py): the round-2 per-call
-// stream-ordered pool scratch that came back corrupted, and variants that
-// bisect it -- "pool" as it was (release threshold max, hipMemsetAsync),
-// "pool_sync" + a stream sync after the allocations, "pool_fill" a fill kernel
-// instead of hipMemsetAsync, "pool_nothresh" the pool's default threshold.
-static int dedup_pool_diag(const char* mode, rf_ctx* ctx, const void* d_digests32, uint32_t n, void* d_canon,
-                           void* d_n_unique, hipStream_t s) {
-    static std::once_flag once;
-    if (strcmp(mode, "pool_nothresh") != 0)
-        std::call_once(once, [&] {
-            hipMemPool_t pool = nullptr;
-            if (hipDeviceGetDefaultMemPool(&pool, ctx->device) == hipSuccess && pool) {
-                uint64_t keep = ~0ull;
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-            }
-        });
-    void *tab = nullptr, *slot_of = nullptr;
-    const size_t tab_bytes = 4ull * dedup_table_slots(n);
-    HIPC(hipMallocAsync(&tab, tab_bytes, s));
-    HIPC(hipMallocAsync(&slot_of, 4ull * std::max<uint32_t>(n, 1), s));
-    if (strcmp(mode, "pool_sync") == 0) HIPC(hipStreamSynchronize(s));
-    if (strcmp(mode, "pool_fill") == 0) HIPC(launch_fill_u32(static_cast<uint32_t*>(tab), 0xffffffffu, tab_bytes / 4, s));
-    hipError_t e = launch_dedup(static_cast<const uint8_t*>(d_digests32), n, static_cast<uint32_t*>(tab),
-                                static_cast<uint32_t*>(slot_of), static_cast<uint32_t*>(d_canon),
-                                static_cast<uint32_t*>(d_n_unique), s, strcmp(mode, "pool_fill") != 0);
-    (void)hipFreeAsync(slot_of, s);
-    (void)hipFreeAsync(tab, s);
-    if (e != hipSuccess) return fail(RF_EDEVICE, "dedup: %s", hipGetErrorString(e));
-    if (getenv("RF_DEDUP_PTRS"))
-        fprintf(stderr, "[dedup %s] tab %p slot_of %p canon %p n_unique %p stream %p\n", mode, tab, slot_of, d_canon,
-                d_n_unique, (void*)s);
-    return RF_OK;
-}
-
 static int dedup_on_stream(rf_ctx* ctx, const void* d_digests32, uint32_t n, void* d_canon, void* d_n_unique,
                            hipStream_t s) {
-    if (const char* mode = getenv("RF_DEDUP_SCRATCH"))
-        if (strncmp(mode, "pool", 4) == 0) return dedup_pool_diag(mode, ctx, d_digests32, n, d_canon, d_n_unique, s);
     StreamScratch& sc = ctx->sc_dedup;
     std::lock_guard<std::mutex> lk(sc.mu);
     const size_t tab_bytes = 4ull * dedup_table_slots(n);

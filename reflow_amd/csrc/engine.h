@@ -122,6 +122,13 @@ struct GraphDev {
     // upper bound of the chains that can reach the level), the level's size
     // the other bound (merge-tree levels stay in the latency form)
     uint64_t step_marked = 0, thru_slots = ~0ull, thru_slots_wide = ~0ull;  // (wide: inc_level 2)
+    // The thresholds themselves, fixed per graph: defaults (or RF_K2_THRU /
+    // RF_K2_THRU_WIDE read once when the graph is loaded or restored), or
+    // rf_graph_set_forms; cfg_thru_mark: the mark kernel's lean form
+    // (k3_mark_slots_lf) from this many changed slots
+    uint64_t cfg_thru = 0, cfg_thru_wide = 0, cfg_thru_mark = 0;
+    // what the last plain step / mark launch chose (rf_graph_stats)
+    uint32_t last_levels_lf = 0, last_mark_lf = 0;
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     unsigned long long* wgst = nullptr;    // diagnostic per-workgroup records [L][2048][4] (RF_K2_WGSTAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the
@@ -134,7 +141,7 @@ struct GraphDev {
 // start[i] (64-B units) into mid[2i..2i+1] (state words); IV when lead[i] = 0.
 hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, const uint32_t* lead, uint32_t n,
                                   uint4* mid, hipStream_t s);
-hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
+hipError_t launch_graph_mark_slots(GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);
 // k3_mark_slots as a graph kernel node: argument values + node parameters
 struct MarkArgs {

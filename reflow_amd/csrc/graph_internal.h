@@ -49,8 +49,10 @@ struct rf_graph {
     hipGraphNode_t upd_mark = nullptr;
     bool timed = false;
     bool time_next = false;  // record e0/e1 around the next plain recompute (synchronous callers)
-    // input slots written (set_slots / update / imports) since the last
-    // incremental step: picks that step's level-kernel form (graph_enqueue)
+    // input slots written since the last incremental step (set_slots,
+    // set_slots_device, update; a partition's imports before a post-exchange
+    // pass that is a step of its own): picks that step's level-kernel forms
+    // (graph_enqueue); rf_graph_save refuses while it is non-zero
     uint64_t marked = 0;
     uint32_t* last_counts = nullptr;  // device cursors of the last recompute (counts_last, or a plain step's half)
     GraphPart* part = nullptr;  // multi-GPU partition (rf_graph_set_part), else null
@@ -61,5 +63,6 @@ struct rf_graph {
 int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s, uint32_t lvl_lo = 0, uint32_t lvl_hi = ~0u,
                            bool swap = true);
 bool graph_plain_steps();  // incremental steps are plain launches (not RF_K2_GRAPH=1)
+void graph_forms_from_env(rf::GraphDev& G);  // form thresholds at load / restore
 int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes);
 void graph_part_release(rf_graph* gr);

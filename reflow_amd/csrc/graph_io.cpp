@@ -97,35 +97,90 @@ void hash_chunks(rf_ctx* ctx, const uint8_t* buf, uint64_t n, uint8_t* out) {
     });
 }
 
-// Range checks of a piece [o, o + n) of a device section: every index a
-// kernel follows stays inside its array.  kStage keeps records whole.
-int check_piece(const char* name, const uint8_t* p, uint64_t n, uint64_t o, const Header& h) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
-    const uint64_t J = h.n_jobs, S = h.n_slots, H = h.n_holes, TB = h.tmpl_bytes / 64;
-    if (!strcmp(name, "meta")) {
-        for (uint64_t r = 0; r < n / 32; ++r) {
-            const uint32_t* m = w + 8 * r;
-            if ((uint64_t)m[0] + m[1] > TB || m[2] > m[3] || m[3] > H || m[4] >= S || m[5] > m[6] || m[6] > H ||
-                (m[7] != 0xffffffffu && m[7] >= J))
-                return fail(RF_EINTEGRITY, "graph restore: job record %llu out of range",
-                            (unsigned long long)(o / 32 + r));
+// Consistency checks of a file being restored, section by section, before
+// any of it reaches a kernel: every index a kernel follows stays inside its
+// array, and the structure the kernels assume holds (a file whose checksums
+// match may still come from anywhere).  Sections arrive in file order
+// (lvl_start, inc_level, ext2int, meta, holes, cons_ptr, cons_job, ...), the
+// device ones in pieces [o, o + n) that keep records whole (kStage).
+struct Validator {
+    const Header& h;
+    const std::vector<uint32_t>& lvl;      // level layout (host section, complete before the device ones)
+    std::vector<uint32_t>& out_slot;       // internal job -> out slot (from the records)
+    std::vector<uint8_t> one_hole;         // internal job has exactly one hole
+    std::vector<uint8_t> produced;         // slot is some job's output
+    std::vector<uint32_t> cons_ptr;        // host copy: slot -> its reverse-edge range
+    uint64_t slot = 0;                     // cons_job cursor: the slot whose range holds the next edge
+
+    Validator(const Header& hh, const std::vector<uint32_t>& l, std::vector<uint32_t>& os)
+        : h(hh), lvl(l), out_slot(os) {}
+
+    // a host section, once complete
+    int host_done(const char* name, const std::vector<uint32_t>* ext2int) {
+        if (!strcmp(name, "lvl_start")) {
+            if (lvl[0] != 0 || lvl[h.n_levels] != h.n_jobs)
+                return fail(RF_EINTEGRITY, "graph restore: bad level layout");
+            for (uint32_t l = 0; l < h.n_levels; ++l)
+                if (lvl[l] > lvl[l + 1]) return fail(RF_EINTEGRITY, "graph restore: bad level layout");
+        } else if (!strcmp(name, "ext2int")) {  // a permutation of the internal ids
+            std::vector<uint8_t> seen(h.n_jobs, 0);
+            for (uint32_t i : *ext2int) {
+                if (i >= h.n_jobs || seen[i]) return fail(RF_EINTEGRITY, "graph restore: job numbering damaged");
+                seen[i] = 1;
+            }
         }
-    } else if (!strcmp(name, "holes")) {
-        for (uint64_t r = 0; r < n / 8; ++r)
-            if (w[2 * r + 1] >= S || w[2 * r] >= (1u << 24))
-                return fail(RF_EINTEGRITY, "graph restore: hole %llu out of range", (unsigned long long)(o / 8 + r));
-    } else if (!strcmp(name, "cons_ptr")) {
-        for (uint64_t r = 0; r < n / 4; ++r)
-            if (w[r] > H || (o + 4 * r > 0 && r > 0 && w[r] < w[r - 1]))
-                return fail(RF_EINTEGRITY, "graph restore: reverse-edge index out of range");
-    } else if (!strcmp(name, "cons_job")) {
-        for (uint64_t r = 0; r < n / 8; ++r)
-            if (w[2 * r] >= J || (w[2 * r + 1] & 0x7fffffffu) >= h.n_levels)
-                return fail(RF_EINTEGRITY, "graph restore: reverse edge %llu out of range",
-                            (unsigned long long)(o / 8 + r));
+        return RF_OK;
     }
-    return RF_OK;
-}
+
+    int piece(const char* name, const uint8_t* p, uint64_t n, uint64_t o) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+        const uint64_t J = h.n_jobs, S = h.n_slots, H = h.n_holes, TB = h.tmpl_bytes / 64;
+        if (!strcmp(name, "meta")) {
+            if (o == 0) one_hole.assign(J, 0), produced.assign(S, 0);
+            for (uint64_t r = 0; r < n / 32; ++r) {
+                const uint32_t* m = w + 8 * r;
+                if ((uint64_t)m[0] + m[1] > TB || m[2] > m[3] || m[3] > H || m[4] >= S || m[5] > m[6] || m[6] > H ||
+                    (m[7] != 0xffffffffu && m[7] >= J))
+                    return fail(RF_EINTEGRITY, "graph restore: job record %llu out of range",
+                                (unsigned long long)(o / 32 + r));
+                const uint64_t j = o / 32 + r;
+                out_slot[j] = m[4];
+                one_hole[j] = m[3] - m[2] == 1;
+                produced[m[4]] = 1;
+            }
+        } else if (!strcmp(name, "holes")) {
+            for (uint64_t r = 0; r < n / 8; ++r)
+                if (w[2 * r + 1] >= S || w[2 * r] >= (1u << 24))
+                    return fail(RF_EINTEGRITY, "graph restore: hole %llu out of range",
+                                (unsigned long long)(o / 8 + r));
+        } else if (!strcmp(name, "cons_ptr")) {
+            if (o == 0) cons_ptr.reserve(S + 1);
+            for (uint64_t r = 0; r < n / 4; ++r) {
+                if (w[r] > H || (!cons_ptr.empty() && w[r] < cons_ptr.back()))
+                    return fail(RF_EINTEGRITY, "graph restore: reverse-edge index out of range");
+                cons_ptr.push_back(w[r]);
+            }
+            if (o + n == 4 * (S + 1) && (cons_ptr.size() != S + 1 || cons_ptr[0] != 0 || cons_ptr[S] != H))
+                return fail(RF_EINTEGRITY, "graph restore: reverse-edge index out of range");
+        } else if (!strcmp(name, "cons_job")) {
+            // edge e = {consumer x, its level y | kSlotFused}: x must lie in
+            // level y (append_jobs writes list[lvl_start[y] + count] and its
+            // record there), and the slot-fused flag may mark only the first
+            // edge of an input slot's range, pointing at a one-hole job (the
+            // mark kernel hashes that job with the slot's digest in its hole)
+            for (uint64_t r = 0; r < n / 8; ++r) {
+                const uint64_t e = o / 8 + r;
+                while (slot < S && cons_ptr[slot + 1] <= e) ++slot;
+                const uint32_t x = w[2 * r], y = w[2 * r + 1] & 0x7fffffffu;
+                const bool fused = (w[2 * r + 1] & 0x80000000u) != 0;
+                if (x >= J || y >= h.n_levels || x < lvl[y] || x >= lvl[y + 1] || slot >= S ||
+                    (fused && (e != cons_ptr[slot] || produced[slot] || !one_hole[x])))
+                    return fail(RF_EINTEGRITY, "graph restore: reverse edge %llu inconsistent", (unsigned long long)e);
+            }
+        }
+        return RF_OK;
+    }
+};
 
 struct Stage {  // pinned staging, released on every path
     HostBuf b;
@@ -145,6 +200,11 @@ extern "C" int rf_graph_save(rf_graph* gr, const char* path) {
     ARG(gr && path && *path, "null argument");
     rf_ctx* ctx = gr->ctx;
     std::lock_guard<std::mutex> lk(ctx->mu);
+    // The file holds slot digests, not the change set pending between a
+    // set_slots and the recompute that consumes it (the queued flags and
+    // per-level lists): a slot set but not yet propagated would be saved
+    // with stale consumers and restored with nothing queued.  Refuse.
+    if (gr->marked) return fail(RF_EPRECONDITION, "graph save: input slots set since the last recompute");
     DevGuard dg(ctx->device);
     // steps queued on callers' streams must be complete before the state is read
     HIPC(hipDeviceSynchronize());
@@ -238,6 +298,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
         const char* v = getenv("RF_K2_STREAM");
         G.stream_handover = v && atoi(v) == 1;
     }
+    graph_forms_from_env(G);
     if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes)) return rc;
     const bool has_mid = (h.flags & kHasMid) != 0;
     if (has_mid) {
@@ -249,6 +310,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     std::vector<uint32_t> ext2int(h.n_jobs);
     std::vector<Section> secs = sections(gr, lvl, inc, ext2int, has_mid);
     std::vector<uint32_t> out_slot(h.n_jobs);  // internal job -> out slot (from the records)
+    Validator val(h, lvl, out_slot);
     Stage st;
     HostBuf& stage = st.b;
     HIPC(stage.ensure(kStage));
@@ -264,13 +326,13 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
             const size_t d0 = digests.size();
             digests.resize(d0 + 32 * ((n + kChunk - 1) / kChunk));
             hash_chunks(ctx, dst, n, digests.data() + d0);
-            // the indices the kernels follow are range-checked as on load (a
-            // file with valid checksums may still come from anywhere)
-            if (int rc = check_piece(sc.name, dst, n, o, h)) return rc;
-            if (!strcmp(sc.name, "meta"))  // kStage is a multiple of the 32-B record
-                for (uint64_t r = 0; r < n / 32; ++r) memcpy(&out_slot[o / 32 + r], dst + 32 * r + 16, 4);
+            // the indices and structure the kernels follow are checked before
+            // the piece reaches the device (kStage keeps records whole)
+            if (int rc = val.piece(sc.name, dst, n, o)) return rc;
             if (sc.dev) HIPC(sync_copy(ctx, static_cast<uint8_t*>(sc.dev) + o, dst, n, hipMemcpyHostToDevice));
         }
+        if (!sc.dev)
+            if (int rc = val.host_done(sc.name, &ext2int)) return rc;
     }
     uint64_t nd = 0;
     uint8_t root[32], want[32], end[8];
@@ -284,11 +346,8 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     host_sha256(all.data(), all.size(), root);
     if (memcmp(root, want, 32) != 0 || stored != digests)
         return fail(RF_EINTEGRITY, "graph restore: %s does not match its checksums", path);
-    // host-side state: level layout (and its device copy, which every level
-    // kernel reads), and slot -> producing (external) job
-    for (uint32_t l = 0; l < h.n_levels; ++l)
-        if (lvl[l] > lvl[l + 1] || lvl[l + 1] > h.n_jobs) return fail(RF_EINTEGRITY, "graph restore: bad level layout");
-    if (lvl[0] != 0 || lvl[h.n_levels] != h.n_jobs) return fail(RF_EINTEGRITY, "graph restore: bad level layout");
+    // host-side state: level layout (checked as it arrived; its device copy
+    // every level kernel reads), and slot -> producing (external) job
     HIPC(sync_copy(ctx, gr->b_lvl_start.p, lvl.data(), 4ull * (h.n_levels + 1), hipMemcpyHostToDevice));
     G.lvl_start.assign(lvl.begin(), lvl.end());
     G.inc_level.assign(inc.begin(), inc.end());

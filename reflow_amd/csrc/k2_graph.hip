@@ -1794,9 +1794,9 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
 }
 
 constexpr uint32_t kMarkBlock = 64;
-// change sets from this size mark in k3_mark_slots_lf (the resident waves of
-// k3_mark_slots, two per SIMD at 240 VGPRs, hold 131k lanes)
-constexpr uint64_t kThruMark = 98304;
+// change sets from GraphDev::cfg_thru_mark slots (RF_K2_THRU_MARK_DEFAULT =
+// 98,304) mark in k3_mark_slots_lf (the resident waves of k3_mark_slots, two
+// per SIMD at 240 VGPRs, hold 131k lanes)
 
 // set_slots: write input digests; a changed slot queues (or hashes) its consumers.
 __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __restrict__ sl,
@@ -1894,7 +1894,7 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
 }
 
 // k3_mark_slots for change sets that fill the chip (GraphDev::thru form
-// choice, at least kThruMark slots): the slot-fused chains without the
+// choice, at least cfg_thru_mark slots): the slot-fused chains without the
 // look-ahead (hash_fused_chain_lean), so three waves fit a SIMD instead of
 // two and a 100M-node DAG's 141k changed slots run in one round of resident
 // waves.
@@ -2075,14 +2075,13 @@ static LevelArgs mark_level_args(const GraphDev& g) {
     return a;
 }
 
-hipError_t launch_graph_mark_slots(const GraphDev& g, const uint32_t* slots, const uint8_t* digests,
+hipError_t launch_graph_mark_slots(GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s) {
     if (!n) return hipSuccess;
-    // RF_K2_THRU (as for the level kernels; read per call): the lean form from
-    // kThruMark slots
-    const char* tv = getenv("RF_K2_THRU");
-    const uint64_t thr = tv ? strtoull(tv, nullptr, 10) : kThruMark;
-    if (n >= thr)
+    g.last_mark_lf = n >= g.cfg_thru_mark ? 1u : 0u;
+    // the lean form from g.cfg_thru_mark slots (default RF_K2_THRU_MARK_DEFAULT; fixed per
+    // graph, rf_graph_set_forms)
+    if (n >= g.cfg_thru_mark)
         hipLaunchKernelGGL(k3_mark_slots_lf, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, slots, digests, n,
                            mark_level_args(g));
     else

@@ -222,6 +222,10 @@ static int recompute_rounds(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn
         if (!P->n_import) continue;
         HIPC(launch_part_apply(gr->g, P->d_import_slot.as<uint32_t>(), P->d_import_bid.as<uint32_t>(), P->n_import,
                                nullptr, P->d_gather.as<uint8_t>(), s));
+        // the imports are this pass's marked input slots (an upper bound:
+        // only changed ones queue anything) -- except in a deferred step,
+        // whose passes must pick the same forms (the sink list's launch)
+        if (!defer) gr->marked += P->n_import;
         if (int rc = graph_recompute_locked(gr, 0, s, lo)) return rc;
         if (out_recomputed)
             if (int rc = part_counts(gr, s, &tot)) return rc;
@@ -266,9 +270,11 @@ extern "C" int rf_graph_recompute_part(rf_graph* gr, rf_comm* comm, rf_host_allg
         }
         if (int rc = part_gather(gr, comm, fn, user, s)) return rc;
         if (!P->any_import) break;  // exports observed, nobody consumes them
-        if (run)
+        if (run) {
             HIPC(launch_part_apply(gr->g, P->d_import_slot.as<uint32_t>(), P->d_import_bid.as<uint32_t>(),
                                    P->n_import, P->d_bits.as<uint32_t>(), P->d_gather.as<uint8_t>(), s));
+            gr->marked += P->n_import;  // (upper bound of the next superstep's changed inputs)
+        }
     }
     P->last_supersteps = steps;
     if (out_recomputed) *out_recomputed = tot;

@@ -160,3 +160,120 @@ def test_restored_pieces_resume_partitioned(tmp_path):
             c.close()
 
     assert all(PC.run_threads(nr, body))
+
+
+def test_save_refused_with_pending_change(ctx, tmp_path):
+    """A slot set but not yet recomputed is a change set the file cannot hold
+    (its consumers' queued flags and lists): save refuses with
+    RF_EPRECONDITION; after the recompute it saves, and the restored graph
+    takes a further change to the oracle's digests."""
+    dag = Dag1000(6, 4)
+    a = dag.arrays()
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+    g = _load(ctx, dag)
+    g.recompute(full=True)
+    sa, _, na = dag.change_set(0.2, seed=5)
+    g.set_slots(sa, na)
+    path = str(tmp_path / "p.ckpt")
+    with pytest.raises(capi.RfError) as e:
+        g.save(path)
+    assert e.value.code == capi.RF_EPRECONDITION
+    assert not os.path.exists(path) and not os.path.exists(path + ".tmp")
+    g.recompute(full=False)
+    g.save(path)
+    g.close()
+    r = capi.Graph.restore(ctx, path)
+    sb, _, nb = dag.change_set(0.2, seed=6)
+    r.set_slots(sb, nb)
+    r.recompute(full=False)
+    og = O.OGraph(a)
+    og.set_inputs(dag.file_slots, dag.leaf_ids)
+    og.full()
+    og.update(sa, na)
+    og.update(sb, nb)
+    assert (r.get_slots(every) == og.slots[:a["n_slots"]]).all()
+    og.close()
+    r.close()
+
+
+def _sections(raw):
+    """(offset, length) of each section of a checkpoint file (graph_io.cpp:
+    128-B header, n_sections x {u64 length, bytes}, then the chunk digests,
+    the root digest and the end marker)."""
+    import struct
+    n_sec = struct.unpack_from("<Q", raw, 64)[0]
+    out, o = [], 128
+    for _ in range(n_sec):
+        ln = struct.unpack_from("<Q", raw, o)[0]
+        out.append((o + 8, ln))
+        o += 8 + ln
+    return out, o
+
+
+def _rechecksum(raw):
+    """The same file with every chunk digest and the root recomputed: a
+    structurally damaged file whose checksums all match."""
+    import hashlib
+    import struct
+    chunk = 64 << 20
+    secs, end = _sections(raw)
+    digs = b""
+    for o, ln in secs:
+        for c in range(0, ln, chunk):
+            digs += hashlib.sha256(raw[o + c:o + min(ln, c + chunk)]).digest()
+    root = hashlib.sha256(raw[:128] + digs).digest()
+    return raw[:end] + struct.pack("<Q", len(digs) // 32) + digs + root + raw[-8:]
+
+
+def test_structurally_damaged_checkpoints_refused(ctx, tmp_path):
+    """Files whose checksums match but whose structure is inconsistent are
+    refused before anything reaches a kernel: a reverse edge
+    naming a consumer outside its level, the slot-fused flag on an edge that
+    is not its input slot's first, and a job numbering that is not a
+    permutation.  The untouched file, re-checksummed the same way, restores."""
+    import struct
+    dag = Dag1000(3, 4)
+    g = _load(ctx, dag)
+    g.recompute(full=True)
+    path = str(tmp_path / "s.ckpt")
+    g.save(path)
+    g.close()
+    raw = open(path, "rb").read()
+    secs, _ = _sections(raw)
+    names = ["lvl_start", "inc_level", "ext2int", "meta", "holes", "cons_ptr", "cons_job", "tmpl", "slots", "mid"]
+    sec = dict(zip(names, secs))
+    lvl = np.frombuffer(raw, np.uint32, sec["lvl_start"][1] // 4, sec["lvl_start"][0])
+    cons_ptr = np.frombuffer(raw, np.uint32, sec["cons_ptr"][1] // 4, sec["cons_ptr"][0])
+    cons = np.frombuffer(raw, np.uint32, sec["cons_job"][1] // 4, sec["cons_job"][0]).reshape(-1, 2)
+
+    def restore(data):
+        p = str(tmp_path / "x.ckpt")
+        open(p, "wb").write(_rechecksum(data))
+        return capi.Graph.restore(ctx, p)
+
+    restore(raw).close()  # the rewriter itself keeps an intact file intact
+
+    def refused(data):
+        with pytest.raises(capi.RfError) as e:
+            restore(data)
+        assert e.value.code == capi.RF_EINTEGRITY, e.value
+
+    # 1. an edge's level word pointing at another level than its consumer's
+    e0 = 0
+    x, y = int(cons[e0, 0]), int(cons[e0, 1]) & 0x7fffffff
+    other = next(lv for lv in range(len(lvl) - 1) if lv != y and not (lvl[lv] <= x < lvl[lv + 1]))
+    bad = bytearray(raw)
+    struct.pack_into("<I", bad, sec["cons_job"][0] + 8 * e0 + 4, other | (int(cons[e0, 1]) & 0x80000000))
+    refused(bytes(bad))
+    # 2. the slot-fused flag on an edge that is not the first of its slot's range
+    mid_edges = [e for s in range(len(cons_ptr) - 1) for e in range(int(cons_ptr[s]) + 1, int(cons_ptr[s + 1]))]
+    assert mid_edges
+    e1 = mid_edges[0]
+    bad = bytearray(raw)
+    struct.pack_into("<I", bad, sec["cons_job"][0] + 8 * e1 + 4, int(cons[e1, 1]) | 0x80000000)
+    refused(bytes(bad))
+    # 3. two external jobs mapped to one internal id
+    bad = bytearray(raw)
+    first = struct.unpack_from("<I", bad, sec["ext2int"][0])[0]
+    struct.pack_into("<I", bad, sec["ext2int"][0] + 4, first)
+    refused(bytes(bad))

@@ -3,8 +3,8 @@ hand-over (RF_K2_STREAM=1: k2_level_pl<2, true>, whose chunk flags are
 published after an LDS wait -- ADVICE r02), every queueable level run as a
 three-wave "wide" workgroup (RF_K2_WIDE=1: k2_level_pl<3>), and every
 incremental step in the lane-per-job throughput form (RF_K2_THRU=0:
-k2_level_lf).  The first two are read when a graph is loaded, the third per
-step, so one process covers them.  Checked against the
+k2_level_lf).  All three are read once, when a graph is loaded, so one
+process covers them.  Checked against the
 oracle on the random fused-chain graphs and the 1000align DAG, and on a
 larger 1000align DAG against the default mode's incremental recompute."""
 import numpy as np
@@ -19,7 +19,8 @@ from test_gpu_dag_fusion import load as load_jobs
 pytestmark = pytest.mark.gpu
 
 # RF_K2_THRU=0: every incremental step in the lane-per-job throughput form
-# (k2_level_lf), which the library picks for change sets of >= 64k slots
+# (k2_level_lf), which the library picks by itself for levels that can
+# receive >= 24k chains (tests/test_gpu_dag_default_forms.py)
 MODES = [("RF_K2_STREAM", "1"), ("RF_K2_WIDE", "1"), ("RF_K2_THRU", "0")]
 
 
@@ -81,7 +82,7 @@ def test_forced_mode_dag1000(ctx, monkeypatch, var, val):
         gg.recompute(full=False)
 
     gf = load_dag(ctx, big)
-    run(gf)  # with the mode set (load-time and per-step variables alike)
+    run(gf)  # loaded with the mode set
     monkeypatch.delenv(var)
     gd = load_dag(ctx, big)
     run(gd)

@@ -1,7 +1,7 @@
 """A/B of the incremental level-kernel forms on the bench's DAGs, one process,
 one graph load each: every level in k2_level_pl (two-lane latency form), every
 level in k2_level_lf (lane-per-job throughput form), and the library's
-per-level choice -- set per step by RF_K2_THRU (read per step).  For each
+per-level choice -- set between steps by rf_graph_set_forms.  For each
 graph: ms/step of each form over the same toggled 1 % change set, and every
 slot of each form compared after an odd step.
 
@@ -23,8 +23,8 @@ from reflow_amd import capi  # noqa: E402
 from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
 # pl: every level in the latency form; lf: every level in the throughput
-# form; auto: the library's per-level choice (RF_K2_THRU unset)
-FORMS = {"pl": str(1 << 62), "lf": "0", "auto": None}
+# form; auto: the library's per-level choice (the default thresholds)
+FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None}
 
 
 def run(ctx, name, g, slots, old, new, steps):
@@ -36,9 +36,9 @@ def run(ctx, name, g, slots, old, new, steps):
     for rep in range(2):
         for form, thr in FORMS.items():
             if thr is None:
-                os.environ.pop("RF_K2_THRU", None)
+                g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
             else:
-                os.environ["RF_K2_THRU"] = thr
+                g.set_forms(thr)
             state = {"v": 0}
 
             def step():
@@ -64,7 +64,7 @@ def run(ctx, name, g, slots, old, new, steps):
                 ctx.sync()
             print(name, form, "%.4f ms/step" % ms, file=sys.stderr, flush=True)
     res["slots_equal"] = bool(all((snaps["pl"] == snaps[f]).all() for f in snaps))
-    os.environ.pop("RF_K2_THRU", None)
+    g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
     for b in (d_slots, d_old, d_new):
         b.free()
     return res
