@@ -1448,6 +1448,24 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
             }
         for (uint32_t l = 0; l < L; ++l)
             if (qall[l]) gr->g.inc_level[l] = (wide && qj[l] && qb[l] >= wide * qj[l]) ? 2 : 1;
+        // the octo form (k2_level_oct) for levels of few long jobs -- a merge
+        // tree above the fill level: at most kOctMaxLevel queueable jobs, each
+        // without a fusion target, with <= kOctMaxBlocks blocks and <=
+        // kOctMaxHoles holes (its whole material staged in LDS).  RF_K2_OCT=0:
+        // off (A/B)
+        static const bool oct_on = [] {
+            const char* v = getenv("RF_K2_OCT");
+            return !(v && atoi(v) == 0);
+        }();
+        if (oct_on) {
+            std::vector<uint8_t> ok(L, 1);
+            for (uint32_t j = 0; j < J; ++j)  // (every job of the level: rf_graph_restore checks the same)
+                if (fuse[j] >= 0 || nblk[j] > kOctMaxBlocks || d->hole_ptr[j + 1] - d->hole_ptr[j] > kOctMaxHoles)
+                    ok[level[j]] = 0;
+            for (uint32_t l = 0; l < L; ++l)
+                if ((gr->g.inc_level[l] & kLvlForm) == 2 && ok[l] && qall[l] <= kOctMaxLevel)
+                    gr->g.inc_level[l] |= kLvlOct;
+        }
         if (sink_fill != ~0u) {
             gr->g.inc_level[L - 1] |= kLvlSink;
             gr->g.inc_level[sink_fill] |= kLvlFill;
@@ -1651,17 +1669,31 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
             if (sink != ~0u && fill != ~0u && G.sink_attach_ok) {
                 for (uint32_t l = fill + 1; l-- > smin && attach == ~0u;)
                     if ((G.inc_level[l] & kLvlForm) && graph_level_lf(G, l)) attach = l;
+                // no throughput-form level to fill: the last level above the
+                // fill level (a merge tree's root: one job on a nearly idle
+                // chip) rather than the fill level itself, whose latency-form
+                // chains the sinks' workgroups would share CUs with (the
+                // 8-rank piece's OpK level: 67 us, its chains alone ~50);
+                // RF_K2_SINK_LAST=0: the fill level (A/B)
+                static const bool last = [] {
+                    const char* v = getenv("RF_K2_SINK_LAST");
+                    return !(v && atoi(v) == 0);
+                }();
+                if (attach == ~0u && last)
+                    for (uint32_t l = sink; l-- > fill + 1 && attach == ~0u;)
+                        if ((G.inc_level[l] & kLvlForm) && !(G.inc_level[l] & kLvlOct)) attach = l;
                 if (attach == ~0u) attach = fill;
             }
         }
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
-        if (lvl_lo == 0) G.last_levels_lf = 0;
+        if (lvl_lo == 0) G.last_levels_lf = G.last_levels_oct = 0;
         for (uint32_t l = lvl_lo; l < std::min(lvl_hi, G.n_levels); ++l) {
             if (!(G.inc_level[l] & kLvlForm) || (l == sink && attach != ~0u)) continue;
             HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr, l == attach ? sink : ~0u));
             G.last_levels_lf += graph_level_lf(G, l) ? 1u : 0u;
+            G.last_levels_oct += (G.inc_level[l] & kLvlOct) && l != attach ? 1u : 0u;
             first = false;
         }
         gr->last_counts = G.counts;
@@ -1969,6 +2001,7 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
     out->last_recomputed = gr->last_recomputed;
     out->last_levels_lf = gr->g.last_levels_lf;
     out->last_mark_lf = gr->g.last_mark_lf;
+    out->last_levels_oct = gr->g.last_levels_oct;
     if (gr->timed) {
         HIPC(hipEventSynchronize(gr->e1));
         HIPC(hipEventElapsedTime(&out->last_ms, gr->e0, gr->e1));

@@ -72,6 +72,12 @@ hipError_t launch_gen_fill(uint8_t* arena, const uint64_t* offs, const uint64_t*
 // fill the SIMDs a wide level's waves leave idle -- else to the fill level's
 // launch.
 constexpr uint8_t kLvlForm = 3, kLvlSinkMin = 0x20, kLvlFill = 0x40, kLvlSink = 0x80;
+// kLvlOct: a level of few long jobs (form 2, at most kOctMaxLevel jobs, each
+// with no fusion target, <= kOctMaxBlocks blocks and <= kOctMaxHoles holes)
+// runs in the octo form (k2_level_oct): 8 jobs per workgroup, each job's whole
+// material staged in LDS, K1's 8-instruction octo chain
+constexpr uint8_t kLvlOct = 0x10;
+constexpr uint32_t kOctMaxBlocks = 32, kOctMaxHoles = 64, kOctMaxLevel = 4096;
 struct GraphDev {
     uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;
     // jobs in internal (level) order
@@ -128,7 +134,7 @@ struct GraphDev {
     // (k3_mark_slots_lf) from this many changed slots
     uint64_t cfg_thru = 0, cfg_thru_wide = 0, cfg_thru_mark = 0;
     // what the last plain step / mark launch chose (rf_graph_stats)
-    uint32_t last_levels_lf = 0, last_mark_lf = 0;
+    uint32_t last_levels_lf = 0, last_mark_lf = 0, last_levels_oct = 0;
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     unsigned long long* wgst = nullptr;    // diagnostic per-workgroup records [L][2048][4] (RF_K2_WGSTAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the

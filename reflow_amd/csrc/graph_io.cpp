@@ -106,14 +106,16 @@ void hash_chunks(rf_ctx* ctx, const uint8_t* buf, uint64_t n, uint8_t* out) {
 struct Validator {
     const Header& h;
     const std::vector<uint32_t>& lvl;      // level layout (host section, complete before the device ones)
+    const std::vector<uint8_t>& inc;       // per-level flags (host section, ditto)
     std::vector<uint32_t>& out_slot;       // internal job -> out slot (from the records)
+    uint32_t lv = 0;                       // meta cursor: the level of the next record
     std::vector<uint8_t> one_hole;         // internal job has exactly one hole
     std::vector<uint8_t> produced;         // slot is some job's output
     std::vector<uint32_t> cons_ptr;        // host copy: slot -> its reverse-edge range
     uint64_t slot = 0;                     // cons_job cursor: the slot whose range holds the next edge
 
-    Validator(const Header& hh, const std::vector<uint32_t>& l, std::vector<uint32_t>& os)
-        : h(hh), lvl(l), out_slot(os) {}
+    Validator(const Header& hh, const std::vector<uint32_t>& l, const std::vector<uint8_t>& in, std::vector<uint32_t>& os)
+        : h(hh), lvl(l), inc(in), out_slot(os) {}
 
     // a host section, once complete
     int host_done(const char* name, const std::vector<uint32_t>* ext2int) {
@@ -144,6 +146,12 @@ struct Validator {
                     return fail(RF_EINTEGRITY, "graph restore: job record %llu out of range",
                                 (unsigned long long)(o / 32 + r));
                 const uint64_t j = o / 32 + r;
+                // a level run in the octo form stages each job whole in LDS
+                while (lv < h.n_levels && lvl[lv + 1] <= j) ++lv;
+                if (lv < h.n_levels && (inc[lv] & kLvlOct) &&
+                    (m[1] > kOctMaxBlocks || m[3] - m[2] > kOctMaxHoles || m[7] != 0xffffffffu))
+                    return fail(RF_EINTEGRITY, "graph restore: job record %llu exceeds its level's form",
+                                (unsigned long long)j);
                 out_slot[j] = m[4];
                 one_hole[j] = m[3] - m[2] == 1;
                 produced[m[4]] = 1;
@@ -310,7 +318,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     std::vector<uint32_t> ext2int(h.n_jobs);
     std::vector<Section> secs = sections(gr, lvl, inc, ext2int, has_mid);
     std::vector<uint32_t> out_slot(h.n_jobs);  // internal job -> out slot (from the records)
-    Validator val(h, lvl, out_slot);
+    Validator val(h, lvl, inc, out_slot);
     Stage st;
     HostBuf& stage = st.b;
     HIPC(stage.ensure(kStage));

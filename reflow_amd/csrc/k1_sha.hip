@@ -396,22 +396,7 @@ __global__ __launch_bounds__(128) void k1_sha256_duo(SoloArgs a) {
 // feed-forward; the wave runs that group 0 for its longest message after the
 // loop.  Shorter messages of the wave keep hashing rows nobody wrote (their
 // lanes' results are never stored again).
-#define RF_OCT_STEP(x0, x1, x2, x3, z, zn, k) \
-    RF_LAG_STEP_P(x0, x1, x2, x3, z, zn, k, "quad_perm:[1,2,0,1]", "quad_perm:[2,0,1,2]", "row_half_mirror")
-#define RF_OCT_GROUP                                        \
-    RF_OCT_STEP("a", "b", "c", "d", "z", "y", "k1")         \
-    RF_OCT_STEP("d", "a", "b", "c", "y", "z", "k2")         \
-    RF_OCT_STEP("c", "d", "a", "b", "z", "y", "k3")         \
-    RF_OCT_STEP("b", "c", "d", "a", "y", "z", "k4")
-#define RF_OCT_GROUP0                                        \
-    "s_nop 1\n\t" RF_LAG_FF("0x5", "a", "b", "c", "d")       \
-    "v_add_u32 %[z], %[z], %[kw0]\n\t"                       \
-    RF_OCT_STEP("a", "b", "c", "d", "z", "y", "k1")          \
-    RF_OCT_STEP("d", "a", "b", "c", "y", "z", "k2")          \
-    RF_LAG_FF("0xa", "c", "d", "a", "b")                     \
-    RF_OCT_STEP("c", "d", "a", "b", "z", "y", "k3")          \
-    RF_OCT_STEP("b", "c", "d", "a", "y", "z", "k4")          \
-    RF_LAG_CORR_P("row_half_mirror", "0x5", "0xa")
+// RF_OCT_* (the octo chain's step, group, group 0): lag_chain.h
 
 // Producer lane l: block c + (l & 7) of message l >> 3 into its row of buffer kwb.
 __device__ __forceinline__ void fill_oct_row(uint32_t* kwb, const uint8_t* p, uint64_t len, uint64_t nb,

@@ -1941,6 +1941,234 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
     count_fused(a, hashed);
 }
 
+// ---- the octo form: levels of few long jobs (GraphDev kLvlOct) ---------------
+// k2_level_pl keeps 64 jobs per workgroup on two-lane chains (9 VALU a round)
+// fed by a producer that assembles one block a step through a hole pipeline;
+// on a level of a few hundred 18-block, 32-hole merge jobs (the merge tree
+// above the fill level) the chip is nearly idle and that pipeline's chunk
+// transitions set the pace: 1.3-1.7 us a block (the 8-rank piece's merge
+// levels: 33 + 32 + 28 us, profiles/r03/s3/wg_c4r8.log).  Here a workgroup
+// takes 8 jobs.  Every hole's digest is final when the level starts (level-
+// synchronous), so the producer wave stages each job's WHOLE material in LDS
+// first -- template blocks and hole records, then the holes' digests, each
+// batch of loads issued back to back: two dependent HBM round trips for the 8
+// jobs -- and then expands 8 blocks of each job per step (one lane per (job,
+// block), double-buffered rows); the chain wave runs K1's octo chain (8 lanes
+// a job, the duo's 8-instruction round: lag_chain.h RF_OCT_*).  Jobs have no
+// fusion target, at most kOctMaxBlocks blocks and kOctMaxHoles holes
+// (rf_graph_load's kLvlOct analysis); no sink list rides on this launch.
+constexpr uint32_t kOctStage = kOctMaxBlocks * 16 + 4;  // words per job's staged material (16-B aligned)
+
+// OR digest D (8 LE words) into the linear material stage m at byte `pos`
+// (or_digest without the ring wrap).
+__device__ __forceinline__ void or_digest_lin(uint32_t* m, uint32_t pos, const uint32_t (&D)[8]) {
+    const uint32_t x = pos >> 2, sh = 32 - 8 * (pos & 3);
+    uint32_t prev = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const uint32_t cur = k < 8 ? D[k] : 0u;
+        const uint32_t v = (uint32_t)((((uint64_t)cur << 32) | prev) >> sh);
+        if (v) atomicOr(&m[x + k], v);
+        prev = cur;
+    }
+}
+
+__global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
+    // two buffers of 8 blocks x 8 jobs K+W rows (row j * 8 + f), then the
+    // a-lanes' k row (as k1_sha256_octo); the 8 jobs' staged materials
+    __shared__ __attribute__((aligned(16))) uint32_t kw[129 * kPcRow];
+    __shared__ __attribute__((aligned(16))) uint32_t mat[8 * kOctStage];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t f = lane >> 3;  // the lane's job of the group (both waves)
+    uint32_t* const ones = &kw[128 * kPcRow];
+    if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        ones[lane] = lane ? 1u : 0u;
+        if (lane < kPcRow - 64) ones[64 + lane] = 1u;
+    }
+    const bool elane = (lane & 4) == 0;
+    const uint32_t q3 = lane & 3;
+    const uint32_t shq = elane ? (q3 == 1 ? 11u : q3 == 2 ? 25u : 6u) : (q3 == 1 ? 13u : q3 == 2 ? 22u : 2u);
+    const uint32_t M = elane ? 0u : ~0u;
+    const uint32_t one = 1u, zero = 0u;
+    constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    zero_other_counts(a);
+    WgStamp ws;
+    ws.begin(a);
+    const uint32_t n = a.counts[a.lvl];
+    const uint4* T4 = reinterpret_cast<const uint4*>(a.tmpl);
+    for (uint32_t base = blockIdx.x * 8; base < n; base += gridDim.x * 8) {
+        if (threadIdx.x == 0) ws.jobs += min(8u, n - base);
+        const uint32_t i = base + f;
+        const bool has = i < n;
+        uint32_t p = 0;
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        if (has) {
+            const uint32_t ii = a.s + (a.rev ? n - 1 - i : i);
+            p = a.list[ii];
+            m0 = a.lmeta[2ull * ii];
+            m1 = a.lmeta[2ull * ii + 1];
+        }
+        const uint32_t nb = min(m0.y, kOctMaxBlocks);  // (0 without a job; the clamp only guards the stage)
+        uint32_t maxnb = nb;
+        for (int o = 8; o < 64; o <<= 1) maxnb = max(maxnb, (uint32_t)__shfl_xor((int)maxnb, o, 64));
+        maxnb = __builtin_amdgcn_readfirstlane(maxnb);
+        // (producer) K+W rows of blocks 8c .. 8c+7 of each job into buffer c & 1
+        auto expand = [&](uint32_t c) {
+            const uint32_t j = lane & 7, b = 8 * c + j;
+            if (b < nb) {
+                const uint4* src = reinterpret_cast<const uint4*>(&mat[f * kOctStage + 16 * b]);
+                uint32_t w[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint4 v = src[q];
+                    w[4 * q] = bswap32(v.x); w[4 * q + 1] = bswap32(v.y);
+                    w[4 * q + 2] = bswap32(v.z); w[4 * q + 3] = bswap32(v.w);
+                }
+                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((c & 1) * 64 + j * 8 + f) * kPcRow]));
+            }
+        };
+        // (chain) the job's start state and old digest, fetched now, used at the end
+        uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
+        uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
+        if (wave == 0) {
+            if (has && a.mid) {
+                hlo = a.mid[2ull * p];
+                hhi = a.mid[2ull * p + 1];
+            }
+            if (has) {
+                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+                olo = od[0];
+                ohi = od[1];
+            }
+        } else {
+            // 1. the 8 jobs' templates and hole records (one lane per hole)
+            uint4 tv[8][2];
+            uint2 hr[8];
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t tb = __builtin_amdgcn_readlane(m0.x, 8 * g);
+                const uint32_t bg = min(__builtin_amdgcn_readlane(m0.y, 8 * g), kOctMaxBlocks);
+                const uint32_t hb = __builtin_amdgcn_readlane(m0.z, 8 * g);
+                const uint32_t he = __builtin_amdgcn_readlane(m0.w, 8 * g);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const uint32_t q = lane + 64 * k;
+                    tv[g][k] = q < 4 * bg ? T4[4ull * tb + q] : make_uint4(0, 0, 0, 0);
+                }
+                hr[g] = hb + lane < he ? a.holes[hb + lane] : make_uint2(~0u, 0u);
+            }
+            // 2. the holes' digests
+            uint4 dlo[8], dhi[8];
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * (hr[g].x != ~0u ? hr[g].y : 0u));
+                dlo[g] = src[0];
+                dhi[g] = src[1];
+            }
+            // 3. templates into the stage, then each digest OR-ed into its zero hole
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t bg = min(__builtin_amdgcn_readlane(m0.y, 8 * g), kOctMaxBlocks);
+                uint4* st = reinterpret_cast<uint4*>(&mat[g * kOctStage]);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const uint32_t q = lane + 64 * k;
+                    if (q < 4 * bg) st[q] = tv[g][k];
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                if (hr[g].x <= kOctMaxBlocks * 64 - 32) {
+                    const uint32_t D[8] = {dlo[g].x, dlo[g].y, dlo[g].z, dlo[g].w, dhi[g].x, dhi[g].y, dhi[g].z, dhi[g].w};
+                    or_digest_lin(&mat[g * kOctStage], hr[g].x, D);
+                }
+            }
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            expand(0);
+        }
+        __syncthreads();  // chunk 0's rows
+        uint32_t Hr0 = elane ? hhi.x : hlo.x, Hr1 = elane ? hhi.y : hlo.y;
+        uint32_t Hr2 = elane ? hhi.z : hlo.z, Hr3 = elane ? hhi.w : hlo.w;
+        uint32_t Pa = 0, Pb = 0, Pc = 0, Pd = 0;
+        uint32_t Z = elane ? hhi.w + hlo.w : 0u, Y = 0;
+        uint32_t c63 = 0, c64 = elane ? hlo.z : 0u - hhi.x, c65 = elane ? hlo.y : 0u - hlo.w;
+        uint32_t t0, t1, t3;
+        uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+        uint4 v = make_uint4(0, 0, 0, 0), vn = v;
+        for (uint32_t c = 0; 8 * c < maxnb; ++c) {
+            if (wave == 1) {
+                if (8 * (c + 1) < maxnb) expand(c + 1);
+            } else {
+                const uint32_t cnt = min(8u, maxnb - 8 * c);
+                // e-lanes read their job's rows, a-lanes the ones row
+                const uint32_t ones_off = 128 * kPcRow * 4, buf_off = ((c & 1) * 64 + f) * kPcRow * 4;
+                const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
+                                                                 ((M & ones_off) | (~M & buf_off)));
+                v = r4[0];
+                vn = r4[1];
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    const uint32_t nrow_off = buf_off + (j + 1 < cnt ? j + 1 : j) * 8 * kPcRow * 4;
+                    const uint4* r4n = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
+                                                                      ((M & ones_off) | (~M & nrow_off)));
+                    uint4 vnn = r4[2];
+                    {
+                        const uint32_t k1 = v.y + c64, k2 = v.z + c65;
+                        asm volatile(RF_OCT_GROUP0
+                                     : RF_LAG_STATE, RF_LAG_TMP, RF_LAG_H, [c63] "=&v"(c63), [c64] "+v"(c64),
+                                       [c65] "+v"(c65)
+                                     : RF_LAG_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one), [zero] "v"(zero));
+                    }
+                    if (8 * c + j == nb) {  // the job's final chaining value
+                        D0 = Hr0; D1 = Hr1; D2 = Hr2; D3 = Hr3;
+                    }
+                    v = vn;
+                    vn = vnn;
+#pragma unroll
+                    for (int g = 1; g < 16; ++g) {
+                        vnn = g < 14 ? r4[g + 2] : r4n[g - 14];
+                        const uint32_t k4 = g == 15 ? c63 : vn.x;
+                        asm volatile(RF_OCT_GROUP : RF_LAG_STATE, RF_LAG_TMP : RF_LAG_IN(v.y, v.z, v.w, k4));
+                        v = vn;
+                        vn = vnn;
+                    }
+                    r4 = r4n;
+                }
+            }
+            __syncthreads();
+        }
+        if (wave == 0) {
+            {  // group 0 of block maxnb: the longest jobs' final value
+                const uint32_t k1 = v.y + c64, k2 = v.z + c65;
+                asm volatile(RF_OCT_GROUP0
+                             : RF_LAG_STATE, RF_LAG_TMP, RF_LAG_H, [c63] "=&v"(c63), [c64] "+v"(c64), [c65] "+v"(c65)
+                             : RF_LAG_IN(k1, k2, v.w, vn.x), [kw0] "v"(v.x), [one] "v"(one), [zero] "v"(zero));
+            }
+            if (nb == maxnb) {
+                D0 = Hr0; D1 = Hr1; D2 = Hr2; D3 = Hr3;
+            }
+            // lane 8f (e) holds H4..H7, lane 8f + 4 (a) H0..H3
+            ShaState st;
+            st.h[0] = (uint32_t)__shfl((int)D0, (int)lane + 4, 64);
+            st.h[1] = (uint32_t)__shfl((int)D1, (int)lane + 4, 64);
+            st.h[2] = (uint32_t)__shfl((int)D2, (int)lane + 4, 64);
+            st.h[3] = (uint32_t)__shfl((int)D3, (int)lane + 4, 64);
+            st.h[4] = D0; st.h[5] = D1; st.h[6] = D2; st.h[7] = D3;
+            const bool own = has && (lane & 7) == 0;
+            bool changed = false;
+            if (own) {
+                changed = finish_job_pre(a, m1, st, olo, ohi);
+                a.dirty[p] = 0u;
+            }
+            // no fusion target (kLvlOct): every consumer of a changed digest is queued
+            propagate(a, own && changed ? m1.y : 0u, own && changed ? m1.z : 0u);
+        }
+    }
+    ws.end(a);
+}
+
 // ---- partitioned DAG exchange (partition.cpp) --------------------------------
 // Exports whose digest changed since last sent: their bit (bit0 + i) in the
 // boundary bitset, the snapshot updated, the digest into the send block.
@@ -2177,6 +2405,12 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_CHAIN");
             return v && atoi(v) == 14;
         }();
+        // a level of few long jobs (kLvlOct): the octo form, 8 jobs a workgroup
+        if ((g.inc_level[lvl] & kLvlOct) && sink_lvl == ~0u && !one_lane) {
+            const uint32_t og = std::min<uint32_t>((e - b + 7) / 8, 1024u);
+            hipLaunchKernelGGL(k2_level_oct, dim3(og), dim3(128), 0, s, a);
+            return hipGetLastError();
+        }
         const bool wide = (g.inc_level[lvl] & kLvlForm) == 2;
         // g.stream_handover (RF_K2_STREAM=1 at load): the streamed hand-over
         // (measured no faster on configs[2]: the producer serializes a fused

@@ -106,3 +106,25 @@ constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
 #define RF_L2_TMP [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
 #define RF_L2_IN(k1v, k2v, k3v, k4v) \
     [s1] "v"(sh1), [s2] "v"(sh2), [s3] "v"(sh3), [m] "v"(M), [k1] "v"(k1v), [k2] "v"(k2v), [k3] "v"(k3v), [k4] "v"(k4v)
+
+// The octo layout (k1_sha256_octo, k2_level_oct): eight jobs per wave, lanes
+// 8f..8f+3 the e-half of job f, 8f+4..8f+7 its a-half; every lane of a quad
+// ends a round with the full sigma (positions 0..2 rotate by the half's three
+// amounts, position 3 repeats position 0's), the partner's X0 from the
+// mirrored lane of the half-row, the halves' feed-forwards by banks 0x5 / 0xa.
+#define RF_OCT_STEP(x0, x1, x2, x3, z, zn, k) \
+    RF_LAG_STEP_P(x0, x1, x2, x3, z, zn, k, "quad_perm:[1,2,0,1]", "quad_perm:[2,0,1,2]", "row_half_mirror")
+#define RF_OCT_GROUP                                        \
+    RF_OCT_STEP("a", "b", "c", "d", "z", "y", "k1")         \
+    RF_OCT_STEP("d", "a", "b", "c", "y", "z", "k2")         \
+    RF_OCT_STEP("c", "d", "a", "b", "z", "y", "k3")         \
+    RF_OCT_STEP("b", "c", "d", "a", "y", "z", "k4")
+#define RF_OCT_GROUP0                                        \
+    "s_nop 1\n\t" RF_LAG_FF("0x5", "a", "b", "c", "d")       \
+    "v_add_u32 %[z], %[z], %[kw0]\n\t"                       \
+    RF_OCT_STEP("a", "b", "c", "d", "z", "y", "k1")          \
+    RF_OCT_STEP("d", "a", "b", "c", "y", "z", "k2")          \
+    RF_LAG_FF("0xa", "c", "d", "a", "b")                     \
+    RF_OCT_STEP("c", "d", "a", "b", "z", "y", "k3")          \
+    RF_OCT_STEP("b", "c", "d", "a", "y", "z", "k4")          \
+    RF_LAG_CORR_P("row_half_mirror", "0x5", "0xa")
