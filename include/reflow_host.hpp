@@ -25,6 +25,7 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <memory>
 #include <optional>
 #include <string>
 #include <unordered_map>
@@ -247,9 +248,16 @@ class FlowArena {
         nodes_.push_back(std::move(f));
         return &nodes_.back();
     }
+    // n default-constructed nodes, contiguous (Canonicalize's copies: an
+    // Eval then maps a copy to its slot by address, no hash lookup)
+    Flow* NewN(size_t n) {
+        blocks_.emplace_back(new Flow[n ? n : 1]);
+        return blocks_.back().get();
+    }
 
    private:
     std::deque<Flow> nodes_;
+    std::vector<std::unique_ptr<Flow[]>> blocks_;
 };
 
 // test/flow/constructor.go:17-74
@@ -277,11 +285,17 @@ Flow* Val(FlowArena& a, const Fileset& v);
 Flow* Data(FlowArena& a, const std::string& b);
 }  // namespace flow
 
+class Eval;
 // Canonicalize (flow.go:814-843): copies merged with `config`, semantically
 // equal nodes (equal digests) collapsed to the first one in visit order.
-// Digests come from the device (two graph evaluations).
+// The copies' digests come from the device: an Eval (file slots on) over the
+// copies, lowered, loaded and fully recomputed.  `lowered` (optional): when
+// no two copies share a digest, the canonical graph IS the copies' graph and
+// that Eval is handed over ready for FlowDigest / CacheKeys / SetFileID +
+// Recompute -- the caller's Eval.Add + Build of the same graph (what a fresh
+// Eval does after Canonicalize, eval.go:240-272) is skipped; null otherwise.
 Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config,
-                   const std::string& universe = "");
+                   const std::string& universe = "", std::unique_ptr<Eval>* lowered = nullptr);
 
 // Batched Flow.Digest / PhysicalDigest / CacheKeys over a whole DAG: the DAG
 // is lowered to rf_graph jobs (one logical job per node, one physical job per
@@ -303,19 +317,26 @@ class Eval {
     size_t Jobs() const { return out_slot_.size(); }
 
    private:
+    friend Flow* Canonicalize(Engine&, FlowArena&, Flow*, Config, const std::string&, std::unique_ptr<Eval>*);
     using Holes = std::vector<std::pair<uint32_t, uint32_t>>;  // (byte pos, slot)
-    // a job's material is built in the scratch of its recursion depth (a
-    // dep's job is lowered while its consumer's material is being written),
-    // then appended to the graph's arrays: no allocation per job
-    struct Scratch {
-        std::string t;
-        Holes h;
+    // File IDs referenced from a job's material (file slots): (its hole's
+    // index in the job, the ID) -- slots are given after the parallel phase
+    using FileRefs = std::vector<std::pair<uint32_t, Digest>>;
+    struct Part;  // one range of nodes' jobs, built by one thread (reflow_host.cpp)
+    // a contiguous run of nodes (FlowArena::NewN) whose logical slots are
+    // slot0 + index: found by address, never hashed
+    struct Block {
+        const Flow* base;
+        size_t n;
+        uint32_t slot0;
+        std::vector<uint32_t> phys;  // physical slot per node, ~0u: none
     };
-    void material(const Flow* f, std::string& out, Holes& holes);
-    void fileset_material(const Fileset& v, std::string& out, Holes& holes);
-    uint32_t lower(const Flow* f);
-    void lower_physical(const Flow* f);
-    void commit(const Scratch& sc, uint32_t out);
+    void material(const Flow* f, std::string& out, Holes& holes, FileRefs& files) const;
+    void fileset_material(const Fileset& v, std::string& out, Holes& holes, FileRefs& files) const;
+    void lower_nodes(const std::vector<const Flow*>* nodes, const Block* blk, const std::vector<uint32_t>& phys);
+    void add_block(const Flow* base, size_t n);
+    const uint32_t* slot_of(const Flow* f) const;
+    const uint32_t* phys_slot_of(const Flow* f) const;
     uint32_t new_slot() { return n_slots_++; }
 
     Engine& e_;
@@ -326,8 +347,7 @@ class Eval {
     std::vector<uint32_t> out_slot_, tmpl_len_, hole_pos_, hole_slot_;
     std::vector<uint64_t> tmpl_off_, hole_ptr_{0};
     std::string blob_;
-    std::deque<Scratch> scratch_;  // deque: growing it keeps the outer depths' references valid
-    uint32_t depth_ = 0;
+    std::vector<Block> blocks_;
     detail::FlatMap<const Flow*, uint32_t, detail::PtrHash> logical_, physical_;
     detail::FlatMap<Digest, uint32_t, DigestHash> file_slot_;
     rf_graph* g_ = nullptr;

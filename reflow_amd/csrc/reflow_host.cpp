@@ -6,6 +6,10 @@
 #include "reflow_host.hpp"
 
 #include <algorithm>
+#include <exception>
+#include <thread>
+#include <mutex>
+#include <atomic>
 #include <functional>
 #include <memory>
 #include <unordered_set>
@@ -298,6 +302,61 @@ static void exec_suffix(const Flow* f, std::string& w) {
         for (const ExecArg& a : *f->Argmap) writeN(w, a.Out ? -(int64_t)a.Index : a.Index);
 }
 
+// op names without a string allocation per node (DigestString's table)
+static void append_op_name(std::string& w, Op op) {
+    static const char* names[] = {"OpExec", "OpIntern", "OpExtern", "OpGroupby", "OpMap",
+                                  "OpCollect", "OpMerge", "OpVal", "OpPullup", "OpK",
+                                  "OpCoerce", "OpRequirements", "maxOp"};
+    const int i = (int)op - 1;
+    if (i < 0 || i >= 13)
+        w += DigestString(op);
+    else
+        w += names[i];
+}
+
+// Host threads for the lowering: the engine's host-leg width (the process's
+// CPU share, min(60, share) / ranks per node), at least 1; RF_LOWER_THREADS
+// overrides.
+static unsigned lower_threads(Engine& e) {
+    if (const char* v = getenv("RF_LOWER_THREADS")) return std::max(1, atoi(v));
+    int th = 0, ext = 0;
+    double rate = 0;
+    if (rf_host_info(e.ctx(), &th, &rate, &ext) != RF_OK || th < 1) {
+        const unsigned h = std::thread::hardware_concurrency();
+        th = (int)std::min(h ? h : 1u, 16u);
+    }
+    return (unsigned)th;
+}
+
+// Ranges [lo, hi) of n items of `grain` each, claimed by `threads` threads;
+// fn(range index, lo, hi).  The first exception a worker throws is rethrown.
+template <class F>
+static void parallel_ranges(size_t n, size_t grain, unsigned threads, F fn) {
+    const size_t nr = (n + grain - 1) / grain;
+    if (nr <= 1 || threads <= 1) {
+        for (size_t r = 0; r < nr; ++r) fn(r, r * grain, std::min(n, (r + 1) * grain));
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::exception_ptr err;
+    std::mutex mu;
+    auto work = [&]() {
+        try {
+            for (size_t r; (r = next.fetch_add(1)) < nr;) fn(r, r * grain, std::min(n, (r + 1) * grain));
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+            next.store(nr);
+        }
+    };
+    std::vector<std::thread> th;
+    const unsigned t = (unsigned)std::min<size_t>(threads, nr);
+    for (unsigned i = 1; i < t; ++i) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    if (err) std::rethrow_exception(err);
+}
+
 Eval::Eval(Engine& e, std::string universe, bool file_slots)
     : e_(e), U_(std::move(universe)), file_slots_(file_slots) {}
 
@@ -305,24 +364,40 @@ Eval::~Eval() {
     if (g_) rf_graph_destroy(g_);
 }
 
-void Eval::fileset_material(const Fileset& v, std::string& out, Holes& holes) {
+const uint32_t* Eval::slot_of(const Flow* f) const {
+    for (const Block& b : blocks_)
+        if (f >= b.base && f < b.base + b.n) {
+            // (a static per thread: the slot is returned by pointer like the map's)
+            thread_local uint32_t s;
+            s = b.slot0 + (uint32_t)(f - b.base);
+            return &s;
+        }
+    return logical_.find(f);
+}
+
+const uint32_t* Eval::phys_slot_of(const Flow* f) const {
+    for (const Block& b : blocks_)
+        if (f >= b.base && f < b.base + b.n) {
+            const uint32_t* s = &b.phys[f - b.base];
+            return *s == ~0u ? nullptr : s;
+        }
+    return physical_.find(f);
+}
+
+// With file slots, a File ID becomes a hole whose slot is given after the
+// parallel phase (one slot per distinct ID); else WD(ID) inline.
+void Eval::fileset_material(const Fileset& v, std::string& out, Holes& holes, FileRefs& files) const {
     if (v.List) {
-        for (const Fileset& c : *v.List) fileset_material(c, out, holes);
+        for (const Fileset& c : *v.List) fileset_material(c, out, holes, files);
         return;
     }
     for (const auto& [path, file] : v.Map) {
         out += path;
         if (file_slots_) {
-            uint32_t s;
-            if (const uint32_t* p = file_slot_.find(file.ID)) {
-                s = *p;
-            } else {
-                s = new_slot();
-                file_slot_.insert(file.ID, s);
-            }
             out.push_back('\0');
             out.push_back('\5');
-            holes.emplace_back((uint32_t)out.size(), s);
+            files.emplace_back((uint32_t)holes.size(), file.ID);
+            holes.emplace_back((uint32_t)out.size(), 0u);
             out.append(32, '\0');
         } else {
             WriteDigest(out, file.ID);
@@ -334,40 +409,42 @@ void Eval::fileset_material(const Fileset& v, std::string& out, Holes& holes) {
 // node's own Config.HashV1 decides whether its deps are inlined (flow.go:
 // 692-697); an inlined dep follows its own config in turn, and so does a
 // Parent (Canonicalize merges the config into the copies it makes, never
-// into f.Parent: flow.go:818-843).
-void Eval::material(const Flow* f, std::string& out, Holes& holes) {
+// into f.Parent: flow.go:818-843).  Every dep already has its slot (the
+// nodes are numbered before any material is built), so this only reads.
+void Eval::material(const Flow* f, std::string& out, Holes& holes, FileRefs& files) const {
     out += U_;
     if (f->op == OpRequirements) {
-        material(f->Deps.at(0), out, holes);
+        material(f->Deps.at(0), out, holes, files);
         return;
     }
     if (f->Parent) {
-        material(f->Parent, out, holes);
+        material(f->Parent, out, holes, files);
         return;
     }
     for (const Flow* d : f->Deps) {
         if (f->config.HashV1) {
-            material(d, out, holes);
+            material(d, out, holes, files);
         } else {
-            const uint32_t s = lower(d);
+            const uint32_t* s = slot_of(d);
+            if (!s) throw Error(RF_EINVAL, "dependency not numbered (a Flow reachable only after Add)");
             out.push_back('\0');
             out.push_back('\5');
-            holes.emplace_back((uint32_t)out.size(), s);
+            holes.emplace_back((uint32_t)out.size(), *s);
             out.append(32, '\0');
         }
     }
-    out += DigestString(f->op);
+    append_op_name(out, f->op);
     switch (f->op) {
     case OpIntern:
     case OpExtern: out += f->URL; break;
     case OpExec: exec_suffix(f, out); break;
     case OpGroupby: out += f->Re; break;
-    case OpMap: material(f->MapFlow, out, holes); break;
+    case OpMap: material(f->MapFlow, out, holes, files); break;
     case OpCollect: out += f->Re; out += f->Repl; break;
     case OpVal:
         if (f->Err) throw Error(RF_EINVAL, "error OpVal digests are random (flow.go:722-731)");
         if (f->Value) {
-            fileset_material(*f->Value, out, holes);
+            fileset_material(*f->Value, out, holes, files);
         } else {
             if (f->FlowDigest.IsZero()) throw Error(RF_EINVAL, "invalid flow digest");
             WriteDigest(out, f->FlowDigest);
@@ -383,76 +460,147 @@ void Eval::material(const Flow* f, std::string& out, Holes& holes) {
     }
 }
 
-void Eval::commit(const Scratch& sc, uint32_t out) {
-    out_slot_.push_back(out);
-    tmpl_off_.push_back(blob_.size());
-    tmpl_len_.push_back((uint32_t)sc.t.size());
-    blob_ += sc.t;
-    for (const auto& [pos, slot] : sc.h) {
-        hole_pos_.push_back(pos);
-        hole_slot_.push_back(slot);
-    }
-    hole_ptr_.push_back(hole_pos_.size());
-}
-
-uint32_t Eval::lower(const Flow* f) {
-    if (const uint32_t* s = logical_.find(f)) return *s;
-    if (scratch_.size() <= depth_) scratch_.resize(depth_ + 1);
-    Scratch& sc = scratch_[depth_];
-    sc.t.clear();
-    sc.h.clear();
-    ++depth_;
-    try {
-        material(f, sc.t, sc.h);
-    } catch (...) {
-        --depth_;
-        throw;
-    }
-    --depth_;
-    // (a dep lowered inside material() may have grown scratch_: re-index)
-    const uint32_t out = new_slot();
-    logical_.insert(f, out);
-    commit(scratch_[depth_], out);
-    return out;
-}
-
-// Flow.PhysicalDigest (flow.go:764-792): no Universe, no op name, no WD.
-void Eval::lower_physical(const Flow* f) {
-    if (f->op != OpExec && f->op != OpExtern) return;
-    if (physical_.find(f)) return;
+// Flow.PhysicalDigest (flow.go:764-792) exists for OpExec / OpExtern whose
+// deps are all FlowDone: no Universe, no op name, no WD.
+static bool has_physical(const Flow* f) {
+    if (f->op != OpExec && f->op != OpExtern) return false;
     for (const Flow* d : f->Deps)
-        if (!d->Done) return;
-    if (scratch_.size() <= depth_) scratch_.resize(depth_ + 1);
-    Scratch& sc = scratch_[depth_];
-    sc.t.clear();
-    sc.h.clear();
-    for (const Flow* d : f->Deps) {
-        if (!d->Value) throw Error(RF_EINVAL, "done dependency without a Fileset value");
-        fileset_material(*d->Value, sc.t, sc.h);
-    }
-    if (f->op == OpExtern)
-        sc.t += f->URL;
-    else
-        exec_suffix(f, sc.t);
-    const uint32_t out = new_slot();
-    physical_.insert(f, out);
-    commit(sc, out);
+        if (!d->Done) return false;
+    return true;
 }
 
+struct Eval::Part {
+    std::string blob;
+    std::vector<uint32_t> out_slot, tmpl_len, hole_pos, hole_slot;
+    std::vector<uint64_t> tmpl_off, hole_end;     // per job: local template offset, local hole end
+    std::vector<std::pair<uint64_t, Digest>> files;  // (local hole index, File ID)
+};
+
+// The logical (and physical) jobs of nodes -- `nodes`, or every node of
+// `blk` -- whose slots are all given: materials built on host threads, one
+// part per range of nodes, then the File IDs' slots (in part order, so the
+// numbering is deterministic) and the parts appended in order.
+void Eval::lower_nodes(const std::vector<const Flow*>* nodes, const Block* blk, const std::vector<uint32_t>& phys) {
+    const size_t n = nodes ? nodes->size() : blk->n;
+    constexpr size_t kGrain = 8192;
+    std::vector<Part> parts((n + kGrain - 1) / kGrain);
+    parallel_ranges(n, kGrain, lower_threads(e_), [&](size_t r, size_t lo, size_t hi) {
+        Part& P = parts[r];
+        std::string t;
+        Holes h;
+        FileRefs files;
+        auto commit = [&](uint32_t out) {
+            P.out_slot.push_back(out);
+            P.tmpl_off.push_back(P.blob.size());
+            P.tmpl_len.push_back((uint32_t)t.size());
+            P.blob += t;
+            for (const auto& [hi_, d] : files) P.files.emplace_back(P.hole_pos.size() + hi_, d);
+            for (const auto& [pos, slot] : h) {
+                P.hole_pos.push_back(pos);
+                P.hole_slot.push_back(slot);
+            }
+            P.hole_end.push_back(P.hole_pos.size());
+        };
+        for (size_t i = lo; i < hi; ++i) {
+            const Flow* f = nodes ? (*nodes)[i] : blk->base + i;
+            t.clear();
+            h.clear();
+            files.clear();
+            material(f, t, h, files);
+            commit(nodes ? *slot_of(f) : blk->slot0 + (uint32_t)i);
+            if (phys[i] != ~0u) {
+                t.clear();
+                h.clear();
+                files.clear();
+                for (const Flow* d : f->Deps) {
+                    if (!d->Value) throw Error(RF_EINVAL, "done dependency without a Fileset value");
+                    fileset_material(*d->Value, t, h, files);
+                }
+                if (f->op == OpExtern)
+                    t += f->URL;
+                else
+                    exec_suffix(f, t);
+                commit(phys[i]);
+            }
+        }
+    });
+    size_t jobs = 0, holes = 0, bytes = 0;
+    for (const Part& P : parts) {
+        jobs += P.out_slot.size();
+        holes += P.hole_pos.size();
+        bytes += P.blob.size();
+    }
+    out_slot_.reserve(out_slot_.size() + jobs);
+    tmpl_off_.reserve(tmpl_off_.size() + jobs);
+    tmpl_len_.reserve(tmpl_len_.size() + jobs);
+    hole_ptr_.reserve(hole_ptr_.size() + jobs);
+    hole_pos_.reserve(hole_pos_.size() + holes);
+    hole_slot_.reserve(hole_slot_.size() + holes);
+    blob_.reserve(blob_.size() + bytes);
+    for (Part& P : parts) {
+        for (const auto& [hi_, id] : P.files) {  // one slot per distinct File ID
+            uint32_t s;
+            if (const uint32_t* q = file_slot_.find(id)) {
+                s = *q;
+            } else {
+                s = new_slot();
+                file_slot_.insert(id, s);
+            }
+            P.hole_slot[hi_] = s;
+        }
+        const uint64_t b0 = blob_.size(), h0 = hole_pos_.size();
+        blob_ += P.blob;
+        out_slot_.insert(out_slot_.end(), P.out_slot.begin(), P.out_slot.end());
+        tmpl_len_.insert(tmpl_len_.end(), P.tmpl_len.begin(), P.tmpl_len.end());
+        for (uint64_t o : P.tmpl_off) tmpl_off_.push_back(b0 + o);
+        for (uint64_t e : P.hole_end) hole_ptr_.push_back(h0 + e);
+        hole_pos_.insert(hole_pos_.end(), P.hole_pos.begin(), P.hole_pos.end());
+        hole_slot_.insert(hole_slot_.end(), P.hole_slot.begin(), P.hole_slot.end());
+        Part().blob.swap(P.blob);  // release as we go
+    }
+}
+
+// Every node reachable through Deps, MapFlow and Parent that this Eval has
+// not lowered yet: numbered first (logical slot, physical slot), then lowered
+// on host threads (lower_nodes).
 void Eval::Add(Flow* root) {
+    std::vector<const Flow*> todo;
     std::vector<const Flow*> stack{root};
-    detail::FlatMap<const Flow*, char, detail::PtrHash> seen;
     while (!stack.empty()) {
         const Flow* f = stack.back();
         stack.pop_back();
-        if (!f || seen.find(f)) continue;
-        seen.insert(f, 1);
-        lower(f);
-        lower_physical(f);
+        if (!f || slot_of(f)) continue;
+        logical_.insert(f, new_slot());
+        todo.push_back(f);
         for (const Flow* d : f->Deps) stack.push_back(d);
         if (f->MapFlow) stack.push_back(f->MapFlow);
         if (f->Parent) stack.push_back(f->Parent);
     }
+    std::vector<uint32_t> phys(todo.size(), ~0u);
+    for (size_t i = 0; i < todo.size(); ++i)
+        if (has_physical(todo[i]) && !physical_.find(todo[i])) {
+            phys[i] = new_slot();
+            physical_.insert(todo[i], phys[i]);
+        }
+    lower_nodes(&todo, nullptr, phys);
+}
+
+// A contiguous run of nodes whose deps and map flows lie in the run (or were
+// added before): slots by address.  Nodes reachable only through a Parent
+// outside the run take the general path afterwards.
+void Eval::add_block(const Flow* base, size_t n) {
+    Block b{base, n, n_slots_, std::vector<uint32_t>(n, ~0u)};
+    n_slots_ += (uint32_t)n;
+    for (size_t i = 0; i < n; ++i)
+        if (has_physical(base + i)) b.phys[i] = new_slot();
+    blocks_.push_back(std::move(b));
+    const Block& blk = blocks_.back();
+    std::vector<const Flow*> parents;
+    for (size_t i = 0; i < n; ++i)
+        if (base[i].Parent && !slot_of(base[i].Parent)) parents.push_back(base[i].Parent);
+    // the run's own deps must be numbered before its materials are built
+    for (const Flow* p : parents) Add(const_cast<Flow*>(p));
+    lower_nodes(nullptr, &blk, blk.phys);
 }
 
 void Eval::Build() {
@@ -502,7 +650,7 @@ void Eval::fetch() const {
 
 Digest Eval::FlowDigest(const Flow* f) const {
     fetch();
-    const uint32_t* s = logical_.find(f);
+    const uint32_t* s = slot_of(f);
     if (!s) throw Error(RF_ENOTFOUND, "flow not in this Eval");
     Digest d;
     memcpy(d.b.data(), cache_.data() + 32ull * *s, 32);
@@ -510,7 +658,7 @@ Digest Eval::FlowDigest(const Flow* f) const {
 }
 
 std::optional<Digest> Eval::PhysicalDigest(const Flow* f) const {
-    const uint32_t* s = physical_.find(f);
+    const uint32_t* s = phys_slot_of(f);
     if (!s) return std::nullopt;
     fetch();
     Digest d;
@@ -539,12 +687,14 @@ void Eval::SetFileID(const Digest& old_id, const Digest& new_id) {
 }
 
 // ---- Canonicalize ------------------------------------------------------------
-Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const std::string& U) {
-    // 1. one copy per original node, config merged, deps (and MapFlow) pointing
-    //    at copies -- the f.Copy()/Config.Merge/recursion of flow.go:820-839.
-    //    Iterative post-order (a node is copied when its deps are).
-    detail::FlatMap<const Flow*, Flow*, detail::PtrHash> copy;
-    std::vector<Flow*> post;  // copies in post-order (the order of m.Put)
+Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const std::string& U,
+                   std::unique_ptr<Eval>* lowered) {
+    if (lowered) lowered->reset();
+    // 1. the originals reachable through Deps and MapFlow in post-order (deps,
+    //    then the map flow, then the node: the order of flowMap.Put,
+    //    flow.go:820-839); each one's index in it.
+    detail::FlatMap<const Flow*, uint32_t, detail::PtrHash> index;
+    std::vector<Flow*> post;
     struct Frame {
         Flow* f;
         size_t next;  // next dep (then MapFlow) to visit
@@ -557,45 +707,52 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
         if (fr.next < nd) {
             Flow* d = fr.next < f->Deps.size() ? f->Deps[fr.next] : f->MapFlow;
             ++fr.next;
-            if (!copy.find(d)) st.push_back(Frame{d, 0});
+            if (!index.find(d)) st.push_back(Frame{d, 0});
             continue;
         }
         st.pop_back();
-        if (copy.find(f)) continue;  // reached twice before its first copy completed
-        Flow c = *f;
-        c.config.Merge(config);
-        Flow* cp = arena.New(std::move(c));
-        for (Flow*& d : cp->Deps) d = *copy.find(d);
-        if (cp->MapFlow) cp->MapFlow = *copy.find(cp->MapFlow);
-        copy.insert(f, cp);
-        post.push_back(cp);
+        if (index.find(f)) continue;  // reached twice before its first visit completed
+        index.insert(f, (uint32_t)post.size());
+        post.push_back(f);
     }
-    Flow* croot = *copy.find(root);
-    // 2. digests of every copy on the device
-    Eval ev(e, U);
-    ev.Add(croot);
-    ev.Build();
-    // 3. flowMap.Put: first copy with a digest wins (K5 on the device: the
-    //    smallest post-order index of each digest class); deps re-pointed at
-    //    it (equal digests by construction, so digests do not change)
-    std::vector<uint8_t> digs(32 * post.size());
-    for (size_t i = 0; i < post.size(); ++i) {
-        const Digest d = ev.FlowDigest(post[i]);
-        memcpy(&digs[32 * i], d.b.data(), 32);
-    }
-    std::vector<uint32_t> first(post.size());
+    const size_t n = post.size();
+    // 2. one copy per original, contiguous in post-order (f.Copy() +
+    //    Config.Merge, deps and map flow pointing at copies), on host threads
+    Flow* cp = arena.NewN(n);
+    parallel_ranges(n, 16384, lower_threads(e), [&](size_t, size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            Flow& c = cp[i];
+            c = *post[i];
+            c.config.Merge(config);
+            for (Flow*& d : c.Deps) d = cp + *index.find(d);
+            if (c.MapFlow) c.MapFlow = cp + *index.find(c.MapFlow);
+        }
+    });
+    // 3. digests of every copy on the device: copy i in slot i
+    auto ev = std::make_unique<Eval>(e, U, true);
+    ev->add_block(cp, n);
+    ev->Build();
+    // 4. flowMap.Put: first copy with a digest wins (K5 on the device: the
+    //    smallest post-order index of each digest class) -- the copies'
+    //    digests are slots [0, n) in post-order
+    ev->fetch();
+    std::vector<uint32_t> first(n);
     uint32_t n_unique = 0;
-    if (!post.empty())
-        Check(rf_dedup_digests(e.ctx(), digs.data(), (uint32_t)post.size(), first.data(), &n_unique));
-    detail::FlatMap<const Flow*, uint32_t, detail::PtrHash> index;
-    index.reserve(post.size());
-    for (size_t i = 0; i < post.size(); ++i) index.insert(post[i], (uint32_t)i);
-    auto canon = [&](Flow* c) { return post[first[*index.find(c)]]; };
-    for (Flow* c : post) {
-        for (Flow*& d : c->Deps) d = canon(d);
-        if (c->MapFlow) c->MapFlow = canon(c->MapFlow);
+    if (n) Check(rf_dedup_digests(e.ctx(), ev->cache_.data(), (uint32_t)n, first.data(), &n_unique));
+    Flow* croot = cp + (n - 1);
+    if (n_unique == n) {  // nothing collapsed: the copies' graph is the canonical one
+        if (lowered) *lowered = std::move(ev);
+        return croot;
     }
-    return canon(croot);
+    // deps re-pointed at each class's first copy (equal digests by
+    // construction, so no digest changes)
+    parallel_ranges(n, 16384, lower_threads(e), [&](size_t, size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            for (Flow*& d : cp[i].Deps) d = cp + first[d - cp];
+            if (cp[i].MapFlow) cp[i].MapFlow = cp + first[cp[i].MapFlow - cp];
+        }
+    });
+    return cp + first[n - 1];
 }
 
 // ---- Liveset ---------------------------------------------------------------------

@@ -6,17 +6,20 @@
 // by phase:
 //   build         the Flow nodes (a program's evaluation would create them)
 //   canonicalize  reflow::Canonicalize (flow.go:814-843): copies, their digests
-//                 on the device, flowMap dedup (K5)
+//                 on the device (an Eval over the copies: lowered on host
+//                 threads, loaded, recomputed), flowMap dedup (K5)
 //   lower         Eval::Add: materials + holes for every logical and physical
-//                 job (flow.go:675-792)
+//                 job (flow.go:675-792) -- 0 when Canonicalize handed its Eval
+//                 over (nothing collapsed: it is the canonical graph's)
 //   load          Eval::Build: blob assembly, rf_graph_load, the File-ID
-//                 inputs, one full recompute
+//                 inputs, one full recompute (0 likewise)
 //   incremental   1% of the File IDs replaced (Eval::SetFileID) + Recompute,
 //                 checked slot for slot against a full recompute
 // Output: one JSON object on stdout.  usage: lower_bench <samples> <pairs>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -43,6 +46,13 @@ static Digest id_of(uint64_t tag, uint64_t i) {  // synthetic File IDs (splitmix
 static Digest fd(const char* s) {  // a FlowDigest constant (K / Coerce)
     Digest d = id_of(0xFD, (uint64_t)std::hash<std::string>{}(s));
     return d;
+}
+
+static int lower_threads_in_use(Engine& e) {
+    if (const char* v = getenv("RF_LOWER_THREADS")) return atoi(v);
+    int th = 0, ext = 0;
+    double rate = 0;
+    return rf_host_info(e.ctx(), &th, &rate, &ext) == RF_OK ? th : 0;
 }
 
 static Fileset one(const Digest& id) {
@@ -127,15 +137,23 @@ int main(int argc, char** argv) {
     const uint64_t n_nodes = 4 + S * (P * 14 + 6);
     const double t_build = secs(t0);
     t0 = Clock::now();
-    Flow* c = Canonicalize(e, a, top, Config{false});
+    std::unique_ptr<Eval> lowered;
+    Flow* c = Canonicalize(e, a, top, Config{false}, "", &lowered);
     const double t_canon = secs(t0);
-    Eval ev(e, "", true);
-    t0 = Clock::now();
-    ev.Add(c);
-    const double t_lower = secs(t0);
-    t0 = Clock::now();
-    ev.Build();
-    const double t_load = secs(t0);
+    // Canonicalize hands over its Eval when nothing was collapsed (it IS the
+    // canonical graph's, loaded and recomputed); else the caller lowers again
+    const bool handed_over = lowered != nullptr;
+    double t_lower = 0, t_load = 0;
+    if (!lowered) {
+        lowered = std::make_unique<Eval>(e, "", true);
+        t0 = Clock::now();
+        lowered->Add(c);
+        t_lower = secs(t0);
+        t0 = Clock::now();
+        lowered->Build();
+        t_load = secs(t0);
+    }
+    Eval& ev = *lowered;
     // 1% of the File IDs replaced, one SetFileID each (the shim's per-file call)
     t0 = Clock::now();
     const uint64_t nf = files.size(), nch = nf / 100;
@@ -156,9 +174,10 @@ int main(int argc, char** argv) {
     printf("{\"samples\": %llu, \"pairs\": %llu, \"nodes\": %llu, \"jobs\": %zu, \"build_s\": %.3f, "
            "\"canonicalize_s\": %.3f, \"lower_s\": %.3f, \"load_s\": %.3f, \"set_file_ids_s\": %.3f, "
            "\"files_changed\": %llu, \"incremental_s\": %.4f, \"jobs_rehashed\": %llu, "
-           "\"incremental_equals_full\": %s, \"root\": \"%s\"}\n",
+           "\"incremental_equals_full\": %s, \"canonicalize_handed_over\": %s, \"lower_threads\": %d, "
+           "\"root\": \"%s\"}\n",
            (unsigned long long)S, (unsigned long long)P, (unsigned long long)n_nodes, ev.Jobs(), t_build, t_canon,
            t_lower, t_load, t_set, (unsigned long long)nch, t_inc, (unsigned long long)hashed, same ? "true" : "false",
-           inc_root.String().c_str());
+           handed_over ? "true" : "false", lower_threads_in_use(e), inc_root.String().c_str());
     return same ? 0 : 1;
 }
