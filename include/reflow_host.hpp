@@ -124,6 +124,11 @@ class FlatMap {
         for (const Slot& s : slots_)
             if (s.used) f(s.k, s.v);
     }
+    template <class F>
+    void for_each_mut(F f) {
+        for (Slot& s : slots_)
+            if (s.used) f(s.k, s.v);
+    }
 
    private:
     struct Slot {
@@ -142,6 +147,28 @@ class FlatMap {
     std::vector<Slot> slots_;
     size_t mask_ = 0, n_ = 0;
 };
+// std::vector whose resize default-initialises (no zero fill of the new
+// elements): gigabytes of lowered templates are written once, in parallel
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using RawVec = std::vector<T, DefaultInitAlloc<T>>;
 struct PtrHash {
     size_t operator()(const void* p) const {
         uint64_t x = (uint64_t)(uintptr_t)p;
@@ -344,12 +371,22 @@ class Eval {
     bool file_slots_;
     uint32_t n_slots_ = 0;
     // the jobs, as the rf_graph_desc arrays
-    std::vector<uint32_t> out_slot_, tmpl_len_, hole_pos_, hole_slot_;
-    std::vector<uint64_t> tmpl_off_, hole_ptr_{0};
-    std::string blob_;
+    // (grown without zero-filling: the parallel append writes every element)
+    detail::RawVec<uint32_t> out_slot_, tmpl_len_, hole_pos_, hole_slot_;
+    detail::RawVec<uint64_t> tmpl_off_, hole_ptr_{0};
+    detail::RawVec<char> blob_;
     std::vector<Block> blocks_;
     detail::FlatMap<const Flow*, uint32_t, detail::PtrHash> logical_, physical_;
-    detail::FlatMap<Digest, uint32_t, DigestHash> file_slot_;
+    // File ID -> its input slot, in kFileShards shards by hash (the lowering
+    // resolves a batch's IDs shard by shard on host threads)
+    static constexpr unsigned kFileShards = 64;
+    static unsigned file_shard(const Digest& id) { return (unsigned)(DigestHash{}(id) >> 58); }
+    std::vector<detail::FlatMap<Digest, uint32_t, DigestHash>> file_slot_{kFileShards};
+    size_t n_files() const {
+        size_t n = 0;
+        for (const auto& m : file_slot_) n += m.size();
+        return n;
+    }
     rf_graph* g_ = nullptr;
     mutable std::vector<uint8_t> cache_;  // all slots after the last recompute
     mutable bool cache_ok_ = false;

@@ -6,6 +6,8 @@
 #include "reflow_host.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <exception>
 #include <thread>
 #include <mutex>
@@ -328,6 +330,21 @@ static unsigned lower_threads(Engine& e) {
     return (unsigned)th;
 }
 
+// RF_LOWER_TIMING=1: phase times of the lowering on stderr
+static bool lower_timing() {
+    static const bool on = getenv("RF_LOWER_TIMING") != nullptr;
+    return on;
+}
+struct PhaseClock {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* what) {
+        if (!lower_timing()) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[lower] %s %.3f s\n", what, std::chrono::duration<double>(now - t).count());
+        t = now;
+    }
+};
+
 // Ranges [lo, hi) of n items of `grain` each, claimed by `threads` threads;
 // fn(range index, lo, hi).  The first exception a worker throws is rethrown.
 template <class F>
@@ -482,6 +499,7 @@ struct Eval::Part {
 // numbering is deterministic) and the parts appended in order.
 void Eval::lower_nodes(const std::vector<const Flow*>* nodes, const Block* blk, const std::vector<uint32_t>& phys) {
     const size_t n = nodes ? nodes->size() : blk->n;
+    PhaseClock pc;
     constexpr size_t kGrain = 8192;
     std::vector<Part> parts((n + kGrain - 1) / kGrain);
     parallel_ranges(n, kGrain, lower_threads(e_), [&](size_t r, size_t lo, size_t hi) {
@@ -524,46 +542,92 @@ void Eval::lower_nodes(const std::vector<const Flow*>* nodes, const Block* blk, 
             }
         }
     });
-    size_t jobs = 0, holes = 0, bytes = 0;
-    for (const Part& P : parts) {
-        jobs += P.out_slot.size();
-        holes += P.hole_pos.size();
-        bytes += P.blob.size();
-    }
-    out_slot_.reserve(out_slot_.size() + jobs);
-    tmpl_off_.reserve(tmpl_off_.size() + jobs);
-    tmpl_len_.reserve(tmpl_len_.size() + jobs);
-    hole_ptr_.reserve(hole_ptr_.size() + jobs);
-    hole_pos_.reserve(hole_pos_.size() + holes);
-    hole_slot_.reserve(hole_slot_.size() + holes);
-    blob_.reserve(blob_.size() + bytes);
-    for (Part& P : parts) {
-        for (const auto& [hi_, id] : P.files) {  // one slot per distinct File ID
-            uint32_t s;
-            if (const uint32_t* q = file_slot_.find(id)) {
-                s = *q;
-            } else {
-                s = new_slot();
-                file_slot_.insert(id, s);
+    pc.lap("materials (threads)");
+    const unsigned th = lower_threads(e_);
+    // File IDs: one slot per distinct ID, resolved shard by shard on host
+    // threads.  A new ID gets a provisional shard-local number (bit 31), and
+    // after every shard is done the final slots follow shard by shard, first
+    // occurrence in part order within a shard: deterministic.
+    constexpr uint32_t kProv = 0x80000000u;
+    if (n_slots_ & kProv) throw Error(RF_EINVAL, "too many slots");
+    std::vector<uint64_t> ref0(parts.size() + 1, 0);
+    for (size_t r = 0; r < parts.size(); ++r) ref0[r + 1] = ref0[r] + parts[r].files.size();
+    std::vector<uint32_t> ref_val(ref0.back());
+    std::vector<uint32_t> new_in(kFileShards, 0);
+    parallel_ranges(kFileShards, 1, th, [&](size_t sh, size_t, size_t) {
+        auto& m = file_slot_[sh];
+        uint32_t fresh = 0;
+        for (size_t r = 0; r < parts.size(); ++r) {
+            const auto& F = parts[r].files;
+            for (size_t k = 0; k < F.size(); ++k) {
+                if (file_shard(F[k].second) != sh) continue;
+                uint32_t v;
+                if (const uint32_t* q = m.find(F[k].second)) {
+                    v = *q;
+                } else {
+                    v = kProv | fresh++;
+                    m.insert(F[k].second, v);
+                }
+                ref_val[ref0[r] + k] = v;
             }
-            P.hole_slot[hi_] = s;
         }
-        const uint64_t b0 = blob_.size(), h0 = hole_pos_.size();
-        blob_ += P.blob;
-        out_slot_.insert(out_slot_.end(), P.out_slot.begin(), P.out_slot.end());
-        tmpl_len_.insert(tmpl_len_.end(), P.tmpl_len.begin(), P.tmpl_len.end());
-        for (uint64_t o : P.tmpl_off) tmpl_off_.push_back(b0 + o);
-        for (uint64_t e : P.hole_end) hole_ptr_.push_back(h0 + e);
-        hole_pos_.insert(hole_pos_.end(), P.hole_pos.begin(), P.hole_pos.end());
-        hole_slot_.insert(hole_slot_.end(), P.hole_slot.begin(), P.hole_slot.end());
-        Part().blob.swap(P.blob);  // release as we go
+        new_in[sh] = fresh;
+    });
+    pc.lap("file refs (threads)");
+    std::vector<uint32_t> sbase(kFileShards);
+    for (unsigned sh = 0; sh < kFileShards; ++sh) {
+        sbase[sh] = n_slots_;
+        n_slots_ += new_in[sh];
+        if (n_slots_ & kProv) throw Error(RF_EINVAL, "too many slots");
     }
+    parallel_ranges(kFileShards, 1, th, [&](size_t sh, size_t, size_t) {
+        if (new_in[sh])
+            file_slot_[sh].for_each_mut([&](const Digest&, uint32_t& v) {
+                if (v & kProv) v = sbase[sh] + (v & ~kProv);
+            });
+    });
+    pc.lap("file slots final");
+    // the parts appended in order (offsets first, then copied on host threads)
+    const size_t J0 = out_slot_.size(), H0 = hole_pos_.size(), B0 = blob_.size();
+    std::vector<size_t> pj(parts.size() + 1, J0), ph(parts.size() + 1, H0), pb(parts.size() + 1, B0);
+    for (size_t r = 0; r < parts.size(); ++r) {
+        pj[r + 1] = pj[r] + parts[r].out_slot.size();
+        ph[r + 1] = ph[r] + parts[r].hole_pos.size();
+        pb[r + 1] = pb[r] + parts[r].blob.size();
+    }
+    out_slot_.resize(pj.back());
+    tmpl_off_.resize(pj.back());
+    tmpl_len_.resize(pj.back());
+    hole_ptr_.resize(pj.back() + 1);
+    hole_pos_.resize(ph.back());
+    hole_slot_.resize(ph.back());
+    blob_.resize(pb.back());
+    pc.lap("resize");
+    parallel_ranges(parts.size(), 1, th, [&](size_t r, size_t, size_t) {
+        Part& P = parts[r];
+        for (size_t k = 0; k < P.files.size(); ++k) {
+            const uint32_t v = ref_val[ref0[r] + k];
+            P.hole_slot[P.files[k].first] = (v & kProv) ? sbase[file_shard(P.files[k].second)] + (v & ~kProv) : v;
+        }
+        memcpy(&blob_[pb[r]], P.blob.data(), P.blob.size());
+        std::copy(P.out_slot.begin(), P.out_slot.end(), out_slot_.begin() + pj[r]);
+        std::copy(P.tmpl_len.begin(), P.tmpl_len.end(), tmpl_len_.begin() + pj[r]);
+        for (size_t k = 0; k < P.tmpl_off.size(); ++k) {
+            tmpl_off_[pj[r] + k] = pb[r] + P.tmpl_off[k];
+            hole_ptr_[pj[r] + k + 1] = ph[r] + P.hole_end[k];
+        }
+        std::copy(P.hole_pos.begin(), P.hole_pos.end(), hole_pos_.begin() + ph[r]);
+        std::copy(P.hole_slot.begin(), P.hole_slot.end(), hole_slot_.begin() + ph[r]);
+        Part().blob.swap(P.blob);
+    });
+    pc.lap("append (threads)");
 }
 
 // Every node reachable through Deps, MapFlow and Parent that this Eval has
 // not lowered yet: numbered first (logical slot, physical slot), then lowered
 // on host threads (lower_nodes).
 void Eval::Add(Flow* root) {
+    PhaseClock pc;
     std::vector<const Flow*> todo;
     std::vector<const Flow*> stack{root};
     while (!stack.empty()) {
@@ -582,6 +646,7 @@ void Eval::Add(Flow* root) {
             phys[i] = new_slot();
             physical_.insert(todo[i], phys[i]);
         }
+    pc.lap("numbering");
     lower_nodes(&todo, nullptr, phys);
 }
 
@@ -618,15 +683,16 @@ void Eval::Build() {
     if (g_) rf_graph_destroy(g_);
     g_ = nullptr;
     Check(rf_graph_load(e_.ctx(), &d, &g_));
-    if (file_slot_.size()) {
+    if (const size_t nf = n_files()) {
         std::vector<uint32_t> s;
         std::vector<uint8_t> ids;
-        s.reserve(file_slot_.size());
-        ids.reserve(32 * file_slot_.size());
-        file_slot_.for_each([&](const Digest& id, uint32_t slot) {
-            s.push_back(slot);
-            ids.insert(ids.end(), id.b.begin(), id.b.end());
-        });
+        s.reserve(nf);
+        ids.reserve(32 * nf);
+        for (const auto& m : file_slot_)
+            m.for_each([&](const Digest& id, uint32_t slot) {
+                s.push_back(slot);
+                ids.insert(ids.end(), id.b.begin(), id.b.end());
+            });
         Check(rf_graph_set_slots(g_, s.data(), ids.data(), (uint32_t)s.size()));
     }
     Recompute(true);
@@ -675,14 +741,16 @@ std::vector<Digest> Eval::CacheKeys(const Flow* f) const {
 }
 
 void Eval::SetFileID(const Digest& old_id, const Digest& new_id) {
-    const uint32_t* p = file_slot_.find(old_id);
+    auto& mo = file_slot_[file_shard(old_id)];
+    const uint32_t* p = mo.find(old_id);
     if (!p) throw Error(RF_ENOTFOUND, "file id not referenced: " + old_id.String());
     const uint32_t s = *p;
-    file_slot_.erase(old_id);
-    if (uint32_t* q = file_slot_.find(new_id))
+    mo.erase(old_id);
+    auto& mn = file_slot_[file_shard(new_id)];
+    if (uint32_t* q = mn.find(new_id))
         *q = s;  // (an ID already in use elsewhere: the map keeps the last slot, as before)
     else
-        file_slot_.insert(new_id, s);
+        mn.insert(new_id, s);
     Check(rf_graph_set_slots(g_, &s, new_id.b.data(), 1));
 }
 
@@ -690,6 +758,7 @@ void Eval::SetFileID(const Digest& old_id, const Digest& new_id) {
 Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const std::string& U,
                    std::unique_ptr<Eval>* lowered) {
     if (lowered) lowered->reset();
+    PhaseClock pc;
     // 1. the originals reachable through Deps and MapFlow in post-order (deps,
     //    then the map flow, then the node: the order of flowMap.Put,
     //    flow.go:820-839); each one's index in it.
@@ -716,6 +785,7 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
         post.push_back(f);
     }
     const size_t n = post.size();
+    pc.lap("canonicalize: post-order");
     // 2. one copy per original, contiguous in post-order (f.Copy() +
     //    Config.Merge, deps and map flow pointing at copies), on host threads
     Flow* cp = arena.NewN(n);
@@ -728,10 +798,13 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
             if (c.MapFlow) c.MapFlow = cp + *index.find(c.MapFlow);
         }
     });
+    pc.lap("canonicalize: copies (threads)");
     // 3. digests of every copy on the device: copy i in slot i
     auto ev = std::make_unique<Eval>(e, U, true);
     ev->add_block(cp, n);
+    pc.lap("canonicalize: lowered");
     ev->Build();
+    pc.lap("canonicalize: load + full recompute");
     // 4. flowMap.Put: first copy with a digest wins (K5 on the device: the
     //    smallest post-order index of each digest class) -- the copies'
     //    digests are slots [0, n) in post-order
@@ -739,6 +812,7 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
     std::vector<uint32_t> first(n);
     uint32_t n_unique = 0;
     if (n) Check(rf_dedup_digests(e.ctx(), ev->cache_.data(), (uint32_t)n, first.data(), &n_unique));
+    pc.lap("canonicalize: dedup");
     Flow* croot = cp + (n - 1);
     if (n_unique == n) {  // nothing collapsed: the copies' graph is the canonical one
         if (lowered) *lowered = std::move(ev);
