@@ -141,12 +141,20 @@ struct GraphDev {
     // constant blocks its template starts with -- the record's template
     // offset and block count already skip them); null when no job has any
     uint4* mid = nullptr;
+    // split block 0 (k2_level_pl cb0 = 2): the fusion targets' template-only
+    // block 1 as K+W rows, 16 uint4 each, row kw1_idx[job] (~0u: none),
+    // computed at load (launch_graph_kw1); null: off (RF_K2_SPLIT=0)
+    uint4* kw1 = nullptr;
+    uint32_t* kw1_idx = nullptr;
+    uint32_t kw1_rows = 0;
 };
 // Midstates of the jobs' leading constant blocks, hashed once at load: job i
 // (internal order) hashes lead[i] blocks of its template from block
 // start[i] (64-B units) into mid[2i..2i+1] (state words); IV when lead[i] = 0.
 hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, const uint32_t* lead, uint32_t n,
                                   uint4* mid, hipStream_t s);
+// K+W rows of block 1 of internal jobs jobs[0..n) into g.kw1 rows 0..n-1.
+hipError_t launch_graph_kw1(const GraphDev& g, const uint32_t* jobs, uint32_t n, hipStream_t s);
 hipError_t launch_graph_mark_slots(GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);
 // k3_mark_slots as a graph kernel node: argument values + node parameters
@@ -154,7 +162,7 @@ struct MarkArgs {
     const uint32_t* sl;
     const uint8_t* dig;
     uint32_t n;
-    alignas(16) unsigned char a[176];  // the kernel's LevelArgs (k2_graph.hip), by value
+    alignas(16) unsigned char a[192];  // the kernel's LevelArgs (k2_graph.hip), by value
     void* ptrs[4];
 };
 void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,

@@ -72,6 +72,11 @@ struct LevelArgs {
     // list (at s2) is taken after this level's own, in the same launch
     // (graph_enqueue, GraphDev kLvlSink); lvl2 = ~0u: none
     uint32_t s2 = 0, lvl2 = ~0u;
+    // split block 0 (k2_level_pl<2> cb0 = 2, GraphDev::kw1): the fusion
+    // targets' template-only block 1 as precomputed K+W rows (16 uint4 each,
+    // row kw1_idx[job], ~0u: none); null: off
+    const uint4* kw1 = nullptr;
+    const uint32_t* kw1_idx = nullptr;
 };
 
 // Entries of a level launch: the level's own list (from its end when rev),
@@ -916,6 +921,7 @@ __device__ __forceinline__ void lds_publish_prev(volatile uint32_t* flag, uint32
 
 // K+W[16c .. 16c+15] of a block into its row (kw_expand_store in chunks; w
 // is the rolling 16-word schedule window, as there)
+template <bool kStore = true>
 __device__ __forceinline__ void kw_expand_chunk(uint32_t (&w)[16], uint4* row, int c) {
     constexpr uint32_t K[64] = RF_SHA_K;
 #pragma unroll
@@ -933,7 +939,7 @@ __device__ __forceinline__ void kw_expand_chunk(uint32_t (&w)[16], uint4* row, i
             }
             v[u] = K[t] + wt;
         }
-        row[t4] = make_uint4(v[0], v[1], v[2], v[3]);
+        if (kStore) row[t4] = make_uint4(v[0], v[1], v[2], v[3]);
     }
 }
 
@@ -943,12 +949,14 @@ __device__ __forceinline__ void kw_expand_chunk(uint32_t (&w)[16], uint4* row, i
 // sigma0(W[t-15]) + W[t-16], summed across the pair by one DPP add -- and the
 // pair stores K+W into the job's row.  ~9 instructions per word instead of the
 // producer's ~12, and no hand-over: the chain starts the rounds right after.
+// kQ4 < 16 (split block 0): only K+W[0 .. 4 kQ4) -- the producer expands the rest.
+template <int kQ4 = 16>
 __device__ __forceinline__ void chain_expand_b0(uint32_t (&w)[16], bool elane, uint4* row) {
     constexpr uint32_t K[64] = RF_SHA_K;
     const uint32_t r1 = elane ? 17u : 7u, r2 = elane ? 19u : 18u, r3 = elane ? 10u : 3u;
     const uint32_t E = elane ? ~0u : 0u;  // selects by mask (one bitop3), never by address
 #pragma unroll
-    for (int t4 = 0; t4 < 16; ++t4) {
+    for (int t4 = 0; t4 < kQ4; ++t4) {
         uint32_t v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -998,7 +1006,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint32_t s_flag[3], s_cons[2];
     __shared__ uint32_t s_nbx[64];  // fused targets' block counts (the next iteration's max)
     __shared__ uint4 s_pp[64][2];   // cb0: a finished job's {id, consumer range, valid}, first two edges
-    __shared__ uint32_t s_w0[kStream ? 64 * 17 : 1];  // stream cb0: W[0..15] per job, staged by the chain
+    // W[0..15] per job, staged by the chain: stream cb0, and the split block 0
+    __shared__ uint32_t s_w0[kW == 2 ? 64 * 17 : 1];
+    __shared__ uint32_t s_split;  // split block 0: 2 sid + 1 / + 2 once K+W[32..47] / [48..63] are in
     __shared__ uint32_t s_cw[2];                      // ... block id + 1 staged, per chain wave
     __shared__ uint32_t s_hq[64 * kHq];               // the producer's hole chunks (ChunkCursor)
     __shared__ unsigned long long s_stamp[2][64];
@@ -1021,6 +1031,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         s_flag[0] = s_flag[1] = s_flag[2] = 0;
         s_cons[0] = s_cons[1] = 0;
         s_cw[0] = s_cw[1] = 0;
+        s_split = 0;
     }
     if (a.stamps && threadIdx.x < 128) s_stamp[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     lds_barrier();
@@ -1052,6 +1063,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     auto body = [&](auto rc) {
         constexpr uint32_t R = decltype(rc)::value;
         constexpr bool kChain = R < 2, kIsProd = R == kProd, kIsExp = R == kExp;
+        // split passes so far (every role counts them alike: the flag values)
+        uint32_t sid = 0, known_sp = 0;
         for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
             if (threadIdx.x == 0) ws.jobs += min(64u, n - base);
             const uint32_t i = base + jl;
@@ -1073,6 +1086,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
             uint4 nt[8];
             uint2 nr = make_uint2(0, 0);
+            uint32_t nki = ~0u;  // (producer) the fusion target's kw1 row, fetched a job ahead
             uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
             uint4 nmlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nmhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
             uint32_t sk = 0;
@@ -1106,6 +1120,11 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             while (maxnb) {
                 RF_STAMP_PL(sk); ++sk;
                 const bool cb0 = kCB && a.cb0 && pass > 0;  // workgroup-uniform
+                // split block 0 (cb0 = 2 with precomputed block-1 rows): the
+                // chain expands K+W[16..31] only and the producer K+W[32..63]
+                // of block 0 from the W[0..15] the chain staged, beside
+                // copying block 1's precomputed rows
+                const bool split = kCB && a.cb0 == 2 && a.kw1 != nullptr && pass > 0;
                 // streamed hand-over with a register-built block 0: the chain
                 // writes chunk 0 (K+W[0..15]) itself and stages W[0..15] for the
                 // producer, which expands chunks 1-3 while the chain runs rounds 0-15
@@ -1126,6 +1145,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     }
                 }
                 const bool nfu = has && m1.w != ~0u;
+                const uint32_t ki = fused ? nki : ~0u;  // (producer) this job's kw1 row
                 if (nfu && !fused) {
                     nm0 = a.meta[2ull * m1.w];
                     nm1 = a.meta[2ull * m1.w + 1];
@@ -1220,6 +1240,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 }
                 uint32_t t0, t1, t2, t3;
                 uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+                bool spl0 = false;  // (chain) the block step below is a split block 0
                 const uint32_t nbl = m0.y;  // this lane's job's blocks (0: no job)
                 // one block step of the chain over block b's rows (group 0 first
                 // finishes block b-1: feed-forward, the a-half's last two rounds)
@@ -1254,6 +1275,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             known = lds_poll(&s_flag[bi], 4 * bufb + (g + 2) / 4 + 1, known);
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                         }
+                        if (!kStream && spl0 && (g == 6 || g == 10))  // split block 0: the producer's chunks 2, 3
+                            known_sp = lds_poll(&s_split, 2 * sid + (g == 6 ? 1u : 2u), known_sp);
                         if (g < 14) vnn = r4[g + 2];
                         const uint32_t k4 = g == 15 ? c63 : vn.x;
                         asm volatile(RF_L2_GROUP : RF_LAG_STATE, RF_L2_TMP : RF_L2_IN(v.y, v.z, v.w, k4));
@@ -1366,7 +1389,41 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 for (uint32_t it = 0; it < iters; ++it) {
                     if (kIsProd) {
                         const uint32_t pb = cb0 ? it + 1 : it;  // the block this iteration builds
-                        if (pb < m0.y && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
+                        // split: block 1 from its precomputed rows (loads issued
+                        // first), block 0's K+W[32..63] expanded meanwhile
+                        const bool tab = split && it == 0 && has && ki != ~0u && m0.y >= 2;
+                        if (split && it == 0) {
+                            // (the row in two halves of 8, each load in flight
+                            // over an expansion chunk: 32 VGPRs, not 64)
+                            typedef uint32_t v4u __attribute__((ext_vector_type(4)));  // (a uint4 array here went to scratch)
+                            const v4u* src = reinterpret_cast<const v4u*>(a.kw1) + 16ull * (tab ? ki : 0u);
+                            v4u* row1 = reinterpret_cast<v4u*>(&kw[(64 + lane) * kPcRow]);
+                            v4u k1[8];
+                            if (tab) {
+    #pragma unroll
+                                for (int q = 0; q < 8; ++q) k1[q] = src[q];
+                            }
+                            uint32_t w[16];
+    #pragma unroll
+                            for (int q = 0; q < 16; ++q) w[q] = s_w0[lane * 17 + q];
+                            uint4* row0 = reinterpret_cast<uint4*>(&kw[lane * kPcRow]);
+                            kw_expand_chunk<false>(w, row0, 1);  // (K+W[16..31]: the chain's)
+                            kw_expand_chunk(w, row0, 2);
+                            lds_publish(&s_split, 2 * sid + 1, lane);
+                            if (tab) {
+    #pragma unroll
+                                for (int q = 0; q < 8; ++q) row1[q] = k1[q];
+    #pragma unroll
+                                for (int q = 0; q < 8; ++q) k1[q] = src[8 + q];
+                            }
+                            kw_expand_chunk(w, row0, 3);
+                            lds_publish(&s_split, 2 * sid + 2, lane);
+                            if (tab) {
+    #pragma unroll
+                                for (int q = 0; q < 8; ++q) row1[8 + q] = k1[q];
+                            }
+                        }
+                        if (pb < m0.y && !tab && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
                             uint32_t w[16];
                             cur.block(a, pb, ring, w, wfused);
                             // (RF_K2_STAMPS=3: every block's assembly end on the producer)
@@ -1391,6 +1448,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 nnm0 = a.meta[2ull * nm1.w];
                                 nnm1 = a.meta[2ull * nm1.w + 1];
                             }
+                            if (a.kw1) nki = a.kw1_idx[m1.w];
                         }
                         // idle in the last iteration (every block of the pass built):
                         // the fusion target's template blocks 0 and 1 into the ring,
@@ -1425,11 +1483,17 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         // other row buffer (the producer writes it only after the
                         // barrier): the code is then cached when the links start.
                         const bool exb = it == 0 && (cb0 || (kCB && a.cb0 && pass == 0 && a.dbg_twice != 5));
-                        if (exb)
-                            chain_expand_b0(wb0, elane, reinterpret_cast<uint4*>(&kw[((cb0 ? 0u : 64u) + jl) * kPcRow]));
+                        if (exb) {
+                            uint4* row = reinterpret_cast<uint4*>(&kw[((cb0 ? 0u : 64u) + jl) * kPcRow]);
+                            if (!kStream && a.kw1)  // (pass 0: warms the code the split passes run)
+                                chain_expand_b0<8>(wb0, elane, row);
+                            else
+                                chain_expand_b0(wb0, elane, row);
+                        }
                         if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
                         if (cb0 || it >= lag) {
                             const uint32_t cbk = cb0 ? it : it - lag;
+                            spl0 = split && it == 0;
                             chain_block(cbk, cbk, true);
                         }
                         if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
@@ -1506,6 +1570,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     #pragma unroll
                         for (int q = 1; q < 8; ++q) wb0[q] = __builtin_amdgcn_alignbit(H[q - 1], H[q], 16);
                         wb0[8] |= H[7] << 16;
+                        if (!kStream && a.kw1 && elane)  // the next split pass's producer expands from these
+    #pragma unroll
+                            for (int q = 0; q < 16; ++q) s_w0[jl * 17 + q] = wb0[q];
                     }
                     if (elane) {
                         s_next[jl] = next;
@@ -1539,6 +1606,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 fslot = has ? m1.x : ~0u;
                 has = nx != ~0u;
                 p = has ? nx : 0u;
+                if (split) ++sid;
                 ++pass;
             }
             if (kStream && kIsProd) drop_pre();
@@ -1555,6 +1623,24 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     if (a.stamps && blockIdx.x == 0 && (wave == 0 || wave == kProd))
         a.stamps[128 * a.lvl + 64 * (wave != 0) + lane] = s_stamp[wave != 0][lane];
     ws.end(a);
+}
+
+// Load time: block 1 of each listed job (a fusion target whose one hole lies
+// in block 0, so block 1 is template only) as its K+W row, for the split
+// block 0 of k2_level_pl.
+__global__ __launch_bounds__(256) void k2_kw1(const uint8_t* __restrict__ tmpl, const uint4* __restrict__ meta,
+                                              const uint32_t* __restrict__ jobs, uint32_t n, uint4* kw1) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint4 m0 = meta[2ull * jobs[k]];
+        const uint4* T = reinterpret_cast<const uint4*>(tmpl) + 4ull * m0.x + 4;  // block 1
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = T[q];
+            w[4 * q] = bswap32(v.x); w[4 * q + 1] = bswap32(v.y); w[4 * q + 2] = bswap32(v.z); w[4 * q + 3] = bswap32(v.w);
+        }
+        kw_expand_store(w, kw1 + 16ull * k);
+    }
 }
 
 // Load time: the chaining value after each job's constant leading blocks.
@@ -2377,6 +2463,10 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
                 g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
                 full ? nullptr : g.wgst};
+    if (!full && a.cb0 == 2) {  // split block 0 (the precomputed block-1 rows)
+        a.kw1 = g.kw1;
+        a.kw1_idx = g.kw1_idx;
+    }
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
@@ -2451,6 +2541,12 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
     hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_graph_kw1(const GraphDev& g, const uint32_t* jobs, uint32_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k2_kw1, dim3(grid_for(n, 16384)), dim3(256), 0, s, g.tmpl, g.meta, jobs, n, g.kw1);
     return hipGetLastError();
 }
 
