@@ -1725,19 +1725,31 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
             if (sink != ~0u && fill != ~0u && G.sink_attach_ok) {
                 for (uint32_t l = fill + 1; l-- > smin && attach == ~0u;)
                     if ((G.inc_level[l] & kLvlForm) && graph_level_lf(G, l)) attach = l;
-                // no throughput-form level to fill: the last level above the
-                // fill level (a merge tree's root: one job on a nearly idle
-                // chip) rather than the fill level itself, whose latency-form
-                // chains the sinks' workgroups would share CUs with (the
-                // 8-rank piece's OpK level: 67 us, its chains alone ~50);
-                // RF_K2_SINK_LAST=0: the fill level (A/B)
-                static const bool last = [] {
-                    const char* v = getenv("RF_K2_SINK_LAST");
-                    return !(v && atoi(v) == 0);
+                // no throughput-form level to fill: a level above the fill
+                // level (a merge tree: few long jobs on a nearly idle chip)
+                // rather than the fill level itself, whose latency-form chains
+                // the sinks' workgroups would share CUs with (the 8-rank
+                // piece's OpK level: 67 us, its chains alone ~50) -- the one
+                // with the most jobs, so the sinks run beside its longest
+                // stretch of work (octo-form levels take the list in
+                // workgroups of their own).  RF_K2_SINK_AT (A/B, read once):
+                // 0 = the fill level, 1 = the last latency-form level above it
+                static const int sink_at = [] {
+                    const char* v = getenv("RF_K2_SINK_AT");
+                    const char* w = getenv("RF_K2_SINK_LAST");  // (round-4 scripts: =0 the fill level)
+                    return v ? atoi(v) : (w && atoi(w) == 0) ? 0 : 2;
                 }();
-                if (attach == ~0u && last)
+                if (attach == ~0u && sink_at == 1)
                     for (uint32_t l = sink; l-- > fill + 1 && attach == ~0u;)
                         if ((G.inc_level[l] & kLvlForm) && !(G.inc_level[l] & kLvlOct)) attach = l;
+                if (attach == ~0u && sink_at == 2) {
+                    uint32_t most = 0;
+                    for (uint32_t l = fill + 1; l < sink; ++l)
+                        if ((G.inc_level[l] & kLvlForm) && G.lvl_start[l + 1] - G.lvl_start[l] > most) {
+                            most = G.lvl_start[l + 1] - G.lvl_start[l];
+                            attach = l;
+                        }
+                }
                 if (attach == ~0u) attach = fill;
             }
         }
@@ -1749,7 +1761,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
             if (!(G.inc_level[l] & kLvlForm) || (l == sink && attach != ~0u)) continue;
             HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr, l == attach ? sink : ~0u));
             G.last_levels_lf += graph_level_lf(G, l) ? 1u : 0u;
-            G.last_levels_oct += (G.inc_level[l] & kLvlOct) && l != attach ? 1u : 0u;
+            G.last_levels_oct += (G.inc_level[l] & kLvlOct) ? 1u : 0u;  // (RF_K2_CHAIN=14 aside)
             first = false;
         }
         gr->last_counts = G.counts;

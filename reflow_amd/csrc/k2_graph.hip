@@ -77,6 +77,7 @@ struct LevelArgs {
     // row kw1_idx[job], ~0u: none); null: off
     const uint4* kw1 = nullptr;
     const uint32_t* kw1_idx = nullptr;
+    uint32_t oct_wg = 0;  // k2_level_oct: workgroups of the level's own list (the rest run the sink list)
 };
 
 // Entries of a level launch: the level's own list (from its end when rev),
@@ -483,6 +484,15 @@ struct ChunkCursor {
             const uint32_t D[8] = {q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8]};
             or_digest(ring, pos, D);
             ++hn;
+        }
+    }
+    // block b's template-only bookkeeping without assembling it (its K+W
+    // rows came from elsewhere: split block 0's precomputed block 1)
+    __device__ __forceinline__ void skip(uint32_t b, uint32_t* ring) {
+        if (b + 1 < nb) ring_put(ring, ((b & 1) * 16) ^ 16, t);
+        if (b + 2 < nb) {
+            const uint4* s = T + 4 * (b + 2);
+            t[0] = s[0]; t[1] = s[1]; t[2] = s[2]; t[3] = s[3];
         }
     }
     __device__ __forceinline__ void block(const LevelArgs& a, uint32_t b, uint32_t* ring, uint32_t (&w)[16],
@@ -1421,6 +1431,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             if (tab) {
     #pragma unroll
                                 for (int q = 0; q < 8; ++q) row1[8 + q] = k1[q];
+                                cur.skip(1, ring);  // (a longer target's block 2 on from the cursor, as after block 1)
                             }
                         }
                         if (pb < m0.y && !tab && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
@@ -1926,7 +1937,50 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __re
 // CU), so once a level's list is several times the resident set the step is
 // bound by rounds of resident workgroups x link latency (configs[3]'s
 // 100M-node DAG on one GPU), and this form is faster.
-__global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
+// One listed job per lane, the throughput form's body (k2_level_lf, and the
+// sink list riding on an octo-form launch): list entry ii (~0u: none) is
+// hashed in the lane, its fused chain followed in the lane; every lane of the
+// wave calls it (propagate's appends are per wave).  Returns the fused jobs
+// the lane hashed.
+__device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii) {
+    uint32_t p = ~0u;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+    if (ii != ~0u) {
+        p = a.list[ii];
+        m0 = a.lmeta[2ull * ii];
+        m1 = a.lmeta[2ull * ii + 1];
+    }
+    uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
+    uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
+    if (p != ~0u) {
+        MatCursor cur;
+        cur.begin(a, m0, ring);
+        ShaState st;
+        init_state(a, p, st);
+        for (uint32_t b = 0; b < cur.nb; ++b) {
+            uint32_t w[16];
+            cur.block(a, b, ring, w);
+            sha256_compress(st, w);
+        }
+        const bool ch = finish_job(a, m1, st);
+        a.dirty[p] = 0u;
+        const bool nf = m1.w != ~0u;
+        cb = m1.y;
+        cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);
+        if (ch && nf) {
+            nx = m1.w;
+            fslot = m1.x;
+            flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+            fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+            nm0 = a.meta[2ull * nx];
+            nm1 = a.meta[2ull * nx + 1];
+        }
+    }
+    propagate(a, cb, cz);
+    return hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi);
+}
+
+__global__ __launch_bounds__(kLevelBlock, 3) void k2_level_lf(LevelArgs a) {  // (3 waves a SIMD: <= 168 VGPRs)
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
     zero_other_counts(a);
@@ -1938,42 +1992,7 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level_lf(LevelArgs a) {
     for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
         if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
         const uint32_t i = base + threadIdx.x;
-        uint32_t p = ~0u;
-        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-        if (i < n) {
-            const uint32_t ii = ll.at(a, i);
-            p = a.list[ii];
-            m0 = a.lmeta[2ull * ii];
-            m1 = a.lmeta[2ull * ii + 1];
-        }
-        uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
-        uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
-        if (p != ~0u) {
-            MatCursor cur;
-            cur.begin(a, m0, ring);
-            ShaState st;
-            init_state(a, p, st);
-            for (uint32_t b = 0; b < cur.nb; ++b) {
-                uint32_t w[16];
-                cur.block(a, b, ring, w);
-                sha256_compress(st, w);
-            }
-            const bool ch = finish_job(a, m1, st);
-            a.dirty[p] = 0u;
-            const bool nf = m1.w != ~0u;
-            cb = m1.y;
-            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);
-            if (ch && nf) {
-                nx = m1.w;
-                fslot = m1.x;
-                flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
-                fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
-                nm0 = a.meta[2ull * nx];
-                nm1 = a.meta[2ull * nx + 1];
-            }
-        }
-        propagate(a, cb, cz);
-        hashed += hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi);
+        hashed += lf_job(a, ring, i < n ? ll.at(a, i) : ~0u);
     }
     count_fused(a, hashed);
     ws.end(a);
@@ -2042,7 +2061,10 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
 // block), double-buffered rows); the chain wave runs K1's octo chain (8 lanes
 // a job, the duo's 8-instruction round: lag_chain.h RF_OCT_*).  Jobs have no
 // fusion target, at most kOctMaxBlocks blocks and kOctMaxHoles holes
-// (rf_graph_load's kLvlOct analysis); no sink list rides on this launch.
+// (rf_graph_load's kLvlOct analysis).  An attached sink list (LaunchList)
+// runs in the workgroups from a.oct_wg on, one job per lane as k2_level_lf
+// (lf_job, the ring in the kw array): the octo workgroups come first in
+// dispatch order, the short sinks fill the CUs the few long jobs leave idle.
 constexpr uint32_t kOctStage = kOctMaxBlocks * 16 + 4;  // words per job's staged material (16-B aligned)
 
 // OR digest D (8 LE words) into the linear material stage m at byte `pos`
@@ -2064,6 +2086,22 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
     // a-lanes' k row (as k1_sha256_octo); the 8 jobs' staged materials
     __shared__ __attribute__((aligned(16))) uint32_t kw[129 * kPcRow];
     __shared__ __attribute__((aligned(16))) uint32_t mat[8 * kOctStage];
+    static_assert(128 * kRing <= 129 * kPcRow, "the sink lanes' rings live in kw");
+    if (blockIdx.x >= a.oct_wg) {  // the attached sink list, one job per lane
+        WgStamp ws;
+        ws.begin(a);
+        const LaunchList ll(a);
+        const uint32_t g2 = gridDim.x - a.oct_wg;
+        uint32_t hashed = 0;
+        for (uint32_t base = ll.n1 + (blockIdx.x - a.oct_wg) * 128; base < ll.n; base += g2 * 128) {
+            if (threadIdx.x == 0) ws.jobs += min(128u, ll.n - base);
+            const uint32_t i = base + threadIdx.x;
+            hashed += lf_job(a, &kw[threadIdx.x * kRing], i < ll.n ? ll.at(a, i) : ~0u);
+        }
+        count_fused(a, hashed);
+        ws.end(a);
+        return;
+    }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t f = lane >> 3;  // the lane's job of the group (both waves)
@@ -2085,7 +2123,7 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
     ws.begin(a);
     const uint32_t n = a.counts[a.lvl];
     const uint4* T4 = reinterpret_cast<const uint4*>(a.tmpl);
-    for (uint32_t base = blockIdx.x * 8; base < n; base += gridDim.x * 8) {
+    for (uint32_t base = blockIdx.x * 8; base < n; base += a.oct_wg * 8) {
         if (threadIdx.x == 0) ws.jobs += min(8u, n - base);
         const uint32_t i = base + f;
         const bool has = i < n;
@@ -2495,10 +2533,12 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_CHAIN");
             return v && atoi(v) == 14;
         }();
-        // a level of few long jobs (kLvlOct): the octo form, 8 jobs a workgroup
-        if ((g.inc_level[lvl] & kLvlOct) && sink_lvl == ~0u && !one_lane) {
-            const uint32_t og = std::min<uint32_t>((e - b + 7) / 8, 1024u);
-            hipLaunchKernelGGL(k2_level_oct, dim3(og), dim3(128), 0, s, a);
+        // a level of few long jobs (kLvlOct): the octo form, 8 jobs a
+        // workgroup, then an attached sink list's workgroups (128 jobs each)
+        if ((g.inc_level[lvl] & kLvlOct) && !one_lane) {
+            a.oct_wg = std::min<uint32_t>((e - b + 7) / 8, 1024u);
+            const uint32_t sg = std::min<uint32_t>((n2 + 127) / 128, 1024u);
+            hipLaunchKernelGGL(k2_level_oct, dim3(a.oct_wg + sg), dim3(128), 0, s, a);
             return hipGetLastError();
         }
         const bool wide = (g.inc_level[lvl] & kLvlForm) == 2;

@@ -1,8 +1,9 @@
 #!/bin/bash
 # A full GPU-box session: the focus tests, the GPU suite, smoke(), the
-# driver's bench command, then the K2 form A/B (the octo form and the sink
-# placement against round 3's: RF_K2_OCT=0 RF_K2_SINK_LAST=0), per-level
-# workgroup stamps of the 8-rank piece, and the PMC traffic passes.  Every GPU
+# driver's bench command, then the K2 form A/B on one box (default; round 3's
+# forms: RF_K2_OCT=0 RF_K2_SINK_LAST=0 RF_K2_SPLIT=0; split block 0 off;
+# default again), per-level workgroup stamps of the 8-rank piece, and the PMC
+# traffic passes.  Every GPU
 # step has its own time limit; the steps are chained so a failure ends it.
 #   FOCUS="tests/..." bash tools/gpu_s2.sh <tag> A    focus tests, GPU suite, smoke, bench
 #   bash tools/gpu_s2.sh <tag> B                        forms A/B, stamps, PMC passes
@@ -20,8 +21,10 @@ if [ "$2" = A ]; then
     tail -4 $out/bench.log
 else
 step forms && timeout -k 10 400 python -u tools/dag_forms.py --c2 --c4-ranks 8 > $out/forms_new.json 2> $out/forms_new.log &&
-RF_K2_OCT=0 RF_K2_SINK_LAST=0 timeout -k 10 400 python -u tools/dag_forms.py --c2 --c4-ranks 8 > $out/forms_old.json 2> $out/forms_old.log &&
-grep "ms/step" $out/forms_new.log $out/forms_old.log &&
+RF_K2_OCT=0 RF_K2_SINK_LAST=0 RF_K2_SPLIT=0 timeout -k 10 400 python -u tools/dag_forms.py --c2 --c4-ranks 8 > $out/forms_old.json 2> $out/forms_old.log &&
+RF_K2_SPLIT=0 timeout -k 10 400 python -u tools/dag_forms.py --c2 --c4-ranks 8 > $out/forms_nosplit.json 2> $out/forms_nosplit.log &&
+timeout -k 10 400 python -u tools/dag_forms.py --c2 --c4-ranks 8 > $out/forms_new2.json 2> $out/forms_new2.log &&
+grep "ms/step" $out/forms_new.log $out/forms_old.log $out/forms_nosplit.log $out/forms_new2.log &&
 step stamps && RF_K2_WGSTAMPS=1 timeout -k 10 300 python -u tools/stamp_probe.py c4 8 > $out/wg_c4r8.log 2>&1 &&
 step pmc && timeout -k 10 900 bash tools/pmc_round4.sh $out/pmc all 8 > $out/pmc.log 2>&1
 fi
