@@ -1519,18 +1519,9 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         HIPC(sync_copy(ctx, gr->b_meta.p, meta.data(), 32ull * J, hipMemcpyHostToDevice));
         HIPC(sync_copy(ctx, gr->b_holes.p, holes.data(), 8ull * H, hipMemcpyHostToDevice));
     }
-    // split block 0: the fusion targets whose one hole lies in block 0 (so
-    // block 1 is template only) get their block 1's K+W row precomputed
-    if (G.hole_in_b0 && G.fuse_pos2 && graph_split_on()) {
-        std::vector<uint32_t> kw1_idx(J, ~0u);
-        uint32_t nk = 0;
-        for (uint32_t i = 0; i < J; ++i) {
-            const uint32_t* m = &meta[8ull * i];
-            if (!fused_target[perm[i]] || m[1] < 2 || m[3] != m[2] + 1 || holes[2ull * m[2]] + 32 > 64) continue;
-            kw1_idx[i] = nk++;
-        }
-        if (int rc = graph_kw1_build(gr, kw1_idx)) return rc;
-    }
+    // split block 0: every fusion target's one hole at byte 2 (fuse_pos2),
+    // so its block 1 is template only
+    G.split_b0 = G.hole_in_b0 && G.fuse_pos2 && graph_split_on();
     if (getenv("RF_K2_STAMPS")) {  // diagnostic: per-phase times of workgroup 0 of each level
         HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
@@ -1553,8 +1544,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
                           &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_lmeta, &gr->b_counts, &gr->b_counts_last,
-                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst,
-                          &gr->b_kw1, &gr->b_kw1_idx})
+                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);
@@ -1614,10 +1604,6 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
 // block, memory-latency-bound, against the three-wave latency form's ~1.5).
 static constexpr uint64_t kThruSlots = RF_K2_THRU_DEFAULT, kThruSlotsWide = RF_K2_THRU_WIDE_DEFAULT;
 
-// The form thresholds of a graph being loaded or restored: the defaults, or
-// RF_K2_THRU / RF_K2_THRU_WIDE (tests and A/B runs force either form); read
-// here once, never per step (a libc call per step, and racy against setenv
-// in threaded callers).  rf_graph_set_forms changes them later.
 // Split block 0 of the fused links (k2_level_pl cb0 = 2): on unless
 // RF_K2_SPLIT=0 (A/B; read at load and restore, never per step).
 bool graph_split_on() {
@@ -1625,42 +1611,10 @@ bool graph_split_on() {
     return !(v && atoi(v) == 0);
 }
 
-// GraphDev::kw1 for a graph whose templates and records are on the device:
-// kw1_idx[i] = job i's row or ~0u; the rows are K+W of each listed job's block
-// 1 (launch_graph_kw1).  No row at all: the split stays off.
-int graph_kw1_build(rf_graph* gr, const std::vector<uint32_t>& kw1_idx) {
-    rf_ctx* ctx = gr->ctx;
-    GraphDev& G = gr->g;
-    std::vector<uint32_t> jobs;
-    for (uint32_t i = 0; i < (uint32_t)kw1_idx.size(); ++i)
-        if (kw1_idx[i] != ~0u) {
-            if (kw1_idx[i] >= jobs.size()) jobs.resize(kw1_idx[i] + 1, ~0u);
-            jobs[kw1_idx[i]] = i;
-        }
-    for (uint32_t j : jobs)
-        if (j == ~0u) return fail(RF_EINTEGRITY, "split block 0: row numbering not dense");
-    G.kw1 = nullptr;
-    G.kw1_idx = nullptr;
-    if (jobs.empty()) return RF_OK;
-    DevBuf d_jobs;
-    struct Rel {
-        DevBuf& b;
-        ~Rel() { b.release(); }
-    } rel{d_jobs};
-    hipError_t e;
-    if ((e = gr->b_kw1_idx.ensure(4ull * kw1_idx.size())) != hipSuccess ||
-        (e = gr->b_kw1.ensure(256ull * jobs.size())) != hipSuccess || (e = d_jobs.ensure(4ull * jobs.size())) != hipSuccess)
-        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "split block 0 rows: %s", hipGetErrorString(e));
-    HIPC(sync_copy(ctx, gr->b_kw1_idx.p, kw1_idx.data(), 4ull * kw1_idx.size(), hipMemcpyHostToDevice));
-    HIPC(sync_copy(ctx, d_jobs.p, jobs.data(), 4ull * jobs.size(), hipMemcpyHostToDevice));
-    G.kw1 = gr->b_kw1.as<uint4>();
-    G.kw1_rows = (uint32_t)jobs.size();
-    G.kw1_idx = gr->b_kw1_idx.as<uint32_t>();
-    HIPC(launch_graph_kw1(G, d_jobs.as<uint32_t>(), (uint32_t)jobs.size(), ctx->stream));
-    HIPC(hipStreamSynchronize(ctx->stream));
-    return RF_OK;
-}
-
+// The form thresholds of a graph being loaded or restored: the defaults, or
+// RF_K2_THRU / RF_K2_THRU_WIDE (tests and A/B runs force either form); read
+// here once, never per step (a libc call per step, and racy against setenv
+// in threaded callers).  rf_graph_set_forms changes them later.
 void graph_forms_from_env(GraphDev& G) {
     const char* tv = getenv("RF_K2_THRU");
     const char* tw = getenv("RF_K2_THRU_WIDE");
@@ -2070,7 +2024,7 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
     out->last_levels_lf = gr->g.last_levels_lf;
     out->last_mark_lf = gr->g.last_mark_lf;
     out->last_levels_oct = gr->g.last_levels_oct;
-    out->split_rows = gr->g.kw1 ? gr->g.kw1_rows : 0;
+    out->split_block0 = gr->g.split_b0 ? 1u : 0u;
     if (gr->timed) {
         HIPC(hipEventSynchronize(gr->e1));
         HIPC(hipEventElapsedTime(&out->last_ms, gr->e0, gr->e1));

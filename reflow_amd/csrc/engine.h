@@ -141,20 +141,16 @@ struct GraphDev {
     // constant blocks its template starts with -- the record's template
     // offset and block count already skip them); null when no job has any
     uint4* mid = nullptr;
-    // split block 0 (k2_level_pl cb0 = 2): the fusion targets' template-only
-    // block 1 as K+W rows, 16 uint4 each, row kw1_idx[job] (~0u: none),
-    // computed at load (launch_graph_kw1); null: off (RF_K2_SPLIT=0)
-    uint4* kw1 = nullptr;
-    uint32_t* kw1_idx = nullptr;
-    uint32_t kw1_rows = 0;
+    // split block 0 (k2_level_pl cb0 = 2): the producer expands the upper
+    // half of a fusion target's block 0 and builds its template-only block 1
+    // during the job before it; set at load / restore (RF_K2_SPLIT=0: off)
+    bool split_b0 = false;
 };
 // Midstates of the jobs' leading constant blocks, hashed once at load: job i
 // (internal order) hashes lead[i] blocks of its template from block
 // start[i] (64-B units) into mid[2i..2i+1] (state words); IV when lead[i] = 0.
 hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, const uint32_t* lead, uint32_t n,
                                   uint4* mid, hipStream_t s);
-// K+W rows of block 1 of internal jobs jobs[0..n) into g.kw1 rows 0..n-1.
-hipError_t launch_graph_kw1(const GraphDev& g, const uint32_t* jobs, uint32_t n, hipStream_t s);
 hipError_t launch_graph_mark_slots(GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);
 // k3_mark_slots as a graph kernel node: argument values + node parameters

@@ -35,7 +35,7 @@ struct rf_graph {
     std::vector<int64_t> producer;   // slot -> external job or -1
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
-    DevBuf b_stamps, b_mid, b_wgst, b_kw1, b_kw1_idx;
+    DevBuf b_stamps, b_mid, b_wgst;
     DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_lmeta, b_counts,
         b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
@@ -65,7 +65,5 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s, uint32_t lvl_l
 bool graph_plain_steps();  // incremental steps are plain launches (not RF_K2_GRAPH=1)
 void graph_forms_from_env(rf::GraphDev& G);  // form thresholds at load / restore
 bool graph_split_on();                        // RF_K2_SPLIT (default on)
-// the split block 0's table (GraphDev::kw1) from a host kw1_idx [n_jobs]
-int graph_kw1_build(rf_graph* gr, const std::vector<uint32_t>& kw1_idx);
 int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes);
 void graph_part_release(rf_graph* gr);

@@ -111,7 +111,6 @@ struct Validator {
     uint32_t lv = 0;                       // meta cursor: the level of the next record
     std::vector<uint8_t> one_hole;         // internal job has exactly one hole
     std::vector<uint8_t> produced;         // slot is some job's output
-    std::vector<uint8_t> split_b0;         // internal job: bit 0 >= 2 blocks, bit 1 a fusion target (GraphDev::kw1)
     std::vector<uint32_t> cons_ptr;        // host copy: slot -> its reverse-edge range
     uint64_t slot = 0;                     // cons_job cursor: the slot whose range holds the next edge
 
@@ -139,7 +138,7 @@ struct Validator {
         const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
         const uint64_t J = h.n_jobs, S = h.n_slots, H = h.n_holes, TB = h.tmpl_bytes / 64;
         if (!strcmp(name, "meta")) {
-            if (o == 0) one_hole.assign(J, 0), produced.assign(S, 0), split_b0.assign(J, 0);
+            if (o == 0) one_hole.assign(J, 0), produced.assign(S, 0);
             for (uint64_t r = 0; r < n / 32; ++r) {
                 const uint32_t* m = w + 8 * r;
                 if ((uint64_t)m[0] + m[1] > TB || m[2] > m[3] || m[3] > H || m[4] >= S || m[5] > m[6] || m[6] > H ||
@@ -155,8 +154,6 @@ struct Validator {
                                 (unsigned long long)j);
                 out_slot[j] = m[4];
                 one_hole[j] = m[3] - m[2] == 1;
-                split_b0[j] |= m[1] >= 2 ? 1 : 0;
-                if (m[7] != 0xffffffffu) split_b0[m[7]] |= 2;
                 produced[m[4]] = 1;
             }
         } else if (!strcmp(name, "holes")) {
@@ -369,16 +366,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
         if (i >= h.n_jobs || out_slot[i] >= h.n_slots) return fail(RF_EINTEGRITY, "graph restore: bad job record");
         gr->producer[out_slot[i]] = j;
     }
-    // split block 0's precomputed rows (not in the file: rebuilt from the
-    // restored templates, as rf_graph_load builds them; under fuse_pos2 every
-    // fusion target's one hole sits at byte 2 of block 0)
-    if (G.hole_in_b0 && G.fuse_pos2 && graph_split_on()) {
-        std::vector<uint32_t> kw1_idx(h.n_jobs, ~0u);
-        uint32_t nk = 0;
-        for (uint32_t i = 0; i < h.n_jobs; ++i)
-            if (val.split_b0[i] == 3 && val.one_hole[i]) kw1_idx[i] = nk++;
-        if (int rc = graph_kw1_build(gr, kw1_idx)) return rc;
-    }
+    G.split_b0 = G.hole_in_b0 && G.fuse_pos2 && graph_split_on();  // (as rf_graph_load)
     gr->initialized = (h.flags & kInitialized) != 0;
     guard.release();
     *out = gr;

@@ -72,11 +72,10 @@ struct LevelArgs {
     // list (at s2) is taken after this level's own, in the same launch
     // (graph_enqueue, GraphDev kLvlSink); lvl2 = ~0u: none
     uint32_t s2 = 0, lvl2 = ~0u;
-    // split block 0 (k2_level_pl<2> cb0 = 2, GraphDev::kw1): the fusion
-    // targets' template-only block 1 as precomputed K+W rows (16 uint4 each,
-    // row kw1_idx[job], ~0u: none); null: off
-    const uint4* kw1 = nullptr;
-    const uint32_t* kw1_idx = nullptr;
+    // split block 0 (k2_level_pl<2> cb0 = 2, GraphDev::split_b0): the
+    // producer expands the upper half of a fusion target's block 0 and builds
+    // its template-only block 1 during the job before it
+    uint32_t split = 0;
     uint32_t oct_wg = 0;  // k2_level_oct: workgroups of the level's own list (the rest run the sink list)
 };
 
@@ -1096,7 +1095,11 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
             uint4 nt[8];
             uint2 nr = make_uint2(0, 0);
-            uint32_t nki = ~0u;  // (producer) the fusion target's kw1 row, fetched a job ahead
+            // split block 0: the job's block 1 was built during the job before it
+            // (producer, per lane), and the pass's row-buffer parity: block b of
+            // the pass is in buffer (b + xp) & 1 (every role, workgroup-uniform)
+            bool pre1 = false;
+            uint32_t xp = 0;
             uint2 npre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
             uint4 nmlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), nmhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
             uint32_t sk = 0;
@@ -1134,7 +1137,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 // chain expands K+W[16..31] only and the producer K+W[32..63]
                 // of block 0 from the W[0..15] the chain staged, beside
                 // copying block 1's precomputed rows
-                const bool split = kCB && a.cb0 == 2 && a.kw1 != nullptr && pass > 0;
+                const bool split = kCB && a.cb0 == 2 && a.split && pass > 0;
+                // this pass's last iteration builds the fusion targets' block 1
+                // into the buffer its own last block leaves free
+                const bool build1 = kCB && a.cb0 == 2 && a.split;
                 // streamed hand-over with a register-built block 0: the chain
                 // writes chunk 0 (K+W[0..15]) itself and stages W[0..15] for the
                 // producer, which expands chunks 1-3 while the chain runs rounds 0-15
@@ -1155,7 +1161,6 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     }
                 }
                 const bool nfu = has && m1.w != ~0u;
-                const uint32_t ki = fused ? nki : ~0u;  // (producer) this job's kw1 row
                 if (nfu && !fused) {
                     nm0 = a.meta[2ull * m1.w];
                     nm1 = a.meta[2ull * m1.w + 1];
@@ -1248,6 +1253,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         nmhi = a.mid[2ull * m1.w + 1];
                     }
                 }
+                if (kChain && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }  // (the next target's loads issued)
                 uint32_t t0, t1, t2, t3;
                 uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
                 bool spl0 = false;  // (chain) the block step below is a split block 0
@@ -1399,40 +1405,21 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 for (uint32_t it = 0; it < iters; ++it) {
                     if (kIsProd) {
                         const uint32_t pb = cb0 ? it + 1 : it;  // the block this iteration builds
-                        // split: block 1 from its precomputed rows (loads issued
-                        // first), block 0's K+W[32..63] expanded meanwhile
-                        const bool tab = split && it == 0 && has && ki != ~0u && m0.y >= 2;
+                        // split: block 0's K+W[32..63] from the W[0..15] the chain
+                        // staged (chunk 1 only rolls the window: K+W[16..31] are the
+                        // chain's); block 1 was built during the job before
+                        const bool tab = split && it == 0 && has && pre1;
                         if (split && it == 0) {
-                            // (the row in two halves of 8, each load in flight
-                            // over an expansion chunk: 32 VGPRs, not 64)
-                            typedef uint32_t v4u __attribute__((ext_vector_type(4)));  // (a uint4 array here went to scratch)
-                            const v4u* src = reinterpret_cast<const v4u*>(a.kw1) + 16ull * (tab ? ki : 0u);
-                            v4u* row1 = reinterpret_cast<v4u*>(&kw[(64 + lane) * kPcRow]);
-                            v4u k1[8];
-                            if (tab) {
-    #pragma unroll
-                                for (int q = 0; q < 8; ++q) k1[q] = src[q];
-                            }
                             uint32_t w[16];
     #pragma unroll
                             for (int q = 0; q < 16; ++q) w[q] = s_w0[lane * 17 + q];
-                            uint4* row0 = reinterpret_cast<uint4*>(&kw[lane * kPcRow]);
-                            kw_expand_chunk<false>(w, row0, 1);  // (K+W[16..31]: the chain's)
+                            uint4* row0 = reinterpret_cast<uint4*>(&kw[((xp & 1) * 64 + lane) * kPcRow]);
+                            kw_expand_chunk<false>(w, row0, 1);
                             kw_expand_chunk(w, row0, 2);
                             lds_publish(&s_split, 2 * sid + 1, lane);
-                            if (tab) {
-    #pragma unroll
-                                for (int q = 0; q < 8; ++q) row1[q] = k1[q];
-    #pragma unroll
-                                for (int q = 0; q < 8; ++q) k1[q] = src[8 + q];
-                            }
                             kw_expand_chunk(w, row0, 3);
                             lds_publish(&s_split, 2 * sid + 2, lane);
-                            if (tab) {
-    #pragma unroll
-                                for (int q = 0; q < 8; ++q) row1[8 + q] = k1[q];
-                                cur.skip(1, ring);  // (a longer target's block 2 on from the cursor, as after block 1)
-                            }
+                            if (tab) cur.skip(1, ring);  // (a longer target's block 2 on from the cursor)
                         }
                         if (pb < m0.y && !tab && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
                             uint32_t w[16];
@@ -1440,7 +1427,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             // (RF_K2_STAMPS=3: every block's assembly end on the producer)
                             if ((a.dbg_twice == 2 && it == 0) || a.dbg_twice == 8) { RF_STAMP_PL(sk); ++sk; }
                             if (kW == 2) {
-                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[((pb & 1) * 64 + lane) * kPcRow]));
+                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(((pb + xp) & 1) * 64 + lane) * kPcRow]));
                             } else {
                                 uint4* row = reinterpret_cast<uint4*>(&wbuf[((it & 1) * 64 + lane) * kWRow]);
     #pragma unroll
@@ -1459,7 +1446,6 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 nnm0 = a.meta[2ull * nm1.w];
                                 nnm1 = a.meta[2ull * nm1.w + 1];
                             }
-                            if (a.kw1) nki = a.kw1_idx[m1.w];
                         }
                         // idle in the last iteration (every block of the pass built):
                         // the fusion target's template blocks 0 and 1 into the ring,
@@ -1469,6 +1455,19 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             const uint4 b0[4] = {nt[0], nt[1], nt[2], nt[3]}, b1[4] = {nt[4], nt[5], nt[6], nt[7]};
                             ring_put(ring, 0, b0);
                             if (nm0.y > 1) ring_put(ring, 16, b1);
+                        }
+                        // split: the fusion target's block 1 (template only: its one
+                        // hole ends in block 0) into the buffer this pass's last
+                        // block leaves free -- the next pass's block-1 buffer
+                        if (build1 && it + 1 == iters) {
+                            pre1 = nfu && nm0.y >= 2;
+                            if (pre1) {
+                                uint32_t w[16] = {nt[4].x, nt[4].y, nt[4].z, nt[4].w, nt[5].x, nt[5].y, nt[5].z, nt[5].w,
+                                                  nt[6].x, nt[6].y, nt[6].z, nt[6].w, nt[7].x, nt[7].y, nt[7].z, nt[7].w};
+    #pragma unroll
+                                for (int q = 0; q < 16; ++q) w[q] = bswap32(w[q]);
+                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(((maxnb + xp) & 1) * 64 + lane) * kPcRow]));
+                            }
                         }
                     } else if (kIsExp) {
                         if (it >= 1 && it - 1 < m0.y && !((a.dbg_twice == 3 && it >= 2) || a.dbg_twice == 4)) {
@@ -1495,8 +1494,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         // barrier): the code is then cached when the links start.
                         const bool exb = it == 0 && (cb0 || (kCB && a.cb0 && pass == 0 && a.dbg_twice != 5));
                         if (exb) {
-                            uint4* row = reinterpret_cast<uint4*>(&kw[((cb0 ? 0u : 64u) + jl) * kPcRow]);
-                            if (!kStream && a.kw1)  // (pass 0: warms the code the split passes run)
+                            uint4* row = reinterpret_cast<uint4*>(&kw[((cb0 ? (xp & 1) * 64 : 64u) + jl) * kPcRow]);
+                            if (!kStream && a.split)  // (pass 0: warms the code the split passes run)
                                 chain_expand_b0<8>(wb0, elane, row);
                             else
                                 chain_expand_b0(wb0, elane, row);
@@ -1505,7 +1504,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         if (cb0 || it >= lag) {
                             const uint32_t cbk = cb0 ? it : it - lag;
                             spl0 = split && it == 0;
-                            chain_block(cbk, cbk, true);
+                            chain_block(cbk, cbk + xp, true);
                         }
                         if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
                     }
@@ -1528,7 +1527,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                      "v"(nnm0.z), "v"(nnm0.w), "v"(nnm1.x), "v"(nnm1.y), "v"(nnm1.z), "v"(nnm1.w),
                                      "v"(nm0.x), "v"(nm0.y), "v"(nm0.z), "v"(nm0.w));
                     __asm__ volatile("" ::"v"(nm1.x), "v"(nm1.y), "v"(nm1.z), "v"(nm1.w));
-                    chain_block(maxnb, kStream ? gb : maxnb, false);  // group 0 of block maxnb: the longest jobs' final value
+                    chain_block(maxnb, kStream ? gb : maxnb + xp, false);  // group 0 of block maxnb: the longest jobs' final value
                     // the a-lane's half (H0..H3) into its e-lane (H4..H7 there)
                     ShaState st;
                     st.h[0] = __builtin_amdgcn_mov_dpp((int)D0, 0x141, 0xf, 0xf, true);
@@ -1581,7 +1580,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     #pragma unroll
                         for (int q = 1; q < 8; ++q) wb0[q] = __builtin_amdgcn_alignbit(H[q - 1], H[q], 16);
                         wb0[8] |= H[7] << 16;
-                        if (!kStream && a.kw1 && elane)  // the next split pass's producer expands from these
+                        if (!kStream && a.split && elane)  // the next split pass's producer expands from these
     #pragma unroll
                             for (int q = 0; q < 16; ++q) s_w0[jl * 17 + q] = wb0[q];
                     }
@@ -1599,6 +1598,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 lds_barrier();
                 RF_STAMP_PL(sk); ++sk;
                 const uint32_t nx = s_next[jl];
+                // split: the next pass's block 1 sits in the buffer this pass's
+                // last block (maxnb - 1) left free, so its block b goes to
+                // buffer (b + xp') & 1 with (1 + xp') & 1 = (maxnb + xp) & 1
+                if (build1) xp = (maxnb + xp + 1) & 1;
                 maxnb = wave_max_small(s_nbx[lane]);
                 if (kChain) {
                     if (!(kCB && a.cb0) && !pp3) {
@@ -1634,24 +1637,6 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     if (a.stamps && blockIdx.x == 0 && (wave == 0 || wave == kProd))
         a.stamps[128 * a.lvl + 64 * (wave != 0) + lane] = s_stamp[wave != 0][lane];
     ws.end(a);
-}
-
-// Load time: block 1 of each listed job (a fusion target whose one hole lies
-// in block 0, so block 1 is template only) as its K+W row, for the split
-// block 0 of k2_level_pl.
-__global__ __launch_bounds__(256) void k2_kw1(const uint8_t* __restrict__ tmpl, const uint4* __restrict__ meta,
-                                              const uint32_t* __restrict__ jobs, uint32_t n, uint4* kw1) {
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const uint4 m0 = meta[2ull * jobs[k]];
-        const uint4* T = reinterpret_cast<const uint4*>(tmpl) + 4ull * m0.x + 4;  // block 1
-        uint32_t w[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 v = T[q];
-            w[4 * q] = bswap32(v.x); w[4 * q + 1] = bswap32(v.y); w[4 * q + 2] = bswap32(v.z); w[4 * q + 3] = bswap32(v.w);
-        }
-        kw_expand_store(w, kw1 + 16ull * k);
-    }
 }
 
 // Load time: the chaining value after each job's constant leading blocks.
@@ -2501,10 +2486,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
                 g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
                 full ? nullptr : g.wgst};
-    if (!full && a.cb0 == 2) {  // split block 0 (the precomputed block-1 rows)
-        a.kw1 = g.kw1;
-        a.kw1_idx = g.kw1_idx;
-    }
+    a.split = (!full && a.cb0 == 2 && g.split_b0) ? 1u : 0u;
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
@@ -2581,12 +2563,6 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);
     hipLaunchKernelGGL(k2_level, dim3(grid), dim3(kLevelBlock), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_graph_kw1(const GraphDev& g, const uint32_t* jobs, uint32_t n, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k2_kw1, dim3(grid_for(n, 16384)), dim3(256), 0, s, g.tmpl, g.meta, jobs, n, g.kw1);
     return hipGetLastError();
 }
 

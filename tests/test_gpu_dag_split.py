@@ -1,12 +1,15 @@
-"""GPU parity of split block 0 (k2_level_pl cb0 = 2 with GraphDev::kw1): in a
-fused link's chain pass, the producer expands the upper half of the fusion
-target's block-0 schedule (from the W words the chain stages) and drops in the
-target's precomputed block-1 row, while the chain runs the lower half.  The
-reference hashes the same bytes (flow.go:675-750 per node); only the order of
-work on the GPU changes, so the slot table must equal the oracle's and the
-table of the same graph loaded with the split off (RF_K2_SPLIT=0), slot for
-slot, step after step -- and a checkpoint restore rebuilds the rows
-(rf_graph_stats.split_rows) and keeps the same table."""
+"""GPU parity of split block 0 (k2_level_pl cb0 = 2, GraphDev::split_b0): in
+a fused link's chain pass the producer expands the upper half of the fusion
+target's block-0 schedule (from the W words the chain stages) while the chain
+runs the lower half, and the target's template-only block 1 was built by the
+producer during the job before it, into the row buffer that job's last block
+left free (the buffers' parity flips per pass).  Targets of 2 and 3 blocks
+(Dag1000's pair chain) both occur.  The reference hashes the same bytes
+(flow.go:675-750 per node); only the order of work on the GPU changes, so
+the slot table must equal the oracle's and the table of the same graph
+loaded with the split off (RF_K2_SPLIT=0), slot for slot, step after step --
+and a checkpoint restore keeps the split (rf_graph_stats.split_block0) and
+the same table."""
 import numpy as np
 import pytest
 
@@ -34,8 +37,8 @@ def test_split_block0_matches_unsplit_and_oracle(ctx, monkeypatch, tmp_path):
     monkeypatch.setenv("RF_K2_SPLIT", "0")
     gp = load(ctx, dag)
     monkeypatch.delenv("RF_K2_SPLIT")
-    assert g.stats().split_rows > 0  # Dag1000's fused links: one-hole targets, 2+ blocks
-    assert gp.stats().split_rows == 0
+    assert g.stats().split_block0 == 1  # Dag1000: every fusion target's hole at byte 2
+    assert gp.stats().split_block0 == 0
     for gg in (g, gp):
         gg.recompute(full=True)
     full = g.get_slots(every)
@@ -57,7 +60,7 @@ def test_split_block0_matches_unsplit_and_oracle(ctx, monkeypatch, tmp_path):
     path = str(tmp_path / "split.ckpt")
     g.save(path)
     r = capi.Graph.restore(ctx, path)
-    assert r.stats().split_rows == g.stats().split_rows
+    assert r.stats().split_block0 == 1
     slots, old, new = dag.change_set(0.01, seed=7)
     version = np.where((ids[slots] == new).all(axis=1)[:, None], old, new).astype(ids.dtype)
     for gg in (g, r):
