@@ -232,7 +232,8 @@ class GraphStats(ctypes.Structure):
                 ("template_bytes", ctypes.c_uint64), ("last_recomputed", ctypes.c_uint64),
                 ("last_ms", ctypes.c_float), ("last_levels_lf", ctypes.c_uint32),
                 ("last_mark_lf", ctypes.c_uint32), ("last_levels_oct", ctypes.c_uint32),
-                ("split_block0", ctypes.c_uint32)]
+                ("split_block0", ctypes.c_uint32),
+                ("last_sink_attach", ctypes.c_uint32)]
 
 
 _lib = None

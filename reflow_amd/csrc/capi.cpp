@@ -1693,6 +1693,18 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
                     const char* w = getenv("RF_K2_SINK_LAST");  // (round-4 scripts: =0 the fill level)
                     return v ? atoi(v) : (w && atoi(w) == 0) ? 0 : 2;
                 }();
+                // else an earlier latency-form level (from smin) whose chains
+                // leave CUs free -- its workgroups estimated from the step's
+                // marked slots (a bound on the chains reaching it): the sinks
+                // run there one per lane at the lowest priority (k2_level_pl
+                // sink lanes) and the fill level's chains keep their CUs
+                // (configs[2]: the Exec level, 220 workgroups on 256 CUs)
+                if (attach == ~0u && sink_at == 2)
+                    for (uint32_t l = smin; l <= fill && attach == ~0u; ++l)
+                        if ((G.inc_level[l] & kLvlForm) && !(G.inc_level[l] & kLvlOct) && !graph_level_lf(G, l)) {
+                            const uint64_t jobs = std::min<uint64_t>(G.lvl_start[l + 1] - G.lvl_start[l], G.step_marked);
+                            if ((jobs + 63) / 64 + 16 <= gr->ctx->n_cu) attach = l;
+                        }
                 if (attach == ~0u && sink_at == 1)
                     for (uint32_t l = sink; l-- > fill + 1 && attach == ~0u;)
                         if ((G.inc_level[l] & kLvlForm) && !(G.inc_level[l] & kLvlOct)) attach = l;
@@ -1711,6 +1723,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         // step (and set_slots / imports before it) uses that half
         bool first = true;
         if (lvl_lo == 0) G.last_levels_lf = G.last_levels_oct = 0;
+        G.last_sink_attach = attach;
         for (uint32_t l = lvl_lo; l < std::min(lvl_hi, G.n_levels); ++l) {
             if (!(G.inc_level[l] & kLvlForm) || (l == sink && attach != ~0u)) continue;
             HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr, l == attach ? sink : ~0u));
@@ -2025,6 +2038,7 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
     out->last_mark_lf = gr->g.last_mark_lf;
     out->last_levels_oct = gr->g.last_levels_oct;
     out->split_block0 = gr->g.split_b0 ? 1u : 0u;
+    out->last_sink_attach = gr->g.last_sink_attach;
     if (gr->timed) {
         HIPC(hipEventSynchronize(gr->e1));
         HIPC(hipEventElapsedTime(&out->last_ms, gr->e0, gr->e1));

@@ -77,6 +77,10 @@ struct LevelArgs {
     // its template-only block 1 during the job before it
     uint32_t split = 0;
     uint32_t oct_wg = 0;  // k2_level_oct: workgroups of the level's own list (the rest run the sink list)
+    // k2_level_pl: nonzero = workgroups from sink_wg on run the attached sink
+    // list one job per lane at the lowest priority (lf_job), the rest the
+    // level's own list
+    uint32_t sink_wg = 0;
 };
 
 // Entries of a level launch: the level's own list (from its end when rev),
@@ -1000,6 +1004,9 @@ __device__ __forceinline__ uint32_t wave_max_small(uint32_t x) {
     return __builtin_amdgcn_readfirstlane(m);
 }
 
+__device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii);
+__device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed);
+
 template <uint32_t kW, bool kStream>
 __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     static_assert(kW == 2 || kW == 3, "producer (+ expander)");
@@ -1021,6 +1028,27 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint32_t s_cw[2];                      // ... block id + 1 staged, per chain wave
     __shared__ uint32_t s_hq[64 * kHq];               // the producer's hole chunks (ChunkCursor)
     __shared__ unsigned long long s_stamp[2][64];
+    static_assert(64 * (kW + 1) * kRing <= (kBufs * 64 + 1) * kPcRow, "the sink lanes' rings live in kw");
+    if (a.sink_wg && blockIdx.x >= a.sink_wg) {
+        // the attached sink list, one short job per lane, below the chains'
+        // priority: these lanes fill the issue slots the latency form's
+        // waves leave idle instead of taking CUs from its workgroups
+        __builtin_amdgcn_s_setprio(0);
+        WgStamp ws;
+        ws.begin(a);
+        const LaunchList ll(a);
+        constexpr uint32_t nt = 64 * (kW + 1);
+        const uint32_t g2 = gridDim.x - a.sink_wg;
+        uint32_t hashed = 0;
+        for (uint32_t base = ll.n1 + (blockIdx.x - a.sink_wg) * nt; base < ll.n; base += g2 * nt) {
+            if (threadIdx.x == 0) ws.jobs += min(nt, ll.n - base);
+            const uint32_t i = base + threadIdx.x;
+            hashed += lf_job(a, &kw[threadIdx.x * kRing], i < ll.n ? ll.at(a, i) : ~0u);
+        }
+        count_fused(a, hashed);
+        ws.end(a);
+        return;
+    }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* ring = &ring_all[lane * kRing];
@@ -1063,7 +1091,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     WgStamp ws;
     ws.begin(a);
     const LaunchList ll(a);
-    const uint32_t n = ll.n;
+    const uint32_t n = a.sink_wg ? ll.n1 : ll.n;          // (sink lanes: the list's tail is theirs)
+    const uint32_t gstride = a.sink_wg ? a.sink_wg : gridDim.x;
     // One copy of the loop per wave role (chain / producer / expander), each
     // with only its own state: the register allocator then sizes the kernel
     // for the largest role instead of the sum of all roles' live values, and
@@ -1074,7 +1103,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         constexpr bool kChain = R < 2, kIsProd = R == kProd, kIsExp = R == kExp;
         // split passes so far (every role counts them alike: the flag values)
         uint32_t sid = 0, known_sp = 0;
-        for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+        for (uint32_t base = blockIdx.x * 64; base < n; base += gstride * 64) {
             if (threadIdx.x == 0) ws.jobs += min(64u, n - base);
             const uint32_t i = base + jl;
             bool has = i < n;
@@ -1413,13 +1442,21 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             uint32_t w[16];
     #pragma unroll
                             for (int q = 0; q < 16; ++q) w[q] = s_w0[lane * 17 + q];
+                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                             uint4* row0 = reinterpret_cast<uint4*>(&kw[((xp & 1) * 64 + lane) * kPcRow]);
                             kw_expand_chunk<false>(w, row0, 1);
                             kw_expand_chunk(w, row0, 2);
                             lds_publish(&s_split, 2 * sid + 1, lane);
+                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                             kw_expand_chunk(w, row0, 3);
                             lds_publish(&s_split, 2 * sid + 2, lane);
+                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                             if (tab) cur.skip(1, ring);  // (a longer target's block 2 on from the cursor)
+                            // the last pass's frontier atomics here, where the chain's
+                            // rounds of block 0 leave the producer time, not in the
+                            // last iteration, which builds the next block 1
+                            if (pend) producer_propagate();
+                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                         }
                         if (pb < m0.y && !tab && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
                             uint32_t w[16];
@@ -2549,7 +2586,21 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             uint64_t lg = (e - b + n2 + kLevelBlock - 1) / kLevelBlock;
             if (lg > lf_cap) lg = lf_cap;
             hipLaunchKernelGGL(k2_level_lf, dim3((uint32_t)lg), dim3(kLevelBlock), 0, s, a);
-        } else if (one_lane && wide)
+            return hipGetLastError();
+        }
+        // the latency form with an attached sink list: the level's own list
+        // in its workgroups, the sinks one per lane in low-priority
+        // workgroups after them (RF_K2_SINK_LANES=0: sinks as listed jobs, A/B)
+        static const bool sink_lanes = [] {
+            const char* v = getenv("RF_K2_SINK_LANES");
+            return !(v && atoi(v) == 0);
+        }();
+        if (!one_lane && sink_lvl != ~0u && sink_lanes) {
+            const uint32_t nt = wide ? 256u : 192u;
+            a.sink_wg = (uint32_t)std::min<uint64_t>((e - b + 63) / 64, wg_cap);
+            wg = a.sink_wg + std::min<uint64_t>((n2 + nt - 1) / nt, 1024u);
+        }
+        if (one_lane && wide)
             hipLaunchKernelGGL(k2_level_pc<3>, dim3((uint32_t)wg), dim3(192), pad, s, a);
         else if (one_lane)
             hipLaunchKernelGGL(k2_level_pc<2>, dim3((uint32_t)wg), dim3(128), pad, s, a);
