@@ -383,7 +383,7 @@ typedef struct {
     uint32_t last_levels_lf;  /* levels the last plain incremental step ran in the throughput form */
     uint32_t last_mark_lf;    /* the last set_slots batch marked in the throughput form (0/1) */
     uint32_t last_levels_oct; /* levels the last plain incremental step ran in the octo form */
-    uint32_t split_block0;    /* 1: fused links split block 0's schedule over chain and producer (RF_K2_SPLIT) */
+    uint32_t split_block0;    /* fused links split block 0's schedule over chain and producer: 0 off, 1 / 2 (RF_K2_SPLIT) */
     uint32_t last_sink_attach; /* level whose launch ran the sink list in the last plain step (UINT32_MAX: none) */
 } rf_graph_stats;
 int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);

@@ -1521,7 +1521,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     }
     // split block 0: every fusion target's one hole at byte 2 (fuse_pos2),
     // so its block 1 is template only
-    G.split_b0 = G.hole_in_b0 && G.fuse_pos2 && graph_split_on();
+    G.split_b0 = G.hole_in_b0 && G.fuse_pos2 ? graph_split_on() : 0u;
     if (getenv("RF_K2_STAMPS")) {  // diagnostic: per-phase times of workgroup 0 of each level
         HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
@@ -1604,11 +1604,13 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
 // block, memory-latency-bound, against the three-wave latency form's ~1.5).
 static constexpr uint64_t kThruSlots = RF_K2_THRU_DEFAULT, kThruSlotsWide = RF_K2_THRU_WIDE_DEFAULT;
 
-// Split block 0 of the fused links (k2_level_pl cb0 = 2): on unless
-// RF_K2_SPLIT=0 (A/B; read at load and restore, never per step).
-bool graph_split_on() {
+// Split block 0 of the fused links (k2_level_pl cb0 = 2): RF_K2_SPLIT = 0
+// off, 1 the producer expands K+W[32..63], 2 (default) K+W[16..63] (A/B;
+// read at load and restore, never per step).
+uint32_t graph_split_on() {
     const char* v = getenv("RF_K2_SPLIT");
-    return !(v && atoi(v) == 0);
+    const int m = v ? atoi(v) : 2;
+    return m < 0 ? 0u : m > 2 ? 2u : (uint32_t)m;
 }
 
 // The form thresholds of a graph being loaded or restored: the defaults, or
@@ -2037,7 +2039,7 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
     out->last_levels_lf = gr->g.last_levels_lf;
     out->last_mark_lf = gr->g.last_mark_lf;
     out->last_levels_oct = gr->g.last_levels_oct;
-    out->split_block0 = gr->g.split_b0 ? 1u : 0u;
+    out->split_block0 = gr->g.split_b0;
     out->last_sink_attach = gr->g.last_sink_attach;
     if (gr->timed) {
         HIPC(hipEventSynchronize(gr->e1));

@@ -145,7 +145,7 @@ struct GraphDev {
     // split block 0 (k2_level_pl cb0 = 2): the producer expands the upper
     // half of a fusion target's block 0 and builds its template-only block 1
     // during the job before it; set at load / restore (RF_K2_SPLIT=0: off)
-    bool split_b0 = false;
+    uint32_t split_b0 = 0;  // 1: the producer expands K+W[32..63]; 2: K+W[16..63]
 };
 // Midstates of the jobs' leading constant blocks, hashed once at load: job i
 // (internal order) hashes lead[i] blocks of its template from block

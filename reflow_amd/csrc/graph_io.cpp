@@ -366,7 +366,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
         if (i >= h.n_jobs || out_slot[i] >= h.n_slots) return fail(RF_EINTEGRITY, "graph restore: bad job record");
         gr->producer[out_slot[i]] = j;
     }
-    G.split_b0 = G.hole_in_b0 && G.fuse_pos2 && graph_split_on();  // (as rf_graph_load)
+    G.split_b0 = G.hole_in_b0 && G.fuse_pos2 ? graph_split_on() : 0u;  // (as rf_graph_load)
     gr->initialized = (h.flags & kInitialized) != 0;
     guard.release();
     *out = gr;

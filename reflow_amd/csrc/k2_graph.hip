@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint4 s_pp[64][2];   // cb0: a finished job's {id, consumer range, valid}, first two edges
     // W[0..15] per job, staged by the chain: stream cb0, and the split block 0
     __shared__ uint32_t s_w0[kW == 2 ? 64 * 17 : 1];
-    __shared__ uint32_t s_split;  // split block 0: 2 sid + 1 / + 2 once K+W[32..47] / [48..63] are in
+    __shared__ uint32_t s_split;  // split block 0: (split + 1) sid + c once the producer's c-th chunk is in
     __shared__ uint32_t s_cw[2];                      // ... block id + 1 staged, per chain wave
     __shared__ uint32_t s_hq[64 * kHq];               // the producer's hole chunks (ChunkCursor)
     __shared__ unsigned long long s_stamp[2][64];
@@ -1320,8 +1320,11 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             known = lds_poll(&s_flag[bi], 4 * bufb + (g + 2) / 4 + 1, known);
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                         }
-                        if (!kStream && spl0 && (g == 6 || g == 10))  // split block 0: the producer's chunks 2, 3
-                            known_sp = lds_poll(&s_split, 2 * sid + (g == 6 ? 1u : 2u), known_sp);
+                        // split block 0: r4[g + 2] opens the producer's chunk (g + 2) / 4
+                        // (split 1: chunks 2, 3; split 2: chunks 1-3)
+                        if (!kStream && spl0 && (g == 6 || g == 10 || (g == 2 && a.split == 2)))
+                            known_sp = lds_poll(&s_split, (a.split + 1) * sid + (g + 2) / 4 - (a.split == 2 ? 0u : 1u),
+                                                known_sp);
                         if (g < 14) vnn = r4[g + 2];
                         const uint32_t k4 = g == 15 ? c63 : vn.x;
                         asm volatile(RF_L2_GROUP : RF_LAG_STATE, RF_L2_TMP : RF_L2_IN(v.y, v.z, v.w, k4));
@@ -1444,12 +1447,20 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             for (int q = 0; q < 16; ++q) w[q] = s_w0[lane * 17 + q];
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                             uint4* row0 = reinterpret_cast<uint4*>(&kw[((xp & 1) * 64 + lane) * kPcRow]);
-                            kw_expand_chunk<false>(w, row0, 1);
-                            kw_expand_chunk(w, row0, 2);
-                            lds_publish(&s_split, 2 * sid + 1, lane);
+                            const uint32_t fb = (a.split + 1) * sid;  // this pass's flag values: fb + 1 ..
+                            if (a.split == 2) {  // chunks 1-3 (the chain wrote chunk 0 only)
+                                kw_expand_chunk(w, row0, 1);
+                                lds_publish(&s_split, fb + 1, lane);
+                                kw_expand_chunk(w, row0, 2);
+                                lds_publish(&s_split, fb + 2, lane);
+                            } else {  // chunks 2, 3 (chunk 1 only rolls the window)
+                                kw_expand_chunk<false>(w, row0, 1);
+                                kw_expand_chunk(w, row0, 2);
+                                lds_publish(&s_split, fb + 1, lane);
+                            }
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                             kw_expand_chunk(w, row0, 3);
-                            lds_publish(&s_split, 2 * sid + 2, lane);
+                            lds_publish(&s_split, fb + a.split + 1, lane);
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
                             if (tab) cur.skip(1, ring);  // (a longer target's block 2 on from the cursor)
                             // the last pass's frontier atomics here, where the chain's
@@ -1532,7 +1543,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         const bool exb = it == 0 && (cb0 || (kCB && a.cb0 && pass == 0 && a.dbg_twice != 5));
                         if (exb) {
                             uint4* row = reinterpret_cast<uint4*>(&kw[((cb0 ? (xp & 1) * 64 : 64u) + jl) * kPcRow]);
-                            if (!kStream && a.split)  // (pass 0: warms the code the split passes run)
+                            if (!kStream && a.split == 2)  // (pass 0: warms the code the split passes run)
+                                chain_expand_b0<4>(wb0, elane, row);
+                            else if (!kStream && a.split)
                                 chain_expand_b0<8>(wb0, elane, row);
                             else
                                 chain_expand_b0(wb0, elane, row);
@@ -2523,7 +2536,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
                 g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
                 full ? nullptr : g.wgst};
-    a.split = (!full && a.cb0 == 2 && g.split_b0) ? 1u : 0u;
+    a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {

@@ -28,16 +28,20 @@ def ctx():
     c.close()
 
 
-def test_split_block0_matches_unsplit_and_oracle(ctx, monkeypatch, tmp_path):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_split_block0_matches_unsplit_and_oracle(ctx, monkeypatch, tmp_path, mode):
+    """mode 1: the producer expands K+W[32..63] of block 0; 2 (default):
+    K+W[16..63], the chain writes K+W[0..15] only."""
     from reflow_amd import capi
     dag = Dag1000(400, 32)
     a = dag.arrays()
     every = np.arange(a["n_slots"], dtype=np.uint32)
+    monkeypatch.setenv("RF_K2_SPLIT", str(mode))
     g = load(ctx, dag)
     monkeypatch.setenv("RF_K2_SPLIT", "0")
     gp = load(ctx, dag)
-    monkeypatch.delenv("RF_K2_SPLIT")
-    assert g.stats().split_block0 == 1  # Dag1000: every fusion target's hole at byte 2
+    monkeypatch.setenv("RF_K2_SPLIT", str(mode))  # (the restore below reads it too)
+    assert g.stats().split_block0 == mode  # Dag1000: every fusion target's hole at byte 2
     assert gp.stats().split_block0 == 0
     for gg in (g, gp):
         gg.recompute(full=True)
@@ -60,7 +64,7 @@ def test_split_block0_matches_unsplit_and_oracle(ctx, monkeypatch, tmp_path):
     path = str(tmp_path / "split.ckpt")
     g.save(path)
     r = capi.Graph.restore(ctx, path)
-    assert r.stats().split_block0 == 1
+    assert r.stats().split_block0 == mode
     slots, old, new = dag.change_set(0.01, seed=7)
     version = np.where((ids[slots] == new).all(axis=1)[:, None], old, new).astype(ids.dtype)
     for gg in (g, r):
