@@ -1495,6 +1495,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         G.stream_handover = v && atoi(v) == 1;
     }
     graph_forms_from_env(G);
+    G.n_cu = graph_ovf_cus(ctx, &G.ovf_mode);
     if (n_lead && !getenv("RF_K2_NO_MIDSTATE")) {  // (RF_K2_NO_MIDSTATE: A/B)
         struct Tmp {
             DevBuf b;
@@ -1603,6 +1604,17 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
 // of long jobs (inc_level 2: a lane alone hashes an 18-block job at ~5 us a
 // block, memory-latency-bound, against the three-wave latency form's ~1.5).
 static constexpr uint64_t kThruSlots = RF_K2_THRU_DEFAULT, kThruSlotsWide = RF_K2_THRU_WIDE_DEFAULT;
+
+// The CU count the latency form's overflow lanes size for (k2_level_pl
+// ovf): the device's, or RF_K2_OVF_CU (tests: a small graph's levels
+// overflow a pretended 4-CU chip); and their mode, RF_K2_OVF (0 off, 1 on,
+// 2 at the chains' wave priority).  Read at load / restore.
+uint32_t graph_ovf_cus(const rf_ctx* ctx, uint32_t* mode) {
+    const char* m = getenv("RF_K2_OVF");
+    *mode = m ? (uint32_t)std::min(std::max(atoi(m), 0), 2) : 1u;
+    const char* v = getenv("RF_K2_OVF_CU");
+    return v && atoi(v) > 0 ? (uint32_t)atoi(v) : (uint32_t)ctx->n_cu;
+}
 
 // Split block 0 of the fused links (k2_level_pl cb0 = 2): RF_K2_SPLIT = 0
 // off, 1 the producer expands K+W[32..63], 2 (default) K+W[16..63] (A/B;

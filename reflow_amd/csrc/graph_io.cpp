@@ -307,6 +307,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
         G.stream_handover = v && atoi(v) == 1;
     }
     graph_forms_from_env(G);
+    G.n_cu = graph_ovf_cus(ctx, &G.ovf_mode);
     if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes)) return rc;
     const bool has_mid = (h.flags & kHasMid) != 0;
     if (has_mid) {

@@ -79,8 +79,10 @@ struct LevelArgs {
     uint32_t oct_wg = 0;  // k2_level_oct: workgroups of the level's own list (the rest run the sink list)
     // k2_level_pl: nonzero = workgroups from sink_wg on run the attached sink
     // list one job per lane at the lowest priority (lf_job), the rest the
-    // level's own list
-    uint32_t sink_wg = 0;
+    // level's own list; ovf = 1: the own list only up to sink_wg x 64 jobs
+    // (one batch per latency-form workgroup, one per CU), its overflow one
+    // chain per lane in those lane workgroups too, before the sinks
+    uint32_t sink_wg = 0, ovf = 0;
 };
 
 // Entries of a level launch: the level's own list (from its end when rev),
@@ -1030,17 +1032,20 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ unsigned long long s_stamp[2][64];
     static_assert(64 * (kW + 1) * kRing <= (kBufs * 64 + 1) * kPcRow, "the sink lanes' rings live in kw");
     if (a.sink_wg && blockIdx.x >= a.sink_wg) {
-        // the attached sink list, one short job per lane, below the chains'
-        // priority: these lanes fill the issue slots the latency form's
-        // waves leave idle instead of taking CUs from its workgroups
-        __builtin_amdgcn_s_setprio(0);
+        // the attached sink list (and with ovf the own list's overflow), one
+        // job per lane, below the chains' priority: these lanes fill the
+        // issue slots the latency form's waves leave idle instead of taking
+        // CUs from its workgroups
+        // (RF_K2_OVF=2: overflow lanes at the chains' priority, A/B)
+        if (a.ovf == 2) __builtin_amdgcn_s_setprio(3);
         WgStamp ws;
         ws.begin(a);
         const LaunchList ll(a);
         constexpr uint32_t nt = 64 * (kW + 1);
         const uint32_t g2 = gridDim.x - a.sink_wg;
+        const uint32_t lo = a.ovf ? min(ll.n1, a.sink_wg * 64) : ll.n1;
         uint32_t hashed = 0;
-        for (uint32_t base = ll.n1 + (blockIdx.x - a.sink_wg) * nt; base < ll.n; base += g2 * nt) {
+        for (uint32_t base = lo + (blockIdx.x - a.sink_wg) * nt; base < ll.n; base += g2 * nt) {
             if (threadIdx.x == 0) ws.jobs += min(nt, ll.n - base);
             const uint32_t i = base + threadIdx.x;
             hashed += lf_job(a, &kw[threadIdx.x * kRing], i < ll.n ? ll.at(a, i) : ~0u);
@@ -1091,7 +1096,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     WgStamp ws;
     ws.begin(a);
     const LaunchList ll(a);
-    const uint32_t n = a.sink_wg ? ll.n1 : ll.n;          // (sink lanes: the list's tail is theirs)
+    // (lane workgroups: the list's tail is theirs)
+    const uint32_t n = !a.sink_wg ? ll.n : a.ovf ? min(ll.n1, a.sink_wg * 64) : ll.n1;
     const uint32_t gstride = a.sink_wg ? a.sink_wg : gridDim.x;
     // One copy of the loop per wave role (chain / producer / expander), each
     // with only its own state: the register allocator then sizes the kernel
@@ -2608,8 +2614,22 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             const char* v = getenv("RF_K2_SINK_LANES");
             return !(v && atoi(v) == 0);
         }();
-        if (!one_lane && sink_lvl != ~0u && sink_lanes) {
-            const uint32_t nt = wide ? 256u : 192u;
+        // the overflow of a latency-form level a little wider than the chip
+        // (estimated from the step's marked slots: more than one 64-job
+        // workgroup per CU) -- one workgroup per CU takes 64 chains, the rest
+        // run one per lane in workgroups after them, instead of a second
+        // workgroup on a few CUs whose chain waves then share SIMDs (the
+        // 8-rank piece's Exec level: 274 workgroups, 18 CUs doubled, 104 us
+        // against 77 alone).  RF_K2_OVF=0: off (A/B), 2: the lanes at the
+        // chains' priority.
+        const uint32_t ovf_lanes = g.ovf_mode;  // (RF_K2_OVF, read at load)
+        const uint32_t nt = wide ? 256u : 192u;
+        const uint64_t est = std::min<uint64_t>(e - b, g.step_marked);
+        if (!one_lane && ovf_lanes && g.n_cu && est > 64ull * g.n_cu) {
+            a.sink_wg = g.n_cu;
+            a.ovf = ovf_lanes;
+            wg = a.sink_wg + std::min<uint64_t>((e - b - 64ull * g.n_cu + n2 + nt - 1) / nt, 1024u);
+        } else if (!one_lane && sink_lvl != ~0u && sink_lanes) {
             a.sink_wg = (uint32_t)std::min<uint64_t>((e - b + 63) / 64, wg_cap);
             wg = a.sink_wg + std::min<uint64_t>((n2 + nt - 1) / nt, 1024u);
         }
