@@ -1611,7 +1611,7 @@ static constexpr uint64_t kThruSlots = RF_K2_THRU_DEFAULT, kThruSlotsWide = RF_K
 // 2 at the chains' wave priority).  Read at load / restore.
 uint32_t graph_ovf_cus(const rf_ctx* ctx, uint32_t* mode) {
     const char* m = getenv("RF_K2_OVF");
-    *mode = m ? (uint32_t)std::min(std::max(atoi(m), 0), 2) : 1u;
+    *mode = m ? (uint32_t)std::min(std::max(atoi(m), 0), 2) : 0u;  // (off by default: see DESIGN.md §5)
     const char* v = getenv("RF_K2_OVF_CU");
     return v && atoi(v) > 0 ? (uint32_t)atoi(v) : (uint32_t)ctx->n_cu;
 }

@@ -129,7 +129,7 @@ struct GraphDev {
     // the other bound (merge-tree levels stay in the latency form)
     uint64_t step_marked = 0, thru_slots = ~0ull, thru_slots_wide = ~0ull;  // (wide: inc_level 2)
     uint32_t n_cu = 0;      // the device's CUs (latency-form overflow lanes, k2_level_pl)
-    uint32_t ovf_mode = 1;  // overflow lanes: 0 off, 1 on, 2 at the chains' priority (RF_K2_OVF, at load)
+    uint32_t ovf_mode = 0;  // overflow lanes: 0 off, 1 on, 2 at the chains' priority (RF_K2_OVF, at load)
     // The thresholds themselves, fixed per graph: defaults (or RF_K2_THRU /
     // RF_K2_THRU_WIDE read once when the graph is loaded or restored), or
     // rf_graph_set_forms; cfg_thru_mark: the mark kernel's lean form
