@@ -16,7 +16,7 @@ if [ "$2" = A ]; then
     step bench && RF_LOWER_TIMING=1 timeout -k 10 700 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.log &&
     tail -6 $out/bench.log
 else
-    step trace && timeout -k 10 800 rocprofv3 --kernel-trace --stats -d $out/trace -o bench -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $out/trace_bench.json 2> $out/trace_bench.log &&
+    step trace && timeout -k 10 800 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o bench -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $out/trace_bench.json 2> $out/trace_bench.log &&
     step forms100m && timeout -k 10 300 python -u tools/dag_forms.py --c4-ranks 1 --steps 10 > $out/f100m_new.json 2> $out/f100m_new.log &&
     RF_K2_OCT=0 timeout -k 10 300 python -u tools/dag_forms.py --c4-ranks 1 --steps 10 > $out/f100m_nooct.json 2> $out/f100m_nooct.log &&
     grep auto $out/f100m_*.log
