@@ -83,6 +83,7 @@ struct LevelArgs {
     // (one batch per latency-form workgroup, one per CU), its overflow one
     // chain per lane in those lane workgroups too, before the sinks
     uint32_t sink_wg = 0, ovf = 0;
+    uint32_t handoff = 1;  // k2_level_pl cb0 = 2: the producer hands the chain its next target's operands
 };
 
 // Entries of a level launch: the level's own list (from its end when rev),
@@ -1024,6 +1025,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint32_t s_flag[3], s_cons[2];
     __shared__ uint32_t s_nbx[64];  // fused targets' block counts (the next iteration's max)
     __shared__ uint4 s_pp[64][2];   // cb0: a finished job's {id, consumer range, valid}, first two edges
+    __shared__ uint4 s_nnm[64][2];  // cb0 = 2: the fusion target's own target's record, from the producer
     // W[0..15] per job, staged by the chain: stream cb0, and the split block 0
     __shared__ uint32_t s_w0[kW == 2 ? 64 * 17 : 1];
     __shared__ uint32_t s_split;  // split block 0: (split + 1) sid + c once the producer's c-th chunk is in
@@ -1146,13 +1148,21 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             constexpr bool kCB = kW == 2 && !kStream;
             uint32_t pass = 0;
             bool pend = false;  // (producer) s_pp holds the last finished jobs, not yet propagated
+            // cb0 = 2: the chain fetches only the fusion target's old digest;
+            // its template (the producer's ring), its target's record (s_nnm)
+            // and the reverse edges the producer propagates come from the
+            // producer, and its start state is the IV (its hole is at byte 2:
+            // no constant leading block)
+            const bool handoff = kCB && a.cb0 == 2 && a.handoff;
+            uint2 ppe[2] = {make_uint2(0, 0), make_uint2(0, 0)}, pe_pend[2] = {ppe[0], ppe[1]};
             // cb0: the frontier atomics of a finished job run on the producer
             // (idle in a pass's last iteration), not on the chain's critical path
             auto producer_propagate = [&]() {
                 const uint4 q = s_pp[lane][0], e = s_pp[lane][1];
                 const bool v = q.w != 0;
                 if (v) a.dirty[q.x] = 0u;
-                const uint2 pe[2] = {make_uint2(e.x, e.y), make_uint2(e.z, e.w)};
+                const uint2 pe[2] = {handoff ? pe_pend[0] : make_uint2(e.x, e.y),
+                                     handoff ? pe_pend[1] : make_uint2(e.z, e.w)};
                 propagate_pre(a, v ? q.y : 0u, v ? q.z : 0u, pe);
                 pend = false;
             };
@@ -1235,8 +1245,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
                         olo = od[0];
                         ohi = od[1];
-                        if (m1.y < m1.z) pre[0] = a.cons[m1.y];
-                        if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+                        if (!handoff && m1.y < m1.z) pre[0] = a.cons[m1.y];  // (handoff: the producer's)
+                        if (!handoff && m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
                         if (a.mid) {
                             hlo = a.mid[2ull * p];
                             hhi = a.mid[2ull * p + 1];
@@ -1270,6 +1280,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
                     nolo = od[0];
                     nohi = od[1];
+                }
+                if (kChain && has && nfu && !handoff) {
                     if (kW == 2) {
                         nrc = a.holes[nm0.z];
                         if (a.cb0 == 2) {
@@ -1501,6 +1513,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 nnm1 = a.meta[2ull * nm1.w + 1];
                             }
                         }
+                        if (handoff && it == 0 && has) {  // this job's first two reverse edges (propagated next pass)
+                            ppe[0] = m1.y < m1.z ? a.cons[m1.y] : make_uint2(0, 0);
+                            ppe[1] = m1.y + 1 < m1.z ? a.cons[m1.y + 1] : make_uint2(0, 0);
+                        }
                         // idle in the last iteration (every block of the pass built):
                         // the fusion target's template blocks 0 and 1 into the ring,
                         // for the chain to OR the digest into at the hand-over
@@ -1509,6 +1525,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             const uint4 b0[4] = {nt[0], nt[1], nt[2], nt[3]}, b1[4] = {nt[4], nt[5], nt[6], nt[7]};
                             ring_put(ring, 0, b0);
                             if (nm0.y > 1) ring_put(ring, 16, b1);
+                            if (handoff) {
+                                s_nnm[lane][0] = nnm0;
+                                s_nnm[lane][1] = nnm1;
+                            }
                         }
                         // split: the fusion target's block 1 (template only: its one
                         // hole ends in block 0) into the buffer this pass's last
@@ -1627,11 +1647,18 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         H[5] = __builtin_amdgcn_bitop3_b32(E, D1, st.h[1], 0xCA);
                         H[6] = __builtin_amdgcn_bitop3_b32(E, D2, st.h[2], 0xCA);
                         H[7] = __builtin_amdgcn_bitop3_b32(E, D3, st.h[3], 0xCA);
-                        const uint32_t T[16] = {ntc[0].x, ntc[0].y, ntc[0].z, ntc[0].w, ntc[1].x, ntc[1].y,
-                                                ntc[1].z, ntc[1].w, ntc[2].x, ntc[2].y, ntc[2].z, ntc[2].w,
-                                                ntc[3].x, ntc[3].y, ntc[3].z, ntc[3].w};
+                        if (handoff) {  // the target's template block 0, in the producer's ring
     #pragma unroll
-                        for (int q = 0; q < 16; ++q) wb0[q] = bswap32(T[q]);
+                            for (int q = 0; q < 16; ++q) wb0[q] = bswap32(ring_all[jl * kRing + q]);
+                            nnm0 = s_nnm[jl][0];
+                            nnm1 = s_nnm[jl][1];
+                        } else {
+                            const uint32_t T[16] = {ntc[0].x, ntc[0].y, ntc[0].z, ntc[0].w, ntc[1].x, ntc[1].y,
+                                                    ntc[1].z, ntc[1].w, ntc[2].x, ntc[2].y, ntc[2].z, ntc[2].w,
+                                                    ntc[3].x, ntc[3].y, ntc[3].z, ntc[3].w};
+    #pragma unroll
+                            for (int q = 0; q < 16; ++q) wb0[q] = bswap32(T[q]);
+                        }
                         wb0[0] |= H[0] >> 16;
     #pragma unroll
                         for (int q = 1; q < 8; ++q) wb0[q] = __builtin_amdgcn_alignbit(H[q - 1], H[q], 16);
@@ -1646,7 +1673,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         if ((kCB && a.cb0) || pp3) {
                             s_pp[jl][0] = make_uint4(p, m1.y, !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z),
                                                      own ? 1u : 0u);
-                            s_pp[jl][1] = make_uint4(pre[0].x, pre[0].y, pre[1].x, pre[1].y);
+                            if (!handoff) s_pp[jl][1] = make_uint4(pre[0].x, pre[0].y, pre[1].x, pre[1].y);
                         }
                     }
                 }
@@ -1673,6 +1700,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
                 }
                 if (kIsProd && ((kCB && a.cb0) || pp3)) pend = true;
+                if (kIsProd && handoff) {
+                    pe_pend[0] = ppe[0];
+                    pe_pend[1] = ppe[1];
+                }
                 fslot = has ? m1.x : ~0u;
                 has = nx != ~0u;
                 p = has ? nx : 0u;
@@ -2543,6 +2574,11 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                 g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
                 full ? nullptr : g.wgst};
     a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
+    static const uint32_t handoff = [] {  // RF_K2_HANDOFF=0: the chain fetches them itself (A/B)
+        const char* v = getenv("RF_K2_HANDOFF");
+        return (v && atoi(v) == 0) ? 0u : 1u;
+    }();
+    a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
     static const uint32_t inc_cap = [] {
