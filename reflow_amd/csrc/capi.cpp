@@ -1630,6 +1630,11 @@ uint32_t graph_split_on() {
 // here once, never per step (a libc call per step, and racy against setenv
 // in threaded callers).  rf_graph_set_forms changes them later.
 void graph_forms_from_env(GraphDev& G) {
+    {
+        const char* v = getenv("RF_K2_SINK_AT");
+        const char* w = getenv("RF_K2_SINK_LAST");  // (round-4 scripts: =0 the fill level)
+        G.sink_at = v ? (uint32_t)std::min(std::max(atoi(v), 0), 3) : (w && atoi(w) == 0) ? 0u : 2u;
+    }
     const char* tv = getenv("RF_K2_THRU");
     const char* tw = getenv("RF_K2_THRU_WIDE");
     G.cfg_thru = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;
@@ -1700,13 +1705,11 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
                 // piece's OpK level: 67 us, its chains alone ~50) -- the one
                 // with the most jobs, so the sinks run beside its longest
                 // stretch of work (octo-form levels take the list in
-                // workgroups of their own).  RF_K2_SINK_AT (A/B, read once):
-                // 0 = the fill level, 1 = the last latency-form level above it
-                static const int sink_at = [] {
-                    const char* v = getenv("RF_K2_SINK_AT");
-                    const char* w = getenv("RF_K2_SINK_LAST");  // (round-4 scripts: =0 the fill level)
-                    return v ? atoi(v) : (w && atoi(w) == 0) ? 0 : 2;
-                }();
+                // workgroups of their own).  GraphDev::sink_at (RF_K2_SINK_AT,
+                // read at load): 0 = the fill level, 1 = the last latency-form
+                // level above it, 3 = above the fill level without the
+                // spare-CU rule below (A/B and tests), 2 = all of these
+                const uint32_t sink_at = G.sink_at;
                 // else an earlier latency-form level (from smin) whose chains
                 // leave CUs free -- its workgroups estimated from the step's
                 // marked slots (a bound on the chains reaching it): the sinks
@@ -1722,7 +1725,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
                 if (attach == ~0u && sink_at == 1)
                     for (uint32_t l = sink; l-- > fill + 1 && attach == ~0u;)
                         if ((G.inc_level[l] & kLvlForm) && !(G.inc_level[l] & kLvlOct)) attach = l;
-                if (attach == ~0u && sink_at == 2) {
+                if (attach == ~0u && (sink_at == 2 || sink_at == 3)) {
                     uint32_t most = 0;
                     for (uint32_t l = fill + 1; l < sink; ++l)
                         if ((G.inc_level[l] & kLvlForm) && G.lvl_start[l + 1] - G.lvl_start[l] > most) {

@@ -138,6 +138,7 @@ struct GraphDev {
     // what the last plain step / mark launch chose (rf_graph_stats)
     uint32_t last_levels_lf = 0, last_mark_lf = 0, last_levels_oct = 0;
     uint32_t last_sink_attach = ~0u;  // the level whose launch took the sink list last step (~0u: none)
+    uint32_t sink_at = 2;             // where the sink list may run (RF_K2_SINK_AT at load; graph_enqueue)
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     unsigned long long* wgst = nullptr;    // diagnostic per-workgroup records [L][2048][4] (RF_K2_WGSTAMPS)
     // [2J] each job's initial chaining value (IV, or the midstate after the

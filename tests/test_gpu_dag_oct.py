@@ -135,3 +135,49 @@ def test_oct_merge_tree(ctx, monkeypatch, nparts):
         assert (table == gp.get_slots(every)).all()
     g.close()
     gp.close()
+
+
+@pytest.mark.parametrize("sink_at", ["0", "2", "3"])
+def test_sink_list_placements(ctx, monkeypatch, sink_at):
+    """Where the sink list (physical cache keys whose inputs are final by
+    the fill level) runs: 0 the fill level's launch (round 3), 2 the default
+    (a latency-form level with CUs to spare, its sinks in low-priority lane
+    workgroups), 3 the merge level with the most jobs (its octo launch takes
+    the sinks in lane workgroups after its own).  Every placement gives the
+    oracle's table and the table of the fill-level placement, slot for slot;
+    the level is read back from rf_graph_stats.last_sink_attach."""
+    from reflow_amd import capi
+    pc = PartitionedDag1000(130, 2, 1, 0, nparts=2)
+    a = pc.desc
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+
+    def load(mode):
+        monkeypatch.setenv("RF_K2_SINK_AT", mode)
+        gg = capi.Graph.from_arrays(ctx, a)
+        monkeypatch.delenv("RF_K2_SINK_AT")
+        gg.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
+        gg.recompute(full=True)
+        return gg
+
+    g, g0 = load(sink_at), load("0")
+    ids = pc.dag.leaf_ids.copy()
+    attach = set()
+    for frac, seed in ((0.01, 1), (0.3, 2), (0.05, 3)):
+        slots, old, new = pc.dag.change_set(frac, seed=seed)
+        version = np.where((ids[slots] == new).all(axis=1)[:, None], old, new).astype(ids.dtype)
+        for gg in (g, g0):
+            gg.set_slots(slots, version)
+            gg.recompute(full=False)
+        ids[slots] = version
+        attach.add(g.stats().last_sink_attach)
+        table = g.get_slots(every)
+        assert (table[pc.dag.file_slots] == ids).all()
+        assert (table == g0.get_slots(every)).all(), frac
+        bad, first = O.check_slots(a, table, 8)
+        assert bad == 0, (frac, bad, first)
+    assert 0xFFFFFFFF not in attach  # a sink list ran attached every step
+    if sink_at == "3":
+        assert g.stats().last_levels_oct >= 1
+        assert attach != {g0.stats().last_sink_attach}  # above the fill level
+    g.close()
+    g0.close()
