@@ -1148,21 +1148,20 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             constexpr bool kCB = kW == 2 && !kStream;
             uint32_t pass = 0;
             bool pend = false;  // (producer) s_pp holds the last finished jobs, not yet propagated
-            // cb0 = 2: the chain fetches only the fusion target's old digest;
-            // its template (the producer's ring), its target's record (s_nnm)
-            // and the reverse edges the producer propagates come from the
-            // producer, and its start state is the IV (its hole is at byte 2:
-            // no constant leading block)
+            // cb0 = 2: the chain fetches only the fusion target's old digest
+            // and first two reverse edges; its template (the producer's ring)
+            // and its own target's record (s_nnm) come from the producer, and
+            // its start state is the IV (its hole is at byte 2: no constant
+            // leading block)
             const bool handoff = kCB && a.cb0 == 2 && a.handoff;
-            uint2 ppe[2] = {make_uint2(0, 0), make_uint2(0, 0)}, pe_pend[2] = {ppe[0], ppe[1]};
+
             // cb0: the frontier atomics of a finished job run on the producer
             // (idle in a pass's last iteration), not on the chain's critical path
             auto producer_propagate = [&]() {
                 const uint4 q = s_pp[lane][0], e = s_pp[lane][1];
                 const bool v = q.w != 0;
                 if (v) a.dirty[q.x] = 0u;
-                const uint2 pe[2] = {handoff ? pe_pend[0] : make_uint2(e.x, e.y),
-                                     handoff ? pe_pend[1] : make_uint2(e.z, e.w)};
+                const uint2 pe[2] = {make_uint2(e.x, e.y), make_uint2(e.z, e.w)};
                 propagate_pre(a, v ? q.y : 0u, v ? q.z : 0u, pe);
                 pend = false;
             };
@@ -1245,8 +1244,8 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
                         olo = od[0];
                         ohi = od[1];
-                        if (!handoff && m1.y < m1.z) pre[0] = a.cons[m1.y];  // (handoff: the producer's)
-                        if (!handoff && m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
+                        if (m1.y < m1.z) pre[0] = a.cons[m1.y];
+                        if (m1.y + 1 < m1.z) pre[1] = a.cons[m1.y + 1];
                         if (a.mid) {
                             hlo = a.mid[2ull * p];
                             hhi = a.mid[2ull * p + 1];
@@ -1280,6 +1279,10 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * nm1.x);
                     nolo = od[0];
                     nohi = od[1];
+                    if (handoff) {  // (the reverse edges the producer propagates with, as without handoff)
+                        if (nm1.y < nm1.z) npre[0] = a.cons[nm1.y];
+                        if (nm1.y + 1 < nm1.z) npre[1] = a.cons[nm1.y + 1];
+                    }
                 }
                 if (kChain && has && nfu && !handoff) {
                     if (kW == 2) {
@@ -1513,10 +1516,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                 nnm1 = a.meta[2ull * nm1.w + 1];
                             }
                         }
-                        if (handoff && it == 0 && has) {  // this job's first two reverse edges (propagated next pass)
-                            ppe[0] = m1.y < m1.z ? a.cons[m1.y] : make_uint2(0, 0);
-                            ppe[1] = m1.y + 1 < m1.z ? a.cons[m1.y + 1] : make_uint2(0, 0);
-                        }
+
                         // idle in the last iteration (every block of the pass built):
                         // the fusion target's template blocks 0 and 1 into the ring,
                         // for the chain to OR the digest into at the hand-over
@@ -1673,7 +1673,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         if ((kCB && a.cb0) || pp3) {
                             s_pp[jl][0] = make_uint4(p, m1.y, !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z),
                                                      own ? 1u : 0u);
-                            if (!handoff) s_pp[jl][1] = make_uint4(pre[0].x, pre[0].y, pre[1].x, pre[1].y);
+                            s_pp[jl][1] = make_uint4(pre[0].x, pre[0].y, pre[1].x, pre[1].y);
                         }
                     }
                 }
@@ -1700,10 +1700,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
                 }
                 if (kIsProd && ((kCB && a.cb0) || pp3)) pend = true;
-                if (kIsProd && handoff) {
-                    pe_pend[0] = ppe[0];
-                    pe_pend[1] = ppe[1];
-                }
+
                 fslot = has ? m1.x : ~0u;
                 has = nx != ~0u;
                 p = has ? nx : 0u;
