@@ -1010,14 +1010,23 @@ __device__ __forceinline__ uint32_t wave_max_small(uint32_t x) {
 __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii);
 __device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed);
 
-template <uint32_t kW, bool kStream>
-__global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
+// kJ = 64 jobs per workgroup (two chain waves), or 32 (one chain wave: the
+// half workgroup, for levels a little wider than one 64-job workgroup per
+// CU -- three fit a CU, each chain wave on a SIMD of its own)
+template <uint32_t kW, bool kStream, uint32_t kJ = 64>
+__global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs a) {
     static_assert(kW == 2 || kW == 3, "producer (+ expander)");
     static_assert(!kStream || kW == 2, "streamed hand-over: producer + chain only");
+    static_assert(kJ == 64 || (kJ == 32 && kW == 2 && !kStream), "the half workgroup: chain + producer");
     constexpr uint32_t lag = kW - 1;
-    constexpr uint32_t kProd = 2, kExp = 3;  // wave roles: 0, 1 chain
-    constexpr uint32_t kBufs = kStream ? 3 : 2;  // row buffers of 64 rows
-    __shared__ __attribute__((aligned(16))) uint32_t kw[(kBufs * 64 + 1) * kPcRow];  // + the a-lanes' k row
+    constexpr uint32_t kCW = kJ / 32;                  // chain waves
+    constexpr uint32_t kProd = kCW, kExp = kCW + 1;    // wave roles: 0 .. kCW - 1 chain
+    constexpr uint32_t kThreads = 64 * (kCW + kW - 1);
+    constexpr uint32_t kBufs = kStream ? 3 : 2;  // row buffers of kJ rows
+    // + the a-lanes' k row (kBufs kJ) and a junk row the half workgroup's
+    // producer lanes without a job write their split chunks to
+    constexpr uint32_t kOnes = kBufs * kJ, kJunk = kOnes + 1;
+    __shared__ __attribute__((aligned(16))) uint32_t kw[(kBufs * kJ + 2) * kPcRow];
     __shared__ __attribute__((aligned(16))) uint32_t wbuf[kW == 3 ? 2 * 64 * kWRow : 4];
     __shared__ uint32_t ring_all[64 * kRing];
     __shared__ uint4 s_dig[64][2];
@@ -1032,7 +1041,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     __shared__ uint32_t s_cw[2];                      // ... block id + 1 staged, per chain wave
     __shared__ uint32_t s_hq[64 * kHq];               // the producer's hole chunks (ChunkCursor)
     __shared__ unsigned long long s_stamp[2][64];
-    static_assert(64 * (kW + 1) * kRing <= (kBufs * 64 + 1) * kPcRow, "the sink lanes' rings live in kw");
+    static_assert(kThreads * kRing <= (kBufs * kJ + 2) * kPcRow, "the sink lanes' rings live in kw");
     if (a.sink_wg && blockIdx.x >= a.sink_wg) {
         // the attached sink list (and with ovf the own list's overflow), one
         // job per lane, below the chains' priority: these lanes fill the
@@ -1043,9 +1052,9 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
         WgStamp ws;
         ws.begin(a);
         const LaunchList ll(a);
-        constexpr uint32_t nt = 64 * (kW + 1);
+        constexpr uint32_t nt = kThreads;
         const uint32_t g2 = gridDim.x - a.sink_wg;
-        const uint32_t lo = a.ovf ? min(ll.n1, a.sink_wg * 64) : ll.n1;
+        const uint32_t lo = a.ovf ? min(ll.n1, a.sink_wg * kJ) : ll.n1;
         uint32_t hashed = 0;
         for (uint32_t base = lo + (blockIdx.x - a.sink_wg) * nt; base < ll.n; base += g2 * nt) {
             if (threadIdx.x == 0) ws.jobs += min(nt, ll.n - base);
@@ -1063,14 +1072,14 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     const uint32_t hp = lane & 15;
     const bool elane = (hp & 4) == 0;
     const uint32_t ep = elane ? hp : ((hp & 8) | (7 - (hp & 7)));
-    const uint32_t jl = wave < 2 ? 32 * wave + 8 * (lane >> 4) + ((ep & 3) | ((ep >> 3) << 2)) : lane;
-    uint32_t* const ones = &kw[kBufs * 64 * kPcRow];
+    const uint32_t jl = wave < kCW ? 32 * wave + 8 * (lane >> 4) + ((ep & 3) | ((ep >> 3) << 2)) : lane;
+    uint32_t* const ones = &kw[kOnes * kPcRow];
     if (wave == 0) {
         __builtin_amdgcn_s_setprio(3);
         ones[lane] = lane ? 1u : 0u;
         if (lane < kPcRow - 64) ones[64 + lane] = 1u;
     }
-    if (wave == 1) __builtin_amdgcn_s_setprio(3);
+    if (wave == 1 && kCW > 1) __builtin_amdgcn_s_setprio(3);
     if (threadIdx.x == 0) {
         s_flag[0] = s_flag[1] = s_flag[2] = 0;
         s_cons[0] = s_cons[1] = 0;
@@ -1099,7 +1108,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     ws.begin(a);
     const LaunchList ll(a);
     // (lane workgroups: the list's tail is theirs)
-    const uint32_t n = !a.sink_wg ? ll.n : a.ovf ? min(ll.n1, a.sink_wg * 64) : ll.n1;
+    const uint32_t n = !a.sink_wg ? ll.n : a.ovf ? min(ll.n1, a.sink_wg * kJ) : ll.n1;
     const uint32_t gstride = a.sink_wg ? a.sink_wg : gridDim.x;
     // One copy of the loop per wave role (chain / producer / expander), each
     // with only its own state: the register allocator then sizes the kernel
@@ -1108,13 +1117,13 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     // role runs the same barrier sequence (its control comes from LDS).
     auto body = [&](auto rc) {
         constexpr uint32_t R = decltype(rc)::value;
-        constexpr bool kChain = R < 2, kIsProd = R == kProd, kIsExp = R == kExp;
+        constexpr bool kChain = R < kCW, kIsProd = R == kProd, kIsExp = R == kExp;
         // split passes so far (every role counts them alike: the flag values)
         uint32_t sid = 0, known_sp = 0;
-        for (uint32_t base = blockIdx.x * 64; base < n; base += gstride * 64) {
-            if (threadIdx.x == 0) ws.jobs += min(64u, n - base);
+        for (uint32_t base = blockIdx.x * kJ; base < n; base += gstride * kJ) {
+            if (threadIdx.x == 0) ws.jobs += min(kJ, n - base);
             const uint32_t i = base + jl;
-            bool has = i < n;
+            bool has = jl < kJ && i < n;  // (half workgroup: producer lanes kJ.. have none)
             const uint32_t ii = has ? ll.at(a, i) : 0u;  // (list position, when has)
             uint32_t p = has ? a.list[ii] : 0u;
             // the listed job's record (append_jobs wrote it beside the list)
@@ -1127,7 +1136,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             uint32_t maxnb;
             {
                 const uint32_t il = base + lane;
-                maxnb = wave_max_small(il < n ? a.lmeta[2ull * ll.at(a, il)].y : 0u);
+                maxnb = wave_max_small(lane < kJ && il < n ? a.lmeta[2ull * ll.at(a, il)].y : 0u);
             }
             uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, nolo = nm0, nohi = nm0, nnm0 = nm0, nnm1 = nm0;
             uint4 nt[8];
@@ -1159,7 +1168,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             // (idle in a pass's last iteration), not on the chain's critical path
             auto producer_propagate = [&]() {
                 const uint4 q = s_pp[lane][0], e = s_pp[lane][1];
-                const bool v = q.w != 0;
+                const bool v = lane < kJ && q.w != 0;  // (half workgroup: lanes kJ.. hold no job)
                 if (v) a.dirty[q.x] = 0u;
                 const uint2 pe[2] = {make_uint2(e.x, e.y), make_uint2(e.z, e.w)};
                 propagate_pre(a, v ? q.y : 0u, v ? q.z : 0u, pe);
@@ -1316,7 +1325,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                     const uint32_t bi = kStream ? bufb % 3 : (bufb & 1);
                     if (kStream && full && !own0) known = lds_poll(&s_flag[bi], 4 * bufb + 1, 4 * bufb);
                     if (kStream && full && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
-                    const uint32_t row_off = ((bi * 64 + jl) * kPcRow) * 4, ones_off = kBufs * 64 * kPcRow * 4;
+                    const uint32_t row_off = ((bi * kJ + jl) * kPcRow) * 4, ones_off = kOnes * kPcRow * 4;
                     const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
                                                                      ((M & ones_off) | (~M & row_off)));
                     uint4 v = r4[0], vn = r4[1];
@@ -1467,7 +1476,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
     #pragma unroll
                             for (int q = 0; q < 16; ++q) w[q] = s_w0[lane * 17 + q];
                             if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
-                            uint4* row0 = reinterpret_cast<uint4*>(&kw[((xp & 1) * 64 + lane) * kPcRow]);
+                            uint4* row0 = reinterpret_cast<uint4*>(&kw[(lane < kJ ? (xp & 1) * kJ + lane : kJunk) * kPcRow]);
                             const uint32_t fb = (a.split + 1) * sid;  // this pass's flag values: fb + 1 ..
                             if (a.split == 2) {  // chunks 1-3 (the chain wrote chunk 0 only)
                                 kw_expand_chunk(w, row0, 1);
@@ -1496,7 +1505,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                             // (RF_K2_STAMPS=3: every block's assembly end on the producer)
                             if ((a.dbg_twice == 2 && it == 0) || a.dbg_twice == 8) { RF_STAMP_PL(sk); ++sk; }
                             if (kW == 2) {
-                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(((pb + xp) & 1) * 64 + lane) * kPcRow]));
+                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(((pb + xp) & 1) * kJ + lane) * kPcRow]));
                             } else {
                                 uint4* row = reinterpret_cast<uint4*>(&wbuf[((it & 1) * 64 + lane) * kWRow]);
     #pragma unroll
@@ -1540,7 +1549,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                                                   nt[6].x, nt[6].y, nt[6].z, nt[6].w, nt[7].x, nt[7].y, nt[7].z, nt[7].w};
     #pragma unroll
                                 for (int q = 0; q < 16; ++q) w[q] = bswap32(w[q]);
-                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(((maxnb + xp) & 1) * 64 + lane) * kPcRow]));
+                                kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(((maxnb + xp) & 1) * kJ + lane) * kPcRow]));
                             }
                         }
                     } else if (kIsExp) {
@@ -1568,7 +1577,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                         // barrier): the code is then cached when the links start.
                         const bool exb = it == 0 && (cb0 || (kCB && a.cb0 && pass == 0 && a.dbg_twice != 5));
                         if (exb) {
-                            uint4* row = reinterpret_cast<uint4*>(&kw[((cb0 ? (xp & 1) * 64 : 64u) + jl) * kPcRow]);
+                            uint4* row = reinterpret_cast<uint4*>(&kw[((cb0 ? (xp & 1) * kJ : kJ) + jl) * kPcRow]);
                             if (!kStream && a.split == 2)  // (pass 0: warms the code the split passes run)
                                 chain_expand_b0<4>(wb0, elane, row);
                             else if (!kStream && a.split)
@@ -1680,12 +1689,12 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
                 RF_STAMP_PL(sk); ++sk;
                 lds_barrier();
                 RF_STAMP_PL(sk); ++sk;
-                const uint32_t nx = s_next[jl];
+                const uint32_t nx = jl < kJ ? s_next[jl] : ~0u;
                 // split: the next pass's block 1 sits in the buffer this pass's
                 // last block (maxnb - 1) left free, so its block b goes to
                 // buffer (b + xp') & 1 with (1 + xp') & 1 = (maxnb + xp) & 1
                 if (build1) xp = (maxnb + xp + 1) & 1;
-                maxnb = wave_max_small(s_nbx[lane]);
+                maxnb = wave_max_small(lane < kJ ? s_nbx[lane] : 0u);
                 if (kChain) {
                     if (!(kCB && a.cb0) && !pp3) {
                         uint32_t cb = 0, ce = 0;
@@ -1711,7 +1720,7 @@ __global__ __launch_bounds__(64 * (kW + 1)) void k2_level_pl(LevelArgs a) {
             if (kIsProd && (kCB || kW == 3) && pend) producer_propagate();  // the last pass's jobs
         }
     };
-    if (wave < 2) {
+    if (wave < kCW) {
         body(std::integral_constant<uint32_t, 0>{});
     } else if (wave == kProd) {
         body(std::integral_constant<uint32_t, kProd>{});
@@ -2658,6 +2667,28 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         const uint32_t ovf_lanes = g.ovf_mode;  // (RF_K2_OVF, read at load)
         const uint32_t nt = wide ? 256u : 192u;
         const uint64_t est = std::min<uint64_t>(e - b, g.step_marked);
+        // half workgroups (32 jobs, one chain wave: three fit a CU, each chain
+        // on its own SIMD) for a latency-form level estimated at more than one
+        // 64-job workgroup per CU but at most three 32-job ones (the 8-rank
+        // piece's Exec level: 17.5k chains) -- instead of a second 64-job
+        // workgroup on some CUs, whose four chain waves then share SIMDs.
+        // RF_K2_HALF=0: off (A/B)
+        static const bool half_ok = [] {
+            const char* v = getenv("RF_K2_HALF");
+            return !(v && atoi(v) == 0);
+        }();
+        if (half_ok && !one_lane && !wide && no_stream && g.n_cu && est > 64ull * g.n_cu &&
+            est <= 96ull * g.n_cu) {
+            uint64_t hg = (e - b + 31) / 32;
+            if (hg > wg_cap) hg = wg_cap;
+            uint64_t grid = hg;
+            if (sink_lvl != ~0u && sink_lanes) {
+                a.sink_wg = (uint32_t)hg;
+                grid += std::min<uint64_t>((n2 + 127) / 128, 1024u);
+            }
+            hipLaunchKernelGGL((k2_level_pl<2, false, 32>), dim3((uint32_t)grid), dim3(128), pad, s, a);
+            return hipGetLastError();
+        }
         if (!one_lane && ovf_lanes && g.n_cu && est > 64ull * g.n_cu) {
             a.sink_wg = g.n_cu;
             a.ovf = ovf_lanes;
