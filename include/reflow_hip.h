@@ -385,6 +385,7 @@ typedef struct {
     uint32_t last_levels_oct; /* levels the last plain incremental step ran in the octo form */
     uint32_t split_block0;    /* fused links split block 0's schedule over chain and producer: 0 off, 1 / 2 (RF_K2_SPLIT) */
     uint32_t last_sink_attach; /* level whose launch ran the sink list in the last plain step (UINT32_MAX: none) */
+    uint32_t last_levels_half; /* levels the last plain step ran in 32-job latency-form workgroups */
 } rf_graph_stats;
 int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
 

@@ -233,7 +233,7 @@ class GraphStats(ctypes.Structure):
                 ("last_ms", ctypes.c_float), ("last_levels_lf", ctypes.c_uint32),
                 ("last_mark_lf", ctypes.c_uint32), ("last_levels_oct", ctypes.c_uint32),
                 ("split_block0", ctypes.c_uint32),
-                ("last_sink_attach", ctypes.c_uint32)]
+                ("last_sink_attach", ctypes.c_uint32), ("last_levels_half", ctypes.c_uint32)]
 
 
 _lib = None

@@ -1739,13 +1739,14 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         // the first launched level zeroes the previous step's half; the next
         // step (and set_slots / imports before it) uses that half
         bool first = true;
-        if (lvl_lo == 0) G.last_levels_lf = G.last_levels_oct = 0;
+        if (lvl_lo == 0) G.last_levels_lf = G.last_levels_oct = G.last_levels_half = 0;
         G.last_sink_attach = attach;
         for (uint32_t l = lvl_lo; l < std::min(lvl_hi, G.n_levels); ++l) {
             if (!(G.inc_level[l] & kLvlForm) || (l == sink && attach != ~0u)) continue;
             HIPC(launch_graph_level(G, l, 0, s, first ? G.counts_other : nullptr, l == attach ? sink : ~0u));
             G.last_levels_lf += graph_level_lf(G, l) ? 1u : 0u;
             G.last_levels_oct += (G.inc_level[l] & kLvlOct) ? 1u : 0u;  // (RF_K2_CHAIN=14 aside)
+            G.last_levels_half += graph_level_half(G, l) ? 1u : 0u;
             first = false;
         }
         gr->last_counts = G.counts;
@@ -2056,6 +2057,7 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
     out->last_levels_oct = gr->g.last_levels_oct;
     out->split_block0 = gr->g.split_b0;
     out->last_sink_attach = gr->g.last_sink_attach;
+    out->last_levels_half = gr->g.last_levels_half;
     if (gr->timed) {
         HIPC(hipEventSynchronize(gr->e1));
         HIPC(hipEventElapsedTime(&out->last_ms, gr->e0, gr->e1));

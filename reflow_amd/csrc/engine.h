@@ -136,7 +136,7 @@ struct GraphDev {
     // (k3_mark_slots_lf) from this many changed slots
     uint64_t cfg_thru = 0, cfg_thru_wide = 0, cfg_thru_mark = 0;
     // what the last plain step / mark launch chose (rf_graph_stats)
-    uint32_t last_levels_lf = 0, last_mark_lf = 0, last_levels_oct = 0;
+    uint32_t last_levels_lf = 0, last_mark_lf = 0, last_levels_oct = 0, last_levels_half = 0;
     uint32_t last_sink_attach = ~0u;  // the level whose launch took the sink list last step (~0u: none)
     uint32_t sink_at = 2;             // where the sink list may run (RF_K2_SINK_AT at load; graph_enqueue)
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
@@ -171,6 +171,7 @@ const void* graph_mark_kernel();
 hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipStream_t s,
                               uint32_t* zero_counts = nullptr, uint32_t sink_lvl = ~0u);
 bool graph_level_lf(const GraphDev& g, uint32_t lvl);
+bool graph_level_half(const GraphDev& g, uint32_t lvl);
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);

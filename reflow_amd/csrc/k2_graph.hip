@@ -2551,6 +2551,22 @@ bool graph_level_lf(const GraphDev& g, uint32_t lvl) {
            ((g.inc_level[lvl] & kLvlForm) == 2 ? g.thru_slots_wide : g.thru_slots);
 }
 
+// Half workgroups (k2_level_pl<2, false, 32>) for a latency-form level of
+// short jobs estimated at 64-96 chains per CU (RF_K2_HALF=0: never, A/B)
+bool graph_level_half(const GraphDev& g, uint32_t lvl) {
+    static const bool half_ok = [] {
+        const char* v = getenv("RF_K2_HALF");
+        return !(v && atoi(v) == 0);
+    }();
+    static const bool one_lane = [] {
+        const char* v = getenv("RF_K2_CHAIN");
+        return v && atoi(v) == 14;
+    }();
+    const uint64_t est = std::min<uint64_t>(g.lvl_start[lvl + 1] - g.lvl_start[lvl], g.step_marked);
+    return half_ok && !one_lane && (g.inc_level[lvl] & kLvlForm) == 1 && !(g.inc_level[lvl] & kLvlOct) &&
+           !g.stream_handover && g.n_cu && est > 64ull * g.n_cu && est <= 96ull * g.n_cu && !graph_level_lf(g, lvl);
+}
+
 hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStream_t s, uint32_t* zero_counts,
                               uint32_t sink_lvl) {
     const uint32_t b = g.lvl_start[lvl], e = g.lvl_start[lvl + 1];
@@ -2673,12 +2689,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         // piece's Exec level: 17.5k chains) -- instead of a second 64-job
         // workgroup on some CUs, whose four chain waves then share SIMDs.
         // RF_K2_HALF=0: off (A/B)
-        static const bool half_ok = [] {
-            const char* v = getenv("RF_K2_HALF");
-            return !(v && atoi(v) == 0);
-        }();
-        if (half_ok && !one_lane && !wide && no_stream && g.n_cu && est > 64ull * g.n_cu &&
-            est <= 96ull * g.n_cu) {
+        if (graph_level_half(g, lvl)) {
             uint64_t hg = (e - b + 31) / 32;
             if (hg > wg_cap) hg = wg_cap;
             uint64_t grid = hg;

@@ -63,9 +63,9 @@ def run(ctx, name, g, slots, old, new, steps):
                 step()
                 ctx.sync()
             st = g.stats()
-            print(name, form, "%.4f ms/step" % ms, "(sinks on level %d, lf levels %d, octo levels %d, split %d)"
+            print(name, form, "%.4f ms/step" % ms, "(sinks on level %d, lf levels %d, octo levels %d, half levels %d, split %d)"
                   % (st.last_sink_attach if st.last_sink_attach != 0xFFFFFFFF else -1, st.last_levels_lf,
-                     st.last_levels_oct, st.split_block0), file=sys.stderr, flush=True)
+                     st.last_levels_oct, st.last_levels_half, st.split_block0), file=sys.stderr, flush=True)
     res["slots_equal"] = bool(all((snaps["pl"] == snaps[f]).all() for f in snaps))
     g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
     for b in (d_slots, d_old, d_new):
