@@ -1633,7 +1633,7 @@ void graph_forms_from_env(GraphDev& G) {
     {
         const char* v = getenv("RF_K2_SINK_AT");
         const char* w = getenv("RF_K2_SINK_LAST");  // (round-4 scripts: =0 the fill level)
-        G.sink_at = v ? (uint32_t)std::min(std::max(atoi(v), 0), 3) : (w && atoi(w) == 0) ? 0u : 2u;
+        G.sink_at = v ? (uint32_t)std::min(std::max(atoi(v), 0), 4) : (w && atoi(w) == 0) ? 0u : 2u;
     }
     const char* tv = getenv("RF_K2_THRU");
     const char* tw = getenv("RF_K2_THRU_WIDE");
@@ -1696,6 +1696,15 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
                 if (G.inc_level[l] & kLvlSinkMin) smin = l;
             }
             if (sink != ~0u && fill != ~0u && G.sink_attach_ok) {
+                // (sink_at 4: the level above the fill level first, A/B)
+                if (G.sink_at == 4) {
+                    uint32_t most = 0;
+                    for (uint32_t l = fill + 1; l < sink; ++l)
+                        if ((G.inc_level[l] & kLvlForm) && G.lvl_start[l + 1] - G.lvl_start[l] > most) {
+                            most = G.lvl_start[l + 1] - G.lvl_start[l];
+                            attach = l;
+                        }
+                }
                 for (uint32_t l = fill + 1; l-- > smin && attach == ~0u;)
                     if ((G.inc_level[l] & kLvlForm) && graph_level_lf(G, l)) attach = l;
                 // no throughput-form level to fill: a level above the fill
