@@ -1350,6 +1350,7 @@ def parity_summary(sha, c1, dag, dag100, probe, cpu):
         "configs2_checkpoint_slots": get(dag, "checkpoint", "slots_equal"),
         "configs3_incremental_vs_oracle": get(dag100, "digests_equal_oracle"),
         "configs3_incremental_equals_full": get(dag100, "incremental_equals_full"),
+        "configs3_piece8_incremental_equals_full": get(dag100, "piece_8", "incremental_equals_full"),
         "configs3_dirty_jobs_vs_layout": get(dag100, "dirty_jobs_match_device"),
         "configs4_probe_vs_oracle": get(cpu, "probe_bits_equal_gpu"),
         "configs4_no_false_negatives": get(probe, "no_false_negatives"),
