@@ -523,6 +523,11 @@ def bench_lowering(args):
         return {"error": "rc %d: %s" % (r.returncode, (r.stderr or "")[-300:])}
     res = json.loads(r.stdout.strip().splitlines()[-1])
     res["wall_s"] = round(wall, 2)
+    # RF_LOWER_TIMING=1: the lowering's phases (reflow_host.cpp PhaseClock)
+    phases = [ln[len("[lower] "):].rsplit(" ", 2) for ln in (r.stderr or "").splitlines() if ln.startswith("[lower] ")]
+    if phases:
+        res["phases_s"] = {ph[0]: float(ph[1]) for ph in phases if len(ph) == 3}
+        log("lowering phases: " + ", ".join("%s %.2f" % kv for kv in res["phases_s"].items()))
     res["what"] = ("tools/lower_bench: reflow::Canonicalize + Eval lowering (reflow_host.cpp) of a 1000align "
                    "Flow graph of the configs[2] shape; load = blob + rf_graph_load + full recompute")
     log("lowering: %d nodes: build %.1f s, canonicalize %.1f s, lower %.1f s, load %.1f s, incremental %.1f ms"
