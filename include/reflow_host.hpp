@@ -26,6 +26,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <new>
 #include <optional>
 #include <string>
 #include <unordered_map>
@@ -275,16 +276,50 @@ class FlowArena {
         nodes_.push_back(std::move(f));
         return &nodes_.back();
     }
-    // n default-constructed nodes, contiguous (Canonicalize's copies: an
-    // Eval then maps a copy to its slot by address, no hash lookup)
+    // n default-constructed nodes, contiguous (an Eval then maps a node of
+    // the block to its slot by address, no hash lookup)
     Flow* NewN(size_t n) {
-        blocks_.emplace_back(new Flow[n ? n : 1]);
-        return blocks_.back().get();
+        return NewN(n, [](Flow* f, size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; ++i) new (f + i) Flow();
+        });
+    }
+    // n contiguous nodes, each constructed by make(block, lo, hi) -- placement
+    // new of [lo, hi) -- which may split the range over threads (Canonicalize
+    // copy-constructs its copies in place: no default construction first,
+    // and the pages are first touched by the threads that fill them).  make
+    // must construct every node, or throw having constructed none.
+    template <class Make>
+    Flow* NewN(size_t n, Make make) {
+        Block b;
+        b.n = n ? n : 1;
+        b.p = static_cast<Flow*>(::operator new(b.n * sizeof(Flow), std::align_val_t(alignof(Flow))));
+        try {
+            make(b.p, size_t(0), n);
+            if (!n) new (b.p) Flow();
+        } catch (...) {
+            ::operator delete(b.p, std::align_val_t(alignof(Flow)));
+            throw;
+        }
+        blocks_.push_back(b);
+        return b.p;
+    }
+    FlowArena() = default;
+    FlowArena(const FlowArena&) = delete;
+    FlowArena& operator=(const FlowArena&) = delete;
+    ~FlowArena() {
+        for (Block& b : blocks_) {
+            for (size_t i = 0; i < b.n; ++i) b.p[i].~Flow();
+            ::operator delete(b.p, std::align_val_t(alignof(Flow)));
+        }
     }
 
    private:
+    struct Block {
+        Flow* p = nullptr;
+        size_t n = 0;
+    };
     std::deque<Flow> nodes_;
-    std::vector<std::unique_ptr<Flow[]>> blocks_;
+    std::vector<Block> blocks_;
 };
 
 // test/flow/constructor.go:17-74

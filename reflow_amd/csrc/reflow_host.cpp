@@ -788,14 +788,35 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
     pc.lap("canonicalize: post-order");
     // 2. one copy per original, contiguous in post-order (f.Copy() +
     //    Config.Merge, deps and map flow pointing at copies), on host threads
-    Flow* cp = arena.NewN(n);
-    parallel_ranges(n, 16384, lower_threads(e), [&](size_t, size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i) {
-            Flow& c = cp[i];
-            c = *post[i];
-            c.config.Merge(config);
-            for (Flow*& d : c.Deps) d = cp + *index.find(d);
-            if (c.MapFlow) c.MapFlow = cp + *index.find(c.MapFlow);
+    Flow* cp = arena.NewN(n, [&](Flow* blk, size_t, size_t) {
+        // copy-constructed in place on host threads (a node's deps and map
+        // flow point at copies by their post-order index; copies that a
+        // thread already made are never touched by another).  A failing
+        // range's constructed nodes are destroyed by parallel_ranges'
+        // rethrow path below, so none survive an exception.
+        std::vector<std::pair<size_t, size_t>> done;
+        std::mutex mu;
+        try {
+            parallel_ranges(n, 16384, lower_threads(e), [&](size_t, size_t lo, size_t hi) {
+                size_t i = lo;
+                try {
+                    for (; i < hi; ++i) {
+                        Flow* c = new (blk + i) Flow(*post[i]);
+                        c->config.Merge(config);
+                        for (Flow*& d : c->Deps) d = blk + *index.find(d);
+                        if (c->MapFlow) c->MapFlow = blk + *index.find(c->MapFlow);
+                    }
+                } catch (...) {
+                    for (size_t k = lo; k < i; ++k) blk[k].~Flow();
+                    throw;
+                }
+                std::lock_guard<std::mutex> lk(mu);
+                done.emplace_back(lo, hi);
+            });
+        } catch (...) {
+            for (auto& r : done)
+                for (size_t k = r.first; k < r.second; ++k) blk[k].~Flow();
+            throw;
         }
     });
     pc.lap("canonicalize: copies (threads)");
