@@ -69,6 +69,26 @@ struct DigestHash {
 void WriteDigest(std::string& w, const Digest& d);
 
 namespace detail {
+// Allocator for tables that are probed at random (the lowering's maps hold
+// tens of millions of entries, hundreds of MB): from 4 MB on, 2 MB-aligned
+// and marked for transparent huge pages, so a probe costs a cache miss but
+// rarely a TLB miss as well.  Falls back to plain pages where the kernel
+// declines.
+void* huge_page_alloc(size_t bytes);
+void huge_page_free(void* p, size_t bytes) noexcept;
+template <class T>
+struct HugePageAlloc {
+    using value_type = T;
+    HugePageAlloc() = default;
+    template <class U>
+    HugePageAlloc(const HugePageAlloc<U>&) noexcept {}
+    T* allocate(size_t n) { return static_cast<T*>(huge_page_alloc(n * sizeof(T))); }
+    void deallocate(T* p, size_t n) noexcept { huge_page_free(p, n * sizeof(T)); }
+    template <class U>
+    bool operator==(const HugePageAlloc<U>&) const noexcept { return true; }
+    template <class U>
+    bool operator!=(const HugePageAlloc<U>&) const noexcept { return false; }
+};
 // Open-addressing hash map (linear probing, backward-shift erase) for the
 // lowering's hot lookups -- Flow pointers and File IDs, tens of millions of
 // them per Eval: one probe run per lookup instead of a node-based map's
@@ -91,6 +111,11 @@ class FlatMap {
         }
     }
     const V* find(const K& k) const { return const_cast<FlatMap*>(this)->find(k); }
+    // a hint that k is about to be looked up: its probe run's first slot
+    // into the cache (a lookup into a table of hundreds of MB is a miss)
+    void prefetch(const K& k) const {
+        if (!slots_.empty()) __builtin_prefetch(&slots_[Hash{}(k) & mask_]);
+    }
     // k must be absent
     V& insert(const K& k, V v) {
         if (2 * (n_ + 1) > slots_.size()) rehash(slots_.empty() ? 16 : 2 * slots_.size());
@@ -138,14 +163,14 @@ class FlatMap {
         bool used = false;
     };
     void rehash(size_t cap) {
-        std::vector<Slot> old(cap);
+        std::vector<Slot, HugePageAlloc<Slot>> old(cap);
         old.swap(slots_);
         mask_ = cap - 1;
         n_ = 0;
         for (Slot& s : old)
             if (s.used) insert(s.k, std::move(s.v));
     }
-    std::vector<Slot> slots_;
+    std::vector<Slot, HugePageAlloc<Slot>> slots_;
     size_t mask_ = 0, n_ = 0;
 };
 // std::vector whose resize default-initialises (no zero fill of the new

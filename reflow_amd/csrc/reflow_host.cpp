@@ -11,12 +11,33 @@
 #include <exception>
 #include <thread>
 #include <mutex>
+#include <sys/mman.h>
 #include <atomic>
 #include <functional>
 #include <memory>
 #include <unordered_set>
 
 namespace reflow {
+
+namespace detail {
+void* huge_page_alloc(size_t bytes) {
+    constexpr size_t kHuge = 2u << 20;
+    if (bytes < 2 * kHuge) {
+        void* p = ::operator new(bytes);
+        return p;
+    }
+    void* p = nullptr;
+    if (posix_memalign(&p, kHuge, bytes) != 0) throw std::bad_alloc();
+    (void)madvise(p, bytes, MADV_HUGEPAGE);  // (advice only: plain pages if declined)
+    return p;
+}
+void huge_page_free(void* p, size_t bytes) noexcept {
+    if (bytes < 2 * (2u << 20))
+        ::operator delete(p);
+    else
+        free(p);
+}
+}  // namespace detail
 
 void Check(int rc) {
     if (rc != RF_OK) throw Error(rc, rf_last_error());
@@ -769,10 +790,16 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
         size_t next;  // next dep (then MapFlow) to visit
     };
     std::vector<Frame> st{{root, 0}};
+    index.reserve(1u << 16);
     while (!st.empty()) {
         Frame& fr = st.back();
         Flow* f = fr.f;
         const size_t nd = f->Deps.size() + (f->MapFlow ? 1 : 0);
+        if (fr.next == 0)  // (first visit: the deps' index slots and records on their way in)
+            for (Flow* d : f->Deps) {
+                index.prefetch(d);
+                __builtin_prefetch(d);
+            }
         if (fr.next < nd) {
             Flow* d = fr.next < f->Deps.size() ? f->Deps[fr.next] : f->MapFlow;
             ++fr.next;
