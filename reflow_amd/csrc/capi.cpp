@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <new>
 #include <map>
 #include <mutex>
 #include <numeric>
@@ -1180,6 +1181,36 @@ int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_
     return RF_OK;
 }
 
+// fn(lo, hi) over [0, n) in ranges of `grain`, on the context's host threads
+// (the load's copy loops; fn must not throw)
+template <class F>
+static void load_parallel(rf_ctx* ctx, uint64_t n, uint64_t grain, F fn) {
+    const uint64_t nr = (n + grain - 1) / grain;
+    const uint64_t nt = std::min<uint64_t>(std::max(1u, ctx_host_threads(ctx)), nr);
+    if (nt <= 1) {
+        if (n) fn(0, n);
+        return;
+    }
+    std::atomic<uint64_t> next{0};
+    auto work = [&] {
+        for (uint64_t r; (r = next.fetch_add(1)) < nr;) fn(r * grain, std::min(n, (r + 1) * grain));
+    };
+    std::vector<std::thread> pool;
+    for (uint64_t t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+}
+
+// Stable counting sort of idx by key[idx] in [0, nkey) -> out
+static void counting_pass(const std::vector<uint32_t>& idx, const uint32_t* key, uint32_t nkey,
+                          std::vector<uint32_t>& out) {
+    std::vector<uint32_t> at(nkey + 1, 0);
+    for (uint32_t i : idx) at[key[i] + 1]++;
+    for (uint32_t k = 0; k < nkey; ++k) at[k + 1] += at[k];
+    out.resize(idx.size());
+    for (uint32_t i : idx) out[at[key[i]]++] = i;
+}
+
 extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out) {
     ARG(ctx && d && out, "null argument");
     *out = nullptr;
@@ -1194,6 +1225,15 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     auto* gr = new rf_graph();
     std::unique_ptr<rf_graph, void (*)(rf_graph*)> guard(gr, [](rf_graph* x) { rf_graph_destroy(x); });
     gr->ctx = ctx;
+    // RF_LOWER_TIMING=1: this load's phases on stderr (diagnostic, read per load)
+    const bool timing = getenv("RF_LOWER_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[load] %s %.3f s\n", what, std::chrono::duration<double>(now - t_last).count());
+        t_last = now;
+    };
     gr->producer.assign(S, -1);
     std::vector<uint32_t> nblk(J);
     for (uint32_t j = 0; j < J; ++j) {
@@ -1216,6 +1256,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         }
         nblk[j] = (uint32_t)((d->tmpl_len[j] + 9 + 63) / 64);
     }
+    lap("validate");
     // topological levels (Kahn)
     std::vector<uint32_t> indeg(J, 0), level(J, 0);
     std::vector<uint64_t> cptr(S + 1, 0);  // slot -> consumer jobs (external ids)
@@ -1246,6 +1287,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     if (q.size() != J) return fail(RF_EINVAL, "job graph has a cycle (%zu of %u jobs ordered)", q.size(), J);
     uint32_t L = 0;
     for (uint32_t j = 0; j < J; ++j) L = std::max(L, level[j] + 1);
+    lap("levels");
     // Fused chains (k2_level_pc): job j's fusion target is a consumer k whose
     // material has exactly one hole -- j's digest -- so k depends on nothing
     // else and can be hashed right after j, in the same lane, without being
@@ -1354,12 +1396,23 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
                 if (queueable(j) && sink(j) && level[j] < (uint32_t)lq) level[j] = (uint32_t)lq;
         }
     }
+    lap("fusion + sinks");
     // internal order: level ascending, blocks descending (similar lanes per wave)
     std::vector<uint32_t> perm(J);
     std::iota(perm.begin(), perm.end(), 0u);
-    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
-        return level[a] != level[b] ? level[a] < level[b] : nblk[a] > nblk[b];
-    });
+    {
+        const uint32_t maxb = J ? *std::max_element(nblk.begin(), nblk.end()) : 0;
+        if (maxb < (1u << 22)) {  // two stable counting passes: blocks descending, then level
+            std::vector<uint32_t> key(J), tmp;
+            for (uint32_t j = 0; j < J; ++j) key[j] = maxb - nblk[j];
+            counting_pass(perm, key.data(), maxb + 1, tmp);
+            counting_pass(tmp, level.data(), L, perm);
+        } else {
+            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+                return level[a] != level[b] ? level[a] < level[b] : nblk[a] > nblk[b];
+            });
+        }
+    }
     gr->ext2int.assign(J, 0);
     for (uint32_t i = 0; i < J; ++i) gr->ext2int[perm[i]] = i;
     gr->g.lvl_start.assign(L + 1, 0);
@@ -1368,6 +1421,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         gr->max_level_jobs = std::max(gr->max_level_jobs, gr->g.lvl_start[l + 1]);
         gr->g.lvl_start[l + 1] += gr->g.lvl_start[l];
     }
+    lap("order");
     // host arrays in internal order: 32-B job records, {pos, slot} holes,
     // padded templates (64-B blocks, FIPS padding pre-applied)
     std::vector<uint32_t> meta(8ull * J, 0), holes(2ull * H);
@@ -1379,47 +1433,79 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // are hashed only by a full recompute and keep their blocks).
     std::vector<uint32_t> lead(J, 0), lead_start(J, 0);
     uint64_t n_lead = 0;
-    uint64_t tb = 0, hcur = 0;
-    for (uint32_t i = 0; i < J; ++i) {
-        const uint32_t j = perm[i];
-        const uint32_t s = d->out_slot[j];
-        job_off[i] = tb;
-        const uint32_t ld = d->hole_ptr[j + 1] > d->hole_ptr[j]
-                                ? std::min<uint32_t>(d->hole_pos[d->hole_ptr[j]] / 64, nblk[j] - 1) : 0;
-        lead[i] = ld;
-        lead_start[i] = (uint32_t)(tb / 64);
-        n_lead += ld != 0;
-        uint32_t* m = &meta[8ull * i];
-        m[0] = (uint32_t)(tb / 64) + ld;
-        m[1] = nblk[j] - ld;
-        m[2] = (uint32_t)hcur;
-        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h, ++hcur) {
-            holes[2 * hcur] = d->hole_pos[h] - 64 * ld;
-            holes[2 * hcur + 1] = d->hole_slot[h];
+    uint64_t tb = 0;
+    {
+        // offsets first (a prefix pass), then the records on host threads
+        std::vector<uint32_t> hoff(J);
+        uint64_t hcur = 0;
+        for (uint32_t i = 0; i < J; ++i) {
+            const uint32_t j = perm[i];
+            job_off[i] = tb;
+            hoff[i] = (uint32_t)hcur;
+            tb += 64ull * nblk[j];
+            hcur += d->hole_ptr[j + 1] - d->hole_ptr[j];
         }
-        m[3] = (uint32_t)hcur;
-        m[4] = s;
-        m[5] = (uint32_t)cptr[s];
-        m[6] = (uint32_t)cptr[s + 1];
-        m[7] = fuse[j] >= 0 ? gr->ext2int[(uint32_t)fuse[j]] : 0xffffffffu;
-        if (fused_target[j] && holes[2 * m[2]] != 2) gr->g.fuse_pos2 = false;  // (cb0 = 2 needs every one at 2)
-        tb += 64ull * nblk[j];
-        gr->total_blocks += nblk[j] - ld;
+        std::atomic<uint64_t> a_lead{0}, a_blocks{0};
+        std::atomic<bool> pos2{true};
+        load_parallel(ctx, J, 16384, [&](uint64_t i0, uint64_t i1) {
+            uint64_t nl = 0, nb = 0;
+            bool p2 = true;
+            for (uint64_t i = i0; i < i1; ++i) {
+                const uint32_t j = perm[i];
+                const uint32_t s = d->out_slot[j];
+                const uint32_t ld = d->hole_ptr[j + 1] > d->hole_ptr[j]
+                                        ? std::min<uint32_t>(d->hole_pos[d->hole_ptr[j]] / 64, nblk[j] - 1) : 0;
+                lead[i] = ld;
+                lead_start[i] = (uint32_t)(job_off[i] / 64);
+                nl += ld != 0;
+                uint32_t* m = &meta[8ull * i];
+                uint64_t hc = hoff[i];
+                m[0] = (uint32_t)(job_off[i] / 64) + ld;
+                m[1] = nblk[j] - ld;
+                m[2] = (uint32_t)hc;
+                for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h, ++hc) {
+                    holes[2 * hc] = d->hole_pos[h] - 64 * ld;
+                    holes[2 * hc + 1] = d->hole_slot[h];
+                }
+                m[3] = (uint32_t)hc;
+                m[4] = s;
+                m[5] = (uint32_t)cptr[s];
+                m[6] = (uint32_t)cptr[s + 1];
+                m[7] = fuse[j] >= 0 ? gr->ext2int[(uint32_t)fuse[j]] : 0xffffffffu;
+                if (fused_target[j] && holes[2 * m[2]] != 2) p2 = false;  // (cb0 = 2 needs every one at 2)
+                nb += nblk[j] - ld;
+            }
+            a_lead += nl;
+            a_blocks += nb;
+            if (!p2) pos2 = false;
+        });
+        n_lead = a_lead;
+        gr->total_blocks += a_blocks;
+        if (!pos2) gr->g.fuse_pos2 = false;
     }
+    lap("records");
     if (tb / 64 >= 0xffffffffull) return fail(RF_EINVAL, "templates exceed 256 GiB");
-    std::vector<uint8_t> tmpl(std::max<uint64_t>(tb, 64), 0);
-    for (uint32_t i = 0; i < J; ++i) {
-        const uint32_t j = perm[i];
-        uint8_t* t = tmpl.data() + job_off[i];
-        const uint64_t len = d->tmpl_len[j];
-        if (len) memcpy(t, d->blob + d->tmpl_off[j], len);
-        // the kernels OR digests into the holes: keep them zero
-        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) memset(t + d->hole_pos[h], 0, 32);
-        t[len] = 0x80;
-        const uint64_t bits = len * 8;
-        uint8_t* e = t + 64ull * nblk[j];
-        for (int b = 0; b < 8; ++b) e[-1 - b] = (uint8_t)(bits >> (8 * b));
-    }
+    // every byte is written below (template, zero tail, padding): no zero fill
+    const uint64_t tmpl_size = std::max<uint64_t>(tb, 64);
+    std::unique_ptr<uint8_t[]> tmpl(new (std::nothrow) uint8_t[tmpl_size]);
+    if (!tmpl) return fail(RF_ENOMEM, "graph templates: %llu bytes", (unsigned long long)tmpl_size);
+    if (tb < 64) memset(tmpl.get(), 0, 64);
+    load_parallel(ctx, J, 4096, [&](uint64_t i0, uint64_t i1) {
+        for (uint64_t i = i0; i < i1; ++i) {
+            const uint32_t j = perm[i];
+            uint8_t* t = tmpl.get() + job_off[i];
+            const uint64_t len = d->tmpl_len[j];
+            if (len) memcpy(t, d->blob + d->tmpl_off[j], len);
+            // the kernels OR digests into the holes: keep them zero
+            for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) memset(t + d->hole_pos[h], 0, 32);
+            t[len] = 0x80;
+            uint8_t* e = t + 64ull * nblk[j];
+            memset(t + len + 1, 0, (size_t)(e - 8 - (t + len + 1)));
+            const uint64_t bits = len * 8;
+            for (int b = 0; b < 8; ++b) e[-1 - b] = (uint8_t)(bits >> (8 * b));
+        }
+    });
+    lap("templates");
     std::vector<uint32_t> cons_ptr(S + 1), cons_job(2 * H);  // {internal job, level}
     for (uint32_t s = 0; s <= S; ++s) cons_ptr[s] = (uint32_t)cptr[s];
     for (uint64_t c = 0; c < H; ++c) {
@@ -1474,17 +1560,20 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     }
     gr->g.sink_attach_ok = true;
     gr->tmpl_bytes = tb;
+    lap("reverse edges + forms");
     // upload
     GraphDev& G = gr->g;
-    if (int rc = graph_device_alloc(gr, J, S, L, H, tmpl.size())) return rc;
+    if (int rc = graph_device_alloc(gr, J, S, L, H, tmpl_size)) return rc;
     hipError_t e;
     if ((e = sync_copy(ctx, gr->b_meta.p, meta.data(), 32ull * J, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = sync_copy(ctx, gr->b_holes.p, holes.data(), 8ull * H, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = sync_copy(ctx, gr->b_cons_ptr.p, cons_ptr.data(), 4ull * (S + 1), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = sync_copy(ctx, gr->b_cons_job.p, cons_job.data(), 8ull * H, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = sync_copy(ctx, gr->b_tmpl.p, tmpl.data(), tmpl.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = sync_copy(ctx, gr->b_tmpl.p, tmpl.get(), tmpl_size, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = sync_copy(ctx, gr->b_lvl_start.p, G.lvl_start.data(), 4ull * (L + 1), hipMemcpyHostToDevice)) != hipSuccess)
         return fail(RF_EDEVICE, "graph upload: %s", hipGetErrorString(e));
+    tmpl.reset();
+    lap("upload");
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> hipError_t {
         hipError_t e = b.ensure(std::max<size_t>(bytes, 64));
         if (e != hipSuccess) return e;
@@ -1523,6 +1612,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // split block 0: every fusion target's one hole at byte 2 (fuse_pos2),
     // so its block 1 is template only
     G.split_b0 = G.hole_in_b0 && G.fuse_pos2 ? graph_split_on() : 0u;
+    lap("midstates");
     if (getenv("RF_K2_STAMPS")) {  // diagnostic: per-phase times of workgroup 0 of each level
         HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
