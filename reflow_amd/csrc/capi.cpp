@@ -1725,6 +1725,10 @@ void graph_forms_from_env(GraphDev& G) {
         const char* w = getenv("RF_K2_SINK_LAST");  // (round-4 scripts: =0 the fill level)
         G.sink_at = v ? (uint32_t)std::min(std::max(atoi(v), 0), 4) : (w && atoi(w) == 0) ? 0u : 2u;
     }
+    {
+        const char* v = getenv("RF_K2_SPLIT_HALF");
+        G.split_half = v && atoi(v) == 0 ? 0u : 1u;
+    }
     const char* tv = getenv("RF_K2_THRU");
     const char* tw = getenv("RF_K2_THRU_WIDE");
     G.cfg_thru = tv ? (uint64_t)strtoull(tv, nullptr, 10) : kThruSlots;

@@ -2690,6 +2690,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         // workgroup on some CUs, whose four chain waves then share SIMDs.
         // RF_K2_HALF=0: off (A/B)
         if (graph_level_half(g, lvl)) {
+            if (!g.split_half) a.split = 0;
             uint64_t hg = (e - b + 31) / 32;
             if (hg > wg_cap) hg = wg_cap;
             uint64_t grid = hg;
