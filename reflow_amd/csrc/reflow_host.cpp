@@ -783,33 +783,83 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
     // 1. the originals reachable through Deps and MapFlow in post-order (deps,
     //    then the map flow, then the node: the order of flowMap.Put,
     //    flow.go:820-839); each one's index in it.
-    detail::FlatMap<const Flow*, uint32_t, detail::PtrHash> index;
+    using Index = detail::FlatMap<const Flow*, uint32_t, detail::PtrHash>;
+    Index index;
     std::vector<Flow*> post;
     struct Frame {
         Flow* f;
         size_t next;  // next dep (then MapFlow) to visit
     };
-    std::vector<Frame> st{{root, 0}};
-    index.reserve(1u << 16);
-    while (!st.empty()) {
-        Frame& fr = st.back();
-        Flow* f = fr.f;
-        const size_t nd = f->Deps.size() + (f->MapFlow ? 1 : 0);
-        if (fr.next == 0)  // (first visit: the deps' index slots and records on their way in)
-            for (Flow* d : f->Deps) {
-                index.prefetch(d);
-                __builtin_prefetch(d);
+    // the post-order from `start`, skipping (and marking) what `seen` holds
+    auto dfs = [](Flow* start, Index& seen, std::vector<Flow*>& out) {
+        std::vector<Frame> st{{start, 0}};
+        while (!st.empty()) {
+            Frame& fr = st.back();
+            Flow* f = fr.f;
+            const size_t nd = f->Deps.size() + (f->MapFlow ? 1 : 0);
+            if (fr.next == 0)  // (first visit: the deps' index slots and records on their way in)
+                for (Flow* d : f->Deps) {
+                    seen.prefetch(d);
+                    __builtin_prefetch(d);
+                }
+            if (fr.next < nd) {
+                Flow* d = fr.next < f->Deps.size() ? f->Deps[fr.next] : f->MapFlow;
+                ++fr.next;
+                if (!seen.find(d)) st.push_back(Frame{d, 0});
+                continue;
             }
-        if (fr.next < nd) {
-            Flow* d = fr.next < f->Deps.size() ? f->Deps[fr.next] : f->MapFlow;
-            ++fr.next;
-            if (!index.find(d)) st.push_back(Frame{d, 0});
-            continue;
+            st.pop_back();
+            if (seen.find(f)) continue;  // reached twice before its first visit completed
+            seen.insert(f, (uint32_t)out.size());
+            out.push_back(f);
         }
-        st.pop_back();
-        if (index.find(f)) continue;  // reached twice before its first visit completed
-        index.insert(f, (uint32_t)post.size());
-        post.push_back(f);
+    };
+    index.reserve(1u << 16);
+    const size_t nkids = root->Deps.size() + (root->MapFlow ? 1 : 0);
+    const unsigned lt = lower_threads(e);
+    if (nkids >= 256 && lt > 1) {
+        // A wide root (1000align: one dep per sample): the root's children in
+        // contiguous groups, each group's post-order on a host thread with a
+        // visited set of its own, then the groups concatenated in order with
+        // what an earlier group already emitted dropped.  That is the
+        // sequential order exactly: a DFS that finds a node already visited
+        // skips its whole subtree, and everything below a visited node was
+        // visited with it, so group g's walk with the earlier groups' nodes
+        // pre-visited emits its own walk's order minus those nodes.
+        auto kid = [&](size_t i) { return i < root->Deps.size() ? root->Deps[i] : root->MapFlow; };
+        const size_t ng = std::min<size_t>(nkids, 8ull * lt);
+        std::vector<std::vector<Flow*>> part(ng);
+        parallel_ranges(ng, 1, lt, [&](size_t r, size_t, size_t) {
+            Index seen;
+            seen.reserve(1u << 12);
+            for (size_t i = r * nkids / ng; i < (r + 1) * nkids / ng; ++i)
+                if (!seen.find(kid(i))) dfs(kid(i), seen, part[r]);
+        });
+        size_t total = 1;
+        for (const auto& v : part) total += v.size();
+        index.reserve(total);
+        post.reserve(total);
+        for (auto& v : part) {
+            for (Flow* f : v)
+                if (!index.find(f)) {
+                    index.insert(f, (uint32_t)post.size());
+                    post.push_back(f);
+                }
+            std::vector<Flow*>().swap(v);
+        }
+        if (!index.find(root)) {
+            index.insert(root, (uint32_t)post.size());
+            post.push_back(root);
+        }
+        if (getenv("RF_LOWER_CHECK_ORDER")) {  // diagnostic: the sequential walk, compared node for node
+            Index seen;
+            std::vector<Flow*> seq;
+            dfs(root, seen, seq);
+            if (seq != post) throw std::runtime_error("Canonicalize: parallel post-order differs from the sequential one");
+            fprintf(stderr, "[lower] canonicalize: parallel post-order == sequential (%zu nodes)\n", seq.size());
+        }
+    } else {
+        dfs(root, index, post);
     }
     const size_t n = post.size();
     pc.lap("canonicalize: post-order");
