@@ -294,6 +294,16 @@ struct Flow {
     std::string Data;                 // OpData
 };
 
+namespace detail {
+using PtrIndex = FlatMap<const Flow*, uint32_t, PtrHash>;
+// Canonicalize's walk (flow.go:820-839, the order of flowMap.Put): the nodes
+// reachable from root through Deps and MapFlow in post-order (deps, then the
+// map flow, then the node) into post, each one's position into index.  A
+// wide root's children are walked in groups on up to `threads` host threads;
+// the order is the sequential walk's exactly.
+void PostOrder(Flow* root, unsigned threads, std::vector<Flow*>& post, PtrIndex& index);
+}  // namespace detail
+
 // Owns Flow nodes (the Go GC's job in the reference).
 class FlowArena {
    public:

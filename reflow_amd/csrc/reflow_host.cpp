@@ -776,16 +776,10 @@ void Eval::SetFileID(const Digest& old_id, const Digest& new_id) {
 }
 
 // ---- Canonicalize ------------------------------------------------------------
-Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const std::string& U,
-                   std::unique_ptr<Eval>* lowered) {
-    if (lowered) lowered->reset();
-    PhaseClock pc;
-    // 1. the originals reachable through Deps and MapFlow in post-order (deps,
-    //    then the map flow, then the node: the order of flowMap.Put,
-    //    flow.go:820-839); each one's index in it.
-    using Index = detail::FlatMap<const Flow*, uint32_t, detail::PtrHash>;
-    Index index;
-    std::vector<Flow*> post;
+namespace detail {
+// (reflow_host.hpp)
+void PostOrder(Flow* root, unsigned threads, std::vector<Flow*>& post, PtrIndex& index) {
+    using Index = PtrIndex;
     struct Frame {
         Flow* f;
         size_t next;  // next dep (then MapFlow) to visit
@@ -815,8 +809,9 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
         }
     };
     index.reserve(1u << 16);
+    post.clear();
     const size_t nkids = root->Deps.size() + (root->MapFlow ? 1 : 0);
-    const unsigned lt = lower_threads(e);
+    const unsigned lt = threads;
     if (nkids >= 256 && lt > 1) {
         // A wide root (1000align: one dep per sample): the root's children in
         // contiguous groups, each group's post-order on a host thread with a
@@ -861,6 +856,19 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
     } else {
         dfs(root, index, post);
     }
+}
+}  // namespace detail
+
+Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const std::string& U,
+                   std::unique_ptr<Eval>* lowered) {
+    if (lowered) lowered->reset();
+    PhaseClock pc;
+    // 1. the originals reachable through Deps and MapFlow in post-order (deps,
+    //    then the map flow, then the node: the order of flowMap.Put,
+    //    flow.go:820-839); each one's index in it.
+    detail::PtrIndex index;
+    std::vector<Flow*> post;
+    detail::PostOrder(root, lower_threads(e), post, index);
     const size_t n = post.size();
     pc.lap("canonicalize: post-order");
     // 2. one copy per original, contiguous in post-order (f.Copy() +

@@ -408,7 +408,36 @@ static void test_flat_map() {
     }
 }
 
+// Canonicalize's walk: a wide root's children walked in groups on host
+// threads give the sequential post-order node for node (random DAGs with
+// shared subgraphs, map flows and a root that lists some children twice)
+static void test_post_order() {
+    std::mt19937_64 rng(7);
+    for (int trial = 0; trial < 4; ++trial) {
+        const size_t n = 20000 + 5000 * trial;
+        std::vector<reflow::Flow> nodes(n + 1);
+        for (size_t i = 0; i < n; ++i) {
+            const size_t lo = i > 400 ? i - 400 : 0;
+            const int nd = i ? (int)(rng() % 5) : 0;
+            for (int k = 0; k < nd; ++k) nodes[i].Deps.push_back(&nodes[lo + rng() % (i - lo)]);
+            if (i && rng() % 17 == 0) nodes[i].MapFlow = &nodes[lo + rng() % (i - lo)];
+        }
+        reflow::Flow& root = nodes[n];
+        const size_t nk = 300 + 700 * (size_t)trial;
+        for (size_t k = 0; k < nk; ++k) root.Deps.push_back(&nodes[rng() % n]);
+        if (trial & 1) root.MapFlow = &nodes[rng() % n];
+        std::vector<reflow::Flow*> seq, par;
+        reflow::detail::PtrIndex iseq, ipar;
+        reflow::detail::PostOrder(&root, 1, seq, iseq);
+        reflow::detail::PostOrder(&root, 4, par, ipar);
+        EXPECT(seq == par);
+        EXPECT(!seq.empty() && seq.back() == &root && iseq.size() == seq.size() && ipar.size() == par.size());
+        for (size_t k = 0; k < par.size(); ++k) EXPECT(ipar.find(par[k]) && *ipar.find(par[k]) == k);
+    }
+}
+
 int main() {
+    test_post_order();
     test_flat_map();
     test_fileset_json();
     test_bloom_wire();
