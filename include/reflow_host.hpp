@@ -321,18 +321,20 @@ class FlowArena {
     // n contiguous nodes, each constructed by make(block, lo, hi) -- placement
     // new of [lo, hi) -- which may split the range over threads (Canonicalize
     // copy-constructs its copies in place: no default construction first,
-    // and the pages are first touched by the threads that fill them).  make
-    // must construct every node, or throw having constructed none.
+    // and the pages are first touched by the threads that fill them; a
+    // multi-GB block sits on huge-page-advised storage, so filling it is not
+    // a page fault per 4 KiB).  make must construct every node, or throw
+    // having constructed none.
     template <class Make>
     Flow* NewN(size_t n, Make make) {
         Block b;
         b.n = n ? n : 1;
-        b.p = static_cast<Flow*>(::operator new(b.n * sizeof(Flow), std::align_val_t(alignof(Flow))));
+        b.p = static_cast<Flow*>(detail::huge_page_alloc(b.n * sizeof(Flow)));
         try {
             make(b.p, size_t(0), n);
             if (!n) new (b.p) Flow();
         } catch (...) {
-            ::operator delete(b.p, std::align_val_t(alignof(Flow)));
+            detail::huge_page_free(b.p, b.n * sizeof(Flow));
             throw;
         }
         blocks_.push_back(b);
@@ -344,7 +346,7 @@ class FlowArena {
     ~FlowArena() {
         for (Block& b : blocks_) {
             for (size_t i = 0; i < b.n; ++i) b.p[i].~Flow();
-            ::operator delete(b.p, std::align_val_t(alignof(Flow)));
+            detail::huge_page_free(b.p, b.n * sizeof(Flow));
         }
     }
 
