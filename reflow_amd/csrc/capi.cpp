@@ -1727,7 +1727,7 @@ void graph_forms_from_env(GraphDev& G) {
     }
     {
         const char* v = getenv("RF_K2_SPLIT_HALF");
-        G.split_half = v && atoi(v) == 0 ? 0u : 1u;
+        G.split_half = v && atoi(v) == 1 ? 1u : 0u;
     }
     const char* tv = getenv("RF_K2_THRU");
     const char* tw = getenv("RF_K2_THRU_WIDE");

@@ -149,7 +149,10 @@ struct GraphDev {
     // half of a fusion target's block 0 and builds its template-only block 1
     // during the job before it; set at load / restore (RF_K2_SPLIT=0: off)
     uint32_t split_b0 = 0;  // 1: the producer expands K+W[32..63]; 2: K+W[16..63]
-    uint32_t split_half = 1;  // split block 0 in the 32-job workgroups too (RF_K2_SPLIT_HALF at load)
+    // split block 0 in the 32-job workgroups too (RF_K2_SPLIT_HALF=1 at load;
+    // off by default: the 8-rank piece 0.2997 -> 0.2973 ms without it,
+    // profiles/r04/sw3)
+    uint32_t split_half = 0;
 };
 // Midstates of the jobs' leading constant blocks, hashed once at load: job i
 // (internal order) hashes lead[i] blocks of its template from block

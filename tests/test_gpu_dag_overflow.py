@@ -58,20 +58,24 @@ def test_overflow_lanes_match_oracle(ctx, monkeypatch, ovf):
     gp.close()
 
 
-def test_half_workgroups_match_oracle(ctx, monkeypatch):
+@pytest.mark.parametrize("split_half", ["0", "1"])
+def test_half_workgroups_match_oracle(ctx, monkeypatch, split_half):
     """Half workgroups (k2_level_pl<2, false, 32>: one chain wave and the
     producer, 32 jobs) run a latency-form level estimated at more than 64
     chains per CU and at most 96: on a pretended 6-CU chip, 512 marked slots
     (2 % of the leaf files) put the Exec level there.  Its pass structure,
     split block 0 and sink lanes are those of the 64-job form; the table must
     equal the 64-job form's (the device's CUs: one 64-job round) and the
-    oracle's, step after step."""
+    oracle's, step after step; with and without block 0 split in them
+    (RF_K2_SPLIT_HALF, read at load)."""
     dag = Dag1000(400, 32)
     a = dag.arrays()
     every = np.arange(a["n_slots"], dtype=np.uint32)
     monkeypatch.setenv("RF_K2_OVF_CU", "6")
+    monkeypatch.setenv("RF_K2_SPLIT_HALF", split_half)
     g = load(ctx, dag)
     monkeypatch.delenv("RF_K2_OVF_CU")
+    monkeypatch.delenv("RF_K2_SPLIT_HALF")
     gp = load(ctx, dag)
     for gg in (g, gp):
         gg.recompute(full=True)
