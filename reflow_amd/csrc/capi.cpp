@@ -1154,13 +1154,13 @@ int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_
         (e = gr->b_dirty.ensure(4ull * (J + 1))) != hipSuccess ||
         (e = gr->b_list.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_lmeta.ensure(32ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_counts.ensure(8ull * (L + 1))) != hipSuccess ||  // two halves (plain-step parity)
+        (e = gr->b_counts.ensure(8ull * (L + 1 + kCountsExtra))) != hipSuccess ||  // two halves (plain-step parity)
         (e = gr->b_counts_last.ensure(4ull * (L + 1))) != hipSuccess ||
         (e = gr->b_lvl_start.ensure(std::max<size_t>(4ull * (L + 1), 64))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph alloc: %s", hipGetErrorString(e));
     HIPC(sync_memset(ctx, gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
     HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * (J + 1)));
-    HIPC(sync_memset(ctx, gr->b_counts.p, 0, 8ull * (L + 1)));
+    HIPC(sync_memset(ctx, gr->b_counts.p, 0, 8ull * (L + 1 + kCountsExtra)));
     HIPC(sync_memset(ctx, gr->b_counts_last.p, 0, 4ull * (L + 1)));
     G.meta = gr->b_meta.as<uint4>();
     G.holes = gr->b_holes.as<uint2>();
@@ -1172,7 +1172,7 @@ int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_
     G.list = gr->b_list.as<uint32_t>();
     G.lmeta = gr->b_lmeta.as<uint4>();
     G.counts = gr->b_counts.as<uint32_t>();
-    G.counts_other = G.counts + (L + 1);
+    G.counts_other = G.counts + (L + 1 + kCountsExtra);
     G.counts_last = gr->b_counts_last.as<uint32_t>();
     gr->last_counts = G.counts_last;
     G.lvl_start_dev = gr->b_lvl_start.as<uint32_t>();
@@ -1728,6 +1728,8 @@ void graph_forms_from_env(GraphDev& G) {
     {
         const char* v = getenv("RF_K2_SPLIT_HALF");
         G.split_half = v && atoi(v) == 1 ? 1u : 0u;
+        const char* m = getenv("RF_K2_DBG_MARK");
+        G.dbg_mark = m ? (uint32_t)atoi(m) : 0u;
     }
     const char* tv = getenv("RF_K2_THRU");
     const char* tw = getenv("RF_K2_THRU_WIDE");
@@ -1862,7 +1864,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
     gr->last_counts = G.counts_last;
     if (full) {
         HIPC(hipMemsetAsync(G.dirty, 0, 4ull * (G.n_jobs + 1), s));
-        HIPC(hipMemsetAsync(G.counts_other, 0, 4ull * (G.n_levels + 1), s));  // both halves clear
+        HIPC(hipMemsetAsync(G.counts_other, 0, 4ull * (G.n_levels + 1 + kCountsExtra), s));  // both halves clear
     }
     return RF_OK;
 }
@@ -2010,6 +2012,22 @@ extern "C" int rf_graph_update_recompute_async(rf_graph* gr, const void* d_slots
     return RF_OK;
 }
 
+// The last step's jobs per level, [L] the jobs hashed inside fused chains
+// (a plain step's cursor half: its fused parts folded in; k3_step_end has
+// already folded them into counts_last).  Synchronizes s.
+int graph_read_counts(rf_graph* gr, hipStream_t s, std::vector<uint32_t>& counts) {
+    const uint32_t L = gr->g.n_levels;
+    const bool half = gr->last_counts != gr->g.counts_last;
+    std::vector<uint32_t> raw(L + 1 + (half ? kCountsExtra : 0u), 0);
+    if (L) HIPC(hipMemcpyAsync(raw.data(), gr->last_counts, 4ull * raw.size(), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (L && half)
+        for (uint32_t k = 0; k < kFusedParts; ++k) raw[L] += raw[L + 1 + kPartStride * k];
+    raw.resize(L + 1);
+    counts.swap(raw);
+    return RF_OK;
+}
+
 extern "C" int rf_graph_recompute_async(rf_graph* gr, int full, void* stream) {
     ARG(gr, "null graph");
     std::lock_guard<std::mutex> lk(gr->ctx->mu);
@@ -2088,11 +2106,8 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
     const int rc0 = graph_recompute_locked(gr, full, ctx->stream);
     gr->time_next = false;
     if (rc0) return rc0;
-    std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
-    if (gr->g.n_levels)  // [L]: jobs hashed inside fused chains
-        HIPC(hipMemcpyAsync(counts.data(), gr->last_counts, 4ull * (gr->g.n_levels + 1),
-                            hipMemcpyDeviceToHost, ctx->stream));
-    HIPC(hipStreamSynchronize(ctx->stream));
+    std::vector<uint32_t> counts;
+    if (int rc = graph_read_counts(gr, ctx->stream, counts)) return rc;
     uint64_t tot = 0;
     for (uint32_t l = 0; l <= gr->g.n_levels; ++l) tot += counts[l];
     if (gr->g.wgst && !full) wgst_report(gr);

@@ -78,6 +78,13 @@ constexpr uint8_t kLvlForm = 3, kLvlSinkMin = 0x20, kLvlFill = 0x40, kLvlSink = 
 // material staged in LDS, K1's 8-instruction octo chain
 constexpr uint8_t kLvlOct = 0x10;
 constexpr uint32_t kOctMaxBlocks = 32, kOctMaxHoles = 64, kOctMaxLevel = 4096;
+// The fused-job count (jobs hashed inside fused chains, never queued) is
+// added by every chain wave; one counter took every wave's atomic in turn at
+// the memory side (~19 ns each: the 100M step's lean mark kernel, 2,200
+// waves, waited 41 us for them).  It is spread over kFusedParts counters
+// kPartStride words apart after each cursor half's L + 1 level counts, and
+// folded into [L] where it is read (k3_step_end, graph_read_counts).
+constexpr uint32_t kFusedParts = 64, kPartStride = 32, kCountsExtra = kFusedParts * kPartStride;
 struct GraphDev {
     uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;
     // jobs in internal (level) order
@@ -94,7 +101,7 @@ struct GraphDev {
     uint32_t* dirty = nullptr;       // [J] queued-this-step flag per internal id (a word each)
     uint32_t* list = nullptr;        // [J] per-level work lists (level l at lvl_start[l])
     uint4* lmeta = nullptr;          // [2J] each listed job's record, at its list position
-    uint32_t* counts = nullptr;      // [L+1] list lengths (append cursors); [L] = fused jobs hashed
+    uint32_t* counts = nullptr;      // [L+1] list lengths (append cursors); [L] + the parts after it = fused jobs hashed
     uint32_t* counts_last = nullptr; // [L+1] jobs hashed per level by the last recompute; [L] fused
     // Plain-launch incremental steps alternate between two halves of the
     // cursor array (counts = the half the next step appends to and reads,
@@ -153,6 +160,7 @@ struct GraphDev {
     // off by default: the 8-rank piece 0.2997 -> 0.2973 ms without it,
     // profiles/r04/sw3)
     uint32_t split_half = 0;
+    uint32_t dbg_mark = 0;  // diagnostic (RF_K2_DBG_MARK=1 at load): the lean mark kernel skips its fused-job count (stats wrong, digests right)
 };
 // Midstates of the jobs' leading constant blocks, hashed once at load: job i
 // (internal order) hashes lead[i] blocks of its template from block

@@ -65,6 +65,7 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s, uint32_t lvl_l
 bool graph_plain_steps();  // incremental steps are plain launches (not RF_K2_GRAPH=1)
 void graph_forms_from_env(rf::GraphDev& G);  // form thresholds at load / restore
 uint32_t graph_split_on();
+int graph_read_counts(rf_graph* gr, hipStream_t s, std::vector<uint32_t>& counts);
 uint32_t graph_ovf_cus(const rf_ctx* ctx, uint32_t* mode);  // RF_K2_OVF_CU / RF_K2_OVF                        // RF_K2_SPLIT (default on)
 int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes);
 void graph_part_release(rf_graph* gr);

@@ -120,11 +120,18 @@ struct WgStamp {
     }
 };
 
+// This wave's fused-job counter (engine.h kFusedParts): one of the parts
+// after the half's level counts, picked by workgroup and wave.
+__device__ __forceinline__ uint32_t* fused_part(const LevelArgs& a) {
+    const uint32_t k = (blockIdx.x * 5u + (threadIdx.x >> 6)) & (kFusedParts - 1);
+    return &a.counts[a.n_levels + 1 + kPartStride * k];
+}
+
 // (first level kernel of a plain incremental step) the previous step's
 // cursor half back to zero -- nobody reads or appends to it during this step
 __device__ __forceinline__ void zero_other_counts(const LevelArgs& a) {
     if (a.zero_counts && blockIdx.x == 0)
-        for (uint32_t l = threadIdx.x; l <= a.n_levels; l += blockDim.x) a.zero_counts[l] = 0;
+        for (uint32_t l = threadIdx.x; l < a.n_levels + 1 + kCountsExtra; l += blockDim.x) a.zero_counts[l] = 0;
 }
 
 // Reverse edges of an INPUT slot: bit 31 of the level field flags its
@@ -850,7 +857,7 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
                 }
                 propagate_pre(a, cb, ce, pre);
                 const uint64_t fb = __ballot(nx != ~0u);
-                if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));  // fused jobs hashed
+                if (lane == 0 && fb) atomicAdd(fused_part(a), (uint32_t)__popcll(fb));  // fused jobs hashed
             }
             fslot = has ? m1.x : ~0u;
             has = nx != ~0u;
@@ -1706,7 +1713,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                         propagate_pre(a, cb, ce, pre);
                     }
                     const uint64_t fb = __ballot(own && nx != ~0u);
-                    if (lane == 0 && fb) atomicAdd(&a.counts[a.n_levels], (uint32_t)__popcll(fb));
+                    if (lane == 0 && fb) atomicAdd(fused_part(a), (uint32_t)__popcll(fb));
                 }
                 if (kIsProd && ((kCB && a.cb0) || pp3)) pend = true;
 
@@ -1866,11 +1873,11 @@ __device__ __forceinline__ uint32_t hash_fused_chain(const LevelArgs& a, uint32_
     return hashed;
 }
 
-// Adds the wave's fused-chain job counts to counts[L] (jobs hashed outside
+// Adds the wave's fused-chain job counts to its fused part (jobs hashed outside
 // the level lists, k3_step_end / rf_graph_recompute's total).
 __device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed) {
     for (int o = 32; o > 0; o >>= 1) hashed += __shfl_xor(hashed, o, 64);
-    if (__lane_id() == 0 && hashed) atomicAdd(&a.counts[a.n_levels], hashed);
+    if (__lane_id() == 0 && hashed) atomicAdd(fused_part(a), hashed);
 }
 
 // A changed input slot s (digest nlo/nhi, already stored; cp0/cp1 its
@@ -2121,7 +2128,7 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
         hashed += hash_fused_chain_lean(a, ring, p, m0, m1, s, nlo, nhi);
         propagate(a, c, ce);  // the slot's other consumers
     }
-    count_fused(a, hashed);
+    if (a.dbg_twice != 16) count_fused(a, hashed);
 }
 
 // ---- the octo form: levels of few long jobs (GraphDev kLvlOct) ---------------
@@ -2457,11 +2464,18 @@ __global__ __launch_bounds__(kMarkBlock) void k_part_apply(const uint32_t* __res
 // End of a recompute: record what each level hashed, reset the lists.
 __global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __restrict__ ls, uint32_t L,
                             int full) {
-    // counts[L]: jobs hashed inside fused chains (never queued)
-    for (uint32_t l = threadIdx.x; l <= L; l += blockDim.x) {
-        last[l] = l == L ? (full ? 0u : counts[L]) : full ? ls[l + 1] - ls[l] : counts[l];
+    // counts[L] + the fused parts: jobs hashed inside fused chains (never queued)
+    for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
+        last[l] = full ? ls[l + 1] - ls[l] : counts[l];
         counts[l] = 0;
     }
+    if (threadIdx.x == 0) {
+        uint32_t f = counts[L];
+        for (uint32_t k = 0; k < kFusedParts; ++k) f += counts[L + 1 + kPartStride * k];
+        last[L] = full ? 0u : f;
+    }
+    __syncthreads();
+    for (uint32_t l = L + threadIdx.x; l < L + 1 + kCountsExtra; l += blockDim.x) counts[l] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_gather_slots(const uint8_t* __restrict__ slots,
@@ -2502,6 +2516,7 @@ static uint32_t grid_mark(uint64_t items) {
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
+    if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic: k3_mark_slots_lf skips its count)
     return a;
 }
 

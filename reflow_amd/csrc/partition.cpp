@@ -186,10 +186,8 @@ static int part_gather(rf_graph* gr, rf_comm* comm, rf_host_allgather_fn fn, voi
 }
 
 static int part_counts(rf_graph* gr, hipStream_t s, uint64_t* tot) {
-    std::vector<uint32_t> counts(gr->g.n_levels + 1, 0);
-    if (gr->g.n_levels)
-        HIPC(hipMemcpyAsync(counts.data(), gr->last_counts, 4ull * (gr->g.n_levels + 1), hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
+    std::vector<uint32_t> counts;
+    if (int rc = graph_read_counts(gr, s, counts)) return rc;
     for (uint32_t c : counts) *tot += c;
     return RF_OK;
 }
