@@ -85,6 +85,20 @@ constexpr uint32_t kOctMaxBlocks = 32, kOctMaxHoles = 64, kOctMaxLevel = 4096;
 // kPartStride words apart after each cursor half's L + 1 level counts, and
 // folded into [L] where it is read (k3_step_end, graph_read_counts).
 constexpr uint32_t kFusedParts = 64, kPartStride = 32, kCountsExtra = kFusedParts * kPartStride;
+// The flow step's control block (k2_flow), after each cursor half's fused
+// parts: per level F (jobs finished), Q (jobs queued by flow lanes) and D
+// (jobs parked), then the watermark, the ready queue's tail and head and the
+// parking cursor words, each on a 128-B line of its own.  Zero between steps
+// (the half is zeroed like the level counts).
+constexpr uint32_t kFlowCtl = 128;
+constexpr uint32_t kFlowLW = 0, kFlowTail = 32, kFlowHead = 64;
+constexpr uint32_t kFlowList = 96;  // the candidate-list cursor
+constexpr uint32_t kFlowMaxLevels = 4096;  // range levels one flow launch takes (its LDS tables)
+constexpr uint32_t kFlowErr = 100;  // nonzero: the launch gave up (k2_flow kFlowTimeout)
+__host__ __device__ constexpr uint32_t counts_flow_base(uint32_t L) { return L + 1 + kCountsExtra; }
+__host__ __device__ constexpr uint32_t counts_half_words(uint32_t L) {
+    return counts_flow_base(L) + 3 * L + kFlowCtl;
+}
 struct GraphDev {
     uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;
     // jobs in internal (level) order
@@ -161,6 +175,34 @@ struct GraphDev {
     // profiles/r04/sw3)
     uint32_t split_half = 0;
     uint32_t dbg_mark = 0;  // diagnostic (RF_K2_DBG_MARK=1 at load): the lean mark kernel skips its fused-job count (stats wrong, digests right)
+    // ---- the flow step (k2_flow: readiness-driven, no level barrier) ----
+    // A queueable job's "head" is itself; a fusion target's is its chain's
+    // first job.  cout_rng[h] / cout: every queueable consumer {job, level}
+    // of any slot of h's fused chain except the fusion edges (the jobs h's
+    // chain completes for); wlev[k]: the highest level of a queueable head
+    // among k's producers (k cannot gain producers once every level below it
+    // has drained); pend[k]: producers of k queued this step and not yet
+    // finished (zero between steps); dstart[w]: the parking list of jobs
+    // with wlev w; rq / dq: the ready queue and parking lists, entries tagged
+    // with the step's epoch.  All built at load (rf_graph_load) or restored.
+    uint2* cout_rng = nullptr;
+    uint2* cout = nullptr;
+    uint2* jlv = nullptr;  // [J] {level, wlev}
+    uint32_t* pend = nullptr;
+    uint32_t* dstart = nullptr;
+    unsigned long long* rq = nullptr;
+    unsigned long long* dq = nullptr;
+    uint64_t n_cout = 0;
+    uint32_t epoch = 0;
+    // flow steps (rf_graph_set_flow): 0 never, 1 (default) when the step's
+    // first launchable levels up to the fill level all run in the throughput
+    // form, 2 every launchable level whenever possible (tests)
+    uint32_t flow_mode = 1;
+    // this step's flow range, fixed by its first mark (graph_flow_decide):
+    // levels [flo, fhi] and the sink level fsink run in one k2_flow launch;
+    // flo = ~0u: the step runs level by level
+    uint32_t flo = ~0u, fhi = 0, fsink = ~0u;
+    uint32_t last_flow = 0;  // the last plain step ran a flow launch (rf_graph_stats)
 };
 // Midstates of the jobs' leading constant blocks, hashed once at load: job i
 // (internal order) hashes lead[i] blocks of its template from block
@@ -174,7 +216,7 @@ struct MarkArgs {
     const uint32_t* sl;
     const uint8_t* dig;
     uint32_t n;
-    alignas(16) unsigned char a[192];  // the kernel's LevelArgs (k2_graph.hip), by value
+    alignas(16) unsigned char a[320];  // the kernel's LevelArgs (k2_graph.hip), by value
     void* ptrs[4];
 };
 void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* digests, uint32_t n,
@@ -185,6 +227,8 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipSt
 bool graph_level_lf(const GraphDev& g, uint32_t lvl);
 bool graph_level_half(const GraphDev& g, uint32_t lvl);
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
+// The flow launch (k2_flow) of a plain incremental step over g.flo..g.fhi + g.fsink.
+hipError_t launch_graph_flow(const GraphDev& g, hipStream_t s, uint32_t* zero_counts);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);
 // Partitioned DAG exchange: pack changed exports (bits at bit0 + i), test the

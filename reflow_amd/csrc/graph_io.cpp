@@ -37,7 +37,7 @@ namespace {
 
 constexpr char kMagic[8] = {'R', 'F', 'G', 'R', 'A', 'P', 'H', '1'};
 constexpr char kEnd[8] = {'R', 'F', 'G', 'R', 'E', 'N', 'D', '1'};
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;  // 2: + the flow step's sections (jlv, cout_rng, cout, dstart)
 constexpr uint64_t kChunk = 64ull << 20;   // checksum granule
 constexpr uint64_t kStage = 256ull << 20;  // D2H / H2D staging (4 chunks)
 
@@ -49,7 +49,8 @@ struct Header {
     uint32_t n_jobs, n_slots, n_levels, max_level_jobs;
     uint64_t n_holes, tmpl_bytes, total_blocks, chunk;
     uint64_t n_sections;
-    uint8_t reserved[128 - 8 - 6 * 4 - 5 * 8];
+    uint64_t n_cout;  // chain-out edges (the flow step)
+    uint8_t reserved[128 - 8 - 6 * 4 - 6 * 8];
 };
 static_assert(sizeof(Header) == 128, "header layout");
 
@@ -78,6 +79,10 @@ std::vector<Section> sections(rf_graph* gr, std::vector<uint32_t>& lvl, std::vec
         {"slots", 32 * S, nullptr, gr->b_slots.p},
     };
     if (has_mid) v.push_back({"mid", 32 * J, nullptr, gr->b_mid.p});
+    v.push_back({"jlv", 8 * J, nullptr, gr->b_jlv.p});
+    v.push_back({"cout_rng", 8 * J, nullptr, gr->b_cout_rng.p});
+    v.push_back({"cout", 8 * G.n_cout, nullptr, gr->b_cout.p});
+    v.push_back({"dstart", 4 * (L + 1), nullptr, gr->b_dstart.p});
     return v;
 }
 
@@ -113,6 +118,22 @@ struct Validator {
     std::vector<uint8_t> produced;         // slot is some job's output
     std::vector<uint32_t> cons_ptr;        // host copy: slot -> its reverse-edge range
     uint64_t slot = 0;                     // cons_job cursor: the slot whose range holds the next edge
+    // fusion targets: job t fused behind j must have exactly one
+    // hole reading j's out slot -- at byte 2 when the file says kFusePos2 (the
+    // chain builds its block 0 in registers, from the IV: no midstate) --
+    // else a file with valid checksums restores into wrong digests
+    std::vector<uint32_t> exp_slot;                   // target -> its producer's out slot (~0: not a target)
+    std::vector<std::pair<uint64_t, uint32_t>> tgt_holes;  // (the target's hole index, expected slot), ascending
+    size_t tgt_cur = 0;
+    uint64_t jl_cur = 0, jl_lv = 0;        // jlv cursor: the level of the next record
+    std::vector<uint64_t> wcount;          // jobs per wlev (the parking lists' sizes)
+    std::vector<uint32_t> dstart;          // host copy
+
+    // after the structure sections: every fusion target's hole was seen
+    int done() const {
+        if (tgt_cur != tgt_holes.size()) return fail(RF_EINTEGRITY, "graph restore: fusion target holes missing");
+        return RF_OK;
+    }
 
     Validator(const Header& hh, const std::vector<uint32_t>& l, const std::vector<uint8_t>& in, std::vector<uint32_t>& os)
         : h(hh), lvl(l), inc(in), out_slot(os) {}
@@ -138,7 +159,7 @@ struct Validator {
         const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
         const uint64_t J = h.n_jobs, S = h.n_slots, H = h.n_holes, TB = h.tmpl_bytes / 64;
         if (!strcmp(name, "meta")) {
-            if (o == 0) one_hole.assign(J, 0), produced.assign(S, 0);
+            if (o == 0) one_hole.assign(J, 0), produced.assign(S, 0), exp_slot.assign(J, ~0u);
             for (uint64_t r = 0; r < n / 32; ++r) {
                 const uint32_t* m = w + 8 * r;
                 if ((uint64_t)m[0] + m[1] > TB || m[2] > m[3] || m[3] > H || m[4] >= S || m[5] > m[6] || m[6] > H ||
@@ -155,12 +176,30 @@ struct Validator {
                 out_slot[j] = m[4];
                 one_hole[j] = m[3] - m[2] == 1;
                 produced[m[4]] = 1;
+                if (exp_slot[j] != ~0u) {  // j is a fusion target (its producer's record came first)
+                    if (m[3] - m[2] != 1) return fail(RF_EINTEGRITY, "graph restore: fusion target %llu has %u holes",
+                                                     (unsigned long long)j, m[3] - m[2]);
+                    tgt_holes.push_back({m[2], exp_slot[j]});
+                }
+                if (m[7] != 0xffffffffu) {
+                    if (m[7] <= j || exp_slot[m[7]] != ~0u)
+                        return fail(RF_EINTEGRITY, "graph restore: fusion target of job %llu inconsistent",
+                                    (unsigned long long)j);
+                    exp_slot[m[7]] = m[4];
+                }
             }
         } else if (!strcmp(name, "holes")) {
-            for (uint64_t r = 0; r < n / 8; ++r)
+            for (uint64_t r = 0; r < n / 8; ++r) {
+                const uint64_t hi = o / 8 + r;
                 if (w[2 * r + 1] >= S || w[2 * r] >= (1u << 24))
-                    return fail(RF_EINTEGRITY, "graph restore: hole %llu out of range",
-                                (unsigned long long)(o / 8 + r));
+                    return fail(RF_EINTEGRITY, "graph restore: hole %llu out of range", (unsigned long long)hi);
+                if (tgt_cur < tgt_holes.size() && tgt_holes[tgt_cur].first == hi) {
+                    if (w[2 * r + 1] != tgt_holes[tgt_cur].second || ((h.flags & 2u) && w[2 * r] != 2))  // (kFusePos2)
+                        return fail(RF_EINTEGRITY, "graph restore: fusion target hole %llu inconsistent",
+                                    (unsigned long long)hi);
+                    ++tgt_cur;
+                }
+            }
         } else if (!strcmp(name, "cons_ptr")) {
             if (o == 0) cons_ptr.reserve(S + 1);
             for (uint64_t r = 0; r < n / 4; ++r) {
@@ -184,6 +223,45 @@ struct Validator {
                 if (x >= J || y >= h.n_levels || x < lvl[y] || x >= lvl[y + 1] || slot >= S ||
                     (fused && (e != cons_ptr[slot] || produced[slot] || !one_hole[x])))
                     return fail(RF_EINTEGRITY, "graph restore: reverse edge %llu inconsistent", (unsigned long long)e);
+            }
+        } else if (!strcmp(name, "mid")) {
+            // a kFusePos2 fusion target starts from the IV (k2_level_pl hands
+            // its block 0 over in registers and never loads its midstate)
+            static const uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                           0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+            for (uint64_t r = 0; r < n / 32; ++r) {
+                const uint64_t j = o / 32 + r;
+                if ((h.flags & 2u) && exp_slot[j] != ~0u && memcmp(w + 8 * r, IV, 32) != 0)
+                    return fail(RF_EINTEGRITY, "graph restore: fusion target %llu has a midstate", (unsigned long long)j);
+            }
+        } else if (!strcmp(name, "jlv")) {  // {level, wlev}: the level the layout gives, wlev below it
+            if (o == 0) wcount.assign(h.n_levels + 1, 0);
+            for (uint64_t r = 0; r < n / 8; ++r, ++jl_cur) {
+                while (jl_lv < h.n_levels && lvl[jl_lv + 1] <= jl_cur) ++jl_lv;
+                if (w[2 * r] != jl_lv || w[2 * r + 1] >= h.n_levels)
+                    return fail(RF_EINTEGRITY, "graph restore: flow record %llu inconsistent", (unsigned long long)jl_cur);
+                wcount[w[2 * r + 1]]++;
+            }
+        } else if (!strcmp(name, "cout_rng")) {
+            for (uint64_t r = 0; r < n / 8; ++r)
+                if (w[2 * r] > w[2 * r + 1] || w[2 * r + 1] > h.n_cout)
+                    return fail(RF_EINTEGRITY, "graph restore: chain-out range %llu out of range",
+                                (unsigned long long)(o / 8 + r));
+        } else if (!strcmp(name, "cout")) {  // {job, its level}, as the reverse edges
+            for (uint64_t r = 0; r < n / 8; ++r) {
+                const uint32_t x = w[2 * r], y = w[2 * r + 1];
+                if (x >= J || y >= h.n_levels || x < lvl[y] || x >= lvl[y + 1])
+                    return fail(RF_EINTEGRITY, "graph restore: chain-out edge %llu inconsistent",
+                                (unsigned long long)(o / 8 + r));
+            }
+        } else if (!strcmp(name, "dstart")) {  // the parking lists: at least the jobs of each wlev
+            for (uint64_t r = 0; r < n / 4; ++r) dstart.push_back(w[r]);
+            if (o + n == 4ull * (h.n_levels + 1)) {
+                if (dstart[0] != 0 || dstart[h.n_levels] > J)
+                    return fail(RF_EINTEGRITY, "graph restore: parking lists inconsistent");
+                for (uint32_t l = 0; l < h.n_levels; ++l)
+                    if (dstart[l + 1] < dstart[l] || dstart[l + 1] - dstart[l] < wcount[l])
+                        return fail(RF_EINTEGRITY, "graph restore: parking lists inconsistent");
             }
         }
         return RF_OK;
@@ -236,6 +314,7 @@ extern "C" int rf_graph_save(rf_graph* gr, const char* path) {
     h.total_blocks = gr->total_blocks;
     h.chunk = kChunk;
     h.n_sections = secs.size();
+    h.n_cout = G.n_cout;
     const std::string tmp = std::string(path) + ".tmp";
     File out;
     if (!(out.f = fopen(tmp.c_str(), "wb"))) return fail(RF_EIO, "graph save: cannot create %s", tmp.c_str());
@@ -288,7 +367,8 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
         return fail(RF_EINVAL, "graph restore: %s is not a graph checkpoint", path);
     if (h.version != kVersion || h.chunk != kChunk)
         return fail(RF_EINVAL, "graph restore: checkpoint version %u not supported", h.version);
-    if (h.n_sections != ((h.flags & kHasMid) ? 10u : 9u) || h.n_jobs > (1u << 31) || h.n_levels > h.n_jobs + 1)
+    if (h.n_sections != ((h.flags & kHasMid) ? 14u : 13u) || h.n_jobs > (1u << 31) || h.n_levels > h.n_jobs + 1 ||
+        h.n_cout >= 0xffffffffull)
         return fail(RF_EINTEGRITY, "graph restore: corrupt header");
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
@@ -308,7 +388,8 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     }
     graph_forms_from_env(G);
     G.n_cu = graph_ovf_cus(ctx, &G.ovf_mode);
-    if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes)) return rc;
+    if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes, h.n_cout))
+        return rc;
     const bool has_mid = (h.flags & kHasMid) != 0;
     if (has_mid) {
         HIPC(gr->b_mid.ensure(std::max<size_t>(32ull * h.n_jobs, 64)));
@@ -343,6 +424,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
         if (!sc.dev)
             if (int rc = val.host_done(sc.name, &ext2int)) return rc;
     }
+    if (int rc = val.done()) return rc;
     uint64_t nd = 0;
     uint8_t root[32], want[32], end[8];
     if (!get(&nd, 8) || nd != digests.size() / 32) return fail(RF_EINTEGRITY, "graph restore: checksum list damaged");

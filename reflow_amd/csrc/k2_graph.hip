@@ -84,7 +84,23 @@ struct LevelArgs {
     // chain per lane in those lane workgroups too, before the sinks
     uint32_t sink_wg = 0, ovf = 0;
     uint32_t handoff = 1;  // k2_level_pl cb0 = 2: the producer hands the chain its next target's operands
+    // the flow step (k2_flow, GraphDev "flow"): levels [flo, fhi] and fsink
+    // run in one readiness-driven launch; flo = ~0u: none this step (the mark
+    // kernels then queue as before)
+    const uint2* __restrict__ cout_rng = nullptr;
+    const uint2* __restrict__ cout = nullptr;
+    const uint2* __restrict__ jlv = nullptr;  // [J] {level, wlev}
+    uint32_t* pend = nullptr;
+    const uint32_t* __restrict__ dstart = nullptr;
+    unsigned long long* rq = nullptr;
+    unsigned long long* dq = nullptr;
+    uint32_t flo = ~0u, fhi = 0, fsink = ~0u, epoch = 0;
 };
+
+// Whether level l runs in this step's flow launch.
+__device__ __forceinline__ bool flow_level(const LevelArgs& a, uint32_t l) {
+    return a.flo != ~0u && ((l >= a.flo && l <= a.fhi) || (l == a.fsink && l != ~0u));
+}
 
 // Entries of a level launch: the level's own list (from its end when rev),
 // then the attached sink list.  Offsets into a.list / a.lmeta.
@@ -131,7 +147,7 @@ __device__ __forceinline__ uint32_t* fused_part(const LevelArgs& a) {
 // cursor half back to zero -- nobody reads or appends to it during this step
 __device__ __forceinline__ void zero_other_counts(const LevelArgs& a) {
     if (a.zero_counts && blockIdx.x == 0)
-        for (uint32_t l = threadIdx.x; l < a.n_levels + 1 + kCountsExtra; l += blockDim.x) a.zero_counts[l] = 0;
+        for (uint32_t l = threadIdx.x; l < counts_half_words(a.n_levels); l += blockDim.x) a.zero_counts[l] = 0;
 }
 
 // Reverse edges of an INPUT slot: bit 31 of the level field flags its
@@ -183,17 +199,30 @@ __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint3
 // Mark consumers [c, ce) of the lanes whose slot changed (c == ce otherwise)
 // dirty, queueing the newly dirty ones (their records are fetched beside the
 // dirty-flag atomic).  Wave-uniform loop.
+// A job k newly queued at a level of this step's flow range (by the mark
+// kernels, before the flow launch, or by a flow lane): every consumer its
+// chain completes for waits for it -- pend + 1 per chain-out edge inside the
+// range (k2_flow decrements them when k's chain ends).
+__device__ __forceinline__ void flow_count_out(const LevelArgs& a, uint2 r) {
+    for (uint32_t e = r.x; e < r.y; ++e) {
+        const uint2 o = a.cout[e];
+        if (flow_level(a, o.y)) atomicAdd(&a.pend[o.x], 1u);
+    }
+}
+
 __device__ __forceinline__ void propagate(const LevelArgs& a, uint32_t c, uint32_t ce) {
     while (__any(c < ce)) {
         bool need = false;
-        uint2 jl = make_uint2(0, 0);
+        uint2 jl = make_uint2(0, 0), cr = make_uint2(0, 0);
         uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
         if (c < ce) {
             jl = a.cons[c++];
             q0 = a.meta[2ull * jl.x];
             q1 = a.meta[2ull * jl.x + 1];
+            if (flow_level(a, jl.y)) cr = a.cout_rng[jl.x];  // (the mark kernels of a flow step)
             need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
         }
+        if (need) flow_count_out(a, cr);
         append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
 }
@@ -232,7 +261,32 @@ struct PendingHole {
     uint4 lo, hi;
 };
 
-struct MatCursor {
+// Agent-scope (sc1) accesses: the flow step hands digests between CUs inside
+// one launch, and a CU's L1 is never refreshed by another CU's stores
+// (MI355X_MICROARCH.md, inter-workgroup visibility): the producer stores a
+// digest write-through and drains (vmcnt(0)) before the atomic that signals
+// it; the consumer, told by an atomic, reads it with sc1 loads.
+__device__ __forceinline__ uint32_t ld_ag(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_ag64(const unsigned long long* p) {
+    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ag64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_drain() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// a 32-B slot digest as two uint4 (lo, hi), sc1
+__device__ __forceinline__ void ld_dig_ag(const uint8_t* slot, uint4& lo, uint4& hi) {
+    const unsigned long long* s = reinterpret_cast<const unsigned long long*>(slot);
+    const unsigned long long a0 = ld_ag64(s), a1 = ld_ag64(s + 1), a2 = ld_ag64(s + 2), a3 = ld_ag64(s + 3);
+    lo = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
+    hi = make_uint4((uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)a3, (uint32_t)(a3 >> 32));
+}
+
+// kAg: the hole digests are read with agent-scope loads (k2_flow)
+template <bool kAg>
+struct MatCursorT {
     // holes hn .. hn+3 in flight with their slot digests, and the records of
     // hn+4 and hn+5: a block applies at most two holes (they are >= 32 B apart),
     // so a record arrives a block before its digest load is issued, and the
@@ -254,9 +308,14 @@ struct MatCursor {
     }
     __device__ __forceinline__ void digest(const LevelArgs& a, PendingHole& q, const uint2& r) const {
         q.r = r;
-        const uint4* src = reinterpret_cast<const uint4*>(a.slots + 32ull * (q.r.y == ~0u ? 0u : q.r.y));
-        q.lo = src[0];
-        q.hi = src[1];
+        const uint8_t* slot = a.slots + 32ull * (q.r.y == ~0u ? 0u : q.r.y);
+        if constexpr (kAg) {
+            ld_dig_ag(slot, q.lo, q.hi);
+        } else {
+            const uint4* src = reinterpret_cast<const uint4*>(slot);
+            q.lo = src[0];
+            q.hi = src[1];
+        }
     }
     __device__ __forceinline__ void apply(uint32_t* ring, const PendingHole& q) const {
         const bool f = q.r.y == fslot;
@@ -376,6 +435,7 @@ struct MatCursor {
         for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
     }
 };
+using MatCursor = MatCursorT<false>;
 
 // The producer wave's material cursor in k2_level_pl: MatCursor's template
 // stream, with the holes in chunks of kHC per job.  While chunk c is applied
@@ -2131,6 +2191,397 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
     if (a.dbg_twice != 16) count_fused(a, hashed);
 }
 
+// ---- the flow step: readiness-driven, no level barrier ----------------------
+// One launch runs every level of the step's flow range (GraphDev flo..fhi and
+// the sink level; graph_flow_decide picks it): instead of one kernel per
+// level, each waiting for the whole level below it, a job starts as soon as
+// the jobs it reads have finished -- the reference evaluator's "gather Flows
+// that are ready ... wait for one task ... gather any new Flows that have
+// become ready" (/root/reference/eval.go:376-411, todo :902-955), with the
+// early cut-off of Flow.Digest memoization kept (flow.go:653-750): a job whose
+// inputs all come back unchanged is never hashed.
+//
+// Per job k (GraphDev "flow"): pend[k] counts k's producer chains queued this
+// step and not yet finished (+1 per chain-out edge when the chain's head is
+// queued -- flow_count_out, by the mark kernels or a flow lane -- and -1 when
+// that chain ends, changed or not); dirty[k] bit 0 = queued (an input
+// changed), bit 1 = claimed (started), bit 2 = parked.  k may start when pend[k]
+// is 0 AND no producer of k can still be queued: every level below wlev[k]
+// (the highest level of a queueable head among k's producers) has drained --
+// the watermark LW, advanced level by level as each level's finished count
+// reaches its queued count (mark-listed + flow-queued).  A job whose pend
+// reaches 0 before its watermark waits in the parking list of its wlev,
+// swept when LW passes it.  Whoever brings pend[k] to 0 with k queued
+// claims it and runs it in its own lane next (the OpK of a sample starts in
+// the lane whose pair chain finished last); further ready jobs go to a ready
+// queue of epoch-tagged entries that idle lanes take tickets on.  The jobs
+// the mark kernel queued are the initial candidates, taken through a
+// cursor in a scattered order (waves get a mix of long and short work).
+// Lanes hash one job (one link of a fused chain) per iteration, one-lane
+// SHA-256 as k2_level_lf; digests cross CUs write-through and are read with
+// agent-scope loads (MatCursorT<true>, finish_job_ag).  Termination: every
+// lane leaves when LW has passed the whole range (every queued job finished).
+constexpr uint32_t kFlowMaxLev = kFlowMaxLevels;
+#ifndef RF_FLOW_WAVES
+#define RF_FLOW_WAVES 2  // waves per SIMD (the register budget: 256 VGPRs at 2)
+#endif
+// every wave leaves a flow launch that has run this long (s_memrealtime, 100
+// MHz: 2 s, ~2,000x a 100M-node step) and flags it: a scheduling fault must
+// end the kernel, not hang the device (the host reports RF_EDEVICE)
+constexpr unsigned long long kFlowTimeout = 200000000ull;
+
+struct FlowCtl {
+    uint32_t *F, *Q, *D, *lw, *tail, *head, *lcur, *err;
+    uint32_t nlev, R;
+    __device__ __forceinline__ explicit FlowCtl(const LevelArgs& a) {
+        uint32_t* fb = a.counts + counts_flow_base(a.n_levels);
+        F = fb;
+        Q = fb + a.n_levels;
+        D = fb + 2 * a.n_levels;
+        uint32_t* ctl = fb + 3 * a.n_levels;
+        lw = ctl + kFlowLW;
+        tail = ctl + kFlowTail;
+        head = ctl + kFlowHead;
+        lcur = ctl + kFlowList;
+        err = ctl + kFlowErr;
+        nlev = a.fhi - a.flo + 1;
+        R = nlev + (a.fsink != ~0u ? 1u : 0u);
+    }
+    // the range level at watermark position p (levels flo..fhi, then the sink level)
+    __device__ __forceinline__ uint32_t level_at(const LevelArgs& a, uint32_t p) const {
+        return p < nlev ? a.flo + p : a.fsink;
+    }
+    // the watermark position at which every level below w has drained
+    __device__ __forceinline__ uint32_t need(const LevelArgs& a, uint32_t w) const {
+        return w <= a.flo ? 0u : min(w - a.flo, nlev);
+    }
+};
+
+__device__ __forceinline__ unsigned long long flow_tag(const LevelArgs& a, uint32_t k) {
+    return ((unsigned long long)a.epoch << 32) | k;
+}
+
+// Claim queued, unclaimed job k (bit 1): k, or ~0u if it is not queued or
+// someone else has it.  A CAS, not an OR: a job already run and reset to 0
+// must stay 0.
+__device__ __forceinline__ uint32_t flow_claim(const LevelArgs& a, uint32_t k) {
+    uint32_t v = ld_ag(&a.dirty[k]);
+    while ((v & 3u) == 1u) {
+        const uint32_t o = atomicCAS(&a.dirty[k], v, v | 2u);
+        if (o == v) return k;
+        v = o;
+    }
+    return ~0u;
+}
+
+__device__ __forceinline__ void flow_push(const LevelArgs& a, const FlowCtl& fc, uint32_t k) {
+    const uint32_t t = atomicAdd(fc.tail, 1u);
+    st_ag64(&a.rq[t], flow_tag(a, k));
+}
+
+// k's pend is 0 but its watermark is not reached: into the parking list of
+// wlev w (once per step: bit 2).  The entry is stored before LW is read
+// again, and the sweeper advances LW before it reads the list, so one of
+// the two sees the other (both may try: the claim decides).
+__device__ __forceinline__ uint32_t flow_park(const LevelArgs& a, const FlowCtl& fc, uint32_t k, uint32_t w,
+                                              uint32_t nd) {
+    uint32_t v = ld_ag(&a.dirty[k]);
+    for (;;) {
+        if ((v & 7u) != 1u) return ~0u;  // claimed, or parked already
+        const uint32_t o = atomicCAS(&a.dirty[k], v, v | 4u);
+        if (o == v) break;
+        v = o;
+    }
+    const uint32_t i = atomicAdd(&fc.D[w], 1u);
+    st_ag64(&a.dq[a.dstart[w] + i], flow_tag(a, k));
+    vm_drain();
+    if (ld_ag(fc.lw) >= nd) return flow_claim(a, k);
+    return ~0u;
+}
+
+// pend[k] has just reached 0 (or k is a mark-listed candidate with pend 0):
+// claim it if it is queued and its watermark is reached, else park it.
+__device__ __forceinline__ uint32_t flow_trigger(const LevelArgs& a, const FlowCtl& fc, uint32_t k) {
+    if ((ld_ag(&a.dirty[k]) & 3u) != 1u) return ~0u;  // not queued (no input changed so far), or claimed
+    const uint32_t w = a.jlv[k].y, nd = fc.need(a, w);
+    if (ld_ag(fc.lw) >= nd) return flow_claim(a, k);
+    return flow_park(a, fc, k, w, nd);
+}
+
+// Advance the watermark over every drained level; the jobs parked on the
+// level it opens are claimed and queued by the wave's lanes.  Called by
+// every lane of the wave.
+__device__ __forceinline__ void flow_advance(const LevelArgs& a, const FlowCtl& fc) {
+    const uint32_t lane = __lane_id();
+    for (;;) {
+        uint32_t p = 0, st = 0;  // st: 0 stop, 1 advanced p -> p + 1, 2 lost a race: look again
+        if (lane == 0) {
+            p = ld_ag(fc.lw);
+            if (p < fc.R) {
+                const uint32_t l = fc.level_at(a, p);
+                const uint32_t q = ld_ag(&a.counts[l]) + ld_ag(&fc.Q[l]);
+                if (ld_ag(&fc.F[l]) == q) st = atomicCAS(fc.lw, p, p + 1) == p ? 1u : 2u;
+            }
+        }
+        st = __builtin_amdgcn_readfirstlane(__shfl(st, 0, 64));
+        p = __builtin_amdgcn_readfirstlane(__shfl(p, 0, 64));
+        if (st == 0) return;
+        if (st == 2) continue;
+        if (p + 1 < fc.nlev) {
+            const uint32_t w = a.flo + p + 1, n = ld_ag(&fc.D[w]), base = a.dstart[w];
+            for (uint32_t i = lane; i < n; i += 64) {
+                const unsigned long long e = ld_ag64(&a.dq[base + i]);
+                if ((uint32_t)(e >> 32) != a.epoch) continue;  // not written yet: its parker sees LW and claims it
+                const uint32_t k = (uint32_t)e;
+                if (ld_ag(&a.pend[k]) != 0u) continue;  // a producer still runs: its end triggers k
+                const uint32_t t = flow_claim(a, k);
+                if (t != ~0u) flow_push(a, fc, t);
+            }
+        }
+    }
+}
+
+// A changed job's consumers (reverse edges [c, ce), the fusion edge
+// excluded): one inside the flow range is queued -- its queued flag, the
+// level's flow-queued count and its own chain-out pend -- and waits for
+// pend; one outside it joins its level's list for the level kernels after
+// the flow launch.  Wave-uniform loop.
+__device__ __forceinline__ void flow_propagate(const LevelArgs& a, const FlowCtl& fc, uint32_t c, uint32_t ce) {
+    while (__any(c < ce)) {
+        bool need = false, inr = false;
+        uint2 jl = make_uint2(0, 0), cr = make_uint2(0, 0);
+        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+        if (c < ce) {
+            jl = a.cons[c++];
+            inr = flow_level(a, jl.y);
+            if (inr) {
+                cr = a.cout_rng[jl.x];
+            } else {
+                q0 = a.meta[2ull * jl.x];
+                q1 = a.meta[2ull * jl.x + 1];
+            }
+            need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
+        }
+        if (need && inr) {
+            atomicAdd(&fc.Q[jl.y], 1u);
+            flow_count_out(a, cr);
+        }
+        append_jobs(a, need && !inr, jl.x, jl.y, q0, q1);
+    }
+}
+
+// As finish_job_pre, the new digest stored write-through (agent scope): a
+// consumer on another CU reads it inside this launch.
+__device__ __forceinline__ bool finish_job_ag(const LevelArgs& a, const uint4& m1, const ShaState& st,
+                                              const uint4& olo, const uint4& ohi) {
+    uint32_t n[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) n[i] = bswap32(st.h[i]);
+    const bool changed = (olo.x != n[0]) | (olo.y != n[1]) | (olo.z != n[2]) | (olo.w != n[3]) |
+                         (ohi.x != n[4]) | (ohi.y != n[5]) | (ohi.z != n[6]) | (ohi.w != n[7]);
+    if (changed) {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.slots + 32ull * m1.x);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st_ag64(dst + i, (unsigned long long)n[2 * i] | ((unsigned long long)n[2 * i + 1] << 32));
+    }
+    return changed;
+}
+
+__global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs a) {
+    __shared__ uint32_t ring_all[kLevelBlock * kRing];
+    __shared__ uint32_t s_pref[kFlowMaxLev + 1];  // prefix of the range levels' mark-listed counts
+    __shared__ uint32_t s_base[kFlowMaxLev];      // list position of each range level's first entry - its prefix
+    uint32_t* ring = &ring_all[threadIdx.x * kRing];
+    zero_other_counts(a);
+    const FlowCtl fc(a);
+    // (the mark kernel that listed them has finished: plain loads)
+    for (uint32_t q = threadIdx.x; q < fc.R; q += blockDim.x) {
+        const uint32_t l = fc.level_at(a, q);
+        s_pref[q + 1] = a.counts[l];
+        s_base[q] = a.lvl_start[l];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_pref[0] = 0;
+        for (uint32_t q = 0; q < fc.R; ++q) {
+            s_pref[q + 1] += s_pref[q];
+            s_base[q] -= s_pref[q];
+        }
+    }
+    __syncthreads();
+    const uint32_t n_list = s_pref[fc.R];
+    // levels no job was queued at drain at once (else only chain ends advance
+    // the watermark, and a step with nothing to hash would never end)
+    if (blockIdx.x == 0 && threadIdx.x < 64) flow_advance(a, fc);
+    const uint32_t lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t p = ~0u, hd = 0, hl = 0, tk = ~0u, fslot = ~0u;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, flo4 = m0, fhi4 = m0;
+    uint2 cr = make_uint2(0, 0);
+    bool fresh = false, lists = n_list > 0;
+    uint32_t hashed = 0;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    auto start = [&](uint32_t k) {
+        p = hd = k;
+        fresh = true;
+        m0 = a.meta[2ull * k];
+        m1 = a.meta[2ull * k + 1];
+        hl = a.jlv[k].x;
+        cr = a.cout_rng[k];
+    };
+    for (;;) {
+        // 1. idle lanes: a candidate the mark kernel listed, else a ticket
+        {
+            const bool want = p == ~0u && tk == ~0u && lists;
+            const uint64_t wm = __ballot(want);
+            if (wm) {
+                uint32_t base = 0;
+                if (lane == (uint32_t)__ffsll((unsigned long long)wm) - 1)
+                    base = atomicAdd(fc.lcur, (uint32_t)__popcll(wm));
+                base = __shfl(base, (uint32_t)__ffsll((unsigned long long)wm) - 1, 64);
+                if (want) {
+                    const uint32_t i = base + (uint32_t)__popcll(wm & lt);
+                    if (i >= n_list) {
+                        lists = false;
+                    } else {
+                        // a scattered order over the lists (a bijection of [0, n_list))
+                        const uint32_t pos = (uint32_t)(((uint64_t)i * 2654435761ull) % n_list);
+                        uint32_t lo = 0, hi = fc.R;  // s_pref[lo] <= pos < s_pref[hi]
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (s_pref[mid] <= pos) lo = mid; else hi = mid;
+                        }
+                        const uint32_t k = a.list[s_base[lo] + pos];
+                        // pend > 0: a producer chain still runs, its end triggers k
+                        const uint32_t t = ld_ag(&a.pend[k]) == 0u ? flow_trigger(a, fc, k) : ~0u;
+                        if (t != ~0u) start(t);
+                    }
+                }
+            }
+            const bool tw = p == ~0u && tk == ~0u && !lists;
+            const uint64_t tm = __ballot(tw);
+            if (tm) {
+                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)tm) - 1;
+                uint32_t base = 0;
+                if (lane == ld) base = atomicAdd(fc.head, (uint32_t)__popcll(tm));
+                base = __shfl(base, ld, 64);
+                if (tw) tk = base + (uint32_t)__popcll(tm & lt);
+            }
+            if (p == ~0u && tk != ~0u && tk < a.e) {  // (a ticket past the queue's capacity gets no job)
+                const unsigned long long e = ld_ag64(&a.rq[tk]);
+                if ((uint32_t)(e >> 32) == a.epoch) {
+                    tk = ~0u;
+                    start((uint32_t)e);
+                }
+            }
+        }
+        if (__all(p == ~0u)) {
+            uint32_t done = 0;
+            if (lane == 0) {
+                done = ld_ag(fc.lw) >= fc.R;
+                if (!done && __builtin_amdgcn_s_memrealtime() - t_start > kFlowTimeout) {
+                    if (atomicExch(fc.err, 1u) == 0u) {  // the first to give up records where the step stood
+                        const uint32_t p0 = ld_ag(fc.lw), l0 = fc.level_at(a, min(p0, fc.R - 1));
+                        fc.err[1] = p0;
+                        fc.err[2] = l0;
+                        fc.err[3] = ld_ag(&a.counts[l0]);
+                        fc.err[4] = ld_ag(&fc.Q[l0]);
+                        fc.err[5] = ld_ag(&fc.F[l0]);
+                        fc.err[6] = ld_ag(fc.tail);
+                        fc.err[7] = ld_ag(fc.head);
+                    }
+                    done = 1;
+                }
+            }
+            if (__builtin_amdgcn_readfirstlane(__shfl(done, 0, 64))) break;
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+        }
+        // 2. one job (a chain head, or the next link of a fused chain) per lane
+        uint32_t cb = 0, cz = 0, nx = ~0u;
+        bool endc = false;
+        if (p != ~0u) {
+            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);  // (its own slot: written by no one else)
+            const uint4 olo = od[0], ohi = od[1];
+            const bool nf = m1.w != ~0u;
+            uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0;
+            if (nf) {
+                nm0 = a.meta[2ull * m1.w];
+                nm1 = a.meta[2ull * m1.w + 1];
+            }
+            MatCursorT<true> cur;
+            cur.fslot = fslot;
+            cur.flo = flo4;
+            cur.fhi = fhi4;
+            if (fresh)
+                cur.begin(a, m0, ring);
+            else
+                cur.begin_fused(a, m0, ring);
+            ShaState st;
+            init_state(a, p, st);
+            for (uint32_t b = 0; b < cur.nb; ++b) {
+                uint32_t w[16];
+                cur.block(a, b, ring, w, !fresh);
+                sha256_compress(st, w);
+            }
+            const bool ch = finish_job_ag(a, m1, st, olo, ohi);
+            hashed += fresh ? 0u : 1u;
+            cb = m1.y;
+            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
+            if (ch && nf) {
+                nx = m1.w;
+                fslot = m1.x;
+                flo4 = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                fhi4 = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+                m0 = nm0;
+                m1 = nm1;
+            } else {
+                endc = true;
+            }
+        }
+        // 3. the changed job's other consumers
+        flow_propagate(a, fc, cb, cz);
+        // 4. a chain's end: the jobs it completes for (pend - 1 each; the one
+        //    that reaches 0 with its job queued and its watermark reached
+        //    starts here next, any further one goes to the ready queue)
+        uint32_t next = ~0u;
+        if (endc) {
+            vm_drain();  // its digests (write-through) and queue counts first
+            for (uint32_t e = cr.x; e < cr.y; e += 4) {
+                uint2 o[4];
+                uint32_t r[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) o[u] = e + u < cr.y ? a.cout[e + u] : make_uint2(0, ~0u);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) r[u] = flow_level(a, o[u].y) ? atomicSub(&a.pend[o[u].x], 1u) : 0u;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (r[u] != 1u) continue;
+                    const uint32_t t = flow_trigger(a, fc, o[u].x);
+                    if (t == ~0u) continue;
+                    if (next == ~0u) next = t; else flow_push(a, fc, t);
+                }
+            }
+            atomicExch(&a.dirty[hd], 0u);
+            vm_drain();
+            atomicAdd(&fc.F[hl], 1u);
+            vm_drain();
+        }
+        if (__any(endc)) flow_advance(a, fc);
+        if (p != ~0u) {
+            if (!endc) {
+                p = nx;
+                fresh = false;
+            } else if (next != ~0u) {
+                start(next);
+            } else {
+                p = ~0u;
+            }
+        }
+    }
+    count_fused(a, hashed);
+}
+
 // ---- the octo form: levels of few long jobs (GraphDev kLvlOct) ---------------
 // k2_level_pl keeps 64 jobs per workgroup on two-lane chains (9 VALU a round)
 // fed by a producer that assembles one block a step through a hole pipeline;
@@ -2475,7 +2926,7 @@ __global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __
         last[L] = full ? 0u : f;
     }
     __syncthreads();
-    for (uint32_t l = L + threadIdx.x; l < L + 1 + kCountsExtra; l += blockDim.x) counts[l] = 0;
+    for (uint32_t l = L + threadIdx.x; l < counts_half_words(L); l += blockDim.x) counts[l] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_gather_slots(const uint8_t* __restrict__ slots,
@@ -2513,11 +2964,41 @@ static uint32_t grid_mark(uint64_t items) {
 }
 
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
+// the flow fields of a launch's LevelArgs (this step's range, GraphDev flo; none: flo = ~0u)
+static void flow_args(const GraphDev& g, LevelArgs& a) {
+    a.cout_rng = g.cout_rng;
+    a.cout = g.cout;
+    a.jlv = g.jlv;
+    a.pend = g.pend;
+    a.dstart = g.dstart;
+    a.rq = g.rq;
+    a.dq = g.dq;
+    a.flo = g.flo;
+    a.fhi = g.fhi;
+    a.fsink = g.fsink;
+    a.epoch = g.epoch;
+}
+
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic: k3_mark_slots_lf skips its count)
+    flow_args(g, a);  // a flow step's mark queues with chain-out counts (propagate)
     return a;
+}
+
+// The flow launch of a plain incremental step (GraphDev flo..fhi, fsink): the
+// step's first kernel (it zeroes the previous step's cursor half), one
+// resident round of 256-lane workgroups (three per CU: lanes that run out of
+// work wait on the ready queue, so no grid-stride is needed).
+hipError_t launch_graph_flow(const GraphDev& g, hipStream_t s, uint32_t* zero_counts) {
+    if (g.flo == ~0u || g.fhi - g.flo + 2 > kFlowMaxLev) return hipErrorInvalidValue;
+    LevelArgs a = mark_level_args(g);
+    a.zero_counts = zero_counts;
+    a.e = g.n_jobs;  // (k2_flow: the ready queue's capacity)
+    const uint32_t grid = std::max<uint32_t>(1u, (g.n_cu ? g.n_cu : 256u) * RF_FLOW_WAVES);
+    hipLaunchKernelGGL(k2_flow, dim3(grid), dim3(kLevelBlock), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_graph_mark_slots(GraphDev& g, const uint32_t* slots, const uint8_t* digests,

@@ -240,7 +240,8 @@ def test_structurally_damaged_checkpoints_refused(ctx, tmp_path):
     g.close()
     raw = open(path, "rb").read()
     secs, _ = _sections(raw)
-    names = ["lvl_start", "inc_level", "ext2int", "meta", "holes", "cons_ptr", "cons_job", "tmpl", "slots", "mid"]
+    names = ["lvl_start", "inc_level", "ext2int", "meta", "holes", "cons_ptr", "cons_job", "tmpl", "slots", "mid",
+             "jlv", "cout_rng", "cout", "dstart"]
     sec = dict(zip(names, secs))
     lvl = np.frombuffer(raw, np.uint32, sec["lvl_start"][1] // 4, sec["lvl_start"][0])
     cons_ptr = np.frombuffer(raw, np.uint32, sec["cons_ptr"][1] // 4, sec["cons_ptr"][0])
@@ -276,4 +277,32 @@ def test_structurally_damaged_checkpoints_refused(ctx, tmp_path):
     bad = bytearray(raw)
     first = struct.unpack_from("<I", bad, sec["ext2int"][0])[0]
     struct.pack_into("<I", bad, sec["ext2int"][0] + 4, first)
+    refused(bytes(bad))
+    # 4. a fusion target whose one hole sits elsewhere than byte
+    # 2, or reads another slot than its producer's output: the chain builds
+    # that block 0 in registers from the producer's digest at byte 2
+    meta = np.frombuffer(raw, np.uint32, sec["meta"][1] // 4, sec["meta"][0]).reshape(-1, 8)
+    j = next(i for i in range(len(meta)) if meta[i, 7] != 0xFFFFFFFF)
+    t = int(meta[j, 7])
+    hole = int(meta[t, 2])
+    assert struct.unpack_from("<II", raw, sec["holes"][0] + 8 * hole) == (2, int(meta[j, 4]))
+    bad = bytearray(raw)
+    struct.pack_into("<I", bad, sec["holes"][0] + 8 * hole, 40)
+    refused(bytes(bad))
+    bad = bytearray(raw)
+    struct.pack_into("<I", bad, sec["holes"][0] + 8 * hole + 4, int(meta[j, 4]) ^ 1)
+    refused(bytes(bad))
+    # 5. the flow step's structures: a chain-out edge naming a job outside
+    # its level, and a parking list too short for its wlev's jobs
+    cout = np.frombuffer(raw, np.uint32, sec["cout"][1] // 4, sec["cout"][0]).reshape(-1, 2)
+    assert len(cout)
+    x, y = int(cout[0, 0]), int(cout[0, 1])
+    other = next(lv for lv in range(len(lvl) - 1) if lv != y and not (lvl[lv] <= x < lvl[lv + 1]))
+    bad = bytearray(raw)
+    struct.pack_into("<I", bad, sec["cout"][0] + 4, other)
+    refused(bytes(bad))
+    dst = np.frombuffer(raw, np.uint32, sec["dstart"][1] // 4, sec["dstart"][0])
+    w = next(i for i in range(len(dst) - 1) if dst[i + 1] > dst[i])
+    bad = bytearray(raw)
+    struct.pack_into("<I", bad, sec["dstart"][0] + 4 * (w + 1), int(dst[w + 1]) - 1)
     refused(bytes(bad))
