@@ -763,20 +763,59 @@ def bench_dag100m(args, dist, ctx, comm, budget):
     return res
 
 
-def bench_piece(args, ctx, ranks, n1_ms):
+# The strong-scaling bound of a layout: a rank's piece can step no faster than
+# its critical path -- the longest chain of dependent compressions a change
+# starts -- at the measured per-block rate of a one-message chain: K1's duo
+# chain (the fastest measured, us_per_chain_block of the SHA leg's duo launch,
+# else its round-4 figure) and K2's two-lane link rounds (1.44 us a block,
+# DESIGN.md §5).  The exchange is one all-gather of the part roots' 32-B
+# digests a step (RCCL over xGMI); its latency is an ESTIMATE, not measured
+# on this one-GPU box, and is not folded into any measured time.
+DUO_US_PER_BLOCK_R04 = 1.13
+K2_US_PER_BLOCK = 1.44
+EXCHANGE_EST_US = 20.0
+
+
+def piece_bounds(crit_blocks, n1_ms, duo_us=None):
+    duo = duo_us or DUO_US_PER_BLOCK_R04
+    f_duo, f_k2 = crit_blocks * duo * 1e-3, crit_blocks * K2_US_PER_BLOCK * 1e-3
+    return {"critical_path_blocks": int(crit_blocks),
+            "floor_ms": round(f_duo, 4), "floor_ms_k2_link_rate": round(f_k2, 4),
+            "floor_rate_us_per_block": round(duo, 4),
+            "speedup_bound_8": round(n1_ms / f_duo, 3) if f_duo else None,
+            "speedup_bound_8_with_exchange_est": round(n1_ms / (f_duo + EXCHANGE_EST_US * 1e-3), 3) if f_duo else None,
+            "exchange_est_us": EXCHANGE_EST_US,
+            "bound_kind": "N = 1 ms / (critical path blocks x the measured one-chain rate: K1 duo %s us/block); "
+                          "the exchange term (one boundary all-gather a step) is an estimate, not measured"
+                          % round(duo, 3)}
+
+
+def bench_piece(args, ctx, ranks, n1_ms, duo_us=None, per_sample=False):
     """N = 1 only: rank 0's piece of the strong-scaling layout at `ranks`
-    ranks (8/ranks parts of configs[3]'s DAG, the global root included),
-    stepped on this GPU like bench_dag100m's rank 0 but with no exchange --
-    what one GPU of a `ranks`-GPU run hashes per step, so the 1 -> N curve's
-    DAG ceiling is visible before the driver's SCALE run."""
+    ranks, stepped on this GPU like bench_dag100m's rank 0 but with no
+    exchange -- what one GPU of a `ranks`-GPU run hashes per step, so the
+    1 -> N curve's DAG ceiling is visible before the driver's SCALE run.
+    Layouts: the bench's (8/ranks parts of configs[3]'s DAG, each with a
+    fan-in-32 Merge tree, the global root on rank 0), or per_sample -- SURVEY
+    §8(d) C3/C4 as written: per-sample roots only (no Merge tree, no global
+    root; /root/reference/doc/1000align/1000align.rf:1-50 is per sample), the
+    shared reference-index chain replicated, an empty boundary."""
     S, P, nparts = args.c4_samples, args.dag_pairs, args.c4_parts
-    pc = PartitionedDag1000(S, P, ranks, 0, nparts=nparts)
-    g = capi.Graph.from_arrays(ctx, pc.desc)
-    g.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
+    if per_sample:
+        dag = Dag1000(S * nparts // ranks, P)
+        desc, crit_of = dag.arrays(), dag.critical_path
+        slots, old, new = dag.change_set(0.01, n_global=2 * P * S * nparts)
+        n_nodes, file_slots, leaf_ids = dag.n_nodes, dag.file_slots, dag.leaf_ids
+    else:
+        pc = PartitionedDag1000(S, P, ranks, 0, nparts=nparts)
+        desc, crit_of = pc.desc, pc.critical_path
+        slots, old, new = pc.dag.change_set(0.01, n_global=2 * P * S * nparts)
+        n_nodes, file_slots, leaf_ids = pc.n_nodes, pc.dag.file_slots, pc.dag.leaf_ids
+    g = capi.Graph.from_arrays(ctx, desc)
+    g.set_slots(file_slots, leaf_ids)
     g.recompute(True)
-    slots, old, new = pc.dag.change_set(0.01, n_global=2 * P * S * nparts)
     d_slots, d_old, d_new = ctx.upload(slots), ctx.upload(old), ctx.upload(new)
-    every = np.arange(pc.desc["n_slots"], dtype=np.uint32)
+    every = np.arange(desc["n_slots"], dtype=np.uint32)
     full = g.get_slots(every)
     state = {"v": 0}
 
@@ -801,12 +840,76 @@ def bench_piece(args, ctx, ranks, n1_ms):
     for b in (d_slots, d_old, d_new):
         b.free()
     g.close()
-    log("  rank 0's piece at %d ranks: %d nodes, %.4f ms/step (N = 1: %.4f ms, ratio %.2f)"
-        % (ranks, pc.n_nodes, ms, n1_ms, n1_ms / ms))
-    return {"ranks": ranks, "nodes": int(pc.n_nodes), "changed_slots": int(len(slots)), "ms_per_step": round(ms, 4),
+    log("  rank 0's piece at %d ranks%s: %d nodes, %.4f ms/step (N = 1: %.4f ms, ratio %.2f)"
+        % (ranks, " (per-sample roots)" if per_sample else "", n_nodes, ms, n1_ms, n1_ms / ms))
+    return {"ranks": ranks, "nodes": int(n_nodes), "changed_slots": int(len(slots)), "ms_per_step": round(ms, 4),
             "projected_speedup": round(n1_ms / ms, 3), "incremental_equals_full": same,
-            "what": "rank 0's piece of the strong layout at %d ranks, local step only (no exchange), on this GPU; "
-                    "projected_speedup = incremental_100m.ms_per_step (N = 1) / this" % ranks}
+            **piece_bounds(crit_of(slots), n1_ms, duo_us),
+            "what": "rank 0's piece of the %s layout at %d ranks, local step only (no exchange), on this GPU; "
+                    "projected_speedup = the layout's N = 1 ms/step / this"
+                    % ("per-sample-root (SURVEY C3/C4)" if per_sample else "strong Merge-tree", ranks)}
+
+
+def bench_persample(args, ctx, duo_us=None):
+    """SURVEY §8(d) C3/C4's DAG as written: 8 x c4_samples samples of the
+    1000align DAG (100M nodes) with per-sample roots and no Merge tree, on
+    one GPU (N = 1), and rank 0's piece of it at 8 ranks -- the layout a
+    sample-partitioned run needs no exchange for.  Reported beside the bench's
+    Merge-tree layout so the 8-GPU projection is judged against what each
+    layout permits."""
+    S, P, nparts = args.c4_samples, args.dag_pairs, args.c4_parts
+    t0 = time.perf_counter()
+    dag = Dag1000(S * nparts, P)
+    a = dag.arrays()
+    g = capi.Graph.from_arrays(ctx, a)
+    g.set_slots(dag.file_slots, dag.leaf_ids)
+    g.recompute(True)
+    slots, old, new = dag.change_set(0.01)
+    d_slots, d_old, d_new = ctx.upload(slots), ctx.upload(old), ctx.upload(new)
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+    full = g.get_slots(every)
+    state = {"v": 0}
+
+    def step():
+        ver = d_new if state["v"] == 0 else d_old
+        state["v"] ^= 1
+        g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
+        g.recompute_async(False, ctx.stream)
+
+    for _ in range(2):
+        step()
+    ctx.sync()
+    t1 = time.perf_counter()
+    for _ in range(args.dag_steps):
+        step()
+    ctx.sync()
+    ms = (time.perf_counter() - t1) / args.dag_steps * 1e3
+    if state["v"] == 1:
+        step()
+    ctx.sync()
+    same = bool((g.get_slots(every) == full).all())
+    st = g.stats()
+    for b in (d_slots, d_old, d_new):
+        b.free()
+    g.close()
+    del full
+    f = np.asarray(slots, dtype=np.int64)
+    pairs, samples = np.unique(f // 2), np.unique(f // 2 // P)
+    n_dirty = int(2 * len(f) + 10 * len(pairs) + 5 * len(samples))  # Val + Coerce a file, the pair chain, the tail
+    log("  per-sample-root layout (SURVEY C3/C4): %d nodes, %.4f ms/step at N = 1 (flow %d), built+loaded in %.1f s"
+        % (dag.n_nodes, ms, st.last_flow, time.perf_counter() - t0))
+    res = {"workload": "SURVEY §8(d) C3/C4 as written: 1000align DAG of %d samples x P=%d (%d nodes), per-sample "
+                       "roots, no Merge tree or global root; 1%% of leaf File IDs toggled per step" % (S * nparts, P,
+                                                                                                   dag.n_nodes),
+           "nodes": int(dag.n_nodes), "ms_per_step": round(ms, 4), "incremental_equals_full": same,
+           "flow_step": bool(st.last_flow), "dirty_nodes_per_step": n_dirty,
+           "mnodes_per_s": round(n_dirty / (ms * 1e-3) / 1e6, 1),
+           "critical_path_blocks": int(dag.critical_path(slots))}
+    del dag, a
+    pc8 = bench_piece(args, ctx, 8, ms, duo_us, per_sample=True)
+    res["piece_8"] = pc8
+    res["piece_ms_8"], res["projected_speedup_8"] = pc8["ms_per_step"], pc8["projected_speedup"]
+    return res
 
 
 def oracle_check_table(a, table):
@@ -1136,6 +1239,45 @@ def gather_ceiling(table_bytes, n_threads, reads):
     return n_threads * r / (ms * 1e-3) / 1e9 if ms > 0 else None
 
 
+def valu_ceiling():
+    """SHA-256's measured VALU ceiling on this GPU, T int32 ops/s: every lane
+    of 8 waves per SIMD compresses register data (tools/micro.hip k_compute,
+    the same sha256_compress as the K1/K2 lane paths; 1464 canonical ops a
+    block).  Beside the 78.6 T spec peak every VALU roofline is also given
+    against this (the op mix's 8-byte VOP3 forms issue slower
+    than the spec's one op per lane per clock).  None without tools/_micro.so."""
+    import ctypes
+    so = os.path.join(ROOT, "tools", "_micro.so")
+    if not os.path.exists(so):
+        return None
+    L = ctypes.CDLL(so)
+    L.micro_compute.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.micro_compute.restype = ctypes.c_float
+    grid, nblk = N_CU * 8, 1000
+    L.micro_compute(grid, 20)  # (code and clocks warm)
+    ms = L.micro_compute(grid, nblk)
+    return grid * 256 * nblk * SHA_OPS_PER_BLOCK / (ms * 1e-3) / 1e12 if ms > 0 else None
+
+
+def with_measured_valu(line, tops):
+    """Every VALU frac of the line, again against the measured ceiling."""
+    if not tops:
+        return
+    gbps = tops * 1e12 / SHA_OPS_PER_BLOCK * 64 / 1e9
+    for r in [line.get("roofline")] + list(line.get("roofline_gpu_legs") or []) + [line.get("roofline_gpu_only")]:
+        if r and r.get("frac_of_valu_peak") is not None:
+            r["frac_of_measured_valu"] = round(r["frac_of_valu_peak"] * SHA_VALU_PEAK_GBS / gbps, 6)
+    inc = line.get("incremental") or {}
+    if inc.get("roofline_full"):
+        rf = inc["roofline_full"]
+        rf["frac_of_measured_valu"] = round(rf["achieved"] / gbps, 4)
+    for d in (line.get("incremental_100m") or {}, (line.get("incremental_100m") or {}).get("per_sample_layout") or {}):
+        ri = d.get("roofline_incremental")
+        if ri:
+            ri["frac_of_measured_valu"] = round(ri["achieved_tops"] / tops, 4)
+            ri["measured_valu_tops"] = round(tops, 2)
+
+
 # ----------------------------------------------------------- CPU baseline --
 def cpu_model():
     try:
@@ -1393,7 +1535,8 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=16.0)
     ap.add_argument("--gpu-only-run", type=int, default=1, help="one GPU-only run (duo roofline)")
     ap.add_argument("--budget-s", type=float, default=420.0)
-    ap.add_argument("--skip", default="", help="comma list of: lower,c1,install,dag,dag100m,piece,checkpoint,probe,cpu")
+    ap.add_argument("--skip", default="",
+                    help="comma list of: lower,c1,install,dag,dag100m,piece,persample,checkpoint,probe,cpu")
     args = ap.parse_args()
     args.skip = set(filter(None, args.skip.split(",")))
     budget = Budget(args.budget_s)
@@ -1460,10 +1603,15 @@ def main():
         dag_res = bench_dag(args, dist, ctx, budget)
     if "dag100m" not in args.skip and budget.allow("dag100m", 150):
         dag100 = bench_dag100m(args, dist, ctx, comm, budget)
+        duo_us = next((r.get("us_per_chain_block") for r in sha["roofline_gpu_legs"]
+                       if r.get("kernel") == "k1_sha256_duo"), None)
         if dist.world == 1 and "piece" not in args.skip and budget.allow("piece_8", 20):
-            pc8 = bench_piece(args, ctx, 8, dag100["ms_per_step"])
+            pc8 = bench_piece(args, ctx, 8, dag100["ms_per_step"], duo_us)
             dag100["piece_8"] = pc8
             dag100["piece_ms_8"], dag100["projected_speedup_8"] = pc8["ms_per_step"], pc8["projected_speedup"]
+        # SURVEY C3/C4 as written (per-sample roots): its N = 1 step and 8-rank piece
+        if dist.world == 1 and "persample" not in args.skip and budget.allow("persample", 60):
+            dag100["per_sample_layout"] = bench_persample(args, ctx, duo_us)
     probe = bench_probe(args, dist, ctx, budget) if "probe" not in args.skip and budget.allow("probe", 30) else None
     cpu = None
     if dist.rank == 0 and dist.world == 1 and "cpu" not in args.skip and budget.allow("cpu", 60):
@@ -1482,6 +1630,7 @@ def main():
         dag_res.pop("_cpu", None)
     sha["_arena"].free()
     parity = parity_summary(sha, c1, dag_res, dag100, probe, cpu)
+    valu_tops = valu_ceiling() if dist.rank == 0 else None
 
     if dist.rank == 0:
         workload = sha["workload"]
@@ -1493,6 +1642,12 @@ def main():
         line = {
             "metric": "SHA-256 digest GB/s + incremental cache-key recompute Mnodes/s, 1/2/4/8 GPU",
             "value": round(sha["value"], 4), "unit": "GB/s", "n_gpus": dist.world,
+            # the metric's other halves beside value: the
+            # GPU-only SHA rate of the same set, and the DAG legs' dirty nodes/s
+            "gpu_only_gbps": round(sha["gpu_only"]["gbps"], 4) if sha.get("gpu_only") else None,
+            "incremental_mnodes_per_s": round(dag_res["mnodes_per_s"], 1) if dag_res else None,
+            "incremental_100m_mnodes_per_s": round(dag100["mnodes_per_s"], 1) if dag100 else None,
+            "valu_measured_tops": round(valu_tops, 2) if valu_tops else None,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(sha["ms_per_step"], 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 content generated in HBM)",
@@ -1519,6 +1674,7 @@ def main():
             "budget": {"seconds": args.budget_s, "skipped": budget.skipped,
                        "elapsed_s": round(time.perf_counter() - T_START, 1)},
         }
+        with_measured_valu(line, valu_tops)
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(line) + "\n").encode())
     if comm is not None:

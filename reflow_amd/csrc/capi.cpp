@@ -2224,10 +2224,10 @@ int graph_read_counts(rf_graph* gr, hipStream_t s, std::vector<uint32_t>& counts
     if (L && half)
         for (uint32_t k = 0; k < kFusedParts; ++k) raw[L] += raw[L + 1 + kPartStride * k];
     if (L && half && gr->g.last_flow) {  // a flow step's jobs queued by flow lanes (never listed)
-        const uint32_t* er = &raw[counts_flow_base(L) + 3 * L + kFlowErr];
+        const uint32_t* er = &raw[counts_flow_base(L) + flow_ctl_off(L) + kFlowErr];
         if (er[0]) {
             // where it stood, and the first unfinished jobs of the level it waited on
-            const uint32_t l = er[2], b = gr->g.lvl_start[l], e = gr->g.lvl_start[l + 1];
+            const uint32_t l = std::min(er[2], L - 1), b = gr->g.lvl_start[l], e = gr->g.lvl_start[l + 1];
             std::vector<uint32_t> dirty(e - b), pend(e - b);
             std::string stuck;
             if (hipMemcpy(dirty.data(), gr->g.dirty + b, 4ull * (e - b), hipMemcpyDeviceToHost) == hipSuccess &&
@@ -2240,10 +2240,19 @@ int graph_read_counts(rf_graph* gr, hipStream_t s, std::vector<uint32_t>& counts
                     }
             return fail(RF_EDEVICE,
                         "flow step gave up (scheduling fault; the graph's digests are not current): watermark %u "
-                        "level %u queued %u+%u finished %u, ready queue %u/%u;%s",
-                        er[1], l, er[3], er[4], er[5], er[6], er[7], stuck.c_str());
+                        "level %u queued %u+%u finished %u, ready queue %u/%u, guard %u;%s",
+                        er[1], l, er[3], er[4], er[5], er[6], er[7], er[8], stuck.c_str());
         }
-        for (uint32_t l = 0; l < L; ++l) raw[l] += raw[counts_flow_base(L) + L + l];
+        for (uint32_t l = 0; l < L; ++l)
+            for (uint32_t sh = 0; sh < kFlowShards; ++sh)
+                raw[l] += raw[counts_flow_base(L) + (kFlowShards + sh) * flow_lp(L) + l];
+#ifdef RF_FLOW_PROFILE
+        const uint32_t* pw = er + 16;
+        fprintf(stderr, "[flow] wave-iterations %u (all idle %u), lanes hashing %u, long batches %u (%u jobs), "
+                "list starts %u, short takes %u, lane-blocks %u of %u issued (%.3f), longest wave %u us, waves %u\n",
+                pw[0], pw[1], pw[2], pw[3], pw[4], pw[5], pw[6], pw[7], pw[8], pw[8] ? (double)pw[7] / pw[8] : 0.0,
+                pw[9], pw[10]);
+#endif
     }
     raw.resize(L + 1);
     counts.swap(raw);

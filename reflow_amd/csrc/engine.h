@@ -86,18 +86,26 @@ constexpr uint32_t kOctMaxBlocks = 32, kOctMaxHoles = 64, kOctMaxLevel = 4096;
 // folded into [L] where it is read (k3_step_end, graph_read_counts).
 constexpr uint32_t kFusedParts = 64, kPartStride = 32, kCountsExtra = kFusedParts * kPartStride;
 // The flow step's control block (k2_flow), after each cursor half's fused
-// parts: per level F (jobs finished), Q (jobs queued by flow lanes) and D
-// (jobs parked), then the watermark, the ready queue's tail and head and the
-// parking cursor words, each on a 128-B line of its own.  Zero between steps
-// (the half is zeroed like the level counts).
-constexpr uint32_t kFlowCtl = 128;
+// parts: per level F (jobs finished) and Q (jobs queued by flow lanes), each
+// in kFlowShards shards (a wave adds to its own: one counter took every chain
+// end's atomic in turn at the memory side, ~19 ns each -- 6.9 ms a 100M step),
+// shard s of level l at s * Lp + l (Lp = L rounded up to 32 words: a level's
+// shards on lines of their own); D (jobs parked) per level; then the
+// watermark, the ready queue's tail and head, the candidate cursor and the
+// error words, each on a 128-B line of its own.  Zero between steps (the half
+// is zeroed like the level counts).
+constexpr uint32_t kFlowShards = 16, kFlowListShards = 32;
+constexpr uint32_t kFlowCtl = 256 + 32 * kFlowListShards;  // + the candidate cursors, a line each, from word 256
+__host__ __device__ constexpr uint32_t flow_lp(uint32_t L) { return (L + 31) / 32 * 32; }
 constexpr uint32_t kFlowLW = 0, kFlowTail = 32, kFlowHead = 64;
-constexpr uint32_t kFlowList = 96;  // the candidate-list cursor
+constexpr uint32_t kFlowLTail = 128, kFlowLHead = 160;  // the long-job queue (k2_flow)
+constexpr uint32_t kFlowList = 256;  // the candidate cursors (kFlowListShards, 32 words apart)
 constexpr uint32_t kFlowMaxLevels = 4096;  // range levels one flow launch takes (its LDS tables)
-constexpr uint32_t kFlowErr = 100;  // nonzero: the launch gave up (k2_flow kFlowTimeout)
+constexpr uint32_t kFlowErr = 96;  // nonzero: the launch gave up (k2_flow kFlowTimeout); then where it stood
 __host__ __device__ constexpr uint32_t counts_flow_base(uint32_t L) { return L + 1 + kCountsExtra; }
+__host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFlowShards * flow_lp(L) + L; }
 __host__ __device__ constexpr uint32_t counts_half_words(uint32_t L) {
-    return counts_flow_base(L) + 3 * L + kFlowCtl;
+    return counts_flow_base(L) + flow_ctl_off(L) + kFlowCtl;
 }
 struct GraphDev {
     uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;

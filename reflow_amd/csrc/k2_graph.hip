@@ -2231,17 +2231,21 @@ constexpr uint32_t kFlowMaxLev = kFlowMaxLevels;
 constexpr unsigned long long kFlowTimeout = 200000000ull;
 
 struct FlowCtl {
-    uint32_t *F, *Q, *D, *lw, *tail, *head, *lcur, *err;
-    uint32_t nlev, R;
+    uint32_t *F, *Q, *D, *lw, *tail, *head, *ltail, *lhead, *lcur, *err;
+    uint32_t nlev, R, lp, sh;  // sh: this wave's shard of F and Q
     __device__ __forceinline__ explicit FlowCtl(const LevelArgs& a) {
         uint32_t* fb = a.counts + counts_flow_base(a.n_levels);
+        lp = flow_lp(a.n_levels);
         F = fb;
-        Q = fb + a.n_levels;
-        D = fb + 2 * a.n_levels;
-        uint32_t* ctl = fb + 3 * a.n_levels;
+        Q = fb + kFlowShards * lp;
+        D = fb + 2 * kFlowShards * lp;
+        sh = (blockIdx.x * 5u + (threadIdx.x >> 6)) % kFlowShards;
+        uint32_t* ctl = fb + flow_ctl_off(a.n_levels);
         lw = ctl + kFlowLW;
         tail = ctl + kFlowTail;
         head = ctl + kFlowHead;
+        ltail = ctl + kFlowLTail;
+        lhead = ctl + kFlowLHead;
         lcur = ctl + kFlowList;
         err = ctl + kFlowErr;
         nlev = a.fhi - a.flo + 1;
@@ -2274,9 +2278,38 @@ __device__ __forceinline__ uint32_t flow_claim(const LevelArgs& a, uint32_t k) {
     return ~0u;
 }
 
+// The ready queue: jobs a chain end made ready beyond the one its lane runs
+// next, and jobs a sweep of the parking lists claimed.
+constexpr uint32_t kFlowChunk = 4;  // blocks a lane hashes per iteration
+// An index a flow structure gives that falls outside its array: record the
+// site (the host reports it with the step's failure) and skip the access --
+// a scheduling fault must not become a device fault.
+#define RF_FLOW_GUARD(cond, site, fc)                                             \
+    (__builtin_expect(!(cond), 0) ? (atomicCAS((fc).err + 8, 0u, (uint32_t)(site)), \
+                                     atomicExch((fc).err, 1u), false)              \
+                                  : true)
 __device__ __forceinline__ void flow_push(const LevelArgs& a, const FlowCtl& fc, uint32_t k) {
     const uint32_t t = atomicAdd(fc.tail, 1u);
-    st_ag64(&a.rq[t], flow_tag(a, k));
+    if (RF_FLOW_GUARD(t < a.e, 1, fc)) st_ag64(&a.rq[t], flow_tag(a, k));
+}
+// Up to n reserved entries of a queue (head < tail), no overshoot: the first
+// taken index (the lanes poll their entries: a pusher writes its entry right
+// after reserving it).  One lane.
+// The two loads are sampled in no fixed order (another wave's take may move
+// head past the tail value read): t <= h takes nothing.  Polled with loads,
+// never atomics: every idle wave polls, and same-address atomics serialize
+// at the memory side.
+__device__ __forceinline__ uint32_t flow_take(uint32_t* head, uint32_t* tail, uint32_t n, uint32_t& got) {
+    uint32_t h = ld_ag(head);
+    for (;;) {
+        const uint32_t t = ld_ag(tail);
+        const uint32_t m = t > h ? min(n, t - h) : 0u;
+        got = m;
+        if (!m) return 0;
+        const uint32_t o = atomicCAS(head, h, h + m);
+        if (o == h) return h;
+        h = o;
+    }
 }
 
 // k's pend is 0 but its watermark is not reached: into the parking list of
@@ -2293,7 +2326,7 @@ __device__ __forceinline__ uint32_t flow_park(const LevelArgs& a, const FlowCtl&
         v = o;
     }
     const uint32_t i = atomicAdd(&fc.D[w], 1u);
-    st_ag64(&a.dq[a.dstart[w] + i], flow_tag(a, k));
+    if (RF_FLOW_GUARD(a.dstart[w] + i < a.dstart[w + 1], 2, fc)) st_ag64(&a.dq[a.dstart[w] + i], flow_tag(a, k));
     vm_drain();
     if (ld_ag(fc.lw) >= nd) return flow_claim(a, k);
     return ~0u;
@@ -2314,21 +2347,28 @@ __device__ __forceinline__ uint32_t flow_trigger(const LevelArgs& a, const FlowC
 __device__ __forceinline__ void flow_advance(const LevelArgs& a, const FlowCtl& fc) {
     const uint32_t lane = __lane_id();
     for (;;) {
-        uint32_t p = 0, st = 0;  // st: 0 stop, 1 advanced p -> p + 1, 2 lost a race: look again
-        if (lane == 0) {
-            p = ld_ag(fc.lw);
-            if (p < fc.R) {
-                const uint32_t l = fc.level_at(a, p);
-                const uint32_t q = ld_ag(&a.counts[l]) + ld_ag(&fc.Q[l]);
-                if (ld_ag(&fc.F[l]) == q) st = atomicCAS(fc.lw, p, p + 1) == p ? 1u : 2u;
-            }
-        }
+        const uint32_t p = __builtin_amdgcn_readfirstlane(ld_ag(fc.lw));
+        if (p >= fc.R) return;
+        // level l's queued - finished, over the shards: the finished count
+        // first (lanes 0..15), then -- after it has arrived -- the queued
+        // ones (flow-queued shards on lanes 16..31, the mark-listed count on
+        // lane 32): a job is queued before it finishes, so finished(t1) ==
+        // queued(t2 > t1) means nothing queued by t2 was unfinished at t1
+        // (and nothing more can be queued here: the levels below drained)
+        const uint32_t l = fc.level_at(a, p);
+        int32_t v = lane < kFlowShards ? -(int32_t)ld_ag(&fc.F[lane * fc.lp + l]) : 0;
+        vm_drain();
+        if (lane >= kFlowShards && lane < 2 * kFlowShards) v = (int32_t)ld_ag(&fc.Q[(lane - kFlowShards) * fc.lp + l]);
+        else if (lane == 2 * kFlowShards) v = (int32_t)ld_ag(&a.counts[l]);
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (v != 0) return;  // (uniform: the reduction's result is the same in every lane)
+        uint32_t st = 0;  // 1 advanced p -> p + 1, 2 lost a race: look again
+        if (lane == 0) st = atomicCAS(fc.lw, p, p + 1) == p ? 1u : 2u;
         st = __builtin_amdgcn_readfirstlane(__shfl(st, 0, 64));
-        p = __builtin_amdgcn_readfirstlane(__shfl(p, 0, 64));
-        if (st == 0) return;
         if (st == 2) continue;
         if (p + 1 < fc.nlev) {
-            const uint32_t w = a.flo + p + 1, n = ld_ag(&fc.D[w]), base = a.dstart[w];
+            const uint32_t w = a.flo + p + 1, base = a.dstart[w];
+            const uint32_t n = min(ld_ag(&fc.D[w]), a.dstart[w + 1] - base);
             for (uint32_t i = lane; i < n; i += 64) {
                 const unsigned long long e = ld_ag64(&a.dq[base + i]);
                 if ((uint32_t)(e >> 32) != a.epoch) continue;  // not written yet: its parker sees LW and claims it
@@ -2338,6 +2378,20 @@ __device__ __forceinline__ void flow_advance(const LevelArgs& a, const FlowCtl& 
                 if (t != ~0u) flow_push(a, fc, t);
             }
         }
+    }
+}
+
+// counter[l] += the lanes with `add` at level l, one atomic per distinct
+// level in the wave (this wave's shard).  Called by every lane of the wave.
+__device__ __forceinline__ void flow_wave_add(uint32_t* counter, bool add, uint32_t l) {
+    uint64_t mask = __ballot(add);
+    while (mask) {
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
+        const uint32_t lv = __builtin_amdgcn_readfirstlane(__shfl(l, leader, 64));
+        const uint64_t same = __ballot(add && l == lv);
+        if (__lane_id() == leader) atomicAdd(&counter[lv], (uint32_t)__popcll(same));
+        add = add && l != lv;
+        mask = __ballot(add);
     }
 }
 
@@ -2362,10 +2416,8 @@ __device__ __forceinline__ void flow_propagate(const LevelArgs& a, const FlowCtl
             }
             need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
         }
-        if (need && inr) {
-            atomicAdd(&fc.Q[jl.y], 1u);
-            flow_count_out(a, cr);
-        }
+        if (need && inr) flow_count_out(a, cr);
+        flow_wave_add(fc.Q + fc.sh * fc.lp, need && inr, jl.y);
         append_jobs(a, need && !inr, jl.x, jl.y, q0, q1);
     }
 }
@@ -2415,67 +2467,109 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
     if (blockIdx.x == 0 && threadIdx.x < 64) flow_advance(a, fc);
     const uint32_t lane = __lane_id();
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint32_t p = ~0u, hd = 0, hl = 0, tk = ~0u, fslot = ~0u;
-    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, flo4 = m0, fhi4 = m0;
+    // the lane's chain: its head (hd, level hl, chain-out range cr), the job
+    // it is on (p; fresh = the head itself, else a fused link whose hole's
+    // digest is flo4/fhi4 in registers), and -- once begun -- that job's
+    // cursor, state and next block b (a job's blocks run kFlowChunk per
+    // iteration: one 18-block job no longer holds its wave's other lanes,
+    // on 2-block links, for 16 blocks)
+    uint32_t p = ~0u, hd = 0, hl = 0, tk = ~0u, b = 0;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, olo = m0, ohi = m0;
     uint2 cr = make_uint2(0, 0);
-    bool fresh = false, lists = n_list > 0;
-    uint32_t hashed = 0;
+    bool fresh = false, begun = false;
+    MatCursorT<true> cur;  // (cur.fslot / flo / fhi: the digest a fused link's hole reads, in registers)
+    cur.fslot = ~0u;
+    ShaState st;
+    uint32_t hashed = 0, idle_n = 0;
+    // the candidates in kFlowListShards slices of the scattered order, each
+    // with a cursor; a wave starts on its own slice and moves on when it is
+    // used up (wave-uniform: ls, ltried)
+    const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    uint32_t ls = wid % kFlowListShards, ltried = n_list ? 0u : kFlowListShards;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#ifdef RF_FLOW_PROFILE
+    // diagnostic build: per-wave tallies added to the control block's words
+    // 112.. at the end (tools/flow_probe.py)
+    uint32_t pr_it = 0, pr_idle = 0, pr_lanes = 0, pr_list = 0, pr_sq = 0, pr_blk = 0, pr_slot = 0;
+#define RF_PROF(...) __VA_ARGS__
+#else
+#define RF_PROF(...)
+#endif
     auto start = [&](uint32_t k) {
+        if (!RF_FLOW_GUARD(k < a.e, 9, fc)) return;
         p = hd = k;
         fresh = true;
+        begun = false;
         m0 = a.meta[2ull * k];
         m1 = a.meta[2ull * k + 1];
         hl = a.jlv[k].x;
         cr = a.cout_rng[k];
     };
     for (;;) {
-        // 1. idle lanes: a candidate the mark kernel listed, else a ticket
+        // 1. work for idle lanes: the candidates the mark kernel listed, else
+        //    ready jobs another lane's chain end queued
         {
-            const bool want = p == ~0u && tk == ~0u && lists;
+            const bool want = p == ~0u && tk == ~0u && ltried < kFlowListShards;
             const uint64_t wm = __ballot(want);
             if (wm) {
+                const uint32_t cnt = (uint32_t)__popcll(wm);
+                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)wm) - 1;
+                const uint32_t lo = (uint32_t)((uint64_t)n_list * ls / kFlowListShards);
+                const uint32_t hi = (uint32_t)((uint64_t)n_list * (ls + 1) / kFlowListShards);
                 uint32_t base = 0;
-                if (lane == (uint32_t)__ffsll((unsigned long long)wm) - 1)
-                    base = atomicAdd(fc.lcur, (uint32_t)__popcll(wm));
-                base = __shfl(base, (uint32_t)__ffsll((unsigned long long)wm) - 1, 64);
-                if (want) {
-                    const uint32_t i = base + (uint32_t)__popcll(wm & lt);
-                    if (i >= n_list) {
-                        lists = false;
-                    } else {
-                        // a scattered order over the lists (a bijection of [0, n_list))
-                        const uint32_t pos = (uint32_t)(((uint64_t)i * 2654435761ull) % n_list);
-                        uint32_t lo = 0, hi = fc.R;  // s_pref[lo] <= pos < s_pref[hi]
-                        while (hi - lo > 1) {
-                            const uint32_t mid = (lo + hi) >> 1;
-                            if (s_pref[mid] <= pos) lo = mid; else hi = mid;
-                        }
-                        const uint32_t k = a.list[s_base[lo] + pos];
-                        // pend > 0: a producer chain still runs, its end triggers k
-                        const uint32_t t = ld_ag(&a.pend[k]) == 0u ? flow_trigger(a, fc, k) : ~0u;
-                        if (t != ~0u) start(t);
-                    }
+                if (lane == ld) base = atomicAdd(&fc.lcur[32 * ls], cnt);
+                base = __builtin_amdgcn_readfirstlane(__shfl(base, ld, 64));
+                if (lo + base + cnt >= hi) {  // this slice is used up: the next one (wave-uniform)
+                    ls = (ls + 1) % kFlowListShards;
+                    ++ltried;
                 }
-            }
-            const bool tw = p == ~0u && tk == ~0u && !lists;
-            const uint64_t tm = __ballot(tw);
-            if (tm) {
-                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)tm) - 1;
-                uint32_t base = 0;
-                if (lane == ld) base = atomicAdd(fc.head, (uint32_t)__popcll(tm));
-                base = __shfl(base, ld, 64);
-                if (tw) tk = base + (uint32_t)__popcll(tm & lt);
-            }
-            if (p == ~0u && tk != ~0u && tk < a.e) {  // (a ticket past the queue's capacity gets no job)
-                const unsigned long long e = ld_ag64(&a.rq[tk]);
-                if ((uint32_t)(e >> 32) == a.epoch) {
-                    tk = ~0u;
-                    start((uint32_t)e);
+                const uint32_t i = lo + base + (uint32_t)__popcll(wm & lt);
+                if (want && i < hi) {
+                    // a scattered order over the lists (a bijection of [0, n_list))
+                    const uint32_t pos = (uint32_t)(((uint64_t)i * 2654435761ull) % n_list);
+                    uint32_t a0 = 0, a1 = fc.R;  // s_pref[a0] <= pos < s_pref[a1]
+                    while (a1 - a0 > 1) {
+                        const uint32_t mid = (a0 + a1) >> 1;
+                        if (s_pref[mid] <= pos) a0 = mid; else a1 = mid;
+                    }
+                    const uint32_t li = s_base[a0] + pos;
+                    const uint32_t k = RF_FLOW_GUARD(li < a.e, 4, fc) ? a.list[li] : 0u;
+                    // pend > 0: a producer chain still runs, its end triggers k
+                    const uint32_t t = ld_ag(&a.pend[k]) == 0u ? flow_trigger(a, fc, k) : ~0u;
+                    if (t != ~0u) start(t);
+                    RF_PROF(pr_list += t != ~0u ? 1u : 0u;)
                 }
             }
         }
+        {
+            const bool tw = p == ~0u && tk == ~0u && ltried >= kFlowListShards;
+            const uint64_t tm = __ballot(tw);
+            if (tm) {
+                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)tm) - 1;
+                uint32_t got = 0, base = 0;
+                if (lane == ld) base = flow_take(fc.head, fc.tail, (uint32_t)__popcll(tm), got);
+                got = __builtin_amdgcn_readfirstlane(__shfl(got, ld, 64));
+                base = __builtin_amdgcn_readfirstlane(__shfl(base, ld, 64));
+                const uint32_t r = (uint32_t)__popcll(tm & lt);
+                if (tw && r < got) tk = base + r;
+                RF_PROF(pr_sq += got;)
+            }
+        }
+        if (p == ~0u && tk != ~0u) {  // a taken entry: its pusher writes it right after reserving it
+            const unsigned long long e = RF_FLOW_GUARD(tk < a.e, 6, fc) ? ld_ag64(&a.rq[tk]) : 0ull;
+            if (tk >= a.e) tk = ~0u;
+            if ((uint32_t)(e >> 32) == a.epoch && RF_FLOW_GUARD((uint32_t)e < a.e, 7, fc)) {
+                tk = ~0u;
+                start((uint32_t)e);
+            }
+        }
+        RF_PROF(++pr_it;)
         if (__all(p == ~0u)) {
+            // nothing to hash in the wave: advance the watermark, leave once
+            // it has passed the range, else back off (every idle wave polls
+            // the same few lines)
+            RF_PROF(++pr_idle;)
+            if ((idle_n & 3) == 0) flow_advance(a, fc);
             uint32_t done = 0;
             if (lane == 0) {
                 done = ld_ag(fc.lw) >= fc.R;
@@ -2485,8 +2579,13 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
                         fc.err[1] = p0;
                         fc.err[2] = l0;
                         fc.err[3] = ld_ag(&a.counts[l0]);
-                        fc.err[4] = ld_ag(&fc.Q[l0]);
-                        fc.err[5] = ld_ag(&fc.F[l0]);
+                        uint32_t qs = 0, fs = 0;
+                        for (uint32_t k = 0; k < kFlowShards; ++k) {
+                            qs += ld_ag(&fc.Q[k * fc.lp + l0]);
+                            fs += ld_ag(&fc.F[k * fc.lp + l0]);
+                        }
+                        fc.err[4] = qs;
+                        fc.err[5] = fs;
                         fc.err[6] = ld_ag(fc.tail);
                         fc.err[7] = ld_ag(fc.head);
                     }
@@ -2494,54 +2593,62 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
                 }
             }
             if (__builtin_amdgcn_readfirstlane(__shfl(done, 0, 64))) break;
-            __builtin_amdgcn_s_sleep(4);
+            ++idle_n;
+            __builtin_amdgcn_s_sleep(32);
             continue;
         }
-        // 2. one job (a chain head, or the next link of a fused chain) per lane
-        uint32_t cb = 0, cz = 0, nx = ~0u;
-        bool endc = false;
-        if (p != ~0u) {
+        idle_n = 0;
+        // 2. a job's start: its old digest, its fusion target's records, the
+        //    cursor (a head: every hole; a fused link: the one hole handed over)
+        if (p != ~0u && !begun) {
             const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);  // (its own slot: written by no one else)
-            const uint4 olo = od[0], ohi = od[1];
-            const bool nf = m1.w != ~0u;
-            uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0;
-            if (nf) {
-                nm0 = a.meta[2ull * m1.w];
-                nm1 = a.meta[2ull * m1.w + 1];
-            }
-            MatCursorT<true> cur;
-            cur.fslot = fslot;
-            cur.flo = flo4;
-            cur.fhi = fhi4;
+            olo = od[0];
+            ohi = od[1];
             if (fresh)
                 cur.begin(a, m0, ring);
             else
                 cur.begin_fused(a, m0, ring);
-            ShaState st;
             init_state(a, p, st);
-            for (uint32_t b = 0; b < cur.nb; ++b) {
-                uint32_t w[16];
-                cur.block(a, b, ring, w, !fresh);
-                sha256_compress(st, w);
-            }
+            b = 0;
+            begun = true;
+        }
+        // 3. up to kFlowChunk blocks of it
+        for (uint32_t c = 0; c < kFlowChunk; ++c) {
+            if (!(begun && b < cur.nb)) continue;
+            uint32_t w[16];
+            cur.block(a, b, ring, w, !fresh);
+            sha256_compress(st, w);
+            ++b;
+            RF_PROF(++pr_blk;)
+        }
+        RF_PROF({
+            uint32_t nl = p != ~0u ? 1u : 0u;
+            for (int o = 32; o > 0; o >>= 1) nl += __shfl_xor(nl, o, 64);
+            pr_slot += kFlowChunk * 64;
+            pr_lanes += nl;
+        })
+        // 4. a finished job: its digest; the next link, or the chain's end
+        uint32_t cb = 0, cz = 0;
+        bool endc = false, adv = false;
+        if (begun && b == cur.nb) {
+            begun = false;
+            const bool nf = m1.w != ~0u;
             const bool ch = finish_job_ag(a, m1, st, olo, ohi);
             hashed += fresh ? 0u : 1u;
             cb = m1.y;
             cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
             if (ch && nf) {
-                nx = m1.w;
-                fslot = m1.x;
-                flo4 = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
-                fhi4 = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
-                m0 = nm0;
-                m1 = nm1;
+                adv = true;
+                cur.fslot = m1.x;
+                cur.flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                cur.fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
             } else {
                 endc = true;
             }
         }
-        // 3. the changed job's other consumers
+        // 5. the finished job's other consumers
         flow_propagate(a, fc, cb, cz);
-        // 4. a chain's end: the jobs it completes for (pend - 1 each; the one
+        // 6. a chain's end: the jobs it completes for (pend - 1 each; the one
         //    that reaches 0 with its job queued and its watermark reached
         //    starts here next, any further one goes to the ready queue)
         uint32_t next = ~0u;
@@ -2563,23 +2670,44 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
                 }
             }
             atomicExch(&a.dirty[hd], 0u);
-            vm_drain();
-            atomicAdd(&fc.F[hl], 1u);
-            vm_drain();
         }
-        if (__any(endc)) flow_advance(a, fc);
-        if (p != ~0u) {
-            if (!endc) {
-                p = nx;
-                fresh = false;
-            } else if (next != ~0u) {
-                start(next);
-            } else {
-                p = ~0u;
-            }
+        // finished (after every queue count and chain-out count of these
+        // chains: the wave's drain), added once per level by the wave; the
+        // watermark is advanced by idle waves (the jobs that wait on it are
+        // few: only jobs with a producer above the range's first level)
+        if (__any(endc)) {
+            vm_drain();
+            flow_wave_add(fc.F + fc.sh * fc.lp, endc, hl);
+        }
+        if (adv) {
+            p = m1.w;
+            fresh = false;
+            m0 = a.meta[2ull * p];
+            m1 = a.meta[2ull * p + 1];
+        } else if (endc) {
+            p = ~0u;
+            if (next != ~0u) start(next);
         }
     }
     count_fused(a, hashed);
+#ifdef RF_FLOW_PROFILE
+    for (int o = 32; o > 0; o >>= 1) {
+        pr_blk += __shfl_xor(pr_blk, o, 64);
+        pr_list += __shfl_xor(pr_list, o, 64);
+    }
+    if (lane == 0) {
+        uint32_t* w = fc.err + 16;  // (control-block words 112..)
+        atomicAdd(w + 0, pr_it);
+        atomicAdd(w + 1, pr_idle);
+        atomicAdd(w + 2, pr_lanes);
+        atomicAdd(w + 5, pr_list);
+        atomicAdd(w + 6, pr_sq);
+        atomicAdd(w + 7, pr_blk);
+        atomicAdd(w + 8, pr_slot);
+        atomicMax(w + 9, (uint32_t)((__builtin_amdgcn_s_memrealtime() - t_start) / 100));  // us
+        atomicAdd(w + 10, 1u);
+    }
+#endif
 }
 
 // ---- the octo form: levels of few long jobs (GraphDev kLvlOct) ---------------
