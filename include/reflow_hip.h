@@ -363,10 +363,12 @@ int rf_graph_set_forms(rf_graph *g, uint64_t thru, uint64_t thru_wide, uint64_t 
 /* The flow step (readiness-driven: one launch in which a job starts as soon
  * as the jobs it reads have finished, instead of one kernel per level that
  * waits for the whole level below; the reference evaluator's ready loop,
- * /root/reference/eval.go:376-411, todo :902-955).  mode 1 (default): a step
- * whose first levels up to the fill level all run in the throughput form
- * runs them and the sink level in one flow launch; 0: never; 2: every
- * launchable level whenever possible (tests).  Results never depend on it.
+ * /root/reference/eval.go:376-411, todo :902-955).  mode 1: a step whose
+ * first levels up to the fill level all run in the throughput form runs them
+ * and the sink level in one flow launch; 2: every launchable level whenever
+ * possible; 0 (default): never -- on configs[3]'s 100M-node DAG the flow
+ * launch measured slower than the level-by-level step.
+ * Results never depend on it.
  * Takes effect from the next step's first set_slots (a step in progress
  * keeps the choice its first set_slots made). */
 int rf_graph_set_flow(rf_graph *g, int mode);

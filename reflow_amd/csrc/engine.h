@@ -100,7 +100,7 @@ __host__ __device__ constexpr uint32_t flow_lp(uint32_t L) { return (L + 31) / 3
 constexpr uint32_t kFlowLW = 0, kFlowTail = 32, kFlowHead = 64;
 constexpr uint32_t kFlowLTail = 128, kFlowLHead = 160;  // the long-job queue (k2_flow)
 constexpr uint32_t kFlowList = 256;  // the candidate cursors (kFlowListShards, 32 words apart)
-constexpr uint32_t kFlowMaxLevels = 4096;  // range levels one flow launch takes (its LDS tables)
+constexpr uint32_t kFlowMaxLevels = 1024;  // range levels one flow launch takes (its LDS tables)
 constexpr uint32_t kFlowErr = 96;  // nonzero: the launch gave up (k2_flow kFlowTimeout); then where it stood
 __host__ __device__ constexpr uint32_t counts_flow_base(uint32_t L) { return L + 1 + kCountsExtra; }
 __host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFlowShards * flow_lp(L) + L; }
@@ -202,10 +202,12 @@ struct GraphDev {
     unsigned long long* dq = nullptr;
     uint64_t n_cout = 0;
     uint32_t epoch = 0;
-    // flow steps (rf_graph_set_flow): 0 never, 1 (default) when the step's
+    // flow steps (rf_graph_set_flow): 0 (default) never, 1 when the step's
     // first launchable levels up to the fill level all run in the throughput
-    // form, 2 every launchable level whenever possible (tests)
-    uint32_t flow_mode = 1;
+    // form, 2 every launchable level whenever possible.  Off by default: on
+    // configs[3]'s 100M-node step it measured 1.12-1.16 ms of device time
+    // against the level-by-level 0.70-0.72 (DESIGN.md §5 "The flow step")
+    uint32_t flow_mode = 0;
     // this step's flow range, fixed by its first mark (graph_flow_decide):
     // levels [flo, fhi] and the sink level fsink run in one k2_flow launch;
     // flo = ~0u: the step runs level by level

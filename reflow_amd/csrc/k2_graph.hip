@@ -2280,7 +2280,6 @@ __device__ __forceinline__ uint32_t flow_claim(const LevelArgs& a, uint32_t k) {
 
 // The ready queue: jobs a chain end made ready beyond the one its lane runs
 // next, and jobs a sweep of the parking lists claimed.
-constexpr uint32_t kFlowChunk = 4;  // blocks a lane hashes per iteration
 // An index a flow structure gives that falls outside its array: record the
 // site (the host reports it with the step's failure) and skip the access --
 // a scheduling fault must not become a device fault.
@@ -2439,6 +2438,54 @@ __device__ __forceinline__ bool finish_job_ag(const LevelArgs& a, const uint4& m
     return changed;
 }
 
+// hash_fused_chain_lean for the flow step: the links' digests stored
+// write-through, their other consumers queued by flow_propagate.  Returns the
+// links this lane hashed.  Called by every lane of the wave.
+__device__ __forceinline__ uint32_t flow_chain(const LevelArgs& a, const FlowCtl& fc, uint32_t* ring, uint32_t p,
+                                               uint4 m0, uint4 m1, uint32_t fslot, uint4 flo, uint4 fhi) {
+    uint32_t hashed = 0;
+    while (__any(p != ~0u)) {
+        uint32_t cb = 0, cz = 0, nx = ~0u;
+        if (p != ~0u) {
+            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
+            const uint4 olo = od[0], ohi = od[1];
+            const bool nf = m1.w != ~0u;
+            uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0;
+            if (nf) {
+                nm0 = a.meta[2ull * m1.w];
+                nm1 = a.meta[2ull * m1.w + 1];
+            }
+            MatCursorT<true> cur;
+            cur.fslot = fslot;
+            cur.flo = flo;
+            cur.fhi = fhi;
+            cur.begin_fused(a, m0, ring);
+            ShaState st;
+            init_state(a, p, st);
+            for (uint32_t b = 0; b < cur.nb; ++b) {
+                uint32_t w[16];
+                cur.block(a, b, ring, w, true);
+                sha256_compress(st, w);
+            }
+            const bool ch = finish_job_ag(a, m1, st, olo, ohi);
+            ++hashed;
+            cb = m1.y;
+            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);
+            if (ch && nf) {
+                nx = m1.w;
+                fslot = m1.x;
+                flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+                m0 = nm0;
+                m1 = nm1;
+            }
+        }
+        flow_propagate(a, fc, cb, cz);
+        p = nx;
+    }
+    return hashed;
+}
+
 __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs a) {
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     __shared__ uint32_t s_pref[kFlowMaxLev + 1];  // prefix of the range levels' mark-listed counts
@@ -2467,25 +2514,18 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
     if (blockIdx.x == 0 && threadIdx.x < 64) flow_advance(a, fc);
     const uint32_t lane = __lane_id();
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    // the lane's chain: its head (hd, level hl, chain-out range cr), the job
-    // it is on (p; fresh = the head itself, else a fused link whose hole's
-    // digest is flo4/fhi4 in registers), and -- once begun -- that job's
-    // cursor, state and next block b (a job's blocks run kFlowChunk per
-    // iteration: one 18-block job no longer holds its wave's other lanes,
-    // on 2-block links, for 16 blocks)
-    uint32_t p = ~0u, hd = 0, hl = 0, tk = ~0u, b = 0;
-    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, olo = m0, ohi = m0;
+    // the lane's chain: its head (hd, level hl, chain-out range cr, records
+    // m0 / m1); a whole fused chain runs per iteration, as k2_level_lf's
+    // lanes do (hash_fused_chain_lean: each link's old digest and its fusion
+    // target's records fetched at its start, the digest handed over in
+    // registers), and only its end pays the flow protocol
+    uint32_t p = ~0u, hd = 0, hl = 0, tk = ~0u;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
     uint2 cr = make_uint2(0, 0);
-    bool fresh = false, begun = false;
-    MatCursorT<true> cur;  // (cur.fslot / flo / fhi: the digest a fused link's hole reads, in registers)
-    cur.fslot = ~0u;
-    ShaState st;
     uint32_t hashed = 0, idle_n = 0;
-    // the candidates in kFlowListShards slices of the scattered order, each
-    // with a cursor; a wave starts on its own slice and moves on when it is
-    // used up (wave-uniform: ls, ltried)
-    const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    uint32_t ls = wid % kFlowListShards, ltried = n_list ? 0u : kFlowListShards;
+    // the candidates in list order (level by level: a wave's lanes take
+    // jobs of one kind), one cursor drawn by whole waves
+    bool lists = n_list > 0;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #ifdef RF_FLOW_PROFILE
     // diagnostic build: per-wave tallies added to the control block's words
@@ -2498,8 +2538,6 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
     auto start = [&](uint32_t k) {
         if (!RF_FLOW_GUARD(k < a.e, 9, fc)) return;
         p = hd = k;
-        fresh = true;
-        begun = false;
         m0 = a.meta[2ull * k];
         m1 = a.meta[2ull * k + 1];
         hl = a.jlv[k].x;
@@ -2509,24 +2547,17 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
         // 1. work for idle lanes: the candidates the mark kernel listed, else
         //    ready jobs another lane's chain end queued
         {
-            const bool want = p == ~0u && tk == ~0u && ltried < kFlowListShards;
+            const bool want = p == ~0u && tk == ~0u && lists;
             const uint64_t wm = __ballot(want);
             if (wm) {
                 const uint32_t cnt = (uint32_t)__popcll(wm);
                 const uint32_t ld = (uint32_t)__ffsll((unsigned long long)wm) - 1;
-                const uint32_t lo = (uint32_t)((uint64_t)n_list * ls / kFlowListShards);
-                const uint32_t hi = (uint32_t)((uint64_t)n_list * (ls + 1) / kFlowListShards);
                 uint32_t base = 0;
-                if (lane == ld) base = atomicAdd(&fc.lcur[32 * ls], cnt);
+                if (lane == ld) base = atomicAdd(fc.lcur, cnt);
                 base = __builtin_amdgcn_readfirstlane(__shfl(base, ld, 64));
-                if (lo + base + cnt >= hi) {  // this slice is used up: the next one (wave-uniform)
-                    ls = (ls + 1) % kFlowListShards;
-                    ++ltried;
-                }
-                const uint32_t i = lo + base + (uint32_t)__popcll(wm & lt);
-                if (want && i < hi) {
-                    // a scattered order over the lists (a bijection of [0, n_list))
-                    const uint32_t pos = (uint32_t)(((uint64_t)i * 2654435761ull) % n_list);
+                if (base + cnt >= n_list) lists = false;  // (wave-uniform)
+                const uint32_t pos = base + (uint32_t)__popcll(wm & lt);
+                if (want && pos < n_list) {
                     uint32_t a0 = 0, a1 = fc.R;  // s_pref[a0] <= pos < s_pref[a1]
                     while (a1 - a0 > 1) {
                         const uint32_t mid = (a0 + a1) >> 1;
@@ -2542,7 +2573,7 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
             }
         }
         {
-            const bool tw = p == ~0u && tk == ~0u && ltried >= kFlowListShards;
+            const bool tw = p == ~0u && tk == ~0u && !lists;
             const uint64_t tm = __ballot(tw);
             if (tm) {
                 const uint32_t ld = (uint32_t)__ffsll((unsigned long long)tm) - 1;
@@ -2598,62 +2629,53 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
             continue;
         }
         idle_n = 0;
-        // 2. a job's start: its old digest, its fusion target's records, the
-        //    cursor (a head: every hole; a fused link: the one hole handed over)
-        if (p != ~0u && !begun) {
-            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);  // (its own slot: written by no one else)
-            olo = od[0];
-            ohi = od[1];
-            if (fresh)
-                cur.begin(a, m0, ring);
-            else
-                cur.begin_fused(a, m0, ring);
-            init_state(a, p, st);
-            b = 0;
-            begun = true;
-        }
-        // 3. up to kFlowChunk blocks of it
-        for (uint32_t c = 0; c < kFlowChunk; ++c) {
-            if (!(begun && b < cur.nb)) continue;
-            uint32_t w[16];
-            cur.block(a, b, ring, w, !fresh);
-            sha256_compress(st, w);
-            ++b;
-            RF_PROF(++pr_blk;)
-        }
         RF_PROF({
             uint32_t nl = p != ~0u ? 1u : 0u;
             for (int o = 32; o > 0; o >>= 1) nl += __shfl_xor(nl, o, 64);
-            pr_slot += kFlowChunk * 64;
             pr_lanes += nl;
         })
-        // 4. a finished job: its digest; the next link, or the chain's end
-        uint32_t cb = 0, cz = 0;
-        bool endc = false, adv = false;
-        if (begun && b == cur.nb) {
-            begun = false;
-            const bool nf = m1.w != ~0u;
-            const bool ch = finish_job_ag(a, m1, st, olo, ohi);
-            hashed += fresh ? 0u : 1u;
-            cb = m1.y;
-            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
-            if (ch && nf) {
-                adv = true;
-                cur.fslot = m1.x;
-                cur.flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
-                cur.fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
-            } else {
-                endc = true;
+        // 2. each lane's job (every hole from the slot table), then its fused
+        //    chain (the one hole's digest handed over in registers); the wave
+        //    runs until every lane's chain has ended
+        const bool had = p != ~0u;
+        {
+            uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
+            uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
+            if (had) {
+                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);  // (its own slot)
+                const uint4 olo = od[0], ohi = od[1];
+                MatCursorT<true> cur;
+                cur.begin(a, m0, ring);
+                ShaState st;
+                init_state(a, p, st);
+                for (uint32_t bb = 0; bb < cur.nb; ++bb) {
+                    uint32_t w[16];
+                    cur.block(a, bb, ring, w);
+                    sha256_compress(st, w);
+                }
+                RF_PROF(pr_blk += cur.nb;)
+                const bool ch = finish_job_ag(a, m1, st, olo, ohi);
+                const bool nf = m1.w != ~0u;
+                cb = m1.y;
+                cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
+                if (ch && nf) {
+                    nx = m1.w;
+                    fslot = m1.x;
+                    flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
+                    fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
+                    nm0 = a.meta[2ull * nx];
+                    nm1 = a.meta[2ull * nx + 1];
+                }
             }
+            flow_propagate(a, fc, cb, cz);
+            hashed += flow_chain(a, fc, ring, nx, nm0, nm1, fslot, flo, fhi);
         }
-        // 5. the finished job's other consumers
-        flow_propagate(a, fc, cb, cz);
-        // 6. a chain's end: the jobs it completes for (pend - 1 each; the one
-        //    that reaches 0 with its job queued and its watermark reached
-        //    starts here next, any further one goes to the ready queue)
+        // 3. the chain's end: the jobs it completes for (pend - 1 each; the
+        //    one that reaches 0 with its job queued and its watermark reached
+        //    starts in this lane next, any further one goes to the ready queue)
         uint32_t next = ~0u;
-        if (endc) {
-            vm_drain();  // its digests (write-through) and queue counts first
+        vm_drain();  // the chains' digests (write-through) and queue counts first
+        if (had) {
             for (uint32_t e = cr.x; e < cr.y; e += 4) {
                 uint2 o[4];
                 uint32_t r[4];
@@ -2672,22 +2694,13 @@ __global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs 
             atomicExch(&a.dirty[hd], 0u);
         }
         // finished (after every queue count and chain-out count of these
-        // chains: the wave's drain), added once per level by the wave; the
-        // watermark is advanced by idle waves (the jobs that wait on it are
-        // few: only jobs with a producer above the range's first level)
-        if (__any(endc)) {
-            vm_drain();
-            flow_wave_add(fc.F + fc.sh * fc.lp, endc, hl);
-        }
-        if (adv) {
-            p = m1.w;
-            fresh = false;
-            m0 = a.meta[2ull * p];
-            m1 = a.meta[2ull * p + 1];
-        } else if (endc) {
-            p = ~0u;
-            if (next != ~0u) start(next);
-        }
+        // chains), added once per level by the wave; the watermark is
+        // advanced by idle waves (the jobs that wait on it are few: only jobs
+        // with a producer above the range's first level)
+        vm_drain();
+        flow_wave_add(fc.F + fc.sh * fc.lp, had, hl);
+        p = ~0u;
+        if (next != ~0u) start(next);
     }
     count_fused(a, hashed);
 #ifdef RF_FLOW_PROFILE

@@ -118,7 +118,7 @@ def _steps(g, slots, versions):
 
 @pytest.mark.parametrize("frac", [0.01, 0.3])
 def test_flow_auto_equals_levels(ctx, frac):
-    """The default choice (mode 1) on a 0.45M-node 1000align DAG whose levels
+    """The automatic choice (mode 1) on a 0.45M-node 1000align DAG whose levels
     all run in the throughput form (set_forms(0)): the Exec, OpK and sink
     levels in one flow launch; slot for slot and count for count against the
     same graph stepped level by level."""
@@ -126,6 +126,7 @@ def test_flow_auto_equals_levels(ctx, frac):
     sl, old, new = dag.change_set(frac)
     every = np.arange(dag.n_slots, dtype=np.uint32)
     gf, gl = load_dag(ctx, dag), load_dag(ctx, dag)
+    gf.set_flow(1)
     gl.set_flow(0)
     for g in (gf, gl):
         g.recompute(full=True)
@@ -151,6 +152,7 @@ def test_flow_merge_tree_vs_oracle(ctx):
     g.set_slots(pc.dag.file_slots, pc.dag.leaf_ids)
     g.recompute(True)
     g.set_forms(0)
+    g.set_flow(1)
     every = np.arange(pc.desc["n_slots"], dtype=np.uint32)
     ids = pc.dag.leaf_ids.copy()
     slots, old, new = pc.dag.change_set(0.05)

@@ -24,8 +24,8 @@ from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
 # pl: every level in the latency form; lf: every level in the throughput
 # form; auto: the library's per-level choice (the default thresholds)
-# noflow: the library's choice with the flow step off (rf_graph_set_flow 0)
-FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None, "noflow": None}
+# flow: the library's choice with the flow step on (rf_graph_set_flow 1; off by default)
+FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None, "flow": None}
 
 
 def run(ctx, name, g, slots, old, new, steps):
@@ -40,7 +40,7 @@ def run(ctx, name, g, slots, old, new, steps):
                 g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
             else:
                 g.set_forms(thr)
-            g.set_flow(0 if form == "noflow" else 1)
+            g.set_flow(1 if form == "flow" else 0)
             state = {"v": 0}
 
             def step():
@@ -71,7 +71,7 @@ def run(ctx, name, g, slots, old, new, steps):
                   file=sys.stderr, flush=True)
     res["slots_equal"] = bool(all((snaps["pl"] == snaps[f]).all() for f in snaps))
     g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
-    g.set_flow(1)
+    g.set_flow(0)
     for b in (d_slots, d_old, d_new):
         b.free()
     return res
