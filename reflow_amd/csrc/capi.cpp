@@ -1350,10 +1350,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // queued either.  RF_K2_SLOT_FUSE=0: off (A/B).
     std::vector<uint8_t> slot_fused(J, 0);
     {
-        static const bool on = [] {
-            const char* v = getenv("RF_K2_SLOT_FUSE");
-            return !(v && atoi(v) == 0);
-        }();
+        static const bool on = RF_DIAG_KNOB("RF_K2_SLOT_FUSE", 1) != 0;
         if (on)
             for (uint32_t s = 0; s < S; ++s) {
                 if (gr->producer[s] >= 0) continue;
@@ -1388,10 +1385,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // ms/step, sink_attach_ab.log).  1: the last level (A/B); 0: off.
     uint32_t sink_fill = ~0u, sink_min = 0;
     {
-        static const int alap = [] {
-            const char* v = getenv("RF_K2_SINK_ALAP");
-            return v ? atoi(v) : 2;
-        }();
+        static const int alap = (int)RF_DIAG_KNOB("RF_K2_SINK_ALAP", 2);
         auto sink = [&](uint32_t j) { return cptr[d->out_slot[j]] == cptr[d->out_slot[j] + 1]; };
         int64_t lq = -1;
         std::vector<uint64_t> nsq(L, 0);
@@ -1683,10 +1677,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         if (e != hipSuccess) return e;
         return bytes ? sync_copy(ctx, b.p, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
     };
-    {
-        const char* v = getenv("RF_K2_STREAM");  // (opt-in variant, read per load)
-        G.stream_handover = v && atoi(v) == 1;
-    }
+    G.stream_handover = RF_DIAG_KNOB("RF_K2_STREAM", 0) == 1;  // (the streamed hand-over: diagnostic builds)
     graph_forms_from_env(G);
     G.n_cu = graph_ovf_cus(ctx, &G.ovf_mode);
     if (n_lead && !getenv("RF_K2_NO_MIDSTATE")) {  // (RF_K2_NO_MIDSTATE: A/B)
@@ -1717,12 +1708,12 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // so its block 1 is template only
     G.split_b0 = G.hole_in_b0 && G.fuse_pos2 ? graph_split_on() : 0u;
     lap("midstates");
-    if (getenv("RF_K2_STAMPS")) {  // diagnostic: per-phase times of workgroup 0 of each level
+    if (RF_DIAG_KNOB("RF_K2_STAMPS", 0)) {  // diagnostic build: per-phase times of workgroup 0 of each level
         HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
         G.stamps = static_cast<unsigned long long*>(gr->b_stamps.p);
     }
-    if (getenv("RF_K2_WGSTAMPS")) {  // diagnostic: every incremental level kernel's workgroups
+    if (RF_DIAG_KNOB("RF_K2_WGSTAMPS", 0)) {  // diagnostic build: every incremental level kernel's workgroups
         const uint64_t bytes = 8ull * 4 * 2048 * std::max<uint32_t>(L, 1);
         HIPC(gr->b_wgst.ensure(bytes));
         HIPC(sync_memset(ctx, gr->b_wgst.p, 0, bytes));
@@ -1810,8 +1801,8 @@ static constexpr uint64_t kThruSlots = RF_K2_THRU_DEFAULT, kThruSlotsWide = RF_K
 // overflow a pretended 4-CU chip); and their mode, RF_K2_OVF (0 off, 1 on,
 // 2 at the chains' wave priority).  Read at load / restore.
 uint32_t graph_ovf_cus(const rf_ctx* ctx, uint32_t* mode) {
-    const char* m = getenv("RF_K2_OVF");
-    *mode = m ? (uint32_t)std::min(std::max(atoi(m), 0), 2) : 0u;  // (off by default: see DESIGN.md §5)
+    // the overflow lanes (measured slower): diagnostic builds only
+    *mode = (uint32_t)std::min<long>(std::max<long>(RF_DIAG_KNOB("RF_K2_OVF", 0), 0), 2);
     const char* v = getenv("RF_K2_OVF_CU");
     return v && atoi(v) > 0 ? (uint32_t)atoi(v) : (uint32_t)ctx->n_cu;
 }
@@ -1832,14 +1823,12 @@ uint32_t graph_split_on() {
 void graph_forms_from_env(GraphDev& G) {
     {
         const char* v = getenv("RF_K2_SINK_AT");
-        const char* w = getenv("RF_K2_SINK_LAST");  // (round-4 scripts: =0 the fill level)
-        G.sink_at = v ? (uint32_t)std::min(std::max(atoi(v), 0), 4) : (w && atoi(w) == 0) ? 0u : 2u;
+        G.sink_at = v ? (uint32_t)std::min(std::max(atoi(v), 0), 4) : 2u;
     }
     {
         const char* v = getenv("RF_K2_SPLIT_HALF");
         G.split_half = v && atoi(v) == 1 ? 1u : 0u;
-        const char* m = getenv("RF_K2_DBG_MARK");
-        G.dbg_mark = m ? (uint32_t)atoi(m) : 0u;
+        G.dbg_mark = (uint32_t)RF_DIAG_KNOB("RF_K2_DBG_MARK", 0);  // (diagnostic builds: stats wrong, digests right)
     }
     const char* tv = getenv("RF_K2_THRU");
     const char* tw = getenv("RF_K2_THRU_WIDE");
@@ -2056,7 +2045,10 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
         if (swap) std::swap(G.counts, G.counts_other);
         return RF_OK;
     }
-    G.thru_slots = G.thru_slots_wide = ~0ull;  // (captured sequences: the latency form)
+    // captured sequences: the latency form, 64-job workgroups (no per-step
+    // choice may be frozen into a graph from the last plain step's change set)
+    G.thru_slots = G.thru_slots_wide = ~0ull;
+    G.step_marked = 0;
     for (uint32_t l = 0; l < G.n_levels; ++l) HIPC(launch_graph_level(G, l, full, s));
     HIPC(launch_graph_step_end(G, full, s));
     gr->last_counts = G.counts_last;
@@ -2093,15 +2085,12 @@ static int graph_capture(rf_graph* gr, int full, hipGraphExec_t* out) {
 // graph.  RF_K2_GRAPH=1: the incremental graph (A/B).
 // RF_K2_EVENTS=1: record the timing events on asynchronous recomputes too
 static bool events_always() {
-    static const bool on = getenv("RF_K2_EVENTS") && atoi(getenv("RF_K2_EVENTS")) == 1;
+    static const bool on = RF_DIAG_KNOB("RF_K2_EVENTS", 0) == 1;
     return on;
 }
 
 static bool inc_plain() {
-    static const bool on = [] {
-        const char* v = getenv("RF_K2_GRAPH");
-        return !(v && atoi(v) == 1);
-    }();
+    static const bool on = RF_DIAG_KNOB("RF_K2_GRAPH", 0) != 1;
     return on;
 }
 
@@ -2110,10 +2099,7 @@ bool graph_plain_steps() { return inc_plain(); }
 int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s, uint32_t lvl_lo, uint32_t lvl_hi, bool swap) {
     if (!gr->initialized) full = 1;
     const bool no_graph = inc_plain();
-    static const bool full_plain = [] {  // RF_K2_FULL_GRAPH=0 (A/B): the full recompute as plain launches too
-        const char* v = getenv("RF_K2_FULL_GRAPH");
-        return v && atoi(v) == 0;
-    }();
+    static const bool full_plain = RF_DIAG_KNOB("RF_K2_FULL_GRAPH", 1) == 0;  // (A/B: the full recompute as plain launches)
     if ((no_graph && !full) || (full_plain && full)) {
         // the timing events (rf_graph_stats.last_ms) only where a caller waits
         // anyway: each event record put a ~6 us bubble on either side of the

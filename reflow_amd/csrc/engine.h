@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include "diag.h"
+
 namespace rf {
 
 // ---- K1: batched SHA-256 -------------------------------------------------

@@ -382,10 +382,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     GraphDev& G = gr->g;
     G.hole_in_b0 = (h.flags & kHoleInB0) != 0;
     G.fuse_pos2 = (h.flags & kFusePos2) != 0;
-    {
-        const char* v = getenv("RF_K2_STREAM");
-        G.stream_handover = v && atoi(v) == 1;
-    }
+    G.stream_handover = RF_DIAG_KNOB("RF_K2_STREAM", 0) == 1;
     graph_forms_from_env(G);
     G.n_cu = graph_ovf_cus(ctx, &G.ovf_mode);
     if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes, h.n_cout))

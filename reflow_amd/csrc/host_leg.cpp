@@ -11,16 +11,13 @@
 #include <chrono>
 #include <cmath>
 
+#include "diag.h"
 #include "host_sha.h"
 
 namespace rf {
 
 uint64_t host_chunk_bytes() {
-    static const uint64_t c = [] {
-        const char* v = getenv("RF_HOST_CHUNK_MB");
-        const uint64_t mb = v ? (uint64_t)std::max(1, atoi(v)) : 8ull;
-        return mb << 20;
-    }();
+    static const uint64_t c = (uint64_t)std::max<long>(1, RF_DIAG_KNOB("RF_HOST_CHUNK_MB", 8)) << 20;
     return c;
 }
 
@@ -141,10 +138,7 @@ hipError_t HostPool::stage(unsigned w, int ways, Stage** out) {
 }
 
 int host_ways() {
-    static const int w = [] {
-        const char* v = getenv("RF_HOST_WAYS");
-        return v ? std::min(4, std::max(1, atoi(v))) : 2;
-    }();
+    static const int w = (int)std::min<long>(4, std::max<long>(1, RF_DIAG_KNOB("RF_HOST_WAYS", 2)));
     return w;
 }
 

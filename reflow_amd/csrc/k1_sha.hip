@@ -701,10 +701,7 @@ hipError_t launch_sha_octo(const SoloArgs& a, hipStream_t s) {
     if (a.n_order == 0) return hipSuccess;
     uint32_t grid = (a.n_order + 7) / 8;
     if (grid > 8192) grid = 8192;
-    static const size_t reserve = [] {
-        const char* v = getenv("RF_OCTO_LDS_KB");
-        return v ? (size_t)atoi(v) * 1024 : (size_t)0;
-    }();
+    static const size_t reserve = (size_t)RF_DIAG_KNOB("RF_OCTO_LDS_KB", 0) * 1024;
     hipLaunchKernelGGL(k1_sha256_octo, dim3(grid), dim3(128), reserve, s, a);
     return hipGetLastError();
 }

@@ -3123,7 +3123,9 @@ static void flow_args(const GraphDev& g, LevelArgs& a) {
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
-    if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic: k3_mark_slots_lf skips its count)
+#ifdef RF_DIAG
+    if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
+#endif
     flow_args(g, a);  // a flow step's mark queues with chain-out counts (propagate)
     return a;
 }
@@ -3191,14 +3193,8 @@ bool graph_level_lf(const GraphDev& g, uint32_t lvl) {
 // Half workgroups (k2_level_pl<2, false, 32>) for a latency-form level of
 // short jobs estimated at 64-96 chains per CU (RF_K2_HALF=0: never, A/B)
 bool graph_level_half(const GraphDev& g, uint32_t lvl) {
-    static const bool half_ok = [] {
-        const char* v = getenv("RF_K2_HALF");
-        return !(v && atoi(v) == 0);
-    }();
-    static const bool one_lane = [] {
-        const char* v = getenv("RF_K2_CHAIN");
-        return v && atoi(v) == 14;
-    }();
+    static const bool half_ok = RF_DIAG_KNOB("RF_K2_HALF", 1) != 0;
+    static const bool one_lane = RF_DIAG_KNOB("RF_K2_CHAIN", 9) == 14;
     const uint64_t est = std::min<uint64_t>(g.lvl_start[lvl + 1] - g.lvl_start[lvl], g.step_marked);
     return half_ok && !one_lane && (g.inc_level[lvl] & kLvlForm) == 1 && !(g.inc_level[lvl] & kLvlOct) &&
            !g.stream_handover && g.n_cu && est > 64ull * g.n_cu && est <= 96ull * g.n_cu && !graph_level_lf(g, lvl);
@@ -3213,37 +3209,26 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     // skips assembling + expanding blocks >= 1 (3) or every block (4); =5
     // (A/B, digests right): no instruction-cache warm-up in k2_level_pl's pass 0;
     // =6 (A/B): k2_level_pl<3>'s frontier atomics on the chain, not the producer
-    static const uint32_t dbg2 = getenv("RF_DBG_HASH2") ? 1u
-                                 : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 2) ? 2u
-                                 : (getenv("RF_K2_STAMPS") && atoi(getenv("RF_K2_STAMPS")) == 3) ? 8u
-                                 : getenv("RF_K2_DBG_NOEXP") ? (uint32_t)atoi(getenv("RF_K2_DBG_NOEXP"))
-                                                              : 0u;
+    // (diagnostic build only) RF_DBG_HASH2 -> 1, RF_K2_STAMPS=2|3 -> 2|8,
+    // else RF_K2_DBG_NOEXP (3|4: WRONG digests, a timing probe)
+    static const uint32_t dbg2 = RF_DIAG_KNOB("RF_DBG_HASH2", 0) ? 1u
+                                 : RF_DIAG_KNOB("RF_K2_STAMPS", 0) == 2 ? 2u
+                                 : RF_DIAG_KNOB("RF_K2_STAMPS", 0) == 3 ? 8u
+                                                                       : (uint32_t)RF_DIAG_KNOB("RF_K2_DBG_NOEXP", 0);
     // RF_K2_CB0=0: fused jobs' block 0 built by the producer (A/B), else by the chain
-    static const uint32_t cb0 = [] {
-        const char* v = getenv("RF_K2_CB0");
-        return (v && atoi(v) == 0) ? 0u : 1u;
-    }();
+    static const uint32_t cb0 = RF_DIAG_KNOB("RF_K2_CB0", 1) == 0 ? 0u : 1u;
     // RF_K2_REV=0: the list in append order (A/B)
-    static const uint32_t rev = [] {
-        const char* v = getenv("RF_K2_REV");
-        return (v && atoi(v) == 0) ? 0u : 1u;
-    }();
+    static const uint32_t rev = RF_DIAG_KNOB("RF_K2_REV", 1) == 0 ? 0u : 1u;
     LevelArgs a{b, e, lvl, full, dbg2, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, g.stamps, g.mid, g.cons_ptr, g.lmeta,
                 g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
                 full ? nullptr : g.wgst};
     a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
-    static const uint32_t handoff = [] {  // RF_K2_HANDOFF=0: the chain fetches them itself (A/B)
-        const char* v = getenv("RF_K2_HANDOFF");
-        return (v && atoi(v) == 0) ? 0u : 1u;
-    }();
+    static const uint32_t handoff = RF_DIAG_KNOB("RF_K2_HANDOFF", 1) == 0 ? 0u : 1u;  // (0: the chain fetches them itself)
     a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
     // per CU, all resident) cover any level's list with a grid-stride loop
-    static const uint32_t inc_cap = [] {
-        const char* v = getenv("RF_INC_GRID");
-        return v ? (uint32_t)atoi(v) : 1024u;
-    }();
+    static const uint32_t inc_cap = (uint32_t)RF_DIAG_KNOB("RF_INC_GRID", 1024);
     if (!full) {
         if (!(g.inc_level[lvl] & kLvlForm)) return hipSuccess;  // every job of the level is a fusion target
         // an attached sink list: its jobs after the level's own, same launch
@@ -3255,17 +3240,11 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         }
         // grid cap (RF_K2_GRID): workgroups past the dirty count exit at once,
         // but each still costs a dispatch before the kernel can end
-        static const uint64_t wg_cap = [] {
-            const char* v = getenv("RF_K2_GRID");
-            return v ? (uint64_t)strtoull(v, nullptr, 10) : 2048ull;
-        }();
+        static const uint64_t wg_cap = (uint64_t)RF_DIAG_KNOB("RF_K2_GRID", 2048);
         uint64_t wg = (e - b + n2 + 63) / 64;
         if (wg > wg_cap) wg = wg_cap;
         // RF_K2_CHAIN=14: the one-lane chain (k2_level_pc), for A/B runs
-        static const bool one_lane = [] {
-            const char* v = getenv("RF_K2_CHAIN");
-            return v && atoi(v) == 14;
-        }();
+        static const bool one_lane = RF_DIAG_KNOB("RF_K2_CHAIN", 9) == 14;
         // a level of few long jobs (kLvlOct): the octo form, 8 jobs a
         // workgroup, then an attached sink list's workgroups (128 jobs each)
         if ((g.inc_level[lvl] & kLvlOct) && !one_lane) {
@@ -3282,10 +3261,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         // RF_K2_PAD_KB: dynamic LDS per workgroup on top of the static arrays
         // (A/B: enough to keep a second workgroup off the CU, so no wave
         // shares a SIMD with another workgroup's prioritised chain wave)
-        static const uint32_t pad = [] {
-            const char* v = getenv("RF_K2_PAD_KB");
-            return v ? (uint32_t)atoi(v) * 1024u : 0u;
-        }();
+        static const uint32_t pad = (uint32_t)RF_DIAG_KNOB("RF_K2_PAD_KB", 0) * 1024u;
         if (one_lane && sink_lvl != ~0u) {  // (k2_level_pc takes no attached list: the sink level after it)
             if (hipError_t err = launch_graph_level(g, lvl, 0, s, zero_counts)) return err;
             return launch_graph_level(g, sink_lvl, 0, s);
@@ -3293,10 +3269,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         if (graph_level_lf(g, lvl)) {
             // the throughput form: 256 lanes per workgroup, four resident per
             // CU, grid-stride over the device-side count
-            static const uint64_t lf_cap = [] {
-                const char* v = getenv("RF_K2_LF_GRID");
-                return v ? (uint64_t)strtoull(v, nullptr, 10) : 1024ull;
-            }();
+            static const uint64_t lf_cap = (uint64_t)RF_DIAG_KNOB("RF_K2_LF_GRID", 1024);
             uint64_t lg = (e - b + n2 + kLevelBlock - 1) / kLevelBlock;
             if (lg > lf_cap) lg = lf_cap;
             hipLaunchKernelGGL(k2_level_lf, dim3((uint32_t)lg), dim3(kLevelBlock), 0, s, a);
@@ -3305,10 +3278,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
         // the latency form with an attached sink list: the level's own list
         // in its workgroups, the sinks one per lane in low-priority
         // workgroups after them (RF_K2_SINK_LANES=0: sinks as listed jobs, A/B)
-        static const bool sink_lanes = [] {
-            const char* v = getenv("RF_K2_SINK_LANES");
-            return !(v && atoi(v) == 0);
-        }();
+        static const bool sink_lanes = RF_DIAG_KNOB("RF_K2_SINK_LANES", 1) != 0;
         // the overflow of a latency-form level a little wider than the chip
         // (estimated from the step's marked slots: more than one 64-job
         // workgroup per CU) -- one workgroup per CU takes 64 chains, the rest

@@ -122,8 +122,7 @@ extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
     // wait for the exchange -- a step then hashes each import reader once
     // (configs[3]'s global root on rank 0: 1+1 hashes of 5 blocks and five
     // empty level launches fewer).  RF_PART_DEFER=0: off (A/B).
-    const char* dv = getenv("RF_PART_DEFER");
-    if (P->rounds && P->nranks > 1 && P->n_import && !(dv && atoi(dv) == 0)) {
+    if (P->rounds && P->nranks > 1 && P->n_import && RF_DIAG_KNOB("RF_PART_DEFER", 1) != 0) {
         const GraphDev& G = gr->g;
         uint32_t lmin = ~0u;
         for (uint32_t i = 0; i < p->n_import; ++i) {

@@ -3,6 +3,7 @@
 // of flow.go:675-792 / executor.go:214-233; every SHA-256 is
 // computed by the device through rf_graph_* / rf_sha256_batch /
 // rf_fileset_digest_batch.
+#include "diag.h"
 #include "reflow_host.hpp"
 
 #include <algorithm>
@@ -848,7 +849,7 @@ void PostOrder(Flow* root, unsigned threads, std::vector<Flow*>& post, PtrIndex&
             index.insert(root, (uint32_t)post.size());
             post.push_back(root);
         }
-        if (getenv("RF_LOWER_CHECK_ORDER")) {  // diagnostic: the sequential walk, compared node for node
+        if (RF_DIAG_KNOB("RF_LOWER_CHECK_ORDER", 0)) {  // diagnostic build: the sequential walk, compared node for node
             Index seen;
             std::vector<Flow*> seq;
             dfs(root, seen, seq);
