@@ -502,20 +502,13 @@ def bench_c1_install(ctx, arena, offs, want_fsd, cpu_leg=False):
 
 
 # ---------------------------------------------------------- lowering leg --
-def bench_lowering(args):
-    """The per-Eval host cost a Go shim pays before the device sees a job:
-    tools/lower_bench (the product's C++ host mirror, include/reflow_host.hpp)
-    builds a configs[2]-sized 1000align Flow graph, Canonicalizes it, lowers
-    it to rf_graph jobs, loads it, and takes one 1%-of-files incremental step
-    (checked against a full recompute)."""
+def _lower_run(args, dup):
     import subprocess
     exe = os.path.join(ROOT, "tools", "lower_bench")
-    if not os.path.exists(exe):
-        return {"skipped": "tools/lower_bench not built"}
     t0 = time.perf_counter()
+    cmd = [exe, str(args.dag_samples), str(args.dag_pairs)] + (["dup"] if dup else [])
     try:
-        r = subprocess.run([exe, str(args.dag_samples), str(args.dag_pairs)], capture_output=True, text=True,
-                           timeout=300)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     except subprocess.TimeoutExpired:
         return {"error": "timed out after 300 s"}
     wall = time.perf_counter() - t0
@@ -528,11 +521,36 @@ def bench_lowering(args):
     if phases:
         res["phases_s"] = {ph[0]: float(ph[1]) for ph in phases if len(ph) == 3}
         log("lowering phases: " + ", ".join("%s %.2f" % kv for kv in res["phases_s"].items()))
+    log("lowering%s: %d nodes: build %.1f s, canonicalize %.1f s (%d collapsed), lower %.1f s, load %.1f s, "
+        "incremental %.1f ms" % (" (per-sample reference chains)" if dup else "", res["nodes"], res["build_s"],
+                                 res["canonicalize_s"], res.get("collapsed", 0), res["lower_s"], res["load_s"],
+                                 res["incremental_s"] * 1e3))
+    return res
+
+
+def bench_lowering(args):
+    """The per-Eval host cost a Go shim pays before the device sees a job:
+    tools/lower_bench (the product's C++ host mirror, include/reflow_host.hpp)
+    builds a configs[2]-sized 1000align Flow graph, Canonicalizes it, lowers
+    it to rf_graph jobs, loads it, and takes one 1%-of-files incremental step
+    (checked against a full recompute).  Run twice: the shared reference
+    chain (nothing collapses), and every sample with its own copy of it
+    ("collapsed_graph": Canonicalize collapses the copies and hands over its
+    Eval with their jobs dropped -- its root must equal the first run's)."""
+    if not os.path.exists(os.path.join(ROOT, "tools", "lower_bench")):
+        return {"skipped": "tools/lower_bench not built"}
+    res = _lower_run(args, False)
+    if "error" in res:
+        return res
     res["what"] = ("tools/lower_bench: reflow::Canonicalize + Eval lowering (reflow_host.cpp) of a 1000align "
                    "Flow graph of the configs[2] shape; load = blob + rf_graph_load + full recompute")
-    log("lowering: %d nodes: build %.1f s, canonicalize %.1f s, lower %.1f s, load %.1f s, incremental %.1f ms"
-        % (res["nodes"], res["build_s"], res["canonicalize_s"], res["lower_s"], res["load_s"],
-           res["incremental_s"] * 1e3))
+    dup = _lower_run(args, True)
+    if "error" not in dup:
+        dup["root_equals_shared_chain"] = dup.get("root") == res.get("root")
+        res["collapsed"] = dup.get("collapsed", 0)
+        res["collapsed_canonicalize_s"] = dup.get("canonicalize_s")
+        res["collapsed_incremental_equals_full"] = dup.get("incremental_equals_full")
+    res["collapsed_graph"] = dup
     return res
 
 

@@ -388,11 +388,14 @@ class Eval;
 // Canonicalize (flow.go:814-843): copies merged with `config`, semantically
 // equal nodes (equal digests) collapsed to the first one in visit order.
 // The copies' digests come from the device: an Eval (file slots on) over the
-// copies, lowered, loaded and fully recomputed.  `lowered` (optional): when
-// no two copies share a digest, the canonical graph IS the copies' graph and
-// that Eval is handed over ready for FlowDigest / CacheKeys / SetFileID +
-// Recompute -- the caller's Eval.Add + Build of the same graph (what a fresh
-// Eval does after Canonicalize, eval.go:240-272) is skipped; null otherwise.
+// copies, lowered, loaded and fully recomputed.  `lowered` (optional): that
+// Eval handed over ready for FlowDigest / CacheKeys / SetFileID + Recompute
+// of the canonical graph -- the caller's Eval.Add + Build of the same graph
+// (what a fresh Eval does after Canonicalize, eval.go:240-272) is skipped.
+// When copies collapsed, the handed-over Eval's duplicate jobs are dropped,
+// holes that named a duplicate name its class's first copy, and a duplicate's
+// lookups answer with its first copy's slots (Eval::Collapsed() counts them);
+// the table is reloaded and recomputed without a second lowering.
 Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config,
                    const std::string& universe = "", std::unique_ptr<Eval>* lowered = nullptr);
 
@@ -414,6 +417,7 @@ class Eval {
     void SetFileID(const Digest& old_id, const Digest& new_id);
     uint64_t Recompute(bool full = false);
     size_t Jobs() const { return out_slot_.size(); }
+    size_t Collapsed() const { return collapsed_; }  // copies Canonicalize collapsed into a first copy
 
    private:
     friend Flow* Canonicalize(Engine&, FlowArena&, Flow*, Config, const std::string&, std::unique_ptr<Eval>*);
@@ -429,11 +433,17 @@ class Eval {
         size_t n;
         uint32_t slot0;
         std::vector<uint32_t> phys;  // physical slot per node, ~0u: none
+        std::vector<uint32_t> canon;  // (after a collapse) node -> its class's first node; empty: itself
+        size_t at(const Flow* f) const {
+            const size_t i = (size_t)(f - base);
+            return canon.empty() ? i : canon[i];
+        }
     };
     void material(const Flow* f, std::string& out, Holes& holes, FileRefs& files) const;
     void fileset_material(const Fileset& v, std::string& out, Holes& holes, FileRefs& files) const;
     void lower_nodes(const std::vector<const Flow*>* nodes, const Block* blk, const std::vector<uint32_t>& phys);
     void add_block(const Flow* base, size_t n);
+    void collapse(const std::vector<uint32_t>& first);
     const uint32_t* slot_of(const Flow* f) const;
     const uint32_t* phys_slot_of(const Flow* f) const;
     uint32_t new_slot() { return n_slots_++; }
@@ -442,6 +452,7 @@ class Eval {
     std::string U_;
     bool file_slots_;
     uint32_t n_slots_ = 0;
+    size_t collapsed_ = 0;
     // the jobs, as the rf_graph_desc arrays
     // (grown without zero-filling: the parallel append writes every element)
     detail::RawVec<uint32_t> out_slot_, tmpl_len_, hole_pos_, hole_slot_;

@@ -408,7 +408,7 @@ const uint32_t* Eval::slot_of(const Flow* f) const {
         if (f >= b.base && f < b.base + b.n) {
             // (a static per thread: the slot is returned by pointer like the map's)
             thread_local uint32_t s;
-            s = b.slot0 + (uint32_t)(f - b.base);
+            s = b.slot0 + (uint32_t)b.at(f);
             return &s;
         }
     return logical_.find(f);
@@ -417,7 +417,7 @@ const uint32_t* Eval::slot_of(const Flow* f) const {
 const uint32_t* Eval::phys_slot_of(const Flow* f) const {
     for (const Block& b : blocks_)
         if (f >= b.base && f < b.base + b.n) {
-            const uint32_t* s = &b.phys[f - b.base];
+            const uint32_t* s = &b.phys[b.at(f)];
             return *s == ~0u ? nullptr : s;
         }
     return physical_.find(f);
@@ -935,7 +935,85 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
             if (cp[i].MapFlow) cp[i].MapFlow = cp + first[cp[i].MapFlow - cp];
         }
     });
+    pc.lap("canonicalize: deps re-pointed");
+    if (lowered) {
+        // the copies' lowered jobs, collapsed the same way: handed over
+        ev->collapse(first);
+        *lowered = std::move(ev);
+    }
     return cp + first[n - 1];
+}
+
+// Canonicalize's collapse (flowMap.Put: the first copy with a digest wins,
+// flow.go:826-839) applied to the copies' lowered jobs (block 0, copy i in
+// slot slot0 + i): a duplicate's logical and physical jobs are dropped,
+// every hole naming a duplicate's slot names its class's first copy (equal
+// digests, so no digest changes), and a duplicate's lookups alias its first
+// copy.  The compacted table (templates left in place in the blob) is loaded
+// and recomputed; nothing is lowered again.
+void Eval::collapse(const std::vector<uint32_t>& first) {
+    PhaseClock pc;
+    Block& b = blocks_.front();
+    const uint32_t s0 = b.slot0, nb = (uint32_t)b.n;
+    if (first.size() != b.n) throw Error(RF_EINVAL, "collapse: class table size");
+    std::vector<uint8_t> drop(n_slots_, 0);
+    size_t dups = 0;
+    for (uint32_t i = 0; i < nb; ++i)
+        if (first[i] != i) {
+            if (first[i] > i) throw Error(RF_EINVAL, "collapse: a class's first copy follows a member");
+            ++dups;
+            drop[s0 + i] = 1;
+            if (b.phys[i] != ~0u) drop[b.phys[i]] = 1;
+        }
+    const size_t J = out_slot_.size();
+    constexpr size_t kGrain = 1 << 16;
+    const size_t nr = (J + kGrain - 1) / kGrain;
+    std::vector<uint64_t> kj(nr + 1, 0), kh(nr + 1, 0);  // kept jobs / holes before each range
+    const unsigned th = lower_threads(e_);
+    parallel_ranges(J, kGrain, th, [&](size_t r, size_t lo, size_t hi) {
+        uint64_t j = 0, h = 0;
+        for (size_t k = lo; k < hi; ++k)
+            if (!drop[out_slot_[k]]) {
+                ++j;
+                h += hole_ptr_[k + 1] - hole_ptr_[k];
+            }
+        kj[r + 1] = j;
+        kh[r + 1] = h;
+    });
+    for (size_t r = 0; r < nr; ++r) {
+        kj[r + 1] += kj[r];
+        kh[r + 1] += kh[r];
+    }
+    detail::RawVec<uint32_t> out(kj[nr]), tlen(kj[nr]), hpos(kh[nr]), hslot(kh[nr]);
+    detail::RawVec<uint64_t> toff(kj[nr]), hptr(kj[nr] + 1);
+    hptr[0] = 0;
+    parallel_ranges(J, kGrain, th, [&](size_t r, size_t lo, size_t hi) {
+        uint64_t j = kj[r], h = kh[r];
+        for (size_t k = lo; k < hi; ++k) {
+            if (drop[out_slot_[k]]) continue;
+            out[j] = out_slot_[k];
+            tlen[j] = tmpl_len_[k];
+            toff[j] = tmpl_off_[k];
+            for (uint64_t x = hole_ptr_[k]; x < hole_ptr_[k + 1]; ++x, ++h) {
+                uint32_t s = hole_slot_[x];
+                if (s - s0 < nb) s = s0 + first[s - s0];
+                hpos[h] = hole_pos_[x];
+                hslot[h] = s;
+            }
+            hptr[++j] = h;
+        }
+    });
+    out_slot_.swap(out);
+    tmpl_len_.swap(tlen);
+    tmpl_off_.swap(toff);
+    hole_ptr_.swap(hptr);
+    hole_pos_.swap(hpos);
+    hole_slot_.swap(hslot);
+    b.canon = first;
+    collapsed_ = dups;
+    pc.lap("canonicalize: collapse (threads)");
+    Build();
+    pc.lap("canonicalize: collapsed load + full recompute");
 }
 
 // ---- Liveset ---------------------------------------------------------------------

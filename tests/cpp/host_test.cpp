@@ -2,6 +2,7 @@
 // mirror (include/reflow_hip_host.hpp) running on the device.
 //   TestDigestStability   flow_test.go:24-44
 //   TestCanonicalize      flow_test.go:46-58
+//   TestCanonicalizeHandOver  collapsed copies: the handed-over Eval == a fresh lowering
 //   TestValueDigest       executor_test.go:62-86
 //   TestDigestExec        syntax/digest_test.go:13-29 (the evaluated flow chain)
 //   TestCacheKeys         flow.go:764-802 (physical key first)
@@ -68,6 +69,60 @@ static void TestCanonicalize(Engine& e) {
     evc.Build();
     EXPECT(evc.FlowDigest(canon) == ev.FlowDigest(merged), "canonical digest changed");
     EXPECT(canon->Deps[0] == canon->Deps[1], "flow is not canonical");
+}
+
+static Fileset one(const Digest& id);
+
+// Canonicalize's hand-over when copies collapse: per-branch duplicated
+// reference chains (the same Intern -> Exec -> Coerce in every branch) collapse
+// to the first branch's; the handed-over Eval drops the duplicates' jobs and
+// must equal a fresh lowering of the canonical graph -- digests, cache keys,
+// job count, and a SetFileID + Recompute step (count and digests).
+static Flow* dup_chains(FlowArena& a, Digester& D, const Digest& ref_id, int branches) {
+    std::vector<Flow*> outs;
+    for (int b = 0; b < branches; ++b) {
+        Flow* r0 = flow::Val(a, one(ref_id));
+        Flow* r1 = flow::Exec(a, "bwa", "index %s %s", {r0});
+        r1->Argmap = std::vector<ExecArg>{{false, 0}, {true, 0}};
+        r1->Done = true;  // (so the mem exec has a physical key, and r1 one of its own)
+        r1->Value = one(D.FromString("index"));
+        Flow* rd = flow::Val(a, one(D.FromString("reads" + std::to_string(b))));
+        Flow* m = flow::Exec(a, "bwa", "mem %s %s %s", {r1, rd});
+        m->Argmap = std::vector<ExecArg>{{false, 0}, {false, 1}, {true, 0}};
+        outs.push_back(flow::Extern(a, "s3://out/" + std::to_string(b), m));
+    }
+    return flow::Merge(a, outs);
+}
+
+static void TestCanonicalizeHandOver(Engine& e) {
+    Digester D(e);
+    const Digest ref = D.FromString("reference"), ref2 = D.FromString("reference v2");
+    FlowArena a;
+    std::unique_ptr<Eval> ev;
+    Flow* canon = Canonicalize(e, a, dup_chains(a, D, ref, 5), Config{}, "", &ev);
+    EXPECT(ev != nullptr, "no Eval handed over");
+    if (!ev) return;
+    EXPECT(ev->Collapsed() == 8, "collapsed %zu copies, want 8 (4 branches x Val, Exec)", ev->Collapsed());
+    Eval fresh(e, "", true);
+    fresh.Add(canon);
+    fresh.Build();
+    EXPECT(ev->Jobs() == fresh.Jobs(), "handed-over jobs %zu, fresh lowering %zu", ev->Jobs(), fresh.Jobs());
+    const Flow* mem = canon->Deps[3]->Deps[0];
+    EXPECT(ev->FlowDigest(canon) == fresh.FlowDigest(canon), "root digest");
+    EXPECT(ev->CacheKeys(mem).size() == 2 && ev->CacheKeys(mem) == fresh.CacheKeys(mem), "cache keys");
+    ev->SetFileID(ref, ref2);
+    fresh.SetFileID(ref, ref2);
+    const uint64_t n1 = ev->Recompute(), n2 = fresh.Recompute();
+    EXPECT(n1 == n2, "incremental counts %llu vs %llu", (unsigned long long)n1, (unsigned long long)n2);
+    EXPECT(ev->FlowDigest(canon) == fresh.FlowDigest(canon) && ev->CacheKeys(mem) == fresh.CacheKeys(mem),
+           "incremental digests");
+    // and against a graph built with the new reference ID from the start
+    FlowArena a2;
+    Flow* c2 = Canonicalize(e, a2, dup_chains(a2, D, ref2, 5), Config{});
+    Eval ev2(e, "", true);
+    ev2.Add(c2);
+    ev2.Build();
+    EXPECT(ev->FlowDigest(canon) == ev2.FlowDigest(c2), "incremental != built with the new ID");
 }
 
 static void TestValueDigest(Engine& e) {
@@ -289,6 +344,7 @@ int main() {
         Engine e(0);
         TestDigestStability(e);
         TestCanonicalize(e);
+        TestCanonicalizeHandOver(e);
         TestValueDigest(e);
         TestValueJSON(e);
         TestDigestExec(e);

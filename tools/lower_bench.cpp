@@ -15,7 +15,12 @@
 //                 inputs, one full recompute (0 likewise)
 //   incremental   1% of the File IDs replaced (Eval::SetFileID) + Recompute,
 //                 checked slot for slot against a full recompute
-// Output: one JSON object on stdout.  usage: lower_bench <samples> <pairs>
+// With "dup" (a third argument) every sample builds its own copy of the
+// reference-index chain (Intern -> Exec(bwa index) -> Coerce): equal digests,
+// so Canonicalize collapses 3 x (samples - 1) copies and hands over its Eval
+// with the duplicates' jobs dropped ("collapsed"); the canonical root digest
+// equals the shared-chain graph's.
+// Output: one JSON object on stdout.  usage: lower_bench <samples> <pairs> [dup]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -63,6 +68,7 @@ static Fileset one(const Digest& id) {
 
 int main(int argc, char** argv) {
     const uint64_t S = argc > 1 ? strtoull(argv[1], nullptr, 10) : 22075, P = argc > 2 ? strtoull(argv[2], nullptr, 10) : 32;
+    const bool dup = argc > 3 && std::string(argv[3]) == "dup";
     Engine e(0);
     FlowArena a;
     auto t0 = Clock::now();
@@ -86,16 +92,20 @@ int main(int argc, char** argv) {
         x->Value = one(out);
         return x;
     };
-    Flow* r0 = flow::Intern(a, "s3://1000genomes/technical/reference/human_g1k_v37.fasta.gz");
-    r0->Done = true;
-    r0->Value = one(id_of(1, 0));
-    Flow* r1 = exec("biocontainers/bwa", "\n\tgunzip -c %s > %s/g1k_v37.fa\n\tbwa index -a bwtsw g1k_v37.fa\n", {r0},
-                    id_of(2, 0));
-    Flow* r2 = op1(OpCoerce, r1, fd_out, r1->Value);
+    auto ref_chain = [&]() {
+        Flow* r0 = flow::Intern(a, "s3://1000genomes/technical/reference/human_g1k_v37.fasta.gz");
+        r0->Done = true;
+        r0->Value = one(id_of(1, 0));
+        Flow* r1 = exec("biocontainers/bwa", "\n\tgunzip -c %s > %s/g1k_v37.fa\n\tbwa index -a bwtsw g1k_v37.fa\n",
+                        {r0}, id_of(2, 0));
+        return op1(OpCoerce, r1, fd_out, r1->Value);
+    };
+    Flow* r2 = ref_chain();
     std::vector<Flow*> roots;
     std::vector<Digest> files;
     char buf[256];
     for (uint64_t s = 0; s < S; ++s) {
+        if (dup && s) r2 = ref_chain();
         std::vector<Flow*> bams;
         for (uint64_t p = 0; p < P; ++p) {
             const uint64_t q = s * P + p;
@@ -134,14 +144,14 @@ int main(int argc, char** argv) {
         roots.push_back(flow::Extern(a, buf, op1(OpCoerce, es, fd_out, es->Value)));
     }
     Flow* top = flow::Merge(a, roots);
-    const uint64_t n_nodes = 4 + S * (P * 14 + 6);
+    const uint64_t n_nodes = 4 + S * (P * 14 + 6) + (dup && S ? 3 * (S - 1) : 0);
     const double t_build = secs(t0);
     t0 = Clock::now();
     std::unique_ptr<Eval> lowered;
     Flow* c = Canonicalize(e, a, top, Config{false}, "", &lowered);
     const double t_canon = secs(t0);
-    // Canonicalize hands over its Eval when nothing was collapsed (it IS the
-    // canonical graph's, loaded and recomputed); else the caller lowers again
+    // Canonicalize hands over its Eval (the canonical graph's, loaded and
+    // recomputed; collapsed copies' jobs dropped)
     const bool handed_over = lowered != nullptr;
     double t_lower = 0, t_load = 0;
     if (!lowered) {
@@ -174,10 +184,11 @@ int main(int argc, char** argv) {
     printf("{\"samples\": %llu, \"pairs\": %llu, \"nodes\": %llu, \"jobs\": %zu, \"build_s\": %.3f, "
            "\"canonicalize_s\": %.3f, \"lower_s\": %.3f, \"load_s\": %.3f, \"set_file_ids_s\": %.3f, "
            "\"files_changed\": %llu, \"incremental_s\": %.4f, \"jobs_rehashed\": %llu, "
-           "\"incremental_equals_full\": %s, \"canonicalize_handed_over\": %s, \"lower_threads\": %d, "
-           "\"root\": \"%s\"}\n",
+           "\"incremental_equals_full\": %s, \"canonicalize_handed_over\": %s, \"collapsed\": %zu, "
+           "\"dup_ref_chains\": %s, \"lower_threads\": %d, \"root\": \"%s\"}\n",
            (unsigned long long)S, (unsigned long long)P, (unsigned long long)n_nodes, ev.Jobs(), t_build, t_canon,
            t_lower, t_load, t_set, (unsigned long long)nch, t_inc, (unsigned long long)hashed, same ? "true" : "false",
-           handed_over ? "true" : "false", lower_threads_in_use(e), inc_root.String().c_str());
+           handed_over ? "true" : "false", ev.Collapsed(), dup ? "true" : "false", lower_threads_in_use(e),
+           inc_root.String().c_str());
     return same ? 0 : 1;
 }

@@ -591,3 +591,33 @@ extern "C" float micro_barrier(uint32_t grid, uint32_t block, uint32_t iters, in
     hipFree(d);
     return ms;
 }
+
+// ---------------------------------------------------------------------------
+// Same-address atomic contention (the level lists' append cursors): `waves`
+// 64-lane workgroups, each spins `work` dependent VALU iterations (so the
+// waves arrive together, as the mark kernel's do after their chains), then
+// lane 0 issues one atomicAdd to counter (wave % n_addr), counters 256 B
+// apart; n_addr = 0: no atomic (the baseline).
+__global__ __launch_bounds__(64) void k_atomic(uint32_t work, uint32_t n_addr, uint32_t* ctr, uint32_t* sink) {
+    uint32_t x = threadIdx.x + blockIdx.x;
+    for (uint32_t i = 0; i < work; ++i) x = x * 1664525u + 1013904223u;
+    if (n_addr && threadIdx.x == 0) x += atomicAdd(&ctr[64u * (blockIdx.x % n_addr)], 1u);
+    if (x == 0x12345678u) sink[0] = x;
+}
+
+struct AArgs { uint32_t waves, work, n_addr; uint32_t *ctr, *sink; };
+static void run_atomic(void* p) {
+    auto* a = (AArgs*)p;
+    hipLaunchKernelGGL(k_atomic, dim3(a->waves), dim3(64), 0, 0, a->work, a->n_addr, a->ctr, a->sink);
+}
+
+extern "C" float micro_atomic(uint32_t waves, uint32_t work, uint32_t n_addr) {
+    uint32_t *ctr, *sink;
+    if (hipMalloc(&ctr, 256 * 4096) != hipSuccess || hipMalloc(&sink, 64) != hipSuccess) return -2.f;
+    hipMemset(ctr, 0, 256 * 4096);
+    AArgs a{waves, work, n_addr > 4096 ? 4096u : n_addr, ctr, sink};
+    float ms = time_launch(run_atomic, &a);
+    hipFree(ctr);
+    hipFree(sink);
+    return ms;
+}

@@ -19,6 +19,20 @@ def main():
         if len(sys.argv) > 1 and sys.argv[1] == "build":
             return
     L = ctypes.CDLL(SO)
+    if len(sys.argv) > 1 and sys.argv[1] == "atomic":
+        # same-address atomics from waves that arrive together (the level
+        # lists' append cursors): launch time vs the number of counters
+        L.micro_atomic.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.micro_atomic.restype = ctypes.c_float
+        for waves in (256, 2200, 8800):
+            for work in (0, 20000):
+                base = L.micro_atomic(waves, work, 0)
+                row = ["waves %5d work %5d: none %.1f us" % (waves, work, base * 1e3)]
+                for n_addr in (1, 8, 64, 512):
+                    ms = L.micro_atomic(waves, work, n_addr)
+                    row.append("%d addr %+.1f us" % (n_addr, (ms - base) * 1e3))
+                print(", ".join(row))
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "barrier":
         L.micro_barrier.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
         L.micro_barrier.restype = ctypes.c_float
