@@ -517,9 +517,16 @@ def _lower_run(args, dup):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     res["wall_s"] = round(wall, 2)
     # RF_LOWER_TIMING=1: the lowering's phases (reflow_host.cpp PhaseClock)
-    phases = [ln[len("[lower] "):].rsplit(" ", 2) for ln in (r.stderr or "").splitlines() if ln.startswith("[lower] ")]
+    phases = [ln[1:].replace("] ", ": ", 1).rsplit(" ", 2) for ln in (r.stderr or "").splitlines()
+              if ln.startswith("[lower] ") or ln.startswith("[load] ")]
     if phases:
-        res["phases_s"] = {ph[0]: float(ph[1]) for ph in phases if len(ph) == 3}
+        res["phases_s"] = {}
+        for ph in phases:  # (a phase seen again -- the second load of a collapse -- gets its ordinal)
+            if len(ph) == 3:
+                k, n = ph[0], 2
+                while k in res["phases_s"]:
+                    k, n = "%s (%d)" % (ph[0], n), n + 1
+                res["phases_s"][k] = float(ph[1])
         log("lowering phases: " + ", ".join("%s %.2f" % kv for kv in res["phases_s"].items()))
     log("lowering%s: %d nodes: build %.1f s, canonicalize %.1f s (%d collapsed), lower %.1f s, load %.1f s, "
         "incremental %.1f ms" % (" (per-sample reference chains)" if dup else "", res["nodes"], res["build_s"],

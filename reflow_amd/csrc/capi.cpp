@@ -2207,8 +2207,11 @@ int graph_read_counts(rf_graph* gr, hipStream_t s, std::vector<uint32_t>& counts
     std::vector<uint32_t> raw(half ? counts_half_words(L) : L + 1, 0);
     if (L) HIPC(hipMemcpyAsync(raw.data(), gr->last_counts, 4ull * raw.size(), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    if (L && half)
+    if (L && half) {
         for (uint32_t k = 0; k < kFusedParts; ++k) raw[L] += raw[L + 1 + kPartStride * k];
+        for (uint32_t l = 0; l < L; ++l)  // the levels' list runs (engine.h kListShards)
+            for (uint32_t k = 0; k < kListShards; ++k) raw[l] += raw[list_shard_off(L) + k * flow_lp(L) + l];
+    }
     if (L && half && gr->g.last_flow) {  // a flow step's jobs queued by flow lanes (never listed)
         const uint32_t* er = &raw[counts_flow_base(L) + flow_ctl_off(L) + kFlowErr];
         if (er[0]) {

@@ -106,8 +106,27 @@ constexpr uint32_t kFlowMaxLevels = 1024;  // range levels one flow launch takes
 constexpr uint32_t kFlowErr = 96;  // nonzero: the launch gave up (k2_flow kFlowTimeout); then where it stood
 __host__ __device__ constexpr uint32_t counts_flow_base(uint32_t L) { return L + 1 + kCountsExtra; }
 __host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFlowShards * flow_lp(L) + L; }
-__host__ __device__ constexpr uint32_t counts_half_words(uint32_t L) {
+// The level lists' append cursors, kListShards per level: level l's list
+// region [lvl_start[l], lvl_start[l+1]) is cut by job id into kListShards
+// runs of 2^sh jobs (list_shard_shift), and a job joins the run its own id
+// falls in -- so a run never overflows (a job is listed at most once a step)
+// and the waves appending to one level spread their atomics over the runs'
+// cursors instead of taking one cursor in turn at the memory side (~19 ns
+// each: the 100M step's lean mark kernel, 2,200 waves appending to the Exec
+// level).  Shard k of level l at list_shard_off(L) + k * Lp + l (a level's
+// cursors on lines of their own).  Flow-range levels keep the single cursor
+// counts[l] (k2_flow reads its levels' lists as one run each).
+constexpr uint32_t kListShards = 16;
+__host__ __device__ constexpr uint32_t list_shard_off(uint32_t L) {
     return counts_flow_base(L) + flow_ctl_off(L) + kFlowCtl;
+}
+__host__ __device__ constexpr uint32_t counts_half_words(uint32_t L) {
+    return list_shard_off(L) + kListShards * flow_lp(L);
+}
+// log2 of a level's run length: the least sh with ceil(C / 2^sh) <= kListShards
+__host__ __device__ inline uint32_t list_shard_shift(uint32_t C) {
+    const uint32_t q = (C + kListShards - 1) / kListShards;
+    return q <= 1 ? 0u : 32u - (uint32_t)__builtin_clz(q - 1);
 }
 struct GraphDev {
     uint32_t n_jobs = 0, n_slots = 0, n_levels = 0;

@@ -102,14 +102,46 @@ __device__ __forceinline__ bool flow_level(const LevelArgs& a, uint32_t l) {
     return a.flo != ~0u && ((l >= a.flo && l <= a.fhi) || (l == a.fsink && l != ~0u));
 }
 
+// A level's append cursors (engine.h kListShards): run k of level l holds
+// the listed jobs whose ids fall in [lvl_start[l] + k * 2^sh, ... + 2^sh),
+// its cursor at list_shard_off(L) + k * Lp + l.
+__device__ __forceinline__ const uint32_t* shard_cursors(const LevelArgs& a, uint32_t l) {
+    return a.counts + list_shard_off(a.n_levels) + l;
+}
+// Jobs listed at level l this step (a level-launch level: never flow-range).
+__device__ __forceinline__ uint32_t level_count(const LevelArgs& a, uint32_t l) {
+    const uint32_t* c = shard_cursors(a, l);
+    const uint32_t lp = flow_lp(a.n_levels);
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kListShards; ++k) n += c[k * lp];
+    return n;
+}
+// The list position of level l's i-th listed job: runs in order, each run's
+// entries from its start (branch-free over the runs).
+__device__ __forceinline__ uint32_t level_pos(const LevelArgs& a, uint32_t l, uint32_t i) {
+    const uint32_t* c = shard_cursors(a, l);
+    const uint32_t lp = flow_lp(a.n_levels), b = a.lvl_start[l];
+    const uint32_t sh = list_shard_shift(a.lvl_start[l + 1] - b);
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kListShards; ++q) {
+        const uint32_t cq = c[q * lp];
+        const bool past = k == q && i >= cq;
+        i -= past ? cq : 0u;
+        k += past ? 1u : 0u;
+    }
+    return b + (k << sh) + i;
+}
+
 // Entries of a level launch: the level's own list (from its end when rev),
 // then the attached sink list.  Offsets into a.list / a.lmeta.
 struct LaunchList {
     uint32_t n1, n;
     __device__ __forceinline__ explicit LaunchList(const LevelArgs& a)
-        : n1(a.counts[a.lvl]), n(n1 + (a.lvl2 != ~0u ? a.counts[a.lvl2] : 0u)) {}
+        : n1(level_count(a, a.lvl)), n(n1 + (a.lvl2 != ~0u ? level_count(a, a.lvl2) : 0u)) {}
     __device__ __forceinline__ uint32_t at(const LevelArgs& a, uint32_t i) const {
-        return i < n1 ? a.s + (a.rev ? n1 - 1 - i : i) : a.s2 + (i - n1);
+        return i < n1 ? level_pos(a, a.lvl, a.rev ? n1 - 1 - i : i) : level_pos(a, a.lvl2, i - n1);
     }
 };
 
@@ -170,29 +202,55 @@ __device__ __forceinline__ void init_state(const LevelArgs& a, uint32_t p, ShaSt
 // Append the lanes' jobs j (need) at level lv to their levels' lists, each
 // with its 32-B record (q0, q1) beside it in lmeta, so a level kernel's first
 // job starts one HBM round trip earlier (list -> record -> template was three
-// dependent loads); one atomicAdd per distinct level in the wave.  Called by
+// dependent loads).  A job joins its level's run (engine.h kListShards, by
+// its id; a flow-range level has one run, counts[lv]): one atomicAdd per
+// distinct run in the wave, all issued before any result is used.  Called by
 // every lane of the wave.
 __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint32_t j, uint32_t lv, const uint4& q0,
                                             const uint4& q1) {
     const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint64_t mask = __ballot(need);
+    // the lane's run: its key k (kListShards: the flow range's single run) and first position rb
+    uint32_t k = 0, rb = 0;
+    if (need) {
+        const uint32_t b = a.lvl_start[lv];
+        if (flow_level(a, lv)) {
+            k = kListShards;
+            rb = b;
+        } else {
+            const uint32_t sh = list_shard_shift(a.lvl_start[lv + 1] - b);
+            k = (j - b) >> sh;
+            rb = b + (k << sh);
+        }
+    }
+    uint32_t old = 0, ml = 0;
+    uint64_t ms = 0;
+    bool left = need;
+    uint64_t mask = __ballot(left);
     while (mask) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
         const uint32_t lvl = __builtin_amdgcn_readfirstlane(__shfl(lv, leader, 64));
-        const bool mine = need && lv == lvl;
+        const uint32_t kk = __builtin_amdgcn_readfirstlane(__shfl(k, leader, 64));
+        const bool mine = left && lv == lvl && k == kk;
         const uint64_t same = __ballot(mine);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&a.counts[lvl], (uint32_t)__popcll(same));
-        base = a.lvl_start[lvl] + __shfl(base, leader, 64);
-        if (mine) {
-            const uint32_t at = base + (uint32_t)__popcll(same & lt);
-            a.list[at] = j;
-            a.lmeta[2ull * at] = q0;
-            a.lmeta[2ull * at + 1] = q1;
-            need = false;
+        if (lane == leader) {
+            uint32_t* cur = kk == kListShards ? &a.counts[lvl]
+                                              : &a.counts[list_shard_off(a.n_levels) + kk * flow_lp(a.n_levels) + lvl];
+            old = atomicAdd(cur, (uint32_t)__popcll(same));
         }
-        mask = __ballot(need);
+        if (mine) {
+            ml = leader;
+            ms = same;
+            left = false;
+        }
+        mask = __ballot(left);
+    }
+    const uint32_t base = (uint32_t)__shfl((int)old, (int)ml, 64);
+    if (need) {
+        const uint32_t at = rb + base + (uint32_t)__popcll(ms & lt);
+        a.list[at] = j;
+        a.lmeta[2ull * at] = q0;
+        a.lmeta[2ull * at + 1] = q1;
     }
 }
 
@@ -681,13 +739,12 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
 __global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
-    const uint32_t n = a.full ? (a.e - a.s) : a.counts[a.lvl];
-    const uint32_t* lst = a.list + a.s;
+    const uint32_t n = a.full ? (a.e - a.s) : level_count(a, a.lvl);
     for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
         const uint32_t i = base + threadIdx.x;
         uint32_t cb = 0, ce = 0;
         if (i < n) {
-            const uint32_t p = a.full ? a.s + i : lst[i];
+            const uint32_t p = a.full ? a.s + i : a.list[level_pos(a, a.lvl, i)];
             const bool changed = hash_job(a, p, ring, cb, ce);
             if (!a.full) {
                 a.dirty[p] = 0u;
@@ -753,12 +810,11 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t* ring = &ring_all[lane * kRing];
     zero_other_counts(a);
-    const uint32_t n = a.counts[a.lvl];
-    const uint32_t* lst = a.list + a.s;
+    const uint32_t n = level_count(a, a.lvl);
     for (uint32_t base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
         const uint32_t i = base + lane;
         bool has = i < n;
-        uint32_t p = has ? lst[i] : 0u;
+        uint32_t p = has ? a.list[level_pos(a, a.lvl, i)] : 0u;
         uint32_t fslot = ~0u;  // the previous job's out slot (fused hand-over)
         uint32_t sk = 0;
         // the fusion target's meta, first template blocks, hole record (producer)
@@ -2798,7 +2854,7 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
     zero_other_counts(a);
     WgStamp ws;
     ws.begin(a);
-    const uint32_t n = a.counts[a.lvl];
+    const uint32_t n = level_count(a, a.lvl);
     const uint4* T4 = reinterpret_cast<const uint4*>(a.tmpl);
     for (uint32_t base = blockIdx.x * 8; base < n; base += a.oct_wg * 8) {
         if (threadIdx.x == 0) ws.jobs += min(8u, n - base);
@@ -2807,7 +2863,7 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
         uint32_t p = 0;
         uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
         if (has) {
-            const uint32_t ii = a.s + (a.rev ? n - 1 - i : i);
+            const uint32_t ii = level_pos(a, a.lvl, a.rev ? n - 1 - i : i);
             p = a.list[ii];
             m0 = a.lmeta[2ull * ii];
             m1 = a.lmeta[2ull * ii + 1];
@@ -3058,7 +3114,9 @@ __global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __
                             int full) {
     // counts[L] + the fused parts: jobs hashed inside fused chains (never queued)
     for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
-        last[l] = full ? ls[l + 1] - ls[l] : counts[l];
+        uint32_t c = counts[l];  // (a flow-range level's single run)
+        for (uint32_t k = 0; k < kListShards; ++k) c += counts[list_shard_off(L) + k * flow_lp(L) + l];
+        last[l] = full ? ls[l + 1] - ls[l] : c;
         counts[l] = 0;
     }
     if (threadIdx.x == 0) {

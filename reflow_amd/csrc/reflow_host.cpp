@@ -691,6 +691,7 @@ void Eval::add_block(const Flow* base, size_t n) {
 }
 
 void Eval::Build() {
+    PhaseClock pc;
     const uint32_t J = (uint32_t)out_slot_.size();
     rf_graph_desc d{J,
                     n_slots_,
@@ -705,6 +706,7 @@ void Eval::Build() {
     if (g_) rf_graph_destroy(g_);
     g_ = nullptr;
     Check(rf_graph_load(e_.ctx(), &d, &g_));
+    pc.lap("build: rf_graph_load");
     if (const size_t nf = n_files()) {
         std::vector<uint32_t> s;
         std::vector<uint8_t> ids;
@@ -716,8 +718,10 @@ void Eval::Build() {
                 ids.insert(ids.end(), id.b.begin(), id.b.end());
             });
         Check(rf_graph_set_slots(g_, s.data(), ids.data(), (uint32_t)s.size()));
+        pc.lap("build: file IDs set");
     }
     Recompute(true);
+    pc.lap("build: full recompute");
 }
 
 uint64_t Eval::Recompute(bool full) {
