@@ -372,6 +372,18 @@ int rf_graph_set_forms(rf_graph *g, uint64_t thru, uint64_t thru_wide, uint64_t 
  * Takes effect from the next step's first set_slots (a step in progress
  * keeps the choice its first set_slots made). */
 int rf_graph_set_flow(rf_graph *g, int mode);
+/* Canonicalize's hand-over when copies collapse (flow.go:814-843, the
+ * flowMap's first copy wins, :881-907): g, just loaded from the copies'
+ * job table with the duplicates' jobs dropped and every hole re-pointed at
+ * its class's first copy (same slot numbering), takes src's whole slot table
+ * -- src is the copies' graph, fully recomputed -- device to device, and is
+ * ready for incremental steps without a full recompute (the state
+ * rf_graph_restore leaves).  Both graphs of one context, equal n_slots, no
+ * change set pending on either, src recomputed: RF_EINVAL /
+ * RF_EPRECONDITION otherwise.  The caller vouches that src's digests are
+ * what g's jobs compute (they are: every kept job is src's, reading slots of
+ * equal digests). */
+int rf_graph_adopt_slots(rf_graph *g, rf_graph *src);
 /* Asynchronous form (no count readback). */
 int rf_graph_recompute_async(rf_graph *g, int full, void *stream);
 /* rf_graph_set_slots_device + rf_graph_recompute_async(g, 0, stream) in one

@@ -444,6 +444,7 @@ class Eval {
     void lower_nodes(const std::vector<const Flow*>* nodes, const Block* blk, const std::vector<uint32_t>& phys);
     void add_block(const Flow* base, size_t n);
     void collapse(const std::vector<uint32_t>& first);
+    void load();
     const uint32_t* slot_of(const Flow* f) const;
     const uint32_t* phys_slot_of(const Flow* f) const;
     uint32_t new_slot() { return n_slots_++; }

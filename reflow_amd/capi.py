@@ -32,6 +32,7 @@ EXPORTS = [
     "rf_install_destroy",
     "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
     "rf_graph_save", "rf_graph_restore", "rf_graph_set_forms", "rf_graph_set_flow",
+    "rf_graph_adopt_slots",
     "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
     "rf_bloom_destroy", "rf_bloom_probe", "rf_bloom_probe_device", "rf_bloom_add",
@@ -303,6 +304,7 @@ def lib():
             "rf_graph_get_slots": ([vp, vp, u32, vp], i32),
             "rf_graph_stats_get": ([vp, vp, ctypes.c_size_t], i32),
             "rf_graph_set_flow": ([vp, i32], i32),
+            "rf_graph_adopt_slots": ([vp, vp], i32),
             "rf_bloom_load": ([vp, u64, u64, vp, u64, u64, vp], i32),
             "rf_bloom_load_json": ([vp, ctypes.c_char_p, ctypes.c_size_t, vp], i32),
             "rf_bloom_load_binary": ([vp, vp, ctypes.c_size_t, vp], i32),
@@ -809,9 +811,15 @@ class Graph:
         return s
 
     def set_flow(self, mode):
-        """rf_graph_set_flow: 0 never, 1 auto (default), 2 every launchable
-        level in one readiness-driven flow launch whenever possible."""
+        """rf_graph_set_flow: 0 never (default), 1 the first launchable levels
+        through the fill level, 2 every launchable level in one
+        readiness-driven flow launch whenever possible."""
         _check(lib().rf_graph_set_flow(self._h, int(mode)))
+
+    def adopt_slots(self, src):
+        """rf_graph_adopt_slots: take src's whole slot table (same numbering),
+        ready for incremental steps without a full recompute."""
+        _check(lib().rf_graph_adopt_slots(self._h, src._h))
 
     # kernel-form thresholds (include/reflow_hip.h RF_K2_THRU*_DEFAULT)
     THRU_DEFAULT, THRU_WIDE_DEFAULT, THRU_MARK_DEFAULT = 24576, 65536, 98304

@@ -1909,6 +1909,24 @@ extern "C" int rf_graph_set_flow(rf_graph* gr, int mode) {
     return RF_OK;
 }
 
+extern "C" int rf_graph_adopt_slots(rf_graph* gr, rf_graph* src) {
+    ARG(gr && src && gr != src, "null argument");
+    ARG(gr->ctx == src->ctx, "graphs of different contexts");
+    rf_ctx* ctx = gr->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DevGuard dg(ctx->device);
+    if (gr->g.n_slots != src->g.n_slots)
+        return fail(RF_EINVAL, "adopt_slots: slot tables differ: %u vs %u slots", gr->g.n_slots, src->g.n_slots);
+    if (gr->marked || src->marked) return fail(RF_EPRECONDITION, "adopt_slots: a change set is pending");
+    if (!src->initialized) return fail(RF_EPRECONDITION, "adopt_slots: the source graph was never recomputed");
+    if (gr->g.n_slots) {
+        HIPC(hipMemcpyAsync(gr->g.slots, src->g.slots, 32ull * gr->g.n_slots, hipMemcpyDeviceToDevice, ctx->stream));
+        HIPC(hipStreamSynchronize(ctx->stream));
+    }
+    gr->initialized = true;
+    return RF_OK;
+}
+
 // The launch sequence (one kernel per level + a step-end kernel) only reads
 // device-side list lengths, so it is fixed for a loaded graph: capture it once
 // per mode into a hipGraph and replay (kernel boundaries ~1.5 us instead of a

@@ -692,20 +692,7 @@ void Eval::add_block(const Flow* base, size_t n) {
 
 void Eval::Build() {
     PhaseClock pc;
-    const uint32_t J = (uint32_t)out_slot_.size();
-    rf_graph_desc d{J,
-                    n_slots_,
-                    out_slot_.data(),
-                    tmpl_off_.data(),
-                    tmpl_len_.data(),
-                    hole_ptr_.data(),
-                    hole_pos_.empty() ? nullptr : hole_pos_.data(),
-                    hole_slot_.empty() ? nullptr : hole_slot_.data(),
-                    reinterpret_cast<const uint8_t*>(blob_.data()),
-                    blob_.size()};
-    if (g_) rf_graph_destroy(g_);
-    g_ = nullptr;
-    Check(rf_graph_load(e_.ctx(), &d, &g_));
+    load();
     pc.lap("build: rf_graph_load");
     if (const size_t nf = n_files()) {
         std::vector<uint32_t> s;
@@ -722,6 +709,24 @@ void Eval::Build() {
     }
     Recompute(true);
     pc.lap("build: full recompute");
+}
+
+// The job arrays onto the device (rf_graph_load), replacing any graph loaded before.
+void Eval::load() {
+    const uint32_t J = (uint32_t)out_slot_.size();
+    rf_graph_desc d{J,
+                    n_slots_,
+                    out_slot_.data(),
+                    tmpl_off_.data(),
+                    tmpl_len_.data(),
+                    hole_ptr_.data(),
+                    hole_pos_.empty() ? nullptr : hole_pos_.data(),
+                    hole_slot_.empty() ? nullptr : hole_slot_.data(),
+                    reinterpret_cast<const uint8_t*>(blob_.data()),
+                    blob_.size()};
+    if (g_) rf_graph_destroy(g_);
+    g_ = nullptr;
+    Check(rf_graph_load(e_.ctx(), &d, &g_));
 }
 
 uint64_t Eval::Recompute(bool full) {
@@ -954,7 +959,9 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
 // every hole naming a duplicate's slot names its class's first copy (equal
 // digests, so no digest changes), and a duplicate's lookups alias its first
 // copy.  The compacted table (templates left in place in the blob) is loaded
-// and recomputed; nothing is lowered again.
+// and takes the copies' graph's slot table as it stands (rf_graph_adopt_slots:
+// every kept job is one of the copies' jobs, reading slots of equal digests),
+// so nothing is lowered again and nothing is recomputed.
 void Eval::collapse(const std::vector<uint32_t>& first) {
     PhaseClock pc;
     Block& b = blocks_.front();
@@ -1016,8 +1023,17 @@ void Eval::collapse(const std::vector<uint32_t>& first) {
     b.canon = first;
     collapsed_ = dups;
     pc.lap("canonicalize: collapse (threads)");
-    Build();
-    pc.lap("canonicalize: collapsed load + full recompute");
+    rf_graph* copies = g_;
+    g_ = nullptr;
+    try {
+        load();
+        Check(rf_graph_adopt_slots(g_, copies));
+    } catch (...) {
+        rf_graph_destroy(copies);
+        throw;
+    }
+    rf_graph_destroy(copies);
+    pc.lap("canonicalize: collapsed load + slot table adopted");
 }
 
 // ---- Liveset ---------------------------------------------------------------------

@@ -306,3 +306,40 @@ def test_structurally_damaged_checkpoints_refused(ctx, tmp_path):
     bad = bytearray(raw)
     struct.pack_into("<I", bad, sec["dstart"][0] + 4 * (w + 1), int(dst[w + 1]) - 1)
     refused(bytes(bad))
+
+
+def test_adopt_slots(ctx):
+    """rf_graph_adopt_slots (Canonicalize's collapse hand-over, flow.go:814-843):
+    a fresh load of the same job table takes a recomputed graph's slot table
+    device to device and then steps incrementally exactly like it -- no full
+    recompute in between; refused across slot-table sizes, from a graph never
+    recomputed, and with a change set pending."""
+    dag = Dag1000(12, 6)
+    a = dag.arrays()
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+    src = _load(ctx, dag)
+    src.recompute(full=True)
+    g = capi.Graph.from_arrays(ctx, a)
+    g.adopt_slots(src)
+    assert (g.get_slots(every) == src.get_slots(every)).all()
+    sl, _, nv = dag.change_set(0.1, seed=3)
+    counts = []
+    for x in (src, g):
+        x.set_slots(sl, nv)
+        counts.append(x.recompute(full=False))
+    assert counts[0] == counts[1] and 0 < counts[0] < len(a["out_slot"])
+    assert (g.get_slots(every) == src.get_slots(every)).all()
+    fresh = _load(ctx, dag)
+    with pytest.raises(capi.RfError):  # pending change set (the loaded file IDs) and never recomputed
+        g.adopt_slots(fresh)
+    fresh.recompute(full=True)
+    small = Dag1000(4, 6)
+    other = _load(ctx, small)
+    other.recompute(full=True)
+    with pytest.raises(capi.RfError):  # slot tables of different sizes
+        g.adopt_slots(other)
+    g.set_slots(sl[:1], nv[:1])
+    with pytest.raises(capi.RfError):  # a change set pending on the adopter
+        g.adopt_slots(fresh)
+    for x in (src, g, fresh, other):
+        x.close()
