@@ -134,14 +134,49 @@ __device__ __forceinline__ uint32_t level_pos(const LevelArgs& a, uint32_t l, ui
     return b + (k << sh) + i;
 }
 
+// A level launch's list runs, staged in LDS once per workgroup (stage_runs,
+// then a barrier): per list -- the level's own, then the attached sink
+// level's -- the runs' prefix counts [0 .. kListShards], the level's first
+// list position and its run shift.  (Mapping from the cursors in global
+// memory at every lookup put the latency form over its register budget:
+// 256 VGPRs + an AGPR, one wave a SIMD.)
+constexpr uint32_t kRunWords = kListShards + 3;
+__device__ __forceinline__ void stage_runs(const LevelArgs& a, uint32_t* sr) {
+    if (threadIdx.x < 2) {
+        const uint32_t l = threadIdx.x ? a.lvl2 : a.lvl;
+        uint32_t* p = sr + kRunWords * threadIdx.x;
+        const uint32_t* c = shard_cursors(a, l == ~0u ? 0u : l);
+        const uint32_t lp = flow_lp(a.n_levels);
+        uint32_t acc = 0;
+        p[0] = 0;
+        for (uint32_t k = 0; k < kListShards; ++k) {
+            acc += l == ~0u ? 0u : c[k * lp];
+            p[k + 1] = acc;
+        }
+        const uint32_t b = l == ~0u ? 0u : a.lvl_start[l];
+        p[kListShards + 1] = b;
+        p[kListShards + 2] = l == ~0u ? 0u : list_shard_shift(a.lvl_start[l + 1] - b);
+    }
+}
+// The list position of a staged list's i-th entry (i < its count): the run
+// holding it by binary search over the prefix counts (empty runs skipped).
+__device__ __forceinline__ uint32_t run_pos(const uint32_t* p, uint32_t i) {
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t st = kListShards / 2; st; st >>= 1) k += p[k + st] <= i ? st : 0u;
+    return p[kListShards + 1] + (k << p[kListShards + 2]) + (i - p[k]);
+}
+
 // Entries of a level launch: the level's own list (from its end when rev),
-// then the attached sink list.  Offsets into a.list / a.lmeta.
+// then the attached sink list.  Offsets into a.list / a.lmeta; sr: the
+// workgroup's staged runs (stage_runs, after its barrier).
 struct LaunchList {
+    const uint32_t* sr;
     uint32_t n1, n;
-    __device__ __forceinline__ explicit LaunchList(const LevelArgs& a)
-        : n1(level_count(a, a.lvl)), n(n1 + (a.lvl2 != ~0u ? level_count(a, a.lvl2) : 0u)) {}
+    __device__ __forceinline__ LaunchList(const LevelArgs&, const uint32_t* staged)
+        : sr(staged), n1(staged[kListShards]), n(n1 + staged[kRunWords + kListShards]) {}
     __device__ __forceinline__ uint32_t at(const LevelArgs& a, uint32_t i) const {
-        return i < n1 ? level_pos(a, a.lvl, a.rev ? n1 - 1 - i : i) : level_pos(a, a.lvl2, i - n1);
+        return i < n1 ? run_pos(sr, a.rev ? n1 - 1 - i : i) : run_pos(sr + kRunWords, i - n1);
     }
 };
 
@@ -1164,7 +1199,9 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
     __shared__ uint32_t s_cw[2];                      // ... block id + 1 staged, per chain wave
     __shared__ uint32_t s_hq[64 * kHq];               // the producer's hole chunks (ChunkCursor)
     __shared__ unsigned long long s_stamp[2][64];
+    __shared__ uint32_t s_runs[2 * kRunWords];
     static_assert(kThreads * kRing <= (kBufs * kJ + 2) * kPcRow, "the sink lanes' rings live in kw");
+    stage_runs(a, s_runs);
     if (a.sink_wg && blockIdx.x >= a.sink_wg) {
         // the attached sink list (and with ovf the own list's overflow), one
         // job per lane, below the chains' priority: these lanes fill the
@@ -1174,7 +1211,8 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
         if (a.ovf == 2) __builtin_amdgcn_s_setprio(3);
         WgStamp ws;
         ws.begin(a);
-        const LaunchList ll(a);
+        __syncthreads();
+        const LaunchList ll(a, s_runs);
         constexpr uint32_t nt = kThreads;
         const uint32_t g2 = gridDim.x - a.sink_wg;
         const uint32_t lo = a.ovf ? min(ll.n1, a.sink_wg * kJ) : ll.n1;
@@ -1229,7 +1267,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
     zero_other_counts(a);
     WgStamp ws;
     ws.begin(a);
-    const LaunchList ll(a);
+    const LaunchList ll(a, s_runs);  // (staged before the barrier above)
     // (lane workgroups: the list's tail is theirs)
     const uint32_t n = !a.sink_wg ? ll.n : a.ovf ? min(ll.n1, a.sink_wg * kJ) : ll.n1;
     const uint32_t gstride = a.sink_wg ? a.sink_wg : gridDim.x;
@@ -2183,11 +2221,14 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
 
 __global__ __launch_bounds__(kLevelBlock, 3) void k2_level_lf(LevelArgs a) {  // (3 waves a SIMD: <= 168 VGPRs)
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
+    __shared__ uint32_t s_runs[2 * kRunWords];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
+    stage_runs(a, s_runs);
     zero_other_counts(a);
     WgStamp ws;
     ws.begin(a);
-    const LaunchList ll(a);
+    __syncthreads();
+    const LaunchList ll(a, s_runs);
     const uint32_t n = ll.n;
     uint32_t hashed = 0;
     for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
@@ -2819,11 +2860,14 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
     // a-lanes' k row (as k1_sha256_octo); the 8 jobs' staged materials
     __shared__ __attribute__((aligned(16))) uint32_t kw[129 * kPcRow];
     __shared__ __attribute__((aligned(16))) uint32_t mat[8 * kOctStage];
+    __shared__ uint32_t s_runs[2 * kRunWords];
     static_assert(128 * kRing <= 129 * kPcRow, "the sink lanes' rings live in kw");
+    stage_runs(a, s_runs);
+    __syncthreads();
+    const LaunchList ll(a, s_runs);
     if (blockIdx.x >= a.oct_wg) {  // the attached sink list, one job per lane
         WgStamp ws;
         ws.begin(a);
-        const LaunchList ll(a);
         const uint32_t g2 = gridDim.x - a.oct_wg;
         uint32_t hashed = 0;
         for (uint32_t base = ll.n1 + (blockIdx.x - a.oct_wg) * 128; base < ll.n; base += g2 * 128) {
@@ -2854,7 +2898,7 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
     zero_other_counts(a);
     WgStamp ws;
     ws.begin(a);
-    const uint32_t n = level_count(a, a.lvl);
+    const uint32_t n = ll.n1;
     const uint4* T4 = reinterpret_cast<const uint4*>(a.tmpl);
     for (uint32_t base = blockIdx.x * 8; base < n; base += a.oct_wg * 8) {
         if (threadIdx.x == 0) ws.jobs += min(8u, n - base);
@@ -2863,7 +2907,7 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
         uint32_t p = 0;
         uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
         if (has) {
-            const uint32_t ii = level_pos(a, a.lvl, a.rev ? n - 1 - i : i);
+            const uint32_t ii = ll.at(a, i);
             p = a.list[ii];
             m0 = a.lmeta[2ull * ii];
             m1 = a.lmeta[2ull * ii + 1];
