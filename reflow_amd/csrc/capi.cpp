@@ -1310,17 +1310,38 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     }
     std::vector<uint32_t> q;
     q.reserve(J);
-    for (uint32_t j = 0; j < J; ++j)
-        if (!indeg[j]) q.push_back(j);
-    for (size_t qi = 0; qi < q.size(); ++qi) {
-        const uint32_t j = q[qi], s = d->out_slot[j];
-        for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
-            const uint32_t k = cjob[c];
-            level[k] = std::max(level[k], level[j] + 1);
-            if (--indeg[k] == 0) q.push_back(k);
+    // jobs given producers first (the C++ lowering's post-order, the bench
+    // layouts): the levels in one forward pass, q = the given order
+    bool ordered = true;
+    for (uint32_t j = 0; j < J && ordered; ++j) {
+        uint32_t lv = 0;
+        for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) {
+            const int64_t p = gr->producer[d->hole_slot[h]];
+            if (p < 0) continue;
+            if ((uint64_t)p >= j) {
+                ordered = false;
+                break;
+            }
+            lv = std::max(lv, level[(uint32_t)p] + 1);
         }
+        level[j] = lv;
     }
-    if (q.size() != J) return fail(RF_EINVAL, "job graph has a cycle (%zu of %u jobs ordered)", q.size(), J);
+    if (ordered) {
+        for (uint32_t j = 0; j < J; ++j) q.push_back(j);
+    } else {  // Kahn
+        std::fill(level.begin(), level.end(), 0u);
+        for (uint32_t j = 0; j < J; ++j)
+            if (!indeg[j]) q.push_back(j);
+        for (size_t qi = 0; qi < q.size(); ++qi) {
+            const uint32_t j = q[qi], s = d->out_slot[j];
+            for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
+                const uint32_t k = cjob[c];
+                level[k] = std::max(level[k], level[j] + 1);
+                if (--indeg[k] == 0) q.push_back(k);
+            }
+        }
+        if (q.size() != J) return fail(RF_EINVAL, "job graph has a cycle (%zu of %u jobs ordered)", q.size(), J);
+    }
     uint32_t L = 0;
     for (uint32_t j = 0; j < J; ++j) L = std::max(L, level[j] + 1);
     lap("levels");

@@ -695,16 +695,20 @@ void Eval::Build() {
     load();
     pc.lap("build: rf_graph_load");
     if (const size_t nf = n_files()) {
-        std::vector<uint32_t> s;
-        std::vector<uint8_t> ids;
-        s.reserve(nf);
-        ids.reserve(32 * nf);
-        for (const auto& m : file_slot_)
-            m.for_each([&](const Digest& id, uint32_t slot) {
-                s.push_back(slot);
-                ids.insert(ids.end(), id.b.begin(), id.b.end());
+        // every File ID into its slot, the shards gathered on host threads
+        detail::RawVec<uint32_t> s(nf);
+        detail::RawVec<uint8_t> ids(32 * nf);
+        std::vector<size_t> at(kFileShards + 1, 0);
+        for (unsigned sh = 0; sh < kFileShards; ++sh) at[sh + 1] = at[sh] + file_slot_[sh].size();
+        parallel_ranges(kFileShards, 1, lower_threads(e_), [&](size_t sh, size_t, size_t) {
+            size_t k = at[sh];
+            file_slot_[sh].for_each([&](const Digest& id, uint32_t slot) {
+                s[k] = slot;
+                memcpy(&ids[32 * k], id.b.data(), 32);
+                ++k;
             });
-        Check(rf_graph_set_slots(g_, s.data(), ids.data(), (uint32_t)s.size()));
+        });
+        Check(rf_graph_set_slots(g_, s.data(), ids.data(), (uint32_t)nf));
         pc.lap("build: file IDs set");
     }
     Recompute(true);
