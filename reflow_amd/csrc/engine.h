@@ -116,7 +116,10 @@ __host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFl
 // level).  Shard k of level l at list_shard_off(L) + k * Lp + l (a level's
 // cursors on lines of their own).  Flow-range levels keep the single cursor
 // counts[l] (k2_flow reads its levels' lists as one run each).
-constexpr uint32_t kListShards = 16;
+#ifndef RF_LIST_SHARDS
+#define RF_LIST_SHARDS 16  // (a power of two; 1 = one cursor a level, the A/B build)
+#endif
+constexpr uint32_t kListShards = RF_LIST_SHARDS;
 __host__ __device__ constexpr uint32_t list_shard_off(uint32_t L) {
     return counts_flow_base(L) + flow_ctl_off(L) + kFlowCtl;
 }

@@ -141,21 +141,30 @@ __device__ __forceinline__ uint32_t level_pos(const LevelArgs& a, uint32_t l, ui
 // memory at every lookup put the latency form over its register budget:
 // 256 VGPRs + an AGPR, one wave a SIMD.)
 constexpr uint32_t kRunWords = kListShards + 3;
+static_assert(2 * kListShards <= 64, "one wave stages both lists' runs");
 __device__ __forceinline__ void stage_runs(const LevelArgs& a, uint32_t* sr) {
-    if (threadIdx.x < 2) {
-        const uint32_t l = threadIdx.x ? a.lvl2 : a.lvl;
-        uint32_t* p = sr + kRunWords * threadIdx.x;
-        const uint32_t* c = shard_cursors(a, l == ~0u ? 0u : l);
-        const uint32_t lp = flow_lp(a.n_levels);
-        uint32_t acc = 0;
-        p[0] = 0;
-        for (uint32_t k = 0; k < kListShards; ++k) {
-            acc += l == ~0u ? 0u : c[k * lp];
-            p[k + 1] = acc;
+    // wave 0, lane t < 2 kListShards: list t / kListShards, run t % kListShards --
+    // every cursor loaded at once, then a prefix scan within each list's lanes
+    if (threadIdx.x < 64) {
+        const uint32_t t = threadIdx.x, w = t / kListShards, k = t % kListShards;
+        const uint32_t l = w ? a.lvl2 : a.lvl;
+        const bool on = t < 2 * kListShards && l != ~0u;
+        uint32_t v = on ? shard_cursors(a, l)[k * flow_lp(a.n_levels)] : 0u;
+#pragma unroll
+        for (uint32_t o = 1; o < kListShards; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)v, o, 64);
+            v += k >= o ? u : 0u;
         }
-        const uint32_t b = l == ~0u ? 0u : a.lvl_start[l];
-        p[kListShards + 1] = b;
-        p[kListShards + 2] = l == ~0u ? 0u : list_shard_shift(a.lvl_start[l + 1] - b);
+        if (t < 2 * kListShards) {
+            uint32_t* p = sr + kRunWords * w;
+            p[k + 1] = v;
+            if (k == 0) {
+                const uint32_t b = on ? a.lvl_start[l] : 0u;
+                p[0] = 0;
+                p[kListShards + 1] = b;
+                p[kListShards + 2] = on ? list_shard_shift(a.lvl_start[l + 1] - b) : 0u;
+            }
+        }
     }
 }
 // The list position of a staged list's i-th entry (i < its count): the run
@@ -245,40 +254,39 @@ __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint3
                                             const uint4& q1) {
     const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    // the lane's run: its key k (kListShards: the flow range's single run) and first position rb
-    uint32_t k = 0, rb = 0;
-    if (need) {
-        const uint32_t b = a.lvl_start[lv];
-        if (flow_level(a, lv)) {
-            k = kListShards;
-            rb = b;
-        } else {
-            const uint32_t sh = list_shard_shift(a.lvl_start[lv + 1] - b);
-            k = (j - b) >> sh;
-            rb = b + (k << sh);
-        }
-    }
-    uint32_t old = 0, ml = 0;
+    // per distinct level (its start and run shift in scalar registers), per
+    // distinct run among that level's lanes: one atomic, its result kept in
+    // the leader lane; every lane's slot taken after the last one is issued
+    uint32_t old = 0, ml = 0, rb = 0;
     uint64_t ms = 0;
     bool left = need;
-    uint64_t mask = __ballot(left);
-    while (mask) {
-        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
-        const uint32_t lvl = __builtin_amdgcn_readfirstlane(__shfl(lv, leader, 64));
-        const uint32_t kk = __builtin_amdgcn_readfirstlane(__shfl(k, leader, 64));
-        const bool mine = left && lv == lvl && k == kk;
-        const uint64_t same = __ballot(mine);
-        if (lane == leader) {
-            uint32_t* cur = kk == kListShards ? &a.counts[lvl]
-                                              : &a.counts[list_shard_off(a.n_levels) + kk * flow_lp(a.n_levels) + lvl];
-            old = atomicAdd(cur, (uint32_t)__popcll(same));
+    while (__any(left)) {
+        const uint32_t ld = (uint32_t)__ffsll((unsigned long long)__ballot(left)) - 1;
+        const uint32_t lvl = __builtin_amdgcn_readfirstlane(__shfl(lv, ld, 64));
+        const bool flow = flow_level(a, lvl);
+        const uint32_t b = a.lvl_start[lvl];
+        const uint32_t sh = flow ? 31u : list_shard_shift(a.lvl_start[lvl + 1] - b);
+        const bool here = left && lv == lvl;
+        const uint32_t k = here ? (flow ? kListShards : (j - b) >> sh) : 0u;
+        bool run = here;
+        while (__any(run)) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(run)) - 1;
+            const uint32_t kk = __builtin_amdgcn_readfirstlane(__shfl(k, leader, 64));
+            const bool mine = run && k == kk;
+            const uint64_t same = __ballot(mine);
+            if (lane == leader) {
+                uint32_t* cur = kk == kListShards ? &a.counts[lvl]
+                                                  : &a.counts[list_shard_off(a.n_levels) + kk * flow_lp(a.n_levels) + lvl];
+                old = atomicAdd(cur, (uint32_t)__popcll(same));
+            }
+            if (mine) {
+                ml = leader;
+                ms = same;
+                rb = kk == kListShards ? b : b + (kk << sh);
+                run = false;
+            }
         }
-        if (mine) {
-            ml = leader;
-            ms = same;
-            left = false;
-        }
-        mask = __ballot(left);
+        left = left && !here;
     }
     const uint32_t base = (uint32_t)__shfl((int)old, (int)ml, 64);
     if (need) {

@@ -82,7 +82,11 @@ def main():
     ap.add_argument("--c2", action="store_true")
     ap.add_argument("--c4-ranks", default="")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--lib", default="", help="another build of the library (A/B of builds)")
     a = ap.parse_args()
+    if a.lib:
+        capi.LIB_PATH = os.path.abspath(a.lib)
+        print("library: %s" % capi.LIB_PATH, file=sys.stderr)
     import faulthandler
     faulthandler.dump_traceback_later(500, exit=True)
     ctx = capi.Context(0, host_threads=0)
