@@ -117,9 +117,10 @@ __host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFl
 // cursors on lines of their own).  Flow-range levels keep the single cursor
 // counts[l] (k2_flow reads its levels' lists as one run each).
 #ifndef RF_LIST_SHARDS
-#define RF_LIST_SHARDS 16  // (a power of two; 1 = one cursor a level, the A/B build)
+#define RF_LIST_SHARDS 16  // (a power of two; A/B builds: 1 = one run a level, 0 = round 4's lists)
 #endif
-constexpr uint32_t kListShards = RF_LIST_SHARDS;
+constexpr bool kLegacyLists = RF_LIST_SHARDS == 0;  // one cursor, no staged runs (A/B)
+constexpr uint32_t kListShards = RF_LIST_SHARDS ? RF_LIST_SHARDS : 1;
 __host__ __device__ constexpr uint32_t list_shard_off(uint32_t L) {
     return counts_flow_base(L) + flow_ctl_off(L) + kFlowCtl;
 }

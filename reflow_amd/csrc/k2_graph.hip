@@ -110,6 +110,7 @@ __device__ __forceinline__ const uint32_t* shard_cursors(const LevelArgs& a, uin
 }
 // Jobs listed at level l this step (a level-launch level: never flow-range).
 __device__ __forceinline__ uint32_t level_count(const LevelArgs& a, uint32_t l) {
+    if constexpr (kLegacyLists) return a.counts[l];
     const uint32_t* c = shard_cursors(a, l);
     const uint32_t lp = flow_lp(a.n_levels);
     uint32_t n = 0;
@@ -120,6 +121,7 @@ __device__ __forceinline__ uint32_t level_count(const LevelArgs& a, uint32_t l) 
 // The list position of level l's i-th listed job: runs in order, each run's
 // entries from its start (branch-free over the runs).
 __device__ __forceinline__ uint32_t level_pos(const LevelArgs& a, uint32_t l, uint32_t i) {
+    if constexpr (kLegacyLists) return a.lvl_start[l] + i;
     const uint32_t* c = shard_cursors(a, l);
     const uint32_t lp = flow_lp(a.n_levels), b = a.lvl_start[l];
     const uint32_t sh = list_shard_shift(a.lvl_start[l + 1] - b);
@@ -143,6 +145,7 @@ __device__ __forceinline__ uint32_t level_pos(const LevelArgs& a, uint32_t l, ui
 constexpr uint32_t kRunWords = kListShards + 3;
 static_assert(2 * kListShards <= 64, "one wave stages both lists' runs");
 __device__ __forceinline__ void stage_runs(const LevelArgs& a, uint32_t* sr) {
+    if constexpr (kLegacyLists) return;
     // wave 0, lane t < 2 kListShards: list t / kListShards, run t % kListShards --
     // every cursor loaded at once, then a prefix scan within each list's lanes
     if (threadIdx.x < 64) {
@@ -182,9 +185,12 @@ __device__ __forceinline__ uint32_t run_pos(const uint32_t* p, uint32_t i) {
 struct LaunchList {
     const uint32_t* sr;
     uint32_t n1, n;
-    __device__ __forceinline__ LaunchList(const LevelArgs&, const uint32_t* staged)
-        : sr(staged), n1(staged[kListShards]), n(n1 + staged[kRunWords + kListShards]) {}
+    __device__ __forceinline__ LaunchList(const LevelArgs& a, const uint32_t* staged)
+        : sr(staged),
+          n1(kLegacyLists ? a.counts[a.lvl] : staged[kListShards]),
+          n(n1 + (kLegacyLists ? (a.lvl2 != ~0u ? a.counts[a.lvl2] : 0u) : staged[kRunWords + kListShards])) {}
     __device__ __forceinline__ uint32_t at(const LevelArgs& a, uint32_t i) const {
+        if constexpr (kLegacyLists) return i < n1 ? a.s + (a.rev ? n1 - 1 - i : i) : a.s2 + (i - n1);
         return i < n1 ? run_pos(sr, a.rev ? n1 - 1 - i : i) : run_pos(sr + kRunWords, i - n1);
     }
 };
@@ -254,6 +260,27 @@ __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint3
                                             const uint4& q1) {
     const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if constexpr (kLegacyLists) {  // (A/B build: round 4's one cursor a level)
+        uint64_t mask = __ballot(need);
+        while (mask) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
+            const uint32_t lvl = __builtin_amdgcn_readfirstlane(__shfl(lv, leader, 64));
+            const bool mine = need && lv == lvl;
+            const uint64_t same = __ballot(mine);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&a.counts[lvl], (uint32_t)__popcll(same));
+            base = a.lvl_start[lvl] + __shfl(base, leader, 64);
+            if (mine) {
+                const uint32_t at = base + (uint32_t)__popcll(same & lt);
+                a.list[at] = j;
+                a.lmeta[2ull * at] = q0;
+                a.lmeta[2ull * at + 1] = q1;
+                need = false;
+            }
+            mask = __ballot(need);
+        }
+        return;
+    }
     // per distinct level (its start and run shift in scalar registers), per
     // distinct run among that level's lanes: one atomic, its result kept in
     // the leader lane; every lane's slot taken after the last one is issued

@@ -41,7 +41,10 @@ def main():
     ap.add_argument("--c2", action="store_true")
     ap.add_argument("--c4-ranks", type=int, default=0)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--lib", default="", help="another build of the library (A/B of builds)")
     args = ap.parse_args()
+    if args.lib:
+        capi.LIB_PATH = os.path.abspath(args.lib)
     ctx = capi.Context(0, host_threads=0)
     if args.c2:
         dag = Dag1000(22075, 32)
