@@ -1766,13 +1766,22 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
 }
 
 static int graph_check_inputs(rf_graph* gr, const uint32_t* slots, uint32_t n) {
-    for (uint32_t i = 0; i < n; ++i) {
-        if (slots[i] >= gr->g.n_slots) return fail(RF_EINVAL, "slot %u out of range", slots[i]);
-        if (gr->producer[slots[i]] >= 0)
-            return fail(RF_EINVAL, "slot %u is the output of job %lld", slots[i],
-                        (long long)gr->producer[slots[i]]);
-    }
-    return RF_OK;
+    // the first offending entry in index order (ranges checked on host threads
+    // for large batches: an Eval's every File ID at once)
+    std::atomic<uint64_t> bad{~0ull};
+    load_parallel(gr->ctx, n, 1u << 20, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i)
+            if (slots[i] >= gr->g.n_slots || gr->producer[slots[i]] >= 0) {
+                uint64_t b = bad.load();
+                while (i < b && !bad.compare_exchange_weak(b, i)) {
+                }
+                return;
+            }
+    });
+    const uint64_t i = bad.load();
+    if (i == ~0ull) return RF_OK;
+    if (slots[i] >= gr->g.n_slots) return fail(RF_EINVAL, "slot %u out of range", slots[i]);
+    return fail(RF_EINVAL, "slot %u is the output of job %lld", slots[i], (long long)gr->producer[slots[i]]);
 }
 
 static void graph_flow_decide(rf_graph* gr, uint64_t n);
