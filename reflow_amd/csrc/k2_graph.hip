@@ -2254,7 +2254,10 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
     return hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi);
 }
 
-__global__ __launch_bounds__(kLevelBlock, 3) void k2_level_lf(LevelArgs a) {  // (3 waves a SIMD: <= 168 VGPRs)
+#ifndef RF_LF_WAVES
+#define RF_LF_WAVES 3  // (A/B builds: waves a SIMD the throughput form is compiled for)
+#endif
+__global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArgs a) {  // (3 waves a SIMD: <= 168 VGPRs)
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     __shared__ uint32_t s_runs[2 * kRunWords];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
