@@ -51,3 +51,15 @@ def test_code_object_is_gfx950():
     so = os.path.join(ROOT, "reflow_amd", "libreflow_hip.so")
     data = open(so, "rb").read()
     assert b"gfx950" in data
+
+
+def test_graph_entry_points_refuse_null_arguments():
+    """Entry points that need no device refuse bad arguments with RF_EINVAL
+    before touching one (a binding's misuse fails loudly, never silently)."""
+    from reflow_amd import capi
+    L = capi.lib()
+    assert L.rf_graph_adopt_slots(None, None) == capi.RF_EINVAL
+    assert len(L.rf_last_error()) > 0
+    assert L.rf_graph_set_flow(None, 0) == capi.RF_EINVAL
+    assert L.rf_graph_stats_get(None, None, 0) == capi.RF_EINVAL
+    assert L.rf_graph_set_slots(None, None, None, 1) == capi.RF_EINVAL
