@@ -929,11 +929,32 @@ Flow* Canonicalize(Engine& e, FlowArena& arena, Flow* root, Config config, const
     pc.lap("canonicalize: load + full recompute");
     // 4. flowMap.Put: first copy with a digest wins (K5 on the device: the
     //    smallest post-order index of each digest class) -- the copies'
-    //    digests are slots [0, n) in post-order
-    ev->fetch();
+    //    digests are slots [0, n) in post-order, gathered from the slot table
+    //    on the device (no round trip of the table through the host)
     std::vector<uint32_t> first(n);
     uint32_t n_unique = 0;
-    if (n) Check(rf_dedup_digests(e.ctx(), ev->cache_.data(), (uint32_t)n, first.data(), &n_unique));
+    if (n) {
+        struct Dev {
+            rf_ctx* c;
+            void* p = nullptr;
+            ~Dev() {
+                if (p) rf_free(c, p);
+            }
+        } idx{e.ctx()}, dig{e.ctx()}, canon{e.ctx()}, nu{e.ctx()};
+        std::vector<uint32_t> iota(n);
+        for (size_t i = 0; i < n; ++i) iota[i] = ev->blocks_.front().slot0 + (uint32_t)i;
+        Check(rf_malloc(e.ctx(), 4ull * n, &idx.p));
+        Check(rf_malloc(e.ctx(), 32ull * n, &dig.p));
+        Check(rf_malloc(e.ctx(), 4ull * n, &canon.p));
+        Check(rf_malloc(e.ctx(), 64, &nu.p));
+        Check(rf_memcpy_h2d(e.ctx(), idx.p, iota.data(), 4ull * n));
+        void* st = rf_stream(e.ctx());
+        Check(rf_graph_gather_device(ev->g_, idx.p, (uint32_t)n, dig.p, st));
+        Check(rf_dedup_digests_device(e.ctx(), dig.p, (uint32_t)n, canon.p, nu.p, st));
+        Check(rf_memcpy_d2h(e.ctx(), first.data(), canon.p, 4ull * n));
+        Check(rf_memcpy_d2h(e.ctx(), &n_unique, nu.p, 4));
+        if (n_unique & 0x80000000u) throw Error(RF_EDEVICE, "canonicalize: dedup probe bound reached");
+    }
     pc.lap("canonicalize: dedup");
     Flow* croot = cp + (n - 1);
     if (n_unique == n) {  // nothing collapsed: the copies' graph is the canonical one
