@@ -1790,18 +1790,41 @@ extern "C" int rf_graph_set_slots(rf_graph* gr, const uint32_t* slots, const uin
                                   uint32_t n) {
     ARG(gr && (n == 0 || (slots && digests32)), "null argument");
     if (!n) return RF_OK;
+    // RF_LOWER_TIMING=1: a large batch's phases on stderr (as rf_graph_load's)
+    static const bool timing = getenv("RF_LOWER_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!timing || n < (1u << 20)) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[set_slots] %s %.3f s\n", what, std::chrono::duration<double>(now - t_last).count());
+        t_last = now;
+    };
     if (int rc = graph_check_inputs(gr, slots, n)) return rc;
+    lap("validate");
     rf_ctx* ctx = gr->ctx;
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
     HIPC(gr->b_tmp_idx.ensure(4ull * n));
     HIPC(gr->b_tmp_dig.ensure(32ull * n));
+    lap("buffers");
     HIPC(hipMemcpyAsync(gr->b_tmp_idx.p, slots, 4ull * n, hipMemcpyHostToDevice, ctx->stream));
     HIPC(hipMemcpyAsync(gr->b_tmp_dig.p, digests32, 32ull * n, hipMemcpyHostToDevice, ctx->stream));
-    graph_flow_decide(gr, n);
-    HIPC(launch_graph_mark_slots(gr->g, gr->b_tmp_idx.as<uint32_t>(), gr->b_tmp_dig.as<uint8_t>(), n,
-                                 ctx->stream));
+    if (timing && n >= (1u << 20)) HIPC(hipStreamSynchronize(ctx->stream));
+    lap("upload");
+    if (!gr->initialized) {
+        // never recomputed: the next recompute is a full one, which hashes
+        // every job from the slots as they stand -- the inputs are only
+        // written (an Eval's first File IDs: 20M slot-fused chains hashed and
+        // their consumers queued, all of it discarded by the full pass, 0.4 s)
+        HIPC(launch_scatter_digests(gr->g.slots, gr->b_tmp_idx.as<uint32_t>(), gr->b_tmp_dig.as<uint8_t>(), n,
+                                    ctx->stream));
+    } else {
+        graph_flow_decide(gr, n);
+        HIPC(launch_graph_mark_slots(gr->g, gr->b_tmp_idx.as<uint32_t>(), gr->b_tmp_dig.as<uint8_t>(), n,
+                                     ctx->stream));
+    }
     HIPC(hipStreamSynchronize(ctx->stream));
+    lap("mark");
     gr->marked += n;
     return RF_OK;
 }
@@ -1811,9 +1834,14 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
     ARG(gr && (n == 0 || (d_slots && d_digests32)), "null argument");
     std::lock_guard<std::mutex> lk(gr->ctx->mu);
     DevGuard dg(gr->ctx->device);
-    graph_flow_decide(gr, n);
-    HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
-                                 static_cast<const uint8_t*>(d_digests32), n, pick(gr->ctx, stream)));
+    if (!gr->initialized) {  // (as rf_graph_set_slots: the next recompute is a full one)
+        HIPC(launch_scatter_digests(gr->g.slots, static_cast<const uint32_t*>(d_slots),
+                                    static_cast<const uint8_t*>(d_digests32), n, pick(gr->ctx, stream)));
+    } else {
+        graph_flow_decide(gr, n);
+        HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
+                                     static_cast<const uint8_t*>(d_digests32), n, pick(gr->ctx, stream)));
+    }
     gr->marked += n;
     return RF_OK;
 }
