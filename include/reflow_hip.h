@@ -333,7 +333,9 @@ typedef struct {
 int rf_graph_load(rf_ctx *ctx, const rf_graph_desc *desc, rf_graph **out);
 void rf_graph_destroy(rf_graph *g);
 /* Set input-slot digests (e.g. changed File IDs); marks their transitive
- * dependents dirty.  Setting a job's output slot is RF_EINVAL. */
+ * dependents dirty.  Setting a job's output slot is RF_EINVAL.  On a graph
+ * never recomputed (fresh from rf_graph_load) the digests are only written:
+ * its first recompute is a full one. */
 int rf_graph_set_slots(rf_graph *g, const uint32_t *slots, const uint8_t *digests32, uint32_t n);
 /* Device-resident form of set_slots (indices and digests in HBM). */
 int rf_graph_set_slots_device(rf_graph *g, const void *d_slots, const void *d_digests32, uint32_t n,
