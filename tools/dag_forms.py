@@ -24,8 +24,9 @@ from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
 # pl: every level in the latency form; lf: every level in the throughput
 # form; auto: the library's per-level choice (the default thresholds)
-# flow: the library's choice with the flow step on (rf_graph_set_flow 1; off by default)
-FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None, "flow": None}
+# flow: the library's choice with the flow step on (rf_graph_set_flow 1; off by default);
+# flow2: every launchable level in the flow launch (rf_graph_set_flow 2)
+FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None, "flow": None, "flow2": None}
 
 
 def run(ctx, name, g, slots, old, new, steps):
@@ -40,7 +41,7 @@ def run(ctx, name, g, slots, old, new, steps):
                 g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
             else:
                 g.set_forms(thr)
-            g.set_flow(1 if form == "flow" else 0)
+            g.set_flow({"flow": 1, "flow2": 2}.get(form, 0))
             state = {"v": 0}
 
             def step():
@@ -83,6 +84,7 @@ def main():
     ap.add_argument("--c4-ranks", default="")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--lib", default="", help="another build of the library (A/B of builds)")
+    ap.add_argument("--persample", default="", help="per-sample-root layout (SURVEY C3/C4): ranks, e.g. 8,1")
     a = ap.parse_args()
     if a.lib:
         capi.LIB_PATH = os.path.abspath(a.lib)
@@ -112,6 +114,20 @@ def main():
         out.append(res)
         g.close()
         del pc, g
+    for r in [int(x) for x in a.persample.split(",") if x]:
+        # SURVEY §8(d) C3/C4 as written: per-sample roots, no Merge tree; rank
+        # 0's piece at r ranks is its first 8/r parts' samples (no exchange)
+        t0 = time.perf_counter()
+        dag = Dag1000(27594 * 8 // r, 32)
+        g = capi.Graph.from_arrays(ctx, dag.arrays())
+        g.set_slots(dag.file_slots, dag.leaf_ids)
+        g.recompute(True)
+        slots, old, new = dag.change_set(0.01, n_global=2 * 32 * 27594 * 8)
+        print("per-sample r=%d loaded in %.1f s" % (r, time.perf_counter() - t0), file=sys.stderr, flush=True)
+        out.append(run(ctx, "per-sample roots, rank 0 of %d (%d samples)" % (r, 27594 * 8 // r), g, slots, old,
+                       new, a.steps))
+        g.close()
+        del dag, g
     print(json.dumps(out), flush=True)
     ctx.close()
 
