@@ -15,13 +15,21 @@ Merge tree, the global root merging the 8 rank roots
       all-gather (RCCL needs one GPU per rank): every rank's slots equal
       (a)'s, before and after the change.
 
+  (c) the oracle ((a) and (b) alone compare the engine with
+      itself): after the change, every one of the 121.6M jobs re-derived on
+      the host from its own hole digests in the table (the oracle's job-local
+      check, orc_graph_check, 16 threads) -- and the input slots hold the
+      changed File IDs.
+
 The oracle's CPU evaluator would take minutes per full pass at this size; the
-oracle pins the same generator and protocol at small sizes
-(test_gpu_partition.py, test_gpu_dag.py, test_gpu_scale.py's configs[2])."""
+job-local check takes seconds, and the oracle pins the same generator and
+protocol end to end at small sizes (test_gpu_partition.py, test_gpu_dag.py,
+test_gpu_scale.py's configs[2])."""
 import numpy as np
 import pytest
 
 import partition_case as PC
+import reflow_oracle as O
 from reflow_amd import capi
 from reflow_amd.workloads import PartitionedDag1000
 
@@ -71,6 +79,15 @@ def test_configs3_single_rank_incremental_equals_full(c4):
         g.recompute(full=True)
         assert (g.get_slots(every) == inc).all(), "incremental != full recompute"
         c4["after"] = inc
+        # (c) the oracle, job by job over the whole table, and the inputs
+        ids = G.leaf_ids.copy()
+        order = np.argsort(G.file_slots, kind="stable")
+        pos = order[np.searchsorted(G.file_slots[order], slots)]
+        assert (G.file_slots[pos] == slots).all()
+        ids[pos] = new
+        assert (inc[G.file_slots] == ids).all(), "input slots"
+        bad, first = O.check_slots(a, inc, 16)
+        assert bad == 0, ("oracle: jobs whose digest is not the hash of their material", bad, first)
         # and back: the old IDs restore the original digests
         g.set_slots(slots, old)
         g.recompute(full=False)
