@@ -277,6 +277,50 @@ struct Config {
     void Merge(const Config& d) { HashV1 = HashV1 || d.HashV1; }
 };
 
+// A Flow's Fileset value, read like std::optional<Fileset> but SHARED by a
+// node and its copies: Go's Flow.Copy (flow.go:818-843) copies the struct,
+// and a Fileset's Map is a reference there, so the copies Canonicalize makes
+// share their originals' values instead of duplicating every map (on a
+// 10M-node graph the value copies were most of the copy phase).  Assigning a
+// Fileset gives the node a value of its own; writing through * or -> is seen
+// by every node sharing it, as in Go.
+class FlowValue {
+   public:
+    FlowValue() = default;
+    FlowValue(std::nullopt_t) {}
+    FlowValue(const Fileset& v) : p_(std::make_shared<Fileset>(v)) {}
+    FlowValue(Fileset&& v) : p_(std::make_shared<Fileset>(std::move(v))) {}
+    FlowValue(const std::optional<Fileset>& v) {
+        if (v) p_ = std::make_shared<Fileset>(*v);
+    }
+    FlowValue& operator=(std::nullopt_t) {
+        p_.reset();
+        return *this;
+    }
+    FlowValue& operator=(const Fileset& v) {
+        p_ = std::make_shared<Fileset>(v);
+        return *this;
+    }
+    FlowValue& operator=(Fileset&& v) {
+        p_ = std::make_shared<Fileset>(std::move(v));
+        return *this;
+    }
+    explicit operator bool() const { return p_ != nullptr; }
+    bool has_value() const { return p_ != nullptr; }
+    const Fileset& operator*() const { return *p_; }
+    Fileset& operator*() { return *p_; }
+    const Fileset* operator->() const { return p_.get(); }
+    Fileset* operator->() { return p_.get(); }
+    const Fileset& value() const {
+        if (!p_) throw std::bad_optional_access();
+        return *p_;
+    }
+    void reset() { p_.reset(); }
+
+   private:
+    std::shared_ptr<Fileset> p_;
+};
+
 struct Flow {
     Op op = OpVal;
     Flow* Parent = nullptr;
@@ -289,7 +333,7 @@ struct Flow {
     std::optional<std::vector<ExecArg>> Argmap;
     Digest FlowDigest;                // OpVal (non-Fileset), OpK, OpCoerce
     bool Done = false;                // State == FlowDone
-    std::optional<Fileset> Value;     // Fileset value
+    FlowValue Value;                  // Fileset value (shared with copies)
     bool Err = false;                 // error values digest randomly (not supported here)
     std::string Data;                 // OpData
 };

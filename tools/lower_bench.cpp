@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "reflow_host.hpp"
@@ -66,15 +67,61 @@ static Fileset one(const Digest& id) {
     return v;
 }
 
+// Canonicalize's post-order and copy loop (reflow_host.cpp) on host threads,
+// timed: whole copies, and copies without their Fileset values.
+static int copy_probe(Flow* top, unsigned th) {
+    auto t0 = Clock::now();
+    std::vector<Flow*> post;
+    detail::PtrIndex index;
+    detail::PostOrder(top, th, post, index);
+    const double t_walk = secs(t0);
+    const size_t n = post.size();
+    for (int variant = 0; variant < 2; ++variant) {
+        FlowArena arena;
+        t0 = Clock::now();
+        arena.NewN(n, [&](Flow* blk, size_t, size_t) {
+            std::vector<std::thread> pool;
+            for (unsigned t = 0; t < th; ++t)
+                pool.emplace_back([&, t] {
+                    for (size_t i = n * t / th; i < n * (t + 1) / th; ++i) {
+                        Flow* c = variant ? new (blk + i) Flow() : new (blk + i) Flow(*post[i]);
+                        if (variant) {  // the fields without the value
+                            const Flow& o = *post[i];
+                            c->op = o.op;
+                            c->Parent = o.Parent;
+                            c->Deps = o.Deps;
+                            c->Image = o.Image;
+                            c->Cmd = o.Cmd;
+                            c->URL = o.URL;
+                            c->Argmap = o.Argmap;
+                            c->FlowDigest = o.FlowDigest;
+                            c->Done = o.Done;
+                        }
+                        for (Flow*& d : c->Deps) d = blk + *index.find(d);
+                    }
+                });
+            for (auto& x : pool) x.join();
+        });
+        printf("{\"nodes\": %zu, \"threads\": %u, \"walk_s\": %.3f, \"copy_s\": %.3f, \"values\": %s}\n", n, th,
+               t_walk, secs(t0), variant ? "false" : "true");
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const uint64_t S = argc > 1 ? strtoull(argv[1], nullptr, 10) : 22075, P = argc > 2 ? strtoull(argv[2], nullptr, 10) : 32;
     const bool dup = argc > 3 && std::string(argv[3]) == "dup";
-    Engine e(0);
+    // "copyprobe" (a diagnostic, host only -- no device): the graph built,
+    // then Canonicalize's walk and copy loop timed on host threads, whole
+    // nodes and without their Fileset values
+    const bool copyprobe = argc > 3 && std::string(argv[3]) == "copyprobe";
+    std::unique_ptr<Engine> eng;
+    if (!copyprobe) eng = std::make_unique<Engine>(0);
     FlowArena a;
     auto t0 = Clock::now();
     const Digest fd_coerce = fd("file.fs$file"), fd_force = fd("Eval.Force"), fd_fs = fd("coerceFlowToFileset"),
                  fd_out = fd("coerceExecOutput"), fd_merge = fd("Force.merge");
-    auto op1 = [&](Op op, Flow* dep, const Digest& d, const std::optional<Fileset>& v) {
+    auto op1 = [&](Op op, Flow* dep, const Digest& d, const FlowValue& v) {
         Flow f;
         f.op = op;
         f.Deps = {dep};
@@ -144,6 +191,8 @@ int main(int argc, char** argv) {
         roots.push_back(flow::Extern(a, buf, op1(OpCoerce, es, fd_out, es->Value)));
     }
     Flow* top = flow::Merge(a, roots);
+    if (copyprobe) return copy_probe(top, (unsigned)(argc > 4 ? atoi(argv[4]) : 8));
+    Engine& e = *eng;
     const uint64_t n_nodes = 4 + S * (P * 14 + 6) + (dup && S ? 3 * (S - 1) : 0);
     const double t_build = secs(t0);
     t0 = Clock::now();
