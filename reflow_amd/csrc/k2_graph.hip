@@ -355,30 +355,6 @@ __device__ __forceinline__ void propagate(const LevelArgs& a, uint32_t c, uint32
     }
 }
 
-// One reverse edge whose consumer's record and queued flag are fetched ahead
-// (issue) and whose append waits (finish): the mark kernels fetch an input
-// slot's first consumer after its slot-fused one -- e.g. a physical key's job
-// -- in the same round trips as the slot-fused job's record, so its dirty
-// flag's atomic returns while the chain hashes instead of after it.
-struct EdgeAhead {
-    uint2 jl = make_uint2(0, 0), cr = make_uint2(0, 0);
-    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
-    bool need = false;
-    __device__ __forceinline__ void issue(const LevelArgs& a, bool has, uint2 e) {
-        if (!has) return;
-        jl = e;
-        q0 = a.meta[2ull * jl.x];
-        q1 = a.meta[2ull * jl.x + 1];
-        if (flow_level(a, jl.y)) cr = a.cout_rng[jl.x];
-        need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
-    }
-    // every lane of the wave
-    __device__ __forceinline__ void finish(const LevelArgs& a) {
-        if (need) flow_count_out(a, cr);
-        append_jobs(a, need, jl.x, jl.y, q0, q1);
-    }
-};
-
 // OR digest D (8 LE words) into the lane's ring at material byte `pos`; the
 // template holds zero bytes there, and the 00 05 prefix around it.
 __device__ __forceinline__ void or_digest(uint32_t* ring, uint32_t pos, const uint32_t (&D)[8]) {
@@ -2104,25 +2080,15 @@ __device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed)
 // with its record, first two template blocks, hole record, old digest and
 // start state in registers: they and the next job's record are fetched while
 // the job before it is hashed.  Called by every lane of the wave.
-#ifndef RF_MARK_AHEAD
-#define RF_MARK_AHEAD 1  // (A/B builds: 0 = a slot's consumers after its chain only)
-#endif
-template <bool kAhead = (RF_MARK_AHEAD != 0)>  // (k_part_apply: false -- its register budget)
 __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ring, bool changed, uint32_t s,
                                                 const uint4& nlo, const uint4& nhi, uint32_t cp0, uint32_t cp1) {
     constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     uint32_t c = changed ? cp0 : 0u, ce = changed ? cp1 : 0u, p = ~0u;
-    const uint2 f = a.cons[c < ce ? c : 0u], f2 = a.cons[c + 1 < ce ? c + 1 : 0u];
-    const bool fused = c < ce && (f.y & kSlotFused);
-    if (fused) {
+    const uint2 f = a.cons[c < ce ? c : 0u];
+    if (c < ce && (f.y & kSlotFused)) {
         p = f.x;
         ++c;
-    }
-    EdgeAhead ea;  // the slot's next consumer, fetched beside the fused job's record
-    if constexpr (kAhead) {
-        ea.issue(a, c < ce, fused ? f2 : f);
-        if (c < ce) ++c;
     }
     // the job's operands (fetched a job ahead after the first)
     uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, nm0 = m0, nm1 = m0, olo = m0, ohi = m0;
@@ -2139,8 +2105,7 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
         }
     }
     const uint32_t hashed = hash_fused_chain(a, ring, p, m0, m1, nm0, nm1, t, r, olo, ohi, hlo, hhi, s, nlo, nhi);
-    if constexpr (kAhead) ea.finish(a);
-    // the slot's further consumers
+    // the slot's other consumers
     propagate(a, c, ce);
     count_fused(a, hashed);
 }
@@ -2348,22 +2313,15 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
         if (!changed) c = ce = 0;
         uint32_t p = ~0u;
         uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-        const uint2 f = a.cons[c < ce ? c : 0u], f2 = a.cons[c + 1 < ce ? c + 1 : 0u];
-        const bool fused = c < ce && (f.y & kSlotFused);
-        if (fused) {
+        const uint2 f = a.cons[c < ce ? c : 0u];
+        if (c < ce && (f.y & kSlotFused)) {
             p = f.x;
             ++c;
             m0 = a.meta[2ull * p];
             m1 = a.meta[2ull * p + 1];
         }
-        EdgeAhead ea;  // the slot's next consumer, fetched beside the fused job's record
-        if (RF_MARK_AHEAD) {
-            ea.issue(a, c < ce, fused ? f2 : f);
-            if (c < ce) ++c;
-        }
         hashed += hash_fused_chain_lean(a, ring, p, m0, m1, s, nlo, nhi);
-        if (RF_MARK_AHEAD) ea.finish(a);
-        propagate(a, c, ce);  // the slot's further consumers
+        propagate(a, c, ce);  // the slot's other consumers
     }
     if (a.dbg_twice != 16) count_fused(a, hashed);
 }
@@ -3229,7 +3187,7 @@ __global__ __launch_bounds__(kMarkBlock) void k_part_apply(const uint32_t* __res
                 }
             }
         }
-        mark_input_slot<false>(a, ring, changed, s, nlo, nhi, cp0, cp1);
+        mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
     }
 }
 
