@@ -11,6 +11,12 @@ import sys
 os.environ.setdefault("RF_K2_STAMPS", "1")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from reflow_amd import capi  # noqa: E402
+
+# the stamps exist only in a diagnostic build (make -C reflow_amd/csrc
+# EXTRA=-DRF_DIAG BUILD=build_diag OUT=../../tools/_ab/libreflow_diag.so ...):
+# STAMP_LIB=path picks it
+if os.environ.get("STAMP_LIB"):
+    capi.LIB_PATH = os.path.abspath(os.environ["STAMP_LIB"])
 from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
 ctx = capi.Context(0, host_threads=0)
