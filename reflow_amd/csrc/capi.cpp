@@ -1247,6 +1247,18 @@ int graph_flow_upload(rf_graph* gr, const FlowHost& f) {
     return RF_OK;
 }
 
+int graph_build_plan(rf_graph* gr) {
+    GraphDev& G = gr->g;
+    if (!RF_SLOT_PLAN) return RF_OK;
+    hipError_t e = gr->b_plan.ensure(48ull * std::max<uint32_t>(G.n_slots, 1));
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph plan: %s", hipGetErrorString(e));
+    G.plan = gr->b_plan.as<uint4>();
+    HIPC(launch_slot_plan(G, gr->ctx->stream));
+    HIPC(hipStreamSynchronize(gr->ctx->stream));
+    return RF_OK;
+}
+
 extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out) {
     ARG(ctx && d && out, "null argument");
     *out = nullptr;
@@ -1729,6 +1741,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     // so its block 1 is template only
     G.split_b0 = G.hole_in_b0 && G.fuse_pos2 ? graph_split_on() : 0u;
     lap("midstates");
+    if (int rc = graph_build_plan(gr)) return rc;
     if (RF_DIAG_KNOB("RF_K2_STAMPS", 0)) {  // diagnostic build: per-phase times of workgroup 0 of each level
         HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
         HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
@@ -1751,7 +1764,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
                           &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_lmeta, &gr->b_counts, &gr->b_counts_last,
-                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst,
+                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst, &gr->b_plan,
                           &gr->b_cout_rng, &gr->b_cout, &gr->b_jlv, &gr->b_pend, &gr->b_dstart, &gr->b_rq, &gr->b_dq})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);

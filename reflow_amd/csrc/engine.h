@@ -116,6 +116,9 @@ __host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFl
 // level).  Shard k of level l at list_shard_off(L) + k * Lp + l (a level's
 // cursors on lines of their own).  Flow-range levels keep the single cursor
 // counts[l] (k2_flow reads its levels' lists as one run each).
+#ifndef RF_SLOT_PLAN
+#define RF_SLOT_PLAN 1  // the mark kernels' per-slot plan (GraphDev::plan; A/B builds: 0 = off)
+#endif
 #ifndef RF_LIST_SHARDS
 #define RF_LIST_SHARDS 16  // (a power of two; A/B builds: 1 = one run a level, 0 = round 4's lists)
 #endif
@@ -142,6 +145,13 @@ struct GraphDev {
     uint4* meta = nullptr;           // [2J]
     uint2* holes = nullptr;          // [H] {byte position, slot}
     uint32_t* cons_ptr = nullptr;    // [S+1] slot -> consumer jobs (internal ids)
+    // [3S] the mark kernels' per-slot plan, built at load / restore from the
+    // records above (launch_slot_plan): plan[3s] = {first reverse edge after
+    // the slot-fused one, reverse-edge end, slot-fused job or ~0, 0},
+    // plan[3s+1..2] = that job's record -- a changed input slot reaches its
+    // slot-fused job's template, hole and old digest in one dependent load
+    // instead of three (cons_ptr -> cons -> meta)
+    uint4* plan = nullptr;
     uint2* cons = nullptr;           // [C] {consumer job, its level}
     uint8_t* tmpl = nullptr;         // padded templates, zero at the holes (read-only)
     uint8_t* slots = nullptr;        // [S][32] digest table
@@ -244,6 +254,9 @@ struct GraphDev {
 // start[i] (64-B units) into mid[2i..2i+1] (state words); IV when lead[i] = 0.
 hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, const uint32_t* lead, uint32_t n,
                                   uint4* mid, hipStream_t s);
+// The per-slot plan (GraphDev::plan) of a graph whose meta / cons_ptr / cons
+// are on the device.
+hipError_t launch_slot_plan(const GraphDev& g, hipStream_t s);
 hipError_t launch_graph_mark_slots(GraphDev& g, const uint32_t* slots, const uint8_t* digests,
                                    uint32_t n, hipStream_t s);
 // k3_mark_slots as a graph kernel node: argument values + node parameters

@@ -35,7 +35,7 @@ struct rf_graph {
     std::vector<int64_t> producer;   // slot -> external job or -1
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
-    DevBuf b_stamps, b_mid, b_wgst;
+    DevBuf b_stamps, b_mid, b_wgst, b_plan;
     // the flow step's structures (GraphDev "flow")
     DevBuf b_cout_rng, b_cout, b_jlv, b_pend, b_dstart, b_rq, b_dq;
     DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_lmeta, b_counts,
@@ -81,4 +81,5 @@ struct FlowHost {
     std::vector<uint32_t> dstart;   // [L+1]
 };
 int graph_flow_upload(rf_graph* gr, const FlowHost& f);
+int graph_build_plan(rf_graph* gr);  // GraphDev::plan, after the records are on the device
 void graph_part_release(rf_graph* gr);

@@ -447,6 +447,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
         gr->producer[out_slot[i]] = j;
     }
     G.split_b0 = G.hole_in_b0 && G.fuse_pos2 ? graph_split_on() : 0u;  // (as rf_graph_load)
+    if (int rc = graph_build_plan(gr)) return rc;
     gr->initialized = (h.flags & kInitialized) != 0;
     guard.release();
     *out = gr;

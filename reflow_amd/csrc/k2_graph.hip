@@ -95,6 +95,7 @@ struct LevelArgs {
     unsigned long long* rq = nullptr;
     unsigned long long* dq = nullptr;
     uint32_t flo = ~0u, fhi = 0, fsink = ~0u, epoch = 0;
+    const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
 };
 
 // Whether level l runs in this step's flow launch.
@@ -2080,24 +2081,17 @@ __device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed)
 // with its record, first two template blocks, hole record, old digest and
 // start state in registers: they and the next job's record are fetched while
 // the job before it is hashed.  Called by every lane of the wave.
-__device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ring, bool changed, uint32_t s,
-                                                const uint4& nlo, const uint4& nhi, uint32_t cp0, uint32_t cp1) {
+__device__ __forceinline__ void mark_input_slot_from(const LevelArgs& a, uint32_t* ring, uint32_t s, const uint4& nlo,
+                                                     const uint4& nhi, uint32_t c, uint32_t ce, uint32_t p, uint4 m0,
+                                                     uint4 m1) {
     constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    uint32_t c = changed ? cp0 : 0u, ce = changed ? cp1 : 0u, p = ~0u;
-    const uint2 f = a.cons[c < ce ? c : 0u];
-    if (c < ce && (f.y & kSlotFused)) {
-        p = f.x;
-        ++c;
-    }
     // the job's operands (fetched a job ahead after the first)
-    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0, nm0 = m0, nm1 = m0, olo = m0, ohi = m0;
+    uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0, olo = nm0, ohi = nm0;
     uint4 hlo = make_uint4(IV[0], IV[1], IV[2], IV[3]), hhi = make_uint4(IV[4], IV[5], IV[6], IV[7]);
     uint4 t[8];
     uint2 r = make_uint2(~0u, 0u);
     if (p != ~0u) {
-        m0 = a.meta[2ull * p];
-        m1 = a.meta[2ull * p + 1];
         fetch_fused_ops(a, p, m0, m1, t, r, olo, ohi, hlo, hhi);
         if (m1.w != ~0u) {
             nm0 = a.meta[2ull * m1.w];
@@ -2109,6 +2103,34 @@ __device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ri
     propagate(a, c, ce);
     count_fused(a, hashed);
 }
+
+// The same from the slot's reverse-edge range cp0/cp1 (no plan: the
+// slot-fused job is the range's first edge, its record one more load away).
+__device__ __forceinline__ void mark_input_slot(const LevelArgs& a, uint32_t* ring, bool changed, uint32_t s,
+                                                const uint4& nlo, const uint4& nhi, uint32_t cp0, uint32_t cp1) {
+    uint32_t c = changed ? cp0 : 0u, ce = changed ? cp1 : 0u, p = ~0u;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+    const uint2 f = a.cons[c < ce ? c : 0u];
+    if (c < ce && (f.y & kSlotFused)) {
+        p = f.x;
+        ++c;
+        m0 = a.meta[2ull * p];
+        m1 = a.meta[2ull * p + 1];
+    }
+    mark_input_slot_from(a, ring, s, nlo, nhi, c, ce, p, m0, m1);
+}
+
+// A slot's plan entry (GraphDev::plan) beside its old digest: {c, ce, p} and
+// p's record, loaded in the round trip that reads the slot.
+struct SlotPlan {
+    uint4 v, m0, m1;
+    __device__ __forceinline__ void load(const LevelArgs& a, uint32_t s) {
+        const uint4* P = a.plan + 3ull * s;
+        v = P[0];
+        m0 = P[1];
+        m1 = P[2];
+    }
+};
 
 // Hashes, one lane per chain, the fused chain that starts at job p (~0u:
 // none) with records m0/m1 and its one hole reading slot fslot, whose new
@@ -2179,14 +2201,21 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __re
         bool changed = false;
         uint32_t s = 0, cp0 = 0, cp1 = 0;
         uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
+        SlotPlan pl;
+        pl.v = make_uint4(0, 0, ~0u, 0);
+        pl.m0 = pl.m1 = nlo;
         if (i < n) {
             s = sl[i];
             const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
             uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
             nlo = src[0];
             nhi = src[1];
-            cp0 = a.cons_ptr[s];  // with the digests, not after the compare
-            cp1 = a.cons_ptr[s + 1];
+            if constexpr (RF_SLOT_PLAN) {
+                pl.load(a, s);  // with the digests, not after the compare
+            } else {
+                cp0 = a.cons_ptr[s];
+                cp1 = a.cons_ptr[s + 1];
+            }
             const uint4 olo = dst[0], ohi = dst[1];
             changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
                       (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
@@ -2195,7 +2224,11 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __re
                 dst[1] = nhi;
             }
         }
-        mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
+        if constexpr (RF_SLOT_PLAN)
+            mark_input_slot_from(a, ring, s, nlo, nhi, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u,
+                                 changed ? pl.v.z : ~0u, pl.m0, pl.m1);
+        else
+            mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
     }
 }
 
@@ -2294,14 +2327,23 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
         bool changed = false;
         uint32_t s = 0, c = 0, ce = 0;
         uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
+        SlotPlan pl;
+        pl.v = make_uint4(0, 0, ~0u, 0);
+        pl.m0 = pl.m1 = nlo;
         if (i < n) {
             s = sl[i];
             const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
             uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
             nlo = src[0];
             nhi = src[1];
-            c = a.cons_ptr[s];
-            ce = a.cons_ptr[s + 1];
+            if constexpr (RF_SLOT_PLAN) {
+                pl.load(a, s);
+                c = pl.v.x;
+                ce = pl.v.y;
+            } else {
+                c = a.cons_ptr[s];
+                ce = a.cons_ptr[s + 1];
+            }
             const uint4 olo = dst[0], ohi = dst[1];
             changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
                       (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
@@ -2313,12 +2355,18 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
         if (!changed) c = ce = 0;
         uint32_t p = ~0u;
         uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-        const uint2 f = a.cons[c < ce ? c : 0u];
-        if (c < ce && (f.y & kSlotFused)) {
-            p = f.x;
-            ++c;
-            m0 = a.meta[2ull * p];
-            m1 = a.meta[2ull * p + 1];
+        if constexpr (RF_SLOT_PLAN) {
+            p = changed ? pl.v.z : ~0u;
+            m0 = pl.m0;
+            m1 = pl.m1;
+        } else {
+            const uint2 f = a.cons[c < ce ? c : 0u];
+            if (c < ce && (f.y & kSlotFused)) {
+                p = f.x;
+                ++c;
+                m0 = a.meta[2ull * p];
+                m1 = a.meta[2ull * p + 1];
+            }
         }
         hashed += hash_fused_chain_lean(a, ring, p, m0, m1, s, nlo, nhi);
         propagate(a, c, ce);  // the slot's other consumers
@@ -3168,6 +3216,9 @@ __global__ __launch_bounds__(kMarkBlock) void k_part_apply(const uint32_t* __res
         bool changed = false;
         uint32_t s = 0, cp0 = 0, cp1 = 0;
         uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
+        SlotPlan pl;
+        pl.v = make_uint4(0, 0, ~0u, 0);
+        pl.m0 = pl.m1 = nlo;
         if (i < n) {
             const uint32_t b = import_bid[i];
             if (!bits || ((bits[b >> 5] >> (b & 31)) & 1u)) {  // null bits: every import (fixed rounds)
@@ -3176,8 +3227,12 @@ __global__ __launch_bounds__(kMarkBlock) void k_part_apply(const uint32_t* __res
                 uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
                 nlo = src[0];
                 nhi = src[1];
-                cp0 = a.cons_ptr[s];
-                cp1 = a.cons_ptr[s + 1];
+                if constexpr (RF_SLOT_PLAN) {
+                    pl.load(a, s);
+                } else {
+                    cp0 = a.cons_ptr[s];
+                    cp1 = a.cons_ptr[s + 1];
+                }
                 const uint4 olo = dst[0], ohi = dst[1];
                 changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
                           (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
@@ -3187,7 +3242,36 @@ __global__ __launch_bounds__(kMarkBlock) void k_part_apply(const uint32_t* __res
                 }
             }
         }
-        mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
+        if constexpr (RF_SLOT_PLAN)
+            mark_input_slot_from(a, ring, s, nlo, nhi, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u,
+                                 changed ? pl.v.z : ~0u, pl.m0, pl.m1);
+        else
+            mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
+    }
+}
+
+// GraphDev::plan from the records: per slot its reverse-edge range past the
+// slot-fused consumer (flagged first in the range at load), that consumer
+// and its record.
+__global__ __launch_bounds__(256) void k_slot_plan(const uint32_t* __restrict__ cons_ptr,
+                                                   const uint2* __restrict__ cons, const uint4* __restrict__ meta,
+                                                   uint32_t S, uint4* __restrict__ plan) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < S; s += gridDim.x * blockDim.x) {
+        uint32_t c = cons_ptr[s], p = ~0u;
+        const uint32_t ce = cons_ptr[s + 1];
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        if (c < ce) {
+            const uint2 f = cons[c];
+            if (f.y & kSlotFused) {
+                p = f.x;
+                ++c;
+                m0 = meta[2ull * p];
+                m1 = meta[2ull * p + 1];
+            }
+        }
+        plan[3ull * s] = make_uint4(c, ce, p, 0u);
+        plan[3ull * s + 1] = m0;
+        plan[3ull * s + 2] = m1;
     }
 }
 
@@ -3267,6 +3351,7 @@ static LevelArgs mark_level_args(const GraphDev& g) {
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
 #endif
     flow_args(g, a);  // a flow step's mark queues with chain-out counts (propagate)
+    a.plan = g.plan;
     return a;
 }
 
@@ -3281,6 +3366,13 @@ hipError_t launch_graph_flow(const GraphDev& g, hipStream_t s, uint32_t* zero_co
     a.e = g.n_jobs;  // (k2_flow: the ready queue's capacity)
     const uint32_t grid = std::max<uint32_t>(1u, (g.n_cu ? g.n_cu : 256u) * RF_FLOW_WAVES);
     hipLaunchKernelGGL(k2_flow, dim3(grid), dim3(kLevelBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_slot_plan(const GraphDev& g, hipStream_t s) {
+    if (!g.n_slots) return hipSuccess;
+    hipLaunchKernelGGL(k_slot_plan, dim3(grid_for(g.n_slots, 8192)), dim3(256), 0, s, g.cons_ptr, g.cons, g.meta,
+                       g.n_slots, g.plan);
     return hipGetLastError();
 }
 
