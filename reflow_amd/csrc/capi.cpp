@@ -1743,8 +1743,8 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     lap("midstates");
     if (int rc = graph_build_plan(gr)) return rc;
     if (RF_DIAG_KNOB("RF_K2_STAMPS", 0)) {  // diagnostic build: per-phase times of workgroup 0 of each level
-        HIPC(gr->b_stamps.ensure(8ull * 128 * std::max<uint32_t>(L, 1)));
-        HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * std::max<uint32_t>(L, 1)));
+        HIPC(gr->b_stamps.ensure(8ull * 128 * (L + 1)));  // (row L: the mark kernel's)
+        HIPC(sync_memset(ctx, gr->b_stamps.p, 0, 8ull * 128 * (L + 1)));
         G.stamps = static_cast<unsigned long long*>(gr->b_stamps.p);
     }
     if (RF_DIAG_KNOB("RF_K2_WGSTAMPS", 0)) {  // diagnostic build: every incremental level kernel's workgroups
@@ -2434,6 +2434,21 @@ extern "C" int rf_graph_recompute(rf_graph* gr, int full, uint64_t* out_recomput
                 for (int k = 1; k < 64 && x[k]; ++k) fprintf(stderr, " %.2f", (x[k] - x[k - 1]) * 0.01);
                 fprintf(stderr, " (us)\n");
             }
+        // the mark kernel's workgroups 0..31: start (from the first), then the
+        // lanes' latest time at each phase end (MarkStamp)
+        std::vector<unsigned long long> mk(128);
+        HIPC(sync_copy(ctx, mk.data(), gr->g.stamps + 128ull * gr->g.n_levels, 8 * mk.size(), hipMemcpyDeviceToHost));
+        unsigned long long m0 = ~0ull;
+        for (int b = 0; b < 32; ++b)
+            if (mk[4 * b + 3]) m0 = std::min(m0, mk[4 * b]);
+        for (int b = 0; b < 32; ++b) {
+            const unsigned long long* x = &mk[4 * b];
+            if (!x[3]) continue;
+            fprintf(stderr, "[mark stamps] wg %d: start +%.2f, slot loaded %.2f, chain %.2f, appends %.2f, drained %.2f us\n",
+                    b, (x[0] - m0) * 0.01, (uint32_t)x[1] * 0.01, (uint32_t)(x[1] >> 32) * 0.01,
+                    (uint32_t)x[2] * 0.01, (uint32_t)(x[2] >> 32) * 0.01);
+        }
+        (void)sync_memset(ctx, gr->g.stamps + 128ull * gr->g.n_levels, 0, 8 * mk.size());
     }
     gr->last_recomputed = tot;
     if (out_recomputed) *out_recomputed = tot;

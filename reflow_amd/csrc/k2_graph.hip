@@ -2081,9 +2081,39 @@ __device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed)
 // with its record, first two template blocks, hole record, old digest and
 // start state in registers: they and the next job's record are fetched while
 // the job before it is hashed.  Called by every lane of the wave.
+// MarkStamp (diagnostic builds): a lane's phase times, reduced per wave.
+struct MarkStamp {
+#ifdef RF_DIAG
+    unsigned long long t0 = 0;
+    uint32_t d[4] = {0, 0, 0, 0};
+    __device__ __forceinline__ MarkStamp* sink(const LevelArgs& a) { return a.stamps ? this : nullptr; }
+    __device__ __forceinline__ void begin() { t0 = __builtin_amdgcn_s_memrealtime(); }
+    __device__ __forceinline__ void lap(int k) { d[k] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0); }
+    // workgroups 0..31 of k3_mark_slots: {start, max over lanes of each lap}
+    // into stamps row L (the level rows' stamps are [L][128])
+    __device__ __forceinline__ void end(const LevelArgs& a) {
+        if (!a.stamps || blockIdx.x >= 32) return;
+        for (int k = 0; k < 4; ++k)
+            for (int o = 32; o > 0; o >>= 1) d[k] = max(d[k], (uint32_t)__shfl_xor((int)d[k], o, 64));
+        if (threadIdx.x == 0) {
+            unsigned long long* r = a.stamps + 128ull * a.n_levels + 4 * blockIdx.x;
+            r[0] = t0;
+            r[1] = d[0] | ((unsigned long long)d[1] << 32);
+            r[2] = d[2] | ((unsigned long long)d[3] << 32);
+            r[3] = 1;
+        }
+    }
+#else
+    __device__ __forceinline__ MarkStamp* sink(const LevelArgs&) { return nullptr; }
+    __device__ __forceinline__ void begin() {}
+    __device__ __forceinline__ void lap(int) {}
+    __device__ __forceinline__ void end(const LevelArgs&) {}
+#endif
+};
+
 __device__ __forceinline__ void mark_input_slot_from(const LevelArgs& a, uint32_t* ring, uint32_t s, const uint4& nlo,
                                                      const uint4& nhi, uint32_t c, uint32_t ce, uint32_t p, uint4 m0,
-                                                     uint4 m1) {
+                                                     uint4 m1, MarkStamp* ms = nullptr) {
     constexpr uint32_t IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     // the job's operands (fetched a job ahead after the first)
@@ -2099,9 +2129,15 @@ __device__ __forceinline__ void mark_input_slot_from(const LevelArgs& a, uint32_
         }
     }
     const uint32_t hashed = hash_fused_chain(a, ring, p, m0, m1, nm0, nm1, t, r, olo, ohi, hlo, hhi, s, nlo, nhi);
+    if (ms) ms->lap(1);
     // the slot's other consumers
     propagate(a, c, ce);
+    if (ms) ms->lap(2);
     count_fused(a, hashed);
+    if (ms) {
+        vm_drain();
+        ms->lap(3);
+    }
 }
 
 // The same from the slot's reverse-edge range cp0/cp1 (no plan: the
@@ -2192,12 +2228,28 @@ constexpr uint32_t kMarkBlock = 64;
 // per SIMD at 240 VGPRs, hold 131k lanes)
 
 // set_slots: write input digests; a changed slot queues (or hashes) its consumers.
-__global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __restrict__ sl,
-                                                            const uint8_t* __restrict__ dig, uint32_t n, LevelArgs a) {
+#ifndef RF_MARK_SPLIT
+#define RF_MARK_SPLIT 1  // (A/B builds: 0 = one wave a workgroup, the slot's other consumers after its chain)
+#endif
+// k3_mark_slots' waves per workgroup: wave 0 hashes the 64 slots' fused
+// chains, wave 1 queues the same slots' other consumers (their reverse edges,
+// dirty bits and list appends: ~2.5 us of dependent round trips that followed
+// the chain in its lane), told which slots changed through LDS
+constexpr uint32_t kMarkWaves = (RF_MARK_SPLIT && RF_SLOT_PLAN) ? 2u : 1u;
+
+__global__ __launch_bounds__(kMarkBlock * kMarkWaves) void k3_mark_slots(const uint32_t* __restrict__ sl,
+                                                                         const uint8_t* __restrict__ dig, uint32_t n,
+                                                                         LevelArgs a) {
     __shared__ uint32_t ring_all[kMarkBlock * kRing];
-    uint32_t* ring = &ring_all[threadIdx.x * kRing];
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
+    __shared__ unsigned long long s_ch[2];
+    const uint32_t wave = kMarkWaves > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
+    const uint32_t lane = threadIdx.x & (kMarkBlock - 1);
+    uint32_t* ring = &ring_all[lane * kRing];
+    MarkStamp ms;
+    ms.begin();
+    uint32_t it = 0;
+    for (uint32_t base = blockIdx.x * kMarkBlock; base < n; base += gridDim.x * kMarkBlock, ++it) {
+        const uint32_t i = base + lane;
         bool changed = false;
         uint32_t s = 0, cp0 = 0, cp1 = 0;
         uint4 nlo = make_uint4(0, 0, 0, 0), nhi = nlo;
@@ -2206,30 +2258,52 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots(const uint32_t* __re
         pl.m0 = pl.m1 = nlo;
         if (i < n) {
             s = sl[i];
-            const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
-            uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
-            nlo = src[0];
-            nhi = src[1];
             if constexpr (RF_SLOT_PLAN) {
                 pl.load(a, s);  // with the digests, not after the compare
             } else {
                 cp0 = a.cons_ptr[s];
                 cp1 = a.cons_ptr[s + 1];
             }
-            const uint4 olo = dst[0], ohi = dst[1];
-            changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
-                      (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
-            if (changed) {
-                dst[0] = nlo;
-                dst[1] = nhi;
+            if (wave == 0) {
+                const uint4* src = reinterpret_cast<const uint4*>(dig + 32ull * i);
+                uint4* dst = reinterpret_cast<uint4*>(a.slots + 32ull * s);
+                nlo = src[0];
+                nhi = src[1];
+                const uint4 olo = dst[0], ohi = dst[1];
+                changed = (olo.x != nlo.x) | (olo.y != nlo.y) | (olo.z != nlo.z) | (olo.w != nlo.w) |
+                          (ohi.x != nhi.x) | (ohi.y != nhi.y) | (ohi.z != nhi.z) | (ohi.w != nhi.w);
+                if (changed) {
+                    dst[0] = nlo;
+                    dst[1] = nhi;
+                }
             }
         }
-        if constexpr (RF_SLOT_PLAN)
+#ifdef RF_DIAG
+        if (a.stamps) {
+            __asm__ volatile("" ::"v"(pl.v.x), "v"(pl.m0.x), "v"(pl.m1.x), "v"(cp0));
+            ms.lap(0);  // the slot's loads arrived (compare done)
+        }
+#endif
+        if constexpr (kMarkWaves > 1) {
+            if (wave == 0) {
+                const unsigned long long ch = __ballot(changed);
+                if (lane == 0) s_ch[it & 1] = ch;
+            }
+            __syncthreads();
+            if (wave == 1) {  // the slots' other consumers, beside the chains
+                changed = (s_ch[it & 1] >> lane) & 1ull;
+                propagate(a, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u);
+                continue;
+            }
+            mark_input_slot_from(a, ring, s, nlo, nhi, 0u, 0u, changed ? pl.v.z : ~0u, pl.m0, pl.m1, ms.sink(a));
+        } else if constexpr (RF_SLOT_PLAN) {
             mark_input_slot_from(a, ring, s, nlo, nhi, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u,
-                                 changed ? pl.v.z : ~0u, pl.m0, pl.m1);
-        else
+                                 changed ? pl.v.z : ~0u, pl.m0, pl.m1, ms.sink(a));
+        } else {
             mark_input_slot(a, ring, changed, s, nlo, nhi, cp0, cp1);
+        }
     }
+    if (wave == 0) ms.end(a);
 }
 
 // Throughput form of an incremental level (chosen per level and step when
@@ -3349,6 +3423,7 @@ static LevelArgs mark_level_args(const GraphDev& g) {
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
 #ifdef RF_DIAG
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
+    a.stamps = g.stamps;                     // (k3_mark_slots: MarkStamp into row L)
 #endif
     flow_args(g, a);  // a flow step's mark queues with chain-out counts (propagate)
     a.plan = g.plan;
@@ -3386,7 +3461,7 @@ hipError_t launch_graph_mark_slots(GraphDev& g, const uint32_t* slots, const uin
         hipLaunchKernelGGL(k3_mark_slots_lf, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, slots, digests, n,
                            mark_level_args(g));
     else
-        hipLaunchKernelGGL(k3_mark_slots, dim3(grid_mark(n)), dim3(kMarkBlock), 0, s, slots, digests, n,
+        hipLaunchKernelGGL(k3_mark_slots, dim3(grid_mark(n)), dim3(kMarkBlock * kMarkWaves), 0, s, slots, digests, n,
                            mark_level_args(g));
     return hipGetLastError();
 }
@@ -3405,7 +3480,7 @@ void graph_mark_params(const GraphDev& g, const uint32_t* slots, const uint8_t* 
     for (int i = 0; i < 4; ++i) args->ptrs[i] = v[i];
     p->func = reinterpret_cast<void*>(k3_mark_slots);
     p->gridDim = dim3(n ? grid_mark(n) : 1);  // an empty batch still runs (and marks nothing)
-    p->blockDim = dim3(kMarkBlock);
+    p->blockDim = dim3(kMarkBlock * kMarkWaves);
     p->sharedMemBytes = 0;
     p->kernelParams = args->ptrs;
     p->extra = nullptr;
