@@ -1979,8 +1979,10 @@ __device__ __forceinline__ void fetch_fused_ops(const LevelArgs& a, uint32_t q, 
 // olo/ohi, hlo/hhi) and its fusion target's records nm0/nm1 are in
 // registers, and its one hole reads slot fslot, whose new digest flo/fhi is
 // handed over in registers.  Each job whose digest changed hands it to its
-// fusion target; a job's other consumers are queued (propagate).  Returns the
-// jobs this lane hashed.  Called by every lane of the wave.
+// fusion target; a job's other consumers are queued (propagate) -- unless
+// kProp is false (k3_mark_slots' split form: another wave queued them).
+// Returns the jobs this lane hashed.  Called by every lane of the wave.
+template <bool kProp = true>
 __device__ __forceinline__ uint32_t hash_fused_chain(const LevelArgs& a, uint32_t* ring, uint32_t p, uint4 m0,
                                                      uint4 m1, uint4 nm0, uint4 nm1, uint4 (&t)[8], uint2 r,
                                                      uint4 olo, uint4 ohi, uint4 hlo, uint4 hhi, uint32_t fslot,
@@ -2057,7 +2059,7 @@ __device__ __forceinline__ uint32_t hash_fused_chain(const LevelArgs& a, uint32_
                 nm1 = nnm1;
             }
         }
-        propagate(a, cb, cz);
+        if constexpr (kProp) propagate(a, cb, cz);
         p = nx;
     }
     return hashed;
@@ -2111,6 +2113,7 @@ struct MarkStamp {
 #endif
 };
 
+template <bool kProp = true>
 __device__ __forceinline__ void mark_input_slot_from(const LevelArgs& a, uint32_t* ring, uint32_t s, const uint4& nlo,
                                                      const uint4& nhi, uint32_t c, uint32_t ce, uint32_t p, uint4 m0,
                                                      uint4 m1, MarkStamp* ms = nullptr) {
@@ -2128,7 +2131,8 @@ __device__ __forceinline__ void mark_input_slot_from(const LevelArgs& a, uint32_
             nm1 = a.meta[2ull * m1.w + 1];
         }
     }
-    const uint32_t hashed = hash_fused_chain(a, ring, p, m0, m1, nm0, nm1, t, r, olo, ohi, hlo, hhi, s, nlo, nhi);
+    const uint32_t hashed =
+        hash_fused_chain<kProp>(a, ring, p, m0, m1, nm0, nm1, t, r, olo, ohi, hlo, hhi, s, nlo, nhi);
     if (ms) ms->lap(1);
     // the slot's other consumers
     propagate(a, c, ce);
@@ -2232,9 +2236,14 @@ constexpr uint32_t kMarkBlock = 64;
 #define RF_MARK_SPLIT 1  // (A/B builds: 0 = one wave a workgroup, the slot's other consumers after its chain)
 #endif
 // k3_mark_slots' waves per workgroup: wave 0 hashes the 64 slots' fused
-// chains, wave 1 queues the same slots' other consumers (their reverse edges,
-// dirty bits and list appends: ~2.5 us of dependent round trips that followed
-// the chain in its lane), told which slots changed through LDS
+// chains, wave 1 queues every consumer the slots and their chains' jobs
+// reach (reverse edges, dirty bits and list appends: dependent round trips
+// that followed each job's hash in the chain's lane), told which slots
+// changed through LDS.  A chain's jobs have one hole each, their
+// predecessor's digest (the first: the slot's), so each job's digest changes
+// with its input -- short of a SHA-256 collision, where the consumers queued
+// ahead are re-hashed to the same digests: extra work, never a different
+// digest.
 constexpr uint32_t kMarkWaves = (RF_MARK_SPLIT && RF_SLOT_PLAN) ? 2u : 1u;
 
 __global__ __launch_bounds__(kMarkBlock * kMarkWaves) void k3_mark_slots(const uint32_t* __restrict__ sl,
@@ -2290,12 +2299,31 @@ __global__ __launch_bounds__(kMarkBlock * kMarkWaves) void k3_mark_slots(const u
                 if (lane == 0) s_ch[it & 1] = ch;
             }
             __syncthreads();
-            if (wave == 1) {  // the slots' other consumers, beside the chains
+            if (wave == 1) {  // the consumers, beside the chains
                 changed = (s_ch[it & 1] >> lane) & 1ull;
-                propagate(a, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u);
+                uint32_t p = changed ? pl.v.z : ~0u;
+                uint4 m1 = pl.m1;
+                propagate(a, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u);  // the slot's other consumers
+                while (__any(p != ~0u)) {  // each chain job's, but its fusion target's edge (the range's last)
+                    uint32_t cb = 0, cz = 0, nx = ~0u;
+                    uint4 nm1 = m1;
+                    if (p != ~0u) {
+                        const bool nf = m1.w != ~0u;
+                        cb = m1.y;
+                        cz = nf ? m1.z - 1 : m1.z;
+                        if (nf) {
+                            nx = m1.w;
+                            nm1 = a.meta[2ull * nx + 1];
+                        }
+                    }
+                    propagate(a, cb, cz);
+                    p = nx;
+                    m1 = nm1;
+                }
                 continue;
             }
-            mark_input_slot_from(a, ring, s, nlo, nhi, 0u, 0u, changed ? pl.v.z : ~0u, pl.m0, pl.m1, ms.sink(a));
+            mark_input_slot_from<false>(a, ring, s, nlo, nhi, 0u, 0u, changed ? pl.v.z : ~0u, pl.m0, pl.m1,
+                                        ms.sink(a));
         } else if constexpr (RF_SLOT_PLAN) {
             mark_input_slot_from(a, ring, s, nlo, nhi, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u,
                                  changed ? pl.v.z : ~0u, pl.m0, pl.m1, ms.sink(a));
