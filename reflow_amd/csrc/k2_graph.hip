@@ -2226,6 +2226,33 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
     return hashed;
 }
 
+// k3_mark_slots' append wave (wave 1) for one changed slot (changed, plan
+// pl): the slot's other consumers, then each job of its fused chain's
+// consumers but its fusion target's edge (the range's last), walking the
+// chain by its records -- the next job's record loaded before the current
+// job's appends.  Called by every lane of the wave.
+__device__ __forceinline__ void queue_chain_consumers(const LevelArgs& a, bool changed, const SlotPlan& pl) {
+    uint32_t p = changed ? pl.v.z : ~0u;
+    uint4 m1 = pl.m1;
+    propagate(a, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u);
+    while (__any(p != ~0u)) {
+        uint32_t cb = 0, cz = 0, nx = ~0u;
+        uint4 nm1 = m1;
+        if (p != ~0u) {
+            const bool nf = m1.w != ~0u;
+            cb = m1.y;
+            cz = nf ? m1.z - 1 : m1.z;
+            if (nf) {
+                nx = m1.w;
+                nm1 = a.meta[2ull * nx + 1];
+            }
+        }
+        propagate(a, cb, cz);
+        p = nx;
+        m1 = nm1;
+    }
+}
+
 constexpr uint32_t kMarkBlock = 64;
 // change sets from GraphDev::cfg_thru_mark slots (RF_K2_THRU_MARK_DEFAULT =
 // 98,304) mark in k3_mark_slots_lf (the resident waves of k3_mark_slots, two
@@ -2300,26 +2327,7 @@ __global__ __launch_bounds__(kMarkBlock * kMarkWaves) void k3_mark_slots(const u
             }
             __syncthreads();
             if (wave == 1) {  // the consumers, beside the chains
-                changed = (s_ch[it & 1] >> lane) & 1ull;
-                uint32_t p = changed ? pl.v.z : ~0u;
-                uint4 m1 = pl.m1;
-                propagate(a, changed ? pl.v.x : 0u, changed ? pl.v.y : 0u);  // the slot's other consumers
-                while (__any(p != ~0u)) {  // each chain job's, but its fusion target's edge (the range's last)
-                    uint32_t cb = 0, cz = 0, nx = ~0u;
-                    uint4 nm1 = m1;
-                    if (p != ~0u) {
-                        const bool nf = m1.w != ~0u;
-                        cb = m1.y;
-                        cz = nf ? m1.z - 1 : m1.z;
-                        if (nf) {
-                            nx = m1.w;
-                            nm1 = a.meta[2ull * nx + 1];
-                        }
-                    }
-                    propagate(a, cb, cz);
-                    p = nx;
-                    m1 = nm1;
-                }
+                queue_chain_consumers(a, (s_ch[it & 1] >> lane) & 1ull, pl);
                 continue;
             }
             mark_input_slot_from<false>(a, ring, s, nlo, nhi, 0u, 0u, changed ? pl.v.z : ~0u, pl.m0, pl.m1,
