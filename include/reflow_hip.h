@@ -330,6 +330,10 @@ typedef struct {
     uint64_t blob_len;
 } rf_graph_desc;
 
+/* Device footprint of a loaded graph: ~140 B a job (records, queued flags,
+ * lists, the flow step's per-job state, midstates), 84 B a slot (digest,
+ * reverse-edge pointer, the mark kernels' 48-B per-slot plan), 16 B a hole,
+ * 8 B a chain-out edge, and the templates padded to 64-B blocks. */
 int rf_graph_load(rf_ctx *ctx, const rf_graph_desc *desc, rf_graph **out);
 void rf_graph_destroy(rf_graph *g);
 /* Set input-slot digests (e.g. changed File IDs); marks their transitive
