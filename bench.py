@@ -921,13 +921,13 @@ def bench_persample(args, ctx, duo_us=None):
     f = np.asarray(slots, dtype=np.int64)
     pairs, samples = np.unique(f // 2), np.unique(f // 2 // P)
     n_dirty = int(2 * len(f) + 10 * len(pairs) + 5 * len(samples))  # Val + Coerce a file, the pair chain, the tail
-    log("  per-sample-root layout (SURVEY C3/C4): %d nodes, %.4f ms/step at N = 1 (flow %d), built+loaded in %.1f s"
-        % (dag.n_nodes, ms, st.last_flow, time.perf_counter() - t0))
+    log("  per-sample-root layout (SURVEY C3/C4): %d nodes, %.4f ms/step at N = 1, built+loaded in %.1f s"
+        % (dag.n_nodes, ms, time.perf_counter() - t0))
     res = {"workload": "SURVEY §8(d) C3/C4 as written: 1000align DAG of %d samples x P=%d (%d nodes), per-sample "
                        "roots, no Merge tree or global root; 1%% of leaf File IDs toggled per step" % (S * nparts, P,
                                                                                                    dag.n_nodes),
            "nodes": int(dag.n_nodes), "ms_per_step": round(ms, 4), "incremental_equals_full": same,
-           "flow_step": bool(st.last_flow), "dirty_nodes_per_step": n_dirty,
+           "dirty_nodes_per_step": n_dirty,
            "mnodes_per_s": round(n_dirty / (ms * 1e-3) / 1e6, 1),
            "critical_path_blocks": int(dag.critical_path(slots))}
     del dag, a

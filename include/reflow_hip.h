@@ -330,10 +330,10 @@ typedef struct {
     uint64_t blob_len;
 } rf_graph_desc;
 
-/* Device footprint of a loaded graph: ~140 B a job (records, queued flags,
- * lists, the flow step's per-job state, midstates), 84 B a slot (digest,
- * reverse-edge pointer, the mark kernels' 48-B per-slot plan), 16 B a hole,
- * 8 B a chain-out edge, and the templates padded to 64-B blocks. */
+/* Device footprint of a loaded graph: ~104 B a job (records, queued flags,
+ * lists, midstates), 84 B a slot (digest, reverse-edge pointer, the mark
+ * kernels' 48-B per-slot plan), 16 B a hole, and the templates padded to
+ * 64-B blocks. */
 int rf_graph_load(rf_ctx *ctx, const rf_graph_desc *desc, rf_graph **out);
 void rf_graph_destroy(rf_graph *g);
 /* Set input-slot digests (e.g. changed File IDs); marks their transitive
@@ -366,18 +366,6 @@ int rf_graph_recompute(rf_graph *g, int full, uint64_t *out_recomputed);
  * UINT64_MAX = never.  Not thread-safe against a step in flight on the
  * graph: call it between steps (the caller owns the graph, as for set_slots). */
 int rf_graph_set_forms(rf_graph *g, uint64_t thru, uint64_t thru_wide, uint64_t thru_mark);
-/* The flow step (readiness-driven: one launch in which a job starts as soon
- * as the jobs it reads have finished, instead of one kernel per level that
- * waits for the whole level below; the reference evaluator's ready loop,
- * /root/reference/eval.go:376-411, todo :902-955).  mode 1: a step whose
- * first levels up to the fill level all run in the throughput form runs them
- * and the sink level in one flow launch; 2: every launchable level whenever
- * possible; 0 (default): never -- on configs[3]'s 100M-node DAG the flow
- * launch measured slower than the level-by-level step.
- * Results never depend on it.
- * Takes effect from the next step's first set_slots (a step in progress
- * keeps the choice its first set_slots made). */
-int rf_graph_set_flow(rf_graph *g, int mode);
 /* Canonicalize's hand-over when copies collapse (flow.go:814-843, the
  * flowMap's first copy wins, :881-907): g, just loaded from the copies'
  * job table with the duplicates' jobs dropped and every hole re-pointed at
@@ -416,13 +404,11 @@ typedef struct {
     uint32_t split_block0;    /* fused links split block 0's schedule over chain and producer: 0 off, 1 / 2 (RF_K2_SPLIT) */
     uint32_t last_sink_attach; /* level whose launch ran the sink list in the last plain step (UINT32_MAX: none) */
     uint32_t last_levels_half; /* levels the last plain step ran in 32-job latency-form workgroups */
-    uint32_t last_flow;        /* the last plain step ran its first levels in one flow launch (k2_flow) */
-    uint32_t flow_mode;        /* rf_graph_set_flow */
 } rf_graph_stats;
-/* out_size = sizeof(rf_graph_stats) as the caller was compiled: the call
- * writes that many bytes at most (a caller built against an older, shorter
- * struct gets its prefix; the fields only ever grow at the end). */
-int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out, size_t out_size);
+/* Fills the whole struct above (its round-4 layout, unchanged since; a field
+ * added later comes with a new, sized entry point rather than a change to
+ * this one). */
+int rf_graph_stats_get(rf_graph *g, rf_graph_stats *out);
 
 /* ---- Checkpoint / resume of a loaded DAG ------------------------
  * Reference: a run's State is marshalled after every runner step

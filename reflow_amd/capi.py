@@ -31,7 +31,7 @@ EXPORTS = [
     "rf_fileset_digest_device", "rf_install_dir", "rf_install_info", "rf_install_entries",
     "rf_install_destroy",
     "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
-    "rf_graph_save", "rf_graph_restore", "rf_graph_set_forms", "rf_graph_set_flow",
+    "rf_graph_save", "rf_graph_restore", "rf_graph_set_forms",
     "rf_graph_adopt_slots",
     "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
@@ -234,8 +234,7 @@ class GraphStats(ctypes.Structure):
                 ("last_ms", ctypes.c_float), ("last_levels_lf", ctypes.c_uint32),
                 ("last_mark_lf", ctypes.c_uint32), ("last_levels_oct", ctypes.c_uint32),
                 ("split_block0", ctypes.c_uint32),
-                ("last_sink_attach", ctypes.c_uint32), ("last_levels_half", ctypes.c_uint32),
-                ("last_flow", ctypes.c_uint32), ("flow_mode", ctypes.c_uint32)]
+                ("last_sink_attach", ctypes.c_uint32), ("last_levels_half", ctypes.c_uint32)]
 
 
 _lib = None
@@ -302,8 +301,7 @@ def lib():
             "rf_graph_recompute": ([vp, i32, vp], i32),
             "rf_graph_recompute_async": ([vp, i32, vp], i32),
             "rf_graph_get_slots": ([vp, vp, u32, vp], i32),
-            "rf_graph_stats_get": ([vp, vp, ctypes.c_size_t], i32),
-            "rf_graph_set_flow": ([vp, i32], i32),
+            "rf_graph_stats_get": ([vp, vp], i32),
             "rf_graph_adopt_slots": ([vp, vp], i32),
             "rf_bloom_load": ([vp, u64, u64, vp, u64, u64, vp], i32),
             "rf_bloom_load_json": ([vp, ctypes.c_char_p, ctypes.c_size_t, vp], i32),
@@ -807,14 +805,8 @@ class Graph:
 
     def stats(self) -> GraphStats:
         s = GraphStats()
-        _check(lib().rf_graph_stats_get(self._h, ctypes.byref(s), ctypes.sizeof(s)))
+        _check(lib().rf_graph_stats_get(self._h, ctypes.byref(s)))
         return s
-
-    def set_flow(self, mode):
-        """rf_graph_set_flow: 0 never (default), 1 the first launchable levels
-        through the fill level, 2 every launchable level in one
-        readiness-driven flow launch whenever possible."""
-        _check(lib().rf_graph_set_flow(self._h, int(mode)))
 
     def adopt_slots(self, src):
         """rf_graph_adopt_slots: take src's whole slot table (same numbering),

@@ -1138,8 +1138,7 @@ extern "C" int rf_fileset_value_digest_batch(rf_ctx* ctx, const rf_fileset_tree*
 // tmpl_bytes of padded templates (contents not uploaded: rf_graph_load and
 // rf_graph_restore fill them), the per-step state zeroed and gr->g pointed at
 // them.  Caller holds ctx->mu.
-int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes,
-                       uint64_t n_cout) {
+int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes) {
     rf_ctx* ctx = gr->ctx;
     GraphDev& G = gr->g;
     G.n_jobs = J;
@@ -1157,28 +1156,8 @@ int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_
         (e = gr->b_lmeta.ensure(32ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
         (e = gr->b_counts.ensure(8ull * counts_half_words(L))) != hipSuccess ||  // two halves (plain-step parity)
         (e = gr->b_counts_last.ensure(4ull * (L + 1))) != hipSuccess ||
-        (e = gr->b_lvl_start.ensure(std::max<size_t>(4ull * (L + 1), 64))) != hipSuccess ||
-        (e = gr->b_cout_rng.ensure(8ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_cout.ensure(8ull * std::max<uint64_t>(n_cout, 1))) != hipSuccess ||
-        (e = gr->b_jlv.ensure(8ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_pend.ensure(4ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_dstart.ensure(std::max<size_t>(4ull * (L + 1), 64))) != hipSuccess ||
-        (e = gr->b_rq.ensure(8ull * std::max<uint32_t>(J, 1))) != hipSuccess ||
-        (e = gr->b_dq.ensure(8ull * std::max<uint32_t>(J, 1))) != hipSuccess)
+        (e = gr->b_lvl_start.ensure(std::max<size_t>(4ull * (L + 1), 64))) != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph alloc: %s", hipGetErrorString(e));
-    // pend is zero between steps; the queues' entries carry the step's epoch
-    // (from 1), so zero is never a live entry
-    HIPC(sync_memset(ctx, gr->b_pend.p, 0, 4ull * std::max<uint32_t>(J, 1)));
-    HIPC(sync_memset(ctx, gr->b_rq.p, 0, 8ull * std::max<uint32_t>(J, 1)));
-    HIPC(sync_memset(ctx, gr->b_dq.p, 0, 8ull * std::max<uint32_t>(J, 1)));
-    G.cout_rng = gr->b_cout_rng.as<uint2>();
-    G.cout = gr->b_cout.as<uint2>();
-    G.jlv = gr->b_jlv.as<uint2>();
-    G.pend = gr->b_pend.as<uint32_t>();
-    G.dstart = gr->b_dstart.as<uint32_t>();
-    G.rq = gr->b_rq.as<unsigned long long>();
-    G.dq = gr->b_dq.as<unsigned long long>();
-    G.n_cout = n_cout;
     HIPC(sync_memset(ctx, gr->b_slots.p, 0, 32ull * std::max<uint32_t>(S, 1)));
     HIPC(sync_memset(ctx, gr->b_dirty.p, 0, 4ull * (J + 1)));
     HIPC(sync_memset(ctx, gr->b_counts.p, 0, 8ull * counts_half_words(L)));
@@ -1230,21 +1209,6 @@ static void counting_pass(const std::vector<uint32_t>& idx, const uint32_t* key,
     for (uint32_t k = 0; k < nkey; ++k) at[k + 1] += at[k];
     out.resize(idx.size());
     for (uint32_t i : idx) out[at[key[i]]++] = i;
-}
-
-int graph_flow_upload(rf_graph* gr, const FlowHost& f) {
-    rf_ctx* ctx = gr->ctx;
-    const GraphDev& G = gr->g;
-    hipError_t e;
-    if ((e = sync_copy(ctx, gr->b_jlv.p, f.jlv.data(), 4ull * f.jlv.size(), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = sync_copy(ctx, gr->b_cout_rng.p, f.cout_rng.data(), 4ull * f.cout_rng.size(), hipMemcpyHostToDevice)) !=
-            hipSuccess ||
-        (e = f.cout.empty() ? hipSuccess
-                            : sync_copy(ctx, gr->b_cout.p, f.cout.data(), 4ull * f.cout.size(), hipMemcpyHostToDevice)) !=
-            hipSuccess ||
-        (e = sync_copy(ctx, gr->b_dstart.p, f.dstart.data(), 4ull * (G.n_levels + 1), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail(RF_EDEVICE, "graph upload (flow): %s", hipGetErrorString(e));
-    return RF_OK;
 }
 
 int graph_build_plan(rf_graph* gr) {
@@ -1624,77 +1588,9 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     gr->g.sink_attach_ok = true;
     gr->tmpl_bytes = tb;
     lap("reverse edges + forms");
-    // The flow step's structures (k2_flow, GraphDev "flow"): every job's chain
-    // head (itself, or -- a fusion target -- its chain's first job, found in
-    // topological order), wlev (the highest level of a queueable head among a
-    // job's producers), and each queueable head's chain-out edges (every
-    // consumer of every slot of its fused chain but the fusion edges).
-    FlowHost flow;
-    {
-        std::vector<uint32_t> head(J);
-        for (uint32_t j : q)
-            head[j] = fused_target[j] ? head[(uint32_t)gr->producer[d->hole_slot[d->hole_ptr[j]]]] : j;
-        flow.jlv.assign(2ull * J, 0);
-        flow.cout_rng.assign(2ull * J, 0);
-        std::vector<uint32_t> n_out(J, 0);  // internal order
-        load_parallel(ctx, J, 16384, [&](uint64_t i0, uint64_t i1) {
-            for (uint64_t i = i0; i < i1; ++i) {
-                const uint32_t j = perm[i];
-                uint32_t w = 0;
-                for (uint64_t h = d->hole_ptr[j]; h < d->hole_ptr[j + 1]; ++h) {
-                    const int64_t pj = gr->producer[d->hole_slot[h]];
-                    if (pj < 0) continue;
-                    const uint32_t hd = head[(uint32_t)pj];
-                    if (queueable(hd)) w = std::max(w, level[hd]);
-                }
-                flow.jlv[2 * i] = level[j];
-                flow.jlv[2 * i + 1] = w;
-                if (!queueable(j)) continue;
-                uint32_t n = 0;
-                for (int64_t x = j; x >= 0; x = fuse[(uint32_t)x]) {
-                    const uint32_t s = d->out_slot[(uint32_t)x];
-                    for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c)
-                        n += (int64_t)cjob[c] != fuse[(uint32_t)x] && queueable(cjob[c]);
-                }
-                n_out[i] = n;
-            }
-        });
-        uint64_t E = 0;
-        for (uint32_t i = 0; i < J; ++i) {
-            flow.cout_rng[2 * i] = (uint32_t)E;
-            E += n_out[i];
-            flow.cout_rng[2 * i + 1] = (uint32_t)E;
-        }
-        if (E >= 0xffffffffull) return fail(RF_EINVAL, "too many chain-out edges");
-        flow.cout.assign(2 * E, 0);
-        load_parallel(ctx, J, 16384, [&](uint64_t i0, uint64_t i1) {
-            for (uint64_t i = i0; i < i1; ++i) {
-                const uint32_t j = perm[i];
-                if (!n_out[i]) continue;
-                uint64_t o = flow.cout_rng[2 * i];
-                for (int64_t x = j; x >= 0; x = fuse[(uint32_t)x]) {
-                    const uint32_t s = d->out_slot[(uint32_t)x];
-                    for (uint64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
-                        const uint32_t k = cjob[c];
-                        if ((int64_t)k == fuse[(uint32_t)x] || !queueable(k)) continue;
-                        flow.cout[2 * o] = gr->ext2int[k];
-                        flow.cout[2 * o + 1] = level[k];
-                        ++o;
-                    }
-                }
-            }
-        });
-        // a job parks at most once a step, in the list of its wlev (sized
-        // for every job of that wlev: a restore can check it from jlv alone)
-        flow.dstart.assign(L + 1, 0);
-        for (uint32_t i = 0; i < J; ++i) flow.dstart[flow.jlv[2 * i + 1] + 1]++;
-        for (uint32_t l = 0; l < L; ++l) flow.dstart[l + 1] += flow.dstart[l];
-    }
-    lap("flow structures");
     // upload
     GraphDev& G = gr->g;
-    if (int rc = graph_device_alloc(gr, J, S, L, H, tmpl_size, flow.cout.size() / 2)) return rc;
-    if (int rc = graph_flow_upload(gr, flow)) return rc;
+    if (int rc = graph_device_alloc(gr, J, S, L, H, tmpl_size)) return rc;
     hipError_t e;
     if ((e = sync_copy(ctx, gr->b_meta.p, meta.data(), 32ull * J, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = sync_copy(ctx, gr->b_holes.p, holes.data(), 8ull * H, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -1764,8 +1660,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
                           &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_lmeta, &gr->b_counts, &gr->b_counts_last,
-                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst, &gr->b_plan,
-                          &gr->b_cout_rng, &gr->b_cout, &gr->b_jlv, &gr->b_pend, &gr->b_dstart, &gr->b_rq, &gr->b_dq})
+                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst, &gr->b_plan})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);
@@ -1797,7 +1692,6 @@ static int graph_check_inputs(rf_graph* gr, const uint32_t* slots, uint32_t n) {
     return fail(RF_EINVAL, "slot %u is the output of job %lld", slots[i], (long long)gr->producer[slots[i]]);
 }
 
-static void graph_flow_decide(rf_graph* gr, uint64_t n);
 
 extern "C" int rf_graph_set_slots(rf_graph* gr, const uint32_t* slots, const uint8_t* digests32,
                                   uint32_t n) {
@@ -1832,7 +1726,6 @@ extern "C" int rf_graph_set_slots(rf_graph* gr, const uint32_t* slots, const uin
         HIPC(launch_scatter_digests(gr->g.slots, gr->b_tmp_idx.as<uint32_t>(), gr->b_tmp_dig.as<uint8_t>(), n,
                                     ctx->stream));
     } else {
-        graph_flow_decide(gr, n);
         HIPC(launch_graph_mark_slots(gr->g, gr->b_tmp_idx.as<uint32_t>(), gr->b_tmp_dig.as<uint8_t>(), n,
                                      ctx->stream));
     }
@@ -1851,7 +1744,6 @@ extern "C" int rf_graph_set_slots_device(rf_graph* gr, const void* d_slots, cons
         HIPC(launch_scatter_digests(gr->g.slots, static_cast<const uint32_t*>(d_slots),
                                     static_cast<const uint8_t*>(d_digests32), n, pick(gr->ctx, stream)));
     } else {
-        graph_flow_decide(gr, n);
         HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
                                      static_cast<const uint8_t*>(d_digests32), n, pick(gr->ctx, stream)));
     }
@@ -1917,69 +1809,6 @@ extern "C" int rf_graph_set_forms(rf_graph* gr, uint64_t thru, uint64_t thru_wid
     return RF_OK;
 }
 
-// This step's flow range (GraphDev flo..fhi, fsink: one k2_flow launch
-// instead of one kernel per level), fixed by the step's first mark, whose
-// kernels then queue with chain-out counts: from the first launchable level
-// up to the fill level (the last level wide enough to hold the sinks' list),
-// when every launchable level there runs in the throughput form -- the
-// step's change set fills the chip, so a level barrier leaves SIMDs idle
-// behind each level's slowest waves -- plus the sink level; flow_mode 2:
-// every launchable level.  None for a partitioned graph (imports are queued
-// between passes), a captured sequence, a graph not yet fully recomputed,
-// or more levels than a flow launch takes.
-static void graph_flow_decide(rf_graph* gr, uint64_t n) {
-    GraphDev& G = gr->g;
-    if (gr->marked) return;  // (the step's first mark decided)
-    G.flo = ~0u;
-    if (!n || !G.flow_mode || gr->part || !graph_plain_steps() || !gr->initialized || !G.pend) return;
-    uint32_t first = ~0u, last = ~0u, fill = ~0u, sink = ~0u, n_launch = 0;
-    for (uint32_t l = 0; l < G.n_levels; ++l) {
-        if (G.inc_level[l] & kLvlSink) sink = l;
-        if (G.inc_level[l] & kLvlFill) fill = l;
-        if (!(G.inc_level[l] & kLvlForm)) continue;
-        if (first == ~0u) first = l;
-        last = l;
-    }
-    if (first == ~0u) return;
-    uint32_t lo = first, hi, fs = ~0u;
-    if (G.flow_mode == 2) {
-        hi = last;
-    } else {
-        if (fill == ~0u || sink == ~0u || fill < first) return;
-        hi = fill;
-        fs = sink;
-        G.step_marked = n;
-        G.thru_slots = G.cfg_thru;
-        G.thru_slots_wide = G.cfg_thru_wide;
-        for (uint32_t l = lo; l <= hi; ++l)
-            if ((G.inc_level[l] & kLvlForm) && (!graph_level_lf(G, l) || (G.inc_level[l] & kLvlOct))) return;
-    }
-    for (uint32_t l = lo; l <= hi; ++l) n_launch += (G.inc_level[l] & kLvlForm) ? 1u : 0u;
-    if (n_launch + (fs != ~0u) < 2 || hi - lo + 2 > kFlowMaxLevels) return;
-    G.flo = lo;
-    G.fhi = hi;
-    G.fsink = fs;
-    ++G.epoch;
-}
-
-// A flow range decided for a step that then does not run one (a full
-// recompute, a partitioned or captured step): the chain-out counts its
-// marks added are dropped with the queued set.
-static int graph_flow_cancel(rf_graph* gr, hipStream_t s) {
-    GraphDev& G = gr->g;
-    if (G.flo == ~0u) return RF_OK;
-    G.flo = ~0u;
-    HIPC(hipMemsetAsync(G.pend, 0, 4ull * std::max<uint32_t>(G.n_jobs, 1), s));
-    return RF_OK;
-}
-
-extern "C" int rf_graph_set_flow(rf_graph* gr, int mode) {
-    ARG(gr && mode >= 0 && mode <= 2, "flow mode must be 0, 1 or 2");
-    std::lock_guard<std::mutex> lk(gr->ctx->mu);
-    gr->g.flow_mode = (uint32_t)mode;  // (a step in progress keeps the range its first mark fixed)
-    return RF_OK;
-}
-
 extern "C" int rf_graph_adopt_slots(rf_graph* gr, rf_graph* src) {
     ARG(gr && src && gr != src, "null argument");
     ARG(gr->ctx == src->ctx, "graphs of different contexts");
@@ -2020,32 +1849,7 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
     } marked_reset{gr, swap || full || !plain};
     bool any = false;
     for (uint32_t l = 0; l < G.n_levels; ++l) any |= (G.inc_level[l] & kLvlForm) != 0;
-    if (G.flo != ~0u && (full || !plain || !any || lvl_lo != 0 || lvl_hi != ~0u || !swap || gr->part))
-        if (int rc = graph_flow_cancel(gr, s)) return rc;
-    if (plain && !full && any && G.flo != ~0u) {
-        // the flow step: one k2_flow launch over [flo, fhi] and the sink
-        // level, then the levels above the range one by one (a merge tree)
-        HIPC(launch_graph_flow(G, s, G.counts_other));
-        G.last_flow = 1;
-        G.last_levels_lf = G.last_levels_oct = G.last_levels_half = 0;
-        G.last_sink_attach = ~0u;
-        G.step_marked = gr->marked;
-        G.thru_slots = G.cfg_thru;
-        G.thru_slots_wide = G.cfg_thru_wide;
-        for (uint32_t l = G.fhi + 1; l < G.n_levels; ++l) {
-            if (!(G.inc_level[l] & kLvlForm) || l == G.fsink) continue;
-            HIPC(launch_graph_level(G, l, 0, s, nullptr, ~0u));
-            G.last_levels_lf += graph_level_lf(G, l) ? 1u : 0u;
-            G.last_levels_oct += (G.inc_level[l] & kLvlOct) ? 1u : 0u;
-            G.last_levels_half += graph_level_half(G, l) ? 1u : 0u;
-        }
-        G.flo = ~0u;
-        gr->last_counts = G.counts;
-        std::swap(G.counts, G.counts_other);
-        return RF_OK;
-    }
     if (plain && !full && any) {
-        G.last_flow = 0;
         // the level-kernel forms for this step: a level that can receive at
         // least cfg_thru chains (default kThruSlots; cfg_thru_wide, default
         // kThruSlotsWide, for levels of long jobs) fills the chip, and the
@@ -2201,7 +2005,6 @@ int graph_recompute_locked(rf_graph* gr, int full, hipStream_t s, uint32_t lvl_l
         gr->initialized = true;
         return RF_OK;
     }
-    if (int rc = graph_flow_cancel(gr, s)) return rc;
     hipGraphExec_t& ex = full ? gr->exec_full : gr->exec_inc;
     if (!ex && gr->g.n_levels)
         if (int rc = graph_capture(gr, full, &ex)) return rc;
@@ -2265,7 +2068,6 @@ extern "C" int rf_graph_update_recompute_async(rf_graph* gr, const void* d_slots
     DevGuard dg(gr->ctx->device);
     hipStream_t s = pick(gr->ctx, stream);
     if (!gr->initialized || inc_plain()) {  // mark, then the level launches (first call: the full sequence)
-        graph_flow_decide(gr, n);
         HIPC(launch_graph_mark_slots(gr->g, static_cast<const uint32_t*>(d_slots),
                                      static_cast<const uint8_t*>(d_digests32), n, s));
         gr->marked += n;
@@ -2299,38 +2101,7 @@ int graph_read_counts(rf_graph* gr, hipStream_t s, std::vector<uint32_t>& counts
     if (L && half) {
         for (uint32_t k = 0; k < kFusedParts; ++k) raw[L] += raw[L + 1 + kPartStride * k];
         for (uint32_t l = 0; l < L; ++l)  // the levels' list runs (engine.h kListShards)
-            for (uint32_t k = 0; k < kListShards; ++k) raw[l] += raw[list_shard_off(L) + k * flow_lp(L) + l];
-    }
-    if (L && half && gr->g.last_flow) {  // a flow step's jobs queued by flow lanes (never listed)
-        const uint32_t* er = &raw[counts_flow_base(L) + flow_ctl_off(L) + kFlowErr];
-        if (er[0]) {
-            // where it stood, and the first unfinished jobs of the level it waited on
-            const uint32_t l = std::min(er[2], L - 1), b = gr->g.lvl_start[l], e = gr->g.lvl_start[l + 1];
-            std::vector<uint32_t> dirty(e - b), pend(e - b);
-            std::string stuck;
-            if (hipMemcpy(dirty.data(), gr->g.dirty + b, 4ull * (e - b), hipMemcpyDeviceToHost) == hipSuccess &&
-                hipMemcpy(pend.data(), gr->g.pend + b, 4ull * (e - b), hipMemcpyDeviceToHost) == hipSuccess)
-                for (uint32_t i = 0, n = 0; i < e - b && n < 6; ++i)
-                    if (dirty[i] || pend[i]) {
-                        stuck += " job " + std::to_string(b + i) + " dirty " + std::to_string(dirty[i]) + " pend " +
-                                 std::to_string(pend[i]);
-                        ++n;
-                    }
-            return fail(RF_EDEVICE,
-                        "flow step gave up (scheduling fault; the graph's digests are not current): watermark %u "
-                        "level %u queued %u+%u finished %u, ready queue %u/%u, guard %u;%s",
-                        er[1], l, er[3], er[4], er[5], er[6], er[7], er[8], stuck.c_str());
-        }
-        for (uint32_t l = 0; l < L; ++l)
-            for (uint32_t sh = 0; sh < kFlowShards; ++sh)
-                raw[l] += raw[counts_flow_base(L) + (kFlowShards + sh) * flow_lp(L) + l];
-#ifdef RF_FLOW_PROFILE
-        const uint32_t* pw = er + 16;
-        fprintf(stderr, "[flow] wave-iterations %u (all idle %u), lanes hashing %u, long batches %u (%u jobs), "
-                "list starts %u, short takes %u, lane-blocks %u of %u issued (%.3f), longest wave %u us, waves %u\n",
-                pw[0], pw[1], pw[2], pw[3], pw[4], pw[5], pw[6], pw[7], pw[8], pw[8] ? (double)pw[7] / pw[8] : 0.0,
-                pw[9], pw[10]);
-#endif
+            for (uint32_t k = 0; k < kListShards; ++k) raw[l] += raw[list_shard_off(L) + k * cursor_lp(L) + l];
     }
     raw.resize(L + 1);
     counts.swap(raw);
@@ -2482,11 +2253,11 @@ extern "C" int rf_graph_gather_device(rf_graph* gr, const void* d_slots, uint32_
     return RF_OK;
 }
 
-extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* dst, size_t dst_size) {
-    ARG(gr && dst && dst_size, "null argument");
+extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* out) {
+    ARG(gr && out, "null argument");
     std::lock_guard<std::mutex> lk(gr->ctx->mu);
     DevGuard dg(gr->ctx->device);
-    rf_graph_stats st{}, *out = &st;
+    *out = rf_graph_stats{};
     out->n_jobs = gr->g.n_jobs;
     out->n_slots = gr->g.n_slots;
     out->n_levels = gr->g.n_levels;
@@ -2501,15 +2272,10 @@ extern "C" int rf_graph_stats_get(rf_graph* gr, rf_graph_stats* dst, size_t dst_
     out->split_block0 = gr->g.split_b0;
     out->last_sink_attach = gr->g.last_sink_attach;
     out->last_levels_half = gr->g.last_levels_half;
-    out->last_flow = gr->g.last_flow;
-    out->flow_mode = gr->g.flow_mode;
     if (gr->timed) {
         HIPC(hipEventSynchronize(gr->e1));
         HIPC(hipEventElapsedTime(&out->last_ms, gr->e0, gr->e1));
     }
-    // a caller built against an older (shorter) rf_graph_stats gets its prefix
-    memset(dst, 0, dst_size);
-    memcpy(dst, out, std::min(dst_size, sizeof st));
     return RF_OK;
 }
 

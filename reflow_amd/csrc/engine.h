@@ -87,25 +87,9 @@ constexpr uint32_t kOctMaxBlocks = 32, kOctMaxHoles = 64, kOctMaxLevel = 4096;
 // kPartStride words apart after each cursor half's L + 1 level counts, and
 // folded into [L] where it is read (k3_step_end, graph_read_counts).
 constexpr uint32_t kFusedParts = 64, kPartStride = 32, kCountsExtra = kFusedParts * kPartStride;
-// The flow step's control block (k2_flow), after each cursor half's fused
-// parts: per level F (jobs finished) and Q (jobs queued by flow lanes), each
-// in kFlowShards shards (a wave adds to its own: one counter took every chain
-// end's atomic in turn at the memory side, ~19 ns each -- 6.9 ms a 100M step),
-// shard s of level l at s * Lp + l (Lp = L rounded up to 32 words: a level's
-// shards on lines of their own); D (jobs parked) per level; then the
-// watermark, the ready queue's tail and head, the candidate cursor and the
-// error words, each on a 128-B line of its own.  Zero between steps (the half
-// is zeroed like the level counts).
-constexpr uint32_t kFlowShards = 16, kFlowListShards = 32;
-constexpr uint32_t kFlowCtl = 256 + 32 * kFlowListShards;  // + the candidate cursors, a line each, from word 256
-__host__ __device__ constexpr uint32_t flow_lp(uint32_t L) { return (L + 31) / 32 * 32; }
-constexpr uint32_t kFlowLW = 0, kFlowTail = 32, kFlowHead = 64;
-constexpr uint32_t kFlowLTail = 128, kFlowLHead = 160;  // the long-job queue (k2_flow)
-constexpr uint32_t kFlowList = 256;  // the candidate cursors (kFlowListShards, 32 words apart)
-constexpr uint32_t kFlowMaxLevels = 1024;  // range levels one flow launch takes (its LDS tables)
-constexpr uint32_t kFlowErr = 96;  // nonzero: the launch gave up (k2_flow kFlowTimeout); then where it stood
-__host__ __device__ constexpr uint32_t counts_flow_base(uint32_t L) { return L + 1 + kCountsExtra; }
-__host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFlowShards * flow_lp(L) + L; }
+// A level's append cursors sit Lp words apart (Lp = L rounded up to 32
+// words: a level's cursors on lines of their own).
+__host__ __device__ constexpr uint32_t cursor_lp(uint32_t L) { return (L + 31) / 32 * 32; }
 // The level lists' append cursors, kListShards per level: level l's list
 // region [lvl_start[l], lvl_start[l+1]) is cut by job id into kListShards
 // runs of 2^sh jobs (list_shard_shift), and a job joins the run its own id
@@ -114,8 +98,7 @@ __host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFl
 // cursors instead of taking one cursor in turn at the memory side (~19 ns
 // each: the 100M step's lean mark kernel, 2,200 waves appending to the Exec
 // level).  Shard k of level l at list_shard_off(L) + k * Lp + l (a level's
-// cursors on lines of their own).  Flow-range levels keep the single cursor
-// counts[l] (k2_flow reads its levels' lists as one run each).
+// cursors on lines of their own).
 #ifndef RF_SLOT_PLAN
 #define RF_SLOT_PLAN 1  // the mark kernels' per-slot plan (GraphDev::plan; A/B builds: 0 = off)
 #endif
@@ -125,10 +108,10 @@ __host__ __device__ constexpr uint32_t flow_ctl_off(uint32_t L) { return 2 * kFl
 constexpr bool kLegacyLists = RF_LIST_SHARDS == 0;  // one cursor, no staged runs (A/B)
 constexpr uint32_t kListShards = RF_LIST_SHARDS ? RF_LIST_SHARDS : 1;
 __host__ __device__ constexpr uint32_t list_shard_off(uint32_t L) {
-    return counts_flow_base(L) + flow_ctl_off(L) + kFlowCtl;
+    return L + 1 + kCountsExtra;
 }
 __host__ __device__ constexpr uint32_t counts_half_words(uint32_t L) {
-    return list_shard_off(L) + kListShards * flow_lp(L);
+    return list_shard_off(L) + kListShards * cursor_lp(L);
 }
 // log2 of a level's run length: the least sh with ceil(C / 2^sh) <= kListShards
 __host__ __device__ inline uint32_t list_shard_shift(uint32_t C) {
@@ -218,36 +201,6 @@ struct GraphDev {
     // profiles/r04/sw3)
     uint32_t split_half = 0;
     uint32_t dbg_mark = 0;  // diagnostic (RF_K2_DBG_MARK=1 at load): the lean mark kernel skips its fused-job count (stats wrong, digests right)
-    // ---- the flow step (k2_flow: readiness-driven, no level barrier) ----
-    // A queueable job's "head" is itself; a fusion target's is its chain's
-    // first job.  cout_rng[h] / cout: every queueable consumer {job, level}
-    // of any slot of h's fused chain except the fusion edges (the jobs h's
-    // chain completes for); wlev[k]: the highest level of a queueable head
-    // among k's producers (k cannot gain producers once every level below it
-    // has drained); pend[k]: producers of k queued this step and not yet
-    // finished (zero between steps); dstart[w]: the parking list of jobs
-    // with wlev w; rq / dq: the ready queue and parking lists, entries tagged
-    // with the step's epoch.  All built at load (rf_graph_load) or restored.
-    uint2* cout_rng = nullptr;
-    uint2* cout = nullptr;
-    uint2* jlv = nullptr;  // [J] {level, wlev}
-    uint32_t* pend = nullptr;
-    uint32_t* dstart = nullptr;
-    unsigned long long* rq = nullptr;
-    unsigned long long* dq = nullptr;
-    uint64_t n_cout = 0;
-    uint32_t epoch = 0;
-    // flow steps (rf_graph_set_flow): 0 (default) never, 1 when the step's
-    // first launchable levels up to the fill level all run in the throughput
-    // form, 2 every launchable level whenever possible.  Off by default: on
-    // configs[3]'s 100M-node step it measured 1.12-1.16 ms of device time
-    // against the level-by-level 0.70-0.72 (DESIGN.md §5 "The flow step")
-    uint32_t flow_mode = 0;
-    // this step's flow range, fixed by its first mark (graph_flow_decide):
-    // levels [flo, fhi] and the sink level fsink run in one k2_flow launch;
-    // flo = ~0u: the step runs level by level
-    uint32_t flo = ~0u, fhi = 0, fsink = ~0u;
-    uint32_t last_flow = 0;  // the last plain step ran a flow launch (rf_graph_stats)
 };
 // Midstates of the jobs' leading constant blocks, hashed once at load: job i
 // (internal order) hashes lead[i] blocks of its template from block
@@ -275,8 +228,6 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t level, int full, hipSt
 bool graph_level_lf(const GraphDev& g, uint32_t lvl);
 bool graph_level_half(const GraphDev& g, uint32_t lvl);
 hipError_t launch_graph_step_end(const GraphDev& g, int full, hipStream_t s);
-// The flow launch (k2_flow) of a plain incremental step over g.flo..g.fhi + g.fsink.
-hipError_t launch_graph_flow(const GraphDev& g, hipStream_t s, uint32_t* zero_counts);
 hipError_t launch_gather_slots(const uint8_t* slots, const uint32_t* idx, uint32_t n, uint8_t* out,
                                hipStream_t s);
 // Partitioned DAG exchange: pack changed exports (bits at bit0 + i), test the

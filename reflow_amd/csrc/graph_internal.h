@@ -36,8 +36,6 @@ struct rf_graph {
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
     DevBuf b_stamps, b_mid, b_wgst, b_plan;
-    // the flow step's structures (GraphDev "flow")
-    DevBuf b_cout_rng, b_cout, b_jlv, b_pend, b_dstart, b_rq, b_dq;
     DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_lmeta, b_counts,
         b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;
@@ -69,17 +67,6 @@ void graph_forms_from_env(rf::GraphDev& G);  // form thresholds at load / restor
 uint32_t graph_split_on();
 int graph_read_counts(rf_graph* gr, hipStream_t s, std::vector<uint32_t>& counts);
 uint32_t graph_ovf_cus(const rf_ctx* ctx, uint32_t* mode);  // RF_K2_OVF_CU / RF_K2_OVF                        // RF_K2_SPLIT (default on)
-int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes,
-                       uint64_t n_cout);
-// The flow structures of a loaded graph (rf_graph_load; GraphDev "flow"),
-// host side: per internal job {level, wlev}, its chain-out range and edges,
-// and the parking lists' starts by wlev.
-struct FlowHost {
-    std::vector<uint32_t> jlv;      // [2J]
-    std::vector<uint32_t> cout_rng; // [2J]
-    std::vector<uint32_t> cout;     // [2E]
-    std::vector<uint32_t> dstart;   // [L+1]
-};
-int graph_flow_upload(rf_graph* gr, const FlowHost& f);
+int graph_device_alloc(rf_graph* gr, uint32_t J, uint32_t S, uint32_t L, uint64_t H, uint64_t tmpl_bytes);
 int graph_build_plan(rf_graph* gr);  // GraphDev::plan, after the records are on the device
 void graph_part_release(rf_graph* gr);

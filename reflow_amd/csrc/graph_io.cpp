@@ -37,7 +37,10 @@ namespace {
 
 constexpr char kMagic[8] = {'R', 'F', 'G', 'R', 'A', 'P', 'H', '1'};
 constexpr char kEnd[8] = {'R', 'F', 'G', 'R', 'E', 'N', 'D', '1'};
-constexpr uint32_t kVersion = 2;  // 2: + the flow step's sections (jlv, cout_rng, cout, dstart)
+// 1 (round 4) and 3 share one layout; 2 (round 5) appended four sections
+// of the since-removed flow step (jlv, cout_rng, cout, dstart), which a
+// restore reads, checks against the checksums and drops
+constexpr uint32_t kVersion = 3;
 constexpr uint64_t kChunk = 64ull << 20;   // checksum granule
 constexpr uint64_t kStage = 256ull << 20;  // D2H / H2D staging (4 chunks)
 
@@ -49,13 +52,13 @@ struct Header {
     uint32_t n_jobs, n_slots, n_levels, max_level_jobs;
     uint64_t n_holes, tmpl_bytes, total_blocks, chunk;
     uint64_t n_sections;
-    uint64_t n_cout;  // chain-out edges (the flow step)
+    uint64_t n_cout;  // version 2 only: the flow step's chain-out edges (its "cout" section: 8 B each); else 0
     uint8_t reserved[128 - 8 - 6 * 4 - 6 * 8];
 };
 static_assert(sizeof(Header) == 128, "header layout");
 
 // One section of the file: host bytes, or a device buffer moved through the
-// pinned stage.
+// pinned stage, or (neither) a version-2 section a restore reads and drops.
 struct Section {
     const char* name;
     uint64_t bytes;
@@ -64,7 +67,8 @@ struct Section {
 };
 
 std::vector<Section> sections(rf_graph* gr, std::vector<uint32_t>& lvl, std::vector<uint8_t>& inc,
-                              std::vector<uint32_t>& ext2int, bool has_mid) {
+                              std::vector<uint32_t>& ext2int, bool has_mid, uint32_t version = kVersion,
+                              uint64_t n_cout = 0) {
     const GraphDev& G = gr->g;
     const uint64_t J = G.n_jobs, S = G.n_slots, L = G.n_levels, H = gr->hole_count;
     std::vector<Section> v = {
@@ -79,10 +83,10 @@ std::vector<Section> sections(rf_graph* gr, std::vector<uint32_t>& lvl, std::vec
         {"slots", 32 * S, nullptr, gr->b_slots.p},
     };
     if (has_mid) v.push_back({"mid", 32 * J, nullptr, gr->b_mid.p});
-    v.push_back({"jlv", 8 * J, nullptr, gr->b_jlv.p});
-    v.push_back({"cout_rng", 8 * J, nullptr, gr->b_cout_rng.p});
-    v.push_back({"cout", 8 * G.n_cout, nullptr, gr->b_cout.p});
-    v.push_back({"dstart", 4 * (L + 1), nullptr, gr->b_dstart.p});
+    if (version == 2)
+        for (Section x : {Section{"jlv", 8 * J}, Section{"cout_rng", 8 * J}, Section{"cout", 8 * n_cout},
+                          Section{"dstart", 4 * (L + 1)}})
+            v.push_back(x);
     return v;
 }
 
@@ -125,9 +129,6 @@ struct Validator {
     std::vector<uint32_t> exp_slot;                   // target -> its producer's out slot (~0: not a target)
     std::vector<std::pair<uint64_t, uint32_t>> tgt_holes;  // (the target's hole index, expected slot), ascending
     size_t tgt_cur = 0;
-    uint64_t jl_cur = 0, jl_lv = 0;        // jlv cursor: the level of the next record
-    std::vector<uint64_t> wcount;          // jobs per wlev (the parking lists' sizes)
-    std::vector<uint32_t> dstart;          // host copy
 
     // after the structure sections: every fusion target's hole was seen
     int done() const {
@@ -234,35 +235,6 @@ struct Validator {
                 if ((h.flags & 2u) && exp_slot[j] != ~0u && memcmp(w + 8 * r, IV, 32) != 0)
                     return fail(RF_EINTEGRITY, "graph restore: fusion target %llu has a midstate", (unsigned long long)j);
             }
-        } else if (!strcmp(name, "jlv")) {  // {level, wlev}: the level the layout gives, wlev below it
-            if (o == 0) wcount.assign(h.n_levels + 1, 0);
-            for (uint64_t r = 0; r < n / 8; ++r, ++jl_cur) {
-                while (jl_lv < h.n_levels && lvl[jl_lv + 1] <= jl_cur) ++jl_lv;
-                if (w[2 * r] != jl_lv || w[2 * r + 1] >= h.n_levels)
-                    return fail(RF_EINTEGRITY, "graph restore: flow record %llu inconsistent", (unsigned long long)jl_cur);
-                wcount[w[2 * r + 1]]++;
-            }
-        } else if (!strcmp(name, "cout_rng")) {
-            for (uint64_t r = 0; r < n / 8; ++r)
-                if (w[2 * r] > w[2 * r + 1] || w[2 * r + 1] > h.n_cout)
-                    return fail(RF_EINTEGRITY, "graph restore: chain-out range %llu out of range",
-                                (unsigned long long)(o / 8 + r));
-        } else if (!strcmp(name, "cout")) {  // {job, its level}, as the reverse edges
-            for (uint64_t r = 0; r < n / 8; ++r) {
-                const uint32_t x = w[2 * r], y = w[2 * r + 1];
-                if (x >= J || y >= h.n_levels || x < lvl[y] || x >= lvl[y + 1])
-                    return fail(RF_EINTEGRITY, "graph restore: chain-out edge %llu inconsistent",
-                                (unsigned long long)(o / 8 + r));
-            }
-        } else if (!strcmp(name, "dstart")) {  // the parking lists: at least the jobs of each wlev
-            for (uint64_t r = 0; r < n / 4; ++r) dstart.push_back(w[r]);
-            if (o + n == 4ull * (h.n_levels + 1)) {
-                if (dstart[0] != 0 || dstart[h.n_levels] > J)
-                    return fail(RF_EINTEGRITY, "graph restore: parking lists inconsistent");
-                for (uint32_t l = 0; l < h.n_levels; ++l)
-                    if (dstart[l + 1] < dstart[l] || dstart[l + 1] - dstart[l] < wcount[l])
-                        return fail(RF_EINTEGRITY, "graph restore: parking lists inconsistent");
-            }
         }
         return RF_OK;
     }
@@ -314,7 +286,6 @@ extern "C" int rf_graph_save(rf_graph* gr, const char* path) {
     h.total_blocks = gr->total_blocks;
     h.chunk = kChunk;
     h.n_sections = secs.size();
-    h.n_cout = G.n_cout;
     const std::string tmp = std::string(path) + ".tmp";
     File out;
     if (!(out.f = fopen(tmp.c_str(), "wb"))) return fail(RF_EIO, "graph save: cannot create %s", tmp.c_str());
@@ -365,10 +336,11 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     Header h;
     if (!get(&h, sizeof h) || memcmp(h.magic, kMagic, 8) != 0)
         return fail(RF_EINVAL, "graph restore: %s is not a graph checkpoint", path);
-    if (h.version != kVersion || h.chunk != kChunk)
+    if (h.version < 1 || h.version > kVersion || h.chunk != kChunk)
         return fail(RF_EINVAL, "graph restore: checkpoint version %u not supported", h.version);
-    if (h.n_sections != ((h.flags & kHasMid) ? 14u : 13u) || h.n_jobs > (1u << 31) || h.n_levels > h.n_jobs + 1 ||
-        h.n_cout >= 0xffffffffull)
+    const uint64_t n_sec = ((h.flags & kHasMid) ? 10u : 9u) + (h.version == 2 ? 4u : 0u);
+    if (h.n_sections != n_sec || h.n_jobs > (1u << 31) || h.n_levels > h.n_jobs + 1 ||
+        (h.version == 2 ? h.n_cout >= 0xffffffffull : h.n_cout != 0))
         return fail(RF_EINTEGRITY, "graph restore: corrupt header");
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
@@ -385,8 +357,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     G.stream_handover = RF_DIAG_KNOB("RF_K2_STREAM", 0) == 1;
     graph_forms_from_env(G);
     G.n_cu = graph_ovf_cus(ctx, &G.ovf_mode);
-    if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes, h.n_cout))
-        return rc;
+    if (int rc = graph_device_alloc(gr, h.n_jobs, h.n_slots, h.n_levels, h.n_holes, h.tmpl_bytes)) return rc;
     const bool has_mid = (h.flags & kHasMid) != 0;
     if (has_mid) {
         HIPC(gr->b_mid.ensure(std::max<size_t>(32ull * h.n_jobs, 64)));
@@ -395,7 +366,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
     std::vector<uint32_t> lvl(h.n_levels + 1);
     std::vector<uint8_t> inc(h.n_levels);
     std::vector<uint32_t> ext2int(h.n_jobs);
-    std::vector<Section> secs = sections(gr, lvl, inc, ext2int, has_mid);
+    std::vector<Section> secs = sections(gr, lvl, inc, ext2int, has_mid, h.version, h.n_cout);
     std::vector<uint32_t> out_slot(h.n_jobs);  // internal job -> out slot (from the records)
     Validator val(h, lvl, inc, out_slot);
     Stage st;
@@ -408,7 +379,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
             return fail(RF_EINTEGRITY, "graph restore: section %s truncated or resized", sc.name);
         for (uint64_t o = 0; o < sc.bytes; o += kStage) {
             const uint64_t n = std::min(kStage, sc.bytes - o);
-            uint8_t* dst = sc.dev ? stage.bytes() : static_cast<uint8_t*>(sc.host) + o;
+            uint8_t* dst = sc.host ? static_cast<uint8_t*>(sc.host) + o : stage.bytes();
             if (!get(dst, n)) return fail(RF_EINTEGRITY, "graph restore: section %s truncated", sc.name);
             const size_t d0 = digests.size();
             digests.resize(d0 + 32 * ((n + kChunk - 1) / kChunk));
@@ -418,7 +389,7 @@ extern "C" int rf_graph_restore(rf_ctx* ctx, const char* path, rf_graph** out) {
             if (int rc = val.piece(sc.name, dst, n, o)) return rc;
             if (sc.dev) HIPC(sync_copy(ctx, static_cast<uint8_t*>(sc.dev) + o, dst, n, hipMemcpyHostToDevice));
         }
-        if (!sc.dev)
+        if (sc.host)
             if (int rc = val.host_done(sc.name, &ext2int)) return rc;
     }
     if (int rc = val.done()) return rc;

@@ -41,7 +41,18 @@ namespace rf {
 
 constexpr uint32_t kLevelBlock = 256;
 constexpr uint32_t kRing = 33;  // words per lane: a 32-word ring + 1 (odd stride: no bank conflicts)
+// Diagnostic builds (-DRF_DIAG, diag.h) only: the phase stamps, the
+// per-workgroup records, the timing probes (LevelArgs::dbg_twice) and the
+// measured-dead kernel forms.  In the release build every such branch folds
+// away at compile time and the dead forms are not instantiated.
+#ifdef RF_DIAG
+constexpr bool kDiag = true;
+#else
+constexpr bool kDiag = false;
+#endif
 
+struct LevelArgs;
+__device__ __forceinline__ uint32_t dbg_mode(const LevelArgs& a);
 struct LevelArgs {
     uint32_t s, e, lvl;  // internal job range of the level
     int full;
@@ -84,24 +95,10 @@ struct LevelArgs {
     // chain per lane in those lane workgroups too, before the sinks
     uint32_t sink_wg = 0, ovf = 0;
     uint32_t handoff = 1;  // k2_level_pl cb0 = 2: the producer hands the chain its next target's operands
-    // the flow step (k2_flow, GraphDev "flow"): levels [flo, fhi] and fsink
-    // run in one readiness-driven launch; flo = ~0u: none this step (the mark
-    // kernels then queue as before)
-    const uint2* __restrict__ cout_rng = nullptr;
-    const uint2* __restrict__ cout = nullptr;
-    const uint2* __restrict__ jlv = nullptr;  // [J] {level, wlev}
-    uint32_t* pend = nullptr;
-    const uint32_t* __restrict__ dstart = nullptr;
-    unsigned long long* rq = nullptr;
-    unsigned long long* dq = nullptr;
-    uint32_t flo = ~0u, fhi = 0, fsink = ~0u, epoch = 0;
     const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
 };
-
-// Whether level l runs in this step's flow launch.
-__device__ __forceinline__ bool flow_level(const LevelArgs& a, uint32_t l) {
-    return a.flo != ~0u && ((l >= a.flo && l <= a.fhi) || (l == a.fsink && l != ~0u));
-}
+// The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
+__device__ __forceinline__ uint32_t dbg_mode(const LevelArgs& a) { return kDiag ? dbg_mode(a) : 0u; }
 
 // A level's append cursors (engine.h kListShards): run k of level l holds
 // the listed jobs whose ids fall in [lvl_start[l] + k * 2^sh, ... + 2^sh),
@@ -109,11 +106,11 @@ __device__ __forceinline__ bool flow_level(const LevelArgs& a, uint32_t l) {
 __device__ __forceinline__ const uint32_t* shard_cursors(const LevelArgs& a, uint32_t l) {
     return a.counts + list_shard_off(a.n_levels) + l;
 }
-// Jobs listed at level l this step (a level-launch level: never flow-range).
+// Jobs listed at level l this step.
 __device__ __forceinline__ uint32_t level_count(const LevelArgs& a, uint32_t l) {
     if constexpr (kLegacyLists) return a.counts[l];
     const uint32_t* c = shard_cursors(a, l);
-    const uint32_t lp = flow_lp(a.n_levels);
+    const uint32_t lp = cursor_lp(a.n_levels);
     uint32_t n = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kListShards; ++k) n += c[k * lp];
@@ -124,7 +121,7 @@ __device__ __forceinline__ uint32_t level_count(const LevelArgs& a, uint32_t l) 
 __device__ __forceinline__ uint32_t level_pos(const LevelArgs& a, uint32_t l, uint32_t i) {
     if constexpr (kLegacyLists) return a.lvl_start[l] + i;
     const uint32_t* c = shard_cursors(a, l);
-    const uint32_t lp = flow_lp(a.n_levels), b = a.lvl_start[l];
+    const uint32_t lp = cursor_lp(a.n_levels), b = a.lvl_start[l];
     const uint32_t sh = list_shard_shift(a.lvl_start[l + 1] - b);
     uint32_t k = 0;
 #pragma unroll
@@ -153,7 +150,7 @@ __device__ __forceinline__ void stage_runs(const LevelArgs& a, uint32_t* sr) {
         const uint32_t t = threadIdx.x, w = t / kListShards, k = t % kListShards;
         const uint32_t l = w ? a.lvl2 : a.lvl;
         const bool on = t < 2 * kListShards && l != ~0u;
-        uint32_t v = on ? shard_cursors(a, l)[k * flow_lp(a.n_levels)] : 0u;
+        uint32_t v = on ? shard_cursors(a, l)[k * cursor_lp(a.n_levels)] : 0u;
 #pragma unroll
         for (uint32_t o = 1; o < kListShards; o <<= 1) {
             const uint32_t u = (uint32_t)__shfl_up((int)v, o, 64);
@@ -204,10 +201,10 @@ struct WgStamp {
     unsigned long long t0 = 0;
     uint32_t jobs = 0;
     __device__ __forceinline__ void begin(const LevelArgs& a) {
-        if (a.wgst && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        if (kDiag && a.wgst && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
     }
     __device__ __forceinline__ void end(const LevelArgs& a) {
-        if (!a.wgst || threadIdx.x != 0 || blockIdx.x >= kWgStamps) return;
+        if (!(kDiag && a.wgst) || threadIdx.x != 0 || blockIdx.x >= kWgStamps) return;
         uint32_t hw, xcc;
         __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
                          : "=s"(hw), "=s"(xcc));
@@ -254,7 +251,7 @@ __device__ __forceinline__ void init_state(const LevelArgs& a, uint32_t p, ShaSt
 // with its 32-B record (q0, q1) beside it in lmeta, so a level kernel's first
 // job starts one HBM round trip earlier (list -> record -> template was three
 // dependent loads).  A job joins its level's run (engine.h kListShards, by
-// its id; a flow-range level has one run, counts[lv]): one atomicAdd per
+// its id): one atomicAdd per
 // distinct run in the wave, all issued before any result is used.  Called by
 // every lane of the wave.
 __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint32_t j, uint32_t lv, const uint4& q0,
@@ -291,26 +288,23 @@ __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint3
     while (__any(left)) {
         const uint32_t ld = (uint32_t)__ffsll((unsigned long long)__ballot(left)) - 1;
         const uint32_t lvl = __builtin_amdgcn_readfirstlane(__shfl(lv, ld, 64));
-        const bool flow = flow_level(a, lvl);
         const uint32_t b = a.lvl_start[lvl];
-        const uint32_t sh = flow ? 31u : list_shard_shift(a.lvl_start[lvl + 1] - b);
+        const uint32_t sh = list_shard_shift(a.lvl_start[lvl + 1] - b);
         const bool here = left && lv == lvl;
-        const uint32_t k = here ? (flow ? kListShards : (j - b) >> sh) : 0u;
+        const uint32_t k = here ? (j - b) >> sh : 0u;
         bool run = here;
         while (__any(run)) {
             const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(run)) - 1;
             const uint32_t kk = __builtin_amdgcn_readfirstlane(__shfl(k, leader, 64));
             const bool mine = run && k == kk;
             const uint64_t same = __ballot(mine);
-            if (lane == leader) {
-                uint32_t* cur = kk == kListShards ? &a.counts[lvl]
-                                                  : &a.counts[list_shard_off(a.n_levels) + kk * flow_lp(a.n_levels) + lvl];
-                old = atomicAdd(cur, (uint32_t)__popcll(same));
-            }
+            if (lane == leader)
+                old = atomicAdd(&a.counts[list_shard_off(a.n_levels) + kk * cursor_lp(a.n_levels) + lvl],
+                                (uint32_t)__popcll(same));
             if (mine) {
                 ml = leader;
                 ms = same;
-                rb = kk == kListShards ? b : b + (kk << sh);
+                rb = b + (kk << sh);
                 run = false;
             }
         }
@@ -328,30 +322,17 @@ __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint3
 // Mark consumers [c, ce) of the lanes whose slot changed (c == ce otherwise)
 // dirty, queueing the newly dirty ones (their records are fetched beside the
 // dirty-flag atomic).  Wave-uniform loop.
-// A job k newly queued at a level of this step's flow range (by the mark
-// kernels, before the flow launch, or by a flow lane): every consumer its
-// chain completes for waits for it -- pend + 1 per chain-out edge inside the
-// range (k2_flow decrements them when k's chain ends).
-__device__ __forceinline__ void flow_count_out(const LevelArgs& a, uint2 r) {
-    for (uint32_t e = r.x; e < r.y; ++e) {
-        const uint2 o = a.cout[e];
-        if (flow_level(a, o.y)) atomicAdd(&a.pend[o.x], 1u);
-    }
-}
-
 __device__ __forceinline__ void propagate(const LevelArgs& a, uint32_t c, uint32_t ce) {
     while (__any(c < ce)) {
         bool need = false;
-        uint2 jl = make_uint2(0, 0), cr = make_uint2(0, 0);
+        uint2 jl = make_uint2(0, 0);
         uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
         if (c < ce) {
             jl = a.cons[c++];
             q0 = a.meta[2ull * jl.x];
             q1 = a.meta[2ull * jl.x + 1];
-            if (flow_level(a, jl.y)) cr = a.cout_rng[jl.x];  // (the mark kernels of a flow step)
             need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
         }
-        if (need) flow_count_out(a, cr);
         append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
 }
@@ -390,32 +371,9 @@ struct PendingHole {
     uint4 lo, hi;
 };
 
-// Agent-scope (sc1) accesses: the flow step hands digests between CUs inside
-// one launch, and a CU's L1 is never refreshed by another CU's stores
-// (MI355X_MICROARCH.md, inter-workgroup visibility): the producer stores a
-// digest write-through and drains (vmcnt(0)) before the atomic that signals
-// it; the consumer, told by an atomic, reads it with sc1 loads.
-__device__ __forceinline__ uint32_t ld_ag(const uint32_t* p) {
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_ag64(const unsigned long long* p) {
-    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_ag64(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void vm_drain() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// a 32-B slot digest as two uint4 (lo, hi), sc1
-__device__ __forceinline__ void ld_dig_ag(const uint8_t* slot, uint4& lo, uint4& hi) {
-    const unsigned long long* s = reinterpret_cast<const unsigned long long*>(slot);
-    const unsigned long long a0 = ld_ag64(s), a1 = ld_ag64(s + 1), a2 = ld_ag64(s + 2), a3 = ld_ag64(s + 3);
-    lo = make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
-    hi = make_uint4((uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)a3, (uint32_t)(a3 >> 32));
-}
 
-// kAg: the hole digests are read with agent-scope loads (k2_flow)
-template <bool kAg>
-struct MatCursorT {
+struct MatCursor {
     // holes hn .. hn+3 in flight with their slot digests, and the records of
     // hn+4 and hn+5: a block applies at most two holes (they are >= 32 B apart),
     // so a record arrives a block before its digest load is issued, and the
@@ -438,13 +396,9 @@ struct MatCursorT {
     __device__ __forceinline__ void digest(const LevelArgs& a, PendingHole& q, const uint2& r) const {
         q.r = r;
         const uint8_t* slot = a.slots + 32ull * (q.r.y == ~0u ? 0u : q.r.y);
-        if constexpr (kAg) {
-            ld_dig_ag(slot, q.lo, q.hi);
-        } else {
-            const uint4* src = reinterpret_cast<const uint4*>(slot);
-            q.lo = src[0];
-            q.hi = src[1];
-        }
+        const uint4* src = reinterpret_cast<const uint4*>(slot);
+        q.lo = src[0];
+        q.hi = src[1];
     }
     __device__ __forceinline__ void apply(uint32_t* ring, const PendingHole& q) const {
         const bool f = q.r.y == fslot;
@@ -564,7 +518,6 @@ struct MatCursorT {
         for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
     }
 };
-using MatCursor = MatCursorT<false>;
 
 // The producer wave's material cursor in k2_level_pl: MatCursor's template
 // stream, with the holes in chunks of kHC per job.  While chunk c is applied
@@ -789,13 +742,13 @@ __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_
     for (uint32_t b = 0; b < cur.nb; ++b) {
         uint32_t w[16];
         cur.block(a, b, ring, w);
-        if (a.dbg_twice == 1) {  // (2 = RF_K2_STAMPS=2, not a hashing mode)
+        if (dbg_mode(a) == 1) {  // (2 = RF_K2_STAMPS=2, not a hashing mode)
             ShaState s2 = st;
             uint32_t w2[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) w2[i] = w[i] ^ (a.dbg_twice - 1);
+            for (int i = 0; i < 16; ++i) w2[i] = w[i] ^ (dbg_mode(a) - 1);
             sha256_compress(s2, w2);
-            st.h[0] ^= s2.h[0] & (a.dbg_twice - 1);
+            st.h[0] ^= s2.h[0] & (dbg_mode(a) - 1);
         }
         sha256_compress(st, w);
     }
@@ -857,7 +810,7 @@ constexpr uint32_t kPcRow = 68;  // words per K+W row: 16-B reads of 64 rows hit
 // producer's new digest reaches the fused job's material through LDS.
 #define RF_STAMP(k)                                                                        \
     do {                                                                                   \
-        if (a.stamps && blockIdx.x == 0 && lane == 0 && wave < 2 && (k) < 64)             \
+        if (kDiag && a.stamps && blockIdx.x == 0 && lane == 0 && wave < 2 && (k) < 64)             \
             a.stamps[128 * a.lvl + 64 * wave + (k)] = __builtin_amdgcn_s_memrealtime();    \
     } while (0)
 
@@ -868,6 +821,7 @@ constexpr uint32_t kPcRow = 68;  // words per K+W row: 16-B reads of 64 rows hit
 // writes the K+W row a block later; the chain lags two blocks.
 constexpr uint32_t kWRow = 20;  // words per assembled-block row: 16-B accesses of 16 lanes hit distinct banks
 
+#ifdef RF_DIAG  // the one-lane chain form (RF_K2_CHAIN=14, A/B): diagnostic builds only
 template <uint32_t kW>
 __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
     static_assert(kW == 2 || kW == 3, "chain + producer (+ expander)");
@@ -1052,6 +1006,7 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
         }
     }
 }
+#endif  // RF_DIAG
 
 // k2_level_pl: k2_level_pc with two chain waves running the two-lane lagged
 // chain (lag_chain.h RF_L2_*: 9 instructions per round instead of
@@ -1073,7 +1028,7 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
 // for the store's acknowledgement (phases looked ~0.5-1 us longer than they are).
 #define RF_STAMP_PL(k)                                                                                \
     do {                                                                                              \
-        if (a.stamps && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == kProd) && (k) < 64)    \
+        if (kDiag && a.stamps && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == kProd) && (k) < 64)    \
             s_stamp[wave != 0][(k)] = __builtin_amdgcn_s_memrealtime();                              \
     } while (0)
 
@@ -1283,7 +1238,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
         s_cw[0] = s_cw[1] = 0;
         s_split = 0;
     }
-    if (a.stamps && threadIdx.x < 128) s_stamp[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+    if (kDiag && a.stamps && threadIdx.x < 128) s_stamp[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     lds_barrier();
     // streamed: next block id, flags seen, a pre-built block 1 of the next job
     uint32_t gb = 0, known = 0, known_c0 = 0, known_c1 = 0, pre_id = ~0u;
@@ -1374,7 +1329,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
             // kW = 3: as with cb0, a finished job's frontier atomics run on the
             // producer in its idle last iteration of the next pass, not on the
             // chain's critical path (RF_K2_DBG_NOEXP=6: on the chain, A/B)
-            const bool pp3 = kW == 3 && !kStream && a.dbg_twice != 6;
+            const bool pp3 = kW == 3 && !kStream && dbg_mode(a) != 6;
             uint32_t wb0[16];
     #pragma unroll
             for (int q = 0; q < 16; ++q) wb0[q] = lane + q;  // (pass 0's warm-up expands these)
@@ -1422,7 +1377,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                 cur.hq = &s_hq[lane * kHq];
                 uint4 olo = make_uint4(0, 0, 0, 0), ohi = olo;
                 uint2 pre[2] = {make_uint2(0, 0), make_uint2(0, 0)};
-                if (!kStream && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                if (!kStream && dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                 if (kIsProd && has) {
                     cur.fslot = fslot;
                     if (cb0 || sc) {
@@ -1509,7 +1464,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                         nmhi = a.mid[2ull * m1.w + 1];
                     }
                 }
-                if (kChain && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }  // (the next target's loads issued)
+                if (kChain && dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }  // (the next target's loads issued)
                 uint32_t t0, t1, t2, t3;
                 uint32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
                 bool spl0 = false;  // (chain) the block step below is a split block 0
@@ -1521,7 +1476,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                 auto chain_block = [&](uint32_t b, uint32_t bufb, bool full, bool own0 = false) {
                     const uint32_t bi = kStream ? bufb % 3 : (bufb & 1);
                     if (kStream && full && !own0) known = lds_poll(&s_flag[bi], 4 * bufb + 1, 4 * bufb);
-                    if (kStream && full && a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                    if (kStream && full && dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                     const uint32_t row_off = ((bi * kJ + jl) * kPcRow) * 4, ones_off = kOnes * kPcRow * 4;
                     const uint4* r4 = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(kw) +
                                                                      ((M & ones_off) | (~M & row_off)));
@@ -1545,7 +1500,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                         uint4 vnn = vn;
                         if (kStream && (g == 2 || g == 6 || g == 10)) {  // r4[g + 2] opens chunk (g + 2) / 4
                             known = lds_poll(&s_flag[bi], 4 * bufb + (g + 2) / 4 + 1, known);
-                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            if (dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                         }
                         // split block 0: r4[g + 2] opens the producer's chunk (g + 2) / 4
                         // (split 1: chunks 2, 3; split 2: chunks 1-3)
@@ -1567,7 +1522,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                                 known_c0 = lds_poll(&s_cons[0], gb - 2, known_c0);
                                 known_c1 = lds_poll(&s_cons[1], gb - 2, known_c1);
                             }
-                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            if (dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                             const bool mine = b < m0.y;
                             uint32_t w[16];
                             volatile uint32_t* fl = &s_flag[gb % 3];
@@ -1592,7 +1547,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                                         lds_publish(fl, 4 * gb + 1, lane);
                                     else if (c >= 2)  // chunk c - 1, its writes drained behind chunk c's
                                         lds_publish_prev(fl, 4 * gb + c, lane);
-                                    if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                                    if (dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                                 }
                                 lds_publish(fl, 4 * gb + 4, lane);
                             }
@@ -1672,7 +1627,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                             uint32_t w[16];
     #pragma unroll
                             for (int q = 0; q < 16; ++q) w[q] = s_w0[lane * 17 + q];
-                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            if (dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                             uint4* row0 = reinterpret_cast<uint4*>(&kw[(lane < kJ ? (xp & 1) * kJ + lane : kJunk) * kPcRow]);
                             const uint32_t fb = (a.split + 1) * sid;  // this pass's flag values: fb + 1 ..
                             if (a.split == 2) {  // chunks 1-3 (the chain wrote chunk 0 only)
@@ -1685,22 +1640,22 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                                 kw_expand_chunk(w, row0, 2);
                                 lds_publish(&s_split, fb + 1, lane);
                             }
-                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            if (dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                             kw_expand_chunk(w, row0, 3);
                             lds_publish(&s_split, fb + a.split + 1, lane);
-                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            if (dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                             if (tab) cur.skip(1, ring);  // (a longer target's block 2 on from the cursor)
                             // the last pass's frontier atomics here, where the chain's
                             // rounds of block 0 leave the producer time, not in the
                             // last iteration, which builds the next block 1
                             if (pend) producer_propagate();
-                            if (a.dbg_twice == 2) { RF_STAMP_PL(sk); ++sk; }
+                            if (dbg_mode(a) == 2) { RF_STAMP_PL(sk); ++sk; }
                         }
-                        if (pb < m0.y && !tab && !((a.dbg_twice == 3 && pb >= 1) || a.dbg_twice == 4)) {
+                        if (pb < m0.y && !tab && !((dbg_mode(a) == 3 && pb >= 1) || dbg_mode(a) == 4)) {
                             uint32_t w[16];
                             cur.block(a, pb, ring, w, wfused);
                             // (RF_K2_STAMPS=3: every block's assembly end on the producer)
-                            if ((a.dbg_twice == 2 && it == 0) || a.dbg_twice == 8) { RF_STAMP_PL(sk); ++sk; }
+                            if ((dbg_mode(a) == 2 && it == 0) || dbg_mode(a) == 8) { RF_STAMP_PL(sk); ++sk; }
                             if (kW == 2) {
                                 kw_expand_store(w, reinterpret_cast<uint4*>(&kw[(((pb + xp) & 1) * kJ + lane) * kPcRow]));
                             } else {
@@ -1750,7 +1705,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                             }
                         }
                     } else if (kIsExp) {
-                        if (it >= 1 && it - 1 < m0.y && !((a.dbg_twice == 3 && it >= 2) || a.dbg_twice == 4)) {
+                        if (it >= 1 && it - 1 < m0.y && !((dbg_mode(a) == 3 && it >= 2) || dbg_mode(a) == 4)) {
                             const uint32_t bb = (it - 1) & 1;
                             const uint4* row = reinterpret_cast<const uint4*>(&wbuf[(bb * 64 + lane) * kWRow]);
                             uint32_t w[16];
@@ -1772,7 +1727,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                         // runs the expansion there once on dummy words into the
                         // other row buffer (the producer writes it only after the
                         // barrier): the code is then cached when the links start.
-                        const bool exb = it == 0 && (cb0 || (kCB && a.cb0 && pass == 0 && a.dbg_twice != 5));
+                        const bool exb = it == 0 && (cb0 || (kCB && a.cb0 && pass == 0 && dbg_mode(a) != 5));
                         if (exb) {
                             uint4* row = reinterpret_cast<uint4*>(&kw[((cb0 ? (xp & 1) * kJ : kJ) + jl) * kPcRow]);
                             if (!kStream && a.split == 2)  // (pass 0: warms the code the split passes run)
@@ -1782,13 +1737,13 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                             else
                                 chain_expand_b0(wb0, elane, row);
                         }
-                        if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
+                        if (dbg_mode(a) == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
                         if (cb0 || it >= lag) {
                             const uint32_t cbk = cb0 ? it : it - lag;
                             spl0 = split && it == 0;
                             chain_block(cbk, cbk + xp, true);
                         }
-                        if (a.dbg_twice == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
+                        if (dbg_mode(a) == 2 && it == 0) { RF_STAMP_PL(sk); ++sk; }
                     }
                     lds_barrier();
                     RF_STAMP_PL(sk); ++sk;
@@ -1924,7 +1879,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
     } else {
         if constexpr (kW == 3) body(std::integral_constant<uint32_t, kExp>{});
     }
-    if (a.stamps && blockIdx.x == 0 && (wave == 0 || wave == kProd))
+    if (kDiag && a.stamps && blockIdx.x == 0 && (wave == 0 || wave == kProd))
         a.stamps[128 * a.lvl + 64 * (wave != 0) + lane] = s_stamp[wave != 0][lane];
     ws.end(a);
 }
@@ -2481,539 +2436,7 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
         hashed += hash_fused_chain_lean(a, ring, p, m0, m1, s, nlo, nhi);
         propagate(a, c, ce);  // the slot's other consumers
     }
-    if (a.dbg_twice != 16) count_fused(a, hashed);
-}
-
-// ---- the flow step: readiness-driven, no level barrier ----------------------
-// One launch runs every level of the step's flow range (GraphDev flo..fhi and
-// the sink level; graph_flow_decide picks it): instead of one kernel per
-// level, each waiting for the whole level below it, a job starts as soon as
-// the jobs it reads have finished -- the reference evaluator's "gather Flows
-// that are ready ... wait for one task ... gather any new Flows that have
-// become ready" (/root/reference/eval.go:376-411, todo :902-955), with the
-// early cut-off of Flow.Digest memoization kept (flow.go:653-750): a job whose
-// inputs all come back unchanged is never hashed.
-//
-// Per job k (GraphDev "flow"): pend[k] counts k's producer chains queued this
-// step and not yet finished (+1 per chain-out edge when the chain's head is
-// queued -- flow_count_out, by the mark kernels or a flow lane -- and -1 when
-// that chain ends, changed or not); dirty[k] bit 0 = queued (an input
-// changed), bit 1 = claimed (started), bit 2 = parked.  k may start when pend[k]
-// is 0 AND no producer of k can still be queued: every level below wlev[k]
-// (the highest level of a queueable head among k's producers) has drained --
-// the watermark LW, advanced level by level as each level's finished count
-// reaches its queued count (mark-listed + flow-queued).  A job whose pend
-// reaches 0 before its watermark waits in the parking list of its wlev,
-// swept when LW passes it.  Whoever brings pend[k] to 0 with k queued
-// claims it and runs it in its own lane next (the OpK of a sample starts in
-// the lane whose pair chain finished last); further ready jobs go to a ready
-// queue of epoch-tagged entries that idle lanes take tickets on.  The jobs
-// the mark kernel queued are the initial candidates, taken through a
-// cursor in a scattered order (waves get a mix of long and short work).
-// Lanes hash one job (one link of a fused chain) per iteration, one-lane
-// SHA-256 as k2_level_lf; digests cross CUs write-through and are read with
-// agent-scope loads (MatCursorT<true>, finish_job_ag).  Termination: every
-// lane leaves when LW has passed the whole range (every queued job finished).
-constexpr uint32_t kFlowMaxLev = kFlowMaxLevels;
-#ifndef RF_FLOW_WAVES
-#define RF_FLOW_WAVES 2  // waves per SIMD (the register budget: 256 VGPRs at 2)
-#endif
-// every wave leaves a flow launch that has run this long (s_memrealtime, 100
-// MHz: 2 s, ~2,000x a 100M-node step) and flags it: a scheduling fault must
-// end the kernel, not hang the device (the host reports RF_EDEVICE)
-constexpr unsigned long long kFlowTimeout = 200000000ull;
-
-struct FlowCtl {
-    uint32_t *F, *Q, *D, *lw, *tail, *head, *ltail, *lhead, *lcur, *err;
-    uint32_t nlev, R, lp, sh;  // sh: this wave's shard of F and Q
-    __device__ __forceinline__ explicit FlowCtl(const LevelArgs& a) {
-        uint32_t* fb = a.counts + counts_flow_base(a.n_levels);
-        lp = flow_lp(a.n_levels);
-        F = fb;
-        Q = fb + kFlowShards * lp;
-        D = fb + 2 * kFlowShards * lp;
-        sh = (blockIdx.x * 5u + (threadIdx.x >> 6)) % kFlowShards;
-        uint32_t* ctl = fb + flow_ctl_off(a.n_levels);
-        lw = ctl + kFlowLW;
-        tail = ctl + kFlowTail;
-        head = ctl + kFlowHead;
-        ltail = ctl + kFlowLTail;
-        lhead = ctl + kFlowLHead;
-        lcur = ctl + kFlowList;
-        err = ctl + kFlowErr;
-        nlev = a.fhi - a.flo + 1;
-        R = nlev + (a.fsink != ~0u ? 1u : 0u);
-    }
-    // the range level at watermark position p (levels flo..fhi, then the sink level)
-    __device__ __forceinline__ uint32_t level_at(const LevelArgs& a, uint32_t p) const {
-        return p < nlev ? a.flo + p : a.fsink;
-    }
-    // the watermark position at which every level below w has drained
-    __device__ __forceinline__ uint32_t need(const LevelArgs& a, uint32_t w) const {
-        return w <= a.flo ? 0u : min(w - a.flo, nlev);
-    }
-};
-
-__device__ __forceinline__ unsigned long long flow_tag(const LevelArgs& a, uint32_t k) {
-    return ((unsigned long long)a.epoch << 32) | k;
-}
-
-// Claim queued, unclaimed job k (bit 1): k, or ~0u if it is not queued or
-// someone else has it.  A CAS, not an OR: a job already run and reset to 0
-// must stay 0.
-__device__ __forceinline__ uint32_t flow_claim(const LevelArgs& a, uint32_t k) {
-    uint32_t v = ld_ag(&a.dirty[k]);
-    while ((v & 3u) == 1u) {
-        const uint32_t o = atomicCAS(&a.dirty[k], v, v | 2u);
-        if (o == v) return k;
-        v = o;
-    }
-    return ~0u;
-}
-
-// The ready queue: jobs a chain end made ready beyond the one its lane runs
-// next, and jobs a sweep of the parking lists claimed.
-// An index a flow structure gives that falls outside its array: record the
-// site (the host reports it with the step's failure) and skip the access --
-// a scheduling fault must not become a device fault.
-#define RF_FLOW_GUARD(cond, site, fc)                                             \
-    (__builtin_expect(!(cond), 0) ? (atomicCAS((fc).err + 8, 0u, (uint32_t)(site)), \
-                                     atomicExch((fc).err, 1u), false)              \
-                                  : true)
-__device__ __forceinline__ void flow_push(const LevelArgs& a, const FlowCtl& fc, uint32_t k) {
-    const uint32_t t = atomicAdd(fc.tail, 1u);
-    if (RF_FLOW_GUARD(t < a.e, 1, fc)) st_ag64(&a.rq[t], flow_tag(a, k));
-}
-// Up to n reserved entries of a queue (head < tail), no overshoot: the first
-// taken index (the lanes poll their entries: a pusher writes its entry right
-// after reserving it).  One lane.
-// The two loads are sampled in no fixed order (another wave's take may move
-// head past the tail value read): t <= h takes nothing.  Polled with loads,
-// never atomics: every idle wave polls, and same-address atomics serialize
-// at the memory side.
-__device__ __forceinline__ uint32_t flow_take(uint32_t* head, uint32_t* tail, uint32_t n, uint32_t& got) {
-    uint32_t h = ld_ag(head);
-    for (;;) {
-        const uint32_t t = ld_ag(tail);
-        const uint32_t m = t > h ? min(n, t - h) : 0u;
-        got = m;
-        if (!m) return 0;
-        const uint32_t o = atomicCAS(head, h, h + m);
-        if (o == h) return h;
-        h = o;
-    }
-}
-
-// k's pend is 0 but its watermark is not reached: into the parking list of
-// wlev w (once per step: bit 2).  The entry is stored before LW is read
-// again, and the sweeper advances LW before it reads the list, so one of
-// the two sees the other (both may try: the claim decides).
-__device__ __forceinline__ uint32_t flow_park(const LevelArgs& a, const FlowCtl& fc, uint32_t k, uint32_t w,
-                                              uint32_t nd) {
-    uint32_t v = ld_ag(&a.dirty[k]);
-    for (;;) {
-        if ((v & 7u) != 1u) return ~0u;  // claimed, or parked already
-        const uint32_t o = atomicCAS(&a.dirty[k], v, v | 4u);
-        if (o == v) break;
-        v = o;
-    }
-    const uint32_t i = atomicAdd(&fc.D[w], 1u);
-    if (RF_FLOW_GUARD(a.dstart[w] + i < a.dstart[w + 1], 2, fc)) st_ag64(&a.dq[a.dstart[w] + i], flow_tag(a, k));
-    vm_drain();
-    if (ld_ag(fc.lw) >= nd) return flow_claim(a, k);
-    return ~0u;
-}
-
-// pend[k] has just reached 0 (or k is a mark-listed candidate with pend 0):
-// claim it if it is queued and its watermark is reached, else park it.
-__device__ __forceinline__ uint32_t flow_trigger(const LevelArgs& a, const FlowCtl& fc, uint32_t k) {
-    if ((ld_ag(&a.dirty[k]) & 3u) != 1u) return ~0u;  // not queued (no input changed so far), or claimed
-    const uint32_t w = a.jlv[k].y, nd = fc.need(a, w);
-    if (ld_ag(fc.lw) >= nd) return flow_claim(a, k);
-    return flow_park(a, fc, k, w, nd);
-}
-
-// Advance the watermark over every drained level; the jobs parked on the
-// level it opens are claimed and queued by the wave's lanes.  Called by
-// every lane of the wave.
-__device__ __forceinline__ void flow_advance(const LevelArgs& a, const FlowCtl& fc) {
-    const uint32_t lane = __lane_id();
-    for (;;) {
-        const uint32_t p = __builtin_amdgcn_readfirstlane(ld_ag(fc.lw));
-        if (p >= fc.R) return;
-        // level l's queued - finished, over the shards: the finished count
-        // first (lanes 0..15), then -- after it has arrived -- the queued
-        // ones (flow-queued shards on lanes 16..31, the mark-listed count on
-        // lane 32): a job is queued before it finishes, so finished(t1) ==
-        // queued(t2 > t1) means nothing queued by t2 was unfinished at t1
-        // (and nothing more can be queued here: the levels below drained)
-        const uint32_t l = fc.level_at(a, p);
-        int32_t v = lane < kFlowShards ? -(int32_t)ld_ag(&fc.F[lane * fc.lp + l]) : 0;
-        vm_drain();
-        if (lane >= kFlowShards && lane < 2 * kFlowShards) v = (int32_t)ld_ag(&fc.Q[(lane - kFlowShards) * fc.lp + l]);
-        else if (lane == 2 * kFlowShards) v = (int32_t)ld_ag(&a.counts[l]);
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (v != 0) return;  // (uniform: the reduction's result is the same in every lane)
-        uint32_t st = 0;  // 1 advanced p -> p + 1, 2 lost a race: look again
-        if (lane == 0) st = atomicCAS(fc.lw, p, p + 1) == p ? 1u : 2u;
-        st = __builtin_amdgcn_readfirstlane(__shfl(st, 0, 64));
-        if (st == 2) continue;
-        if (p + 1 < fc.nlev) {
-            const uint32_t w = a.flo + p + 1, base = a.dstart[w];
-            const uint32_t n = min(ld_ag(&fc.D[w]), a.dstart[w + 1] - base);
-            for (uint32_t i = lane; i < n; i += 64) {
-                const unsigned long long e = ld_ag64(&a.dq[base + i]);
-                if ((uint32_t)(e >> 32) != a.epoch) continue;  // not written yet: its parker sees LW and claims it
-                const uint32_t k = (uint32_t)e;
-                if (ld_ag(&a.pend[k]) != 0u) continue;  // a producer still runs: its end triggers k
-                const uint32_t t = flow_claim(a, k);
-                if (t != ~0u) flow_push(a, fc, t);
-            }
-        }
-    }
-}
-
-// counter[l] += the lanes with `add` at level l, one atomic per distinct
-// level in the wave (this wave's shard).  Called by every lane of the wave.
-__device__ __forceinline__ void flow_wave_add(uint32_t* counter, bool add, uint32_t l) {
-    uint64_t mask = __ballot(add);
-    while (mask) {
-        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
-        const uint32_t lv = __builtin_amdgcn_readfirstlane(__shfl(l, leader, 64));
-        const uint64_t same = __ballot(add && l == lv);
-        if (__lane_id() == leader) atomicAdd(&counter[lv], (uint32_t)__popcll(same));
-        add = add && l != lv;
-        mask = __ballot(add);
-    }
-}
-
-// A changed job's consumers (reverse edges [c, ce), the fusion edge
-// excluded): one inside the flow range is queued -- its queued flag, the
-// level's flow-queued count and its own chain-out pend -- and waits for
-// pend; one outside it joins its level's list for the level kernels after
-// the flow launch.  Wave-uniform loop.
-__device__ __forceinline__ void flow_propagate(const LevelArgs& a, const FlowCtl& fc, uint32_t c, uint32_t ce) {
-    while (__any(c < ce)) {
-        bool need = false, inr = false;
-        uint2 jl = make_uint2(0, 0), cr = make_uint2(0, 0);
-        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-        if (c < ce) {
-            jl = a.cons[c++];
-            inr = flow_level(a, jl.y);
-            if (inr) {
-                cr = a.cout_rng[jl.x];
-            } else {
-                q0 = a.meta[2ull * jl.x];
-                q1 = a.meta[2ull * jl.x + 1];
-            }
-            need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
-        }
-        if (need && inr) flow_count_out(a, cr);
-        flow_wave_add(fc.Q + fc.sh * fc.lp, need && inr, jl.y);
-        append_jobs(a, need && !inr, jl.x, jl.y, q0, q1);
-    }
-}
-
-// As finish_job_pre, the new digest stored write-through (agent scope): a
-// consumer on another CU reads it inside this launch.
-__device__ __forceinline__ bool finish_job_ag(const LevelArgs& a, const uint4& m1, const ShaState& st,
-                                              const uint4& olo, const uint4& ohi) {
-    uint32_t n[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) n[i] = bswap32(st.h[i]);
-    const bool changed = (olo.x != n[0]) | (olo.y != n[1]) | (olo.z != n[2]) | (olo.w != n[3]) |
-                         (ohi.x != n[4]) | (ohi.y != n[5]) | (ohi.z != n[6]) | (ohi.w != n[7]);
-    if (changed) {
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.slots + 32ull * m1.x);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st_ag64(dst + i, (unsigned long long)n[2 * i] | ((unsigned long long)n[2 * i + 1] << 32));
-    }
-    return changed;
-}
-
-// hash_fused_chain_lean for the flow step: the links' digests stored
-// write-through, their other consumers queued by flow_propagate.  Returns the
-// links this lane hashed.  Called by every lane of the wave.
-__device__ __forceinline__ uint32_t flow_chain(const LevelArgs& a, const FlowCtl& fc, uint32_t* ring, uint32_t p,
-                                               uint4 m0, uint4 m1, uint32_t fslot, uint4 flo, uint4 fhi) {
-    uint32_t hashed = 0;
-    while (__any(p != ~0u)) {
-        uint32_t cb = 0, cz = 0, nx = ~0u;
-        if (p != ~0u) {
-            const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);
-            const uint4 olo = od[0], ohi = od[1];
-            const bool nf = m1.w != ~0u;
-            uint4 nm0 = make_uint4(0, 0, 0, 0), nm1 = nm0;
-            if (nf) {
-                nm0 = a.meta[2ull * m1.w];
-                nm1 = a.meta[2ull * m1.w + 1];
-            }
-            MatCursorT<true> cur;
-            cur.fslot = fslot;
-            cur.flo = flo;
-            cur.fhi = fhi;
-            cur.begin_fused(a, m0, ring);
-            ShaState st;
-            init_state(a, p, st);
-            for (uint32_t b = 0; b < cur.nb; ++b) {
-                uint32_t w[16];
-                cur.block(a, b, ring, w, true);
-                sha256_compress(st, w);
-            }
-            const bool ch = finish_job_ag(a, m1, st, olo, ohi);
-            ++hashed;
-            cb = m1.y;
-            cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);
-            if (ch && nf) {
-                nx = m1.w;
-                fslot = m1.x;
-                flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
-                fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
-                m0 = nm0;
-                m1 = nm1;
-            }
-        }
-        flow_propagate(a, fc, cb, cz);
-        p = nx;
-    }
-    return hashed;
-}
-
-__global__ __launch_bounds__(kLevelBlock, RF_FLOW_WAVES) void k2_flow(LevelArgs a) {
-    __shared__ uint32_t ring_all[kLevelBlock * kRing];
-    __shared__ uint32_t s_pref[kFlowMaxLev + 1];  // prefix of the range levels' mark-listed counts
-    __shared__ uint32_t s_base[kFlowMaxLev];      // list position of each range level's first entry - its prefix
-    uint32_t* ring = &ring_all[threadIdx.x * kRing];
-    zero_other_counts(a);
-    const FlowCtl fc(a);
-    // (the mark kernel that listed them has finished: plain loads)
-    for (uint32_t q = threadIdx.x; q < fc.R; q += blockDim.x) {
-        const uint32_t l = fc.level_at(a, q);
-        s_pref[q + 1] = a.counts[l];
-        s_base[q] = a.lvl_start[l];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        s_pref[0] = 0;
-        for (uint32_t q = 0; q < fc.R; ++q) {
-            s_pref[q + 1] += s_pref[q];
-            s_base[q] -= s_pref[q];
-        }
-    }
-    __syncthreads();
-    const uint32_t n_list = s_pref[fc.R];
-    // levels no job was queued at drain at once (else only chain ends advance
-    // the watermark, and a step with nothing to hash would never end)
-    if (blockIdx.x == 0 && threadIdx.x < 64) flow_advance(a, fc);
-    const uint32_t lane = __lane_id();
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    // the lane's chain: its head (hd, level hl, chain-out range cr, records
-    // m0 / m1); a whole fused chain runs per iteration, as k2_level_lf's
-    // lanes do (hash_fused_chain_lean: each link's old digest and its fusion
-    // target's records fetched at its start, the digest handed over in
-    // registers), and only its end pays the flow protocol
-    uint32_t p = ~0u, hd = 0, hl = 0, tk = ~0u;
-    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-    uint2 cr = make_uint2(0, 0);
-    uint32_t hashed = 0, idle_n = 0;
-    // the candidates in list order (level by level: a wave's lanes take
-    // jobs of one kind), one cursor drawn by whole waves
-    bool lists = n_list > 0;
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-#ifdef RF_FLOW_PROFILE
-    // diagnostic build: per-wave tallies added to the control block's words
-    // 112.. at the end (tools/flow_probe.py)
-    uint32_t pr_it = 0, pr_idle = 0, pr_lanes = 0, pr_list = 0, pr_sq = 0, pr_blk = 0, pr_slot = 0;
-#define RF_PROF(...) __VA_ARGS__
-#else
-#define RF_PROF(...)
-#endif
-    auto start = [&](uint32_t k) {
-        if (!RF_FLOW_GUARD(k < a.e, 9, fc)) return;
-        p = hd = k;
-        m0 = a.meta[2ull * k];
-        m1 = a.meta[2ull * k + 1];
-        hl = a.jlv[k].x;
-        cr = a.cout_rng[k];
-    };
-    for (;;) {
-        // 1. work for idle lanes: the candidates the mark kernel listed, else
-        //    ready jobs another lane's chain end queued
-        {
-            const bool want = p == ~0u && tk == ~0u && lists;
-            const uint64_t wm = __ballot(want);
-            if (wm) {
-                const uint32_t cnt = (uint32_t)__popcll(wm);
-                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)wm) - 1;
-                uint32_t base = 0;
-                if (lane == ld) base = atomicAdd(fc.lcur, cnt);
-                base = __builtin_amdgcn_readfirstlane(__shfl(base, ld, 64));
-                if (base + cnt >= n_list) lists = false;  // (wave-uniform)
-                const uint32_t pos = base + (uint32_t)__popcll(wm & lt);
-                if (want && pos < n_list) {
-                    uint32_t a0 = 0, a1 = fc.R;  // s_pref[a0] <= pos < s_pref[a1]
-                    while (a1 - a0 > 1) {
-                        const uint32_t mid = (a0 + a1) >> 1;
-                        if (s_pref[mid] <= pos) a0 = mid; else a1 = mid;
-                    }
-                    const uint32_t li = s_base[a0] + pos;
-                    const uint32_t k = RF_FLOW_GUARD(li < a.e, 4, fc) ? a.list[li] : 0u;
-                    // pend > 0: a producer chain still runs, its end triggers k
-                    const uint32_t t = ld_ag(&a.pend[k]) == 0u ? flow_trigger(a, fc, k) : ~0u;
-                    if (t != ~0u) start(t);
-                    RF_PROF(pr_list += t != ~0u ? 1u : 0u;)
-                }
-            }
-        }
-        {
-            const bool tw = p == ~0u && tk == ~0u && !lists;
-            const uint64_t tm = __ballot(tw);
-            if (tm) {
-                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)tm) - 1;
-                uint32_t got = 0, base = 0;
-                if (lane == ld) base = flow_take(fc.head, fc.tail, (uint32_t)__popcll(tm), got);
-                got = __builtin_amdgcn_readfirstlane(__shfl(got, ld, 64));
-                base = __builtin_amdgcn_readfirstlane(__shfl(base, ld, 64));
-                const uint32_t r = (uint32_t)__popcll(tm & lt);
-                if (tw && r < got) tk = base + r;
-                RF_PROF(pr_sq += got;)
-            }
-        }
-        if (p == ~0u && tk != ~0u) {  // a taken entry: its pusher writes it right after reserving it
-            const unsigned long long e = RF_FLOW_GUARD(tk < a.e, 6, fc) ? ld_ag64(&a.rq[tk]) : 0ull;
-            if (tk >= a.e) tk = ~0u;
-            if ((uint32_t)(e >> 32) == a.epoch && RF_FLOW_GUARD((uint32_t)e < a.e, 7, fc)) {
-                tk = ~0u;
-                start((uint32_t)e);
-            }
-        }
-        RF_PROF(++pr_it;)
-        if (__all(p == ~0u)) {
-            // nothing to hash in the wave: advance the watermark, leave once
-            // it has passed the range, else back off (every idle wave polls
-            // the same few lines)
-            RF_PROF(++pr_idle;)
-            if ((idle_n & 3) == 0) flow_advance(a, fc);
-            uint32_t done = 0;
-            if (lane == 0) {
-                done = ld_ag(fc.lw) >= fc.R;
-                if (!done && __builtin_amdgcn_s_memrealtime() - t_start > kFlowTimeout) {
-                    if (atomicExch(fc.err, 1u) == 0u) {  // the first to give up records where the step stood
-                        const uint32_t p0 = ld_ag(fc.lw), l0 = fc.level_at(a, min(p0, fc.R - 1));
-                        fc.err[1] = p0;
-                        fc.err[2] = l0;
-                        fc.err[3] = ld_ag(&a.counts[l0]);
-                        uint32_t qs = 0, fs = 0;
-                        for (uint32_t k = 0; k < kFlowShards; ++k) {
-                            qs += ld_ag(&fc.Q[k * fc.lp + l0]);
-                            fs += ld_ag(&fc.F[k * fc.lp + l0]);
-                        }
-                        fc.err[4] = qs;
-                        fc.err[5] = fs;
-                        fc.err[6] = ld_ag(fc.tail);
-                        fc.err[7] = ld_ag(fc.head);
-                    }
-                    done = 1;
-                }
-            }
-            if (__builtin_amdgcn_readfirstlane(__shfl(done, 0, 64))) break;
-            ++idle_n;
-            __builtin_amdgcn_s_sleep(32);
-            continue;
-        }
-        idle_n = 0;
-        RF_PROF({
-            uint32_t nl = p != ~0u ? 1u : 0u;
-            for (int o = 32; o > 0; o >>= 1) nl += __shfl_xor(nl, o, 64);
-            pr_lanes += nl;
-        })
-        // 2. each lane's job (every hole from the slot table), then its fused
-        //    chain (the one hole's digest handed over in registers); the wave
-        //    runs until every lane's chain has ended
-        const bool had = p != ~0u;
-        {
-            uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
-            uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
-            if (had) {
-                const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * m1.x);  // (its own slot)
-                const uint4 olo = od[0], ohi = od[1];
-                MatCursorT<true> cur;
-                cur.begin(a, m0, ring);
-                ShaState st;
-                init_state(a, p, st);
-                for (uint32_t bb = 0; bb < cur.nb; ++bb) {
-                    uint32_t w[16];
-                    cur.block(a, bb, ring, w);
-                    sha256_compress(st, w);
-                }
-                RF_PROF(pr_blk += cur.nb;)
-                const bool ch = finish_job_ag(a, m1, st, olo, ohi);
-                const bool nf = m1.w != ~0u;
-                cb = m1.y;
-                cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);  // the fusion target's edge is the range's last
-                if (ch && nf) {
-                    nx = m1.w;
-                    fslot = m1.x;
-                    flo = make_uint4(bswap32(st.h[0]), bswap32(st.h[1]), bswap32(st.h[2]), bswap32(st.h[3]));
-                    fhi = make_uint4(bswap32(st.h[4]), bswap32(st.h[5]), bswap32(st.h[6]), bswap32(st.h[7]));
-                    nm0 = a.meta[2ull * nx];
-                    nm1 = a.meta[2ull * nx + 1];
-                }
-            }
-            flow_propagate(a, fc, cb, cz);
-            hashed += flow_chain(a, fc, ring, nx, nm0, nm1, fslot, flo, fhi);
-        }
-        // 3. the chain's end: the jobs it completes for (pend - 1 each; the
-        //    one that reaches 0 with its job queued and its watermark reached
-        //    starts in this lane next, any further one goes to the ready queue)
-        uint32_t next = ~0u;
-        vm_drain();  // the chains' digests (write-through) and queue counts first
-        if (had) {
-            for (uint32_t e = cr.x; e < cr.y; e += 4) {
-                uint2 o[4];
-                uint32_t r[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) o[u] = e + u < cr.y ? a.cout[e + u] : make_uint2(0, ~0u);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) r[u] = flow_level(a, o[u].y) ? atomicSub(&a.pend[o[u].x], 1u) : 0u;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (r[u] != 1u) continue;
-                    const uint32_t t = flow_trigger(a, fc, o[u].x);
-                    if (t == ~0u) continue;
-                    if (next == ~0u) next = t; else flow_push(a, fc, t);
-                }
-            }
-            atomicExch(&a.dirty[hd], 0u);
-        }
-        // finished (after every queue count and chain-out count of these
-        // chains), added once per level by the wave; the watermark is
-        // advanced by idle waves (the jobs that wait on it are few: only jobs
-        // with a producer above the range's first level)
-        vm_drain();
-        flow_wave_add(fc.F + fc.sh * fc.lp, had, hl);
-        p = ~0u;
-        if (next != ~0u) start(next);
-    }
-    count_fused(a, hashed);
-#ifdef RF_FLOW_PROFILE
-    for (int o = 32; o > 0; o >>= 1) {
-        pr_blk += __shfl_xor(pr_blk, o, 64);
-        pr_list += __shfl_xor(pr_list, o, 64);
-    }
-    if (lane == 0) {
-        uint32_t* w = fc.err + 16;  // (control-block words 112..)
-        atomicAdd(w + 0, pr_it);
-        atomicAdd(w + 1, pr_idle);
-        atomicAdd(w + 2, pr_lanes);
-        atomicAdd(w + 5, pr_list);
-        atomicAdd(w + 6, pr_sq);
-        atomicAdd(w + 7, pr_blk);
-        atomicAdd(w + 8, pr_slot);
-        atomicMax(w + 9, (uint32_t)((__builtin_amdgcn_s_memrealtime() - t_start) / 100));  // us
-        atomicAdd(w + 10, 1u);
-    }
-#endif
+    if (dbg_mode(a) != 16) count_fused(a, hashed);
 }
 
 // ---- the octo form: levels of few long jobs (GraphDev kLvlOct) ---------------
@@ -3390,8 +2813,8 @@ __global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __
                             int full) {
     // counts[L] + the fused parts: jobs hashed inside fused chains (never queued)
     for (uint32_t l = threadIdx.x; l < L; l += blockDim.x) {
-        uint32_t c = counts[l];  // (a flow-range level's single run)
-        for (uint32_t k = 0; k < kListShards; ++k) c += counts[list_shard_off(L) + k * flow_lp(L) + l];
+        uint32_t c = counts[l];  // (the A/B build's one cursor a level)
+        for (uint32_t k = 0; k < kListShards; ++k) c += counts[list_shard_off(L) + k * cursor_lp(L) + l];
         last[l] = full ? ls[l + 1] - ls[l] : c;
         counts[l] = 0;
     }
@@ -3439,21 +2862,6 @@ static uint32_t grid_mark(uint64_t items) {
 }
 
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
-// the flow fields of a launch's LevelArgs (this step's range, GraphDev flo; none: flo = ~0u)
-static void flow_args(const GraphDev& g, LevelArgs& a) {
-    a.cout_rng = g.cout_rng;
-    a.cout = g.cout;
-    a.jlv = g.jlv;
-    a.pend = g.pend;
-    a.dstart = g.dstart;
-    a.rq = g.rq;
-    a.dq = g.dq;
-    a.flo = g.flo;
-    a.fhi = g.fhi;
-    a.fsink = g.fsink;
-    a.epoch = g.epoch;
-}
-
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
@@ -3461,23 +2869,8 @@ static LevelArgs mark_level_args(const GraphDev& g) {
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
     a.stamps = g.stamps;                     // (k3_mark_slots: MarkStamp into row L)
 #endif
-    flow_args(g, a);  // a flow step's mark queues with chain-out counts (propagate)
     a.plan = g.plan;
     return a;
-}
-
-// The flow launch of a plain incremental step (GraphDev flo..fhi, fsink): the
-// step's first kernel (it zeroes the previous step's cursor half), one
-// resident round of 256-lane workgroups (three per CU: lanes that run out of
-// work wait on the ready queue, so no grid-stride is needed).
-hipError_t launch_graph_flow(const GraphDev& g, hipStream_t s, uint32_t* zero_counts) {
-    if (g.flo == ~0u || g.fhi - g.flo + 2 > kFlowMaxLev) return hipErrorInvalidValue;
-    LevelArgs a = mark_level_args(g);
-    a.zero_counts = zero_counts;
-    a.e = g.n_jobs;  // (k2_flow: the ready queue's capacity)
-    const uint32_t grid = std::max<uint32_t>(1u, (g.n_cu ? g.n_cu : 256u) * RF_FLOW_WAVES);
-    hipLaunchKernelGGL(k2_flow, dim3(grid), dim3(kLevelBlock), 0, s, a);
-    return hipGetLastError();
 }
 
 hipError_t launch_slot_plan(const GraphDev& g, hipStream_t s) {
@@ -3659,16 +3052,20 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             a.sink_wg = (uint32_t)std::min<uint64_t>((e - b + 63) / 64, wg_cap);
             wg = a.sink_wg + std::min<uint64_t>((n2 + nt - 1) / nt, 1024u);
         }
+#ifdef RF_DIAG  // (the measured-dead forms: the one-lane chain, the streamed hand-over)
         if (one_lane && wide)
             hipLaunchKernelGGL(k2_level_pc<3>, dim3((uint32_t)wg), dim3(192), pad, s, a);
         else if (one_lane)
             hipLaunchKernelGGL(k2_level_pc<2>, dim3((uint32_t)wg), dim3(128), pad, s, a);
-        else if (wide)
-            hipLaunchKernelGGL((k2_level_pl<3, false>), dim3((uint32_t)wg), dim3(256), pad, s, a);
-        else if (no_stream)
-            hipLaunchKernelGGL((k2_level_pl<2, false>), dim3((uint32_t)wg), dim3(192), pad, s, a);
-        else
+        else if (!no_stream && !wide)
             hipLaunchKernelGGL((k2_level_pl<2, true>), dim3((uint32_t)wg), dim3(192), pad, s, a);
+        else
+#endif
+        if (wide)
+            hipLaunchKernelGGL((k2_level_pl<3, false>), dim3((uint32_t)wg), dim3(256), pad, s, a);
+        else
+            hipLaunchKernelGGL((k2_level_pl<2, false>), dim3((uint32_t)wg), dim3(192), pad, s, a);
+        (void)no_stream;
         return hipGetLastError();
     }
     const uint32_t grid = grid_for(e - b, full ? 16384u : inc_cap);

@@ -60,6 +60,5 @@ def test_graph_entry_points_refuse_null_arguments():
     L = capi.lib()
     assert L.rf_graph_adopt_slots(None, None) == capi.RF_EINVAL
     assert len(L.rf_last_error()) > 0
-    assert L.rf_graph_set_flow(None, 0) == capi.RF_EINVAL
-    assert L.rf_graph_stats_get(None, None, 0) == capi.RF_EINVAL
+    assert L.rf_graph_stats_get(None, None) == capi.RF_EINVAL
     assert L.rf_graph_set_slots(None, None, None, 1) == capi.RF_EINVAL

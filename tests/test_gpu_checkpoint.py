@@ -240,8 +240,7 @@ def test_structurally_damaged_checkpoints_refused(ctx, tmp_path):
     g.close()
     raw = open(path, "rb").read()
     secs, _ = _sections(raw)
-    names = ["lvl_start", "inc_level", "ext2int", "meta", "holes", "cons_ptr", "cons_job", "tmpl", "slots", "mid",
-             "jlv", "cout_rng", "cout", "dstart"]
+    names = ["lvl_start", "inc_level", "ext2int", "meta", "holes", "cons_ptr", "cons_job", "tmpl", "slots", "mid"]
     sec = dict(zip(names, secs))
     lvl = np.frombuffer(raw, np.uint32, sec["lvl_start"][1] // 4, sec["lvl_start"][0])
     cons_ptr = np.frombuffer(raw, np.uint32, sec["cons_ptr"][1] // 4, sec["cons_ptr"][0])
@@ -292,20 +291,64 @@ def test_structurally_damaged_checkpoints_refused(ctx, tmp_path):
     bad = bytearray(raw)
     struct.pack_into("<I", bad, sec["holes"][0] + 8 * hole + 4, int(meta[j, 4]) ^ 1)
     refused(bytes(bad))
-    # 5. the flow step's structures: a chain-out edge naming a job outside
-    # its level, and a parking list too short for its wlev's jobs
-    cout = np.frombuffer(raw, np.uint32, sec["cout"][1] // 4, sec["cout"][0]).reshape(-1, 2)
-    assert len(cout)
-    x, y = int(cout[0, 0]), int(cout[0, 1])
-    other = next(lv for lv in range(len(lvl) - 1) if lv != y and not (lvl[lv] <= x < lvl[lv + 1]))
-    bad = bytearray(raw)
-    struct.pack_into("<I", bad, sec["cout"][0] + 4, other)
-    refused(bytes(bad))
-    dst = np.frombuffer(raw, np.uint32, sec["dstart"][1] // 4, sec["dstart"][0])
-    w = next(i for i in range(len(dst) - 1) if dst[i + 1] > dst[i])
-    bad = bytearray(raw)
-    struct.pack_into("<I", bad, sec["dstart"][0] + 4 * (w + 1), int(dst[w + 1]) - 1)
-    refused(bytes(bad))
+
+
+def test_older_checkpoint_versions_restore(ctx, tmp_path):
+    """ Version-1 checkpoints (round 4) share version 3's layout
+    and restore; a version-2 file (round 5) carries four more sections for
+    the since-removed flow step (jlv, cout_rng, cout and dstart, sized by the
+    header's n_cout), which a restore reads, checks against the checksums and
+    drops.  Both then step like the saved graph; an unknown version is
+    RF_EINVAL."""
+    import struct
+    dag = Dag1000(3, 4)
+    a = dag.arrays()
+    every = np.arange(a["n_slots"], dtype=np.uint32)
+    g = _load(ctx, dag)
+    g.recompute(full=True)
+    path = str(tmp_path / "s.ckpt")
+    g.save(path)
+    raw = open(path, "rb").read()
+    assert struct.unpack_from("<I", raw, 8)[0] == 3
+    secs, end = _sections(raw)
+    J, L = struct.unpack_from("<I", raw, 16)[0], struct.unpack_from("<I", raw, 24)[0]
+    n_cout = 5
+    extra = b""
+    for ln in (8 * J, 8 * J, 8 * n_cout, 4 * (L + 1)):
+        extra += struct.pack("<Q", ln) + bytes((i * 7) & 0xFF for i in range(ln))
+    v2 = bytearray(raw[:end] + extra + raw[end:])
+    struct.pack_into("<I", v2, 8, 2)
+    struct.pack_into("<Q", v2, 64, len(secs) + 4)
+    struct.pack_into("<Q", v2, 72, n_cout)
+    v1 = bytearray(raw)
+    struct.pack_into("<I", v1, 8, 1)
+    sl, _, nv = dag.change_set(0.2, seed=9)
+    g.set_slots(sl, nv)
+    g.recompute(full=False)
+    want = g.get_slots(every)
+    g.close()
+    for name, data in (("v1", v1), ("v2", v2)):
+        p = str(tmp_path / (name + ".ckpt"))
+        open(p, "wb").write(_rechecksum(bytes(data)))
+        r = capi.Graph.restore(ctx, p)
+        r.set_slots(sl, nv)
+        r.recompute(full=False)
+        assert (r.get_slots(every) == want).all(), name
+        r.close()
+    # a damaged dropped section still fails its checksum
+    bad = bytearray(_rechecksum(bytes(v2)))
+    bad[end + 8] ^= 1
+    p = str(tmp_path / "bad.ckpt")
+    open(p, "wb").write(bytes(bad))
+    with pytest.raises(capi.RfError) as e:
+        capi.Graph.restore(ctx, p)
+    assert e.value.code == capi.RF_EINTEGRITY
+    v4 = bytearray(raw)
+    struct.pack_into("<I", v4, 8, 4)
+    open(p, "wb").write(_rechecksum(bytes(v4)))
+    with pytest.raises(capi.RfError) as e:
+        capi.Graph.restore(ctx, p)
+    assert e.value.code == capi.RF_EINVAL
 
 
 def test_adopt_slots(ctx):

@@ -24,9 +24,7 @@ from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
 # pl: every level in the latency form; lf: every level in the throughput
 # form; auto: the library's per-level choice (the default thresholds)
-# flow: the library's choice with the flow step on (rf_graph_set_flow 1; off by default);
-# flow2: every launchable level in the flow launch (rf_graph_set_flow 2)
-FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None, "flow": None, "flow2": None}
+FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None}
 
 
 def run(ctx, name, g, slots, old, new, steps):
@@ -41,7 +39,6 @@ def run(ctx, name, g, slots, old, new, steps):
                 g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
             else:
                 g.set_forms(thr)
-            g.set_flow({"flow": 1, "flow2": 2}.get(form, 0))
             state = {"v": 0}
 
             def step():
@@ -66,13 +63,12 @@ def run(ctx, name, g, slots, old, new, steps):
                 step()
                 ctx.sync()
             st = g.stats()
-            print(name, form, "%.4f ms/step" % ms, "(flow %d, sinks on level %d, lf levels %d, octo levels %d, half levels %d, "
-                  "split %d)" % (st.last_flow, st.last_sink_attach if st.last_sink_attach != 0xFFFFFFFF else -1,
+            print(name, form, "%.4f ms/step" % ms, "(sinks on level %d, lf levels %d, octo levels %d, half levels %d, "
+                  "split %d)" % (st.last_sink_attach if st.last_sink_attach != 0xFFFFFFFF else -1,
                                  st.last_levels_lf, st.last_levels_oct, st.last_levels_half, st.split_block0),
                   file=sys.stderr, flush=True)
     res["slots_equal"] = bool(all((snaps["pl"] == snaps[f]).all() for f in snaps))
     g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
-    g.set_flow(0)
     for b in (d_slots, d_old, d_new):
         b.free()
     return res
