@@ -79,9 +79,14 @@ class Budget:
     def __init__(self, seconds):
         self.seconds = seconds
         self.skipped = []
+        self.dist = None  # set once the ranks are up: every rank then takes the same decision
 
-    def allow(self, name, est_s):
+    def allow(self, name, est_s, everyone=False):
+        """everyone: every rank calls this and must take the same decision
+        (the section holds collectives): the least time left on any rank."""
         left = self.seconds - (time.perf_counter() - T_START)
+        if everyone and self.dist is not None and self.dist.world > 1:
+            left = -self.dist.max(-left)
         if est_s > left:
             self.skipped.append({"section": name, "estimate_s": est_s, "left_s": round(left, 1)})
             log("SKIP %s: estimated %.0f s, %.0f s left in the budget" % (name, est_s, left))
@@ -267,8 +272,30 @@ def bench_sha(args, dist, ctx, budget):
     out = ctx.alloc(32 * len(lens))
     ctx.gen_fill(arena.ptr, d_offs.ptr, d_lens.ptr, len(lens), seed, arena_bytes)
     ctx.sync()
+    # The all-host plan (every file on the SHA-NI leg, fed from HBM): measured
+    # beside the hybrid, and the run that calibrates the planner's host-leg
+    # feed rate (rf_host_link) before the hybrid plan is made
+    all_host = None
+    link0 = ctx.host_link()
+    if ctx.host_info()[0] and "allhost" not in args.skip:
+        pa = ctx.sha_plan(offs, lens, capi.RF_SHA_ALL_HOST)
+        runs = []
+        for _ in range(3):  # the first one warms the pool and pins the staging
+            t0 = time.perf_counter()
+            pa.run(arena.ptr, out.ptr)
+            sa = pa.stats()
+            runs.append(((time.perf_counter() - t0) * 1e3, sa.last_ms_host))
+        ms_a = float(np.mean([r[0] for r in runs[1:]]))
+        all_host = {"gbps": round(float(lens.sum()) / (ms_a * 1e-3) / 1e9, 3), "ms": round(ms_a, 2),
+                    "host_leg_ms": [round(r[1], 2) for r in runs[1:]], "threads": int(sa.host_threads),
+                    "what": "RF_SHA_ALL_HOST: every file on the host leg (SHA-NI threads fed D2H from HBM), "
+                            "mean of 2 runs after one warm-up"}
+        pa.close()
+    link1 = ctx.host_link()
     plan = ctx.sha_plan(offs, lens, 0)
     st = plan.stats()
+    log("C2: planner's host feed %.1f GB/s (%s; before: %.1f GB/s %s)"
+        % (link1[0] / 1e9, "measured" if link1[1] else "assumed", link0[0] / 1e9, "measured" if link0[1] else "assumed"))
     log("C2: %d files, %.1f GiB, largest %.2f GiB: %d on the host leg (%.1f GiB, %d threads), %d duo, %d lane"
         % (len(lens), lens.sum() / GiB, lens.max() / GiB, st.n_host, st.host_bytes / GiB, st.host_threads,
            st.n_solo, len(lens) - st.n_host - st.n_solo))
@@ -352,8 +379,17 @@ def bench_sha(args, dist, ctx, budget):
                    if legs else None,
                    "note": "value is the whole hybrid step (CPU SHA-NI host leg + GPU kernels, split by the K1 "
                            "planner's makespan model); the GPU-only rate of the same set is gpu_only.gbps"}
+    rank_gbps = float(lens.sum()) / (step_ms * 1e-3) / 1e9
+    if all_host:
+        all_host["hybrid_minus_all_host_gbps"] = round(rank_gbps - all_host["gbps"], 3)
+        all_host["hybrid_ge_all_host"] = bool(rank_gbps >= all_host["gbps"])
+        all_host["planner_feed_gbps"] = round(link1[0] / 1e9, 3)
+        all_host["planner_feed_measured"] = bool(link1[1])
+        all_host["planner_picked_all_host"] = bool(h == len(lens))
+        log("  all-host: %.1f ms (%.2f GB/s); hybrid %.1f ms (%.2f GB/s): the GPU legs add %+.2f GB/s"
+            % (all_host["ms"], all_host["gbps"], step_ms, rank_gbps, rank_gbps - all_host["gbps"]))
     res = dict(value=bytes_all / t / 1e9, ms_per_step=step_ms, roofline=roof, roofline_gpu_legs=gpu_roofs,
-               host_leg=host_leg, composition=composition,
+               host_leg=host_leg, composition=composition, all_host=all_host,
                files=int(len(lens)), bytes_per_gpu=int(lens.sum()), workload=workload, glob=glob_info,
                split={"host": h, "duo": k, "lanes": int(len(lane_ids))},
                step_ms={kk: round(float(np.mean(v)), 3) for kk, v in rec.items()})
@@ -875,21 +911,31 @@ def bench_piece(args, ctx, ranks, n1_ms, duo_us=None, per_sample=False):
                     % ("per-sample-root (SURVEY C3/C4)" if per_sample else "strong Merge-tree", ranks)}
 
 
-def bench_persample(args, ctx, duo_us=None):
+def bench_persample(args, dist, ctx, duo_us=None):
     """SURVEY §8(d) C3/C4's DAG as written: 8 x c4_samples samples of the
-    1000align DAG (100M nodes) with per-sample roots and no Merge tree, on
-    one GPU (N = 1), and rank 0's piece of it at 8 ranks -- the layout a
-    sample-partitioned run needs no exchange for.  Reported beside the bench's
-    Merge-tree layout so the 8-GPU projection is judged against what each
-    layout permits."""
+    1000align DAG (100M nodes) with per-sample roots and no Merge tree --
+    /root/reference/doc/1000align/1000align.rf:37-47 runs one module per
+    sample, so the samples are independent.  Strong scaling like
+    bench_dag100m: N ranks hold S x 8 / N consecutive samples each (the
+    shared reference-index chain replicated), the global change set (1 % of
+    the global leaf File IDs) restricted to each rank's slice, and NO
+    exchange -- the boundary is empty.  At N = 1 also rank 0's piece at 8
+    ranks (bench_piece), the 8-GPU projection; at N > 1 the measured step is
+    the max over ranks.  Reported beside the Merge-tree layout at every N."""
     S, P, nparts = args.c4_samples, args.dag_pairs, args.c4_parts
+    world, rank = dist.world, dist.rank
+    if (S * nparts) % world:
+        raise SystemExit("the per-sample layout's %d samples do not split over %d ranks" % (S * nparts, world))
+    s_rank = S * nparts // world
     t0 = time.perf_counter()
-    dag = Dag1000(S * nparts, P)
+    dag = Dag1000(s_rank, P, sample0=rank * s_rank)
     a = dag.arrays()
     g = capi.Graph.from_arrays(ctx, a)
     g.set_slots(dag.file_slots, dag.leaf_ids)
     g.recompute(True)
-    slots, old, new = dag.change_set(0.01)
+    slots, old, new = dag.change_set(0.01, n_global=2 * P * S * nparts)
+    if not len(slots):
+        raise SystemExit("rank %d: empty change set" % rank)
     d_slots, d_old, d_new = ctx.upload(slots), ctx.upload(old), ctx.upload(new)
     every = np.arange(a["n_slots"], dtype=np.uint32)
     full = g.get_slots(every)
@@ -901,39 +947,36 @@ def bench_persample(args, ctx, duo_us=None):
         g.set_slots_device(d_slots.ptr, ver.ptr, len(slots), ctx.stream)
         g.recompute_async(False, ctx.stream)
 
-    for _ in range(2):
-        step()
-    ctx.sync()
-    t1 = time.perf_counter()
-    for _ in range(args.dag_steps):
-        step()
-    ctx.sync()
-    ms = (time.perf_counter() - t1) / args.dag_steps * 1e3
+    t = timed_steps(dist, ctx, step, args.dag_steps, 2)
+    ms = t / args.dag_steps * 1e3
     if state["v"] == 1:
         step()
     ctx.sync()
-    same = bool((g.get_slots(every) == full).all())
-    st = g.stats()
+    same = dist.max(0.0 if (g.get_slots(every) == full).all() else 1.0) == 0.0
     for b in (d_slots, d_old, d_new):
         b.free()
     g.close()
     del full
     f = np.asarray(slots, dtype=np.int64)
     pairs, samples = np.unique(f // 2), np.unique(f // 2 // P)
-    n_dirty = int(2 * len(f) + 10 * len(pairs) + 5 * len(samples))  # Val + Coerce a file, the pair chain, the tail
-    log("  per-sample-root layout (SURVEY C3/C4): %d nodes, %.4f ms/step at N = 1, built+loaded in %.1f s"
-        % (dag.n_nodes, ms, time.perf_counter() - t0))
+    n_dirty_l = int(2 * len(f) + 10 * len(pairs) + 5 * len(samples))  # Val + Coerce a file, the pair chain, the tail
+    n_dirty = int(dist.sum(n_dirty_l))
+    nodes = int(dist.sum(dag.n_nodes - (3 if rank else 0)))  # (the replicated ref chain counted once)
+    crit = int(dist.max(float(dag.critical_path(slots))))
+    log("  per-sample-root layout (SURVEY C3/C4): %d nodes over %d rank(s), %.4f ms/step, built+loaded in %.1f s"
+        % (nodes, world, ms, time.perf_counter() - t0))
     res = {"workload": "SURVEY §8(d) C3/C4 as written: 1000align DAG of %d samples x P=%d (%d nodes), per-sample "
-                       "roots, no Merge tree or global root; 1%% of leaf File IDs toggled per step" % (S * nparts, P,
-                                                                                                   dag.n_nodes),
-           "nodes": int(dag.n_nodes), "ms_per_step": round(ms, 4), "incremental_equals_full": same,
+                       "roots, no Merge tree or global root, %d samples per rank over %d rank(s), no exchange; 1%% of "
+                       "the global leaf File IDs toggled per step" % (S * nparts, P, nodes, s_rank, world),
+           "nodes": nodes, "ranks": world, "ms_per_step": round(ms, 4), "incremental_equals_full": same,
            "dirty_nodes_per_step": n_dirty,
            "mnodes_per_s": round(n_dirty / (ms * 1e-3) / 1e6, 1),
-           "critical_path_blocks": int(dag.critical_path(slots))}
+           "critical_path_blocks": crit}
     del dag, a
-    pc8 = bench_piece(args, ctx, 8, ms, duo_us, per_sample=True)
-    res["piece_8"] = pc8
-    res["piece_ms_8"], res["projected_speedup_8"] = pc8["ms_per_step"], pc8["projected_speedup"]
+    if world == 1:
+        pc8 = bench_piece(args, ctx, 8, ms, duo_us, per_sample=True)
+        res["piece_8"] = pc8
+        res["piece_ms_8"], res["projected_speedup_8"] = pc8["ms_per_step"], pc8["projected_speedup"]
     return res
 
 
@@ -1169,7 +1212,7 @@ def bench_probe(args, dist, ctx, budget):
     res["_gather_ceiling"] = ceil
     # SURVEY §8(d) C5 second case: n = 1.2e9 keys -> m = 17.25 G bits (2.0 GiB):
     # larger than the 256 MB MALL, so the gathers go to HBM
-    if args.probe_big_keys and budget.allow("probe_2gib_filter", 25):
+    if args.probe_big_keys and budget.allow("probe_2gib_filter", 25, everyone=True):
         rb, hb = probe_case(ctx, dist, args.probe_big_keys, n_probe, args.probe_steps, 0x5EED0015 + dist.rank)
         for x in (hb["keys"], hb["out"]) + hb["extra"]:
             x.free()
@@ -1372,13 +1415,13 @@ def cpu_threads():
 def cpu_baseline(args, sha, dag_res, budget):
     """The headline's CPU leg: the oracle's scalar C port (~Go 1.9/1.10 speed
     class, kind "port") on a bounded sample of configs[1] -- the value; beside
-    it OpenSSL SHA-256 (hashlib; SHA-NI, what Go >= 1.21 crypto/sha256 uses)
-    over the WHOLE set on min(60, CPU share) threads, LPT order; configs[0];
+    it OpenSSL SHA-256 (libcrypto from C on native threads, oracle/
+    baseline_openssl.c; SHA-NI, what Go >= 1.21 crypto/sha256 uses) over the
+    WHOLE set on min(60, CPU share) threads, LPT order; configs[0];
     configs[2] on its own DAG and change set (1 thread: Canonicalize is
     serial)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import reflow_oracle as O  # the oracle: cpu_baseline leg only
-    from concurrent.futures import ThreadPoolExecutor
     L = O.lib()
     threads = cpu_threads()
     lens, offs = sha["_lens"], sha["_offs"]
@@ -1387,20 +1430,17 @@ def cpu_baseline(args, sha, dag_res, budget):
     t0 = time.perf_counter()
     host = sha["_arena"].to_numpy()
     log("cpu: copied the %.1f GiB set to host memory in %.1f s" % (host.nbytes / GiB, time.perf_counter() - t0))
-    mv = memoryview(host)
-    order = np.argsort(-lens.astype(np.int64), kind="stable")
-
-    def one(i):
-        o, ln = int(offs[i]), int(lens[i])
-        return hashlib.sha256(mv[o:o + ln]).digest()
-
+    order = np.ascontiguousarray(np.argsort(-lens.astype(np.int64), kind="stable").astype(np.uint64))
+    a_offs, a_lens = np.ascontiguousarray(offs, dtype=np.uint64), np.ascontiguousarray(lens, dtype=np.uint64)
+    dig = np.zeros((len(lens), 32), dtype=np.uint8)
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        dig = list(ex.map(one, order.tolist()))
+    rc = L.orc_openssl_sha256_batch(host.ctypes.data, a_offs.ctypes.data, a_lens.ctypes.data, order.ctypes.data,
+                                    len(lens), dig.ctypes.data, threads)
     dt = time.perf_counter() - t0
-    ok = all(d == sha["_digests"][int(i)].tobytes() for d, i in zip(dig, order))
+    ok = rc == 0 and bool((dig == sha["_digests"]).all())
     res["openssl"] = {"value": float(lens.sum()) / dt / 1e9, "unit": "GB/s", "kind": "library", "cores": threads,
-                      "what": "SHA-256 of every configs[1] file, hashlib/OpenSSL (SHA-NI), LPT order",
+                      "what": "SHA-256 of every configs[1] file, OpenSSL libcrypto (SHA-NI) on %d native threads "
+                              "taking files largest first from one queue (oracle/baseline_openssl.c)" % threads,
                       "sample": "the whole configs[1] set (%d files, %.1f GiB)" % (len(lens), lens.sum() / GiB),
                       "seconds": dt, "gpu_digests_match": ok}
     # scalar port on a bounded sample (files in generation order up to the budget)
@@ -1429,7 +1469,7 @@ def cpu_baseline(args, sha, dag_res, budget):
                 "value_openssl": res["openssl"]["value"],
                 "note": "value = the scalar port (Go 1.9/1.10 speed class); value_openssl = OpenSSL SHA-NI on the "
                         "same %d threads over the whole set" % threads})
-    del mv, host
+    del host
     # configs[0]: port and OpenSSL
     c1l = np.full(C1_N, C1_LEN, dtype=np.uint64)
     c1o, c1t = arena_layout(c1l, align=64)
@@ -1439,15 +1479,23 @@ def cpu_baseline(args, sha, dag_res, budget):
     t0 = time.perf_counter()
     L.orc_sha256_batch(c1a.ctypes.data, c1o.ctypes.data, c1l.ctypes.data, C1_N, c1out.ctypes.data, threads)
     c1_port = time.perf_counter() - t0
-    c1mv = memoryview(c1a)
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(lambda i: hashlib.sha256(c1mv[int(c1o[i]):int(c1o[i]) + C1_LEN]).digest(), range(C1_N)))
-    c1_ssl = time.perf_counter() - t0
+    c1ssl = np.zeros((C1_N, 32), dtype=np.uint8)
+    c1o64 = np.ascontiguousarray(c1o, dtype=np.uint64)
+    best = None
+    for _ in range(3):  # (1 GiB takes ~30 ms on 16 threads: the best of three)
+        t0 = time.perf_counter()
+        rc = L.orc_openssl_sha256_batch(c1a.ctypes.data, c1o64.ctypes.data, c1l.ctypes.data, None, C1_N,
+                                        c1ssl.ctypes.data, threads)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    c1_ssl = best
     res["c1"] = {"sample": "configs[0] in full: 4096 x 256 KiB", "port_ms": c1_port * 1e3,
                  "port_gbps": C1_N * C1_LEN / c1_port / 1e9, "openssl_ms": c1_ssl * 1e3,
-                 "openssl_gbps": C1_N * C1_LEN / c1_ssl / 1e9, "cores": threads}
-    del c1mv, c1a
+                 "openssl_gbps": C1_N * C1_LEN / c1_ssl / 1e9, "cores": threads,
+                 "openssl_equals_port": rc == 0 and bool((c1ssl == c1out).all()),
+                 "openssl_what": "OpenSSL libcrypto on %d native threads, one shared queue (oracle/baseline_openssl.c; "
+                                 "best of 3)" % threads}
+    del c1a
     # configs[2] on the CPU: the same 10M-node DAG and change set, 1 thread
     c = (dag_res or {}).get("_cpu")
     if c is not None and budget.allow("cpu_dag", 40):
@@ -1567,6 +1615,7 @@ def main():
     budget = Budget(args.budget_s)
 
     dist = Dist(args.gpus)
+    budget.dist = dist
     # the product lowering leg runs first, in a child process of its own,
     # before this process touches the GPU (N = 1 only)
     lowering = None
@@ -1622,11 +1671,11 @@ def main():
                           gpu_legs_ms=round(float(r[5]), 2),
                           gpu_legs_gbps=round(r[2] / (r[5] * 1e-3) / 1e9, 3) if r[5] else None)
                      for i, r in enumerate(np.frombuffer(dist.all_gather_bytes(row), np.float64).reshape(-1, 6))]
-    c1 = bench_c1(args, dist, ctx, budget) if "c1" not in args.skip and budget.allow("c1", 15) else None
+    c1 = bench_c1(args, dist, ctx, budget) if "c1" not in args.skip and budget.allow("c1", 15, everyone=True) else None
     dag_res = dag100 = None
     if dist.world == 1 and "dag" not in args.skip and budget.allow("dag", 30):
         dag_res = bench_dag(args, dist, ctx, budget)
-    if "dag100m" not in args.skip and budget.allow("dag100m", 150):
+    if "dag100m" not in args.skip and budget.allow("dag100m", 150, everyone=True):
         dag100 = bench_dag100m(args, dist, ctx, comm, budget)
         duo_us = next((r.get("us_per_chain_block") for r in sha["roofline_gpu_legs"]
                        if r.get("kernel") == "k1_sha256_duo"), None)
@@ -1634,10 +1683,11 @@ def main():
             pc8 = bench_piece(args, ctx, 8, dag100["ms_per_step"], duo_us)
             dag100["piece_8"] = pc8
             dag100["piece_ms_8"], dag100["projected_speedup_8"] = pc8["ms_per_step"], pc8["projected_speedup"]
-        # SURVEY C3/C4 as written (per-sample roots): its N = 1 step and 8-rank piece
-        if dist.world == 1 and "persample" not in args.skip and budget.allow("persample", 60):
-            dag100["per_sample_layout"] = bench_persample(args, ctx, duo_us)
-    probe = bench_probe(args, dist, ctx, budget) if "probe" not in args.skip and budget.allow("probe", 30) else None
+        # SURVEY C3/C4 as written (per-sample roots) at every N; at N = 1 its 8-rank piece too
+        if "persample" not in args.skip and budget.allow("persample", 60, everyone=True):
+            dag100["per_sample_layout"] = bench_persample(args, dist, ctx, duo_us)
+    probe = bench_probe(args, dist, ctx, budget) if "probe" not in args.skip and budget.allow("probe", 30, everyone=True) \
+        else None
     cpu = None
     if dist.rank == 0 and dist.world == 1 and "cpu" not in args.skip and budget.allow("cpu", 60):
         cpu = cpu_baseline(args, sha, dag_res, budget)
@@ -1670,6 +1720,10 @@ def main():
             # the metric's other halves beside value: the
             # GPU-only SHA rate of the same set, and the DAG legs' dirty nodes/s
             "gpu_only_gbps": round(sha["gpu_only"]["gbps"], 4) if sha.get("gpu_only") else None,
+            # the same set with every file on the host leg (measured), and
+            # what the GPU legs add to one rank's rate over it
+            "all_host_gbps": (sha["all_host"] or {}).get("gbps"),
+            "gpu_marginal_gbps": (sha["all_host"] or {}).get("hybrid_minus_all_host_gbps"),
             "incremental_mnodes_per_s": round(dag_res["mnodes_per_s"], 1) if dag_res else None,
             "incremental_100m_mnodes_per_s": round(dag100["mnodes_per_s"], 1) if dag100 else None,
             "valu_measured_tops": round(valu_tops, 2) if valu_tops else None,
@@ -1700,11 +1754,43 @@ def main():
                        "elapsed_s": round(time.perf_counter() - T_START, 1)},
         }
         with_measured_valu(line, valu_tops)
+        line["summary"] = run_summary(line)  # last: the driver's record keeps the line's tail
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(line) + "\n").encode())
     if comm is not None:
         comm.close()
     ctx.close()
+
+
+def run_summary(line):
+    """The DAG and probe results in a few numbers, written at the END of the
+    line: the driver's record keeps only the line's tail."""
+    def g(d, *ks):
+        for k in ks:
+            if not isinstance(d, dict):
+                return None
+            d = d.get(k)
+        return d
+    inc, big = line.get("incremental"), line.get("incremental_100m")
+    ps = g(big, "per_sample_layout")
+    out = {
+        "sha_gbps": line.get("value"), "sha_all_host_gbps": line.get("all_host_gbps"),
+        "sha_gpu_only_gbps": line.get("gpu_only_gbps"), "sha_gpu_marginal_gbps": line.get("gpu_marginal_gbps"),
+        "configs2_ms_per_step": g(inc, "ms_per_step"), "configs2_device_ms_per_step": g(inc, "device_ms_per_step"),
+        "configs2_mnodes_per_s": g(inc, "mnodes_per_s"),
+        "configs2_latency_frac_of_issue_floor": g(inc, "roofline_latency", "frac_of_issue_floor"),
+        "dag100m_ms_per_step": g(big, "ms_per_step"), "dag100m_mnodes_per_s": g(big, "mnodes_per_s"),
+        "dag100m_frac_of_measured_valu": g(big, "roofline_incremental", "frac_of_measured_valu"),
+        "dag100m_dirty_blocks_per_step": g(big, "dirty_blocks_per_step"),
+        "merge_tree_piece8_ms": g(big, "piece_8", "ms_per_step"),
+        "merge_tree_projected_speedup_8": g(big, "piece_8", "projected_speedup"),
+        "per_sample_ms_per_step": g(ps, "ms_per_step"), "per_sample_mnodes_per_s": g(ps, "mnodes_per_s"),
+        "per_sample_piece8_ms": g(ps, "piece_8", "ms_per_step"),
+        "per_sample_projected_speedup_8": g(ps, "piece_8", "projected_speedup"),
+        "probe_gprobes_per_s": g(line.get("probe"), "gprobes_per_s"),
+        "n_gpus": line.get("n_gpus"), "parity_all": g(line.get("parity"), "all"),
+    }
+    return {k: v for k, v in out.items() if v is not None}
 
 
 if __name__ == "__main__":

@@ -84,6 +84,13 @@ int rf_host_info(rf_ctx *ctx, int *threads, double *core_bytes_per_s, int *sha_e
  * thread's measured rate at that interleave (bytes/s) -- the per-thread peak
  * bench.py prices the host leg against. */
 int rf_host_rate(rf_ctx *ctx, int *ways, double *thread_bytes_per_s);
+/* The feed rate (bytes/s) the K1 planner prices the host leg's HBM-resident
+ * bytes at: measured by the last plan run on this context whose host leg took
+ * >= 1 GiB at the current width (*measured = 1; the leg's bytes over its wall
+ * time, D2H copies and SHA-NI threads together), else the built-in PCIe Gen5
+ * estimate (52 GB/s, *measured = 0).  Plans created after a measurement use
+ * it: a caller calibrates with one RF_SHA_ALL_HOST run, then plans the split. */
+int rf_host_link(rf_ctx *ctx, double *bytes_per_s, int *measured);
 
 /* ---- device memory and timing -------------------------------------------
  * The engine owns its HIP runtime; callers (the cgo shim, bench.py, tests)

@@ -46,7 +46,7 @@ EXPORTS = [
     "rf_dedup_digests", "rf_dedup_digests_device", "rf_assoc_lookup",
     "rf_assoc_new", "rf_assoc_destroy", "rf_assoc_put", "rf_assoc_get", "rf_assoc_get_device",
     "rf_assoc_get_abbrev", "rf_assoc_stats", "rf_assoc_put_device",
-    "rf_set_host_threads", "rf_host_info", "rf_host_rate", "rf_assoc_repair",
+    "rf_set_host_threads", "rf_host_info", "rf_host_rate", "rf_host_link", "rf_assoc_repair",
     "rf_sha_streams_open", "rf_sha_streams_close", "rf_sha_streams_write", "rf_sha_streams_digest",
     "rf_sha_streams_len", "rf_sha_streams_verify", "rf_sha256_verify", "rf_flow_dirty",
     "rf_coalescer_open", "rf_coalescer_close", "rf_coalesce_sha256", "rf_coalesce_probe", "rf_coalesce_assoc_get",
@@ -354,6 +354,7 @@ def lib():
             "rf_graph_piece_desc": ([vp, vp], i32), "rf_graph_piece_part": ([vp, vp], i32),
             "rf_graph_piece_slots": ([vp, vp, vp], i32),
             "rf_host_info": ([vp, vp, vp, vp], i32), "rf_host_rate": ([vp, vp, vp], i32),
+            "rf_host_link": ([vp, vp, vp], i32),
             "rf_bloom_parse_binary": ([vp, u64, vp, vp, vp, vp, u64, vp], i32),
             "rf_bloom_parse_json": ([vp, u64, vp, vp, vp, vp, u64, vp], i32),
             "rf_bloom_format_binary": ([u64, u64, u64, vp, u64, vp, u64, vp], i32),
@@ -413,6 +414,13 @@ class Context:
         t, r, e = ctypes.c_int(0), ctypes.c_double(0), ctypes.c_int(0)
         _check(lib().rf_host_info(self._h, ctypes.byref(t), ctypes.byref(r), ctypes.byref(e)))
         return t.value, r.value, bool(e.value)
+
+    def host_link(self):
+        """rf_host_link: (bytes/s the planner prices the host leg's HBM feed at,
+        whether a run on this context measured it)."""
+        r, m = ctypes.c_double(0), ctypes.c_int(0)
+        _check(lib().rf_host_link(self._h, ctypes.byref(r), ctypes.byref(m)))
+        return r.value, bool(m.value)
 
     def host_rate(self):
         """(chains per host-leg thread, one thread's measured bytes/s at that interleave)."""

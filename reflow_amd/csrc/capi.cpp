@@ -130,6 +130,16 @@ extern "C" int rf_host_rate(rf_ctx* ctx, int* ways, double* thread_bytes_per_s) 
     return RF_OK;
 }
 
+extern "C" int rf_host_link(rf_ctx* ctx, double* bytes_per_s, int* measured) {
+    ARG(ctx, "null ctx");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const unsigned threads = ctx_host_threads(ctx);
+    const bool m = ctx->host_link_bps > 0 && ctx->host_link_threads == threads;
+    if (bytes_per_s) *bytes_per_s = host_link_rate(ctx, threads);
+    if (measured) *measured = m ? 1 : 0;
+    return RF_OK;
+}
+
 extern "C" int rf_host_info(rf_ctx* ctx, int* threads, double* core_bytes_per_s, int* sha_ext) {
     ARG(ctx, "null ctx");
     if (threads) *threads = (int)ctx_host_threads(ctx);
@@ -362,8 +372,23 @@ struct HostModel {
 };
 
 // Sustained D2H rate the host leg's copies reach on the MI355X box (PCIe
-// Gen5 x16; tools/host_leg_probe.py all-host runs).
+// Gen5 x16; tools/host_leg_probe.py all-host runs) -- the
+// planner's assumption until a run measures the leg (rf_ctx::host_link_bps):
+// round 5's model kept three duo chains (1,314 ms) beside a host leg that
+// finished in 1,266 ms at 53.3 GB/s, because this figure and the 2 % margin
+// priced moving them to the host above the chains.
 static constexpr double kD2HLink = 52e9;
+static constexpr uint64_t kLinkCalibBytes = 1ull << 30;  // a host leg this large calibrates the link
+
+// The feed rate the planner prices the host leg's HBM-resident bytes at:
+// the context's last measurement at the current width (a whole leg's bytes
+// over its wall time: the D2H copies and the SHA-NI threads together), else
+// kD2HLink.  (caller holds ctx->mu)
+static double host_link_rate(const rf_ctx* ctx, unsigned threads) {
+    if (ctx->host_link_bps > 0 && ctx->host_link_threads == threads)
+        return std::min(std::max(ctx->host_link_bps, 0.25 * kD2HLink), 4.0 * kD2HLink);
+    return kD2HLink;
+}
 
 // Which messages go to the host leg (the h largest) and how the rest split
 // over the GPU kernels.  The host leg's makespan for the h largest messages
@@ -478,7 +503,7 @@ static int plan_setup(rf_ctx* ctx, rf_sha_plan* p, const uint64_t* offs, const u
     const int ways = host_ways();
     hm.slots = threads * (unsigned)ways;
     hm.rate = threads ? host_sha_rate(ways) / ways : 0.0;
-    hm.link = host_resident ? 0.0 : kD2HLink;
+    hm.link = host_resident ? 0.0 : host_link_rate(ctx, threads);
     p->ctx = ctx;
     p->n = n;
     p->ran = false;
@@ -629,6 +654,10 @@ static int plan_run_locked(rf_sha_plan* p, const void* d_arena, void* d_out, hip
         if (ctx_lock) ctx_lock->lock();
         if (!ok) return fail(RF_EDEVICE, "%s", err.c_str());
         p->last_ms_host = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (!h_arena && p->st.host_bytes >= kLinkCalibBytes && p->last_ms_host > 0) {  // calibrate the link
+            p->ctx->host_link_bps = (double)p->st.host_bytes / (p->last_ms_host * 1e-3);
+            p->ctx->host_link_threads = (unsigned)pool->size();
+        }
         HIPC(hipMemcpyAsync(p->d_host_dig.p, p->h_host_dig.p, 32ull * p->n_host, hipMemcpyHostToDevice, s));
         HIPC(hipEventRecord(p->e_hcopy, s));
         p->hcopy_pending = true;

@@ -119,6 +119,11 @@ struct rf_ctx {
     // context mutex released keeps its pool alive across rf_set_host_threads
     std::shared_ptr<HostPool> pool;
     StreamScratch sc_dedup, sc_collect;
+    // the host leg's measured feed rate (bytes/s) from HBM-resident messages:
+    // the last run of a plan whose host leg took >= 1 GiB (0: none yet; the
+    // planner then assumes kD2HLink), and the width it ran at
+    double host_link_bps = 0.0;
+    unsigned host_link_threads = 0;
 };
 
 // Host-leg width of a context (0 when the CPU has no SHA extensions).
