@@ -130,16 +130,6 @@ extern "C" int rf_host_rate(rf_ctx* ctx, int* ways, double* thread_bytes_per_s) 
     return RF_OK;
 }
 
-extern "C" int rf_host_link(rf_ctx* ctx, double* bytes_per_s, int* measured) {
-    ARG(ctx, "null ctx");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    const unsigned threads = ctx_host_threads(ctx);
-    const bool m = ctx->host_link_bps > 0 && ctx->host_link_threads == threads;
-    if (bytes_per_s) *bytes_per_s = host_link_rate(ctx, threads);
-    if (measured) *measured = m ? 1 : 0;
-    return RF_OK;
-}
-
 extern "C" int rf_host_info(rf_ctx* ctx, int* threads, double* core_bytes_per_s, int* sha_ext) {
     ARG(ctx, "null ctx");
     if (threads) *threads = (int)ctx_host_threads(ctx);
@@ -388,6 +378,16 @@ static double host_link_rate(const rf_ctx* ctx, unsigned threads) {
     if (ctx->host_link_bps > 0 && ctx->host_link_threads == threads)
         return std::min(std::max(ctx->host_link_bps, 0.25 * kD2HLink), 4.0 * kD2HLink);
     return kD2HLink;
+}
+
+extern "C" int rf_host_link(rf_ctx* ctx, double* bytes_per_s, int* measured) {
+    ARG(ctx, "null ctx");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const unsigned threads = ctx_host_threads(ctx);
+    const bool m = ctx->host_link_bps > 0 && ctx->host_link_threads == threads;
+    if (bytes_per_s) *bytes_per_s = host_link_rate(ctx, threads);
+    if (measured) *measured = m ? 1 : 0;
+    return RF_OK;
 }
 
 // Which messages go to the host leg (the h largest) and how the rest split
