@@ -1260,7 +1260,7 @@ static int graph_build_memo(rf_graph* gr) {
     G.cons_hb = gr->b_cons_hb.as<uint8_t>();
     G.memo_base = nullptr;
     G.memo_entries = G.memo_jobs = 0;
-    static const bool memo_on = [] {
+    const bool memo_on = [] {  // (read per load, like the form thresholds: A/B in one process)
         const char* v = getenv("RF_K2_MEMO");
         return !(v && atoi(v) == 0);
     }();
