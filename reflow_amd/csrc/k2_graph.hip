@@ -104,6 +104,7 @@ struct LevelArgs {
     const uint8_t* __restrict__ cons_hb = nullptr;
     uint32_t memo_sort = 0;  // k2_level_lf: order each workgroup's jobs by the blocks they will hash
     unsigned long long* memo_skip = nullptr;
+    uint32_t n_cu = 256;  // the device's CUs (memo_order's direction by round of resident workgroups)
 };
 // The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
 __device__ __forceinline__ uint32_t dbg_mode(const LevelArgs& a) { return kDiag ? dbg_mode(a) : 0u; }
@@ -2457,11 +2458,15 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
 #define RF_LF_WAVES 3  // (A/B builds: waves a SIMD the throughput form is compiled for)
 #endif
 // A memo level's workgroup orders its 256 list entries by the blocks each
-// job will hash (a memo job from its resume block), longest first, so a
-// wave's lanes run about equally long -- a lane-per-job wave lasts as long as
-// its longest lane, and resume points differ job to job.  Counting sort in
-// LDS (64 bins); entries without a job go last.  Called by every thread.
-__device__ __forceinline__ uint32_t memo_order(const LevelArgs& a, uint32_t ii, uint32_t* s_bin, uint32_t* s_pos) {
+// job will hash (a memo job from its resume block), so a wave's lanes run
+// about equally long -- a lane-per-job wave lasts as long as its longest
+// lane, and resume points differ job to job.  Counting sort in LDS (64
+// bins); entries without a job go last.  The direction alternates by round
+// of one workgroup a CU (desc: longest first): wave w of a workgroup runs on
+// SIMD w of its CU, so the two workgroups a CU holds put their longest and
+// shortest waves on one SIMD instead of both longest.  Called by every thread.
+__device__ __forceinline__ uint32_t memo_order(const LevelArgs& a, uint32_t ii, uint32_t* s_bin, uint32_t* s_pos,
+                                               bool desc) {
     uint32_t key = 0;
     if (ii != ~0u) {
         const uint32_t p = a.list[ii], nb = a.lmeta[2ull * ii].y;
@@ -2470,7 +2475,7 @@ __device__ __forceinline__ uint32_t memo_order(const LevelArgs& a, uint32_t ii, 
         if (mb != ~0u && a.memo_valid[p]) b0 = min(first_changed_block(a.dirty[p]), nb - 1);
         key = min(nb - b0, 63u);
     }
-    const uint32_t bin = 63u - key, t = threadIdx.x;
+    const uint32_t bin = ii == ~0u ? 63u : desc ? 63u - key : key - 1u, t = threadIdx.x;
     if (t < 64) s_bin[t] = 0;
     __syncthreads();
     const uint32_t r = atomicAdd(&s_bin[bin], 1u);
@@ -2509,7 +2514,7 @@ __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArg
         if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
         const uint32_t i = base + threadIdx.x;
         uint32_t ii = i < n ? ll.at(a, i) : ~0u;
-        if (kMemo) ii = memo_order(a, ii, s_bin, s_pos);
+        if (kMemo) ii = memo_order(a, ii, s_bin, s_pos, ((base / kLevelBlock) / a.n_cu & 1u) == 0u);
         hashed += lf_job<kMemo>(a, ring, ii);
     }
     count_fused(a, hashed);
@@ -3206,6 +3211,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
     memo_args(g, a);
     a.memo_sort = g.memo_base && (g.inc_level[lvl] & kLvlForm) == 2 ? 1u : 0u;
+    a.n_cu = g.n_cu ? g.n_cu : 256u;
     static const uint32_t handoff = RF_DIAG_KNOB("RF_K2_HANDOFF", 1) == 0 ? 0u : 1u;  // (0: the chain fetches them itself)
     a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
