@@ -412,17 +412,6 @@ typedef struct {
     uint32_t last_sink_attach; /* level whose launch ran the sink list in the last plain step (UINT32_MAX: none) */
     uint32_t last_levels_half; /* levels the last plain step ran in 32-job latency-form workgroups */
 } rf_graph_stats;
-/* Memoized chaining values (round 6): a job of >= 8 blocks (after its
- * constant leading blocks) with >= 2 holes keeps the SHA-256 chaining value
- * before each of its blocks; when its inputs change, the throughput form
- * resumes it at the first block a changed hole reaches instead of block 0
- * (its holes are written in a fixed order -- deps in Deps order,
- * /root/reference/flow.go:692-698; sorted paths, executor.go:214-233 -- so
- * the blocks before hash as before).  out[0] = memo jobs, out[1] = stored
- * chaining values (32 B each in HBM), out[2] = blocks not hashed since the
- * graph was loaded (synchronises).  Digests never depend on it;
- * RF_K2_MEMO=0 at load turns it off. */
-int rf_graph_memo_stats(rf_graph *g, uint64_t out[3]);
 /* Fills the whole struct above (its round-4 layout, unchanged since; a field
  * added later comes with a new, sized entry point rather than a change to
  * this one). */

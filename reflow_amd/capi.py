@@ -33,7 +33,7 @@ EXPORTS = [
     "rf_graph_load", "rf_graph_destroy", "rf_graph_set_slots", "rf_graph_set_slots_device",
     "rf_graph_save", "rf_graph_restore", "rf_graph_set_forms",
     "rf_graph_adopt_slots",
-    "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get", "rf_graph_memo_stats",
+    "rf_graph_recompute", "rf_graph_recompute_async", "rf_graph_get_slots", "rf_graph_stats_get",
     "rf_bloom_load", "rf_bloom_load_json", "rf_bloom_load_binary", "rf_bloom_new",
     "rf_bloom_destroy", "rf_bloom_probe", "rf_bloom_probe_device", "rf_bloom_add",
     "rf_bloom_add_device", "rf_bloom_params", "rf_bloom_words",
@@ -301,7 +301,7 @@ def lib():
             "rf_graph_recompute": ([vp, i32, vp], i32),
             "rf_graph_recompute_async": ([vp, i32, vp], i32),
             "rf_graph_get_slots": ([vp, vp, u32, vp], i32),
-            "rf_graph_stats_get": ([vp, vp], i32), "rf_graph_memo_stats": ([vp, vp], i32),
+            "rf_graph_stats_get": ([vp, vp], i32),
             "rf_graph_adopt_slots": ([vp, vp], i32),
             "rf_bloom_load": ([vp, u64, u64, vp, u64, u64, vp], i32),
             "rf_bloom_load_json": ([vp, ctypes.c_char_p, ctypes.c_size_t, vp], i32),
@@ -810,13 +810,6 @@ class Graph:
         out = np.zeros((len(slots), 32), dtype=np.uint8)
         _check(lib().rf_graph_get_slots(self._h, _ptr(slots), len(slots), _ptr(out)))
         return out
-
-    def memo_stats(self):
-        """rf_graph_memo_stats: (memo jobs, stored chaining values, blocks not
-        hashed since load)."""
-        out = (ctypes.c_uint64 * 3)()
-        _check(lib().rf_graph_memo_stats(self._h, out))
-        return int(out[0]), int(out[1]), int(out[2])
 
     def stats(self) -> GraphStats:
         s = GraphStats()

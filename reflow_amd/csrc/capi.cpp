@@ -1240,74 +1240,16 @@ static void counting_pass(const std::vector<uint32_t>& idx, const uint32_t* key,
     for (uint32_t i : idx) out[at[key[i]]++] = i;
 }
 
-// The memoized chaining values' structures (GraphDev::memo_*), derived on
-// the device from the records, holes and reverse edges -- so a restored
-// checkpoint gets them the same way and the file format does not change:
-// which jobs are memo jobs and their entries, each entry's first hole, each
-// reverse edge's hole block (0 where the consumer is no memo job), every
-// job's stored values not current.  RF_K2_MEMO=0 at load: none (A/B).
-static int graph_build_memo(rf_graph* gr) {
-    GraphDev& G = gr->g;
-    rf_ctx* ctx = gr->ctx;
-    const uint64_t H = gr->hole_count;
-    hipError_t e;
-    auto nomem = [&](const char* what) {
-        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph memo (%s): %s", what,
-                    hipGetErrorString(e));
-    };
-    if ((e = gr->b_cons_hb.ensure(std::max<uint64_t>(H, 64))) != hipSuccess) return nomem("edges");
-    HIPC(sync_memset(ctx, gr->b_cons_hb.p, 0, std::max<uint64_t>(H, 64)));
-    G.cons_hb = gr->b_cons_hb.as<uint8_t>();
-    G.memo_base = nullptr;
-    G.memo_entries = G.memo_jobs = 0;
-    const bool memo_on = [] {  // (read per load, like the form thresholds: A/B in one process)
-        const char* v = getenv("RF_K2_MEMO");
-        return !(v && atoi(v) == 0);
-    }();
-    if (!memo_on || !G.n_jobs) return RF_OK;
-    if ((e = gr->b_memo_base.ensure(4ull * G.n_jobs + 64)) != hipSuccess) return nomem("jobs");
-    uint32_t* total = gr->b_memo_base.as<uint32_t>() + G.n_jobs;  // (entries, jobs: after the J words)
-    HIPC(sync_memset(ctx, total, 0, 8));
-    G.memo_base = gr->b_memo_base.as<uint32_t>();
-    HIPC(launch_memo_setup(G, total, ctx->stream));
-    uint32_t nt[2] = {0, 0};
-    HIPC(sync_copy(ctx, nt, total, 8, hipMemcpyDeviceToHost));
-    const uint32_t n = nt[0];
-    if (!n || n >= (1u << 31)) {  // none, or more entries than the u32 indices reach: no memo jobs
-        G.memo_base = nullptr;
-        gr->b_memo_base.release();
-        return RF_OK;
-    }
-    if ((e = gr->b_memo_cv.ensure(32ull * n)) != hipSuccess || (e = gr->b_memo_h.ensure(4ull * n)) != hipSuccess ||
-        (e = gr->b_memo_valid.ensure(std::max<uint64_t>(G.n_jobs, 64))) != hipSuccess ||
-        (e = gr->b_memo_skip.ensure(64)) != hipSuccess)
-        return nomem("entries");
-    HIPC(sync_memset(ctx, gr->b_memo_valid.p, 0, G.n_jobs));
-    HIPC(sync_memset(ctx, gr->b_memo_skip.p, 0, 64));
-    G.memo_skip = static_cast<unsigned long long*>(gr->b_memo_skip.p);
-    G.memo_jobs = nt[1];
-    G.memo_cv = gr->b_memo_cv.as<uint4>();
-    G.memo_h = gr->b_memo_h.as<uint32_t>();
-    G.memo_valid = gr->b_memo_valid.as<uint8_t>();
-    G.memo_entries = n;
-    HIPC(launch_memo_finish(G, H, ctx->stream));
-    HIPC(hipStreamSynchronize(ctx->stream));
-    return RF_OK;
-}
-
-// The device structures derived from the uploaded records: the mark
-// kernels' per-slot plan and the memo structures (rf_graph_load, restore).
 int graph_build_plan(rf_graph* gr) {
     GraphDev& G = gr->g;
-    if (RF_SLOT_PLAN) {
-        hipError_t e = gr->b_plan.ensure(48ull * std::max<uint32_t>(G.n_slots, 1));
-        if (e != hipSuccess)
-            return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph plan: %s", hipGetErrorString(e));
-        G.plan = gr->b_plan.as<uint4>();
-        HIPC(launch_slot_plan(G, gr->ctx->stream));
-        HIPC(hipStreamSynchronize(gr->ctx->stream));
-    }
-    return graph_build_memo(gr);
+    if (!RF_SLOT_PLAN) return RF_OK;
+    hipError_t e = gr->b_plan.ensure(48ull * std::max<uint32_t>(G.n_slots, 1));
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? RF_ENOMEM : RF_EDEVICE, "graph plan: %s", hipGetErrorString(e));
+    G.plan = gr->b_plan.as<uint4>();
+    HIPC(launch_slot_plan(G, gr->ctx->stream));
+    HIPC(hipStreamSynchronize(gr->ctx->stream));
+    return RF_OK;
 }
 
 extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out) {
@@ -1747,9 +1689,7 @@ extern "C" void rf_graph_destroy(rf_graph* gr) {
         DevGuard dg(gr->ctx->device);
         for (DevBuf* b : {&gr->b_meta, &gr->b_holes, &gr->b_cons_ptr, &gr->b_cons_job, &gr->b_tmpl,
                           &gr->b_slots, &gr->b_dirty, &gr->b_list, &gr->b_lmeta, &gr->b_counts, &gr->b_counts_last,
-                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst, &gr->b_plan,
-                          &gr->b_cons_hb, &gr->b_memo_base, &gr->b_memo_cv, &gr->b_memo_h, &gr->b_memo_valid,
-                          &gr->b_memo_skip})
+                          &gr->b_lvl_start, &gr->b_tmp_idx, &gr->b_tmp_dig, &gr->b_stamps, &gr->b_mid, &gr->b_wgst, &gr->b_plan})
             b->release();
         if (gr->e0) (void)hipEventDestroy(gr->e0);
         if (gr->e1) (void)hipEventDestroy(gr->e1);
@@ -2036,7 +1976,6 @@ static int graph_enqueue(rf_graph* gr, int full, hipStream_t s, bool plain = fal
     gr->last_counts = G.counts_last;
     if (full) {
         HIPC(hipMemsetAsync(G.dirty, 0, 4ull * (G.n_jobs + 1), s));
-        if (G.memo_base) HIPC(hipMemsetAsync(G.memo_valid, 0, G.n_jobs, s));  // (no stored value is current)
         HIPC(hipMemsetAsync(G.counts_other, 0, 4ull * counts_half_words(G.n_levels), s));  // both halves clear
     }
     return RF_OK;
@@ -2340,20 +2279,6 @@ extern "C" int rf_graph_gather_device(rf_graph* gr, const void* d_slots, uint32_
     DevGuard dg(gr->ctx->device);
     HIPC(launch_gather_slots(gr->g.slots, static_cast<const uint32_t*>(d_slots), n,
                              static_cast<uint8_t*>(d_out32), pick(gr->ctx, stream)));
-    return RF_OK;
-}
-
-extern "C" int rf_graph_memo_stats(rf_graph* gr, uint64_t out[3]) {
-    ARG(gr && out, "null argument");
-    std::lock_guard<std::mutex> lk(gr->ctx->mu);
-    DevGuard dg(gr->ctx->device);
-    out[0] = gr->g.memo_jobs;
-    out[1] = gr->g.memo_entries;
-    out[2] = 0;
-    if (gr->g.memo_skip) {
-        HIPC(hipDeviceSynchronize());  // (steps queued on any stream)
-        HIPC(sync_copy(gr->ctx, &out[2], gr->g.memo_skip, 8, hipMemcpyDeviceToHost));
-    }
     return RF_OK;
 }
 

@@ -188,27 +188,6 @@ struct GraphDev {
     uint32_t sink_at = 2;             // where the sink list may run (RF_K2_SINK_AT at load; graph_enqueue)
     unsigned long long* stamps = nullptr;  // diagnostic phase stamps [L][128] (RF_K2_STAMPS)
     unsigned long long* wgst = nullptr;    // diagnostic per-workgroup records [L][2048][4] (RF_K2_WGSTAMPS)
-    // ---- memoized chaining values of long jobs ----
-    // A job's holes are written in a fixed order (deps in Deps order,
-    // flow.go:692-698; sorted paths, executor.go:214-233), so the blocks
-    // before its first changed hole hash to what they did last time.  A
-    // "memo job" (>= kMemoMinBlocks blocks, >= 2 holes: never a fusion target
-    // or slot-fused) keeps the chaining value before each of its blocks
-    // 1..nb-1 (memo_cv, 32 B an entry from memo_base[j]) and, per entry, the
-    // first hole that reaches into that block (memo_h).  Whoever queues a job
-    // ORs into its queued word 1 | 2 << min(the changed hole's first block,
-    // 30) (cons_hb[e]: that block per reverse edge; 0 where unknown), so the
-    // word's lowest block bit is the first block that can differ, and the
-    // throughput form (lf_job) resumes there from the stored value.  The
-    // other forms hash from block 0 and clear memo_valid[j]; a full
-    // recompute clears them all.
-    uint32_t* memo_base = nullptr;  // [J] first memo entry of job j, ~0u: not a memo job (null: no memo jobs)
-    uint4* memo_cv = nullptr;       // [2 x entries] chaining values (written by lf_job)
-    uint32_t* memo_h = nullptr;     // [entries] first hole overlapping the entry's block
-    uint8_t* memo_valid = nullptr;  // [J] memo_cv holds job j's current chaining values
-    uint8_t* cons_hb = nullptr;     // [H] per reverse edge: first block of the consumer's hole(s) reading the slot
-    unsigned long long* memo_skip = nullptr;  // blocks memo jobs did not hash, since load (rf_graph_memo_stats)
-    uint64_t memo_entries = 0, memo_jobs = 0;
     // [2J] each job's initial chaining value (IV, or the midstate after the
     // constant blocks its template starts with -- the record's template
     // offset and block count already skip them); null when no job has any
@@ -228,13 +207,6 @@ struct GraphDev {
 // start[i] (64-B units) into mid[2i..2i+1] (state words); IV when lead[i] = 0.
 hipError_t launch_graph_midstates(const uint8_t* tmpl, const uint32_t* start, const uint32_t* lead, uint32_t n,
                                   uint4* mid, hipStream_t s);
-constexpr uint32_t kMemoMinBlocks = 8;
-// From the device records: g.memo_base[j] = the first of nb - 1 entries
-// taken for a memo job from *total (zeroed by the caller; any order), else
-// ~0u.  Then (memo_finish, with memo_cv / memo_h allocated for *total
-// entries) the static per-entry hole indices and the per-edge hole blocks.
-hipError_t launch_memo_setup(const GraphDev& g, uint32_t* total, hipStream_t s);
-hipError_t launch_memo_finish(const GraphDev& g, uint64_t n_edges, hipStream_t s);
 // The per-slot plan (GraphDev::plan) of a graph whose meta / cons_ptr / cons
 // are on the device.
 hipError_t launch_slot_plan(const GraphDev& g, hipStream_t s);

@@ -36,7 +36,6 @@ struct rf_graph {
     std::vector<uint32_t> ext2int;   // external job id -> internal
     bool initialized = false;
     DevBuf b_stamps, b_mid, b_wgst, b_plan;
-    DevBuf b_cons_hb, b_memo_base, b_memo_cv, b_memo_h, b_memo_valid, b_memo_skip;  // GraphDev::memo_*
     DevBuf b_meta, b_holes, b_cons_ptr, b_cons_job, b_tmpl, b_slots, b_dirty, b_list, b_lmeta, b_counts,
         b_counts_last, b_lvl_start, b_tmp_idx, b_tmp_dig;
     uint64_t total_blocks = 0, hole_count = 0, tmpl_bytes = 0, last_recomputed = 0;

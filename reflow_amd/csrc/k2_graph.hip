@@ -96,15 +96,6 @@ struct LevelArgs {
     uint32_t sink_wg = 0, ovf = 0;
     uint32_t handoff = 1;  // k2_level_pl cb0 = 2: the producer hands the chain its next target's operands
     const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
-    // memoized chaining values (GraphDev::memo_*; memo_base null: no memo jobs)
-    const uint32_t* __restrict__ memo_base = nullptr;
-    uint4* memo_cv = nullptr;
-    const uint32_t* __restrict__ memo_h = nullptr;
-    uint8_t* memo_valid = nullptr;
-    const uint8_t* __restrict__ cons_hb = nullptr;
-    uint32_t memo_sort = 0;  // k2_level_lf: order each workgroup's jobs by the blocks they will hash
-    unsigned long long* memo_skip = nullptr;
-    uint32_t n_cu = 256;  // the device's CUs (memo_order's direction by round of resident workgroups)
 };
 // The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
 __device__ __forceinline__ uint32_t dbg_mode(const LevelArgs& a) { return kDiag ? dbg_mode(a) : 0u; }
@@ -331,34 +322,16 @@ __device__ __forceinline__ void append_jobs(const LevelArgs& a, bool need, uint3
 // Mark consumers [c, ce) of the lanes whose slot changed (c == ce otherwise)
 // dirty, queueing the newly dirty ones (their records are fetched beside the
 // dirty-flag atomic).  Wave-uniform loop.
-// A job's queued word (GraphDev::dirty): bit 0 queued, bit 1 + b for a
-// changed hole starting in block b (b >= 30: bit 31) -- the first set block
-// bit is where a memo job's material can first differ (GraphDev::memo_*).
-// A marker that does not know the block sets bit 1 (block 0: hash it all).
-__device__ __forceinline__ uint32_t queued_bits(uint32_t hb) { return 1u | (2u << min(hb, 30u)); }
-__device__ __forceinline__ uint32_t first_changed_block(uint32_t d) {
-    const uint32_t x = d >> 1;
-    return x ? (uint32_t)__builtin_ctz(x) : 0u;
-}
-// A queued job hashed from block 0 by a form that keeps no chaining values:
-// its flag cleared, any stored ones no longer current.
-__device__ __forceinline__ void clear_queued(const LevelArgs& a, uint32_t p) {
-    a.dirty[p] = 0u;
-    if (a.memo_base) a.memo_valid[p] = 0;
-}
-
 __device__ __forceinline__ void propagate(const LevelArgs& a, uint32_t c, uint32_t ce) {
     while (__any(c < ce)) {
         bool need = false;
         uint2 jl = make_uint2(0, 0);
         uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
         if (c < ce) {
-            jl = a.cons[c];
-            const uint32_t hb = a.cons_hb[c];  // (issued beside the edge: no extra round trip)
-            ++c;
+            jl = a.cons[c++];
             q0 = a.meta[2ull * jl.x];
             q1 = a.meta[2ull * jl.x + 1];
-            need = atomicOr(&a.dirty[jl.x], queued_bits(hb)) == 0u;
+            need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
         }
         append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
@@ -451,41 +424,6 @@ struct MatCursor {
         ring_put(ring, 0, t);
         if (nb > 1) {
             t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
-        }
-    }
-    // begin() at block b0 of a memo job (lf_job; b0 = 0, h = m0.z: begin()):
-    // h = the first hole reaching into block b0 (GraphDev::memo_h).  A hole
-    // that starts in block b0 - 1 and runs into b0 is applied at once -- its
-    // bytes in the other ring half are overwritten by block b0 + 1's template
-    // before they are read.
-    __device__ __forceinline__ void begin_at(const LevelArgs& a, const uint4& m0, uint32_t* ring, uint32_t b0,
-                                             uint32_t h) {
-        T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
-        nb = m0.y;
-        he = m0.w;
-        hn = h;
-        const uint2 r0 = record(a, hn), r1 = record(a, hn + 1), r2 = record(a, hn + 2), r3 = record(a, hn + 3);
-        r4 = record(a, hn + 4);
-        r5 = record(a, hn + 5);
-        const uint4* tb = T + 4ull * b0;
-        t[0] = tb[0]; t[1] = tb[1]; t[2] = tb[2]; t[3] = tb[3];
-        digest(a, q0, r0);
-        digest(a, q1, r1);
-        digest(a, q2, r2);
-        digest(a, q3, r3);
-        ring_put(ring, (b0 & 1) * 16, t);
-        if (b0 + 1 < nb) {
-            t[0] = tb[4]; t[1] = tb[5]; t[2] = tb[6]; t[3] = tb[7];
-        }
-        if (q0.r.x < 64 * b0) {  // (only for b0 > 0: the hole from block b0 - 1)
-            apply(ring, q0);
-            q0 = q1;
-            q1 = q2;
-            q2 = q3;
-            hn += 1;
-            digest(a, q3, r4);
-            r4 = r5;
-            r5 = record(a, hn + 5);
         }
     }
     // begin() for a fused job: its one hole reads the slot handed over in
@@ -786,7 +724,7 @@ __device__ __forceinline__ void propagate_pre(const LevelArgs& a, uint32_t c, ui
             ++c;
             q0 = a.meta[2ull * jl.x];
             q1 = a.meta[2ull * jl.x + 1];
-            need = atomicOr(&a.dirty[jl.x], queued_bits(0u)) == 0u;  // (block unknown here: from block 0)
+            need = atomicOr(&a.dirty[jl.x], 1u) == 0u;
         }
         append_jobs(a, need, jl.x, jl.y, q0, q1);
     }
@@ -833,7 +771,7 @@ __global__ __launch_bounds__(kLevelBlock) void k2_level(LevelArgs a) {
             const uint32_t p = a.full ? a.s + i : a.list[level_pos(a, a.lvl, i)];
             const bool changed = hash_job(a, p, ring, cb, ce);
             if (!a.full) {
-                clear_queued(a, p);
+                a.dirty[p] = 0u;
                 if (!changed) ce = cb;
             }
         }
@@ -1053,7 +991,7 @@ __global__ __launch_bounds__(64 * kW) void k2_level_pc(LevelArgs a) {
             if (wave == 0) {
                 uint32_t cb = 0, ce = 0;
                 if (has) {
-                    clear_queued(a, p);
+                    a.dirty[p] = 0u;
                     cb = m1.y;
                     // the fusion target's edge is the last of the range
                     ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
@@ -1218,7 +1156,6 @@ __device__ __forceinline__ uint32_t wave_max_small(uint32_t x) {
     return __builtin_amdgcn_readfirstlane(m);
 }
 
-template <bool kMemo>
 __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii);
 __device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed);
 
@@ -1274,7 +1211,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
         for (uint32_t base = lo + (blockIdx.x - a.sink_wg) * nt; base < ll.n; base += g2 * nt) {
             if (threadIdx.x == 0) ws.jobs += min(nt, ll.n - base);
             const uint32_t i = base + threadIdx.x;
-            hashed += lf_job<false>(a, &kw[threadIdx.x * kRing], i < ll.n ? ll.at(a, i) : ~0u);
+            hashed += lf_job(a, &kw[threadIdx.x * kRing], i < ll.n ? ll.at(a, i) : ~0u);
         }
         count_fused(a, hashed);
         ws.end(a);
@@ -1384,7 +1321,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
             auto producer_propagate = [&]() {
                 const uint4 q = s_pp[lane][0], e = s_pp[lane][1];
                 const bool v = lane < kJ && q.w != 0;  // (half workgroup: lanes kJ.. hold no job)
-                if (v) clear_queued(a, q.x);
+                if (v) a.dirty[q.x] = 0u;
                 const uint2 pe[2] = {make_uint2(e.x, e.y), make_uint2(e.z, e.w)};
                 propagate_pre(a, v ? q.y : 0u, v ? q.z : 0u, pe);
                 pend = false;
@@ -1914,7 +1851,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                     if (!(kCB && a.cb0) && !pp3) {
                         uint32_t cb = 0, ce = 0;
                         if (own) {
-                            clear_queued(a, p);
+                            a.dirty[p] = 0u;
                             cb = m1.y;
                             ce = !changed ? m1.y : (m1.w != ~0u ? m1.z - 1 : m1.z);
                         }
@@ -2377,11 +2314,6 @@ __global__ __launch_bounds__(kMarkBlock * kMarkWaves) void k3_mark_slots(const u
 // hashed in the lane, its fused chain followed in the lane; every lane of the
 // wave calls it (propagate's appends are per wave).  Returns the fused jobs
 // the lane hashed.
-// kMemo (k2_level_lf<true>, the levels of long jobs): memo jobs resume (see
-// below); otherwise every job is hashed from block 0 and its stored values,
-// if any, are no longer current (the memo path's registers put the plain
-// form over its 168-VGPR budget).
-template <bool kMemo>
 __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii) {
     uint32_t p = ~0u;
     uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
@@ -2390,48 +2322,20 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
         m0 = a.lmeta[2ull * ii];
         m1 = a.lmeta[2ull * ii + 1];
     }
-    uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u, skipped = 0;
+    uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
     uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
     if (p != ~0u) {
-        // a memo job resumes at the first block its changed holes reach, from
-        // the chaining value stored there, and stores the ones after it
-        uint32_t mb = ~0u, b0 = 0, h0 = m0.z;
-        if (kMemo && a.memo_base) {
-            mb = a.memo_base[p];
-            if (mb != ~0u) {
-                const uint32_t d = a.dirty[p];
-                b0 = a.memo_valid[p] ? min(first_changed_block(d), m0.y - 1) : 0u;
-                if (b0) h0 = a.memo_h[mb + b0 - 1];
-            }
-        }
-        skipped = b0;
         MatCursor cur;
-        cur.begin_at(a, m0, ring, b0, h0);
+        cur.begin(a, m0, ring);
         ShaState st;
-        if (b0) {
-            const uint4 lo = a.memo_cv[2ull * (mb + b0 - 1)], hi = a.memo_cv[2ull * (mb + b0 - 1) + 1];
-            st.h[0] = lo.x; st.h[1] = lo.y; st.h[2] = lo.z; st.h[3] = lo.w;
-            st.h[4] = hi.x; st.h[5] = hi.y; st.h[6] = hi.z; st.h[7] = hi.w;
-        } else {
-            init_state(a, p, st);
-        }
-        for (uint32_t b = b0; b < cur.nb; ++b) {
+        init_state(a, p, st);
+        for (uint32_t b = 0; b < cur.nb; ++b) {
             uint32_t w[16];
             cur.block(a, b, ring, w);
             sha256_compress(st, w);
-            if (kMemo && mb != ~0u && b + 1 < cur.nb) {
-                uint4* cv = a.memo_cv + 2ull * (mb + b);
-                cv[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
-                cv[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
-            }
         }
         const bool ch = finish_job(a, m1, st);
-        if (kMemo) {
-            a.dirty[p] = 0u;
-            if (mb != ~0u) a.memo_valid[p] = 1;
-        } else {
-            clear_queued(a, p);
-        }
+        a.dirty[p] = 0u;
         const bool nf = m1.w != ~0u;
         cb = m1.y;
         cz = !ch ? m1.y : (nf ? m1.z - 1 : m1.z);
@@ -2444,12 +2348,6 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
             nm1 = a.meta[2ull * nx + 1];
         }
     }
-    if (kMemo) {  // the blocks memo jobs did not hash (rf_graph_memo_stats): one atomic a wave
-        uint32_t v = skipped;
-#pragma unroll
-        for (uint32_t o = 32; o; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-        if (__lane_id() == 0 && v) atomicAdd(a.memo_skip, (unsigned long long)v);
-    }
     propagate(a, cb, cz);
     return hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi);
 }
@@ -2457,50 +2355,9 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
 #ifndef RF_LF_WAVES
 #define RF_LF_WAVES 3  // (A/B builds: waves a SIMD the throughput form is compiled for)
 #endif
-// A memo level's workgroup orders its 256 list entries by the blocks each
-// job will hash (a memo job from its resume block), so a wave's lanes run
-// about equally long -- a lane-per-job wave lasts as long as its longest
-// lane, and resume points differ job to job.  Counting sort in LDS (64
-// bins); entries without a job go last.  The direction alternates by round
-// of one workgroup a CU (desc: longest first): wave w of a workgroup runs on
-// SIMD w of its CU, so the two workgroups a CU holds put their longest and
-// shortest waves on one SIMD instead of both longest.  Called by every thread.
-__device__ __forceinline__ uint32_t memo_order(const LevelArgs& a, uint32_t ii, uint32_t* s_bin, uint32_t* s_pos,
-                                               bool desc) {
-    uint32_t key = 0;
-    if (ii != ~0u) {
-        const uint32_t p = a.list[ii], nb = a.lmeta[2ull * ii].y;
-        const uint32_t mb = a.memo_base[p];
-        uint32_t b0 = 0;
-        if (mb != ~0u && a.memo_valid[p]) b0 = min(first_changed_block(a.dirty[p]), nb - 1);
-        key = min(nb - b0, 63u);
-    }
-    const uint32_t bin = ii == ~0u ? 63u : desc ? 63u - key : key - 1u, t = threadIdx.x;
-    if (t < 64) s_bin[t] = 0;
-    __syncthreads();
-    const uint32_t r = atomicAdd(&s_bin[bin], 1u);
-    __syncthreads();
-    if (t < 64) {  // exclusive prefix of the bin counts (wave 0)
-        const uint32_t c = s_bin[t];
-        uint32_t v = c;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)v, o, 64);
-            v += t >= o ? u : 0u;
-        }
-        s_bin[64 + t] = v - c;
-    }
-    __syncthreads();
-    s_pos[s_bin[64 + bin] + r] = ii;
-    __syncthreads();
-    return s_pos[t];
-}
-
-template <bool kMemo>
 __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArgs a) {  // (3 waves a SIMD: <= 168 VGPRs)
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     __shared__ uint32_t s_runs[2 * kRunWords];
-    __shared__ uint32_t s_bin[kMemo ? 128 : 1], s_pos[kMemo ? kLevelBlock : 1];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
     stage_runs(a, s_runs);
     zero_other_counts(a);
@@ -2513,9 +2370,7 @@ __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArg
     for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
         if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
         const uint32_t i = base + threadIdx.x;
-        uint32_t ii = i < n ? ll.at(a, i) : ~0u;
-        if (kMemo) ii = memo_order(a, ii, s_bin, s_pos, ((base / kLevelBlock) / a.n_cu & 1u) == 0u);
-        hashed += lf_job<kMemo>(a, ring, ii);
+        hashed += lf_job(a, ring, i < n ? ll.at(a, i) : ~0u);
     }
     count_fused(a, hashed);
     ws.end(a);
@@ -2637,7 +2492,7 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
         for (uint32_t base = ll.n1 + (blockIdx.x - a.oct_wg) * 128; base < ll.n; base += g2 * 128) {
             if (threadIdx.x == 0) ws.jobs += min(128u, ll.n - base);
             const uint32_t i = base + threadIdx.x;
-            hashed += lf_job<false>(a, &kw[threadIdx.x * kRing], i < ll.n ? ll.at(a, i) : ~0u);
+            hashed += lf_job(a, &kw[threadIdx.x * kRing], i < ll.n ? ll.at(a, i) : ~0u);
         }
         count_fused(a, hashed);
         ws.end(a);
@@ -2825,7 +2680,7 @@ __global__ __launch_bounds__(128) void k2_level_oct(LevelArgs a) {
             bool changed = false;
             if (own) {
                 changed = finish_job_pre(a, m1, st, olo, ohi);
-                clear_queued(a, p);
+                a.dirty[p] = 0u;
             }
             // no fusion target (kLvlOct): every consumer of a changed digest is queued
             propagate(a, own && changed ? m1.y : 0u, own && changed ? m1.z : 0u);
@@ -2953,83 +2808,6 @@ __global__ __launch_bounds__(256) void k_slot_plan(const uint32_t* __restrict__ 
     }
 }
 
-// ---- memoized chaining values (GraphDev::memo_*) ------------------------------
-__device__ __forceinline__ bool memo_eligible(const uint4& m0) {
-    return m0.y >= kMemoMinBlocks && m0.w - m0.z >= 2u;
-}
-// memo_base[j]: nb - 1 entries from a wave-aggregated cursor (one atomic a
-// wave); total[1] counts the memo jobs
-__global__ __launch_bounds__(256) void k_memo_setup(const uint4* __restrict__ meta, uint32_t J,
-                                                    uint32_t* __restrict__ base, uint32_t* total) {
-    const uint32_t lane = __lane_id();
-    for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < J; b0 += gridDim.x * blockDim.x) {
-        const uint32_t j = b0 + threadIdx.x;
-        uint32_t n = 0;
-        if (j < J) {
-            const uint4 m0 = meta[2ull * j];
-            n = memo_eligible(m0) ? m0.y - 1 : 0u;
-        }
-        // inclusive prefix of n over the wave, its total from the last lane
-        uint32_t v = n;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)v, o, 64);
-            v += lane >= o ? u : 0u;
-        }
-        const uint32_t wsum = (uint32_t)__shfl((int)v, 63, 64);
-        const uint32_t wjobs = (uint32_t)__popcll(__ballot(n != 0));
-        uint32_t at = 0;
-        if (lane == 63 && wsum) {
-            at = atomicAdd(total, wsum);
-            atomicAdd(total + 1, wjobs);  // (the memo jobs)
-        }
-        at = (uint32_t)__shfl((int)at, 63, 64);
-        if (j < J) base[j] = n ? at + v - n : ~0u;
-    }
-}
-// memo_h[base + b - 1] = the first hole of the job that reaches into block b
-// (pos + 32 > 64 b), b = 1 .. nb - 1; one lane a memo job
-__global__ __launch_bounds__(256) void k_memo_holes(const uint4* __restrict__ meta, const uint2* __restrict__ holes,
-                                                    const uint32_t* __restrict__ base, uint32_t J,
-                                                    uint32_t* __restrict__ memo_h) {
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < J; j += gridDim.x * blockDim.x) {
-        const uint32_t mb = base[j];
-        if (mb == ~0u) continue;
-        const uint4 m0 = meta[2ull * j];
-        uint32_t h = m0.z;
-        for (uint32_t b = 1; b < m0.y; ++b) {
-            while (h < m0.w && holes[h].x + 32u <= 64u * b) ++h;
-            memo_h[mb + b - 1] = h;
-        }
-    }
-}
-// cons_hb[e] for reverse edge e (slot s -> consumer k) when k is a memo job:
-// the first block of k's holes reading s (capped at 30); 0 otherwise
-__global__ __launch_bounds__(256) void k_cons_hb(const uint32_t* __restrict__ cons_ptr, const uint2* __restrict__ cons,
-                                                 const uint4* __restrict__ meta, const uint2* __restrict__ holes,
-                                                 const uint32_t* __restrict__ base, uint32_t S, uint64_t H,
-                                                 uint8_t* __restrict__ cons_hb) {
-    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < H;
-         e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = cons[e].x;
-        uint32_t hb = 0;
-        if (base[k] != ~0u) {
-            uint32_t lo = 0, hi = S;  // the slot whose range holds e: cons_ptr[s] <= e < cons_ptr[s + 1]
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) / 2;
-                if (cons_ptr[mid] <= e) lo = mid; else hi = mid;
-            }
-            const uint4 m0 = meta[2ull * k];
-            hb = 30u;
-            for (uint32_t h = m0.z; h < m0.w; ++h) {
-                const uint2 r = holes[h];
-                if (r.y == lo) hb = min(hb, r.x >> 6);
-            }
-        }
-        cons_hb[e] = (uint8_t)hb;
-    }
-}
-
 // End of a recompute: record what each level hashed, reset the lists.
 __global__ void k3_step_end(uint32_t* counts, uint32_t* last, const uint32_t* __restrict__ ls, uint32_t L,
                             int full) {
@@ -3084,15 +2862,6 @@ static uint32_t grid_mark(uint64_t items) {
 }
 
 // The level-kernel arguments the mark / apply kernels hash slot-fused jobs with.
-static void memo_args(const GraphDev& g, LevelArgs& a) {
-    a.memo_base = g.memo_base;
-    a.memo_cv = g.memo_cv;
-    a.memo_h = g.memo_h;
-    a.memo_valid = g.memo_valid;
-    a.cons_hb = g.cons_hb;
-    a.memo_skip = g.memo_skip;
-}
-
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
@@ -3101,25 +2870,7 @@ static LevelArgs mark_level_args(const GraphDev& g) {
     a.stamps = g.stamps;                     // (k3_mark_slots: MarkStamp into row L)
 #endif
     a.plan = g.plan;
-    memo_args(g, a);
     return a;
-}
-
-hipError_t launch_memo_setup(const GraphDev& g, uint32_t* total, hipStream_t s) {
-    if (!g.n_jobs) return hipSuccess;
-    hipLaunchKernelGGL(k_memo_setup, dim3(grid_for(g.n_jobs, 8192)), dim3(256), 0, s, g.meta, g.n_jobs,
-                       g.memo_base, total);
-    return hipGetLastError();
-}
-
-hipError_t launch_memo_finish(const GraphDev& g, uint64_t n_edges, hipStream_t s) {
-    if (g.memo_entries)
-        hipLaunchKernelGGL(k_memo_holes, dim3(grid_for(g.n_jobs, 8192)), dim3(256), 0, s, g.meta, g.holes,
-                           g.memo_base, g.n_jobs, g.memo_h);
-    if (n_edges)
-        hipLaunchKernelGGL(k_cons_hb, dim3(grid_for(n_edges, 16384)), dim3(256), 0, s, g.cons_ptr, g.cons, g.meta,
-                           g.holes, g.memo_base, g.n_slots, n_edges, g.cons_hb);
-    return hipGetLastError();
 }
 
 hipError_t launch_slot_plan(const GraphDev& g, hipStream_t s) {
@@ -3209,9 +2960,6 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                 g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
                 full ? nullptr : g.wgst};
     a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
-    memo_args(g, a);
-    a.memo_sort = g.memo_base && (g.inc_level[lvl] & kLvlForm) == 2 ? 1u : 0u;
-    a.n_cu = g.n_cu ? g.n_cu : 256u;
     static const uint32_t handoff = RF_DIAG_KNOB("RF_K2_HANDOFF", 1) == 0 ? 0u : 1u;  // (0: the chain fetches them itself)
     a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
@@ -3260,10 +3008,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
             static const uint64_t lf_cap = (uint64_t)RF_DIAG_KNOB("RF_K2_LF_GRID", 1024);
             uint64_t lg = (e - b + n2 + kLevelBlock - 1) / kLevelBlock;
             if (lg > lf_cap) lg = lf_cap;
-            if (a.memo_sort)
-                hipLaunchKernelGGL(k2_level_lf<true>, dim3((uint32_t)lg), dim3(kLevelBlock), 0, s, a);
-            else
-                hipLaunchKernelGGL(k2_level_lf<false>, dim3((uint32_t)lg), dim3(kLevelBlock), 0, s, a);
+            hipLaunchKernelGGL(k2_level_lf, dim3((uint32_t)lg), dim3(kLevelBlock), 0, s, a);
             return hipGetLastError();
         }
         // the latency form with an attached sink list: the level's own list
