@@ -473,6 +473,8 @@ typedef struct {
     uint32_t rounds;
 } rf_graph_part;
 typedef int (*rf_host_allgather_fn)(void *user, const void *send, void *recv, uint64_t bytes);
+/* Attach (or replace) g's partition.  Between steps only: RF_EPRECONDITION
+ * when input slots were set on a recomputed graph since its last recompute. */
 int rf_graph_set_part(rf_graph *g, const rf_graph_part *p);
 int rf_graph_recompute_part(rf_graph *g, rf_comm *comm, rf_host_allgather_fn fn, void *user, int full,
                             uint64_t *out_recomputed);

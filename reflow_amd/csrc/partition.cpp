@@ -68,6 +68,11 @@ extern "C" int rf_graph_set_part(rf_graph* gr, const rf_graph_part* p) {
     rf_ctx* ctx = gr->ctx;
     std::lock_guard<std::mutex> lk(ctx->mu);
     DevGuard dg(ctx->device);
+    //  a change set marked on a recomputed graph was queued for
+    // the plain step's levels; attach a part between steps, never inside one
+    // (a graph never recomputed only wrote its inputs: its next step is full)
+    if (gr->initialized && gr->marked)
+        return fail(RF_EPRECONDITION, "set_part: input slots set since the last recompute");
     graph_part_release(gr);
     auto* P = new GraphPart();
     gr->part = P;

@@ -138,7 +138,8 @@ def test_strong_layout_counts_match_dirty_work(nranks, nparts):
     """bench.py's strong layout (nparts fixed, nranks | nparts): each rank's
     jobs hashed by an incremental step equal the layout's dirty closure
     (PartitionedDag1000.dirty_work) plus the jobs hashed twice (rank 0's
-    global root: local pass, then after the exchange)."""
+    global root: local pass, then after the exchange).  A part cannot be
+    re-attached while a change set is pending."""
     S, P = 12, 4
     nf = 2 * P * S * nparts
 
@@ -157,6 +158,10 @@ def test_strong_layout_counts_match_dirty_work(nranks, nparts):
             sl, _, nw = pc.dag.change_set(0.05, n_global=nf)
             if len(sl):
                 g.set_slots(sl, nw)
+                #  no part attached inside a step: the change set is pending
+                with pytest.raises(capi.RfError) as e:
+                    g.set_part(pc.part)
+                assert e.value.code == capi.RF_EPRECONDITION
             got = g.recompute_part(allgather=ag, nranks=nranks)
             jobs, _, _ = pc.dirty_work(sl)
             g.close()
