@@ -2134,10 +2134,6 @@ struct SlotPlan {
 // waves of the SIMD cover the round trips, and the registers the look-ahead
 // needs would cost a wave per SIMD).  Returns the jobs this lane hashed.
 // Called by every lane of the wave.
-#ifndef RF_CHAIN_TOUCH
-#define RF_CHAIN_TOUCH 1  // (A/B builds: 0 = no touch of the next link)
-#endif
-constexpr bool kTouch = RF_CHAIN_TOUCH != 0;
 __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, uint32_t* ring, uint32_t p, uint4 m0,
                                                           uint4 m1, uint32_t fslot, uint4 flo, uint4 fhi) {
     uint32_t hashed = 0;
@@ -2159,16 +2155,6 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
             cur.flo = flo;
             cur.fhi = fhi;
             cur.begin_fused(a, m0, ring);
-            // touch the fusion target's template and hole record while this
-            // job hashes: the next link's loads then hit L2 (and the TLB)
-            // instead of HBM -- one dependent round trip a link, the chain's
-            // whole memory latency (the record arrives before this job's own
-            // template: no wait is added); two VGPRs, consumed at the end
-            uint32_t t0 = 0, t1 = 0;
-            if (kTouch && nf) {
-                t0 = reinterpret_cast<const uint32_t*>(a.tmpl)[16ull * nm0.x];
-                t1 = a.holes[nm0.z].x;
-            }
             ShaState st;
             init_state(a, p, st);
             for (uint32_t b = 0; b < cur.nb; ++b) {
@@ -2176,7 +2162,6 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
                 cur.block(a, b, ring, w, true);
                 sha256_compress(st, w);
             }
-            if (kTouch) __asm__ volatile("; touched %0 %1" ::"v"(t0), "v"(t1));
             const bool ch = finish_job_pre(a, m1, st, olo, ohi);
             ++hashed;
             cb = m1.y;
