@@ -94,7 +94,23 @@ class Budget:
         return True
 
 
-PMC_ROUND = "r04"  # traffic is read only from this round's pass over the current library
+PMC_ROUND = "pmc_r06"  # traffic is read only from this round's pass over the current library (profiles/pmc_r06)
+
+
+def k2_traffic(graph):
+    """HBM traffic of a DAG step from this round's committed rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes (tools/pmc_round6.sh -> tools/pmc_dag.py
+    on the same graph and change set; profiles/pmc_r06/k2_traffic_*.json),
+    beside the step's algorithmic bytes; None if absent."""
+    path = os.path.join(ROOT, "profiles", PMC_ROUND, "k2_traffic_%s.json" % graph)
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    return {"traffic_bytes_per_step": round(d["traffic_bytes_per_step"]),
+            "algorithmic_bytes_per_step": d["algorithmic_bytes_per_step"],
+            "traffic_over_algorithmic": d["traffic_over_algorithmic"],
+            "traffic_bytes_per_dirty_block": d["traffic_bytes_per_dirty_block"],
+            "source": os.path.relpath(path, ROOT) + " (separate FETCH_SIZE and WRITE_SIZE passes, raw KiB x 1024)"}
 
 
 def pmc_traffic(kernel, workload, algo_bytes=None):
@@ -817,7 +833,8 @@ def bench_dag100m(args, dist, ctx, comm, budget):
                "peak_tops": round(dist.world * VALU_LANE_OPS / 1e12, 1),
                "frac": round(ops / (t / steps) / (dist.world * VALU_LANE_OPS), 4),
                "note": "dirty material blocks x 1464 ops per step / wall time per step, against the INT32 "
-                       "VALU peak of the ranks' GPUs"}}
+                       "VALU peak of the ranks' GPUs",
+               "traffic": k2_traffic("100m") if not multi else None}}
     for b in (d_slots, d_old, d_new):
         b.free()
     g.close()
@@ -1542,7 +1559,8 @@ def cpu_baseline(args, sha, dag_res, budget):
                 "peak_tops": round(VALU_LANE_OPS / 1e12, 1),
                 "frac": round(ops / (dag_res["device_ms_per_step"] * 1e-3) / VALU_LANE_OPS, 4),
                 "note": "dirty blocks x 1464 ops per step / device time; the step is latency-bound (fused "
-                        "chains of dependent jobs), not throughput-bound"}
+                        "chains of dependent jobs), not throughput-bound",
+                "traffic": k2_traffic("configs2")}
         og.close()
     return res
 
