@@ -153,3 +153,50 @@ def test_dirty_work_matches_oracle(nparts, fanin):
     og.close()
     assert pc.dirty_work(slots)[0] == jobs
     assert pc.dirty_work(slots)[2] == blocks
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_persample_layout_pieces_equal_global_dag(nranks):
+    """bench.py's per-sample-root layout at N ranks (bench_persample: SURVEY
+    §8(d) C3/C4 as written -- samples independent, one module per sample in
+    /root/reference/doc/1000align/1000align.rf:37-47 -- so no exchange): rank
+    r holds samples [r S/N, (r+1) S/N) (Dag1000 sample0), the global change
+    set restricted to its slice (change_set n_global).  Together the pieces'
+    change sets are exactly the global one, and each piece's oracle
+    incremental update gives its samples' digests of the global DAG (every
+    per-sample kind, root included); the bench's dirty-node count sums to
+    the global count."""
+    import reflow_oracle as O
+    S, P = 8, 3
+    G = Dag1000(S, P)
+    gsl, _, gnew = G.change_set(0.1)
+    og = O.OGraph(G.arrays())
+    og.set_inputs(G.file_slots, G.leaf_ids)
+    og.full()
+    og.update(gsl, gnew)
+
+    def n_dirty(f):
+        f = np.asarray(f, dtype=np.int64)
+        return int(2 * len(f) + 10 * len(np.unique(f // 2)) + 5 * len(np.unique(f // 2 // P)))
+
+    s_rank = S // nranks
+    got_changes, dirty_sum = {}, 0
+    for r in range(nranks):
+        d = Dag1000(s_rank, P, sample0=r * s_rank)
+        sl, _, new = d.change_set(0.1, n_global=2 * P * S)
+        for s, v in zip(sl.tolist(), new):
+            got_changes[s + 2 * P * s_rank * r] = bytes(v)  # local file slot -> global file index
+        dirty_sum += n_dirty(sl)
+        o = O.OGraph(d.arrays())
+        o.set_inputs(d.file_slots, d.leaf_ids)
+        o.full()
+        if len(sl):
+            o.update(sl, new)
+        for name in ("KS", "CS1", "ES", "CS2", "XS", "pES", "pXS"):
+            k, gk = d.kinds[name], G.kinds[name]
+            gi = np.arange(k.count) + r * k.count
+            assert (o.slots[k.out_slot] == og.slots[gk.out_slot[gi]]).all(), (r, name)
+        o.close()
+    og.close()
+    assert got_changes == {int(s): bytes(v) for s, v in zip(gsl.tolist(), gnew)}
+    assert dirty_sum == n_dirty(gsl)
