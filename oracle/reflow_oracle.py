@@ -51,6 +51,8 @@ def lib():
         # (baseline_openssl.c: the bench's CPU baseline, OpenSSL on native threads)
         L.orc_openssl_sha256_batch.argtypes = [u8p, u8p, u8p, u8p, ctypes.c_uint64, u8p, ctypes.c_int]
         L.orc_openssl_sha256_batch.restype = ctypes.c_int
+        L.orc_openssl_sha256_files.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_int]
+        L.orc_openssl_sha256_files.restype = ctypes.c_int
         L.orc_fill_stream.argtypes = [ctypes.c_uint64, u8p, ctypes.c_uint64]
         L.orc_mm3_128.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p]
         L.orc_bloom_base_hashes.argtypes = [u8p, ctypes.c_uint64, u8p]
