@@ -2186,6 +2186,16 @@ static void wgst_report(rf_graph* gr) {
         }
         std::vector<double> ds = dur;
         std::sort(ds.begin(), ds.end());
+        // start-time spread: workgroups starting more than 5 / 20 / 50 us
+        // after the first (a launch wider than the resident set waits)
+        uint32_t l5 = 0, l20 = 0, l50 = 0, maxcu = 0;
+        for (uint32_t i : act) {
+            const double st = (r[4 * i] - t0) * 0.01;
+            l5 += st > 5, l20 += st > 20, l50 += st > 50;
+        }
+        for (auto& kv : cu) maxcu = std::max<uint32_t>(maxcu, (uint32_t)kv.second.size());
+        fprintf(stderr, "[wgstamps] level %u: started >5us late %u, >20us %u, >50us %u; most workgroups on one CU %u\n",
+                l, l5, l20, l50, maxcu);
         double sh = 0, al = 0;
         uint32_t nsh = 0, nal = 0, cus_shared = 0;
         for (auto& kv : cu) {

@@ -25,6 +25,10 @@ from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 # pl: every level in the latency form; lf: every level in the throughput
 # form; auto: the library's per-level choice (the default thresholds)
 FORMS = {"pl": capi.Graph.NEVER, "lf": 0, "auto": None}
+# --extra: also "lfs" (levels of short jobs lane-per-job, levels of long jobs
+# in the latency form) and "plw" (the reverse)
+EXTRA = {"lfs": (capi.Graph.THRU_DEFAULT, capi.Graph.NEVER, capi.Graph.THRU_MARK_DEFAULT),
+         "plw": (capi.Graph.NEVER, 0, capi.Graph.THRU_MARK_DEFAULT)}
 
 
 def run(ctx, name, g, slots, old, new, steps):
@@ -37,6 +41,8 @@ def run(ctx, name, g, slots, old, new, steps):
         for form, thr in FORMS.items():
             if thr is None:
                 g.set_forms(g.THRU_DEFAULT, g.THRU_WIDE_DEFAULT, g.THRU_MARK_DEFAULT)
+            elif isinstance(thr, tuple):
+                g.set_forms(*thr)
             else:
                 g.set_forms(thr)
             state = {"v": 0}
@@ -81,7 +87,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--lib", default="", help="another build of the library (A/B of builds)")
     ap.add_argument("--persample", default="", help="per-sample-root layout (SURVEY C3/C4): ranks, e.g. 8,1")
+    ap.add_argument("--extra", action="store_true", help="also the mixed forms (EXTRA)")
     a = ap.parse_args()
+    if a.extra:
+        FORMS.update(EXTRA)
     if a.lib:
         capi.LIB_PATH = os.path.abspath(a.lib)
         print("library: %s" % capi.LIB_PATH, file=sys.stderr)

@@ -4,6 +4,8 @@ hashed per level.
 
   python tools/stamp_probe.py [S]        configs[2] (S samples, default 22075)
   python tools/stamp_probe.py c4 R       rank 0's piece of the 100M layout at R ranks
+  python tools/stamp_probe.py ps R       rank 0's piece of the per-sample-root layout at R ranks
+RF_K2_WGSTAMPS=1 (with RF_K2_STAMPS=0): per-workgroup start / end / CU of every level launch.
 """
 import os
 import sys
@@ -20,7 +22,10 @@ if os.environ.get("STAMP_LIB"):
 from reflow_amd.workloads import Dag1000, PartitionedDag1000  # noqa: E402
 
 ctx = capi.Context(0, host_threads=0)
-if len(sys.argv) > 2 and sys.argv[1] == "c4":
+if len(sys.argv) > 2 and sys.argv[1] == "ps":  # the per-sample-root layout's rank 0 of R (1: the whole 100M DAG)
+    dag = Dag1000(27594 * 8 // int(sys.argv[2]), 32)
+    desc, n_global = dag.arrays(), 2 * 32 * 27594 * 8
+elif len(sys.argv) > 2 and sys.argv[1] == "c4":
     pc = PartitionedDag1000(27594, 32, int(sys.argv[2]), 0, nparts=8)
     dag, desc, n_global = pc.dag, pc.desc, 2 * 32 * 27594 * 8
 else:
