@@ -31,9 +31,12 @@ elif len(sys.argv) > 2 and sys.argv[1] == "c4":
 else:
     dag = Dag1000(int(sys.argv[1]) if len(sys.argv) > 1 else 22075, 32)
     desc, n_global = dag.arrays(), None
+print("built: %d jobs" % len(desc["out_slot"]), flush=True)
 g = capi.Graph.from_arrays(ctx, desc)
+print("loaded", flush=True)
 g.set_slots(dag.file_slots, dag.leaf_ids)
 g.recompute(full=True)
+print("full recompute done", flush=True)
 slots, old, new = dag.change_set(0.01, n_global=n_global) if n_global else dag.change_set(0.01)
 for v in (new, old, new):
     g.set_slots(slots, v)
