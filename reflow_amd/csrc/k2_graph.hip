@@ -98,7 +98,7 @@ struct LevelArgs {
     const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
 };
 // The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
-__device__ __forceinline__ uint32_t dbg_mode(const LevelArgs& a) { return kDiag ? dbg_mode(a) : 0u; }
+__device__ __forceinline__ uint32_t dbg_mode(const LevelArgs& a) { return kDiag ? a.dbg_twice : 0u; }
 
 // A level's append cursors (engine.h kListShards): run k of level l holds
 // the listed jobs whose ids fall in [lvl_start[l] + k * 2^sh, ... + 2^sh),
