@@ -95,6 +95,7 @@ struct LevelArgs {
     // chain per lane in those lane workgroups too, before the sinks
     uint32_t sink_wg = 0, ovf = 0;
     uint32_t handoff = 1;  // k2_level_pl cb0 = 2: the producer hands the chain its next target's operands
+    uint32_t n_cu = 256;   // the device's CUs (k2_level_lf's issue priorities)
     const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
 };
 // The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
@@ -2352,6 +2353,10 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
     return hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi);
 }
 
+#ifndef RF_LF_PRIO
+#define RF_LF_PRIO 0  // (A/B builds: 1 = sink workgroups at low issue priority, 2 = also the third wave a SIMD)
+#endif
+constexpr uint32_t kLfPrio = RF_LF_PRIO;
 #ifndef RF_LF_WAVES
 #define RF_LF_WAVES 3  // (A/B builds: waves a SIMD the throughput form is compiled for)
 #endif
@@ -2369,6 +2374,17 @@ __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArg
     uint32_t hashed = 0;
     for (uint32_t base = blockIdx.x * kLevelBlock; base < n; base += gridDim.x * kLevelBlock) {
         if (threadIdx.x == 0) ws.jobs += min(kLevelBlock, n - base);
+        if (kLfPrio) {
+            // issue priority by what the workgroup holds: the level's own
+            // (long) jobs high, the attached sinks (short, slack until the
+            // long ones end) low; with kLfPrio 2 also own-list workgroups past
+            // two a CU (the third wave on a SIMD) medium
+            const bool own = base < ll.n1;
+            const uint32_t pr = !own ? 0u : (kLfPrio == 2 && blockIdx.x >= 2 * a.n_cu) ? 1u : 2u;
+            if (pr == 0) __builtin_amdgcn_s_setprio(0);
+            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(2);
+        }
         const uint32_t i = base + threadIdx.x;
         hashed += lf_job(a, ring, i < n ? ll.at(a, i) : ~0u);
     }
@@ -2960,6 +2976,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                 g.hole_in_b0 && cb0 ? (g.fuse_pos2 ? 2u : 1u) : 0u, full ? 0u : rev, zero_counts,
                 full ? nullptr : g.wgst};
     a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
+    a.n_cu = g.n_cu ? g.n_cu : 256u;
     static const uint32_t handoff = RF_DIAG_KNOB("RF_K2_HANDOFF", 1) == 0 ? 0u : 1u;  // (0: the chain fetches them itself)
     a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
