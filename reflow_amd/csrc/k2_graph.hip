@@ -736,10 +736,10 @@ __device__ __forceinline__ void propagate_pre(const LevelArgs& a, uint32_t c, ui
 __device__ __forceinline__ bool hash_job(const LevelArgs& a, uint32_t p, uint32_t* ring, uint32_t& cb,
                                          uint32_t& ce) {
     const uint4 m0 = a.meta[2 * p], m1 = a.meta[2 * p + 1];
+    ShaState st;
+    init_state(a, p, st);  // (before the cursor's loads: see hash_fused_chain_lean)
     MatCursor cur;
     cur.begin(a, m0, ring);
-    ShaState st;
-    init_state(a, p, st);
     for (uint32_t b = 0; b < cur.nb; ++b) {
         uint32_t w[16];
         cur.block(a, b, ring, w);
@@ -2151,13 +2151,18 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
                 nm0 = a.meta[2ull * m1.w];
                 nm1 = a.meta[2ull * m1.w + 1];
             }
+            // the start state first: the template's wait in begin_fused then
+            // covers it, so the block loop holds no load of the preheader's
+            // (a midstate load issued after the template made the compiler put a
+            // vmcnt(0) at the top of every block -- a full round trip on the
+            // block b+2 template it had just issued)
+            ShaState st;
+            init_state(a, p, st);
             MatCursor cur;
             cur.fslot = fslot;
             cur.flo = flo;
             cur.fhi = fhi;
             cur.begin_fused(a, m0, ring);
-            ShaState st;
-            init_state(a, p, st);
             for (uint32_t b = 0; b < cur.nb; ++b) {
                 uint32_t w[16];
                 cur.block(a, b, ring, w, true);
@@ -2326,10 +2331,10 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
     uint32_t cb = 0, cz = 0, nx = ~0u, fslot = ~0u;
     uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
     if (p != ~0u) {
+        ShaState st;
+        init_state(a, p, st);  // (before the cursor's loads: see hash_fused_chain_lean)
         MatCursor cur;
         cur.begin(a, m0, ring);
-        ShaState st;
-        init_state(a, p, st);
         for (uint32_t b = 0; b < cur.nb; ++b) {
             uint32_t w[16];
             cur.block(a, b, ring, w);
