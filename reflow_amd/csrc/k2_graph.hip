@@ -352,6 +352,34 @@ __device__ __forceinline__ void or_digest(uint32_t* ring, uint32_t pos, const ui
     }
 }
 
+// w[0..15] = the big-endian words of the 16 ring words at r, the eight
+// two-word LDS reads issued back to back and waited for once (compiled
+// from C++, the throughput form at its register limit issued them one at a
+// time, each waited for in full)
+__device__ __forceinline__ void ring_read16(const uint32_t* r, uint32_t (&w)[16]) {
+    const uint32_t lds = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint32_t*)r);
+    uint64_t x0, x1, x2, x3, x4, x5, x6, x7;
+    __asm__ volatile(
+        "ds_read2_b32 %0, %8 offset1:1\n\t"
+        "ds_read2_b32 %1, %8 offset0:2 offset1:3\n\t"
+        "ds_read2_b32 %2, %8 offset0:4 offset1:5\n\t"
+        "ds_read2_b32 %3, %8 offset0:6 offset1:7\n\t"
+        "ds_read2_b32 %4, %8 offset0:8 offset1:9\n\t"
+        "ds_read2_b32 %5, %8 offset0:10 offset1:11\n\t"
+        "ds_read2_b32 %6, %8 offset0:12 offset1:13\n\t"
+        "ds_read2_b32 %7, %8 offset0:14 offset1:15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(x4), "=&v"(x5), "=&v"(x6), "=&v"(x7)
+        : "v"(lds)
+        : "memory");
+    const uint64_t x[8] = {x0, x1, x2, x3, x4, x5, x6, x7};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        w[2 * k] = bswap32((uint32_t)x[k]);
+        w[2 * k + 1] = bswap32((uint32_t)(x[k] >> 32));
+    }
+}
+
 __device__ __forceinline__ void ring_put(uint32_t* ring, uint32_t half, const uint4 (&t)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -417,15 +445,18 @@ struct MatCursor {
         const uint2 r0 = record(a, hn), r1 = record(a, hn + 1), r2 = record(a, hn + 2), r3 = record(a, hn + 3);
         r4 = record(a, hn + 4);
         r5 = record(a, hn + 5);
-        t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
+        uint4 t0[4];
+        t0[0] = T[0]; t0[1] = T[1]; t0[2] = T[2]; t0[3] = T[3];
+        // block 1's template with block 0's, not after block 0's wait (two
+        // round trips in a row at every job's start)
+        if (nb > 1) {
+            t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
+        }
         digest(a, q0, r0);
         digest(a, q1, r1);
         digest(a, q2, r2);
         digest(a, q3, r3);
-        ring_put(ring, 0, t);
-        if (nb > 1) {
-            t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
-        }
+        ring_put(ring, 0, t0);
     }
     // begin() for a fused job: its one hole reads the slot handed over in
     // registers, and its first two template blocks and hole record were
@@ -452,11 +483,12 @@ struct MatCursor {
         hn = m0.z;
         q0.r = a.holes[m0.z];
         q1.r = q2.r = q3.r = r4 = r5 = make_uint2(~0u, 0u);
-        t[0] = T[0]; t[1] = T[1]; t[2] = T[2]; t[3] = T[3];
-        ring_put(ring, 0, t);
-        if (nb > 1) {
+        uint4 t0[4];
+        t0[0] = T[0]; t0[1] = T[1]; t0[2] = T[2]; t0[3] = T[3];
+        if (nb > 1) {  // (with block 0's: see begin)
             t[0] = T[4]; t[1] = T[5]; t[2] = T[6]; t[3] = T[7];
         }
+        ring_put(ring, 0, t0);
     }
     // begin() for a fused job whose block 0 the chain wave builds (k2_level_pl,
     // cb0): the ring already holds its template blocks 0 and 1 with the
@@ -515,8 +547,7 @@ struct MatCursor {
                 r5 = record(a, hn + 5);
             }
         }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = bswap32(ring[half + i]);
+        ring_read16(ring + half, w);
     }
 };
 
