@@ -2396,10 +2396,29 @@ constexpr uint32_t kLfPrio = RF_LF_PRIO;
 #ifndef RF_LF_WAVES
 #define RF_LF_WAVES 3  // (A/B builds: waves a SIMD the throughput form is compiled for)
 #endif
+// Start delay of the throughput form's second and third resident workgroups
+// on a CU, in 10-ns ticks per round (A/B builds: -DRF_LF_STAGGER=0 off).  A
+// SIMD's waves run the same chains in step and waited for their loads
+// together (the 100M Exec level: ~37 % of the critical SIMDs' issue slots
+// idle with three waves on them); staggered by 3 us a round, 100M 0.7-1 %
+// faster, per-sample 1 % (same box, profiles/r06/ab_stagger*); 7 us: neutral.
+#ifndef RF_LF_STAGGER
+#define RF_LF_STAGGER 300
+#endif
 __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArgs a) {  // (3 waves a SIMD: <= 168 VGPRs)
     __shared__ uint32_t ring_all[kLevelBlock * kRing];
     __shared__ uint32_t s_runs[2 * kRunWords];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
+    if (RF_LF_STAGGER) {
+        // the waves a SIMD holds run the same chains in step, so they wait for
+        // their loads at the same time; start the CU's second and third
+        // workgroups later
+        const uint32_t r = blockIdx.x / a.n_cu;
+        if (r) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)RF_LF_STAGGER * r) __builtin_amdgcn_s_sleep(8);
+        }
+    }
     stage_runs(a, s_runs);
     zero_other_counts(a);
     WgStamp ws;
@@ -2433,12 +2452,22 @@ __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArg
 // look-ahead (hash_fused_chain_lean), so three waves fit a SIMD instead of
 // two and a 100M-node DAG's 141k changed slots run in one round of resident
 // waves.
+#ifndef RF_MARK_STAGGER
+#define RF_MARK_STAGGER 0  // (A/B builds: k3_mark_slots_lf's start delay per round, 10-ns ticks)
+#endif
 __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* __restrict__ sl,
                                                                const uint8_t* __restrict__ dig, uint32_t n,
                                                                LevelArgs a) {
     __shared__ uint32_t ring_all[kMarkBlock * kRing];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
     uint32_t hashed = 0;
+    if (RF_MARK_STAGGER) {  // (as k2_level_lf's stagger; one-wave workgroups, four a round per CU)
+        const uint32_t r = blockIdx.x / (4 * a.n_cu);
+        if (r) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)RF_MARK_STAGGER * r) __builtin_amdgcn_s_sleep(8);
+        }
+    }
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         bool changed = false;
@@ -2917,6 +2946,7 @@ static uint32_t grid_mark(uint64_t items) {
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
+    a.n_cu = g.n_cu ? g.n_cu : 256u;
 #ifdef RF_DIAG
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
     a.stamps = g.stamps;                     // (k3_mark_slots: MarkStamp into row L)
