@@ -2452,22 +2452,12 @@ __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArg
 // look-ahead (hash_fused_chain_lean), so three waves fit a SIMD instead of
 // two and a 100M-node DAG's 141k changed slots run in one round of resident
 // waves.
-#ifndef RF_MARK_STAGGER
-#define RF_MARK_STAGGER 0  // (A/B builds: k3_mark_slots_lf's start delay per round, 10-ns ticks)
-#endif
 __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* __restrict__ sl,
                                                                const uint8_t* __restrict__ dig, uint32_t n,
                                                                LevelArgs a) {
     __shared__ uint32_t ring_all[kMarkBlock * kRing];
     uint32_t* ring = &ring_all[threadIdx.x * kRing];
     uint32_t hashed = 0;
-    if (RF_MARK_STAGGER) {  // (as k2_level_lf's stagger; one-wave workgroups, four a round per CU)
-        const uint32_t r = blockIdx.x / (4 * a.n_cu);
-        if (r) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)RF_MARK_STAGGER * r) __builtin_amdgcn_s_sleep(8);
-        }
-    }
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         bool changed = false;
@@ -2946,7 +2936,6 @@ static uint32_t grid_mark(uint64_t items) {
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
-    a.n_cu = g.n_cu ? g.n_cu : 256u;
 #ifdef RF_DIAG
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
     a.stamps = g.stamps;                     // (k3_mark_slots: MarkStamp into row L)
