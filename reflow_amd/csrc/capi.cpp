@@ -1652,6 +1652,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         G.mid = gr->b_mid.as<uint4>();
     } else if (n_lead) {  // A/B: keep every block, the records as if no job had a constant prefix
         G.hole_in_b0 = false;
+        G.fuse_pos2 = false;  // (a target's hole may move past byte 2: fused_hole loads the records)
         for (uint32_t i = 0; i < J; ++i) {
             if (!lead[i]) continue;
             meta[8ull * i] -= lead[i];

@@ -96,6 +96,10 @@ struct LevelArgs {
     uint32_t sink_wg = 0, ovf = 0;
     uint32_t handoff = 1;  // k2_level_pl cb0 = 2: the producer hands the chain its next target's operands
     uint32_t n_cu = 256;   // the device's CUs (k2_level_lf's issue priorities)
+    // GraphDev::fuse_pos2: every fusion target's one hole at byte 2 of its
+    // first block, reading its producer's slot -- its hole record need not be
+    // loaded (fused_hole)
+    uint32_t fuse_pos2 = 0;
     const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
 };
 // The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
@@ -395,6 +399,18 @@ __device__ __forceinline__ void ring_put(uint32_t* ring, uint32_t half, const ui
 // pipeline: while block b is consumed, the template of block b+2 and the (at
 // most two: holes are >= 32 B apart) holes that start in block b+1 -- records
 // and slot digests -- are in flight.
+// A fusion target's hole record: loaded, or -- when every target's one hole
+// is at byte 2 (LevelArgs::fuse_pos2) -- (2, ~0u) without a load (the slot
+// is its producer's, whose digest the caller hands over).  The record load
+// was a random access into the 1.2 GB hole array at every chain link, ~5 %
+// of the 100M step (timing probe, profiles/r06/probe_loads/).
+// jf: the job is fused to another job (a fusion target); a slot-fused job
+// (the mark kernels' first, reading an input slot) has its hole elsewhere
+// (OpVal: byte 8), its record is always loaded.
+__device__ __forceinline__ uint2 fused_hole(const LevelArgs& a, uint32_t h, bool jf = true) {
+    return jf && a.fuse_pos2 ? make_uint2(2u, ~0u) : a.holes[h];
+}
+
 struct PendingHole {
     uint2 r;  // (material byte, slot), or ~0 past the job's last hole
     uint4 lo, hi;
@@ -476,12 +492,13 @@ struct MatCursor {
     // begin() for a job with one hole, whose digest is handed over in
     // registers (fslot / flo / fhi): only its hole record and template blocks
     // are loaded (hash_fused_chain_lean; then block(..., one = true))
-    __device__ __forceinline__ void begin_fused(const LevelArgs& a, const uint4& m0, uint32_t* ring) {
+    __device__ __forceinline__ void begin_fused(const LevelArgs& a, const uint4& m0, uint32_t* ring, bool jf = true) {
         T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * m0.x;
         nb = m0.y;
         he = m0.w;
         hn = m0.z;
-        q0.r = a.holes[m0.z];
+        q0.r = fused_hole(a, m0.z, jf);
+        q0.r.y = fslot;  // (its one hole reads the handed-over slot: apply uses flo/fhi)
         q1.r = q2.r = q3.r = r4 = r5 = make_uint2(~0u, 0u);
         uint4 t0[4];
         t0[0] = T[0]; t0[1] = T[1]; t0[2] = T[2]; t0[3] = T[3];
@@ -1479,7 +1496,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                 }
                 if (kChain && has && nfu && !handoff) {
                     if (kW == 2) {
-                        nrc = a.holes[nm0.z];
+                        nrc = fused_hole(a, nm0.z);
                         if (a.cb0 == 2) {
                             const uint4* nT = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * nm0.x;
                             ntc[0] = nT[0]; ntc[1] = nT[1]; ntc[2] = nT[2]; ntc[3] = nT[3];
@@ -1589,7 +1606,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                                 if (nm0.y > 1) {
                                     nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
                                 }
-                                nr = a.holes[nm0.z];
+                                nr = fused_hole(a, nm0.z);
                                 if (nm1.w != ~0u) {
                                     nnm0 = a.meta[2ull * nm1.w];
                                     nnm1 = a.meta[2ull * nm1.w + 1];
@@ -1703,7 +1720,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                             if (nm0.y > 1) {
                                 nt[4] = nT[4]; nt[5] = nT[5]; nt[6] = nT[6]; nt[7] = nT[7];
                             }
-                            nr = a.holes[nm0.z];
+                            nr = fused_hole(a, nm0.z);
                             if (nm1.w != ~0u) {
                                 nnm0 = a.meta[2ull * nm1.w];
                                 nnm1 = a.meta[2ull * nm1.w + 1];
@@ -1945,13 +1962,13 @@ __global__ __launch_bounds__(256) void k2_midstates(const uint8_t* __restrict__ 
 // (hl, hh: the midstate, or untouched = IV).
 __device__ __forceinline__ void fetch_fused_ops(const LevelArgs& a, uint32_t q, const uint4& q0, const uint4& q1,
                                                 uint4 (&tt)[8], uint2& rr, uint4& ol, uint4& oh, uint4& hl,
-                                                uint4& hh) {
+                                                uint4& hh, bool jf) {
     const uint4* T = reinterpret_cast<const uint4*>(a.tmpl) + 4ull * q0.x;
     tt[0] = T[0]; tt[1] = T[1]; tt[2] = T[2]; tt[3] = T[3];
     if (q0.y > 1) {
         tt[4] = T[4]; tt[5] = T[5]; tt[6] = T[6]; tt[7] = T[7];
     }
-    rr = a.holes[q0.z];
+    rr = fused_hole(a, q0.z, jf);
     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * q1.x);
     ol = od[0];
     oh = od[1];
@@ -1987,7 +2004,7 @@ __device__ __forceinline__ uint32_t hash_fused_chain(const LevelArgs& a, uint32_
             uint2 nr = r;
             uint4 nnm0 = nm0, nnm1 = nm1;
             if (nf) {
-                fetch_fused_ops(a, m1.w, nm0, nm1, nt, nr, nolo, nohi, nhlo, nhhi);
+                fetch_fused_ops(a, m1.w, nm0, nm1, nt, nr, nolo, nohi, nhlo, nhhi, true);
                 if (nm1.w != ~0u) {
                     nnm0 = a.meta[2ull * nm1.w];
                     nnm1 = a.meta[2ull * nm1.w + 1];
@@ -1998,6 +2015,7 @@ __device__ __forceinline__ uint32_t hash_fused_chain(const LevelArgs& a, uint32_
             cur.flo = flo;
             cur.fhi = fhi;
             cur.begin_pre(m0, T4, t, r, ring);
+            cur.q0.r.y = fslot;  // (its one hole reads the handed-over slot; fused_hole)
             ShaState st;
             st.h[0] = hlo.x; st.h[1] = hlo.y; st.h[2] = hlo.z; st.h[3] = hlo.w;
             st.h[4] = hhi.x; st.h[5] = hhi.y; st.h[6] = hhi.z; st.h[7] = hhi.w;
@@ -2112,7 +2130,7 @@ __device__ __forceinline__ void mark_input_slot_from(const LevelArgs& a, uint32_
     uint4 t[8];
     uint2 r = make_uint2(~0u, 0u);
     if (p != ~0u) {
-        fetch_fused_ops(a, p, m0, m1, t, r, olo, ohi, hlo, hhi);
+        fetch_fused_ops(a, p, m0, m1, t, r, olo, ohi, hlo, hhi, false);  // (slot-fused: its record)
         if (m1.w != ~0u) {
             nm0 = a.meta[2ull * m1.w];
             nm1 = a.meta[2ull * m1.w + 1];
@@ -2166,8 +2184,10 @@ struct SlotPlan {
 // waves of the SIMD cover the round trips, and the registers the look-ahead
 // needs would cost a wave per SIMD).  Returns the jobs this lane hashed.
 // Called by every lane of the wave.
+// jf: p is fused to a job (lf_job), not to an input slot (the mark kernel):
+// its hole record need not be loaded (fused_hole); the chain's later jobs are.
 __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, uint32_t* ring, uint32_t p, uint4 m0,
-                                                          uint4 m1, uint32_t fslot, uint4 flo, uint4 fhi) {
+                                                          uint4 m1, uint32_t fslot, uint4 flo, uint4 fhi, bool jf) {
     uint32_t hashed = 0;
     while (__any(p != ~0u)) {
         uint32_t cb = 0, cz = 0, nx = ~0u;
@@ -2193,7 +2213,8 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
             cur.fslot = fslot;
             cur.flo = flo;
             cur.fhi = fhi;
-            cur.begin_fused(a, m0, ring);
+            cur.begin_fused(a, m0, ring, jf);
+            jf = true;
             for (uint32_t b = 0; b < cur.nb; ++b) {
                 uint32_t w[16];
                 cur.block(a, b, ring, w, true);
@@ -2386,7 +2407,7 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
         }
     }
     propagate(a, cb, cz);
-    return hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi);
+    return hash_fused_chain_lean(a, ring, nx, nm0, nm1, fslot, flo, fhi, true);
 }
 
 #ifndef RF_LF_PRIO
@@ -2504,7 +2525,7 @@ __global__ __launch_bounds__(kMarkBlock) void k3_mark_slots_lf(const uint32_t* _
                 m1 = a.meta[2ull * p + 1];
             }
         }
-        hashed += hash_fused_chain_lean(a, ring, p, m0, m1, s, nlo, nhi);
+        hashed += hash_fused_chain_lean(a, ring, p, m0, m1, s, nlo, nhi, false);
         propagate(a, c, ce);  // the slot's other consumers
     }
     if (dbg_mode(a) != 16) count_fused(a, hashed);
@@ -2936,6 +2957,7 @@ static uint32_t grid_mark(uint64_t items) {
 static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
+    a.fuse_pos2 = g.fuse_pos2 ? 1u : 0u;
 #ifdef RF_DIAG
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
     a.stamps = g.stamps;                     // (k3_mark_slots: MarkStamp into row L)
@@ -3032,6 +3054,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
                 full ? nullptr : g.wgst};
     a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
     a.n_cu = g.n_cu ? g.n_cu : 256u;
+    a.fuse_pos2 = g.fuse_pos2 ? 1u : 0u;
     static const uint32_t handoff = RF_DIAG_KNOB("RF_K2_HANDOFF", 1) == 0 ? 0u : 1u;  // (0: the chain fetches them itself)
     a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
