@@ -1528,7 +1528,10 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
                 m[5] = (uint32_t)cptr[s];
                 m[6] = (uint32_t)cptr[s + 1];
                 m[7] = fuse[j] >= 0 ? gr->ext2int[(uint32_t)fuse[j]] : 0xffffffffu;
-                if (fused_target[j] && holes[2 * m[2]] != 2) p2 = false;  // (cb0 = 2 needs every one at 2)
+                // (cb0 = 2 and fused_hole need every one at material byte 2:
+                // relative byte 2 after constant leading blocks is not enough,
+                // such a target starts from a midstate)
+                if (fused_target[j] && (holes[2 * m[2]] != 2 || ld != 0)) p2 = false;
                 nb += nblk[j] - ld;
             }
             a_lead += nl;

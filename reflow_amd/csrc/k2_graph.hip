@@ -400,8 +400,9 @@ __device__ __forceinline__ void ring_put(uint32_t* ring, uint32_t half, const ui
 // most two: holes are >= 32 B apart) holes that start in block b+1 -- records
 // and slot digests -- are in flight.
 // A fusion target's hole record: loaded, or -- when every target's one hole
-// is at byte 2 (LevelArgs::fuse_pos2) -- (2, ~0u) without a load (the slot
-// is its producer's, whose digest the caller hands over).  The record load
+// is at material byte 2 (LevelArgs::fuse_pos2; then it has no constant
+// leading blocks either and starts from the IV) -- (2, ~0u) without a load
+// (the slot is its producer's, whose digest the caller hands over).  The record load
 // was a random access into the 1.2 GB hole array at every chain link, ~5 %
 // of the 100M step (timing probe, profiles/r06/probe_loads/).
 // jf: the job is fused to another job (a fusion target); a slot-fused job
@@ -1508,7 +1509,7 @@ __global__ __launch_bounds__(64 * (kJ / 32 + kW - 1)) void k2_level_pl(LevelArgs
                         nnm0 = a.meta[2ull * nm1.w];
                         nnm1 = a.meta[2ull * nm1.w + 1];
                     }
-                    if (a.mid) {
+                    if (a.mid && !a.fuse_pos2) {  // (a fuse_pos2 target starts from the IV)
                         nmlo = a.mid[2ull * m1.w];
                         nmhi = a.mid[2ull * m1.w + 1];
                     }
@@ -1972,7 +1973,7 @@ __device__ __forceinline__ void fetch_fused_ops(const LevelArgs& a, uint32_t q, 
     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * q1.x);
     ol = od[0];
     oh = od[1];
-    if (a.mid) {
+    if (a.mid && !(jf && a.fuse_pos2)) {  // (a fuse_pos2 target starts from the IV)
         hl = a.mid[2ull * q];
         hh = a.mid[2ull * q + 1];
     }
@@ -2208,7 +2209,10 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
             // vmcnt(0) at the top of every block -- a full round trip on the
             // block b+2 template it had just issued)
             ShaState st;
-            init_state(a, p, st);
+            if (jf && a.fuse_pos2)
+                st.init();  // (a fuse_pos2 target: no constant leading blocks, no midstate load)
+            else
+                init_state(a, p, st);
             MatCursor cur;
             cur.fslot = fslot;
             cur.flo = flo;
