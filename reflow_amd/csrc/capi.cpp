@@ -1503,9 +1503,15 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         }
         std::atomic<uint64_t> a_lead{0}, a_blocks{0};
         std::atomic<bool> pos2{true};
+        // slot-fused jobs (the mark kernels' first): all without constant
+        // leading blocks and with their hole at one position -> GraphDev::sf_pos
+        std::mutex sf_mu;
+        bool sf_ok = true;
+        uint32_t sf_at = ~0u;
         load_parallel(ctx, J, 16384, [&](uint64_t i0, uint64_t i1) {
             uint64_t nl = 0, nb = 0;
-            bool p2 = true;
+            bool p2 = true, sok = true;
+            uint32_t sat = ~0u;
             for (uint64_t i = i0; i < i1; ++i) {
                 const uint32_t j = perm[i];
                 const uint32_t s = d->out_slot[j];
@@ -1532,12 +1538,22 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
                 // relative byte 2 after constant leading blocks is not enough,
                 // such a target starts from a midstate)
                 if (fused_target[j] && (holes[2 * m[2]] != 2 || ld != 0)) p2 = false;
+                if (slot_fused[j]) {
+                    if (ld != 0 || (sat != ~0u && sat != holes[2 * m[2]])) sok = false;
+                    sat = holes[2 * m[2]];
+                }
                 nb += nblk[j] - ld;
             }
             a_lead += nl;
             a_blocks += nb;
             if (!p2) pos2 = false;
+            if (!sok || sat != ~0u) {
+                std::lock_guard<std::mutex> lk(sf_mu);
+                if (!sok || (sf_at != ~0u && sf_at != sat)) sf_ok = false;
+                sf_at = sat;
+            }
         });
+        gr->g.sf_pos = sf_ok ? sf_at : ~0u;
         n_lead = a_lead;
         gr->total_blocks += a_blocks;
         if (!pos2) gr->g.fuse_pos2 = false;
@@ -1656,6 +1672,7 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
     } else if (n_lead) {  // A/B: keep every block, the records as if no job had a constant prefix
         G.hole_in_b0 = false;
         G.fuse_pos2 = false;  // (a target's hole may move past byte 2: fused_hole loads the records)
+        G.sf_pos = ~0u;
         for (uint32_t i = 0; i < J; ++i) {
             if (!lead[i]) continue;
             meta[8ull * i] -= lead[i];

@@ -165,6 +165,11 @@ struct GraphDev {
     // every fusion target's hole is at material byte 2 (right after its WD
     // prefix: no Universe), so the chain assembles its block 0 in registers
     bool fuse_pos2 = true;
+    // every slot-fused job (an input slot's one-hole consumer, hashed by the
+    // mark kernels) without constant leading blocks and with its hole at this
+    // byte: its record and midstate are not loaded; ~0u: loaded (the default,
+    // and after a checkpoint restore)
+    uint32_t sf_pos = ~0u;
     // RF_K2_STREAM=1 at load: the streamed hand-over variant of k2_level_pl
     // (opt-in, measured slower; kept correct by a forced-mode GPU test)
     bool stream_handover = false;

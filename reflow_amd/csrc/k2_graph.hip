@@ -100,6 +100,7 @@ struct LevelArgs {
     // first block, reading its producer's slot -- its hole record need not be
     // loaded (fused_hole)
     uint32_t fuse_pos2 = 0;
+    uint32_t sf_pos = ~0u;  // GraphDev::sf_pos (slot-fused jobs, the mark kernels)
     const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
 };
 // The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
@@ -409,7 +410,13 @@ __device__ __forceinline__ void ring_put(uint32_t* ring, uint32_t half, const ui
 // (the mark kernels' first, reading an input slot) has its hole elsewhere
 // (OpVal: byte 8), its record is always loaded.
 __device__ __forceinline__ uint2 fused_hole(const LevelArgs& a, uint32_t h, bool jf = true) {
-    return jf && a.fuse_pos2 ? make_uint2(2u, ~0u) : a.holes[h];
+    if (jf) return a.fuse_pos2 ? make_uint2(2u, ~0u) : a.holes[h];
+    return a.sf_pos != ~0u ? make_uint2(a.sf_pos, ~0u) : a.holes[h];  // (slot-fused: GraphDev::sf_pos)
+}
+// Whether a fused job (jf: to a job; else to an input slot) starts from the IV
+// without a midstate load.
+__device__ __forceinline__ bool fused_iv(const LevelArgs& a, bool jf) {
+    return jf ? a.fuse_pos2 != 0 : a.sf_pos != ~0u;
 }
 
 struct PendingHole {
@@ -1973,7 +1980,7 @@ __device__ __forceinline__ void fetch_fused_ops(const LevelArgs& a, uint32_t q, 
     const uint4* od = reinterpret_cast<const uint4*>(a.slots + 32ull * q1.x);
     ol = od[0];
     oh = od[1];
-    if (a.mid && !(jf && a.fuse_pos2)) {  // (a fuse_pos2 target starts from the IV)
+    if (a.mid && !fused_iv(a, jf)) {
         hl = a.mid[2ull * q];
         hh = a.mid[2ull * q + 1];
     }
@@ -2209,8 +2216,8 @@ __device__ __forceinline__ uint32_t hash_fused_chain_lean(const LevelArgs& a, ui
             // vmcnt(0) at the top of every block -- a full round trip on the
             // block b+2 template it had just issued)
             ShaState st;
-            if (jf && a.fuse_pos2)
-                st.init();  // (a fuse_pos2 target: no constant leading blocks, no midstate load)
+            if (fused_iv(a, jf))
+                st.init();  // (no constant leading blocks: no midstate load)
             else
                 init_state(a, p, st);
             MatCursor cur;
@@ -2962,6 +2969,7 @@ static LevelArgs mark_level_args(const GraphDev& g) {
     LevelArgs a{0, 0, 0, 0, 0, g.meta, g.holes, g.cons, g.lvl_start_dev, g.n_levels,
                 g.tmpl, g.slots, g.dirty, g.list, g.counts, nullptr, g.mid, g.cons_ptr, g.lmeta, 0, 0, nullptr, nullptr};
     a.fuse_pos2 = g.fuse_pos2 ? 1u : 0u;
+    a.sf_pos = g.sf_pos;
 #ifdef RF_DIAG
     if (g.dbg_mark == 1) a.dbg_twice = 16;  // (diagnostic build: k3_mark_slots_lf skips its count)
     a.stamps = g.stamps;                     // (k3_mark_slots: MarkStamp into row L)
@@ -3059,6 +3067,7 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     a.split = (!full && a.cb0 == 2) ? g.split_b0 : 0u;
     a.n_cu = g.n_cu ? g.n_cu : 256u;
     a.fuse_pos2 = g.fuse_pos2 ? 1u : 0u;
+    a.sf_pos = g.sf_pos;
     static const uint32_t handoff = RF_DIAG_KNOB("RF_K2_HANDOFF", 1) == 0 ? 0u : 1u;  // (0: the chain fetches them itself)
     a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
