@@ -1558,6 +1558,12 @@ extern "C" int rf_graph_load(rf_ctx* ctx, const rf_graph_desc* d, rf_graph** out
         gr->total_blocks += a_blocks;
         if (!pos2) gr->g.fuse_pos2 = false;
     }
+    // levels none of whose jobs has constant leading blocks: their listed
+    // jobs start from the IV without a midstate load (k2_level_lf)
+    gr->g.lvl_lead0.assign(L, 1);
+    for (uint32_t l = 0; l < L; ++l)
+        for (uint32_t i = gr->g.lvl_start[l]; i < gr->g.lvl_start[l + 1] && gr->g.lvl_lead0[l]; ++i)
+            if (lead[i]) gr->g.lvl_lead0[l] = 0;
     lap("records");
     if (tb / 64 >= 0xffffffffull) return fail(RF_EINVAL, "templates exceed 256 GiB");
     // every byte is written below (template, zero tail, padding): no zero fill

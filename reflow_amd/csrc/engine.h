@@ -170,6 +170,9 @@ struct GraphDev {
     // byte: its record and midstate are not loaded; ~0u: loaded (the default,
     // and after a checkpoint restore)
     uint32_t sf_pos = ~0u;
+    // per level: 1 = no job of it has constant leading blocks (no midstate
+    // load for its listed jobs, k2_level_lf); empty after a restore (loaded)
+    std::vector<uint8_t> lvl_lead0;
     // RF_K2_STREAM=1 at load: the streamed hand-over variant of k2_level_pl
     // (opt-in, measured slower; kept correct by a forced-mode GPU test)
     bool stream_handover = false;

@@ -101,6 +101,8 @@ struct LevelArgs {
     // loaded (fused_hole)
     uint32_t fuse_pos2 = 0;
     uint32_t sf_pos = ~0u;  // GraphDev::sf_pos (slot-fused jobs, the mark kernels)
+    // GraphDev::lvl_lead0 of lvl / lvl2: the listed jobs start from the IV
+    uint32_t lead0 = 0, lead0_2 = 0;
     const uint4* __restrict__ plan = nullptr;  // [3S] the mark kernels' per-slot plan (GraphDev::plan), or null
 };
 // The diagnostic mode of a launch (LevelArgs::dbg_twice): always 0 in a release build.
@@ -1213,7 +1215,7 @@ __device__ __forceinline__ uint32_t wave_max_small(uint32_t x) {
     return __builtin_amdgcn_readfirstlane(m);
 }
 
-__device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii);
+__device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii, bool iv = false);
 __device__ __forceinline__ void count_fused(const LevelArgs& a, uint32_t hashed);
 
 // kJ = 64 jobs per workgroup (two chain waves), or 32 (one chain wave: the
@@ -2383,7 +2385,7 @@ __global__ __launch_bounds__(kMarkBlock * kMarkWaves) void k3_mark_slots(const u
 // hashed in the lane, its fused chain followed in the lane; every lane of the
 // wave calls it (propagate's appends are per wave).  Returns the fused jobs
 // the lane hashed.
-__device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii) {
+__device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, uint32_t ii, bool iv) {
     uint32_t p = ~0u;
     uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
     if (ii != ~0u) {
@@ -2395,7 +2397,10 @@ __device__ __forceinline__ uint32_t lf_job(const LevelArgs& a, uint32_t* ring, u
     uint4 flo = make_uint4(0, 0, 0, 0), fhi = flo, nm0 = flo, nm1 = flo;
     if (p != ~0u) {
         ShaState st;
-        init_state(a, p, st);  // (before the cursor's loads: see hash_fused_chain_lean)
+        if (iv)
+            st.init();  // (its level has no constant leading blocks: LevelArgs::lead0)
+        else
+            init_state(a, p, st);  // (before the cursor's loads: see hash_fused_chain_lean)
         MatCursor cur;
         cur.begin(a, m0, ring);
         for (uint32_t b = 0; b < cur.nb; ++b) {
@@ -2473,7 +2478,7 @@ __global__ __launch_bounds__(kLevelBlock, RF_LF_WAVES) void k2_level_lf(LevelArg
             else __builtin_amdgcn_s_setprio(2);
         }
         const uint32_t i = base + threadIdx.x;
-        hashed += lf_job(a, ring, i < n ? ll.at(a, i) : ~0u);
+        hashed += lf_job(a, ring, i < n ? ll.at(a, i) : ~0u, (i < ll.n1 ? a.lead0 : a.lead0_2) != 0);
     }
     count_fused(a, hashed);
     ws.end(a);
@@ -3068,6 +3073,8 @@ hipError_t launch_graph_level(const GraphDev& g, uint32_t lvl, int full, hipStre
     a.n_cu = g.n_cu ? g.n_cu : 256u;
     a.fuse_pos2 = g.fuse_pos2 ? 1u : 0u;
     a.sf_pos = g.sf_pos;
+    a.lead0 = lvl < g.lvl_lead0.size() ? g.lvl_lead0[lvl] : 0u;
+    a.lead0_2 = sink_lvl < g.lvl_lead0.size() ? g.lvl_lead0[sink_lvl] : 0u;
     static const uint32_t handoff = RF_DIAG_KNOB("RF_K2_HANDOFF", 1) == 0 ? 0u : 1u;  // (0: the chain fetches them itself)
     a.handoff = handoff;
     // incremental: the dirty count is only known on device; 1024 blocks (4
