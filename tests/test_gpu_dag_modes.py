@@ -119,3 +119,55 @@ def test_sink_list_attached_below_fill_level(ctx, monkeypatch):
     assert (g.get_slots(every) == gd.get_slots(every)).all()
     g.close()
     gd.close()
+
+
+def _leading(jobs, kind, seed):
+    """random_jobs with every job's first hole in block 0 ("none": no constant
+    leading blocks, so every level's listed jobs start from the IV --
+    GraphDev::lvl_lead0) or past it ("all": each job with a midstate)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for o, tmpl, holes in jobs:
+        first = holes[0][0]
+        if kind == "none" and first >= 64:
+            tmpl, holes = tmpl[64:], [(p - 64, s) for p, s in holes]
+        elif kind == "all" and first < 64:
+            pad = rng.integers(0, 256, size=64 + 64 * int(rng.integers(0, 2)), dtype=np.uint8).tobytes()
+            tmpl, holes = pad + tmpl, [(p + len(pad), s) for p, s in holes]
+        out.append((o, tmpl, holes))
+    return out
+
+
+@pytest.mark.parametrize("kind", ["none", "all"])
+def test_thru_form_leading_blocks(ctx, monkeypatch, tmp_path, kind):
+    """The throughput form's per-level IV start (LevelArgs::lead0) against the
+    oracle: graphs whose jobs have no constant leading blocks at all, or all
+    have them -- and after a checkpoint restore, which leaves the per-level
+    flags empty (every listed job then loads its midstate)."""
+    from reflow_amd import capi
+    monkeypatch.setenv("RF_K2_THRU", "0")
+    rng = np.random.default_rng(11)
+    n_in = 64
+    jobs = _leading(random_jobs(41, n_in=n_in), kind, 3)
+    assert all((h[0][0] < 64) == (kind == "none") for _, _, h in jobs)
+    inputs = [rng.integers(0, 256, size=32, dtype=np.uint8).tobytes() for _ in range(n_in)]
+    g = load_jobs(ctx, n_in, jobs)
+    g.set_slots(np.arange(n_in, dtype=np.uint32), np.frombuffer(b"".join(inputs), np.uint8).reshape(-1, 32))
+    g.recompute(full=True)
+    outs = np.array([o for o, _, _ in jobs], np.uint32)
+    for step in range(4):
+        if step == 2:
+            path = str(tmp_path / "g.ckpt")
+            g.save(path)
+            g.close()
+            g = capi.Graph.restore(ctx, path)
+        pick = rng.choice(n_in, size=[1, 6, 6, 24][step], replace=False)
+        for i in pick:
+            inputs[i] = rng.integers(0, 256, size=32, dtype=np.uint8).tobytes()
+        g.set_slots(pick.astype(np.uint32), np.frombuffer(b"".join(inputs[i] for i in pick), np.uint8).reshape(-1, 32))
+        g.recompute(full=False)
+        want = evaluate(n_in, jobs, inputs)
+        got = g.get_slots(outs)
+        for i, o in enumerate(outs.tolist()):
+            assert got[i].tobytes() == want[o], (kind, step, o)
+    g.close()
